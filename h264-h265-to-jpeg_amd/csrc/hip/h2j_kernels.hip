@@ -1,0 +1,963 @@
+// MI355X (gfx950, CDNA4, wave64) pixel pipeline for the H.264/H.265 still ->
+// JPEG hot path.  Hand-written HIP; integer work only (no MFMA: small fixed
+// transforms and filters, HBM/latency bound).
+//
+//   K1 h2j_k1_recon    — per picture, one wave walks the transform blocks in
+//                        decoding order: reference-sample gather with z-scan
+//                        availability + substitution (ballot/scan), [1 2 1]
+//                        / strong smoothing, planar/DC/angular prediction,
+//                        dequantisation, column/row inverse transform in LDS
+//                        with zero-bounding-box pruning, clip+store.
+//                        (H.265 8.4.4.2, 8.6.2-8.6.4; H.264 8.3, 8.5)
+//   K2 h2j_k2_deblock  — one thread per 4-line edge segment, vertical pass
+//                        then horizontal pass (H.265 8.7.2, H.264 8.7)
+//   K3 h2j_k3_sao      — one thread per 4 samples, band/edge offsets
+//                        (H.265 8.7.3)
+//   K4 h2j_k4_*        — JPEG forward path of FFmpeg's mjpeg encoder as
+//                        restated in SURVEY.md Appendix A: MB variance ->
+//                        rate control -> AP-922 FDCT -> 16-bit quantiser ->
+//                        zigzag, plus Huffman symbol histograms.
+//
+// Reference call sites replaced: /root/reference/src/Decoder.cpp:324,342
+// (avcodec_send_packet / avcodec_receive_frame) and
+// /root/reference/src/Encoder.cpp:250 (avcodec_send_frame, mjpeg).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+
+#include "h2j_gpu.h"
+
+#define DEVI __device__ __forceinline__
+
+namespace {
+
+// ---------------------------------------------------------------- helpers
+DEVI int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+struct FV {  // frame view
+    const h2j_frame* f;
+    uint8_t* arena;
+    const h2j_ctb* ctbs;
+    const h2j_slice* slices;
+};
+
+template <typename Pel>
+DEVI Pel* plane(const h2j_frame& f, uint8_t* arena, uint64_t base, int c) {
+    return reinterpret_cast<Pel*>(arena + base) + f.pic_off[c];
+}
+
+// 6.4.1 z-scan availability (luma coordinates)
+DEVI bool avail(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, int xc, int yc, int xn,
+                int yn) {
+    if (xn < 0 || yn < 0 || xn >= f.width || yn >= f.height) return false;
+    const int l2 = f.log2ctb;
+    const int cn = (yn >> l2) * f.ctb_w + (xn >> l2);
+    const int cc = (yc >> l2) * f.ctb_w + (xc >> l2);
+    if (cn == cc) {
+        const int m = (1 << l2) - 1;
+        int ax = (xn & m) >> 2, ay = (yn & m) >> 2, bx = (xc & m) >> 2, by = (yc & m) >> 2;
+        int za = 0, zb = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            za |= (((ax >> i) & 1) << (2 * i)) | (((ay >> i) & 1) << (2 * i + 1));
+            zb |= (((bx >> i) & 1) << (2 * i)) | (((by >> i) & 1) << (2 * i + 1));
+        }
+        return za <= zb;
+    }
+    const h2j_ctb& A = ctbs[cn];
+    const h2j_ctb& B = ctbs[cc];
+    if (A.ts > B.ts) return false;
+    if (slices[A.slice].slice_addr_rs != slices[B.slice].slice_addr_rs) return false;
+    return A.tile == B.tile;
+}
+
+// HEVC 32x32 inverse transform matrix entries from the 33 distinct cosines
+__constant__ int8_t kCos33[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                                  61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+__constant__ int8_t kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+__constant__ int8_t kAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
+                                  -5,  -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
+                                  -5,  -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
+__constant__ int16_t kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,    0,    0,
+                                      0,     0,     -4096, -1638, -910, -630, -482, -390, -315,
+                                      -256,  -315,  -390, -482, -630, -910, -1638, -4096, 0};
+__constant__ int8_t kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+
+struct K1Lds {
+    int8_t mat[32][32];
+    int seq[132];
+    int sub[132];
+    int ref[132];
+    int blk[32 * 32];
+    int tmp[32 * 32];
+    int maxx, maxy;
+    int dcsum;
+};
+
+DEVI int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- K1: HEVC
+template <typename Pel>
+__device__ void hevc_recon_frame(const h2j_frame& f, const h2j_tu* tus, const h2j_coef* coefs,
+                                 const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
+                                 uint8_t* arena, K1Lds& s) {
+    const int lane = threadIdx.x;
+    uint8_t* fmap = arena + f.maps;
+    int8_t* qmap = reinterpret_cast<int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
+    const h2j_tu* T = tus + f.tu;
+    const h2j_coef* CO = coefs + f.coef;
+    for (uint32_t t = 0; t < f.ntu; t++) {
+        const h2j_tu tu = T[t];
+        const int c = tu.c;
+        const int log2n = tu.log2n;
+        const int n = 1 << log2n;
+        const int nn = n * n;
+        const int x0 = tu.x, y0 = tu.y;
+        Pel* P = plane<Pel>(f, arena, f.pic, c);
+        const int st = f.pic_stride[c];
+        const int bd = c ? f.bit_depth_c : f.bit_depth;
+        const int maxv = (1 << bd) - 1;
+        const int shc = c ? 1 : 0;
+        const uint8_t flags = tu.flags;
+
+        if (flags & H2J_TU_PCM) {
+            for (int e = lane; e < tu.ncoef; e += 64) {
+                const uint32_t en = CO[tu.coef + e];
+                const int pos = static_cast<int>(en >> 16);
+                P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<Pel>(static_cast<uint16_t>(en & 0xFFFF));
+            }
+        } else {
+            // ---------------- residual (into s.blk) ----------------
+            const bool cbf = (flags & H2J_TU_CBF) != 0;
+            if (cbf) {
+                for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
+                if (lane == 0) { s.maxx = 0; s.maxy = 0; }
+                __syncthreads();
+                const bool bypass = (flags & H2J_TU_BYPASS) != 0;
+                const int qp = tu.qp;
+                const int bdShift = bd + log2n - 5;
+                const int ls = kLevelScale[qp % 6] << (qp / 6);
+                const uint8_t* slt = nullptr;
+                if (f.scaling_list && !((flags & H2J_TU_TSKIP) && n > 4)) {
+                    const int soff = log2n == 2 ? 0 + c * 16 : (log2n == 3 ? 48 + c * 64 : (log2n == 4 ? 240 + c * 256 : 1008));
+                    slt = sl + f.sl + soff;
+                }
+                int mx = 0, my = 0;
+                for (int e = lane; e < tu.ncoef; e += 64) {
+                    const uint32_t en = CO[tu.coef + e];
+                    const int pos = static_cast<int>(en >> 16);
+                    const int lvl = static_cast<int16_t>(en & 0xFFFF);
+                    int d;
+                    if (bypass) {
+                        d = lvl;
+                    } else {
+                        const int m = slt ? slt[pos] : 16;
+                        long long v = static_cast<long long>(lvl) * m * ls;
+                        v = (v + (1ll << (bdShift - 1))) >> bdShift;
+                        d = static_cast<int>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+                    }
+                    s.blk[pos] = d;
+                    mx = max(mx, pos & (n - 1));
+                    my = max(my, pos >> log2n);
+                }
+                if (mx) atomicMax(&s.maxx, mx);
+                if (my) atomicMax(&s.maxy, my);
+                __syncthreads();
+                if (!bypass) {
+                    if (flags & H2J_TU_TSKIP) {
+                        const int bdS = 20 - bd;
+                        for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
+                    } else {
+                        const bool dst = (flags & H2J_TU_DST) != 0;
+                        const int mxx = s.maxx, myy = s.maxy;
+                        const int msh = 5 - log2n;
+                        // column pass: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
+                        for (int i = lane; i < nn; i += 64) {
+                            const int x = i & (n - 1), y = i >> log2n;
+                            int acc = 0;
+                            if (x <= mxx) {
+                                for (int j = 0; j <= myy; j++) {
+                                    const int cf = dst ? kDst4[j][y] : s.mat[j << msh][y];
+                                    acc += cf * s.blk[j * n + x];
+                                }
+                            }
+                            s.tmp[i] = clip3(-32768, 32767, (acc + 64) >> 7);
+                        }
+                        __syncthreads();
+                        const int bdS = 20 - bd;
+                        for (int i = lane; i < nn; i += 64) {
+                            const int x = i & (n - 1), y = i >> log2n;
+                            int acc = 0;
+                            for (int j = 0; j <= mxx; j++) {
+                                const int cf = dst ? kDst4[j][x] : s.mat[j << msh][x];
+                                acc += cf * s.tmp[y * n + j];
+                            }
+                            s.blk[i] = (acc + (1 << (bdS - 1))) >> bdS;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            // ---------------- reference samples ----------------
+            const int L = 4 * n + 1;
+            const int xl = x0 << shc, yl = y0 << shc;
+            unsigned long long m0 = 0, m1 = 0, m2 = 0;
+            for (int base = 0; base < L; base += 64) {
+                const int k = base + lane;
+                bool a = false;
+                if (k < L) {
+                    int xn, yn;
+                    if (k < 2 * n) { xn = x0 - 1; yn = y0 + (2 * n - 1 - k); }
+                    else if (k == 2 * n) { xn = x0 - 1; yn = y0 - 1; }
+                    else { xn = x0 + (k - 2 * n - 1); yn = y0 - 1; }
+                    a = avail(f, ctbs, slices, xl, yl, xn << shc, yn << shc);
+                    s.seq[k] = a ? static_cast<int>(P[yn * st + xn]) : 0;
+                }
+                const unsigned long long bal = __ballot(a);
+                if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
+            }
+            __syncthreads();
+            const bool any = (m0 | m1 | m2) != 0;
+            for (int k = lane; k < L; k += 64) {
+                int v;
+                if (!any) {
+                    v = 1 << (bd - 1);
+                } else {
+                    const int ch = k >> 6, bit = k & 63;
+                    const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
+                    if ((mk >> bit) & 1ull) {
+                        v = s.seq[k];
+                    } else {
+                        int j = -1;
+                        const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
+                        if (below) j = (ch << 6) + 63 - __clzll(below);
+                        else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
+                        else if (ch >= 1 && m0) j = 63 - __clzll(m0);
+                        if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
+                                          : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
+                        v = s.seq[j];
+                    }
+                }
+                s.sub[k] = v;
+            }
+            __syncthreads();
+            const int mode = tu.mode;
+            bool filt = false;
+            if (c == 0 && mode != 1 && n != 4) {
+                const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+                const int md = d26 < d10 ? d26 : d10;
+                const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+                filt = mode == 0 || md > thr;
+            }
+            if (filt) {
+                const int corner = s.sub[2 * n];
+                const bool strong = f.strong_smoothing && n == 32 &&
+                                    abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
+                                    abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
+                for (int k = lane; k < L; k += 64) {
+                    int v;
+                    if (k == 0 || k == 4 * n) v = s.sub[k];
+                    else if (strong) {
+                        if (k == 2 * n) v = corner;
+                        else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
+                        else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
+                    } else {
+                        v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
+                    }
+                    s.ref[k] = v;
+                }
+            } else {
+                for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
+            }
+            __syncthreads();
+            // p(-1,y) = ref[2n-1-y], p(x,-1) = ref[2n+1+x], p(-1,-1) = ref[2n]
+            const int* R = s.ref;
+            int dc = 0;
+            if (mode == 1) {
+                int part = 0;
+                for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
+                dc = (wave_sum(part) + n) >> (log2n + 1);
+            }
+            const int angle = kAngle[mode];
+            const int inv = kInvAngle[mode];
+            for (int i = lane; i < nn; i += 64) {
+                const int x = i & (n - 1), y = i >> log2n;
+                int pv;
+                if (mode == 0) {
+                    pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
+                          (y + 1) * R[n - 1] + n) >> (log2n + 1);
+                } else if (mode == 1) {
+                    pv = dc;
+                    if (c == 0 && n < 32) {
+                        if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
+                        else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                        else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                    }
+                } else if (mode >= 18) {
+                    const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
+                    // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
+                    const int k1 = x + idx + 1, k2 = x + idx + 2;
+                    const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
+                    if (fr) {
+                        const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
+                        pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+                    } else {
+                        pv = r1;
+                    }
+                    if (mode == 26 && c == 0 && n < 32 && x == 0)
+                        pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
+                } else {
+                    const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
+                    // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
+                    const int k1 = y + idx + 1, k2 = y + idx + 2;
+                    const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
+                    if (fr) {
+                        const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
+                        pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+                    } else {
+                        pv = r1;
+                    }
+                    if (mode == 10 && c == 0 && n < 32 && y == 0)
+                        pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
+                }
+                const int r = cbf ? s.blk[i] : 0;
+                P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
+            }
+        }
+        // ---------------- deblocking maps (luma TBs) ----------------
+        if (c == 0) {
+            const int nb = n >> 2;
+            for (int i = lane; i < nb * nb; i += 64) {
+                const int bx = i % nb, by = i / nb;
+                const int idx = ((y0 >> 2) + by) * f.mw + (x0 >> 2) + bx;
+                uint8_t fl = 0;
+                if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
+                if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
+                if (flags & H2J_TU_NOFILT) fl |= 4;
+                fmap[idx] = fl;
+                qmap[idx] = tu.qpy;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(64) h2j_k1_recon(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
+                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
+                                                  uint8_t* arena) {
+    __shared__ K1Lds s;
+    const h2j_frame& f = frames[blockIdx.x];
+    for (int i = threadIdx.x; i < 1024; i += 64) {
+        const int m = i >> 5, nn = i & 31;
+        int a = ((2 * nn + 1) * m) & 127;
+        if (a > 64) a = 128 - a;
+        s.mat[m][nn] = static_cast<int8_t>(a > 32 ? -kCos33[64 - a] : kCos33[a]);
+    }
+    __syncthreads();
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    if (f.codec == H2J_CODEC_HEVC) {
+        if (f.bit_depth == 8) hevc_recon_frame<uint8_t>(f, tus, coefs, C, S, sl, arena, s);
+        else hevc_recon_frame<uint16_t>(f, tus, coefs, C, S, sl, arena, s);
+    }
+}
+
+// ---------------------------------------------------------------- K2: deblocking
+__constant__ uint8_t kBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                                  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                                  34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+__constant__ uint8_t kTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,  1,  1,  1,  1, 1,
+                                2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+DEVI int chroma_qp_tab(int qpi) {
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    const int t[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    return t[qpi - 30];
+}
+
+template <typename Pel>
+DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fmap, const int8_t* qmap,
+                         const h2j_slice& sl, bool vert, int xe, int ye) {
+    const int xp = vert ? xe - 1 : xe, yp = vert ? ye : ye - 1;
+    const int qpq = qmap[(ye >> 2) * f.mw + (xe >> 2)], qpp = qmap[(yp >> 2) * f.mw + (xp >> 2)];
+    const int qpl = (qpq + qpp + 1) >> 1;
+    const int bd = f.bit_depth;
+    const int beta = kBeta[clip3(0, 51, qpl + sl.beta_offset)] * (1 << (bd - 8));
+    const int tc = kTc[clip3(0, 53, qpl + 2 + sl.tc_offset)] * (1 << (bd - 8));
+    const int maxv = (1 << bd) - 1;
+    // sample addressing: line k, distance i (0..3) from the edge
+    const int sa = vert ? st : 1;   // along the edge
+    const int sx = vert ? 1 : st;   // across the edge
+    Pel* q = pl + ye * st + xe;
+    int P[4][4], Q[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            P[k][i] = q[k * sa - (i + 1) * sx];
+            Q[k][i] = q[k * sa + i * sx];
+        }
+    const int dp0 = abs(P[0][2] - 2 * P[0][1] + P[0][0]), dp3 = abs(P[3][2] - 2 * P[3][1] + P[3][0]);
+    const int dq0 = abs(Q[0][2] - 2 * Q[0][1] + Q[0][0]), dq3 = abs(Q[3][2] - 2 * Q[3][1] + Q[3][0]);
+    const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
+    if (dpq0 + dpq3 >= beta) return;
+    const bool s0 = (2 * dpq0 < (beta >> 2)) && (abs(P[0][3] - P[0][0]) + abs(Q[0][0] - Q[0][3]) < (beta >> 3)) &&
+                    (abs(P[0][0] - Q[0][0]) < ((5 * tc + 1) >> 1));
+    const bool s3 = (2 * dpq3 < (beta >> 2)) && (abs(P[3][3] - P[3][0]) + abs(Q[3][0] - Q[3][3]) < (beta >> 3)) &&
+                    (abs(P[3][0] - Q[3][0]) < ((5 * tc + 1) >> 1));
+    const bool dEp = dp < ((beta + (beta >> 1)) >> 3);
+    const bool dEq = dq < ((beta + (beta >> 1)) >> 3);
+    const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
+    const bool nfq = fmap[(ye >> 2) * f.mw + (xe >> 2)] & 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int p0 = P[k][0], p1 = P[k][1], p2 = P[k][2], p3 = P[k][3];
+        const int q0 = Q[k][0], q1 = Q[k][1], q2 = Q[k][2], q3 = Q[k][3];
+        Pel* e = q + k * sa;
+        if (s0 && s3) {
+            if (!nfp) {
+                e[-1 * sx] = static_cast<Pel>(clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3));
+                e[-2 * sx] = static_cast<Pel>(clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2));
+                e[-3 * sx] = static_cast<Pel>(clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3));
+            }
+            if (!nfq) {
+                e[0] = static_cast<Pel>(clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3));
+                e[sx] = static_cast<Pel>(clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2));
+                e[2 * sx] = static_cast<Pel>(clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3));
+            }
+        } else {
+            int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+            if (abs(delta) < tc * 10) {
+                delta = clip3(-tc, tc, delta);
+                if (!nfp) e[-sx] = static_cast<Pel>(clip3(0, maxv, p0 + delta));
+                if (!nfq) e[0] = static_cast<Pel>(clip3(0, maxv, q0 - delta));
+                if (dEp && !nfp) {
+                    const int d2 = clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1);
+                    e[-2 * sx] = static_cast<Pel>(clip3(0, maxv, p1 + d2));
+                }
+                if (dEq && !nfq) {
+                    const int d2 = clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1);
+                    e[sx] = static_cast<Pel>(clip3(0, maxv, q1 + d2));
+                }
+            }
+        }
+    }
+}
+
+template <typename Pel>
+DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, const uint8_t* fmap,
+                           const int8_t* qmap, const h2j_slice& sl, int cqpoff, bool vert, int xc, int yc) {
+    const int xl = xc * 2, yl = yc * 2;
+    const int xp = vert ? xl - 1 : xl, yp = vert ? yl : yl - 1;
+    const int qpq = qmap[(yl >> 2) * f.mw + (xl >> 2)], qpp = qmap[(yp >> 2) * f.mw + (xp >> 2)];
+    const int qpc = chroma_qp_tab(((qpq + qpp + 1) >> 1) + cqpoff);
+    const int bd = f.bit_depth_c;
+    const int tc = kTc[clip3(0, 53, qpc + 2 + sl.tc_offset)] * (1 << (bd - 8));
+    const int maxv = (1 << bd) - 1;
+    const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
+    const bool nfq = fmap[(yl >> 2) * f.mw + (xl >> 2)] & 4;
+    const int sa = vert ? st : 1, sx = vert ? 1 : st;
+    Pel* q = pl + yc * st + xc;
+    for (int k = 0; k < 4; k++) {
+        if (vert ? (yc + k >= ph) : (xc + k >= pw)) break;
+        Pel* e = q + k * sa;
+        const int p0 = e[-sx], p1 = e[-2 * sx], q0 = e[0], q1 = e[sx];
+        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
+        if (!nfp) e[-sx] = static_cast<Pel>(clip3(0, maxv, p0 + delta));
+        if (!nfq) e[0] = static_cast<Pel>(clip3(0, maxv, q0 - delta));
+    }
+}
+
+template <typename Pel>
+DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, uint8_t* arena,
+                         bool vert, int idx) {
+    const int x4 = idx % f.mw, y4 = idx / f.mw;
+    if (y4 >= f.mh) return;
+    const uint8_t* fmap = arena + f.maps;
+    const int8_t* qmap = reinterpret_cast<const int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
+    const uint8_t fl = fmap[idx];
+    if (!(fl & (vert ? 1 : 2))) return;
+    const int xe = x4 * 4, ye = y4 * 4;
+    const int ctb = (ye >> f.log2ctb) * f.ctb_w + (xe >> f.log2ctb);
+    const h2j_slice& sl = slices[ctbs[ctb].slice];
+    hevc_luma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 0), f.pic_stride[0], fmap, qmap, sl, vert, xe, ye);
+    // chroma edges lie on the 16-luma grid; one chroma segment = 8 luma lines
+    if ((vert ? (xe & 15) == 0 && (ye & 7) == 0 : (ye & 15) == 0 && (xe & 7) == 0)) {
+        const int pw = f.width >> 1, ph = f.height >> 1;
+        hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 1), f.pic_stride[1], pw, ph, fmap, qmap, sl,
+                              f.cb_qp_offset, vert, xe >> 1, ye >> 1);
+        hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 2), f.pic_stride[2], pw, ph, fmap, qmap, sl,
+                              f.cr_qp_offset, vert, xe >> 1, ye >> 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                     const h2j_slice* slices, uint8_t* arena, int vert) {
+    const h2j_frame& f = frames[blockIdx.y];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= f.mw * f.mh) return;
+    if (f.codec != H2J_CODEC_HEVC) return;
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    if (f.bit_depth == 8) deblock_thread<uint8_t>(f, C, S, arena, vert != 0, idx);
+    else deblock_thread<uint16_t>(f, C, S, arena, vert != 0, idx);
+}
+
+// ---------------------------------------------------------------- K3: SAO
+DEVI int zscan_luma(const h2j_frame& f, const h2j_ctb* ctbs, int x, int y) {
+    const int l2 = f.log2ctb;
+    const int ctb = (y >> l2) * f.ctb_w + (x >> l2);
+    const int m = (1 << l2) - 1;
+    const int ax = (x & m) >> 2, ay = (y & m) >> 2;
+    int z = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) z |= (((ax >> i) & 1) << (2 * i)) | (((ay >> i) & 1) << (2 * i + 1));
+    return static_cast<int>(ctbs[ctb].ts << (2 * (l2 - 2))) + z;
+}
+
+template <typename Pel>
+DEVI void sao_sample(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, const Pel* src, Pel* dst,
+                     int st, int pw, int ph, int c, int x, int y, const uint8_t* fmap) {
+    const int shc = c ? 1 : 0;
+    const int xl = x << shc, yl = y << shc;
+    const int ctb = (yl >> f.log2ctb) * f.ctb_w + (xl >> f.log2ctb);
+    const h2j_ctb& C = ctbs[ctb];
+    const h2j_slice& S = slices[C.slice];
+    int v = src[y * st + x];
+    const int type = C.type[c];
+    const bool on = type != 0 && (c == 0 ? S.sao_luma : S.sao_chroma) && !(fmap[(yl >> 2) * f.mw + (xl >> 2)] & 4);
+    if (on) {
+        const int bd = c ? f.bit_depth_c : f.bit_depth;
+        int off = 0;
+        if (type == 1) {
+            const int k = ((v >> (bd - 5)) - C.band_pos[c]) & 31;
+            if (k < 4) off = C.off[c][k];
+        } else {
+            const int cls = C.eo_class[c];
+            const int hx0 = cls == 0 ? -1 : (cls == 1 ? 0 : (cls == 2 ? -1 : 1));
+            const int vy0 = cls == 0 ? 0 : -1;
+            const int xa = x + hx0, ya = y + vy0, xb = x - hx0, yb = y - vy0;
+            bool ok = xa >= 0 && ya >= 0 && xa < pw && ya < ph && xb >= 0 && yb >= 0 && xb < pw && yb < ph;
+            if (ok) {
+                // slice / tile boundary restrictions (8.7.3.2)
+                const int nx[2] = {xa, xb}, ny[2] = {ya, yb};
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const int xnl = nx[k] << shc, ynl = ny[k] << shc;
+                    const int cn = (ynl >> f.log2ctb) * f.ctb_w + (xnl >> f.log2ctb);
+                    if (cn != ctb) {
+                        const h2j_ctb& N = ctbs[cn];
+                        const h2j_slice& SN = slices[N.slice];
+                        if (SN.slice_addr_rs != S.slice_addr_rs) {
+                            const int zn = zscan_luma(f, ctbs, xnl, ynl), zc = zscan_luma(f, ctbs, xl, yl);
+                            if (zn < zc && !S.lf_across_slices) ok = false;
+                            if (zc < zn && !SN.lf_across_slices) ok = false;
+                        }
+                        if (!f.lf_across_tiles && N.tile != C.tile) ok = false;
+                    }
+                }
+            }
+            if (ok) {
+                const int a = src[ya * st + xa], b = src[yb * st + xb];
+                int e = 2 + ((v > a) - (v < a)) + ((v > b) - (v < b));
+                e = e == 0 ? 1 : (e == 1 ? 2 : (e == 2 ? 0 : e));
+                if (e) off = C.off[c][e - 1];
+            }
+        }
+        v = clip3(0, (1 << bd) - 1, v + off);
+    }
+    dst[y * st + x] = static_cast<Pel>(v);
+}
+
+template <typename Pel>
+DEVI void sao_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, uint8_t* arena, int idx) {
+    // 4 horizontal samples per thread; luma then Cb then Cr index ranges
+    const int W = f.width, H = f.height;
+    const int lq = (W >> 2) * H;
+    const int cq = (W >> 3) * (H >> 1);
+    int c, x, y;
+    if (idx < lq) { c = 0; y = idx / (W >> 2); x = (idx % (W >> 2)) * 4; }
+    else if (idx < lq + cq) { c = 1; idx -= lq; y = idx / (W >> 3); x = (idx % (W >> 3)) * 4; }
+    else if (idx < lq + 2 * cq) { c = 2; idx -= lq + cq; y = idx / (W >> 3); x = (idx % (W >> 3)) * 4; }
+    else return;
+    const Pel* src = plane<Pel>(f, arena, f.pic, c);
+    Pel* dst = plane<Pel>(f, arena, f.pic2, c);
+    const int st = f.pic_stride[c];
+    const int pw = c ? W >> 1 : W, ph = c ? H >> 1 : H;
+    const uint8_t* fmap = arena + f.maps;
+    for (int k = 0; k < 4 && x + k < pw; k++) {
+        if (f.sao_enabled) sao_sample<Pel>(f, ctbs, slices, src, dst, st, pw, ph, c, x + k, y, fmap);
+        else dst[y * st + x + k] = src[y * st + x + k];
+    }
+}
+
+__global__ void __launch_bounds__(256) h2j_k3_sao(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                 const h2j_slice* slices, uint8_t* arena) {
+    const h2j_frame& f = frames[blockIdx.y];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    if (f.bit_depth == 8) sao_thread<uint8_t>(f, C, S, arena, idx);
+    else sao_thread<uint16_t>(f, C, S, arena, idx);
+}
+
+// ---------------------------------------------------------------- K4: JPEG
+template <typename Pel>
+DEVI int jpeg_sample(const h2j_frame& f, const uint8_t* arena, int c, int x, int y) {
+    const int shc = c ? 1 : 0;
+    const int pw = f.out_w >> shc, ph = f.out_h >> shc;
+    x = x < pw ? x : pw - 1;
+    y = y < ph ? y : ph - 1;
+    const Pel* p = reinterpret_cast<const Pel*>(arena + f.pic2) + f.pic_off[c];
+    int v = p[(y + (f.crop_y >> shc)) * f.pic_stride[c] + x + (f.crop_x >> shc)];
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    if (bd > 8) {
+        v = (v + (1 << (bd - 9))) >> (bd - 8);
+        v = v > 255 ? 255 : v;
+    }
+    return v;
+}
+
+template <typename Pel>
+DEVI long long mb_var(const h2j_frame& f, const uint8_t* arena, int mx, int my) {
+    unsigned s = 0, n = 0;
+    for (int j = 0; j < 16; j++)
+        for (int i = 0; i < 16; i++) {
+            const unsigned p = static_cast<unsigned>(jpeg_sample<Pel>(f, arena, 0, mx * 16 + i, my * 16 + j));
+            s += p;
+            n += p * p;
+        }
+    return static_cast<long long>((n - ((s * s) >> 8) + 500 + 128) >> 8);
+}
+
+__global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* frames, uint8_t* arena) {
+    const h2j_frame& f = frames[blockIdx.y];
+    const int mbw = (f.out_w + 15) >> 4, mbh = (f.out_h + 15) >> 4;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    long long v = 0;
+    if (idx < mbw * mbh) {
+        v = f.bit_depth == 8 ? mb_var<uint8_t>(f, arena, idx % mbw, idx / mbw)
+                             : mb_var<uint16_t>(f, arena, idx % mbw, idx / mbw);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __shared__ long long part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const long long t = part[0] + part[1] + part[2] + part[3];
+        if (t) {
+            h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&js->var_sum), static_cast<unsigned long long>(t));
+        }
+    }
+}
+
+__constant__ uint8_t kMpeg1Intra[64] = {
+    8,  16, 19, 22, 26, 27, 29, 34, 16, 16, 22, 24, 27, 29, 34, 37, 19, 22, 26, 27, 29, 34,
+    34, 38, 22, 22, 26, 27, 29, 34, 37, 40, 22, 26, 27, 29, 32, 35, 40, 48, 26, 27, 29, 32,
+    35, 40, 48, 58, 26, 27, 29, 34, 38, 46, 56, 69, 27, 29, 35, 38, 46, 56, 69, 83};
+__constant__ uint8_t kZigzag[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Rate control of FFmpeg's one-pass RC for frame 0; IEEE
+// double with correctly rounded sqrt/div and no contraction, as on the host.
+__global__ void __launch_bounds__(64) h2j_k4b_ratecontrol(const h2j_frame* frames, uint8_t* arena) {
+#pragma clang fp contract(off)
+    const h2j_frame& f = frames[blockIdx.x];
+    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+    __shared__ int qs_sh;
+    if (threadIdx.x == 0) {
+        const double qp2l = 118.0, qs = 2.0 * 118.0;
+        const long long V = js->var_sum;
+        const int T = static_cast<int>(qp2l * 7.0 * __dsqrt_rn(static_cast<double>(V)) / qs);
+        const double bits = __dsqrt_rn(static_cast<double>(T) * qs) + 1.0;
+        double q = qs * static_cast<double>(T + 1) / (bits > 0.9 ? bits : 0.9);
+        q = 0.8 * q;
+        q = (0.0005 + q) / 1.0005;
+        q = q < 189.0 ? 189.0 : (q > 2926.0 ? 2926.0 : q);
+        const int lambda = static_cast<int>(q + 0.5);
+        int qscale = (lambda * 139 + 128 * 64) >> 14;
+        qscale = qscale < 2 ? 2 : (qscale > 31 ? 31 : qscale);
+        js->qscale = qscale;
+        js->lambda = lambda;
+        qs_sh = qscale;
+    }
+    __syncthreads();
+    const int qscale = qs_sh;
+    const int i = threadIdx.x;
+    int M = i == 0 ? 8 : ((kMpeg1Intra[i] * qscale) >> 3);
+    M = M > 255 ? 255 : M;
+    int q = (2 << 16) / (16 * M);
+    if (q == 0 || q == 128 * 256) q = 128 * 256 - 1;
+    js->dqt[i] = static_cast<uint8_t>(M);
+    js->q16[i] = static_cast<uint16_t>(q);
+    js->b16[i] = static_cast<uint16_t>((96 * 256 + (q >> 1)) / q);
+}
+
+DEVI int16_t sat16(int v) { return static_cast<int16_t>(v > 32767 ? 32767 : (v < -32768 ? -32768 : v)); }
+DEVI int16_t mulhi16(int a, int c) { return static_cast<int16_t>((a * c) >> 16); }
+
+// AP-922 FDCT (ff_fdct_sse2) restated in SURVEY.md A.4, on one 8x8 block
+DEVI void fdct_ap922(int16_t* b) {
+    int16_t t[64];
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        const int x0 = b[x], x1 = b[8 + x], x2 = b[16 + x], x3 = b[24 + x], x4 = b[32 + x], x5 = b[40 + x],
+                  x6 = b[48 + x], x7 = b[56 + x];
+        const int16_t t0 = sat16(sat16(x0 + x7) * 8), t1 = sat16(sat16(x1 + x6) * 8);
+        const int16_t t2 = sat16(sat16(x2 + x5) * 8), t3 = sat16(sat16(x3 + x4) * 8);
+        const int16_t tp03 = sat16(t0 + t3), tm03 = sat16(t0 - t3), tp12 = sat16(t1 + t2), tm12 = sat16(t1 - t2);
+        t[x] = sat16(tp03 + tp12);
+        t[32 + x] = sat16(tp03 - tp12);
+        t[16 + x] = static_cast<int16_t>(sat16(tm03 + mulhi16(tm12, 27146)) | 1);
+        t[48 + x] = static_cast<int16_t>(sat16(mulhi16(tm03, 27146) - tm12) | 1);
+        const int16_t d16 = sat16(sat16(x1 - x6) * 16), d25 = sat16(sat16(x2 - x5) * 16);
+        const int16_t tp65 = static_cast<int16_t>(mulhi16(sat16(d16 + d25), 23170) | 1);
+        const int16_t tm65 = mulhi16(sat16(d16 - d25), 23170);
+        const int16_t t4 = sat16(sat16(x3 - x4) * 8), t7 = sat16(sat16(x0 - x7) * 8);
+        const int16_t tp465 = sat16(t4 + tm65), tm465 = sat16(t4 - tm65);
+        const int16_t tp765 = sat16(t7 + tp65), tm765 = sat16(t7 - tp65);
+        t[8 + x] = static_cast<int16_t>(sat16(tp765 + mulhi16(tp465, 13036)) | 1);
+        t[56 + x] = sat16(mulhi16(tp765, 13036) - tp465);
+        t[24 + x] = sat16(tm765 - sat16(mulhi16(tm465, -21746) + tm465));
+        t[40 + x] = sat16(sat16(mulhi16(tm765, -21746) + tm765) + tm465);
+    }
+    const int kRow[4][7] = {{22725, 21407, 19266, 16384, 12873, 8867, 4520},
+                            {31521, 29692, 26722, 22725, 17855, 12299, 6270},
+                            {29692, 27969, 25172, 21407, 16819, 11585, 5906},
+                            {26722, 25172, 22654, 19266, 15137, 10426, 5315}};
+    const int kSel[8] = {0, 1, 2, 3, 0, 3, 2, 1};
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int* cc = kRow[kSel[r]];
+        const int C1 = cc[0], C2 = cc[1], C3 = cc[2], C4 = cc[3], C5 = cc[4], C6 = cc[5], C7 = cc[6];
+        const int16_t* x = t + r * 8;
+        const int s0 = sat16(x[0] + x[7]), s1 = sat16(x[1] + x[6]), s2 = sat16(x[2] + x[5]), s3 = sat16(x[3] + x[4]);
+        const int d0 = sat16(x[0] - x[7]), d1 = sat16(x[1] - x[6]), d2 = sat16(x[2] - x[5]), d3 = sat16(x[3] - x[4]);
+        int Y[8];
+        Y[0] = C4 * s0 + C4 * s1 + C4 * s2 + C4 * s3;
+        Y[4] = C4 * s0 - C4 * s1 - C4 * s2 + C4 * s3;
+        Y[2] = C2 * s0 + C6 * s1 - C6 * s2 - C2 * s3;
+        Y[6] = C6 * s0 - C2 * s1 + C2 * s2 - C6 * s3;
+        Y[1] = C1 * d0 + C3 * d1 + C5 * d2 + C7 * d3;
+        Y[3] = C3 * d0 - C7 * d1 - C1 * d2 - C5 * d3;
+        Y[5] = C5 * d0 - C1 * d1 + C7 * d2 + C3 * d3;
+        Y[7] = C7 * d0 - C5 * d1 + C3 * d2 - C1 * d3;
+#pragma unroll
+        for (int k = 0; k < 8; k++) b[r * 8 + k] = sat16((Y[k] + 65536) >> 17);
+    }
+}
+
+template <typename Pel>
+DEVI void jpeg_block(const h2j_frame& f, uint8_t* arena, int bi) {
+    const int mbw = (f.out_w + 15) >> 4;
+    const int mcu = bi / 6, b = bi % 6;
+    const int mx = mcu % mbw, my = mcu / mbw;
+    int c, x0, y0;
+    if (b < 4) { c = 0; x0 = mx * 16 + (b & 1) * 8; y0 = my * 16 + (b >> 1) * 8; }
+    else { c = b - 3; x0 = mx * 8; y0 = my * 8; }
+    int16_t blk[64];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) blk[j * 8 + i] = static_cast<int16_t>(jpeg_sample<Pel>(f, arena, c, x0 + i, y0 + j));
+    fdct_ap922(blk);
+    const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
+    int16_t out[64];
+    out[0] = static_cast<int16_t>(((blk[0] >> 2) + 8) / 16);
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+        const int i = kZigzag[k];
+        const int X = blk[i];
+        const unsigned a = static_cast<unsigned>(X < 0 ? -X : X);
+        unsigned tt = a + js->b16[i];
+        tt = tt > 65535u ? 65535u : tt;
+        int L = static_cast<int>((tt * js->q16[i]) >> 16);
+        L = L > 1023 ? 1023 : L;
+        out[k] = static_cast<int16_t>(X < 0 ? -L : L);
+    }
+    int16_t* dst = reinterpret_cast<int16_t*>(arena + f.jcoef) + static_cast<size_t>(bi) * 64;
+#pragma unroll
+    for (int k = 0; k < 64; k += 8) {
+        int4 v;
+        v.x = (static_cast<uint16_t>(out[k]) | (static_cast<uint32_t>(static_cast<uint16_t>(out[k + 1])) << 16));
+        v.y = (static_cast<uint16_t>(out[k + 2]) | (static_cast<uint32_t>(static_cast<uint16_t>(out[k + 3])) << 16));
+        v.z = (static_cast<uint16_t>(out[k + 4]) | (static_cast<uint32_t>(static_cast<uint16_t>(out[k + 5])) << 16));
+        v.w = (static_cast<uint16_t>(out[k + 6]) | (static_cast<uint32_t>(static_cast<uint16_t>(out[k + 7])) << 16));
+        *reinterpret_cast<int4*>(dst + k) = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) h2j_k4c_fdct_quant(const h2j_frame* frames, uint8_t* arena) {
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
+    const int bi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bi >= nblk) return;
+    if (f.bit_depth == 8) jpeg_block<uint8_t>(f, arena, bi);
+    else jpeg_block<uint16_t>(f, arena, bi);
+}
+
+DEVI int nbits16(int v) {
+    const unsigned a = static_cast<unsigned>(v < 0 ? -v : v);
+    return a ? 32 - __clz(a) : 0;
+}
+
+__global__ void __launch_bounds__(256) h2j_k4d_histogram(const h2j_frame* frames, uint8_t* arena) {
+    __shared__ unsigned hist[4][256];
+    for (int i = threadIdx.x; i < 1024; i += 256) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
+    const int bi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bi < nblk) {
+        const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+        const int16_t* z = co + static_cast<size_t>(bi) * 64;
+        const int mcu = bi / 6, b = bi % 6;
+        int prev;
+        if (b < 4) prev = b > 0 ? co[static_cast<size_t>(bi - 1) * 64] : (mcu > 0 ? co[static_cast<size_t>(bi - 3) * 64] : 128);
+        else prev = mcu > 0 ? co[static_cast<size_t>(bi - 6) * 64] : 128;
+        const int tab = b < 4 ? 0 : 1;
+        atomicAdd(&hist[tab][nbits16(z[0] - prev)], 1u);
+        int last = 0;
+        for (int i = 63; i >= 1; i--)
+            if (z[i]) { last = i; break; }
+        int run = 0;
+        for (int i = 1; i <= last; i++) {
+            const int v = z[i];
+            if (!v) { run++; continue; }
+            while (run >= 16) { atomicAdd(&hist[2 + tab][0xF0], 1u); run -= 16; }
+            atomicAdd(&hist[2 + tab][(run << 4) | nbits16(v)], 1u);
+            run = 0;
+        }
+        if (last < 63) atomicAdd(&hist[2 + tab][0], 1u);
+    }
+    __syncthreads();
+    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const unsigned v = (&hist[0][0])[i];
+        if (v) atomicAdd(&js->hist[i >> 8][i & 255], v);
+    }
+}
+
+thread_local char g_err[256] = {0};
+
+int check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return -static_cast<int>(e) - 1000;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+const char* h2j_gpu_last_error(void) { return g_err; }
+
+int h2j_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+int h2j_gpu_set_device(int device) { return check(hipSetDevice(device), "hipSetDevice"); }
+void* h2j_gpu_malloc(size_t bytes) {
+    void* p = nullptr;
+    if (check(hipMalloc(&p, bytes), "hipMalloc")) return nullptr;
+    return p;
+}
+int h2j_gpu_free(void* p) { return check(hipFree(p), "hipFree"); }
+void* h2j_gpu_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (check(hipHostMalloc(&p, bytes, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
+    return p;
+}
+int h2j_gpu_host_free(void* p) { return check(hipHostFree(p), "hipHostFree"); }
+void* h2j_gpu_stream_create(void) {
+    hipStream_t s = nullptr;
+    if (check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate")) return nullptr;
+    return s;
+}
+int h2j_gpu_stream_destroy(void* s) { return check(hipStreamDestroy(static_cast<hipStream_t>(s)), "hipStreamDestroy"); }
+int h2j_gpu_stream_sync(void* s) { return check(hipStreamSynchronize(static_cast<hipStream_t>(s)), "hipStreamSynchronize"); }
+int h2j_gpu_memcpy_h2d(void* dst, const void* src, size_t n, void* s) {
+    return check(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, static_cast<hipStream_t>(s)), "hipMemcpyH2D");
+}
+int h2j_gpu_memcpy_d2h(void* dst, const void* src, size_t n, void* s) {
+    return check(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, static_cast<hipStream_t>(s)), "hipMemcpyD2H");
+}
+int h2j_gpu_memset(void* dst, int v, size_t n, void* s) {
+    return check(hipMemsetAsync(dst, v, n, static_cast<hipStream_t>(s)), "hipMemsetAsync");
+}
+void* h2j_gpu_event_create(void) {
+    hipEvent_t e = nullptr;
+    if (check(hipEventCreate(&e), "hipEventCreate")) return nullptr;
+    return e;
+}
+int h2j_gpu_event_destroy(void* e) { return check(hipEventDestroy(static_cast<hipEvent_t>(e)), "hipEventDestroy"); }
+int h2j_gpu_event_record(void* e, void* s) {
+    return check(hipEventRecord(static_cast<hipEvent_t>(e), static_cast<hipStream_t>(s)), "hipEventRecord");
+}
+float h2j_gpu_event_elapsed_ms(void* a, void* b) {
+    float ms = -1.f;
+    if (check(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)), "hipEventElapsedTime"))
+        return -1.f;
+    return ms;
+}
+
+int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(h2j_k1_recon, dim3(b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
+                       b->slices, b->sl, b->arena);
+    return check(hipGetLastError(), "h2j_k1_recon");
+}
+
+int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int maps = ((b->max_w + 3) >> 2) * ((b->max_h + 3) >> 2);
+    dim3 grid((maps + 255) / 256, b->nframes);
+    hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
+    int r = check(hipGetLastError(), "h2j_k2_deblock(v)");
+    if (r) return r;
+    hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
+    return check(hipGetLastError(), "h2j_k2_deblock(h)");
+}
+
+int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int items = (b->max_w >> 2) * b->max_h + 2 * (b->max_w >> 3) * (b->max_h >> 1);
+    dim3 grid((items + 255) / 256, b->nframes);
+    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena);
+    return check(hipGetLastError(), "h2j_k3_sao");
+}
+
+int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int mbs = b->max_mcu;
+    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    int r = check(hipGetLastError(), "h2j_k4a_variance");
+    if (r) return r;
+    hipLaunchKernelGGL(h2j_k4b_ratecontrol, dim3(b->nframes), dim3(64), 0, s, b->frames, b->arena);
+    r = check(hipGetLastError(), "h2j_k4b_ratecontrol");
+    if (r) return r;
+    const int nblk = mbs * 6;
+    hipLaunchKernelGGL(h2j_k4c_fdct_quant, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    r = check(hipGetLastError(), "h2j_k4c_fdct_quant");
+    if (r) return r;
+    hipLaunchKernelGGL(h2j_k4d_histogram, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    return check(hipGetLastError(), "h2j_k4d_histogram");
+}
+
+}  // extern "C"

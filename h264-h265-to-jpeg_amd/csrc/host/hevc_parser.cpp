@@ -1,0 +1,1293 @@
+// HEVC (H.265 v1 Main/Main10, 4:2:0) intra entropy decoding on the host.
+//
+// Replaces the parsing half of FFmpeg's hevc decoder that the reference
+// reaches through avcodec_send_packet (/root/reference/src/Decoder.cpp:324):
+// VPS/SPS/PPS/slice header (H.265 7.3), CABAC slice data (9.3) including
+// SAO syntax, coding quadtree, intra mode derivation (8.4.2/8.4.3), QP
+// derivation (8.6.1) and residual_coding.  Instead of reconstructing, it
+// emits one h2j_tu per transform block plus the sparse coefficient levels
+// (include/h2j_jobs.h); dequantisation, transforms, intra prediction and
+// the loop filters run on the GPU.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "bitstream.h"
+#include "cabac.h"
+#include "job.h"
+
+namespace h2j {
+namespace {
+
+enum {
+    C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_PART_MODE = 6,
+    C_PREV_INTRA = 7, C_CHROMA_MODE = 8, C_SPLIT_TF = 9, C_CBF_LUMA = 12, C_CBF_CHROMA = 14,
+    C_TSKIP = 18, C_LAST_X = 20, C_LAST_Y = 38, C_CSBF = 56, C_SIG = 60, C_GT1 = 104,
+    C_GT2 = 128, C_QP_DELTA = 134, NUM_CTX = 136
+};
+
+// initValue for initType 0 (I slices), H.265 Tables 9-5 .. 9-37
+const uint8_t kInitI[NUM_CTX] = {
+    153, 200, 139, 141, 157, 154, 184, 184, 63, 153, 138, 138, 111, 141, 94, 138, 182, 154,
+    139, 139,
+    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+    91, 171, 134, 141,
+    111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141,
+    179, 153, 125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153,
+    136, 139, 111, 136, 139, 111, 141, 111,
+    140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166,
+    182, 140, 227, 122, 197,
+    138, 153, 136, 167, 152, 152,
+    154, 154};
+
+struct Sps {
+    bool valid = false;
+    int chroma_format_idc = 0, width = 0, height = 0;
+    int conf_l = 0, conf_r = 0, conf_t = 0, conf_b = 0;
+    int bit_depth = 8, bit_depth_c = 8, log2_max_poc_lsb = 4;
+    int log2_min_cb = 3, log2_ctb = 4, log2_min_tb = 2, log2_max_tb = 5, max_th_depth_intra = 0;
+    int scaling_list_enabled = 0;
+    uint8_t sl[4][6][64];
+    uint8_t sl_dc[4][6];
+    int sao = 0, pcm = 0, pcm_bd = 8, pcm_bd_c = 8, log2_min_pcm = 0, log2_max_pcm = 0, pcm_lf_disabled = 0;
+    int num_st_rps = 0;
+    int st_num_delta[65];
+    int long_term_present = 0, num_lt_sps = 0, temporal_mvp = 0, strong_intra_smoothing = 0;
+};
+
+struct Pps {
+    bool valid = false;
+    int sps_id = 0, dependent_slices = 0, output_flag_present = 0, num_extra_bits = 0, sign_hiding = 0;
+    int init_qp = 26, transform_skip = 0, cu_qp_delta = 0, diff_cu_qp_delta_depth = 0;
+    int cb_qp_offset = 0, cr_qp_offset = 0, slice_chroma_qp_present = 0, transquant_bypass = 0;
+    int tiles = 0, wpp = 0, ntc = 1, ntr = 1, uniform = 1, lf_across_tiles = 1;
+    int col_w[64], row_h[64];
+    int lf_across_slices = 0, deblock_override = 0, deblock_disabled = 0, beta_offset = 0, tc_offset = 0;
+    int sl_present = 0;
+    uint8_t sl[4][6][64];
+    uint8_t sl_dc[4][6];
+    int slice_header_ext = 0;
+};
+
+struct SliceHdr {
+    int first_in_pic = 0, dependent = 0, address = 0, slice_addr_rs = 0, pps_id = 0, type = 0;
+    int sao_luma = 0, sao_chroma = 0, qp_delta = 0, cb_qp_offset = 0, cr_qp_offset = 0;
+    int deblock_disabled = 0, beta_offset = 0, tc_offset = 0, lf_across_slices = 0, slice_qp = 26;
+};
+
+const uint8_t kSlIntra[64] = {
+    16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 16, 17, 16, 17, 18, 17, 18, 18, 17, 18, 21,
+    19, 20, 21, 20, 19, 21, 24, 22, 22, 24, 24, 22, 22, 24, 25, 25, 27, 30, 27, 25, 25, 29,
+    31, 35, 35, 31, 29, 36, 41, 44, 41, 36, 47, 54, 54, 47, 65, 70, 65, 88, 88, 115};
+const uint8_t kSlInter[64] = {
+    16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17, 18, 18, 18, 18, 18, 18, 20,
+    20, 20, 20, 20, 20, 20, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 28,
+    28, 28, 28, 28, 28, 33, 33, 33, 33, 33, 41, 41, 41, 41, 54, 54, 54, 71, 71, 91};
+
+void sl_default(uint8_t sl[4][6][64], uint8_t dc[4][6]) {
+    for (int m = 0; m < 6; m++) {
+        std::memset(sl[0][m], 16, 16);
+        for (int s = 1; s < 4; s++) {
+            std::memcpy(sl[s][m], m < 3 ? kSlIntra : kSlInter, 64);
+            dc[s][m] = 16;
+        }
+        dc[0][m] = 16;
+    }
+}
+
+void parse_scaling_list(BitReader& b, uint8_t sl[4][6][64], uint8_t dc[4][6]) {
+    for (int sizeId = 0; sizeId < 4; sizeId++)
+        for (int m = 0; m < 6; m += (sizeId == 3) ? 3 : 1) {
+            int n = sizeId == 0 ? 16 : 64;
+            if (!b.u(1)) {
+                int delta = static_cast<int>(b.ue());
+                if (delta == 0) {
+                    if (sizeId == 0) std::memset(sl[0][m], 16, 16);
+                    else std::memcpy(sl[sizeId][m], m < 3 ? kSlIntra : kSlInter, 64);
+                    dc[sizeId][m] = 16;
+                } else {
+                    int ref = m - delta * (sizeId == 3 ? 3 : 1);
+                    if (ref < 0) ref = 0;
+                    std::memcpy(sl[sizeId][m], sl[sizeId][ref], static_cast<size_t>(n));
+                    dc[sizeId][m] = dc[sizeId][ref];
+                }
+            } else {
+                int next = 8;
+                if (sizeId > 1) {
+                    next = b.se() + 8;
+                    dc[sizeId][m] = static_cast<uint8_t>(next);
+                }
+                for (int i = 0; i < n; i++) {
+                    next = (next + b.se() + 256) % 256;
+                    sl[sizeId][m][i] = static_cast<uint8_t>(next);
+                }
+                if (sizeId <= 1) dc[sizeId][m] = sl[sizeId][m][0];
+            }
+        }
+}
+
+void skip_ptl(BitReader& b, int msl) {
+    b.u(8); b.u(32); b.u(4); b.u(32); b.u(11); b.u(1); b.u(8);
+    int pp[8] = {0}, lp[8] = {0};
+    for (int i = 0; i < msl; i++) { pp[i] = static_cast<int>(b.u(1)); lp[i] = static_cast<int>(b.u(1)); }
+    if (msl > 0)
+        for (int i = msl; i < 8; i++) b.u(2);
+    for (int i = 0; i < msl; i++) {
+        if (pp[i]) { b.u(32); b.u(32); b.u(24); }
+        if (lp[i]) b.u(8);
+    }
+}
+
+bool parse_st_rps(BitReader& b, Sps& s, int idx) {
+    int inter = 0;
+    if (idx != 0) inter = static_cast<int>(b.u(1));
+    if (inter) {
+        int delta_idx = 1;
+        if (idx == s.num_st_rps) delta_idx = static_cast<int>(b.ue()) + 1;
+        b.u(1);
+        b.ue();
+        int ref = idx - delta_idx;
+        if (ref < 0) return false;
+        int cnt = 0;
+        for (int j = 0; j <= s.st_num_delta[ref]; j++) {
+            int used = static_cast<int>(b.u(1)), use_delta = 1;
+            if (!used) use_delta = static_cast<int>(b.u(1));
+            if (used || use_delta) cnt++;
+        }
+        s.st_num_delta[idx] = cnt;
+    } else {
+        int neg = static_cast<int>(b.ue()), pos = static_cast<int>(b.ue());
+        if (neg > 16 || pos > 16) return false;
+        for (int i = 0; i < neg + pos; i++) { b.ue(); b.u(1); }
+        s.st_num_delta[idx] = neg + pos;
+    }
+    return true;
+}
+
+int parse_sps(BitReader& b, Sps* tab) {
+    b.u(4);
+    int msl = static_cast<int>(b.u(3));
+    b.u(1);
+    skip_ptl(b, msl);
+    uint32_t id = b.ue();
+    if (id > 15) return -1;
+    Sps& s = tab[id];
+    s = Sps();
+    s.chroma_format_idc = static_cast<int>(b.ue());
+    if (s.chroma_format_idc == 3) b.u(1);
+    s.width = static_cast<int>(b.ue());
+    s.height = static_cast<int>(b.ue());
+    if (b.u(1)) {
+        int sw = (s.chroma_format_idc == 1 || s.chroma_format_idc == 2) ? 2 : 1;
+        int shh = s.chroma_format_idc == 1 ? 2 : 1;
+        s.conf_l = static_cast<int>(b.ue()) * sw;
+        s.conf_r = static_cast<int>(b.ue()) * sw;
+        s.conf_t = static_cast<int>(b.ue()) * shh;
+        s.conf_b = static_cast<int>(b.ue()) * shh;
+    }
+    s.bit_depth = static_cast<int>(b.ue()) + 8;
+    s.bit_depth_c = static_cast<int>(b.ue()) + 8;
+    s.log2_max_poc_lsb = static_cast<int>(b.ue()) + 4;
+    int sub = static_cast<int>(b.u(1));
+    for (int i = sub ? 0 : msl; i <= msl; i++) { b.ue(); b.ue(); b.ue(); }
+    s.log2_min_cb = static_cast<int>(b.ue()) + 3;
+    s.log2_ctb = s.log2_min_cb + static_cast<int>(b.ue());
+    s.log2_min_tb = static_cast<int>(b.ue()) + 2;
+    s.log2_max_tb = s.log2_min_tb + static_cast<int>(b.ue());
+    b.ue();
+    s.max_th_depth_intra = static_cast<int>(b.ue());
+    s.scaling_list_enabled = static_cast<int>(b.u(1));
+    sl_default(s.sl, s.sl_dc);
+    if (s.scaling_list_enabled && b.u(1)) parse_scaling_list(b, s.sl, s.sl_dc);
+    b.u(1);
+    s.sao = static_cast<int>(b.u(1));
+    s.pcm = static_cast<int>(b.u(1));
+    if (s.pcm) {
+        s.pcm_bd = static_cast<int>(b.u(4)) + 1;
+        s.pcm_bd_c = static_cast<int>(b.u(4)) + 1;
+        s.log2_min_pcm = static_cast<int>(b.ue()) + 3;
+        s.log2_max_pcm = s.log2_min_pcm + static_cast<int>(b.ue());
+        s.pcm_lf_disabled = static_cast<int>(b.u(1));
+    }
+    s.num_st_rps = static_cast<int>(b.ue());
+    if (s.num_st_rps > 64) return -1;
+    for (int i = 0; i < s.num_st_rps; i++)
+        if (!parse_st_rps(b, s, i)) return -1;
+    s.long_term_present = static_cast<int>(b.u(1));
+    if (s.long_term_present) {
+        s.num_lt_sps = static_cast<int>(b.ue());
+        for (int i = 0; i < s.num_lt_sps; i++) { b.u(s.log2_max_poc_lsb); b.u(1); }
+    }
+    s.temporal_mvp = static_cast<int>(b.u(1));
+    s.strong_intra_smoothing = static_cast<int>(b.u(1));
+    if (s.chroma_format_idc != 1) return -2;
+    if (s.log2_ctb > 6 || s.log2_ctb < 4 || s.log2_max_tb > 5 || s.bit_depth > 12 || s.bit_depth_c != s.bit_depth)
+        return -3;
+    if (s.width <= 0 || s.height <= 0 || s.width > 8192 || s.height > 8192) return -4;
+    s.valid = true;
+    return 0;
+}
+
+int parse_pps(BitReader& b, Pps* tab) {
+    uint32_t id = b.ue();
+    if (id > 63) return -1;
+    Pps& p = tab[id];
+    p = Pps();
+    p.sps_id = static_cast<int>(b.ue());
+    p.dependent_slices = static_cast<int>(b.u(1));
+    p.output_flag_present = static_cast<int>(b.u(1));
+    p.num_extra_bits = static_cast<int>(b.u(3));
+    p.sign_hiding = static_cast<int>(b.u(1));
+    b.u(1);
+    b.ue();
+    b.ue();
+    p.init_qp = 26 + b.se();
+    b.u(1);  // constrained_intra_pred (no effect in all-intra pictures)
+    p.transform_skip = static_cast<int>(b.u(1));
+    p.cu_qp_delta = static_cast<int>(b.u(1));
+    if (p.cu_qp_delta) p.diff_cu_qp_delta_depth = static_cast<int>(b.ue());
+    p.cb_qp_offset = b.se();
+    p.cr_qp_offset = b.se();
+    p.slice_chroma_qp_present = static_cast<int>(b.u(1));
+    b.u(1);
+    b.u(1);
+    p.transquant_bypass = static_cast<int>(b.u(1));
+    p.tiles = static_cast<int>(b.u(1));
+    p.wpp = static_cast<int>(b.u(1));
+    if (p.tiles) {
+        p.ntc = static_cast<int>(b.ue()) + 1;
+        p.ntr = static_cast<int>(b.ue()) + 1;
+        if (p.ntc > 64 || p.ntr > 64) return -1;
+        p.uniform = static_cast<int>(b.u(1));
+        if (!p.uniform) {
+            for (int i = 0; i < p.ntc - 1; i++) p.col_w[i] = static_cast<int>(b.ue()) + 1;
+            for (int i = 0; i < p.ntr - 1; i++) p.row_h[i] = static_cast<int>(b.ue()) + 1;
+        }
+        p.lf_across_tiles = static_cast<int>(b.u(1));
+    }
+    p.lf_across_slices = static_cast<int>(b.u(1));
+    if (b.u(1)) {
+        p.deblock_override = static_cast<int>(b.u(1));
+        p.deblock_disabled = static_cast<int>(b.u(1));
+        if (!p.deblock_disabled) {
+            p.beta_offset = b.se() * 2;
+            p.tc_offset = b.se() * 2;
+        }
+    }
+    p.sl_present = static_cast<int>(b.u(1));
+    if (p.sl_present) {
+        sl_default(p.sl, p.sl_dc);
+        parse_scaling_list(b, p.sl, p.sl_dc);
+    }
+    b.u(1);
+    b.ue();
+    p.slice_header_ext = static_cast<int>(b.u(1));
+    p.valid = true;
+    return 0;
+}
+
+uint8_t g_scan_diag[4][64][2], g_scan_hor[4][64][2], g_scan_ver[4][64][2];
+uint8_t g_diag_pos4[16];  // raster (y*4+x) of 4x4 diag scan
+uint8_t g_diag_pos8[64];
+bool g_scans_ready = false;
+
+void init_scans() {
+    if (g_scans_ready) return;
+    for (int l = 0; l < 4; l++) {
+        int bs = 1 << l, i = 0, x = 0, y = 0;
+        while (i < bs * bs) {
+            while (y >= 0) {
+                if (x < bs && y < bs) {
+                    g_scan_diag[l][i][0] = static_cast<uint8_t>(x);
+                    g_scan_diag[l][i][1] = static_cast<uint8_t>(y);
+                    i++;
+                }
+                y--;
+                x++;
+            }
+            y = x;
+            x = 0;
+        }
+        i = 0;
+        for (y = 0; y < bs; y++)
+            for (x = 0; x < bs; x++, i++) {
+                g_scan_hor[l][i][0] = static_cast<uint8_t>(x);
+                g_scan_hor[l][i][1] = static_cast<uint8_t>(y);
+            }
+        i = 0;
+        for (x = 0; x < bs; x++)
+            for (y = 0; y < bs; y++, i++) {
+                g_scan_ver[l][i][0] = static_cast<uint8_t>(x);
+                g_scan_ver[l][i][1] = static_cast<uint8_t>(y);
+            }
+    }
+    for (int i = 0; i < 16; i++) g_diag_pos4[i] = static_cast<uint8_t>(g_scan_diag[2][i][1] * 4 + g_scan_diag[2][i][0]);
+    for (int i = 0; i < 64; i++) g_diag_pos8[i] = static_cast<uint8_t>(g_scan_diag[3][i][1] * 8 + g_scan_diag[3][i][0]);
+    g_scans_ready = true;
+}
+
+int chroma_qp_table(int qpi) {
+    static const int t[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    return t[qpi - 30];
+}
+
+class HevcParser {
+public:
+    explicit HevcParser(FrameJob& job) : job_(job) {}
+    int run(const uint8_t* data, size_t size);
+
+private:
+    FrameJob& job_;
+    Sps sps_[16];
+    Pps pps_[64];
+    const Sps* s_ = nullptr;
+    const Pps* p_ = nullptr;
+    std::vector<SliceHdr> sh_;
+    std::vector<uint8_t> rbsp_;
+    std::vector<uint8_t> slice_data_;
+    // picture geometry
+    int W = 0, H = 0, log2ctb = 0, ctbs = 0, ctbW = 0, ctbH = 0, nctb = 0, mw = 0, mh = 0;
+    int qpbd = 0;
+    // maps (4x4 granularity)
+    std::vector<int8_t> qp_;
+    std::vector<uint8_t> ipm_, ctd_;
+    std::vector<int> ctb_addr_rs_, ctb_slice_, rs2ts_, ts2rs_, tile_id_, col_bd_;
+    // slice decode state
+    const SliceHdr* cur_ = nullptr;
+    int cur_idx_ = 0;
+    Cabac cc_;
+    const uint8_t* end_ = nullptr;
+    uint8_t ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];
+    bool have_ds_ = false;
+    int qp_y_ = 0, qg_pred_ = 0, qpd_val_ = 0, last_cu_qp_ = 0;
+    bool is_qpd_coded_ = false, first_qg_ = true;
+    int cu_bypass_ = 0;
+    int cu_tu_begin_ = 0;
+    int err_ = 0;
+
+    int parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, const SliceHdr* prev);
+    void setup_picture();
+    void setup_tiles();
+    int decode_slice_data(int shi, const uint8_t* p, const uint8_t* end);
+    void ctb_start_contexts(int rs, int ts, bool first);
+    void init_contexts(int qp) {
+        for (int i = 0; i < NUM_CTX; i++) {
+            int iv = kInitI[i];
+            ctx_[i] = cabac_init_state((iv >> 4) * 5 - 45, ((iv & 15) << 3) - 16, qp);
+        }
+    }
+    bool same_region(int xc, int yc, int xn, int yn) const {
+        if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
+        int cn = (yn >> log2ctb) * ctbW + (xn >> log2ctb);
+        int cc = (yc >> log2ctb) * ctbW + (xc >> log2ctb);
+        if (ctb_slice_[cn] < 0) return false;
+        return ctb_addr_rs_[cn] == ctb_addr_rs_[cc] && tile_id_[rs2ts_[cn]] == tile_id_[rs2ts_[cc]];
+    }
+    void qg_start(int xq, int yq);
+    void parse_sao(int rx, int ry);
+    void coding_quadtree(int x0, int y0, int log2cb, int depth);
+    void coding_unit(int x0, int y0, int log2cb);
+    void transform_tree(int x0, int y0, int xb, int yb, int log2n, int depth, int blk, int max_depth,
+                        int intra_split, int pcb, int pcr, int cm, int cux, int cuy, int log2cb);
+    void transform_unit(int x0, int y0, int xb, int yb, int log2n, int blk, int cbf_l, int cbf_cb,
+                        int cbf_cr, int cm, int cux, int cuy, int log2cb);
+    void residual(int log2n, int c, int mode, h2j_tu& tu);
+    void emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int pred_mode_for_scan);
+    uint8_t edge_flags(int x0, int y0) const;
+    void pcm_sample(int x0, int y0, int log2cb);
+    void set_map(std::vector<uint8_t>& m, int x0, int y0, int n, uint8_t v) {
+        int ye = std::min((y0 + n) >> 2, mh), xe = std::min((x0 + n) >> 2, mw);
+        for (int y = y0 >> 2; y < ye; y++) std::memset(&m[y * mw + (x0 >> 2)], v, static_cast<size_t>(xe - (x0 >> 2)));
+    }
+    void set_qp(int x0, int y0, int n, int qp) {
+        int ye = std::min((y0 + n) >> 2, mh), xe = std::min((x0 + n) >> 2, mw);
+        for (int y = y0 >> 2; y < ye; y++) std::memset(&qp_[y * mw + (x0 >> 2)], qp & 0xFF, static_cast<size_t>(xe - (x0 >> 2)));
+    }
+    int dec(int ctx) { return cc_.decision(ctx_[ctx]); }
+};
+
+int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, const SliceHdr* prev) {
+    sh = SliceHdr();
+    sh.first_in_pic = static_cast<int>(b.u(1));
+    if (nal_type >= 16 && nal_type <= 23) b.u(1);
+    sh.pps_id = static_cast<int>(b.ue());
+    if (sh.pps_id > 63 || !pps_[sh.pps_id].valid) return -1;
+    const Pps& p = pps_[sh.pps_id];
+    if (p.sps_id > 15 || !sps_[p.sps_id].valid) return -1;
+    const Sps& s = sps_[p.sps_id];
+    if (!sh.first_in_pic) {
+        if (p.dependent_slices) sh.dependent = static_cast<int>(b.u(1));
+        int cs = 1 << s.log2_ctb;
+        int n = ((s.width + cs - 1) / cs) * ((s.height + cs - 1) / cs);
+        sh.address = static_cast<int>(b.u(ceil_log2(n)));
+        if (sh.address >= n) return -1;
+    }
+    if (sh.dependent) {
+        if (!prev) return -1;
+        int addr = sh.address, first = sh.first_in_pic;
+        sh = *prev;
+        sh.address = addr;
+        sh.dependent = 1;
+        sh.first_in_pic = first;
+    } else {
+        sh.slice_addr_rs = sh.address;
+        for (int i = 0; i < p.num_extra_bits; i++) b.u(1);
+        sh.type = static_cast<int>(b.ue());
+        if (p.output_flag_present) b.u(1);
+        if (nal_type != 19 && nal_type != 20) {
+            b.u(s.log2_max_poc_lsb);
+            int sps_flag = static_cast<int>(b.u(1));
+            if (!sps_flag) {
+                Sps tmp = s;
+                if (!parse_st_rps(b, tmp, s.num_st_rps)) return -1;
+            } else if (s.num_st_rps > 1) {
+                b.u(ceil_log2(s.num_st_rps));
+            }
+            if (s.long_term_present) {
+                int nsps = 0;
+                if (s.num_lt_sps > 0) nsps = static_cast<int>(b.ue());
+                int npics = static_cast<int>(b.ue());
+                for (int i = 0; i < nsps + npics; i++) {
+                    if (i < nsps) {
+                        if (s.num_lt_sps > 1) b.u(ceil_log2(s.num_lt_sps));
+                    } else {
+                        b.u(s.log2_max_poc_lsb);
+                        b.u(1);
+                    }
+                    if (b.u(1)) b.ue();
+                }
+            }
+            if (s.temporal_mvp) b.u(1);
+        }
+        if (s.sao) {
+            sh.sao_luma = static_cast<int>(b.u(1));
+            sh.sao_chroma = static_cast<int>(b.u(1));
+        }
+        if (sh.type != 2) return -2;
+        sh.qp_delta = b.se();
+        if (p.slice_chroma_qp_present) {
+            sh.cb_qp_offset = b.se();
+            sh.cr_qp_offset = b.se();
+        }
+        int override_ = 0;
+        if (p.deblock_override) override_ = static_cast<int>(b.u(1));
+        sh.deblock_disabled = p.deblock_disabled;
+        sh.beta_offset = p.beta_offset;
+        sh.tc_offset = p.tc_offset;
+        if (override_) {
+            sh.deblock_disabled = static_cast<int>(b.u(1));
+            if (!sh.deblock_disabled) {
+                sh.beta_offset = b.se() * 2;
+                sh.tc_offset = b.se() * 2;
+            }
+        }
+        sh.lf_across_slices = p.lf_across_slices;
+        if (p.lf_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblock_disabled))
+            sh.lf_across_slices = static_cast<int>(b.u(1));
+        sh.slice_qp = p.init_qp + sh.qp_delta;
+        if (sh.slice_qp < -6 * (s.bit_depth - 8) || sh.slice_qp > 51) return -1;
+    }
+    if (p.tiles || p.wpp) {
+        int ne = static_cast<int>(b.ue());
+        if (ne > 0) {
+            int len = static_cast<int>(b.ue()) + 1;
+            if (len > 32) return -1;
+            for (int i = 0; i < ne; i++) b.u(len);
+        }
+    }
+    if (p.slice_header_ext) {
+        int len = static_cast<int>(b.ue());
+        for (int i = 0; i < len; i++) b.u(8);
+    }
+    b.u(1);
+    b.align();
+    return b.overrun() ? -1 : 0;
+}
+
+void HevcParser::setup_picture() {
+    W = s_->width;
+    H = s_->height;
+    log2ctb = s_->log2_ctb;
+    ctbs = 1 << log2ctb;
+    ctbW = (W + ctbs - 1) >> log2ctb;
+    ctbH = (H + ctbs - 1) >> log2ctb;
+    nctb = ctbW * ctbH;
+    mw = (W + 3) >> 2;
+    mh = (H + 3) >> 2;
+    qpbd = 6 * (s_->bit_depth - 8);
+    qp_.assign(static_cast<size_t>(mw) * mh, 0);
+    ipm_.assign(static_cast<size_t>(mw) * mh, 1);
+    ctd_.assign(static_cast<size_t>(mw) * mh, 0);
+    ctb_addr_rs_.assign(nctb, -1);
+    ctb_slice_.assign(nctb, -1);
+    rs2ts_.assign(nctb, 0);
+    ts2rs_.assign(nctb, 0);
+    tile_id_.assign(nctb, 0);
+    setup_tiles();
+    job_.ctbs.assign(nctb, h2j_ctb());
+    for (int rs = 0; rs < nctb; rs++) {
+        job_.ctbs[rs].ts = static_cast<uint32_t>(rs2ts_[rs]);
+        job_.ctbs[rs].tile = static_cast<uint16_t>(tile_id_[rs2ts_[rs]]);
+    }
+    job_.tus.reserve(static_cast<size_t>(W) * H / 24);
+    job_.coefs.reserve(static_cast<size_t>(W) * H / 8);
+    h2j_frame& f = job_.hdr;
+    f.codec = H2J_CODEC_HEVC;
+    f.width = W;
+    f.height = H;
+    f.crop_x = s_->conf_l;
+    f.crop_y = s_->conf_t;
+    f.out_w = W - s_->conf_l - s_->conf_r;
+    f.out_h = H - s_->conf_t - s_->conf_b;
+    f.bit_depth = s_->bit_depth;
+    f.bit_depth_c = s_->bit_depth_c;
+    f.log2ctb = log2ctb;
+    f.ctb_w = ctbW;
+    f.ctb_h = ctbH;
+    f.strong_smoothing = s_->strong_intra_smoothing;
+    f.sao_enabled = s_->sao;
+    f.lf_across_tiles = p_->lf_across_tiles;
+    f.cb_qp_offset = p_->cb_qp_offset;
+    f.cr_qp_offset = p_->cr_qp_offset;
+    f.mw = mw;
+    f.mh = mh;
+    if (s_->scaling_list_enabled) {
+        // ScalingFactor tables (7.4.5): [sizeId][matrixId(c)][y*n+x]
+        const uint8_t(*sl)[6][64] = p_->sl_present ? p_->sl : s_->sl;
+        const uint8_t(*dc)[6] = p_->sl_present ? p_->sl_dc : s_->sl_dc;
+        job_.sl.assign(H2J_SL_BYTES, 16);
+        for (int c = 0; c < 3; c++)
+            for (int i = 0; i < 16; i++) job_.sl[H2J_SL_S0 + c * 16 + g_diag_pos4[i]] = sl[0][c][i];
+        for (int c = 0; c < 3; c++)
+            for (int i = 0; i < 64; i++) job_.sl[H2J_SL_S1 + c * 64 + g_diag_pos8[i]] = sl[1][c][i];
+        for (int c = 0; c < 3; c++) {
+            uint8_t* t = &job_.sl[H2J_SL_S2 + c * 256];
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++) {
+                    int k = 0;
+                    while (g_diag_pos8[k] != (y / 2) * 8 + x / 2) k++;
+                    t[y * 16 + x] = sl[2][c][k];
+                }
+            t[0] = dc[2][c];
+        }
+        uint8_t* t = &job_.sl[H2J_SL_S3];
+        for (int y = 0; y < 32; y++)
+            for (int x = 0; x < 32; x++) {
+                int k = 0;
+                while (g_diag_pos8[k] != (y / 4) * 8 + x / 4) k++;
+                t[y * 32 + x] = sl[3][0][k];
+            }
+        t[0] = dc[3][0];
+        f.scaling_list = 1;
+    }
+}
+
+void HevcParser::setup_tiles() {
+    const Pps& p = *p_;
+    std::vector<int> colw(p.ntc), rowh(p.ntr), cbd(p.ntc + 1), rbd(p.ntr + 1);
+    int s = 0;
+    for (int i = 0; i < p.ntc; i++) {
+        if (p.uniform) colw[i] = ((i + 1) * ctbW) / p.ntc - (i * ctbW) / p.ntc;
+        else colw[i] = i < p.ntc - 1 ? p.col_w[i] : ctbW - s;
+        s += colw[i];
+    }
+    s = 0;
+    for (int j = 0; j < p.ntr; j++) {
+        if (p.uniform) rowh[j] = ((j + 1) * ctbH) / p.ntr - (j * ctbH) / p.ntr;
+        else rowh[j] = j < p.ntr - 1 ? p.row_h[j] : ctbH - s;
+        s += rowh[j];
+    }
+    cbd[0] = 0;
+    for (int i = 0; i < p.ntc; i++) cbd[i + 1] = cbd[i] + colw[i];
+    rbd[0] = 0;
+    for (int j = 0; j < p.ntr; j++) rbd[j + 1] = rbd[j] + rowh[j];
+    for (int rs = 0; rs < nctb; rs++) {
+        int tbx = rs % ctbW, tby = rs / ctbW, tx = 0, ty = 0;
+        for (int i = 0; i < p.ntc; i++)
+            if (tbx >= cbd[i]) tx = i;
+        for (int j = 0; j < p.ntr; j++)
+            if (tby >= rbd[j]) ty = j;
+        int v = 0;
+        for (int i = 0; i < tx; i++) v += rowh[ty] * colw[i];
+        for (int j = 0; j < ty; j++) v += ctbW * rowh[j];
+        v += (tby - rbd[ty]) * colw[tx] + tbx - cbd[tx];
+        if (v < 0 || v >= nctb) v = rs;
+        rs2ts_[rs] = v;
+        ts2rs_[v] = rs;
+    }
+    int tid = 0;
+    for (int j = 0; j < p.ntr; j++)
+        for (int i = 0; i < p.ntc; i++, tid++)
+            for (int y = rbd[j]; y < rbd[j + 1]; y++)
+                for (int x = cbd[i]; x < cbd[i + 1]; x++) tile_id_[rs2ts_[y * ctbW + x]] = tid;
+    col_bd_ = cbd;
+}
+
+void HevcParser::qg_start(int xq, int yq) {
+    int prev = first_qg_ ? cur_->slice_qp : last_cu_qp_;
+    first_qg_ = false;
+    int ctb = (yq >> log2ctb) * ctbW + (xq >> log2ctb);
+    int qa = prev, qb = prev;
+    if (same_region(xq, yq, xq - 1, yq) && (yq >> log2ctb) * ctbW + ((xq - 1) >> log2ctb) == ctb)
+        qa = qp_[(yq >> 2) * mw + ((xq - 1) >> 2)];
+    if (same_region(xq, yq, xq, yq - 1) && ((yq - 1) >> log2ctb) * ctbW + (xq >> log2ctb) == ctb)
+        qb = qp_[((yq - 1) >> 2) * mw + (xq >> 2)];
+    qg_pred_ = (qa + qb + 1) >> 1;
+    qpd_val_ = 0;
+    is_qpd_coded_ = false;
+}
+
+void HevcParser::parse_sao(int rx, int ry) {
+    int ctb = ry * ctbW + rx;
+    h2j_ctb& r = job_.ctbs[ctb];
+    uint32_t ts = r.ts;
+    uint16_t tile = r.tile;
+    std::memset(&r, 0, sizeof(r));
+    r.ts = ts;
+    r.tile = tile;
+    r.slice = static_cast<uint8_t>(cur_idx_);
+    if (!cur_->sao_luma && !cur_->sao_chroma) return;
+    auto copy_from = [&](int src) {
+        const h2j_ctb& o = job_.ctbs[src];
+        std::memcpy(r.type, o.type, 3);
+        std::memcpy(r.band_pos, o.band_pos, 3);
+        std::memcpy(r.eo_class, o.eo_class, 3);
+        std::memcpy(r.off, o.off, sizeof(r.off));
+    };
+    if (rx > 0) {
+        int l = ctb - 1;
+        if (ctb_slice_[l] >= 0 && ctb_addr_rs_[l] == ctb_addr_rs_[ctb] && tile_id_[rs2ts_[l]] == tile_id_[rs2ts_[ctb]]) {
+            if (dec(C_SAO_MERGE)) { copy_from(l); return; }
+        }
+    }
+    if (ry > 0) {
+        int u = ctb - ctbW;
+        if (ctb_slice_[u] >= 0 && ctb_addr_rs_[u] == ctb_addr_rs_[ctb] && tile_id_[rs2ts_[u]] == tile_id_[rs2ts_[ctb]]) {
+            if (dec(C_SAO_MERGE)) { copy_from(u); return; }
+        }
+    }
+    const int bd = s_->bit_depth;
+    const int cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
+    const int shift = bd - (bd < 10 ? bd : 10);
+    for (int c = 0; c < 3; c++) {
+        if ((c == 0 && !cur_->sao_luma) || (c > 0 && !cur_->sao_chroma)) continue;
+        if (c == 2) {
+            r.type[2] = r.type[1];
+            r.eo_class[2] = r.eo_class[1];
+        } else {
+            int t = 0;
+            if (dec(C_SAO_TYPE)) t = cc_.bypass() ? 2 : 1;
+            r.type[c] = static_cast<int8_t>(t);
+        }
+        if (r.type[c] == 0) continue;
+        int a[4];
+        for (int i = 0; i < 4; i++) {
+            int v = 0;
+            while (v < cmax && cc_.bypass()) v++;
+            a[i] = v;
+        }
+        if (r.type[c] == 1) {
+            for (int i = 0; i < 4; i++)
+                if (a[i] && cc_.bypass()) a[i] = -a[i];
+            r.band_pos[c] = static_cast<int8_t>(cc_.bypass_bits(5));
+            for (int i = 0; i < 4; i++) r.off[c][i] = static_cast<int16_t>(a[i] * (1 << shift));
+        } else {
+            r.off[c][0] = static_cast<int16_t>(a[0] << shift);
+            r.off[c][1] = static_cast<int16_t>(a[1] << shift);
+            r.off[c][2] = static_cast<int16_t>(-(a[2] << shift));
+            r.off[c][3] = static_cast<int16_t>(-(a[3] << shift));
+            if (c == 0) r.eo_class[0] = static_cast<int8_t>(cc_.bypass_bits(2));
+            if (c == 1) r.eo_class[1] = static_cast<int8_t>(cc_.bypass_bits(2));
+        }
+    }
+}
+
+uint8_t HevcParser::edge_flags(int x0, int y0) const {
+    if (cur_->deblock_disabled) return 0;
+    uint8_t f = 0;
+    const int mask = ctbs - 1;
+    if ((x0 & 7) == 0 && x0 > 0) {
+        bool ok = true;
+        if ((x0 & mask) == 0) {
+            int cn = (y0 >> log2ctb) * ctbW + ((x0 - 1) >> log2ctb), cc = cn + 1;
+            if (!cur_->lf_across_slices && ctb_addr_rs_[cn] != ctb_addr_rs_[cc]) ok = false;
+            if (!p_->lf_across_tiles && tile_id_[rs2ts_[cn]] != tile_id_[rs2ts_[cc]]) ok = false;
+        }
+        if (ok) f |= H2J_TU_EDGE_L;
+    }
+    if ((y0 & 7) == 0 && y0 > 0) {
+        bool ok = true;
+        if ((y0 & mask) == 0) {
+            int cc = (y0 >> log2ctb) * ctbW + (x0 >> log2ctb), cn = cc - ctbW;
+            if (!cur_->lf_across_slices && ctb_addr_rs_[cn] != ctb_addr_rs_[cc]) ok = false;
+            if (!p_->lf_across_tiles && tile_id_[rs2ts_[cn]] != tile_id_[rs2ts_[cc]]) ok = false;
+        }
+        if (ok) f |= H2J_TU_EDGE_T;
+    }
+    return f;
+}
+
+void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
+    const int n = 1 << log2n;
+    if (p_->transform_skip && !cu_bypass_ && log2n <= 2 && dec(C_TSKIP + (c ? 1 : 0))) tu.flags |= H2J_TU_TSKIP;
+    // last_sig_coeff prefix/suffix
+    int off, shift;
+    if (c == 0) {
+        off = 3 * (log2n - 2) + ((log2n - 1) >> 2);
+        shift = (log2n + 1) >> 2;
+    } else {
+        off = 15;
+        shift = log2n - 2;
+    }
+    const int maxp = (log2n << 1) - 1;
+    int lx = 0, ly = 0;
+    while (lx < maxp && dec(C_LAST_X + off + (lx >> shift))) lx++;
+    while (ly < maxp && dec(C_LAST_Y + off + (ly >> shift))) ly++;
+    if (lx > 3) {
+        int nb = (lx >> 1) - 1;
+        lx = (1 << nb) * (2 + (lx & 1)) + static_cast<int>(cc_.bypass_bits(nb));
+    }
+    if (ly > 3) {
+        int nb = (ly >> 1) - 1;
+        ly = (1 << nb) * (2 + (ly & 1)) + static_cast<int>(cc_.bypass_bits(nb));
+    }
+    int scanIdx = 0;
+    if (log2n == 2 || (log2n == 3 && c == 0)) {
+        if (pred_mode >= 6 && pred_mode <= 14) scanIdx = 2;
+        else if (pred_mode >= 22 && pred_mode <= 30) scanIdx = 1;
+    }
+    if (scanIdx == 2) std::swap(lx, ly);
+    if (lx >= n || ly >= n) { err_ = -20; return; }
+    const uint8_t(*sc)[64][2] = scanIdx == 0 ? g_scan_diag : (scanIdx == 1 ? g_scan_hor : g_scan_ver);
+    const int lsb = log2n - 2;
+    // locate last position in scan order
+    int lastSub = -1, lastPos = -1;
+    {
+        int xs = lx >> 2, ys = ly >> 2, xp = lx & 3, yp = ly & 3;
+        const int nsb = 1 << (2 * lsb);
+        for (int i = 0; i < nsb; i++)
+            if (sc[lsb][i][0] == xs && sc[lsb][i][1] == ys) { lastSub = i; break; }
+        for (int k = 0; k < 16; k++)
+            if (sc[2][k][0] == xp && sc[2][k][1] == yp) { lastPos = k; break; }
+    }
+    uint8_t csbf[8][8];
+    std::memset(csbf, 0, sizeof(csbf));
+    int greater1_ctx = 1;
+    const bool sdh = p_->sign_hiding != 0;
+    const int sbw = 1 << lsb;
+    const uint32_t base = static_cast<uint32_t>(job_.coefs.size());
+    for (int i = lastSub; i >= 0; i--) {
+        const int xs = sc[lsb][i][0], ys = sc[lsb][i][1];
+        bool infer_dc = false;
+        if (i < lastSub && i > 0) {
+            int csr = (xs + 1 < sbw) ? csbf[xs + 1][ys] : 0;
+            int csb = (ys + 1 < sbw) ? csbf[xs][ys + 1] : 0;
+            csbf[xs][ys] = static_cast<uint8_t>(dec(C_CSBF + (csr | csb) + (c ? 2 : 0)));
+            infer_dc = true;
+        } else {
+            csbf[xs][ys] = 1;
+        }
+        uint16_t sigmask = 0;  // bit nn
+        int nstart = 15;
+        if (i == lastSub) {
+            nstart = lastPos - 1;
+            sigmask = static_cast<uint16_t>(1u << lastPos);
+        }
+        if (csbf[xs][ys]) {
+            int prevCsbf = 0;
+            if (xs + 1 < sbw) prevCsbf |= csbf[xs + 1][ys];
+            if (ys + 1 < sbw) prevCsbf |= csbf[xs][ys + 1] << 1;
+            for (int nn = nstart; nn >= 0; nn--) {
+                const int xp = sc[2][nn][0], yp = sc[2][nn][1];
+                if (nn > 0 || !infer_dc) {
+                    int sigCtx;
+                    const int xC = (xs << 2) + xp, yC = (ys << 2) + yp;
+                    if (log2n == 2) {
+                        static const uint8_t m[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+                        sigCtx = m[(yC << 2) + xC];
+                    } else if (xC + yC == 0) {
+                        sigCtx = 0;
+                    } else {
+                        if (prevCsbf == 0) sigCtx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+                        else if (prevCsbf == 1) sigCtx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+                        else if (prevCsbf == 2) sigCtx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+                        else sigCtx = 2;
+                        if (c == 0) {
+                            if (xs > 0 || ys > 0) sigCtx += 3;
+                            sigCtx += (log2n == 3) ? ((scanIdx == 0) ? 9 : 15) : 21;
+                        } else {
+                            sigCtx += (log2n == 3) ? 9 : 12;
+                        }
+                    }
+                    if (dec(C_SIG + (c == 0 ? sigCtx : 27 + sigCtx))) {
+                        sigmask |= static_cast<uint16_t>(1u << nn);
+                        infer_dc = false;
+                    }
+                } else if (infer_dc) {
+                    sigmask |= 1u;  // nn == 0 inferred
+                }
+            }
+        }
+        if (!sigmask) continue;
+        // greater1 / greater2
+        int ctxSet = (i == 0 || c > 0) ? 0 : 2;
+        if (greater1_ctx == 0) ctxSet++;
+        greater1_ctx = 1;
+        int g1mask = 0, numG1 = 0, lastG1 = -1, firstSig = 16, lastSig = -1;
+        for (int nn = 15; nn >= 0; nn--) {
+            if (!((sigmask >> nn) & 1)) continue;
+            if (numG1 < 8) {
+                int flag = dec(C_GT1 + ctxSet * 4 + greater1_ctx + (c ? 16 : 0));
+                numG1++;
+                if (flag) {
+                    g1mask |= 1 << nn;
+                    greater1_ctx = 0;
+                    if (lastG1 == -1) lastG1 = nn;
+                } else if (greater1_ctx > 0 && greater1_ctx < 3) {
+                    greater1_ctx++;
+                }
+            }
+            if (lastSig == -1) lastSig = nn;
+            firstSig = nn;
+        }
+        const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
+        int g2 = 0;
+        if (lastG1 != -1) g2 = dec(C_GT2 + ctxSet + (c ? 4 : 0));
+        int signs = 0;
+        for (int nn = 15; nn >= 0; nn--)
+            if (((sigmask >> nn) & 1) && (!sdh || !hidden || nn != firstSig)) signs |= cc_.bypass() << nn;
+        int numSig = 0, sumAbs = 0, rice = 0;
+        for (int nn = 15; nn >= 0; nn--) {
+            if (!((sigmask >> nn) & 1)) continue;
+            int baseL = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0);
+            int lvl = baseL;
+            if (baseL == ((numSig < 8) ? ((nn == lastG1) ? 3 : 2) : 1)) {
+                int prefix = 0;
+                while (prefix < 32 && cc_.bypass()) prefix++;
+                int rem;
+                if (prefix < 3) rem = (prefix << rice) + static_cast<int>(cc_.bypass_bits(rice));
+                else {
+                    int pm3 = prefix - 3;
+                    if (pm3 + rice > 30) { err_ = -21; return; }
+                    rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc_.bypass_bits(pm3 + rice));
+                }
+                lvl = baseL + rem;
+                if (lvl > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
+            }
+            int v = ((signs >> nn) & 1) ? -lvl : lvl;
+            if (sdh && hidden) {
+                sumAbs += lvl;
+                if (nn == firstSig && (sumAbs & 1)) v = -v;
+            }
+            if (v > 32767) v = 32767;
+            if (v < -32768) v = -32768;
+            const int xC = (xs << 2) + sc[2][nn][0], yC = (ys << 2) + sc[2][nn][1];
+            job_.coefs.push_back((static_cast<uint32_t>(yC * n + xC) << 16) | static_cast<uint16_t>(v));
+            numSig++;
+        }
+    }
+    tu.coef = base - job_.hdr.coef;
+    tu.ncoef = static_cast<uint16_t>(job_.coefs.size() - base);
+    tu.flags |= H2J_TU_CBF;
+}
+
+void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int) {
+    h2j_tu tu;
+    tu.x = static_cast<uint16_t>(x);
+    tu.y = static_cast<uint16_t>(y);
+    tu.log2n = static_cast<uint8_t>(log2n);
+    tu.c = static_cast<uint8_t>(c);
+    tu.mode = static_cast<uint8_t>(mode);
+    tu.flags = flags;
+    tu.qp = 0;
+    tu.qpy = 0;
+    tu.ncoef = 0;
+    tu.coef = 0;
+    if (cbf) residual(log2n, c, mode, tu);
+    job_.tus.push_back(tu);
+}
+
+void HevcParser::transform_unit(int x0, int y0, int xb, int yb, int log2n, int blk, int cbf_l, int cbf_cb,
+                                int cbf_cr, int cm, int cux, int cuy, int log2cb) {
+    if ((cbf_l || cbf_cb || cbf_cr) && p_->cu_qp_delta && !is_qpd_coded_) {
+        int v = 0;
+        if (dec(C_QP_DELTA)) {
+            v = 1;
+            while (v < 5 && dec(C_QP_DELTA + 1)) v++;
+            if (v == 5) {
+                int k = 0;
+                while (k < 32 && cc_.bypass()) k++;
+                if (k > 30) { err_ = -22; return; }
+                v += ((1 << k) - 1) + static_cast<int>(cc_.bypass_bits(k));
+            }
+        }
+        if (v && cc_.bypass()) v = -v;
+        is_qpd_coded_ = true;
+        qpd_val_ = v;
+        qp_y_ = ((qg_pred_ + v + 52 + 2 * qpbd) % (52 + qpbd)) - qpbd;
+        set_qp(cux, cuy, 1 << log2cb, qp_y_);
+    }
+    const int lmode = ipm_[(y0 >> 2) * mw + (x0 >> 2)];
+    uint8_t fl = edge_flags(x0, y0);
+    if (cu_bypass_) fl |= H2J_TU_BYPASS | H2J_TU_NOFILT;
+    uint8_t lfl = fl;
+    if (log2n == 2) lfl |= H2J_TU_DST;
+    emit_tu(x0, y0, log2n, 0, lmode, lfl, cbf_l != 0, lmode);
+    if ((job_.tus.back().flags & (H2J_TU_TSKIP | H2J_TU_BYPASS)) != 0) job_.tus.back().flags &= ~H2J_TU_DST;
+    if (err_) return;
+    uint8_t cfl = cu_bypass_ ? (H2J_TU_BYPASS | H2J_TU_NOFILT) : 0;
+    if (log2n > 2) {
+        emit_tu(x0 >> 1, y0 >> 1, log2n - 1, 1, cm, cfl, cbf_cb != 0, cm);
+        if (err_) return;
+        emit_tu(x0 >> 1, y0 >> 1, log2n - 1, 2, cm, cfl, cbf_cr != 0, cm);
+    } else if (blk == 3) {
+        emit_tu(xb >> 1, yb >> 1, 2, 1, cm, cfl, cbf_cb != 0, cm);
+        if (err_) return;
+        emit_tu(xb >> 1, yb >> 1, 2, 2, cm, cfl, cbf_cr != 0, cm);
+    }
+}
+
+void HevcParser::transform_tree(int x0, int y0, int xb, int yb, int log2n, int depth, int blk, int max_depth,
+                                int intra_split, int pcb, int pcr, int cm, int cux, int cuy, int log2cb) {
+    if (err_) return;
+    int split;
+    if (log2n <= s_->log2_max_tb && log2n > s_->log2_min_tb && depth < max_depth && !(intra_split && depth == 0))
+        split = dec(C_SPLIT_TF + 5 - log2n);
+    else
+        split = log2n > s_->log2_max_tb || (intra_split && depth == 0);
+    int cbf_cb = 0, cbf_cr = 0;
+    if (log2n > 2) {
+        if (depth == 0 || pcb) cbf_cb = dec(C_CBF_CHROMA + depth);
+        if (depth == 0 || pcr) cbf_cr = dec(C_CBF_CHROMA + depth);
+    } else {
+        cbf_cb = pcb;
+        cbf_cr = pcr;
+    }
+    if (split) {
+        if (log2n <= 2) { err_ = -23; return; }
+        int h = 1 << (log2n - 1);
+        transform_tree(x0, y0, x0, y0, log2n - 1, depth + 1, 0, max_depth, intra_split, cbf_cb, cbf_cr, cm, cux, cuy, log2cb);
+        transform_tree(x0 + h, y0, x0, y0, log2n - 1, depth + 1, 1, max_depth, intra_split, cbf_cb, cbf_cr, cm, cux, cuy, log2cb);
+        transform_tree(x0, y0 + h, x0, y0, log2n - 1, depth + 1, 2, max_depth, intra_split, cbf_cb, cbf_cr, cm, cux, cuy, log2cb);
+        transform_tree(x0 + h, y0 + h, x0, y0, log2n - 1, depth + 1, 3, max_depth, intra_split, cbf_cb, cbf_cr, cm, cux, cuy, log2cb);
+    } else {
+        int cbf_l = dec(C_CBF_LUMA + (depth == 0 ? 1 : 0));
+        transform_unit(x0, y0, xb, yb, log2n, blk, cbf_l, cbf_cb, cbf_cr, cm, cux, cuy, log2cb);
+    }
+}
+
+void HevcParser::pcm_sample(int x0, int y0, int log2cb) {
+    const uint8_t* p = cc_.aligned_pos();
+    BitReader b(p, static_cast<size_t>(end_ - p));
+    const int n = 1 << log2cb;
+    const int bd = s_->bit_depth;
+    uint8_t fl = edge_flags(x0, y0) | H2J_TU_PCM | H2J_TU_CBF;
+    if (s_->pcm_lf_disabled) fl |= H2J_TU_NOFILT;
+    for (int c = 0; c < 3; c++) {
+        const int cn = c ? n / 2 : n;
+        h2j_tu tu;
+        tu.x = static_cast<uint16_t>(c ? x0 / 2 : x0);
+        tu.y = static_cast<uint16_t>(c ? y0 / 2 : y0);
+        // PCM blocks can be 64x64 luma; split into <=32x32 records
+        const int sub = cn > 32 ? 32 : cn;
+        for (int sy = 0; sy < cn; sy += sub)
+            for (int sx = 0; sx < cn; sx += sub) {
+                h2j_tu t = tu;
+                t.x = static_cast<uint16_t>(tu.x + sx);
+                t.y = static_cast<uint16_t>(tu.y + sy);
+                t.log2n = static_cast<uint8_t>(sub == 32 ? 5 : (sub == 16 ? 4 : (sub == 8 ? 3 : 2)));
+                t.c = static_cast<uint8_t>(c);
+                t.mode = 1;
+                t.flags = c == 0 ? fl : static_cast<uint8_t>(H2J_TU_PCM | H2J_TU_CBF | (fl & H2J_TU_NOFILT));
+                if (c == 0 && (sx || sy)) {
+                    t.flags = static_cast<uint8_t>((t.flags & ~(H2J_TU_EDGE_L | H2J_TU_EDGE_T)) |
+                                                   (edge_flags(x0 + sx, y0 + sy) & ((sx ? 0 : H2J_TU_EDGE_L) | (sy ? 0 : H2J_TU_EDGE_T))));
+                }
+                t.qp = 0;
+                t.qpy = 0;
+                t.coef = static_cast<uint32_t>(job_.coefs.size()) - job_.hdr.coef;
+                t.ncoef = static_cast<uint16_t>(sub * sub);
+                job_.tus.push_back(t);
+                for (int k = 0; k < sub * sub; k++) job_.coefs.push_back(0);
+            }
+    }
+    // samples are stored in raster order of the whole CU per component: fill
+    // the records just pushed in bitstream order
+    size_t tu_end = job_.tus.size();
+    int recs_y = (n > 32) ? 4 : 1;
+    size_t first = tu_end - static_cast<size_t>(recs_y + 2);
+    for (int c = 0; c < 3; c++) {
+        const int cn = c ? n / 2 : n;
+        const int pbd = c ? s_->pcm_bd_c : s_->pcm_bd;
+        const int sub = cn > 32 ? 32 : cn;
+        for (int y = 0; y < cn; y++)
+            for (int x = 0; x < cn; x++) {
+                int v = static_cast<int>(b.u(pbd)) << (bd - pbd);
+                size_t rec = first + (c == 0 ? static_cast<size_t>((y / sub) * (cn / sub) + x / sub) : static_cast<size_t>(recs_y + c - 1));
+                const h2j_tu& t = job_.tus[rec];
+                int pos = (y % sub) * sub + (x % sub);
+                job_.coefs[job_.hdr.coef + t.coef + pos] = (static_cast<uint32_t>(pos) << 16) | static_cast<uint16_t>(v);
+            }
+    }
+    cc_.init(p + b.byte_pos(), end_);
+}
+
+void HevcParser::coding_unit(int x0, int y0, int log2cb) {
+    const int n = 1 << log2cb;
+    cu_tu_begin_ = static_cast<int>(job_.tus.size());
+    cu_bypass_ = 0;
+    if (p_->transquant_bypass) cu_bypass_ = dec(C_TQ_BYPASS);
+    int part_nxn = 0;
+    if (log2cb == s_->log2_min_cb) part_nxn = !dec(C_PART_MODE);
+    qp_y_ = ((qg_pred_ + qpd_val_ + 52 + 2 * qpbd) % (52 + qpbd)) - qpbd;
+    set_qp(x0, y0, n, qp_y_);
+    int pcm = 0;
+    if (!part_nxn && s_->pcm && log2cb >= s_->log2_min_pcm && log2cb <= s_->log2_max_pcm) pcm = cc_.terminate();
+    if (pcm) {
+        set_map(ipm_, x0, y0, n, 1);
+        pcm_sample(x0, y0, log2cb);
+    } else {
+        const int np = part_nxn ? 4 : 1, pb = part_nxn ? n / 2 : n;
+        int prev[4], mpm[4] = {0, 0, 0, 0}, rem[4] = {0, 0, 0, 0};
+        for (int i = 0; i < np; i++) prev[i] = dec(C_PREV_INTRA);
+        for (int i = 0; i < np; i++) {
+            if (prev[i]) {
+                if (cc_.bypass()) mpm[i] = cc_.bypass() ? 2 : 1;
+            } else {
+                rem[i] = static_cast<int>(cc_.bypass_bits(5));
+            }
+        }
+        for (int i = 0; i < np; i++) {
+            const int xp = x0 + (i & 1) * pb, yp = y0 + (i >> 1) * pb;
+            int ca = 1, cb = 1;
+            if (same_region(xp, yp, xp - 1, yp)) ca = ipm_[(yp >> 2) * mw + ((xp - 1) >> 2)];
+            if (same_region(xp, yp, xp, yp - 1) && ((yp - 1) >> log2ctb) == (yp >> log2ctb))
+                cb = ipm_[((yp - 1) >> 2) * mw + (xp >> 2)];
+            int cand[3];
+            if (ca == cb) {
+                if (ca < 2) { cand[0] = 0; cand[1] = 1; cand[2] = 26; }
+                else { cand[0] = ca; cand[1] = 2 + ((ca + 29) % 32); cand[2] = 2 + ((ca - 2 + 1) % 32); }
+            } else {
+                cand[0] = ca;
+                cand[1] = cb;
+                cand[2] = (ca != 0 && cb != 0) ? 0 : ((ca != 1 && cb != 1) ? 1 : 26);
+            }
+            int mode;
+            if (prev[i]) {
+                mode = cand[mpm[i]];
+            } else {
+                if (cand[0] > cand[1]) std::swap(cand[0], cand[1]);
+                if (cand[0] > cand[2]) std::swap(cand[0], cand[2]);
+                if (cand[1] > cand[2]) std::swap(cand[1], cand[2]);
+                mode = rem[i];
+                for (int k = 0; k < 3; k++)
+                    if (mode >= cand[k]) mode++;
+            }
+            set_map(ipm_, xp, yp, pb, static_cast<uint8_t>(mode));
+        }
+        int icpm = 4;
+        if (dec(C_CHROMA_MODE)) icpm = static_cast<int>(cc_.bypass_bits(2));
+        const int lm = ipm_[(y0 >> 2) * mw + (x0 >> 2)];
+        int cm;
+        if (icpm == 4) cm = lm;
+        else {
+            static const int cmodes[4] = {0, 26, 10, 1};
+            cm = cmodes[icpm] == lm ? 34 : cmodes[icpm];
+        }
+        transform_tree(x0, y0, x0, y0, log2cb, 0, 0, s_->max_th_depth_intra + part_nxn, part_nxn, 0, 0, cm, x0, y0, log2cb);
+    }
+    // patch the CU's QP into its transform blocks (QpY is final now)
+    const int qpy = qp_y_ + qpbd;
+    int qpc[2];
+    for (int k = 0; k < 2; k++) {
+        int off = k == 0 ? p_->cb_qp_offset + cur_->cb_qp_offset : p_->cr_qp_offset + cur_->cr_qp_offset;
+        int qpi = qp_y_ + off;
+        if (qpi < -qpbd) qpi = -qpbd;
+        if (qpi > 57) qpi = 57;
+        qpc[k] = chroma_qp_table(qpi) + qpbd;
+    }
+    for (size_t t = static_cast<size_t>(cu_tu_begin_); t < job_.tus.size(); t++) {
+        h2j_tu& tu = job_.tus[t];
+        tu.qpy = static_cast<int8_t>(qp_y_);
+        tu.qp = static_cast<int8_t>(tu.c == 0 ? qpy : qpc[tu.c - 1]);
+    }
+    last_cu_qp_ = qp_y_;
+}
+
+void HevcParser::coding_quadtree(int x0, int y0, int log2cb, int depth) {
+    if (err_) return;
+    const int n = 1 << log2cb;
+    int split;
+    if (x0 + n <= W && y0 + n <= H && log2cb > s_->log2_min_cb) {
+        int inc = 0;
+        if (same_region(x0, y0, x0 - 1, y0) && ctd_[(y0 >> 2) * mw + ((x0 - 1) >> 2)] > depth) inc++;
+        if (same_region(x0, y0, x0, y0 - 1) && ctd_[((y0 - 1) >> 2) * mw + (x0 >> 2)] > depth) inc++;
+        split = dec(C_SPLIT_CU + inc);
+    } else {
+        split = log2cb > s_->log2_min_cb;
+    }
+    if ((p_->cu_qp_delta && log2cb >= log2ctb - p_->diff_cu_qp_delta_depth) || (!p_->cu_qp_delta && log2cb == log2ctb))
+        qg_start(x0, y0);
+    if (split) {
+        const int h = n >> 1;
+        coding_quadtree(x0, y0, log2cb - 1, depth + 1);
+        if (x0 + h < W) coding_quadtree(x0 + h, y0, log2cb - 1, depth + 1);
+        if (y0 + h < H) coding_quadtree(x0, y0 + h, log2cb - 1, depth + 1);
+        if (x0 + h < W && y0 + h < H) coding_quadtree(x0 + h, y0 + h, log2cb - 1, depth + 1);
+    } else {
+        set_map(ctd_, x0, y0, n, static_cast<uint8_t>(depth));
+        coding_unit(x0, y0, log2cb);
+    }
+}
+
+void HevcParser::ctb_start_contexts(int rs, int ts, bool first) {
+    const int rx = rs % ctbW;
+    const int x0 = rx << log2ctb, y0 = (rs / ctbW) << log2ctb;
+    const bool tile_start = ts == 0 || tile_id_[ts] != tile_id_[ts - 1];
+    bool row_start = false;
+    if (p_->wpp)
+        for (size_t i = 0; i + 1 < col_bd_.size(); i++)
+            if (rx == col_bd_[i]) row_start = true;
+    if (!(first || tile_start || row_start)) return;
+    if (tile_start) {
+        init_contexts(cur_->slice_qp);
+    } else if (row_start) {
+        const int xr = x0 + ctbs, yr = y0 - ctbs;
+        if (xr < W && yr >= 0 && same_region(x0, y0, xr, yr)) std::memcpy(ctx_, ctx_wpp_, NUM_CTX);
+        else init_contexts(cur_->slice_qp);
+    } else if (cur_->dependent && have_ds_) {
+        std::memcpy(ctx_, ctx_ds_, NUM_CTX);
+    } else {
+        init_contexts(cur_->slice_qp);
+    }
+    if (tile_start || row_start) first_qg_ = true;
+}
+
+int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end) {
+    const SliceHdr& sh = sh_[shi];
+    cur_ = &sh;
+    cur_idx_ = shi;
+    end_ = end;
+    cc_.init(p, end);
+    int rs = sh.address, ts = rs2ts_[rs];
+    if (!sh.dependent) {
+        first_qg_ = true;
+        last_cu_qp_ = sh.slice_qp;
+    }
+    bool first = true;
+    for (;;) {
+        const int rx = rs % ctbW, ry = rs / ctbW;
+        ctb_slice_[rs] = shi;
+        ctb_addr_rs_[rs] = sh.slice_addr_rs;
+        ctb_start_contexts(rs, ts, first);
+        first = false;
+        parse_sao(rx, ry);
+        coding_quadtree(rx << log2ctb, ry << log2ctb, log2ctb, 0);
+        if (err_) return err_;
+        int endf = cc_.terminate();
+        if (p_->wpp) {
+            for (size_t i = 0; i + 1 < col_bd_.size(); i++)
+                if (rx == col_bd_[i] + 1 && col_bd_[i] + 1 < col_bd_[i + 1]) std::memcpy(ctx_wpp_, ctx_, NUM_CTX);
+        }
+        ts++;
+        if (endf) break;
+        if (ts >= nctb) return -30;
+        const int nrs = ts2rs_[ts];
+        const bool new_tile = tile_id_[ts] != tile_id_[ts - 1];
+        bool new_row = false;
+        if (p_->wpp)
+            for (size_t i = 0; i + 1 < col_bd_.size(); i++)
+                if (nrs % ctbW == col_bd_[i]) new_row = true;
+        if (new_tile || new_row) {
+            cc_.terminate();
+            cc_.init(cc_.aligned_pos(), end);
+        }
+        rs = nrs;
+    }
+    std::memcpy(ctx_ds_, ctx_, NUM_CTX);
+    have_ds_ = true;
+    return 0;
+}
+
+int HevcParser::run(const uint8_t* data, size_t size) {
+    init_scans();
+    std::vector<Nal> nals;
+    split_annexb(data, size, nals);
+    rbsp_.resize(size + 16);
+    bool have_pic = false;
+    const SliceHdr* prev = nullptr;
+    sh_.reserve(256);
+    for (const Nal& nal : nals) {
+        if (nal.n < 2) continue;
+        const int type = (nal.p[0] >> 1) & 63;
+        const size_t rn = unescape_rbsp(nal.p + 2, nal.n - 2, rbsp_.data());
+        BitReader b(rbsp_.data(), rn);
+        if (type == 33) {
+            if (have_pic) break;
+            if (parse_sps(b, sps_) < 0) { job_.message = "unsupported or invalid SPS"; return -2; }
+        } else if (type == 34) {
+            if (have_pic) break;
+            if (parse_pps(b, pps_) < 0) { job_.message = "invalid PPS"; return -3; }
+        } else if (type <= 21) {
+            if (type >= 10 && type <= 15) continue;
+            const int first = (rbsp_[0] >> 7) & 1;
+            if (first && have_pic) break;
+            if (!first && !have_pic) continue;
+            if (sh_.size() >= 255) { job_.message = "too many slices"; return -4; }
+            sh_.push_back(SliceHdr());
+            SliceHdr& sh = sh_.back();
+            int r = parse_slice_header(b, type, sh, prev);
+            if (r < 0) {
+                job_.message = r == -2 ? "non-intra first picture (P/B slices) unsupported" : "invalid slice header";
+                return r == -2 ? -5 : -6;
+            }
+            if (!have_pic) {
+                p_ = &pps_[sh.pps_id];
+                s_ = &sps_[p_->sps_id];
+                setup_picture();
+                have_pic = true;
+            }
+            p_ = &pps_[sh.pps_id];
+            if (&sps_[p_->sps_id] != s_) { job_.message = "SPS change inside picture"; return -6; }
+            // slice data: the RBSP after the header; copy so it stays valid
+            const size_t off = b.byte_pos();
+            if (off > rn) { job_.message = "truncated slice"; return -6; }
+            std::vector<uint8_t>& keep = slice_data_;
+            keep.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
+            keep.resize(keep.size() + 8, 0);
+            h2j_slice rec{};
+            rec.beta_offset = static_cast<int8_t>(sh.beta_offset);
+            rec.tc_offset = static_cast<int8_t>(sh.tc_offset);
+            rec.sao_luma = static_cast<uint8_t>(sh.sao_luma);
+            rec.sao_chroma = static_cast<uint8_t>(sh.sao_chroma);
+            rec.lf_across_slices = static_cast<uint8_t>(sh.lf_across_slices);
+            rec.deblock_disabled = static_cast<uint8_t>(sh.deblock_disabled);
+            rec.slice_addr_rs = sh.slice_addr_rs;
+            job_.slices.push_back(rec);
+            int e = decode_slice_data(static_cast<int>(sh_.size() - 1), keep.data(), keep.data() + (rn - off));
+            if (e < 0) { job_.message = "slice data decode error"; return -7; }
+            prev = &sh_.back();
+        } else if (type == 35 && have_pic) {
+            break;
+        }
+    }
+    if (!have_pic) { job_.message = "no picture found"; return -8; }
+    job_.hdr.nslice = static_cast<uint32_t>(job_.slices.size());
+    job_.hdr.ntu = static_cast<uint32_t>(job_.tus.size());
+    return 0;
+}
+
+}  // namespace
+
+int hevc_parse_picture(const uint8_t* data, size_t size, FrameJob& job) {
+    job.clear();
+    HevcParser p(job);
+    int r = p.run(data, size);
+    job.error = r;
+    return r;
+}
+
+}  // namespace h2j

@@ -1,0 +1,42 @@
+// Host-side container for one picture's job records (see include/h2j_jobs.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "h2j_jobs.h"
+
+namespace h2j {
+
+struct FrameJob {
+    h2j_frame hdr{};
+    std::vector<h2j_tu> tus;
+    std::vector<h2j_coef> coefs;
+    std::vector<h2j_ctb> ctbs;
+    std::vector<h2j_slice> slices;
+    std::vector<uint8_t> sl;  // scaling factors (2032 B) when hdr.scaling_list
+    int error = 0;            // 0 ok, <0 parse error
+    std::string message;
+
+    void clear() {
+        hdr = h2j_frame{};
+        tus.clear();
+        coefs.clear();
+        ctbs.clear();
+        slices.clear();
+        sl.clear();
+        error = 0;
+        message.clear();
+    }
+};
+
+// Offsets of the scaling-factor tables inside FrameJob::sl
+enum { H2J_SL_S0 = 0, H2J_SL_S1 = 48, H2J_SL_S2 = 240, H2J_SL_S3 = 1008, H2J_SL_BYTES = 2032 };
+
+// Parse the first picture of an HEVC Annex-B stream into job records.
+// Returns 0 on success.
+int hevc_parse_picture(const uint8_t* data, size_t size, FrameJob& job);
+// Same for H.264.
+int h264_parse_picture(const uint8_t* data, size_t size, FrameJob& job);
+
+}  // namespace h2j

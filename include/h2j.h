@@ -1,0 +1,63 @@
+/*
+ * h2j.h — C ABI of libH265ToJpeg.so beyond the reference's C++ surface.
+ *
+ * The reference exports exactly two entry points for this path
+ * (SURVEY.md §8b):
+ *   - IDecoder::getInstance() / virtual bool H265ToJpeg(in, out)
+ *       (/root/reference/export_inc/IDecoder.h:29,35)       -> include/IDecoder.h
+ *   - Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decode
+ *       (/root/reference/src/jni/com_autonavi_socol_occtiltedserver_service_H265DecodeService.h:15-16)
+ * Both are kept verbatim.  The functions below are the batch engine those
+ * entry points sit on; they are what an FFI binding (ctypes, cgo, N-API)
+ * would bind for throughput, see INTEGRATION.md.
+ *
+ * Return values: 0 success, < 0 error (message via h2j_engine_error).
+ */
+#ifndef H2J_H
+#define H2J_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct h2j_engine h2j_engine;
+
+/* device: HIP device ordinal; host_threads: entropy/Huffman worker threads
+ * (<= 0: hardware concurrency, capped at 16). */
+h2j_engine *h2j_engine_create(int device, int host_threads);
+void h2j_engine_destroy(h2j_engine *e);
+const char *h2j_engine_error(h2j_engine *e);
+
+/* Transcode n independent Annex-B stills (H.264 or H.265, first picture of
+ * each) to baseline JPEG.  JPEG i is written at out + out_off[i], length
+ * out_len[i]; status[i] = 0 on success, < 0 on failure for that item.
+ * Returns 0 if the batch ran (per-item failures reported in status), < 0
+ * if the batch could not run (e.g. no GPU, out_cap too small). */
+int h2j_engine_transcode(h2j_engine *e, int n, const uint8_t *const *data, const size_t *sizes,
+                         uint8_t *out, size_t out_cap, size_t *out_off, size_t *out_len, int *status);
+
+/* Test / inspection entry points (one picture).
+ * stage: 0 final decoded picture, 1 pre-loop-filter, 2 deblocked (pre-SAO).
+ * planes_out: uint16 Y (w*h) then U, V ((w/2)*(h/2)) of the cropped picture.
+ * info[0..2] = w, h, bit_depth. */
+int h2j_engine_decode(h2j_engine *e, const uint8_t *data, size_t size, int stage, uint16_t *planes_out,
+                      size_t cap_elems, int *info);
+/* JPEG coefficients int16 [mcu][6][64] zigzag of the decoded picture;
+ * info[0..3] = w, h, qscale, nmcu. */
+int h2j_engine_jpeg_coeffs(h2j_engine *e, const uint8_t *data, size_t size, int16_t *out, size_t cap_elems,
+                           int *info);
+/* Timing of the last h2j_engine_transcode call, milliseconds:
+ * [0] parse (host, wall)  [1] h2d  [2] recon  [3] deblock  [4] sao
+ * [5] jpeg (GPU)  [6] d2h  [7] huffman (host, wall)  [8] total (wall)
+ * [9] frames  [10] algorithmic bytes of the GPU pixel path. */
+int h2j_engine_stats(h2j_engine *e, double *out, int n);
+
+/* Library self-description (version, arch, build). */
+const char *h2j_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

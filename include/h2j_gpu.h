@@ -1,0 +1,78 @@
+/*
+ * h2j_gpu.h — thin C ABI of libh2j_hip.so, the MI355X (gfx950) pixel
+ * pipeline.  Plain pointers and sizes; no torch / HIP types in signatures
+ * (streams and events are opaque void*).
+ *
+ * Boundary: these entry points replace what the reference does inside
+ * FFmpeg after entropy decoding, i.e. the arithmetic behind
+ *   avcodec_send_packet/avcodec_receive_frame (/root/reference/src/Decoder.cpp:324,342):
+ *     dequant + inverse transform + intra prediction   -> h2j_gpu_recon
+ *     deblocking                                       -> h2j_gpu_deblock
+ *     SAO                                              -> h2j_gpu_sao
+ *   avcodec_send_frame (/root/reference/src/Encoder.cpp:250), mjpeg encoder:
+ *     pad + MB variance + rate control + FDCT + quantiser + zigzag + symbol
+ *     statistics                                       -> h2j_gpu_jpeg
+ * The host (libH265ToJpeg.so) builds the optimal Huffman tables from the
+ * statistics and emits the JPEG bitstream (avcodec_receive_packet, :259).
+ *
+ * All functions return 0 on success, a negative code on failure; the text
+ * of the last failure is available from h2j_gpu_last_error().
+ */
+#ifndef H2J_GPU_H
+#define H2J_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "h2j_jobs.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* device / memory / stream plumbing */
+int h2j_gpu_device_count(void);
+int h2j_gpu_set_device(int device);
+void *h2j_gpu_malloc(size_t bytes);
+int h2j_gpu_free(void *p);
+void *h2j_gpu_host_alloc(size_t bytes); /* pinned */
+int h2j_gpu_host_free(void *p);
+void *h2j_gpu_stream_create(void);
+int h2j_gpu_stream_destroy(void *stream);
+int h2j_gpu_stream_sync(void *stream);
+int h2j_gpu_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int h2j_gpu_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int h2j_gpu_memset(void *dst, int value, size_t bytes, void *stream);
+void *h2j_gpu_event_create(void);
+int h2j_gpu_event_destroy(void *ev);
+int h2j_gpu_event_record(void *ev, void *stream);
+float h2j_gpu_event_elapsed_ms(void *start, void *stop);
+const char *h2j_gpu_last_error(void);
+
+/* One batch of pictures resident in HBM.  All pointers are device pointers. */
+typedef struct {
+    int32_t nframes;
+    int32_t max_w, max_h;       /* max coded luma size over the batch */
+    int32_t max_mcu;            /* max JPEG MCUs over the batch */
+    const h2j_frame *frames;
+    const h2j_tu *tus;
+    const h2j_coef *coefs;
+    const h2j_ctb *ctbs;
+    const h2j_slice *slices;
+    const uint8_t *sl;
+    uint8_t *arena;             /* pictures, maps, JPEG coefficients + stats */
+} h2j_gpu_batch;
+
+/* K1: dequantisation + inverse transform + intra prediction (HEVC and H.264),
+ * writes the pre-loop-filter picture to frame.pic and the deblocking maps. */
+int h2j_gpu_recon(const h2j_gpu_batch *b, void *stream);
+/* K2: deblocking (vertical edges, then horizontal edges), in place on frame.pic */
+int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);
+/* K3: SAO frame.pic -> frame.pic2 (copies when SAO is off) */
+int h2j_gpu_sao(const h2j_gpu_batch *b, void *stream);
+/* K4: JPEG forward path on frame.pic2 -> frame.jcoef / frame.jstat */
+int h2j_gpu_jpeg(const h2j_gpu_batch *b, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,122 @@
+/*
+ * h2j_jobs.h — the job records the host entropy decoders ship to HBM.
+ *
+ * This is the data contract between the C++11 host side (Annex-B parsing +
+ * CABAC/CAVLC on pinned host threads) and the CDNA4 HIP pixel pipeline.  It
+ * replaces what happens inside FFmpeg between avcodec_send_packet and the
+ * decoded AVFrame in the reference (/root/reference/src/Decoder.cpp:324-342):
+ * the host emits, per picture, one record per transform block (position,
+ * size, intra mode, QP, flags) plus the sparse quantised coefficients; the
+ * GPU does dequantisation, inverse transform, intra prediction, deblocking,
+ * SAO and the JPEG forward path.
+ *
+ * Plain C, POD only, fixed-width fields: the same bytes are read by hipcc
+ * device code and gcc host code.
+ */
+#ifndef H2J_JOBS_H
+#define H2J_JOBS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum h2j_codec { H2J_CODEC_NONE = 0, H2J_CODEC_H264 = 264, H2J_CODEC_HEVC = 265 };
+
+/* TU record flags */
+enum {
+    H2J_TU_CBF = 1u << 0,     /* residual present (ncoef entries) */
+    H2J_TU_TSKIP = 1u << 1,   /* HEVC transform_skip_flag */
+    H2J_TU_BYPASS = 1u << 2,  /* cu_transquant_bypass / H.264 lossless: residual = levels */
+    H2J_TU_PCM = 1u << 3,     /* coefficients hold raw samples (already scaled to bit depth) */
+    H2J_TU_EDGE_L = 1u << 4,  /* left edge is a deblocking edge (filterEdgeFlag && on 8 grid) */
+    H2J_TU_EDGE_T = 1u << 5,  /* top edge is a deblocking edge */
+    H2J_TU_NOFILT = 1u << 6,  /* samples excluded from deblock/SAO (pcm+lf disabled, bypass) */
+    H2J_TU_DST = 1u << 7      /* HEVC 4x4 luma intra: DST-VII instead of DCT */
+};
+
+/* One transform block of one colour component, in decoding order.
+ * HEVC: every luma/chroma TB of the picture (prediction happens per TB even
+ * when cbf == 0).  x, y, log2n are in the component's sample grid. */
+typedef struct {
+    uint16_t x, y;
+    uint8_t log2n;   /* 2..5 */
+    uint8_t c;       /* 0 Y, 1 Cb, 2 Cr */
+    uint8_t mode;    /* intra prediction mode (HEVC 0..34) */
+    uint8_t flags;   /* H2J_TU_* */
+    int8_t qp;       /* qP for scaling (Qp'Y / Qp'Cb / Qp'Cr, includes QpBdOffset) */
+    int8_t qpy;      /* QpY of the coding unit (deblocking), luma TBs */
+    uint16_t ncoef;  /* entries in the coefficient stream */
+    uint32_t coef;   /* first entry (frame-relative) */
+} h2j_tu;
+
+/* coefficient entry: (pos << 16) | (uint16_t)level, pos = y * n + x */
+typedef uint32_t h2j_coef;
+
+typedef struct {
+    int8_t type[3];     /* 0 off, 1 band, 2 edge */
+    int8_t band_pos[3];
+    int8_t eo_class[3];
+    uint8_t slice;      /* index into the frame's slice table */
+    int16_t off[3][4];  /* SaoOffsetVal[1..4] */
+    uint16_t tile;      /* tile id */
+    uint16_t pad;
+    uint32_t ts;        /* CtbAddrRsToTs */
+} h2j_ctb;
+
+typedef struct {
+    int8_t beta_offset;     /* slice_beta_offset_div2 * 2 */
+    int8_t tc_offset;       /* slice_tc_offset_div2 * 2 */
+    uint8_t sao_luma, sao_chroma;
+    uint8_t lf_across_slices;
+    uint8_t deblock_disabled;
+    uint16_t pad;
+    int32_t slice_addr_rs;
+} h2j_slice;
+
+/* One picture.  Offsets are relative to the start of the batch's arrays. */
+typedef struct {
+    int32_t codec;                  /* h2j_codec */
+    int32_t width, height;          /* coded size (luma) */
+    int32_t crop_x, crop_y;         /* conformance window origin (luma) */
+    int32_t out_w, out_h;           /* cropped output size (luma) */
+    int32_t bit_depth, bit_depth_c;
+    int32_t log2ctb, ctb_w, ctb_h;
+    int32_t strong_smoothing;
+    int32_t sao_enabled;
+    int32_t lf_across_tiles;
+    int32_t cb_qp_offset, cr_qp_offset; /* pps offsets (deblocking) */
+    int32_t scaling_list;           /* 1: scaling factors at sl */
+    uint32_t tu, ntu;               /* h2j_tu range */
+    uint32_t coef;                  /* base of this frame's coefficient entries */
+    uint32_t ctb;                   /* h2j_ctb base (ctb_w * ctb_h records) */
+    uint32_t slice, nslice;         /* h2j_slice range */
+    uint32_t sl;                    /* uint8 scaling factor tables: [sizeId 0..3][c 0..2][32*32]... see DESIGN.md */
+    uint32_t pad0;
+    /* device arena offsets (bytes), filled by the pipeline */
+    uint64_t pic;                   /* reconstruction / deblocking planes */
+    uint64_t pic2;                  /* SAO output planes (final decoded picture) */
+    uint64_t maps;                  /* per-4x4 deblocking maps: flags (u8) then qp (i8) */
+    uint64_t jcoef;                 /* JPEG coefficients int16 [mcu][6][64] */
+    uint64_t jstat;                 /* JPEG per-frame stats (h2j_jstat) */
+    int32_t pic_stride[3];          /* elements */
+    int32_t pic_off[3];             /* element offset of each plane inside pic / pic2 */
+    int32_t mw, mh;                 /* 4x4 map dims */
+    int32_t status;                 /* device-side error code */
+    int32_t pad1;
+} h2j_frame;
+
+/* per-frame JPEG statistics written by the GPU */
+typedef struct {
+    int64_t var_sum;        /* Σ MB variance */
+    int32_t qscale, lambda;
+    uint32_t hist[4][256];  /* DC-Y, DC-C, AC-Y, AC-C symbol counts */
+    uint16_t q16[64];       /* quantiser reciprocal (A.5), natural order */
+    uint16_t b16[64];       /* quantiser bias (A.5) */
+    uint8_t dqt[64];        /* DQT entries, natural order (A.3) */
+} h2j_jstat;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

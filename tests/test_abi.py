@@ -1,0 +1,57 @@
+"""The drop-in boundary: libraries build, load, and export every symbol the
+public headers declare (no GPU needed, no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
+INC = os.path.join(ROOT, "include")
+
+
+def _declared(header):
+    src = open(os.path.join(INC, header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(h2j_[a-z0-9_]+)\s*\(", src)))
+
+
+def _exports(so):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True)
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+@pytest.fixture(scope="module")
+def built():
+    for so in ("libh2j_hip.so", "libH265ToJpeg.so"):
+        if not os.path.exists(os.path.join(PKG, so)):
+            subprocess.check_call(["make", "-s", "-C", PKG])
+    return True
+
+
+def test_gpu_abi_exports(built):
+    ex = _exports(os.path.join(PKG, "libh2j_hip.so"))
+    missing = [s for s in _declared("h2j_gpu.h") if s not in ex]
+    assert not missing, missing
+
+
+def test_host_abi_exports(built):
+    ex = _exports(os.path.join(PKG, "libH265ToJpeg.so"))
+    missing = [s for s in _declared("h2j.h") if s not in ex]
+    assert not missing, missing
+    # reference C++ / JNI surface
+    assert "_ZN8IDecoder11getInstanceEv" in ex
+    assert "Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decode" in ex
+
+
+def test_library_loads(built):
+    lib = ctypes.CDLL(os.path.join(PKG, "libH265ToJpeg.so"))
+    lib.h2j_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.h2j_version()
+
+
+def test_no_ffmpeg_dependency(built):
+    out = subprocess.check_output(["ldd", os.path.join(PKG, "libH265ToJpeg.so")], text=True)
+    assert "avcodec" not in out and "avformat" not in out
