@@ -1,0 +1,185 @@
+"""Benchmark: 1080p H.265 I-frames/s -> JPEG on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): a batch of 1024 x 1080p H.265 Main 8-bit
+I-frames -> baseline JPEG on one GPU.  Inputs are the 16 committed hevcgen
+streams of tests/golden/bench (QP {22,27,32,37} x noise {0,2,4}, SURVEY.md
+§8d recipe) tiled x64; every frame is decoded independently (no dedupe).
+
+One step = one full transcode of the batch: host entropy threads
+(CABAC -> job records), H2D, the HIP pixel pipeline (K1 recon, K2 deblock,
+K3 SAO, K4 JPEG forward path), D2H, host Huffman assembly.  `value` is the
+whole-job frames/s; the GPU-pipeline-only rate and the per-stage times are
+reported beside it.
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): one process per GPU,
+each transcodes its own 1024-frame batch (weak scaling, no data-path
+collective); a barrier brackets the timed region and rank 0 reports the max
+time over ranks.  The only collectives are the counter reductions at the end.
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "h264-h265-to-jpeg_amd"))
+
+METRIC = "1080p H.265 I-frames/sec → JPEG at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+BYTES_PER_FRAME_1080P = 15_552_000  # B = 5S, S = 1.5*W*H
+
+
+def load_streams(pattern):
+    files = sorted(glob.glob(os.path.join(ROOT, pattern)))
+    if not files:
+        raise SystemExit(f"no benchmark streams at {pattern}: run tools/make_streams.py bench")
+    return [open(f, "rb").read() for f in files]
+
+
+def pmc_traffic():
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_k1.json")
+    if os.path.exists(path):
+        try:
+            d = json.load(open(path))
+            return d.get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def cpu_baseline(streams, budget_s=12.0):
+    """Oracle (CPU restatement of the reference path) on 1 host core, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py  # test infrastructure: only the cpu_baseline leg uses it
+    n = 0
+    t0 = time.time()
+    for s in streams:
+        oracle_py.transcode(s)
+        n += 1
+        if time.time() - t0 > budget_s:
+            break
+    dt = time.time() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} of the {len(streams)} distinct 1080p streams, oracle decode+JPEG, 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=1024, help="frames per GPU per step")
+    ap.add_argument("--threads", type=int, default=16, help="host entropy/Huffman threads per GPU")
+    ap.add_argument("--streams", default="tests/golden/bench/hevc1080_*.h265")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        tdist.init_process_group(backend=backend)
+        dist = tdist
+
+    import h2j
+    streams = load_streams(args.streams)
+    n = args.frames
+    batch = [streams[i % len(streams)] for i in range(n)]
+    eng = h2j.Engine(local, args.threads)
+
+    # pre-built ctypes arguments: nothing but the C call inside the timed region
+    bufs = [(ctypes.c_uint8 * len(s)).from_buffer_copy(s) for s in batch]
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    sizes = (ctypes.c_size_t * n)(*[len(s) for s in batch])
+    cap = n * (2 << 20)
+    out = (ctypes.c_uint8 * cap)()
+    offs = (ctypes.c_size_t * n)()
+    lens = (ctypes.c_size_t * n)()
+    status = (ctypes.c_int * n)()
+
+    def step():
+        rc = eng.transcode_raw(ptrs, sizes, n, out, cap, offs, lens, status)
+        if rc != 0:
+            raise RuntimeError(f"transcode failed rc={rc}: {eng.error()}")
+        bad = [i for i in range(n) if status[i] != 0]
+        if bad:
+            raise RuntimeError(f"{len(bad)} frames failed, e.g. #{bad[0]} status {status[bad[0]]}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    stage_sum = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = eng.stats()
+        for k, v in st.items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([n * args.steps], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total_frames = int(c.item())
+    else:
+        total_frames = n * args.steps
+
+    if rank == 0:
+        steps = args.steps
+        per = {k: v / steps for k, v in stage_sum.items()}
+        recon_ms = per["recon_ms"]
+        gpu_ms = per["h2d_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"] + per["d2h_ms"]
+        alg_bytes = BYTES_PER_FRAME_1080P * n
+        achieved = alg_bytes / (recon_ms / 1e3) / 1e9
+        traffic = pmc_traffic()
+        res = {
+            "metric": METRIC,
+            "value": total_frames / elapsed,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: 16 hevcgen 1080p HEVC Main I-frame streams (tests/golden/bench) tiled to the batch",
+            "config": {"workload": "configs[1]: batch of 1024 x 1080p H.265 Main 8-bit I-frames -> JPEG per GPU",
+                       "frames_per_gpu": n, "global_batch": n * world, "host_threads_per_gpu": args.threads,
+                       "parallelism": f"independent replicas x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "h2j_k1_recon", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": recon_ms},
+            "gpu_pipeline_fps": n / (gpu_ms / 1e3),
+            "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
+        }
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(streams)
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -49,3 +49,46 @@ def test_transcode_matches_fixture(engine):
         return j[:2] + j[4 + n:]
     assert strip_com(out) == strip_com(ref)
     assert out == O.transcode(s)
+
+
+import glob
+import json
+import os
+
+HEVC_DIR = golden("hevc")
+PARITY = sorted(glob.glob(os.path.join(HEVC_DIR, "*.h265")))
+
+
+@pytest.mark.parametrize("path", PARITY, ids=[os.path.basename(p) for p in PARITY])
+def test_parity_vectors_prelf_and_final(engine, path):
+    """hevcgen vectors (PCM, bypass, slices, 10-bit, CTB16/32, offsets, SDH...)."""
+    s = read(path)
+    for stage, skip in ((1, True), (0, False)):
+        gy, gu, gv, bd = engine.decode(s, stage=stage)
+        oy, ou, ov, obd = O.decode(s, 265, skip_loop_filter=skip)
+        assert bd == obd
+        for g, o, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
+            diff = np.argwhere(g != o)
+            assert diff.size == 0, f"stage {stage} {name}: {len(diff)} mismatches, first {diff[:4].tolist()}"
+
+
+def test_mixed_batch_transcode_matches_oracle(engine):
+    """One batch mixing sizes, bit depths and features; every JPEG byte-exact."""
+    streams = [read(p) for p in PARITY] + [read(golden("img01.h265"))]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, PARITY + ["img01"]):
+        assert o is not None, p
+        assert o == O.transcode(s), p
+
+
+def test_bench_streams_sample(engine):
+    paths = sorted(glob.glob(os.path.join(golden("bench"), "*.h265")))[::5]
+    streams = [read(p) for p in paths]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, paths):
+        assert o == O.transcode(s), p
+
+
+def test_invalid_inputs_fail_cleanly(engine):
+    outs = engine.transcode([b"", b"\x00\x00\x01\x40garbage", read(golden("img01.h265"))[:1000]])
+    assert outs[0] is None and outs[1] is None

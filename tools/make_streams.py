@@ -1,0 +1,152 @@
+"""Mint the committed HEVC test vectors and benchmark inputs (test infrastructure).
+
+Source content: the reference's own fixture test/img/img01.h265 (tests/golden/),
+decoded by the oracle, cropped / flipped / upsampled, plus seeded Gaussian
+noise (SURVEY.md §8d recipe).  Encoded with tools/hevcgen (our HEVC intra
+encoder; the container has no other HEVC encoder).  Every stream is checked
+here: the oracle's pre-loop-filter decode must equal hevcgen's own
+reconstruction bit-for-bit.
+
+  python tools/make_streams.py bench   -> tests/golden/bench/hevc1080_XX.h265 (16 streams)
+  python tools/make_streams.py parity  -> tests/golden/hevc/*.h265 + manifest.json
+  python tools/make_streams.py 4k      -> tests/golden/bench4k/hevc2160_10b_XX.h265
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_py as O  # noqa: E402
+
+GEN = os.path.join(ROOT, "tools", "hevcgen", "hevcgen")
+
+
+def build_gen():
+    src = GEN + ".c"
+    if not os.path.exists(GEN) or os.path.getmtime(GEN) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O2", "-o", GEN, src, "-lm"])
+
+
+def source_planes():
+    y, u, v, _ = O.decode(open(os.path.join(ROOT, "tests/golden/img01.h265"), "rb").read(), 265)
+    return y.astype(np.int32), u.astype(np.int32), v.astype(np.int32)
+
+
+def make_content(planes, W, H, seed, sigma, bd, upsample=1):
+    rng = np.random.default_rng(seed)
+    y, u, v = planes
+    if upsample > 1:
+        y = np.repeat(np.repeat(y, upsample, 0), upsample, 1)
+        u = np.repeat(np.repeat(u, upsample, 0), upsample, 1)
+        v = np.repeat(np.repeat(v, upsample, 0), upsample, 1)
+    Hs, Ws = y.shape
+    x0 = int(rng.integers(0, (Ws - W) // 2 + 1)) * 2
+    y0 = int(rng.integers(0, (Hs - H) // 2 + 1)) * 2
+    out = []
+    hf, vf = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+    for c, p in enumerate((y, u, v)):
+        s = 1 if c == 0 else 2
+        q = p[y0 // s:(y0 + H) // s, x0 // s:(x0 + W) // s].astype(np.float64)
+        if hf:
+            q = q[:, ::-1]
+        if vf:
+            q = q[::-1, :]
+        scale = 1 << (bd - 8)
+        q = q * scale
+        if bd > 8:
+            q = q + rng.integers(0, scale, q.shape)  # fill the low bits
+        if sigma:
+            q = q + rng.normal(0, sigma * scale, q.shape)
+        out.append(np.clip(np.rint(q), 0, (1 << bd) - 1).astype(np.int32))
+    return out
+
+
+def encode(planes, W, H, bd, qp, seed, path, opts=()):
+    yuv = path + ".yuv"
+    rec = path + ".rec"
+    dt = np.uint8 if bd == 8 else np.dtype("<u2")
+    with open(yuv, "wb") as f:
+        for p in planes:
+            f.write(p.astype(dt).tobytes())
+    subprocess.check_call([GEN, yuv, str(W), str(H), str(bd), str(qp), str(seed), path, "--recon", rec] + list(opts))
+    s = open(path, "rb").read()
+    y, u, v, b = O.decode(s, 265, skip_loop_filter=True)
+    r = np.fromfile(rec, dtype=dt).astype(np.int32)
+    ys, cs = W * H, (W // 2) * (H // 2)
+    ok = (np.array_equal(y, r[:ys].reshape(H, W)) and np.array_equal(u, r[ys:ys + cs].reshape(H // 2, W // 2))
+          and np.array_equal(v, r[ys + cs:].reshape(H // 2, W // 2)))
+    os.remove(yuv)
+    os.remove(rec)
+    if not ok:
+        raise SystemExit(f"{path}: oracle decode != encoder reconstruction")
+    return len(s)
+
+
+def bench(n=16):
+    out_dir = os.path.join(ROOT, "tests/golden/bench")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    qps = [22, 27, 32, 37]
+    sigmas = [0, 2, 4]
+    total = 0
+    for i in range(n):
+        qp, sigma = qps[i % 4], sigmas[(i // 4) % 3]
+        content = make_content(planes, 1920, 1080, i, sigma, 8)
+        path = os.path.join(out_dir, f"hevc1080_{i:02d}.h265")
+        nb = encode(content, 1920, 1080, 8, qp, i, path)
+        total += nb
+        print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+    print("total", total)
+
+
+PARITY = [
+    # name, W, H, bd, qp, seed, sigma, options
+    ("p01_416x240_q22", 416, 240, 8, 22, 11, 2, []),
+    ("p02_416x240_q37_nosdh", 416, 240, 8, 37, 12, 0, ["--sdh", "0"]),
+    ("p03_400x232_pcm_bypass_slices", 400, 232, 8, 30, 13, 3, ["--pcm", "1", "--bypass", "1", "--slices", "1"]),
+    ("p04_416x240_10bit_ctb32_d2", 416, 240, 10, 27, 14, 2, ["--pcm", "1", "--ctb", "32", "--depth", "2"]),
+    ("p05_256x144_ctb16_offsets", 256, 144, 8, 18, 15, 4, ["--ctb", "16", "--cbqp", "3", "--crqp", "-2", "--beta", "2", "--tc", "-1"]),
+    ("p06_352x288_q12_noise", 352, 288, 8, 12, 16, 4, []),
+    ("p07_336x200_q45", 336, 200, 8, 45, 17, 0, ["--beta", "-3", "--tc", "4"]),
+    ("p08_320x180_10bit_q2", 320, 180, 10, 2, 18, 3, ["--depth", "0"]),
+    ("p09_200x120_noqpd_notskip", 200, 120, 8, 24, 19, 2, ["--qpdelta", "0", "--tskip", "0", "--sao", "0"]),
+    ("p10_480x272_slices2", 480, 272, 8, 31, 20, 1, ["--slices", "2", "--bypass", "1"]),
+    ("p11_64x64_tiny", 64, 64, 8, 26, 21, 2, []),
+    ("p12_72x40_odd_crop", 72, 40, 8, 26, 22, 2, ["--ctb", "16"]),
+]
+
+
+def parity():
+    out_dir = os.path.join(ROOT, "tests/golden/hevc")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    manifest = []
+    for name, W, H, bd, qp, seed, sigma, opts in PARITY:
+        content = make_content(planes, W, H, seed, sigma, bd)
+        path = os.path.join(out_dir, name + ".h265")
+        nb = encode(content, W, H, bd, qp, seed, path, opts)
+        manifest.append({"file": name + ".h265", "w": W, "h": H, "bit_depth": bd, "qp": qp, "options": opts})
+        print(f"{path}: {nb} B", flush=True)
+    json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
+def fourk(n=4):
+    out_dir = os.path.join(ROOT, "tests/golden/bench4k")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    for i in range(n):
+        qp = [22, 27, 32, 37][i % 4]
+        content = make_content(planes, 3840, 2160, 100 + i, [0, 2][i % 2], 10, upsample=2)
+        path = os.path.join(out_dir, f"hevc2160_10b_{i:02d}.h265")
+        nb = encode(content, 3840, 2160, 10, qp, 100 + i, path)
+        print(f"{path}: qp {qp} -> {nb} B", flush=True)
+
+
+if __name__ == "__main__":
+    build_gen()
+    what = sys.argv[1] if len(sys.argv) > 1 else "bench"
+    {"bench": bench, "parity": parity, "4k": fourk}[what]()
