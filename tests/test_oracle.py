@@ -55,3 +55,20 @@ def test_fdct_dc_and_flat_block():
     O.lib().oracle_fdct(blk)
     # flat block: only DC, level 128 after ((X>>2)+8)/16
     assert ((blk[0] >> 2) + 8) // 16 == 128
+
+
+def test_h264_decode_matches_appendix_b():
+    y, u, v, bd = O.decode(read(golden("img01.h264")), 264)
+    assert (y.shape, bd) == ((1080, 1920), 8)
+    assert md5_planes((y, u, v)) == H264_YUV
+
+
+def test_h264_pre_deblock_matches_appendix_b():
+    y, u, v, _ = O.decode(read(golden("img01.h264")), 264, skip_loop_filter=True)
+    assert md5_planes((y, u, v)) == H264_PRELF
+
+
+def test_h264_transcode_matches_fixture_jpeg():
+    """The golden img01.h264.jpeg was written by the x86_64 build: byte-exact,
+    COM 'Lavc58.117.101' included."""
+    assert O.transcode(read(golden("img01.h264"))) == read(golden("img01.h264.jpeg"))
