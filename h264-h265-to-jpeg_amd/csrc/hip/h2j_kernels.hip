@@ -347,10 +347,372 @@ __device__ void hevc_recon_frame(const h2j_frame& f, const h2j_tu* tus, const h2
     }
 }
 
+
+// ---------------------------------------------------------------- K1: H.264
+// H.264 8.3 (intra prediction), 8.5 (scaling + transforms).  Records: luma
+// log2n 2 (I4x4), 3 (I8x8), 4 (I16x16, DC levels at (4i,4j)); chroma log2n 3
+// (DC levels at (4i,4j)); PCM.  Macroblocks are the "CTB" records (log2ctb 4).
+__constant__ uint8_t kNorm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+__constant__ uint8_t kNorm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                     {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+
+DEVI int h264_norm4(int m, int i, int j) {
+    if (!(i & 1) && !(j & 1)) return kNorm4[m][0];
+    if ((i & 1) && (j & 1)) return kNorm4[m][1];
+    return kNorm4[m][2];
+}
+DEVI int h264_norm8(int m, int i, int j) {
+    if (!(i & 3) && !(j & 3)) return kNorm8[m][0];
+    if ((i & 1) && (j & 1)) return kNorm8[m][1];
+    if ((i & 3) == 2 && (j & 3) == 2) return kNorm8[m][2];
+    if ((!(i & 3) && (j & 1)) || ((i & 1) && !(j & 3))) return kNorm8[m][3];
+    if ((!(i & 3) && (j & 3) == 2) || ((i & 3) == 2 && !(j & 3))) return kNorm8[m][4];
+    return kNorm8[m][5];
+}
+DEVI int h264_scale4(int lvl, int ls, int qp) {
+    return qp >= 24 ? (lvl * ls) << (qp / 6 - 4) : (lvl * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+}
+DEVI int h264_scale8(int lvl, int ls, int qp) {
+    return qp >= 36 ? (lvl * ls) << (qp / 6 - 6) : (lvl * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+}
+
+DEVI bool h264_avail(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, int xc, int yc, int xn, int yn) {
+    if (xn < 0 || yn < 0 || xn >= f.width || yn >= f.height) return false;
+    const int cn = (yn >> 4) * f.ctb_w + (xn >> 4), cc = (yc >> 4) * f.ctb_w + (xc >> 4);
+    if (cn == cc) {
+        const int ax = (xn & 15) >> 2, ay = (yn & 15) >> 2, bx = (xc & 15) >> 2, by = (yc & 15) >> 2;
+        const int za = (ax & 1) | ((ay & 1) << 1) | ((ax & 2) << 1) | ((ay & 2) << 2);
+        const int zb = (bx & 1) | ((by & 1) << 1) | ((bx & 2) << 1) | ((by & 2) << 2);
+        return za < zb;
+    }
+    if (cn > cc) return false;
+    const h2j_ctb& A = mbs[cn];
+    if (!(A.mbflags & 4)) return false;
+    return slices[A.slice].slice_addr_rs == slices[mbs[cc].slice].slice_addr_rs;
+}
+
+// 4x4 / 8x8 directional prediction; T[-1] / L[-1] = corner
+DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L, int dcv) {
+    switch (mode) {
+    case 0: return T[x];
+    case 1: return L[y];
+    case 2: return dcv;
+    case 3:
+        if (x == n - 1 && y == n - 1) return (T[2 * n - 2] + 3 * T[2 * n - 1] + 2) >> 2;
+        return (T[x + y] + 2 * T[x + y + 1] + T[x + y + 2] + 2) >> 2;
+    case 4:
+        if (x > y) return (T[x - y - 2] + 2 * T[x - y - 1] + T[x - y] + 2) >> 2;
+        if (x < y) return (L[y - x - 2] + 2 * L[y - x - 1] + L[y - x] + 2) >> 2;
+        return (T[0] + 2 * T[-1] + L[0] + 2) >> 2;
+    case 5: {
+        const int z = 2 * x - y;
+        if (z >= 0 && !(z & 1)) return (T[x - (y >> 1) - 1] + T[x - (y >> 1)] + 1) >> 1;
+        if (z >= 0) return (T[x - (y >> 1) - 2] + 2 * T[x - (y >> 1) - 1] + T[x - (y >> 1)] + 2) >> 2;
+        if (z == -1) return (L[0] + 2 * T[-1] + T[0] + 2) >> 2;
+        if (n == 4) return (L[y - 1] + 2 * L[y - 2] + L[y - 3] + 2) >> 2;
+        return (L[y - 2 * x - 1] + 2 * L[y - 2 * x - 2] + L[y - 2 * x - 3] + 2) >> 2;
+    }
+    case 6: {
+        const int z = 2 * y - x;
+        if (z >= 0 && !(z & 1)) return (L[y - (x >> 1) - 1] + L[y - (x >> 1)] + 1) >> 1;
+        if (z >= 0) return (L[y - (x >> 1) - 2] + 2 * L[y - (x >> 1) - 1] + L[y - (x >> 1)] + 2) >> 2;
+        if (z == -1) return (L[0] + 2 * T[-1] + T[0] + 2) >> 2;
+        if (n == 4) return (T[x - 1] + 2 * T[x - 2] + T[x - 3] + 2) >> 2;
+        return (T[x - 2 * y - 1] + 2 * T[x - 2 * y - 2] + T[x - 2 * y - 3] + 2) >> 2;
+    }
+    case 7: {
+        const int i = x + (y >> 1);
+        return !(y & 1) ? (T[i] + T[i + 1] + 1) >> 1 : (T[i] + 2 * T[i + 1] + T[i + 2] + 2) >> 2;
+    }
+    default: {
+        const int z = x + 2 * y, lim = 2 * n - 3;
+        if (z > lim) return L[n - 1];
+        if (z == lim) return (L[n - 2] + 3 * L[n - 1] + 2) >> 2;
+        const int i = y + (x >> 1);
+        return !(z & 1) ? (L[i] + L[i + 1] + 1) >> 1 : (L[i] + 2 * L[i + 1] + L[i + 2] + 2) >> 2;
+    }
+    }
+}
+
+struct H4Lds {
+    int top[40];   // top[0] = corner, top[1 + i] = p[i, -1]
+    int left[20];  // left[0] = corner, left[1 + i] = p[-1, i]
+    int ftop[40], fleft[20];
+    int blk[256];
+    int tmp[256];
+    int dc[16];
+    int flags;     // bit0 top, bit1 left, bit2 corner, bit3 top-right
+    int dcv;
+};
+
+template <typename Pel>
+__device__ void h264_recon_frame(const h2j_frame& f, const h2j_tu* tus, const h2j_coef* coefs, const h2j_ctb* mbs,
+                                 const h2j_slice* slices, const uint8_t* sl, uint8_t* arena, H4Lds& s) {
+    const int lane = threadIdx.x;
+    const h2j_tu* T = tus + f.tu;
+    const h2j_coef* CO = coefs + f.coef;
+    for (uint32_t t = 0; t < f.ntu; t++) {
+        const h2j_tu tu = T[t];
+        const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+        const int x0 = tu.x, y0 = tu.y;
+        Pel* P = plane<Pel>(f, arena, f.pic, c);
+        const int st = f.pic_stride[c];
+        const int bd = c ? f.bit_depth_c : f.bit_depth;
+        const int maxv = (1 << bd) - 1;
+        if (tu.flags & H2J_TU_PCM) {
+            for (int e = lane; e < tu.ncoef; e += 64) {
+                const uint32_t en = CO[tu.coef + e];
+                const int pos = static_cast<int>(en >> 16);
+                P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<Pel>(static_cast<uint16_t>(en & 0xFFFF));
+            }
+            __syncthreads();
+            continue;
+        }
+        // ---------------- residual ----------------
+        const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
+        const int qp = tu.qp, qm = qp % 6;
+        const bool i16 = c == 0 && log2n == 4;
+        const bool chroma = c > 0;
+        if (cbf) {
+            for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
+            __syncthreads();
+            for (int e = lane; e < tu.ncoef; e += 64) {
+                const uint32_t en = CO[tu.coef + e];
+                s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
+            }
+            __syncthreads();
+            const uint8_t* w4 = f.scaling_list ? sl + f.sl + c * 16 : nullptr;
+            if (i16 || chroma) {
+                // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
+                const int nb = n >> 2;  // blocks per side: 4 (luma) / 2 (chroma)
+                if (lane < nb * nb) {
+                    const int r = lane / nb, q = lane % nb;
+                    int acc = 0;
+                    for (int i = 0; i < nb; i++)
+                        for (int j = 0; j < nb; j++) {
+                            const int hr = nb == 4 ? ((r == 0 || (r == 1 && i < 2) || (r == 2 && (i == 0 || i == 3)) || (r == 3 && !(i & 1))) ? 1 : -1)
+                                                   : ((r == 0 || i == 0) ? 1 : -1);
+                            const int hc = nb == 4 ? ((q == 0 || (q == 1 && j < 2) || (q == 2 && (j == 0 || j == 3)) || (q == 3 && !(j & 1))) ? 1 : -1)
+                                                   : ((q == 0 || j == 0) ? 1 : -1);
+                            acc += hr * hc * s.blk[(i * 4) * n + j * 4];
+                        }
+                    const int ls0 = (w4 ? w4[0] : 16) * kNorm4[qm][0];
+                    int v;
+                    if (nb == 4) v = qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+                    else v = ((acc * ls0) << (qp / 6)) >> 5;
+                    s.dc[lane] = v;
+                }
+                __syncthreads();
+                for (int i = lane; i < nn; i += 64) {
+                    const int y = i >> log2n, x = i & (n - 1);
+                    const int by = y >> 2, bx = x >> 2, ry = y & 3, rx = x & 3;
+                    if (ry == 0 && rx == 0) s.blk[i] = s.dc[by * (n >> 2) + bx];
+                    else s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[ry * 4 + rx] : 16) * h264_norm4(qm, ry, rx), qp);
+                }
+            } else if (log2n == 2) {
+                for (int i = lane; i < 16; i += 64)
+                    s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[i] : 16) * h264_norm4(qm, i >> 2, i & 3), qp);
+            } else {
+                const uint8_t* w8 = f.scaling_list ? sl + f.sl + 48 : nullptr;
+                for (int i = lane; i < 64; i += 64)
+                    s.blk[i] = h264_scale8(s.blk[i], (w8 ? w8[i] : 16) * h264_norm8(qm, i >> 3, i & 7), qp);
+            }
+            __syncthreads();
+            if (log2n == 3 && !chroma) {
+                // 8x8 inverse transform: rows (lanes 0..7) then columns
+                if (lane < 16) {
+                    const bool rows = lane < 8;
+                    (void)rows;
+                }
+                for (int pass = 0; pass < 2; pass++) {
+                    if (lane < 8) {
+                        int d[8], o[8];
+                        for (int k = 0; k < 8; k++) d[k] = pass == 0 ? s.blk[lane * 8 + k] : s.tmp[k * 8 + lane];
+                        const int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
+                        const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+                        const int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
+                        const int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
+                        const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+                        o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
+                        o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+                        if (pass == 0) for (int k = 0; k < 8; k++) s.tmp[lane * 8 + k] = o[k];
+                        else for (int k = 0; k < 8; k++) s.blk[k * 8 + lane] = (o[k] + 32) >> 6;
+                    }
+                    __syncthreads();
+                }
+            } else {
+                // 4x4 inverse transforms of all 4x4 blocks: lane = block * 4 + row/col
+                const int nb = n >> 2, nblk = nb * nb;
+                for (int pass = 0; pass < 2; pass++) {
+                    for (int id = lane; id < nblk * 4; id += 64) {
+                        const int b = id >> 2, k = id & 3;
+                        const int bx = (b % nb) * 4, by = (b / nb) * 4;
+                        int d0, d1, d2, d3;
+                        if (pass == 0) {
+                            const int* r = &s.blk[(by + k) * n + bx];
+                            d0 = r[0]; d1 = r[1]; d2 = r[2]; d3 = r[3];
+                        } else {
+                            d0 = s.tmp[(by + 0) * n + bx + k]; d1 = s.tmp[(by + 1) * n + bx + k];
+                            d2 = s.tmp[(by + 2) * n + bx + k]; d3 = s.tmp[(by + 3) * n + bx + k];
+                        }
+                        const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+                        if (pass == 0) {
+                            int* o = &s.tmp[(by + k) * n + bx];
+                            o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
+                        } else {
+                            s.blk[(by + 0) * n + bx + k] = (e0 + e3 + 32) >> 6;
+                            s.blk[(by + 1) * n + bx + k] = (e1 + e2 + 32) >> 6;
+                            s.blk[(by + 2) * n + bx + k] = (e1 - e2 + 32) >> 6;
+                            s.blk[(by + 3) * n + bx + k] = (e0 - e3 + 32) >> 6;
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        // ---------------- prediction ----------------
+        const int shc = c ? 1 : 0;
+        const int xl = x0 << shc, yl = y0 << shc;
+        const bool nxn = c == 0 && log2n <= 3;
+        const int ntop = nxn ? 2 * n : n;
+        if (lane == 0) {
+            int fl = 0;
+            if (h264_avail(f, mbs, slices, xl, yl, xl, yl - 1)) fl |= 1;
+            if (h264_avail(f, mbs, slices, xl, yl, xl - 1, yl)) fl |= 2;
+            if (h264_avail(f, mbs, slices, xl, yl, xl - 1, yl - 1)) fl |= 4;
+            if (nxn && h264_avail(f, mbs, slices, xl, yl, xl + n, yl - 1)) fl |= 8;
+            s.flags = fl;
+        }
+        __syncthreads();
+        const int fl = s.flags;
+        for (int i = lane; i <= ntop; i += 64) {
+            int v = 0;
+            if (i == 0) v = (fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0;
+            else if (i - 1 < n) v = (fl & 1) ? P[(y0 - 1) * st + x0 + i - 1] : 0;
+            else v = (fl & 8) ? P[(y0 - 1) * st + x0 + i - 1] : ((fl & 1) ? P[(y0 - 1) * st + x0 + n - 1] : 0);
+            s.top[i] = v;
+        }
+        for (int i = lane; i <= n; i += 64) s.left[i] = i == 0 ? ((fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0)
+                                                               : ((fl & 2) ? P[(y0 + i - 1) * st + x0 - 1] : 0);
+        __syncthreads();
+        const int mode = tu.mode;
+        const int* TT = s.top + 1;
+        const int* LL = s.left + 1;
+        if (nxn && log2n == 3) {
+            // 8.3.2.2.1 reference sample filtering
+            const bool at = fl & 1, al = fl & 2, ad = fl & 4;
+            for (int i = lane; i <= 16; i += 64) {
+                int v = 0;
+                if (i == 0) {
+                    const int C = s.top[0];
+                    if (!ad) v = C;
+                    else if (at && al) v = (TT[0] + 2 * C + LL[0] + 2) >> 2;
+                    else if (at) v = (3 * C + TT[0] + 2) >> 2;
+                    else if (al) v = (3 * C + LL[0] + 2) >> 2;
+                    else v = C;
+                } else if (at) {
+                    const int x = i - 1;
+                    if (x == 0) v = ad ? (s.top[0] + 2 * TT[0] + TT[1] + 2) >> 2 : (3 * TT[0] + TT[1] + 2) >> 2;
+                    else if (x == 15) v = (TT[14] + 3 * TT[15] + 2) >> 2;
+                    else v = (TT[x - 1] + 2 * TT[x] + TT[x + 1] + 2) >> 2;
+                }
+                s.ftop[i] = v;
+            }
+            for (int i = lane; i < 8; i += 64) {
+                int v = 0;
+                if (al) {
+                    if (i == 0) v = ad ? (s.top[0] + 2 * LL[0] + LL[1] + 2) >> 2 : (3 * LL[0] + LL[1] + 2) >> 2;
+                    else if (i == 7) v = (LL[6] + 3 * LL[7] + 2) >> 2;
+                    else v = (LL[i - 1] + 2 * LL[i] + LL[i + 1] + 2) >> 2;
+                }
+                s.fleft[i + 1] = v;
+            }
+            if (lane == 0) s.fleft[0] = 0;
+            __syncthreads();
+            if (lane == 0) s.fleft[0] = s.ftop[0];
+            __syncthreads();
+            TT = s.ftop + 1;
+            LL = s.fleft + 1;
+        }
+        // DC value
+        if (lane == 0) {
+            const bool at = fl & 1, al = fl & 2;
+            int sum = 0, v;
+            if (chroma) {
+                v = 0;  // per-quadrant below
+            } else {
+                const int lg = log2n;
+                if (at && al) {
+                    for (int i = 0; i < n; i++) sum += TT[i] + LL[i];
+                    v = (sum + n) >> (lg + 1);
+                } else if (al) {
+                    for (int i = 0; i < n; i++) sum += LL[i];
+                    v = (sum + (n >> 1)) >> lg;
+                } else if (at) {
+                    for (int i = 0; i < n; i++) sum += TT[i];
+                    v = (sum + (n >> 1)) >> lg;
+                } else {
+                    v = 1 << (bd - 1);
+                }
+            }
+            s.dcv = v;
+        }
+        __syncthreads();
+        const int dcv = s.dcv;
+        for (int i = lane; i < nn; i += 64) {
+            const int x = i & (n - 1), y = i >> log2n;
+            int pv;
+            if (nxn) {
+                pv = h264_pred_nxn(mode, x, y, n, TT, LL, dcv);
+            } else if (!chroma) {  // 16x16
+                if (mode == 0) pv = TT[x];
+                else if (mode == 1) pv = LL[y];
+                else if (mode == 2) pv = dcv;
+                else {
+                    int H = 0, V = 0;
+                    for (int k = 0; k < 8; k++) {
+                        H += (k + 1) * (TT[8 + k] - TT[6 - k]);
+                        V += (k + 1) * (LL[8 + k] - LL[6 - k]);
+                    }
+                    const int a = 16 * (LL[15] + TT[15]), b = (5 * H + 32) >> 6, cc = (5 * V + 32) >> 6;
+                    pv = clip3(0, maxv, (a + b * (x - 7) + cc * (y - 7) + 16) >> 5);
+                }
+            } else {  // chroma 8x8 (mode: 0 DC, 1 horizontal, 2 vertical, 3 plane)
+                if (mode == 1) pv = LL[y];
+                else if (mode == 2) pv = TT[x];
+                else if (mode == 3) {
+                    int H = 0, V = 0;
+                    for (int k = 0; k < 4; k++) {
+                        H += (k + 1) * (TT[4 + k] - TT[2 - k]);
+                        V += (k + 1) * (LL[4 + k] - LL[2 - k]);
+                    }
+                    const int a = 16 * (LL[7] + TT[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+                    pv = clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+                } else {
+                    const bool at = fl & 1, al = fl & 2;
+                    const int bx = x >> 2, by = y >> 2;
+                    int st4 = 0, sl4 = 0;
+                    for (int k = 0; k < 4; k++) { st4 += TT[bx * 4 + k]; sl4 += LL[by * 4 + k]; }
+                    if (bx == by) pv = (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1)));
+                    else if (bx) pv = at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1));
+                    else pv = al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
+                }
+            }
+            const int r = cbf ? s.blk[i] : 0;
+            P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(64) h2j_k1_recon(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
                                                   const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
                                                   uint8_t* arena) {
-    __shared__ K1Lds s;
+    __shared__ union {
+        K1Lds h5;
+        H4Lds h4;
+    } u;
+    K1Lds& s = u.h5;
     const h2j_frame& f = frames[blockIdx.x];
     for (int i = threadIdx.x; i < 1024; i += 64) {
         const int m = i >> 5, nn = i & 31;
@@ -364,6 +726,9 @@ __global__ void __launch_bounds__(64) h2j_k1_recon(const h2j_frame* frames, cons
     if (f.codec == H2J_CODEC_HEVC) {
         if (f.bit_depth == 8) hevc_recon_frame<uint8_t>(f, tus, coefs, C, S, sl, arena, s);
         else hevc_recon_frame<uint16_t>(f, tus, coefs, C, S, sl, arena, s);
+    } else if (f.codec == H2J_CODEC_H264) {
+        if (f.bit_depth == 8) h264_recon_frame<uint8_t>(f, tus, coefs, C, S, sl, arena, u.h4);
+        else h264_recon_frame<uint16_t>(f, tus, coefs, C, S, sl, arena, u.h4);
     }
 }
 
@@ -507,6 +872,158 @@ __global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* frames, c
     const h2j_slice* S = slices + f.slice;
     if (f.bit_depth == 8) deblock_thread<uint8_t>(f, C, S, arena, vert != 0, idx);
     else deblock_thread<uint16_t>(f, C, S, arena, vert != 0, idx);
+}
+
+
+// ---------------------------------------------------------------- K2': H.264 deblocking
+// H.264 8.7 filters macroblock by macroblock (vertical edges, then
+// horizontal edges) and each macroblock sees the samples already filtered by
+// its left / top / top-right neighbours, so it is not edge-parallel like
+// HEVC.  One workgroup per picture walks the anti-diagonals d = mx + 2*my
+// (all dependencies of an MB lie on earlier diagonals); 16 lanes per MB,
+// one lane per line across each edge phase.
+__constant__ uint8_t kAlpha264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
+                                      5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22, 25,  28,  32,  36,  40,  45,
+                                      50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+__constant__ uint8_t kBeta264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
+                                     2,  3,  3,  3,  3,  4,  4,  4,  6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
+                                     11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+__constant__ uint8_t kTc0_264[52][3] = {
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
+    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
+    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
+    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
+    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+DEVI int chroma_qp_264(int qpi) {
+    if (qpi < 30) return qpi;
+    const int t[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+    return t[qpi - 30];
+}
+
+template <typename Pel>
+DEVI void h264_filt_line(Pel* q, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
+    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
+    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+    if (chroma) {
+        if (bs < 4) {
+            const int tc = tc0 + 1;
+            const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+            q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
+            q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
+        } else {
+            q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
+            q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
+        }
+        return;
+    }
+    const int p2 = q[-3 * step], q2 = q[2 * step];
+    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+    if (bs < 4) {
+        const int tc = tc0 + (ap < beta) + (aq < beta);
+        const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+        q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
+        q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
+        if (ap < beta) q[-2 * step] = static_cast<Pel>(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1));
+        if (aq < beta) q[step] = static_cast<Pel>(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1));
+    } else {
+        const int p3 = q[-4 * step], q3 = q[3 * step];
+        const bool sm = abs(p0 - q0) < ((alpha >> 2) + 2);
+        if (ap < beta && sm) {
+            q[-step] = static_cast<Pel>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+            q[-2 * step] = static_cast<Pel>((p2 + p1 + p0 + q0 + 2) >> 2);
+            q[-3 * step] = static_cast<Pel>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+        } else {
+            q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
+        }
+        if (aq < beta && sm) {
+            q[0] = static_cast<Pel>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+            q[step] = static_cast<Pel>((p0 + q0 + q1 + q2 + 2) >> 2);
+            q[2 * step] = static_cast<Pel>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+        } else {
+            q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
+        }
+    }
+}
+
+// one phase (vertical or horizontal edges) of one MB, one lane = one line
+template <typename Pel>
+DEVI void h264_mb_phase(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, int mx,
+                        int my, bool vert, int l) {
+    const h2j_ctb& m = mbs[my * f.ctb_w + mx];
+    if (!(m.mbflags & 4)) return;
+    const h2j_slice& sl = slices[m.slice];
+    if (sl.deblock_disabled == 1) return;
+    const h2j_ctb* n = nullptr;
+    if (vert && mx > 0) n = &mbs[my * f.ctb_w + mx - 1];
+    if (!vert && my > 0) n = &mbs[(my - 1) * f.ctb_w + mx];
+    bool mb_edge = n != nullptr && (n->mbflags & 4);
+    if (mb_edge && sl.deblock_disabled == 2 && slices[n->slice].slice_addr_rs != sl.slice_addr_rs) mb_edge = false;
+    const int bd = f.bit_depth, bdc = f.bit_depth_c;
+    const int qm = (m.mbflags & 1) ? 0 : m.qp;
+    for (int e = 0; e < 4; e++) {
+        if (e == 0 && !mb_edge) continue;
+        if ((e & 1) && (m.mbflags & 2)) continue;
+        const int bs = e == 0 ? 4 : 3;
+        const int qn = e == 0 ? ((n->mbflags & 1) ? 0 : n->qp) : qm;
+        if (l < 16) {
+            const int qpav = (qn + qm + 1) >> 1;
+            const int ia = clip3(0, 51, qpav + sl.tc_offset), ib = clip3(0, 51, qpav + sl.beta_offset);
+            const int alpha = kAlpha264[ia] << (bd - 8), beta = kBeta264[ib] << (bd - 8);
+            const int tc0 = bs < 4 ? kTc0_264[ia][bs - 1] << (bd - 8) : 0;
+            Pel* Y = plane<Pel>(f, arena, f.pic, 0);
+            const int st = f.pic_stride[0];
+            Pel* q = vert ? &Y[(my * 16 + l) * st + mx * 16 + e * 4] : &Y[(my * 16 + e * 4) * st + mx * 16 + l];
+            h264_filt_line<Pel>(q, vert ? 1 : st, bs, alpha, beta, tc0, false, (1 << bd) - 1);
+        }
+        if ((e == 0 || e == 2)) {
+            const int c = l < 8 ? 1 : 2, k = l & 7;
+            const int off = sl.cqp_offset[c - 1];
+            const int qpp = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qn + off));
+            const int qpq = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qm + off));
+            const int qa = (qpp + qpq + 1) >> 1;
+            const int ia = clip3(0, 51, qa + sl.tc_offset), ib = clip3(0, 51, qa + sl.beta_offset);
+            const int alpha = kAlpha264[ia] << (bdc - 8), beta = kBeta264[ib] << (bdc - 8);
+            const int tc0 = bs < 4 ? kTc0_264[ia][bs - 1] << (bdc - 8) : 0;
+            Pel* C = plane<Pel>(f, arena, f.pic, c);
+            const int st = f.pic_stride[c];
+            Pel* q = vert ? &C[(my * 8 + k) * st + mx * 8 + e * 2] : &C[(my * 8 + e * 2) * st + mx * 8 + k];
+            h264_filt_line<Pel>(q, vert ? 1 : st, bs, alpha, beta, tc0, true, (1 << bdc) - 1);
+        }
+    }
+}
+
+template <typename Pel>
+__device__ void h264_deblock_frame(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena) {
+    const int mbw = f.ctb_w, mbh = f.ctb_h;
+    const int ndiag = mbw + 2 * (mbh - 1);
+    const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const int groups = blockDim.x >> 4;
+    for (int d = 0; d < ndiag; d++) {
+        const int ylo = d - mbw + 1 > 0 ? (d - mbw + 2) / 2 : 0;
+        const int yhi = min(mbh - 1, d / 2);
+        const int count = yhi - ylo + 1;
+        for (int base = 0; base < count; base += groups) {
+            const int k = base + g;
+            const int my = ylo + k, mx = d - 2 * my;
+            const bool act = k < count && mx >= 0 && mx < mbw;
+            if (act) h264_mb_phase<Pel>(f, mbs, slices, arena, mx, my, true, l);
+            __syncthreads();
+            if (act) h264_mb_phase<Pel>(f, mbs, slices, arena, mx, my, false, l);
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(512) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                        const h2j_slice* slices, uint8_t* arena) {
+    const h2j_frame& f = frames[blockIdx.x];
+    if (f.codec != H2J_CODEC_H264) return;
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    if (f.bit_depth == 8) h264_deblock_frame<uint8_t>(f, C, S, arena);
+    else h264_deblock_frame<uint16_t>(f, C, S, arena);
 }
 
 // ---------------------------------------------------------------- K3: SAO
@@ -930,7 +1447,10 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
     int r = check(hipGetLastError(), "h2j_k2_deblock(v)");
     if (r) return r;
     hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
-    return check(hipGetLastError(), "h2j_k2_deblock(h)");
+    r = check(hipGetLastError(), "h2j_k2_deblock(h)");
+    if (r) return r;
+    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->nframes), dim3(512), 0, s, b->frames, b->ctbs, b->slices, b->arena);
+    return check(hipGetLastError(), "h2j_k2_deblock264");
 }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {

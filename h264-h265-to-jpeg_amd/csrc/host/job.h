@@ -32,6 +32,8 @@ struct FrameJob {
 
 // Offsets of the scaling-factor tables inside FrameJob::sl
 enum { H2J_SL_S0 = 0, H2J_SL_S1 = 48, H2J_SL_S2 = 240, H2J_SL_S3 = 1008, H2J_SL_BYTES = 2032 };
+// H.264 weight-scale tables inside FrameJob::sl (raster order): 4x4 intra Y/Cb/Cr, 8x8 intra Y
+enum { H2J_SL264_4 = 0, H2J_SL264_8 = 48, H2J_SL264_BYTES = 112 };
 
 // Parse the first picture of an HEVC Annex-B stream into job records.
 // Returns 0 on success.

@@ -53,25 +53,27 @@ typedef struct {
 /* coefficient entry: (pos << 16) | (uint16_t)level, pos = y * n + x */
 typedef uint32_t h2j_coef;
 
+/* One HEVC CTB or one H.264 macroblock (log2ctb 4). */
 typedef struct {
-    int8_t type[3];     /* 0 off, 1 band, 2 edge */
+    int8_t type[3];     /* HEVC SAO: 0 off, 1 band, 2 edge */
     int8_t band_pos[3];
     int8_t eo_class[3];
     uint8_t slice;      /* index into the frame's slice table */
-    int16_t off[3][4];  /* SaoOffsetVal[1..4] */
+    int16_t off[3][4];  /* HEVC SaoOffsetVal[1..4] */
     uint16_t tile;      /* tile id */
-    uint16_t pad;
-    uint32_t ts;        /* CtbAddrRsToTs */
+    int8_t qp;          /* H.264: QPY of the macroblock (deblocking) */
+    uint8_t mbflags;    /* H.264: bit0 I_PCM, bit1 transform_size_8x8_flag, bit2 decoded */
+    uint32_t ts;        /* CtbAddrRsToTs (H.264: macroblock address) */
 } h2j_ctb;
 
 typedef struct {
-    int8_t beta_offset;     /* slice_beta_offset_div2 * 2 */
-    int8_t tc_offset;       /* slice_tc_offset_div2 * 2 */
+    int8_t beta_offset;     /* HEVC slice_beta_offset_div2 * 2 | H.264 FilterOffsetB */
+    int8_t tc_offset;       /* HEVC slice_tc_offset_div2 * 2   | H.264 FilterOffsetA */
     uint8_t sao_luma, sao_chroma;
     uint8_t lf_across_slices;
-    uint8_t deblock_disabled;
-    uint16_t pad;
-    int32_t slice_addr_rs;
+    uint8_t deblock_disabled; /* HEVC flag | H.264 disable_deblocking_filter_idc (0, 1, 2) */
+    int8_t cqp_offset[2];   /* H.264 chroma_qp_index_offset, second_chroma_qp_index_offset */
+    int32_t slice_addr_rs;  /* first CTB / macroblock of the slice */
 } h2j_slice;
 
 /* One picture.  Offsets are relative to the start of the batch's arrays. */
