@@ -1,0 +1,949 @@
+/*
+ * h264gen — deterministic H.264 (progressive 4:2:0, 8/10-bit, CABAC) intra
+ * still-picture ENCODER used only to mint test vectors and benchmark inputs.
+ * Test infrastructure: never linked into the product.  (The reference ships
+ * libx264.a as a prebuilt binary, which this build may not load.)
+ *
+ * One IDR picture: SPS (Main 77, High 100 or High10 110) + PPS + N slices.
+ * Macroblock decisions are heuristic (variance + SAD) with seeded random
+ * choices that exercise: I4x4 / I8x8 (transform_size_8x8_flag) / I16x16 /
+ * I_PCM, all prediction modes legal for the available neighbours, chroma
+ * modes, mb_qp_delta, chroma QP offsets, multiple slices, deblocking
+ * offsets / disable_deblocking_filter_idc.  Quantisation is generic
+ * least-squares against the decoder's own reconstruction basis, so the
+ * encoder reconstruction equals the decoder's by construction; the
+ * reconstruction is written with --recon for the tests.
+ *
+ * usage: h264gen in.yuv W H bitdepth qp seed out.h264 [options]
+ *   --t8x8 0|1 --pcm 0|1 --qpdelta 0|1 --slices N(MB rows, 0 = one)
+ *   --alpha A --beta B (div2 offsets) --dbidc 0|1|2 --cqp N --cqp2 N --recon out.yuv
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../oracle/bits.h"
+#include "../../oracle/cabac_tables.h"
+
+static uint64_t g_rng = 1;
+static uint32_t rnd(void) {
+    g_rng ^= g_rng << 13;
+    g_rng ^= g_rng >> 7;
+    g_rng ^= g_rng << 17;
+    return (uint32_t)(g_rng >> 11);
+}
+static int rndn(int n) { return (int)(rnd() % (uint32_t)n); }
+static int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* ------------------------------------------------------------ bit writer / NAL */
+typedef struct {
+    uint8_t *buf;
+    size_t cap, n;
+    uint32_t acc;
+    int nb;
+} BW;
+static void bw_init(BW *b) { b->cap = 1 << 16; b->buf = (uint8_t *)malloc(b->cap); b->n = 0; b->acc = 0; b->nb = 0; }
+static void bw_byte(BW *b, uint8_t v) {
+    if (b->n == b->cap) { b->cap *= 2; b->buf = (uint8_t *)realloc(b->buf, b->cap); }
+    b->buf[b->n++] = v;
+}
+static void bw_put(BW *b, uint32_t v, int n) {
+    for (int i = n - 1; i >= 0; i--) {
+        b->acc = (b->acc << 1) | ((v >> i) & 1);
+        if (++b->nb == 8) { bw_byte(b, (uint8_t)b->acc); b->acc = 0; b->nb = 0; }
+    }
+}
+static void bw_ue(BW *b, uint32_t v) {
+    uint32_t x = v + 1;
+    int len = 0;
+    while ((x >> len) > 1) len++;
+    bw_put(b, 0, len);
+    bw_put(b, x, len + 1);
+}
+static void bw_se(BW *b, int v) { bw_ue(b, v > 0 ? (uint32_t)(2 * v - 1) : (uint32_t)(-2 * v)); }
+static void bw_trailing(BW *b) { bw_put(b, 1, 1); while (b->nb) bw_put(b, 0, 1); }
+static void bw_align_zero(BW *b) { while (b->nb) bw_put(b, 0, 1); }
+static void write_nal(FILE *f, int ref_idc, int type, const uint8_t *p, size_t n) {
+    static const uint8_t sc[4] = {0, 0, 0, 1};
+    fwrite(sc, 1, 4, f);
+    uint8_t h = (uint8_t)((ref_idc << 5) | type);
+    fwrite(&h, 1, 1, f);
+    int zeros = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (zeros >= 2 && p[i] <= 3) { uint8_t e = 3; fwrite(&e, 1, 1, f); zeros = 0; }
+        fwrite(&p[i], 1, 1, f);
+        zeros = p[i] == 0 ? zeros + 1 : 0;
+    }
+}
+
+/* ------------------------------------------------------------ CABAC encoder */
+typedef struct {
+    BW *bw;
+    uint32_t low, range;
+    int bits_left, nbuf;
+    uint32_t bufbyte;
+} Enc;
+static void ce_start(Enc *e, BW *bw) { e->bw = bw; e->low = 0; e->range = 510; e->bits_left = 23; e->nbuf = 0; e->bufbyte = 0xff; }
+static void ce_writeout(Enc *e) {
+    uint32_t lead = e->low >> (24 - e->bits_left);
+    e->bits_left += 8;
+    e->low &= 0xffffffffu >> e->bits_left;
+    if (lead == 0xff) { e->nbuf++; return; }
+    if (e->nbuf > 0) {
+        uint32_t carry = lead >> 8, byte = e->bufbyte + carry;
+        e->bufbyte = lead & 0xff;
+        bw_put(e->bw, byte, 8);
+        byte = (0xff + carry) & 0xff;
+        while (e->nbuf > 1) { bw_put(e->bw, byte, 8); e->nbuf--; }
+    } else {
+        e->nbuf = 1;
+        e->bufbyte = lead;
+    }
+}
+static void ce_test(Enc *e) { if (e->bits_left < 12) ce_writeout(e); }
+static const uint8_t k_renorm[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+static void ce_bin(Enc *e, uint8_t *ctx, int bin) {
+    int s = *ctx >> 1, mps = *ctx & 1;
+    uint32_t lps = ora_lps_table[s][(e->range >> 6) & 3];
+    e->range -= lps;
+    if (bin != mps) {
+        int nb = k_renorm[lps >> 3];
+        e->low = (e->low + e->range) << nb;
+        e->range = lps << nb;
+        if (s == 0) mps = 1 - mps;
+        s = ora_trans_lps[s];
+        e->bits_left -= nb;
+    } else {
+        if (s < 62) s++;
+        *ctx = (uint8_t)((s << 1) | mps);
+        if (e->range >= 256) return;
+        e->low <<= 1;
+        e->range <<= 1;
+        e->bits_left--;
+    }
+    *ctx = (uint8_t)((s << 1) | mps);
+    ce_test(e);
+}
+static void ce_byp(Enc *e, int bin) { e->low <<= 1; if (bin) e->low += e->range; e->bits_left--; ce_test(e); }
+static void ce_term(Enc *e, int bin) {
+    e->range -= 2;
+    if (bin) { e->low += e->range; e->low <<= 7; e->range = 2 << 7; e->bits_left -= 7; }
+    else if (e->range >= 256) return;
+    else { e->low <<= 1; e->range <<= 1; e->bits_left--; }
+    ce_test(e);
+}
+static void ce_finish(Enc *e) {
+    if (e->low >> (32 - e->bits_left)) {
+        bw_put(e->bw, e->bufbyte + 1, 8);
+        while (e->nbuf > 1) { bw_put(e->bw, 0x00, 8); e->nbuf--; }
+        e->low -= 1u << (32 - e->bits_left);
+    } else {
+        if (e->nbuf > 0) bw_put(e->bw, e->bufbyte, 8);
+        while (e->nbuf > 1) { bw_put(e->bw, 0xff, 8); e->nbuf--; }
+    }
+    bw_put(e->bw, e->low >> 8, 24 - e->bits_left);
+}
+
+/* ------------------------------------------------------------ CABAC init (I) */
+#include "h264_init_I.inc"
+
+static const uint8_t k_sig8x8[64] = {0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3,
+                                     6, 7, 7, 7, 8, 9, 10, 9, 8, 7, 7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10,
+                                     9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
+static const uint8_t k_last8x8[64] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2,
+                                      2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4,
+                                      4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8, 8};
+static const uint8_t k_zz4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+static const uint8_t k_zz8[64] = {0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
+                                  41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                                  30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+static const uint8_t k_blk_x[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+static const uint8_t k_blk_y[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+static const uint8_t k_blk_of[4][4] = {{0, 1, 4, 5}, {2, 3, 6, 7}, {8, 9, 12, 13}, {10, 11, 14, 15}};
+
+/* ------------------------------------------------------------ state */
+typedef struct {
+    int slice, mb_type, t8x8, cbp, qp, cpm;
+    uint8_t ipm[16], cbf[16], cbf_c[2][4], cbf_dc[3];
+} Mb;
+
+typedef struct {
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2;
+    uint16_t *src[3], *rec[3];
+    int st[3];
+    Mb *mb;
+    int mbx, mby, cur_slice;
+    uint8_t ctx[460];
+    Enc ce;
+    int cur_qp, prev_qpd_nz;
+} G;
+
+static Mb *nb(G *g, int dx, int dy) {
+    int x = g->mbx + dx, y = g->mby + dy;
+    if (x < 0 || y < 0 || x >= g->mbw) return NULL;
+    if (dy > 0 || (dy == 0 && dx >= 0)) return NULL;
+    Mb *m = &g->mb[y * g->mbw + x];
+    return m->slice == g->cur_slice ? m : NULL;
+}
+static Mb *nb_blk(G *g, int bx, int by, int *nblk) {
+    int dx = 0, dy = 0;
+    if (bx < 0) { dx = -1; bx += 4; }
+    if (by < 0) { dy = -1; by += 4; }
+    if (bx > 3) { dx = 1; bx -= 4; }
+    *nblk = k_blk_of[by][bx];
+    return (dx == 0 && dy == 0) ? &g->mb[g->mby * g->mbw + g->mbx] : nb(g, dx, dy);
+}
+static int avail_luma(G *g, int x, int y, int cur_blk4) {
+    if (y < 0 && x < 0) return nb(g, -1, -1) != NULL;
+    if (y < 0 && x >= 16) return nb(g, 1, -1) != NULL;
+    if (y < 0) return nb(g, 0, -1) != NULL;
+    if (x < 0) return nb(g, -1, 0) != NULL;
+    if (x >= 16) return 0;
+    return k_blk_of[y >> 2][x >> 2] < cur_blk4;
+}
+static int px(G *g, int c, int x, int y) { return g->rec[c][y * g->st[c] + x]; }
+
+/* ------------------------------------------------------------ prediction (same formulas as the decoder) */
+typedef struct { int T[16], L[16], C, at, al, ad, atr; } Nb;
+
+static int pred_nxn(int mode, int x, int y, int n, const int *T, const int *L, int C, int dcv) {
+#define TT(i) ((i) < 0 ? C : T[i])
+#define LL(i) ((i) < 0 ? C : L[i])
+    switch (mode) {
+    case 0: return T[x];
+    case 1: return L[y];
+    case 2: return dcv;
+    case 3: return (x == n - 1 && y == n - 1) ? (T[2 * n - 2] + 3 * T[2 * n - 1] + 2) >> 2 : (T[x + y] + 2 * T[x + y + 1] + T[x + y + 2] + 2) >> 2;
+    case 4:
+        if (x > y) return (TT(x - y - 2) + 2 * TT(x - y - 1) + T[x - y] + 2) >> 2;
+        if (x < y) return (LL(y - x - 2) + 2 * LL(y - x - 1) + L[y - x] + 2) >> 2;
+        return (T[0] + 2 * C + L[0] + 2) >> 2;
+    case 5: {
+        int z = 2 * x - y;
+        if (z >= 0 && !(z & 1)) return (TT(x - (y >> 1) - 1) + T[x - (y >> 1)] + 1) >> 1;
+        if (z >= 0) return (TT(x - (y >> 1) - 2) + 2 * TT(x - (y >> 1) - 1) + T[x - (y >> 1)] + 2) >> 2;
+        if (z == -1) return (L[0] + 2 * C + T[0] + 2) >> 2;
+        return (L[y - 2 * x - 1] + 2 * L[y - 2 * x - 2] + LL(y - 2 * x - 3) + 2) >> 2;
+    }
+    case 6: {
+        int z = 2 * y - x;
+        if (z >= 0 && !(z & 1)) return (LL(y - (x >> 1) - 1) + L[y - (x >> 1)] + 1) >> 1;
+        if (z >= 0) return (LL(y - (x >> 1) - 2) + 2 * LL(y - (x >> 1) - 1) + L[y - (x >> 1)] + 2) >> 2;
+        if (z == -1) return (L[0] + 2 * C + T[0] + 2) >> 2;
+        return (T[x - 2 * y - 1] + 2 * T[x - 2 * y - 2] + TT(x - 2 * y - 3) + 2) >> 2;
+    }
+    case 7: { int i = x + (y >> 1); return !(y & 1) ? (T[i] + T[i + 1] + 1) >> 1 : (T[i] + 2 * T[i + 1] + T[i + 2] + 2) >> 2; }
+    default: {
+        int z = x + 2 * y, lim = 2 * n - 3;
+        if (z > lim) return L[n - 1];
+        if (z == lim) return (L[n - 2] + 3 * L[n - 1] + 2) >> 2;
+        int i = y + (x >> 1);
+        return !(z & 1) ? (L[i] + L[i + 1] + 1) >> 1 : (L[i] + 2 * L[i + 1] + L[i + 2] + 2) >> 2;
+    }
+    }
+#undef TT
+#undef LL
+}
+
+static void gather4(G *g, int blk, Nb *o) {
+    int x0 = k_blk_x[blk] * 4, y0 = k_blk_y[blk] * 4, gx = g->mbx * 16 + x0, gy = g->mby * 16 + y0;
+    o->at = avail_luma(g, x0, y0 - 1, blk);
+    o->al = avail_luma(g, x0 - 1, y0, blk);
+    o->ad = avail_luma(g, x0 - 1, y0 - 1, blk);
+    o->atr = avail_luma(g, x0 + 4, y0 - 1, blk);
+    for (int i = 0; i < 4; i++) {
+        o->T[i] = o->at ? px(g, 0, gx + i, gy - 1) : 0;
+        o->L[i] = o->al ? px(g, 0, gx - 1, gy + i) : 0;
+    }
+    for (int i = 4; i < 8; i++) o->T[i] = o->atr ? px(g, 0, gx + i, gy - 1) : o->T[3];
+    o->C = o->ad ? px(g, 0, gx - 1, gy - 1) : 0;
+}
+static void gather8(G *g, int b8, Nb *o) {
+    int x0 = (b8 & 1) * 8, y0 = (b8 >> 1) * 8, gx = g->mbx * 16 + x0, gy = g->mby * 16 + y0, blk4 = b8 * 4;
+    int at = avail_luma(g, x0, y0 - 1, blk4), al = avail_luma(g, x0 - 1, y0, blk4), ad = avail_luma(g, x0 - 1, y0 - 1, blk4);
+    int atr = avail_luma(g, x0 + 8, y0 - 1, blk4);
+    int Tr[16], Lr[8], C = ad ? px(g, 0, gx - 1, gy - 1) : 0;
+    for (int i = 0; i < 8; i++) { Tr[i] = at ? px(g, 0, gx + i, gy - 1) : 0; Lr[i] = al ? px(g, 0, gx - 1, gy + i) : 0; }
+    for (int i = 8; i < 16; i++) Tr[i] = atr ? px(g, 0, gx + i, gy - 1) : Tr[7];
+    memset(o, 0, sizeof(*o));
+    o->at = at; o->al = al; o->ad = ad; o->atr = atr;
+    if (at) {
+        o->T[0] = ad ? (C + 2 * Tr[0] + Tr[1] + 2) >> 2 : (3 * Tr[0] + Tr[1] + 2) >> 2;
+        for (int x = 1; x < 15; x++) o->T[x] = (Tr[x - 1] + 2 * Tr[x] + Tr[x + 1] + 2) >> 2;
+        o->T[15] = (Tr[14] + 3 * Tr[15] + 2) >> 2;
+    }
+    o->C = C;
+    if (ad) {
+        if (at && al) o->C = (Tr[0] + 2 * C + Lr[0] + 2) >> 2;
+        else if (at) o->C = (3 * C + Tr[0] + 2) >> 2;
+        else if (al) o->C = (3 * C + Lr[0] + 2) >> 2;
+    }
+    if (al) {
+        o->L[0] = ad ? (C + 2 * Lr[0] + Lr[1] + 2) >> 2 : (3 * Lr[0] + Lr[1] + 2) >> 2;
+        for (int y = 1; y < 7; y++) o->L[y] = (Lr[y - 1] + 2 * Lr[y] + Lr[y + 1] + 2) >> 2;
+        o->L[7] = (Lr[6] + 3 * Lr[7] + 2) >> 2;
+    }
+}
+static int mode_legal(int mode, const Nb *o) {
+    switch (mode) {
+    case 0: case 3: case 7: return o->at;
+    case 1: case 8: return o->al;
+    case 2: return 1;
+    default: return o->at && o->al && o->ad;
+    }
+}
+static void predict_nxn(G *g, int n, int mode, const Nb *o, int *pred) {
+    int dcv, s = 0, lg = n == 4 ? 2 : 3;
+    if (o->at && o->al) { for (int i = 0; i < n; i++) s += o->T[i] + o->L[i]; dcv = (s + n) >> (lg + 1); }
+    else if (o->al) { for (int i = 0; i < n; i++) s += o->L[i]; dcv = (s + n / 2) >> lg; }
+    else if (o->at) { for (int i = 0; i < n; i++) s += o->T[i]; dcv = (s + n / 2) >> lg; }
+    else dcv = 1 << (g->bd - 1);
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) pred[y * n + x] = pred_nxn(mode, x, y, n, o->T, o->L, o->C, dcv);
+}
+static void pred16(G *g, int mode, int *pred) {
+    int gx = g->mbx * 16, gy = g->mby * 16;
+    int at = nb(g, 0, -1) != NULL, al = nb(g, -1, 0) != NULL, ad = nb(g, -1, -1) != NULL;
+    int T[16], L[16], C = ad ? px(g, 0, gx - 1, gy - 1) : 0, maxv = (1 << g->bd) - 1;
+    for (int i = 0; i < 16; i++) { T[i] = at ? px(g, 0, gx + i, gy - 1) : 0; L[i] = al ? px(g, 0, gx - 1, gy + i) : 0; }
+    if (mode == 0) { for (int i = 0; i < 256; i++) pred[i] = T[i & 15]; return; }
+    if (mode == 1) { for (int i = 0; i < 256; i++) pred[i] = L[i >> 4]; return; }
+    if (mode == 2) {
+        int s = 0;
+        if (at && al) { for (int i = 0; i < 16; i++) s += T[i] + L[i]; s = (s + 16) >> 5; }
+        else if (al) { for (int i = 0; i < 16; i++) s += L[i]; s = (s + 8) >> 4; }
+        else if (at) { for (int i = 0; i < 16; i++) s += T[i]; s = (s + 8) >> 4; }
+        else s = 1 << (g->bd - 1);
+        for (int i = 0; i < 256; i++) pred[i] = s;
+        return;
+    }
+    int H = 0, V = 0;
+    for (int i = 0; i < 8; i++) { H += (i + 1) * (T[8 + i] - (i == 7 ? C : T[6 - i])); V += (i + 1) * (L[8 + i] - (i == 7 ? C : L[6 - i])); }
+    int a = 16 * (L[15] + T[15]), b = (5 * H + 32) >> 6, c = (5 * V + 32) >> 6;
+    for (int y = 0; y < 16; y++) for (int x = 0; x < 16; x++) pred[y * 16 + x] = clip3(0, maxv, (a + b * (x - 7) + c * (y - 7) + 16) >> 5);
+}
+static void predc(G *g, int c, int mode, int *pred) {
+    int gx = g->mbx * 8, gy = g->mby * 8;
+    int at = nb(g, 0, -1) != NULL, al = nb(g, -1, 0) != NULL, ad = nb(g, -1, -1) != NULL;
+    int T[8], L[8], C = ad ? px(g, c, gx - 1, gy - 1) : 0, maxv = (1 << g->bd) - 1;
+    for (int i = 0; i < 8; i++) { T[i] = at ? px(g, c, gx + i, gy - 1) : 0; L[i] = al ? px(g, c, gx - 1, gy + i) : 0; }
+    if (mode == 0) {
+        for (int by = 0; by < 2; by++)
+            for (int bx = 0; bx < 2; bx++) {
+                int st = 0, sl = 0, s;
+                for (int i = 0; i < 4; i++) { st += T[bx * 4 + i]; sl += L[by * 4 + i]; }
+                if (bx == by) s = (at && al) ? (st + sl + 4) >> 3 : at ? (st + 2) >> 2 : al ? (sl + 2) >> 2 : 1 << (g->bd - 1);
+                else if (bx) s = at ? (st + 2) >> 2 : al ? (sl + 2) >> 2 : 1 << (g->bd - 1);
+                else s = al ? (sl + 2) >> 2 : at ? (st + 2) >> 2 : 1 << (g->bd - 1);
+                for (int y = 0; y < 4; y++) for (int x = 0; x < 4; x++) pred[(by * 4 + y) * 8 + bx * 4 + x] = s;
+            }
+        return;
+    }
+    if (mode == 1) { for (int i = 0; i < 64; i++) pred[i] = L[i >> 3]; return; }
+    if (mode == 2) { for (int i = 0; i < 64; i++) pred[i] = T[i & 7]; return; }
+    int H = 0, V = 0;
+    for (int i = 0; i < 4; i++) { H += (i + 1) * (T[4 + i] - (i == 3 ? C : T[2 - i])); V += (i + 1) * (L[4 + i] - (i == 3 ? C : L[2 - i])); }
+    int a = 16 * (L[7] + T[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+    for (int y = 0; y < 8; y++) for (int x = 0; x < 8; x++) pred[y * 8 + x] = clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+}
+
+/* ------------------------------------------------------------ decoder-side residual (dequant + IDCT) */
+static const int k_norm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+static const int k_norm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                  {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+static int norm4(int m, int i, int j) { return (!(i & 1) && !(j & 1)) ? k_norm4[m][0] : ((i & 1) && (j & 1)) ? k_norm4[m][1] : k_norm4[m][2]; }
+static int norm8(int m, int i, int j) {
+    if (!(i & 3) && !(j & 3)) return k_norm8[m][0];
+    if ((i & 1) && (j & 1)) return k_norm8[m][1];
+    if ((i & 3) == 2 && (j & 3) == 2) return k_norm8[m][2];
+    if ((!(i & 3) && (j & 1)) || ((i & 1) && !(j & 3))) return k_norm8[m][3];
+    if ((!(i & 3) && (j & 3) == 2) || ((i & 3) == 2 && !(j & 3))) return k_norm8[m][4];
+    return k_norm8[m][5];
+}
+static int sc4(int l, int ls, int qp) { return qp >= 24 ? (l * ls) << (qp / 6 - 4) : (l * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6); }
+static int sc8(int l, int ls, int qp) { return qp >= 36 ? (l * ls) << (qp / 6 - 6) : (l * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6); }
+static void idct4(int *b) {
+    int t[16];
+    for (int i = 0; i < 4; i++) {
+        int *r = b + i * 4, e0 = r[0] + r[2], e1 = r[0] - r[2], e2 = (r[1] >> 1) - r[3], e3 = r[1] + (r[3] >> 1);
+        t[i * 4] = e0 + e3; t[i * 4 + 1] = e1 + e2; t[i * 4 + 2] = e1 - e2; t[i * 4 + 3] = e0 - e3;
+    }
+    for (int j = 0; j < 4; j++) {
+        int f0 = t[j], f1 = t[4 + j], f2 = t[8 + j], f3 = t[12 + j];
+        int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+        b[j] = (g0 + g3 + 32) >> 6; b[4 + j] = (g1 + g2 + 32) >> 6; b[8 + j] = (g1 - g2 + 32) >> 6; b[12 + j] = (g0 - g3 + 32) >> 6;
+    }
+}
+static void idct8_1d(const int *d, int *o) {
+    int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
+    int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
+    int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
+    int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1; o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+}
+static void idct8(int *b) {
+    int t[64], col[8], o[8];
+    for (int i = 0; i < 8; i++) idct8_1d(b + i * 8, t + i * 8);
+    for (int j = 0; j < 8; j++) {
+        for (int i = 0; i < 8; i++) col[i] = t[i * 8 + j];
+        idct8_1d(col, o);
+        for (int i = 0; i < 8; i++) b[i * 8 + j] = (o[i] + 32) >> 6;
+    }
+}
+/* residual of a 4x4 / 8x8 block from raster levels */
+static void res4(const int *lv, int qp, int *r) {
+    for (int i = 0; i < 16; i++) r[i] = sc4(lv[i], 16 * norm4(qp % 6, i >> 2, i & 3), qp);
+    idct4(r);
+}
+static void res8(const int *lv, int qp, int *r) {
+    for (int i = 0; i < 64; i++) r[i] = sc8(lv[i], 16 * norm8(qp % 6, i >> 3, i & 7), qp);
+    idct8(r);
+}
+/* MB-wide residual for I16x16 (n = 16, luma) or chroma (n = 8): DC levels at (4i,4j) */
+static void res_dc(const int *lv, int n, int qp, int *r) {
+    int nb = n / 4, dc[16];
+    for (int r0 = 0; r0 < nb; r0++)
+        for (int q = 0; q < nb; q++) {
+            int acc = 0;
+            for (int i = 0; i < nb; i++)
+                for (int j = 0; j < nb; j++) {
+                    int hr = nb == 4 ? ((r0 == 0 || (r0 == 1 && i < 2) || (r0 == 2 && (i == 0 || i == 3)) || (r0 == 3 && !(i & 1))) ? 1 : -1) : ((r0 == 0 || i == 0) ? 1 : -1);
+                    int hc = nb == 4 ? ((q == 0 || (q == 1 && j < 2) || (q == 2 && (j == 0 || j == 3)) || (q == 3 && !(j & 1))) ? 1 : -1) : ((q == 0 || j == 0) ? 1 : -1);
+                    acc += hr * hc * lv[(i * 4) * n + j * 4];
+                }
+            int ls0 = 16 * k_norm4[qp % 6][0];
+            dc[r0 * nb + q] = nb == 4 ? (qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6))
+                                      : ((acc * ls0) << (qp / 6)) >> 5;
+        }
+    for (int by = 0; by < nb; by++)
+        for (int bx = 0; bx < nb; bx++) {
+            int b[16];
+            for (int i = 0; i < 16; i++) b[i] = sc4(lv[(by * 4 + (i >> 2)) * n + bx * 4 + (i & 3)], 16 * norm4(qp % 6, i >> 2, i & 3), qp);
+            b[0] = dc[by * nb + bx];
+            idct4(b);
+            for (int i = 0; i < 16; i++) r[(by * 4 + (i >> 2)) * n + bx * 4 + (i & 3)] = b[i];
+        }
+}
+
+/* ------------------------------------------------------------ least-squares quantiser against the decoder basis */
+typedef struct { float *basis; int n, npos; } Basis; /* basis[pos][sample] for unit level */
+static Basis g_b4[64], g_b8[64], g_b16[64], g_bc[64];
+
+static void build_basis(Basis *B, int kind, int qp) {
+    int n = kind == 0 ? 4 : (kind == 1 ? 8 : (kind == 2 ? 16 : 8));
+    if (B->basis) return;
+    B->n = n;
+    B->npos = n * n;
+    B->basis = (float *)calloc((size_t)n * n * n * n, sizeof(float));
+    const int L = 64;
+    for (int p = 0; p < n * n; p++) {
+        int lv[256] = {0}, r[256];
+        if ((kind == 2 || kind == 3) && 0) {}
+        lv[p] = L;
+        if (kind == 0) res4(lv, qp, r);
+        else if (kind == 1) res8(lv, qp, r);
+        else res_dc(lv, n, qp, r);
+        for (int i = 0; i < n * n; i++) B->basis[p * n * n + i] = (float)r[i] / L;
+    }
+}
+/* levels[raster] minimising ||x - Σ l b|| approximately (independent projections + deadzone) */
+static void quantize(const Basis *B, const int *x, int *lv, int maxlev) {
+    int nn = B->npos;
+    for (int p = 0; p < nn; p++) {
+        const float *b = B->basis + (size_t)p * nn;
+        double dot = 0, bb = 0;
+        for (int i = 0; i < nn; i++) { dot += b[i] * x[i]; bb += (double)b[i] * b[i]; }
+        double v = bb > 0 ? dot / bb : 0;
+        int l = (int)(fabs(v) + 0.6667 - 1.0 + 0.3333 * 0 + 0.0);
+        l = (int)(fabs(v) + 1.0 / 3.0);
+        if (l > maxlev) l = maxlev;
+        lv[p] = v < 0 ? -l : l;
+    }
+}
+
+/* ------------------------------------------------------------ CABAC syntax */
+static int bin(G *g, int ctx, int v) { ce_bin(&g->ce, &g->ctx[ctx], v); return v; }
+
+static int cbf_cond(int cat, Mb *N, int nblk, int icbcr) {
+    if (!N) return 1;
+    if (N->mb_type == 25) return 1;
+    switch (cat) {
+    case 0: return (N->mb_type >= 1 && N->mb_type <= 24) ? N->cbf_dc[0] : 0;
+    case 1: case 2: return ((N->cbp >> (nblk >> 2)) & 1) ? N->cbf[nblk] : 0;
+    case 3: return (N->cbp >> 4) ? N->cbf_dc[1 + icbcr] : 0;
+    case 4: return (N->cbp >> 4) == 2 ? N->cbf_c[icbcr][nblk] : 0;
+    }
+    return 0;
+}
+
+/* coeffs in scan order; returns coded */
+static int enc_block(G *g, int cat, int cbf_inc, int maxnum, const int *co) {
+    static const int cbf_off[5] = {0, 4, 8, 12, 16}, sig_off[6] = {0, 15, 29, 44, 47, 0}, abs_off[6] = {0, 10, 20, 30, 39, 0};
+    int last = -1;
+    for (int i = 0; i < maxnum; i++) if (co[i]) last = i;
+    int coded = last >= 0;
+    if (cat != 5) bin(g, 85 + cbf_off[cat] + cbf_inc, coded);
+    if (!coded) return 0;
+    for (int i = 0; i < maxnum - 1; i++) {
+        int sc, lc;
+        if (cat == 5) { sc = 402 + k_sig8x8[i]; lc = 417 + k_last8x8[i]; }
+        else if (cat == 3) { int inc = i < 2 ? i : 2; sc = 105 + sig_off[3] + inc; lc = 166 + sig_off[3] + inc; }
+        else { sc = 105 + sig_off[cat] + i; lc = 166 + sig_off[cat] + i; }
+        bin(g, sc, co[i] != 0);
+        if (co[i]) { bin(g, lc, i == last); if (i == last) break; }
+    }
+    int eq1 = 0, gt1 = 0, absb = cat == 5 ? 426 : 227 + abs_off[cat];
+    for (int i = last; i >= 0; i--) {
+        if (!co[i]) continue;
+        int a = abs(co[i]) - 1;
+        int inc = gt1 ? 0 : (eq1 + 1 < 4 ? eq1 + 1 : 4);
+        bin(g, absb + inc, a > 0);
+        if (a > 0) {
+            int inc2 = 5 + (gt1 < 4 - (cat == 3) ? gt1 : 4 - (cat == 3));
+            int pre = a < 14 ? a : 14;
+            for (int k = 1; k < pre; k++) bin(g, absb + inc2, 1);
+            if (a < 14) bin(g, absb + inc2, 0);
+            else {
+                int s = a - 14, k = 0;
+                while (s >= (1 << k)) { ce_byp(&g->ce, 1); s -= 1 << k; k++; }
+                ce_byp(&g->ce, 0);
+                while (k--) ce_byp(&g->ce, (s >> k) & 1);
+            }
+        }
+        if (a == 0) eq1++; else gt1++;
+        ce_byp(&g->ce, co[i] < 0);
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------ macroblock encode */
+static int chroma_qp(int qpi) {
+    static const int t[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+    return qpi < 30 ? qpi : t[qpi - 30];
+}
+
+static long var16(G *g) {
+    long s = 0, s2 = 0;
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++) { int v = g->src[0][(g->mby * 16 + y) * g->st[0] + g->mbx * 16 + x]; s += v; s2 += (long)v * v; }
+    return (s2 - s * s / 256) / 256;
+}
+
+static void put(G *g, int c, int gx, int gy, int n, const int *pred, const int *r) {
+    int maxv = (1 << g->bd) - 1;
+    for (int y = 0; y < n; y++) for (int x = 0; x < n; x++) g->rec[c][(gy + y) * g->st[c] + gx + x] = (uint16_t)clip3(0, maxv, pred[y * n + x] + r[y * n + x]);
+}
+
+static void encode_mb(G *g) {
+    Mb *m = &g->mb[g->mby * g->mbw + g->mbx];
+    memset(m, 0, sizeof(*m));
+    m->slice = g->cur_slice;
+    const int gx = g->mbx * 16, gy = g->mby * 16;
+    long v = var16(g);
+    int scale = 1 << (2 * (g->bd - 8));
+    int pcm = g->pcm && rndn(40) == 0;
+    int is16 = !pcm && (v < (long)(g->qp * 2) * scale || rndn(12) == 0);
+    int t8 = !pcm && !is16 && g->t8x8 && rndn(2);
+    /* mb_type */
+    Mb *A = nb(g, -1, 0), *B = nb(g, 0, -1);
+    int ctx = (A && A->mb_type != 0) + (B && B->mb_type != 0);
+    /* decide I16x16 mode and levels first (mb_type carries cbp) */
+    int lv16[256] = {0}, lvc[2][64], pred[256], r[256], src[256];
+    int mode16 = 2, qpd = 0;
+    /* mb_qp_delta choice */
+    int new_qp = g->cur_qp;
+    if (g->qpdelta && rndn(4) == 0) new_qp = clip3(-6 * (g->bd - 8), 51, g->qp + rndn(7) - 3);
+    if (pcm) {
+        bin(g, 3 + ctx, 1);
+        ce_term(&g->ce, 1);
+        ce_finish(&g->ce);
+        bw_put(g->ce.bw, 1, 1);
+        bw_align_zero(g->ce.bw);
+        for (int y = 0; y < 16; y++) for (int x = 0; x < 16; x++) {
+            int s = g->src[0][(gy + y) * g->st[0] + gx + x];
+            bw_put(g->ce.bw, (uint32_t)s, g->bd);
+            g->rec[0][(gy + y) * g->st[0] + gx + x] = (uint16_t)s;
+        }
+        for (int c = 1; c < 3; c++) for (int y = 0; y < 8; y++) for (int x = 0; x < 8; x++) {
+            int s = g->src[c][(gy / 2 + y) * g->st[c] + gx / 2 + x];
+            bw_put(g->ce.bw, (uint32_t)s, g->bd);
+            g->rec[c][(gy / 2 + y) * g->st[c] + gx / 2 + x] = (uint16_t)s;
+        }
+        { BW *bw = g->ce.bw; ce_start(&g->ce, bw); }
+        m->mb_type = 25; m->qp = g->cur_qp; m->cbp = 0x2F;
+        memset(m->cbf, 1, 16); memset(m->cbf_c, 1, sizeof(m->cbf_c)); memset(m->cbf_dc, 1, 3);
+        for (int i = 0; i < 16; i++) m->ipm[i] = 2;
+        g->prev_qpd_nz = 0;
+        return;
+    }
+    int qp_use = new_qp; /* QP used for quantisation if the MB ends up coding a delta */
+    int qpl = qp_use + 6 * (g->bd - 8);
+    int maxlev = 2047;
+    if (is16) {
+        int at = B != NULL, al = A != NULL, ad = nb(g, -1, -1) != NULL;
+        long best = -1;
+        for (int md = 0; md < 4; md++) {
+            if ((md == 0 && !at) || (md == 1 && !al) || (md == 3 && !(at && al && ad))) continue;
+            pred16(g, md, pred);
+            long c = 0;
+            for (int i = 0; i < 256; i++) c += abs(g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i]);
+            if (best < 0 || c < best) { best = c; mode16 = md; }
+        }
+        pred16(g, mode16, pred);
+        for (int i = 0; i < 256; i++) src[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
+        Basis *Bs = &g_b16[qpl];
+        build_basis(Bs, 2, qpl);
+        quantize(Bs, src, lv16, maxlev);
+    }
+    /* chroma mode + levels need the chroma QP of the final QP */
+    int at = B != NULL, al = A != NULL, ad = nb(g, -1, -1) != NULL;
+    int cpm = rndn(4);
+    if ((cpm == 1 && !al) || (cpm == 2 && !at) || (cpm == 3 && !(at && al && ad))) cpm = 0;
+    /* chroma residual is computed after luma (recon order doesn't matter: chroma pred uses neighbour MBs only) */
+    int qpc[2];
+    for (int c = 0; c < 2; c++) qpc[c] = chroma_qp(clip3(-6 * (g->bd - 8), 51, qp_use + (c ? g->cqp2 : g->cqp))) + 6 * (g->bd - 8);
+    int predc_[2][64];
+    for (int c = 0; c < 2; c++) {
+        predc(g, 1 + c, cpm, predc_[c]);
+        int x[64];
+        for (int i = 0; i < 64; i++) x[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
+        Basis *Bs = &g_bc[qpc[c]];
+        build_basis(Bs, 3, qpc[c]);
+        quantize(Bs, x, lvc[c], maxlev);
+        if (rndn(5) == 0) for (int i = 0; i < 64; i++) if ((i & 3) || (i >> 3) & 3) lvc[c][i] = 0; /* DC-only chroma */
+    }
+    int chroma_dc = 0, chroma_ac = 0;
+    for (int c = 0; c < 2; c++) for (int i = 0; i < 64; i++) if (lvc[c][i]) { if ((i & 3) == 0 && ((i >> 3) & 3) == 0) chroma_dc = 1; else chroma_ac = 1; }
+    int cbp_c = chroma_ac ? 2 : (chroma_dc ? 1 : 0);
+    if (cbp_c < 2) for (int c = 0; c < 2; c++) for (int i = 0; i < 64; i++) if ((i & 3) || ((i >> 3) & 3)) lvc[c][i] = 0;
+    if (cbp_c == 0) memset(lvc, 0, sizeof(lvc));
+    if (is16) {
+        int ac = 0;
+        for (int i = 0; i < 256; i++) if (lv16[i] && ((i & 3) || ((i >> 4) & 3))) ac = 1;
+        if (!ac) for (int i = 0; i < 256; i++) if ((i & 3) || ((i >> 4) & 3)) lv16[i] = 0;
+        m->mb_type = 1 + mode16 + 4 * cbp_c + (ac ? 12 : 0);
+        m->cbp = (cbp_c << 4) | (ac ? 15 : 0);
+        bin(g, 3 + ctx, 1);
+        ce_term(&g->ce, 0);
+        bin(g, 6, ac);
+        bin(g, 7, cbp_c != 0);
+        if (cbp_c) bin(g, 8, cbp_c == 2);
+        bin(g, 9, mode16 >> 1);
+        bin(g, 10, mode16 & 1);
+    } else {
+        m->mb_type = 0;
+        bin(g, 3 + ctx, 0);
+        if (g->t8x8) {
+            int c8 = (A && A->t8x8) + (B && B->t8x8);
+            bin(g, 399 + c8, t8);
+        }
+        m->t8x8 = t8;
+    }
+    /* luma NxN: choose modes + levels block by block with reconstruction */
+    int lv4[16][16], lv8[4][64];
+    memset(lv4, 0, sizeof(lv4));
+    memset(lv8, 0, sizeof(lv8));
+    if (!is16) {
+        int nblk = t8 ? 4 : 16;
+        for (int i = 0; i < nblk; i++) {
+            int blk = t8 ? i * 4 : i, n = t8 ? 8 : 4;
+            int bx = t8 ? (i & 1) * 8 : k_blk_x[blk] * 4, by = t8 ? (i >> 1) * 8 : k_blk_y[blk] * 4;
+            Nb o;
+            if (t8) gather8(g, i, &o); else gather4(g, blk, &o);
+            long best = -1;
+            int bm = 2, p[64];
+            for (int md = 0; md < 9; md++) {
+                if (!mode_legal(md, &o)) continue;
+                if (md > 2 && rndn(3) == 0) continue;
+                predict_nxn(g, n, md, &o, p);
+                long c = 0;
+                for (int k = 0; k < n * n; k++) c += abs(g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k]);
+                if (best < 0 || c < best) { best = c; bm = md; }
+            }
+            /* signal */
+            int nblkA, nblkB;
+            Mb *NA = nb_blk(g, k_blk_x[blk] - 1, k_blk_y[blk], &nblkA);
+            int ma = !NA ? -1 : (NA->mb_type != 0 ? 2 : NA->ipm[nblkA]);
+            Mb *NB = nb_blk(g, k_blk_x[blk], k_blk_y[blk] - 1, &nblkB);
+            int mb2 = !NB ? -1 : (NB->mb_type != 0 ? 2 : NB->ipm[nblkB]);
+            int pm = (ma < 0 || mb2 < 0) ? 2 : (ma < mb2 ? ma : mb2);
+            bin(g, 68, bm == pm);
+            if (bm != pm) {
+                int rem = bm < pm ? bm : bm - 1;
+                bin(g, 69, rem & 1); bin(g, 69, (rem >> 1) & 1); bin(g, 69, (rem >> 2) & 1);
+            }
+            if (t8) for (int k = 0; k < 4; k++) m->ipm[blk + k] = (uint8_t)bm;
+            else m->ipm[blk] = (uint8_t)bm;
+            /* residual + recon now (later blocks predict from it) */
+            predict_nxn(g, n, bm, &o, p);
+            int x[64], rr[64];
+            for (int k = 0; k < n * n; k++) x[k] = g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k];
+            Basis *Bs = t8 ? &g_b8[qpl] : &g_b4[qpl];
+            build_basis(Bs, t8 ? 1 : 0, qpl);
+            int *lv = t8 ? lv8[i] : lv4[blk];
+            quantize(Bs, x, lv, maxlev);
+            if (t8) res8(lv, qpl, rr); else res4(lv, qpl, rr);
+            put(g, 0, gx + bx, gy + by, n, p, rr);
+        }
+    }
+    /* cbp for NxN */
+    if (!is16) {
+        int cbp = cbp_c << 4;
+        for (int b8 = 0; b8 < 4; b8++) {
+            int nz = 0;
+            if (t8) { for (int k = 0; k < 64; k++) nz |= lv8[b8][k] != 0; }
+            else for (int b4 = 0; b4 < 4; b4++) for (int k = 0; k < 16; k++) nz |= lv4[b8 * 4 + b4][k] != 0;
+            cbp |= nz << b8;
+        }
+        m->cbp = cbp;
+    }
+    /* chroma pred mode */
+    {
+        int c2 = (A && A->mb_type != 25 && A->cpm != 0) + (B && B->mb_type != 25 && B->cpm != 0);
+        bin(g, 64 + c2, cpm != 0);
+        if (cpm) { bin(g, 67, cpm > 1); if (cpm > 1) bin(g, 67, cpm > 2); }
+        m->cpm = cpm;
+    }
+    if (!is16) {
+        int cbp = m->cbp;
+        for (int b8 = 0; b8 < 4; b8++) {
+            int bx = b8 & 1, by = b8 >> 1, ca, cb;
+            if (bx == 0) ca = A ? (A->mb_type == 25 ? 0 : !((A->cbp >> (b8 + 1)) & 1)) : 0;
+            else ca = !((cbp >> (b8 - 1)) & 1);
+            if (by == 0) cb = B ? (B->mb_type == 25 ? 0 : !((B->cbp >> (b8 + 2)) & 1)) : 0;
+            else cb = !((cbp >> (b8 - 2)) & 1);
+            bin(g, 73 + ca + 2 * cb, (cbp >> b8) & 1);
+        }
+        int ac = A ? (A->mb_type == 25 ? 2 : (A->cbp >> 4)) : 0, bc = B ? (B->mb_type == 25 ? 2 : (B->cbp >> 4)) : 0;
+        bin(g, 77 + (ac > 0) + 2 * (bc > 0), cbp_c != 0);
+        if (cbp_c) bin(g, 77 + 4 + (ac == 2) + 2 * (bc == 2), cbp_c == 2);
+    }
+    /* mb_qp_delta: the levels were quantised at qp_use; if the MB codes a
+     * delta it must be qp_use - cur_qp, else QP stays cur_qp (only possible
+     * when nothing is coded, so the residual is zero either way) */
+    if ((m->cbp & 15) || (m->cbp >> 4) || is16) {
+        qpd = qp_use - g->cur_qp;
+        int k = qpd > 0 ? 2 * qpd - 1 : -2 * qpd;
+        int c0 = g->prev_qpd_nz ? 1 : 0;
+        bin(g, 60 + c0, k > 0);
+        if (k > 0) {
+            for (int i = 1; i < k; i++) bin(g, 60 + (i == 1 ? 2 : 3), 1);
+            bin(g, 60 + (k == 1 ? 2 : 3), 0);
+        }
+        g->cur_qp = qp_use;
+    } else if (qp_use != g->cur_qp) {
+        /* nothing coded: re-encode impossible; residual is all zero so recon matches */
+    }
+    g->prev_qpd_nz = qpd != 0;
+    m->qp = g->cur_qp;
+    /* residual syntax */
+    int co[64];
+    if (is16) {
+        for (int k = 0; k < 16; k++) { int rr = k_zz4[k]; co[k] = lv16[(rr >> 2) * 4 * 16 + (rr & 3) * 4]; }
+        m->cbf_dc[0] = (uint8_t)enc_block(g, 0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, co);
+    }
+    for (int b8 = 0; b8 < 4; b8++) {
+        if (!((m->cbp >> b8) & 1)) continue;
+        if (t8) {
+            for (int k = 0; k < 64; k++) co[k] = lv8[b8][k_zz8[k]];
+            enc_block(g, 5, 0, 64, co);
+            for (int k = 0; k < 4; k++) m->cbf[b8 * 4 + k] = 1;
+            continue;
+        }
+        for (int b4 = 0; b4 < 4; b4++) {
+            int blk = b8 * 4 + b4, bx = k_blk_x[blk], by = k_blk_y[blk], nb1;
+            Mb *NA = nb_blk(g, bx - 1, by, &nb1);
+            int ca = cbf_cond(is16 ? 1 : 2, NA, nb1, 0);
+            Mb *NB = nb_blk(g, bx, by - 1, &nb1);
+            int cb = cbf_cond(is16 ? 1 : 2, NB, nb1, 0);
+            if (is16) {
+                for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lv16[(by * 4 + (rr >> 2)) * 16 + bx * 4 + (rr & 3)]; }
+                m->cbf[blk] = (uint8_t)enc_block(g, 1, ca + 2 * cb, 15, co);
+            } else {
+                for (int k = 0; k < 16; k++) co[k] = lv4[blk][k_zz4[k]];
+                m->cbf[blk] = (uint8_t)enc_block(g, 2, ca + 2 * cb, 16, co);
+            }
+        }
+    }
+    if (m->cbp >> 4) {
+        for (int c = 0; c < 2; c++) {
+            for (int k = 0; k < 4; k++) co[k] = lvc[c][(k >> 1) * 4 * 8 + (k & 1) * 4];
+            m->cbf_dc[1 + c] = (uint8_t)enc_block(g, 3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, co);
+        }
+    }
+    if ((m->cbp >> 4) == 2) {
+        for (int c = 0; c < 2; c++)
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx = b4 & 1, by = b4 >> 1;
+                int ca = bx ? m->cbf_c[c][b4 - 1] : cbf_cond(4, A, b4 + 1, c);
+                int cb = by ? m->cbf_c[c][b4 - 2] : cbf_cond(4, B, b4 + 2, c);
+                for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lvc[c][(by * 4 + (rr >> 2)) * 8 + bx * 4 + (rr & 3)]; }
+                m->cbf_c[c][b4] = (uint8_t)enc_block(g, 4, ca + 2 * cb, 15, co);
+            }
+    }
+    /* reconstruction of I16x16 luma and chroma */
+    if (is16) {
+        res_dc(lv16, 16, qpl, r);
+        pred16(g, mode16, pred);
+        put(g, 0, gx, gy, 16, pred, r);
+    }
+    for (int c = 0; c < 2; c++) {
+        int rr[64];
+        res_dc(lvc[c], 8, qpc[c], rr);
+        put(g, 1 + c, gx / 2, gy / 2, 8, predc_[c], rr);
+    }
+    if (!is16) for (int i = 0; i < 16; i++) if (t8) {} /* ipm already set */
+    if (is16) for (int i = 0; i < 16; i++) m->ipm[i] = 2;
+}
+
+/* ------------------------------------------------------------ parameter sets */
+static void write_sps(FILE *f, G *g, int profile) {
+    BW b; bw_init(&b);
+    bw_put(&b, (uint32_t)profile, 8);
+    bw_put(&b, 0, 8);
+    bw_put(&b, 40, 8);
+    bw_ue(&b, 0);
+    if (profile >= 100) {
+        bw_ue(&b, 1);
+        bw_ue(&b, (uint32_t)(g->bd - 8)); bw_ue(&b, (uint32_t)(g->bd - 8));
+        bw_put(&b, 0, 1); /* transform bypass */
+        bw_put(&b, 0, 1); /* seq scaling matrix */
+    }
+    bw_ue(&b, 0);     /* log2_max_frame_num - 4 */
+    bw_ue(&b, 0);     /* poc type 0 */
+    bw_ue(&b, 0);     /* log2_max_poc_lsb - 4 */
+    bw_ue(&b, 1);     /* max_num_ref_frames */
+    bw_put(&b, 0, 1);
+    bw_ue(&b, (uint32_t)(g->mbw - 1));
+    bw_ue(&b, (uint32_t)(g->mbh - 1));
+    bw_put(&b, 1, 1); /* frame_mbs_only */
+    bw_put(&b, 1, 1); /* direct_8x8_inference */
+    int crop = g->outW != g->W || g->outH != g->H;
+    bw_put(&b, (uint32_t)crop, 1);
+    if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / 2); }
+    bw_put(&b, 0, 1); /* vui */
+    bw_trailing(&b);
+    write_nal(f, 3, 7, b.buf, b.n);
+    free(b.buf);
+}
+static void write_pps(FILE *f, G *g, int high) {
+    BW b; bw_init(&b);
+    bw_ue(&b, 0); bw_ue(&b, 0);
+    bw_put(&b, 1, 1); /* CABAC */
+    bw_put(&b, 0, 1);
+    bw_ue(&b, 0);     /* slice groups */
+    bw_ue(&b, 0); bw_ue(&b, 0);
+    bw_put(&b, 0, 1); bw_put(&b, 0, 2);
+    bw_se(&b, 0);     /* init qp 26 */
+    bw_se(&b, 0);
+    bw_se(&b, g->cqp);
+    bw_put(&b, 1, 1); /* deblocking filter control present */
+    bw_put(&b, 0, 1); /* constrained intra */
+    bw_put(&b, 0, 1); /* redundant pic cnt */
+    if (high) {
+        bw_put(&b, (uint32_t)g->t8x8, 1);
+        bw_put(&b, 0, 1);
+        bw_se(&b, g->cqp2);
+    }
+    bw_trailing(&b);
+    write_nal(f, 3, 8, b.buf, b.n);
+    free(b.buf);
+}
+
+static int opt_int(int argc, char **argv, const char *n, int d) { for (int i = 1; i + 1 < argc; i++) if (!strcmp(argv[i], n)) return atoi(argv[i + 1]); return d; }
+static const char *opt_str(int argc, char **argv, const char *n) { for (int i = 1; i + 1 < argc; i++) if (!strcmp(argv[i], n)) return argv[i + 1]; return NULL; }
+
+int main(int argc, char **argv) {
+    if (argc < 8) { fprintf(stderr, "usage: h264gen in.yuv W H bitdepth qp seed out.h264 [options]\n"); return 2; }
+    G *g = (G *)calloc(1, sizeof(G));
+    g->outW = atoi(argv[2]); g->outH = atoi(argv[3]); g->bd = atoi(argv[4]); g->qp = atoi(argv[5]);
+    g_rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)atoll(argv[6]) * 0x100000001B3ull;
+    g->t8x8 = opt_int(argc, argv, "--t8x8", 1);
+    g->pcm = opt_int(argc, argv, "--pcm", 0);
+    g->qpdelta = opt_int(argc, argv, "--qpdelta", 1);
+    g->slice_rows = opt_int(argc, argv, "--slices", 0);
+    g->alpha = opt_int(argc, argv, "--alpha", 0);
+    g->beta = opt_int(argc, argv, "--beta", 0);
+    g->dbidc = opt_int(argc, argv, "--dbidc", 0);
+    g->cqp = opt_int(argc, argv, "--cqp", 0);
+    g->cqp2 = opt_int(argc, argv, "--cqp2", g->cqp);
+    int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp ? 100 : 77));
+    g->W = (g->outW + 15) & ~15; g->H = (g->outH + 15) & ~15;
+    g->mbw = g->W / 16; g->mbh = g->H / 16;
+    FILE *fi = fopen(argv[1], "rb");
+    if (!fi) { perror("input"); return 1; }
+    for (int c = 0; c < 3; c++) {
+        int w = c ? g->W / 2 : g->W, h = c ? g->H / 2 : g->H, iw = c ? g->outW / 2 : g->outW, ih = c ? g->outH / 2 : g->outH;
+        g->st[c] = w;
+        g->src[c] = (uint16_t *)calloc((size_t)w * h, 2);
+        g->rec[c] = (uint16_t *)calloc((size_t)w * h, 2);
+        for (int y = 0; y < ih; y++) for (int x = 0; x < iw; x++) {
+            int v = g->bd == 8 ? fgetc(fi) : (fgetc(fi) | (fgetc(fi) << 8));
+            g->src[c][y * w + x] = (uint16_t)(v < 0 ? 0 : v);
+        }
+        for (int y = 0; y < h; y++) for (int x = 0; x < w; x++) g->src[c][y * w + x] = g->src[c][(y < ih ? y : ih - 1) * w + (x < iw ? x : iw - 1)];
+    }
+    fclose(fi);
+    g->mb = (Mb *)calloc((size_t)g->mbw * g->mbh, sizeof(Mb));
+    for (int i = 0; i < g->mbw * g->mbh; i++) g->mb[i].slice = -1;
+    FILE *fo = fopen(argv[7], "wb");
+    write_sps(fo, g, profile);
+    write_pps(fo, g, profile >= 100);
+    int rows = g->slice_rows > 0 ? g->slice_rows : g->mbh;
+    int nslice = 0;
+    for (int r0 = 0; r0 < g->mbh; r0 += rows, nslice++) {
+        BW b; bw_init(&b);
+        bw_ue(&b, (uint32_t)(r0 * g->mbw)); /* first_mb */
+        bw_ue(&b, 7);                         /* I (all slices I) */
+        bw_ue(&b, 0);                         /* pps */
+        bw_put(&b, 0, 4);                     /* frame_num */
+        bw_ue(&b, 0);                         /* idr_pic_id */
+        bw_put(&b, 0, 4);                     /* poc lsb */
+        bw_put(&b, 0, 1); bw_put(&b, 0, 1);   /* dec_ref_pic_marking (IDR) */
+        int sqp = clip3(-6 * (g->bd - 8), 51, g->qp + (nslice ? rndn(5) - 2 : 0));
+        bw_se(&b, sqp - 26);
+        int idc = g->dbidc;
+        bw_ue(&b, (uint32_t)idc);
+        if (idc != 1) { bw_se(&b, g->alpha); bw_se(&b, g->beta); }
+        while (b.nb) bw_put(&b, 1, 1);        /* cabac_alignment_one_bit */
+        for (int i = 0; i < 460; i++) {
+            int mm = k_init_I[i][0], nn = k_init_I[i][1];
+            int pre = clip3(1, 126, ((mm * clip3(0, 51, sqp)) >> 4) + nn), mps = pre <= 63 ? 0 : 1;
+            g->ctx[i] = (uint8_t)(((mps ? pre - 64 : 63 - pre) << 1) | mps);
+        }
+        ce_start(&g->ce, &b);
+        g->cur_slice = nslice;
+        g->cur_qp = sqp;
+        g->prev_qpd_nz = 0;
+        int r1 = r0 + rows < g->mbh ? r0 + rows : g->mbh;
+        for (int my = r0; my < r1; my++)
+            for (int mx = 0; mx < g->mbw; mx++) {
+                g->mbx = mx; g->mby = my;
+                g->mb[my * g->mbw + mx].slice = nslice;
+                encode_mb(g);
+                ce_term(&g->ce, my == r1 - 1 && mx == g->mbw - 1);
+            }
+        ce_finish(&g->ce);
+        bw_put(&b, 1, 1);
+        bw_align_zero(&b);
+        write_nal(fo, 3, 5, b.buf, b.n);
+        free(b.buf);
+    }
+    fclose(fo);
+    const char *rp = opt_str(argc, argv, "--recon");
+    if (rp) {
+        FILE *fr = fopen(rp, "wb");
+        for (int c = 0; c < 3; c++) {
+            int iw = c ? g->outW / 2 : g->outW, ih = c ? g->outH / 2 : g->outH;
+            for (int y = 0; y < ih; y++) for (int x = 0; x < iw; x++) {
+                uint16_t v = g->rec[c][y * g->st[c] + x];
+                if (g->bd == 8) fputc(v, fr); else { fputc(v & 255, fr); fputc(v >> 8, fr); }
+            }
+        }
+        fclose(fr);
+    }
+    return 0;
+}
