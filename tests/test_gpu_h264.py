@@ -31,3 +31,39 @@ def test_h264_decoded_bit_exact(engine):
 def test_h264_transcode_matches_fixture(engine):
     s = read(golden("img01.h264"))
     assert engine.transcode([s])[0] == read(golden("img01.h264.jpeg"))
+
+
+import glob
+import os
+
+H264_DIR = golden("h264")
+PARITY264 = sorted(glob.glob(os.path.join(H264_DIR, "*.h264")))
+
+
+@pytest.mark.parametrize("path", PARITY264, ids=[os.path.basename(p) for p in PARITY264])
+def test_h264_parity_vectors(engine, path):
+    """h264gen vectors: Main/High/High10, I8x8, PCM, slices, QP deltas,
+    chroma QP offsets, deblocking offsets and disable_deblocking_filter_idc."""
+    s = read(path)
+    for stage, skip in ((1, True), (0, False)):
+        gy, gu, gv, bd = engine.decode(s, stage=stage)
+        oy, ou, ov, obd = O.decode(s, 264, skip_loop_filter=skip)
+        assert bd == obd
+        _cmp((gy, gu, gv), (oy, ou, ov), f"stage {stage}")
+
+
+def test_h264_mixed_codec_batch(engine):
+    """H.264 and H.265 pictures in one batch; every JPEG byte-exact."""
+    streams = [read(p) for p in PARITY264] + [read(golden("img01.h264")), read(golden("img01.h265"))]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, PARITY264 + ["img01.h264", "img01.h265"]):
+        assert o is not None, p
+        assert o == O.transcode(s), p
+
+
+def test_h264_bench_streams_sample(engine):
+    paths = sorted(glob.glob(os.path.join(golden("bench264"), "*.h264")))[::5]
+    streams = [read(p) for p in paths]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, paths):
+        assert o == O.transcode(s), p

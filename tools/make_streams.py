@@ -10,6 +10,8 @@ reconstruction bit-for-bit.
   python tools/make_streams.py bench   -> tests/golden/bench/hevc1080_XX.h265 (16 streams)
   python tools/make_streams.py parity  -> tests/golden/hevc/*.h265 + manifest.json
   python tools/make_streams.py 4k      -> tests/golden/bench4k/hevc2160_10b_XX.h265
+  python tools/make_streams.py parity264 -> tests/golden/h264/*.h264 + manifest.json (tools/h264gen)
+  python tools/make_streams.py bench264  -> tests/golden/bench264/avc1080_XX.h264 (16 streams, High 8x8)
 """
 import json
 import os
@@ -23,12 +25,14 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle_py as O  # noqa: E402
 
 GEN = os.path.join(ROOT, "tools", "hevcgen", "hevcgen")
+GEN264 = os.path.join(ROOT, "tools", "h264gen", "h264gen")
 
 
 def build_gen():
-    src = GEN + ".c"
-    if not os.path.exists(GEN) or os.path.getmtime(GEN) < os.path.getmtime(src):
-        subprocess.check_call(["gcc", "-O2", "-o", GEN, src, "-lm"])
+    for gen in (GEN, GEN264):
+        src = gen + ".c"
+        if not os.path.exists(gen) or os.path.getmtime(gen) < os.path.getmtime(src):
+            subprocess.check_call(["gcc", "-O2", "-o", gen, src, "-lm"])
 
 
 def source_planes():
@@ -65,16 +69,16 @@ def make_content(planes, W, H, seed, sigma, bd, upsample=1):
     return out
 
 
-def encode(planes, W, H, bd, qp, seed, path, opts=()):
+def encode(planes, W, H, bd, qp, seed, path, opts=(), codec=265):
     yuv = path + ".yuv"
     rec = path + ".rec"
     dt = np.uint8 if bd == 8 else np.dtype("<u2")
     with open(yuv, "wb") as f:
         for p in planes:
             f.write(p.astype(dt).tobytes())
-    subprocess.check_call([GEN, yuv, str(W), str(H), str(bd), str(qp), str(seed), path, "--recon", rec] + list(opts))
+    subprocess.check_call([GEN if codec == 265 else GEN264, yuv, str(W), str(H), str(bd), str(qp), str(seed), path, "--recon", rec] + list(opts))
     s = open(path, "rb").read()
-    y, u, v, b = O.decode(s, 265, skip_loop_filter=True)
+    y, u, v, b = O.decode(s, codec, skip_loop_filter=True)
     r = np.fromfile(rec, dtype=dt).astype(np.int32)
     ys, cs = W * H, (W // 2) * (H // 2)
     ok = (np.array_equal(y, r[:ys].reshape(H, W)) and np.array_equal(u, r[ys:ys + cs].reshape(H // 2, W // 2))
@@ -134,6 +138,56 @@ def parity():
     json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
 
 
+PARITY264 = [
+    # name, W, H, bd, qp, seed, sigma, options   (h264gen)
+    ("a01_416x240_q22_main", 416, 240, 8, 22, 31, 2, ["--t8x8", "0"]),
+    ("a02_416x240_q30_high8x8", 416, 240, 8, 30, 32, 2, ["--t8x8", "1"]),
+    ("a03_400x232_pcm_slices", 400, 232, 8, 28, 33, 3, ["--pcm", "1", "--slices", "3"]),
+    ("a04_352x288_10bit_high10", 352, 288, 10, 27, 34, 2, ["--pcm", "1"]),
+    ("a05_256x144_cqp_offsets", 256, 144, 8, 18, 35, 4, ["--cqp", "4", "--cqp2", "-3", "--alpha", "3", "--beta", "-2"]),
+    ("a06_352x288_q12_noise", 352, 288, 8, 12, 36, 6, []),
+    ("a07_336x200_q45", 336, 200, 8, 45, 37, 0, ["--alpha", "-4", "--beta", "5"]),
+    ("a08_320x176_dbidc1", 320, 176, 8, 26, 38, 3, ["--dbidc", "1"]),
+    ("a09_480x272_dbidc2_slices", 480, 272, 8, 33, 39, 2, ["--dbidc", "2", "--slices", "2"]),
+    ("a10_200x120_noqpd", 200, 120, 8, 24, 40, 2, ["--qpdelta", "0"]),
+    ("a11_64x64_tiny", 64, 64, 8, 26, 41, 2, []),
+    ("a12_72x40_odd_crop", 72, 40, 8, 20, 42, 5, ["--pcm", "1"]),
+    ("a13_320x180_10bit_q0", 320, 180, 10, 0, 43, 4, ["--t8x8", "0", "--cqp", "-5"]),
+]
+
+
+def parity264():
+    out_dir = os.path.join(ROOT, "tests/golden/h264")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    manifest = []
+    for name, W, H, bd, qp, seed, sigma, opts in PARITY264:
+        content = make_content(planes, W, H, seed, sigma, bd)
+        path = os.path.join(out_dir, name + ".h264")
+        nb = encode(content, W, H, bd, qp, seed, path, opts, codec=264)
+        manifest.append({"file": name + ".h264", "w": W, "h": H, "bit_depth": bd, "qp": qp, "options": opts})
+        print(f"{path}: {nb} B", flush=True)
+    json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
+def bench264(n=16):
+    """Config 3: 1080p H.264 High (8x8 transform) I-frames."""
+    out_dir = os.path.join(ROOT, "tests/golden/bench264")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    qps = [22, 27, 32, 37]
+    sigmas = [0, 2, 4]
+    total = 0
+    for i in range(n):
+        qp, sigma = qps[i % 4], sigmas[(i // 4) % 3]
+        content = make_content(planes, 1920, 1080, 200 + i, sigma, 8)
+        path = os.path.join(out_dir, f"avc1080_{i:02d}.h264")
+        nb = encode(content, 1920, 1080, 8, qp, 200 + i, path, ["--t8x8", "1"], codec=264)
+        total += nb
+        print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+    print("total", total)
+
+
 def fourk(n=4):
     out_dir = os.path.join(ROOT, "tests/golden/bench4k")
     os.makedirs(out_dir, exist_ok=True)
@@ -149,4 +203,4 @@ def fourk(n=4):
 if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
-    {"bench": bench, "parity": parity, "4k": fourk}[what]()
+    {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264}[what]()
