@@ -29,7 +29,22 @@ sys.path.insert(0, os.path.join(ROOT, "h264-h265-to-jpeg_amd"))
 
 METRIC = "1080p H.265 I-frames/sec → JPEG at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
-BYTES_PER_FRAME_1080P = 15_552_000  # B = 5S, S = 1.5*W*H
+# algorithmic bytes per frame B = 5S, S = 1.5*W*H*bytes_per_sample
+WORKLOADS = {
+    "hevc1080": dict(streams="tests/golden/bench/hevc1080_*.h265", w=1920, h=1080, bps=1,
+                     desc="configs[1]: batch of 1024 x 1080p H.265 Main 8-bit I-frames -> JPEG per GPU",
+                     data="16 hevcgen 1080p HEVC Main I-frame streams (tests/golden/bench)"),
+    "avc1080": dict(streams="tests/golden/bench264/avc1080_*.h264", w=1920, h=1080, bps=1,
+                    desc="configs[2]: batch of 1024 x 1080p H.264 High (8x8 transform) I-frames -> JPEG per GPU",
+                    data="16 h264gen 1080p H.264 High CABAC I-frame streams (tests/golden/bench264)"),
+    "hevc2160": dict(streams="tests/golden/bench4k/hevc2160_10b_*.h265", w=3840, h=2160, bps=2,
+                     desc="configs[3]: 4K H.265 Main10 I-frames, 10-bit decode -> 8-bit JPEG per GPU",
+                     data="4 hevcgen 2160p HEVC Main10 I-frame streams (tests/golden/bench4k)"),
+}
+
+
+def alg_bytes_per_frame(wl):
+    return 5 * (wl["w"] * wl["h"] * 3 // 2) * wl["bps"]
 
 
 def load_streams(pattern):
@@ -64,7 +79,7 @@ def cpu_baseline(streams, budget_s=12.0):
             break
     dt = time.time() - t0
     return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} of the {len(streams)} distinct 1080p streams, oracle decode+JPEG, 1 thread"}
+            "sample": f"{n} of the {len(streams)} distinct benchmark streams, oracle decode+JPEG, 1 thread"}
 
 
 def main():
@@ -74,7 +89,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=1024, help="frames per GPU per step")
     ap.add_argument("--threads", type=int, default=16, help="host entropy/Huffman threads per GPU")
-    ap.add_argument("--streams", default="tests/golden/bench/hevc1080_*.h265")
+    ap.add_argument("--workload", default="hevc1080", choices=sorted(WORKLOADS),
+                    help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]")
+    ap.add_argument("--streams", default=None, help="override the workload's stream glob")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -92,7 +109,8 @@ def main():
         dist = tdist
 
     import h2j
-    streams = load_streams(args.streams)
+    wl = WORKLOADS[args.workload]
+    streams = load_streams(args.streams or wl["streams"])
     n = args.frames
     batch = [streams[i % len(streams)] for i in range(n)]
     eng = h2j.Engine(local, args.threads)
@@ -149,9 +167,9 @@ def main():
         per = {k: v / steps for k, v in stage_sum.items()}
         recon_ms = per["recon_ms"]
         gpu_ms = per["h2d_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"] + per["d2h_ms"]
-        alg_bytes = BYTES_PER_FRAME_1080P * n
+        alg_bytes = alg_bytes_per_frame(wl) * n
         achieved = alg_bytes / (recon_ms / 1e3) / 1e9
-        traffic = pmc_traffic()
+        traffic = pmc_traffic() if args.workload == "hevc1080" else None
         res = {
             "metric": METRIC,
             "value": total_frames / elapsed,
@@ -164,8 +182,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: 16 hevcgen 1080p HEVC Main I-frame streams (tests/golden/bench) tiled to the batch",
-            "config": {"workload": "configs[1]: batch of 1024 x 1080p H.265 Main 8-bit I-frames -> JPEG per GPU",
+            "data": f"synthetic: {wl['data']} tiled to the batch",
+            "config": {"workload": wl["desc"], "workload_key": args.workload,
                        "frames_per_gpu": n, "global_batch": n * world, "host_threads_per_gpu": args.threads,
                        "parallelism": f"independent replicas x{world}"},
             "roofline": {"bound": "hbm", "kernel": "h2j_k1_recon", "achieved": achieved, "peak": HBM_PEAK_GBPS,

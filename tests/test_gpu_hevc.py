@@ -92,3 +92,15 @@ def test_bench_streams_sample(engine):
 def test_invalid_inputs_fail_cleanly(engine):
     outs = engine.transcode([b"", b"\x00\x00\x01\x40garbage", read(golden("img01.h265"))[:1000]])
     assert outs[0] is None and outs[1] is None
+
+
+def test_4k_main10_stream(engine):
+    """configs[3]: 3840x2160 Main10 -> 10-bit decode bit-exact, 8-bit JPEG byte-exact."""
+    path = sorted(glob.glob(os.path.join(golden("bench4k"), "*.h265")))[0]
+    s = read(path)
+    gy, gu, gv, bd = engine.decode(s, stage=0)
+    oy, ou, ov, obd = O.decode(s, 265)
+    assert bd == obd == 10
+    for g, o, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
+        assert np.array_equal(g, o), name
+    assert engine.transcode([s])[0] == O.transcode(s)
