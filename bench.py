@@ -166,7 +166,8 @@ def main():
         steps = args.steps
         per = {k: v / steps for k, v in stage_sum.items()}
         recon_ms = per["recon_ms"]
-        gpu_ms = per["h2d_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"] + per["d2h_ms"]
+        gpu_ms = (per["h2d_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"]
+                  + per["entropy_ms"] + per["d2h_ms"])
         alg_bytes = alg_bytes_per_frame(wl) * n
         achieved = alg_bytes / (recon_ms / 1e3) / 1e9
         traffic = pmc_traffic() if args.workload == "hevc1080" else None

@@ -1,0 +1,562 @@
+// MI355X (gfx950) JPEG entropy stage: symbol histograms, FFmpeg-exact optimal
+// Huffman tables and baseline-JPEG bit emission, all on the GPU, so only the
+// entropy-coded payload (~1/30 of the coefficient bytes) crosses PCIe.
+//
+//   K4d h2j_k4d_histogram  — per 256-block tile: coefficients staged through
+//                            LDS (coalesced 16 B loads, padded rows), per-lane
+//                            non-zero mask walk, LDS histogram, one global
+//                            atomic per (tile, symbol)
+//   K5a h2j_k5a_tables     — one workgroup per (frame, table): AV_QSORT +
+//                            package-merge (max length 16) restated without
+//                            item lists (per-level probability arrays + leaf
+//                            prefix counts), then the length sort and canonical
+//                            code assignment of mjpegenc_huffman.c
+//   K5b h2j_k5b_tile_bits  — bits per 256-block tile
+//   K5c h2j_k5c_scan       — per-frame tile offsets, payload sizes, then the
+//                            batch-level segment offsets (one workgroup)
+//   K5z h2j_k5z_zero       — clears the used part of the segment pool
+//   K5d h2j_k5d_emit       — per lane one block: workgroup scan of block bit
+//                            counts, MSB-first words, atomicOr only on the two
+//                            words a block can share with its neighbours
+//
+// Byte stuffing (0xFF -> 0xFF 0x00) is left to the host, which copies the
+// payload into the JPEG container anyway.  Reference semantics: FFmpeg
+// mjpegenc_common.c / mjpegenc_huffman.c as restated in SURVEY.md Appendix A
+// (A.6) and oracle/jpeg_ref.c; the host restatement is
+// csrc/host/jpeg_writer.cpp.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "h2j_gpu.h"
+
+#define DEVI __device__ __forceinline__
+
+namespace {
+
+constexpr int kTile = 256;      // blocks per workgroup
+constexpr int kRow = 33;        // LDS words per staged block (32 + 1 pad: conflict-free lane-per-block reads)
+
+DEVI int nbits16(int v) {
+    const unsigned a = static_cast<unsigned>(v < 0 ? -v : v);
+    return a ? 32 - __clz(a) : 0;
+}
+
+DEVI int nblocks(const h2j_frame& f) { return ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6; }
+
+// Stage blocks [b0, b0+nb) of a frame's zigzag coefficients into LDS rows.
+DEVI void stage_tile(const int16_t* co, int b0, int nb, uint32_t* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(co + static_cast<size_t>(b0) * 64);
+    for (int i = threadIdx.x; i < nb * 8; i += blockDim.x) {
+        const uint4 v = src[i];
+        uint32_t* d = lds + (i >> 3) * kRow + (i & 7) * 4;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+    }
+}
+
+DEVI int coef_at(const uint32_t* row, int i) {
+    const uint32_t w = row[i >> 1];
+    return static_cast<int16_t>((i & 1) ? (w >> 16) : (w & 0xffff));
+}
+
+// Non-zero mask of AC coefficients 1..63 of a staged block.
+DEVI uint64_t ac_mask(const uint32_t* row) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int w = 0; w < 32; w++) {
+        const uint32_t x = row[w];
+        m |= static_cast<uint64_t>((x & 0xffff) != 0) << (2 * w);
+        m |= static_cast<uint64_t>((x >> 16) != 0) << (2 * w + 1);
+    }
+    return m & ~1ull;
+}
+
+// DC predictor of block bi (MCU order Y0 Y1 Y2 Y3 Cb Cr, FFmpeg last_dc = 128 start)
+DEVI int prev_dc(const int16_t* co, const uint32_t* lds, int b0, int bi) {
+    const int mcu = bi / 6, b = bi - mcu * 6;
+    int pb;
+    if (b < 4) pb = b > 0 ? bi - 1 : (mcu > 0 ? bi - 3 : -1);
+    else pb = mcu > 0 ? bi - 6 : -1;
+    if (pb < 0) return 128;
+    if (pb >= b0) return coef_at(lds + (pb - b0) * kRow, 0);
+    return co[static_cast<size_t>(pb) * 64];
+}
+
+// ---------------------------------------------------------------- K4d
+__global__ void __launch_bounds__(kTile) h2j_k4d_histogram(const h2j_frame* frames, uint8_t* arena) {
+    __shared__ uint32_t lds[kTile * kRow];
+    __shared__ unsigned hist[4][256];
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = nblocks(f);
+    const int b0 = blockIdx.x * kTile;
+    if (b0 >= nblk) return;
+    const int nb = min(kTile, nblk - b0);
+    for (int i = threadIdx.x; i < 1024; i += kTile) (&hist[0][0])[i] = 0;
+    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+    stage_tile(co, b0, nb, lds);
+    __syncthreads();
+    if (static_cast<int>(threadIdx.x) < nb) {
+        const int bi = b0 + threadIdx.x;
+        const uint32_t* row = lds + threadIdx.x * kRow;
+        const int tab = (bi % 6) < 4 ? 0 : 1;
+        atomicAdd(&hist[tab][nbits16(coef_at(row, 0) - prev_dc(co, lds, b0, bi))], 1u);
+        uint64_t m = ac_mask(row);
+        int prev = 0;
+        while (m) {
+            const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
+            m &= m - 1;
+            int run = i - prev - 1;
+            prev = i;
+            if (run >= 16) atomicAdd(&hist[2 + tab][0xF0], static_cast<unsigned>(run >> 4));
+            atomicAdd(&hist[2 + tab][((run & 15) << 4) | nbits16(coef_at(row, i))], 1u);
+        }
+        if (prev < 63) atomicAdd(&hist[2 + tab][0], 1u);
+    }
+    __syncthreads();
+    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+    for (int i = threadIdx.x; i < 1024; i += kTile) {
+        const unsigned v = (&hist[0][0])[i];
+        if (v) atomicAdd(&js->hist[i >> 8][i & 255], v);
+    }
+}
+
+// ---------------------------------------------------------------- K5a
+struct HuffLds {
+    int pv[260], pp[260];     // leaves (symbol, count), sorted by AV_QSORT
+    int P[2][520];            // item probabilities of the previous / current list
+    uint16_t cum[16][520];    // cum[t][m] = leaves among the first m items of list t
+    int nlist[17];
+    int nb[260];              // code length per symbol
+    int hc[256], hl[256];     // (symbol, length) pairs
+    int stk[64][2];
+};
+
+// libavutil/qsort.h AV_QSORT on index range [0, num) (unstable: tie order
+// must be FFmpeg's own, so this is a literal restatement, run by one lane).
+template <typename Cmp, typename Swp>
+DEVI void av_qsort_dev(int num, Cmp cmp, Swp swp, int (*stk)[2]) {
+    if (num <= 0) return;
+    int sp = 1;
+    stk[0][0] = 0;
+    stk[0][1] = num - 1;
+    while (sp) {
+        --sp;
+        int start = stk[sp][0], end = stk[sp][1];
+        while (start < end) {
+            if (start < end - 1) {
+                int checksort = 0;
+                int right = end - 2, left = start + 1, mid = start + ((end - start) >> 1);
+                if (cmp(start, end) > 0) {
+                    if (cmp(end, mid) > 0) swp(start, mid);
+                    else swp(start, end);
+                } else {
+                    if (cmp(start, mid) > 0) swp(start, mid);
+                    else checksort = 1;
+                }
+                if (cmp(mid, end) > 0) {
+                    swp(mid, end);
+                    checksort = 0;
+                }
+                if (start == end - 2) break;
+                swp(end - 1, mid);
+                while (left <= right) {
+                    while (left <= right && cmp(left, end - 1) < 0) left++;
+                    while (left <= right && cmp(right, end - 1) > 0) right--;
+                    if (left <= right) {
+                        swp(left, right);
+                        left++;
+                        right--;
+                    }
+                }
+                swp(end - 1, left);
+                if (checksort && (mid == left - 1 || mid == left)) {
+                    mid = start;
+                    while (mid < end && cmp(mid, mid + 1) <= 0) mid++;
+                    if (mid == end) break;
+                }
+                if (end - left < left - start) {
+                    stk[sp][0] = start;
+                    stk[sp][1] = right;
+                    sp++;
+                    start = left + 1;
+                } else {
+                    stk[sp][0] = left + 1;
+                    stk[sp][1] = end;
+                    sp++;
+                    end = right;
+                }
+            } else {
+                if (cmp(start, end) > 0) swp(start, end);
+                break;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, uint8_t* arena) {
+    __shared__ HuffLds s;
+    const h2j_frame& f = frames[blockIdx.y];
+    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+    const int t = blockIdx.x;
+    if (threadIdx.x != 0) return;  // serial by construction (AV_QSORT tie order)
+    int nval = 0;
+    for (int i = 0; i < 256; i++) {
+        const unsigned c = js->hist[t][i];
+        if (c) {
+            s.pv[nval] = i;
+            s.pp[nval] = static_cast<int>(c);
+            nval++;
+        }
+    }
+    s.pv[nval] = 256;
+    s.pp[nval] = 0;
+    const int size = nval + 1;
+    av_qsort_dev(
+        size, [&](int a, int b) { return s.pp[a] - s.pp[b]; },
+        [&](int a, int b) {
+            int x = s.pv[a]; s.pv[a] = s.pv[b]; s.pv[b] = x;
+            x = s.pp[a]; s.pp[a] = s.pp[b]; s.pp[b] = x;
+        },
+        s.stk);
+    // package-merge, 16 levels + the final pairing round (i not reset)
+    int np = 0, cur = 0, i = 0;
+    for (int lvl = 0; lvl <= 16; lvl++) {
+        int* Pc = s.P[cur];
+        const int* Pp = s.P[cur ^ 1];
+        int j = 0, n = 0, leaves = 0;
+        if (lvl < 16) {
+            i = 0;
+            s.cum[lvl][0] = 0;
+        }
+        while (i < size || j + 1 < np) {
+            if (i < size && (j + 1 >= np || s.pp[i] < Pp[j] + Pp[j + 1])) {
+                Pc[n] = s.pp[i];
+                i++;
+                leaves++;
+            } else {
+                Pc[n] = Pp[j] + Pp[j + 1];
+                j += 2;
+            }
+            n++;
+            if (lvl < 16) s.cum[lvl][n] = static_cast<uint16_t>(leaves);
+        }
+        s.nlist[lvl] = n;
+        np = n;
+        cur ^= 1;
+    }
+    for (int k = 0; k < 257; k++) s.nb[k] = 0;
+    {
+        const int mn = size - 1 < s.nlist[16] ? size - 1 : s.nlist[16];
+        int m = 2 * mn;
+        for (int lvl = 15; lvl >= 0 && m > 0; lvl--) {
+            const int lv = s.cum[lvl][m];
+            for (int k = 0; k < lv; k++) s.nb[s.pv[k]]++;
+            m = 2 * (m - lv);
+        }
+    }
+    int nd = 0;
+    for (int k = 0; k < 256; k++)
+        if (s.nb[k] > 0) {
+            s.hc[nd] = k;
+            s.hl[nd] = s.nb[k];
+            nd++;
+        }
+    av_qsort_dev(
+        nval, [&](int a, int b) { return s.hl[a] - s.hl[b]; },
+        [&](int a, int b) {
+            int x = s.hc[a]; s.hc[a] = s.hc[b]; s.hc[b] = x;
+            x = s.hl[a]; s.hl[a] = s.hl[b]; s.hl[b] = x;
+        },
+        s.stk);
+    for (int k = 0; k < 20; k++) js->bits[t][k] = 0;
+    for (int k = 0; k < 256; k++) {
+        js->len[t][k] = 0;
+        js->code[t][k] = 0;
+    }
+    for (int k = 0; k < nval; k++) {
+        js->val[t][k] = static_cast<uint8_t>(s.hc[k]);
+        js->bits[t][s.hl[k]]++;
+    }
+    js->nval[t] = static_cast<uint32_t>(nval);
+    int c = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+        for (int q = 0; q < js->bits[t][l]; q++, k++) {
+            js->code[t][s.hc[k]] = static_cast<uint16_t>(c++);
+            js->len[t][s.hc[k]] = static_cast<uint8_t>(l);
+        }
+        c <<= 1;
+    }
+}
+
+// ---------------------------------------------------------------- K5b / K5d shared
+struct CodeLds {
+    uint8_t len[4][256];
+    uint16_t code[4][256];
+};
+
+DEVI void load_codes(const h2j_jstat* js, CodeLds& c, bool with_codes) {
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        (&c.len[0][0])[i] = (&js->len[0][0])[i];
+        if (with_codes) (&c.code[0][0])[i] = (&js->code[0][0])[i];
+    }
+}
+
+DEVI uint32_t block_bits(const CodeLds& c, const uint32_t* row, int dc_diff, int tab) {
+    const int nd = nbits16(dc_diff);
+    uint32_t bits = c.len[tab][nd] + nd;
+    uint64_t m = ac_mask(row);
+    int prev = 0;
+    while (m) {
+        const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
+        m &= m - 1;
+        const int run = i - prev - 1;
+        prev = i;
+        const int n = nbits16(coef_at(row, i));
+        bits += (run >> 4) * c.len[2 + tab][0xF0] + c.len[2 + tab][((run & 15) << 4) | n] + n;
+    }
+    if (prev < 63) bits += c.len[2 + tab][0];
+    return bits;
+}
+
+// 256-thread workgroup exclusive scan (4 waves of 64)
+DEVI uint32_t wg_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+    for (int k = 0; k < kTile / 64; k++) {
+        if (k < w) base += sh[k];
+        total += sh[k];
+    }
+    __syncthreads();
+    return base + x - v;
+}
+
+// ---------------------------------------------------------------- K5b
+__global__ void __launch_bounds__(kTile) h2j_k5b_tile_bits(const h2j_frame* frames, uint8_t* arena,
+                                                           uint32_t* tile_bits, int max_tiles) {
+    __shared__ uint32_t lds[kTile * kRow];
+    __shared__ CodeLds cl;
+    __shared__ uint32_t sh[kTile / 64];
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = nblocks(f);
+    const int b0 = blockIdx.x * kTile;
+    if (b0 >= nblk) return;
+    const int nb = min(kTile, nblk - b0);
+    const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
+    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+    load_codes(js, cl, false);
+    stage_tile(co, b0, nb, lds);
+    __syncthreads();
+    uint32_t bits = 0;
+    if (static_cast<int>(threadIdx.x) < nb) {
+        const int bi = b0 + threadIdx.x;
+        const uint32_t* row = lds + threadIdx.x * kRow;
+        bits = block_bits(cl, row, coef_at(row, 0) - prev_dc(co, lds, b0, bi), (bi % 6) < 4 ? 0 : 1);
+    }
+    uint32_t total;
+    wg_excl_scan(bits, sh, total);
+    if (threadIdx.x == 0) tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x] = total;
+}
+
+// ---------------------------------------------------------------- K5c
+// grid (nframes): exclusive scan of the frame's tile bit counts in place.
+__global__ void __launch_bounds__(kTile) h2j_k5c_scan_tiles(const h2j_frame* frames, uint8_t* arena,
+                                                            uint32_t* tile_bits, int max_tiles) {
+    __shared__ uint32_t sh[kTile / 64];
+    const h2j_frame& f = frames[blockIdx.x];
+    const int ntiles = (nblocks(f) + kTile - 1) / kTile;
+    uint32_t* tb = tile_bits + static_cast<size_t>(blockIdx.x) * max_tiles;
+    uint32_t carry = 0;
+    for (int t0 = 0; t0 < ntiles; t0 += kTile) {
+        const int t = t0 + threadIdx.x;
+        const uint32_t v = t < ntiles ? tb[t] : 0;
+        uint32_t total;
+        const uint32_t ex = wg_excl_scan(v, sh, total);
+        if (t < ntiles) tb[t] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) {
+        h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+        js->nbits = carry;
+        js->nbytes = (carry + 7) >> 3;
+    }
+}
+
+// one workgroup: segment offsets of all frames (16-byte aligned) + pool total
+__global__ void __launch_bounds__(kTile) h2j_k5c_scan_frames(const h2j_frame* frames, int nframes, uint8_t* arena,
+                                                             uint64_t seg_cap, uint64_t* seg_total) {
+    __shared__ uint32_t sh[kTile / 64];
+    uint64_t carry = 0;
+    for (int k0 = 0; k0 < nframes; k0 += kTile) {
+        const int k = k0 + threadIdx.x;
+        h2j_jstat* js = k < nframes ? reinterpret_cast<h2j_jstat*>(arena + frames[k].jstat) : nullptr;
+        // sizes in 16-byte units keep the 32-bit scan exact for any batch
+        const uint32_t v = js ? (js->nbytes + 15) >> 4 : 0;
+        uint32_t total;
+        const uint32_t ex = wg_excl_scan(v, sh, total);
+        if (js) {
+            const uint64_t off = (carry + ex) << 4;
+            js->seg_off = off + (static_cast<uint64_t>(v) << 4) <= seg_cap ? off : ~0ull;
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) *seg_total = carry << 4 <= seg_cap ? carry << 4 : seg_cap;
+}
+
+// ---------------------------------------------------------------- K5z
+__global__ void __launch_bounds__(256) h2j_k5z_zero(uint8_t* seg, const uint64_t* seg_total) {
+    const uint64_t n = *seg_total >> 4;
+    uint4* p = reinterpret_cast<uint4*>(seg);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) p[i] = z;
+}
+
+// ---------------------------------------------------------------- K5d
+struct BitSink {
+    uint32_t* out;
+    uint32_t word;
+    uint64_t acc;
+    int nacc;
+    bool first;
+
+    DEVI void store(uint32_t w, bool atomic) {
+        const uint32_t be = __builtin_bswap32(w);
+        if (atomic) atomicOr(out + word, be);
+        else out[word] = be;
+        word++;
+    }
+    DEVI void put(uint32_t v, int n) {
+        acc = (acc << n) | v;
+        nacc += n;
+        if (nacc >= 32) {
+            nacc -= 32;
+            store(static_cast<uint32_t>(acc >> nacc), first);
+            first = false;
+        }
+    }
+    DEVI void finish() {
+        if (nacc > 0) store(static_cast<uint32_t>(acc << (32 - nacc)), true);
+    }
+};
+
+__global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, uint8_t* arena,
+                                                      const uint32_t* tile_bits, int max_tiles, uint8_t* seg) {
+    __shared__ uint32_t lds[kTile * kRow];
+    __shared__ CodeLds cl;
+    __shared__ uint32_t sh[kTile / 64];
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = nblocks(f);
+    const int b0 = blockIdx.x * kTile;
+    if (b0 >= nblk) return;
+    const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
+    if (js->seg_off == ~0ull) return;  // pool overflow: host reports the frame as failed
+    const int nb = min(kTile, nblk - b0);
+    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+    load_codes(js, cl, true);
+    stage_tile(co, b0, nb, lds);
+    __syncthreads();
+    const bool mine = static_cast<int>(threadIdx.x) < nb;
+    const int bi = b0 + threadIdx.x;
+    const uint32_t* row = lds + threadIdx.x * kRow;
+    const int tab = (bi % 6) < 4 ? 0 : 1;
+    int diff = 0;
+    uint32_t bits = 0;
+    if (mine) {
+        diff = coef_at(row, 0) - prev_dc(co, lds, b0, bi);
+        bits = block_bits(cl, row, diff, tab);
+    }
+    uint32_t total;
+    const uint32_t ex = wg_excl_scan(bits, sh, total);
+    if (!mine) return;
+    const uint32_t bit0 = tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x] + ex;
+    BitSink s;
+    s.out = reinterpret_cast<uint32_t*>(seg + js->seg_off);
+    s.word = bit0 >> 5;
+    s.acc = 0;
+    s.nacc = bit0 & 31;
+    s.first = true;
+    const int nd = nbits16(diff);
+    s.put(cl.code[tab][nd], cl.len[tab][nd]);
+    if (nd) s.put(static_cast<uint32_t>(diff < 0 ? diff - 1 : diff) & ((1u << nd) - 1u), nd);
+    const uint8_t* al = cl.len[2 + tab];
+    const uint16_t* ac = cl.code[2 + tab];
+    uint64_t m = ac_mask(row);
+    int prev = 0;
+    while (m) {
+        const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
+        m &= m - 1;
+        int run = i - prev - 1;
+        prev = i;
+        for (; run >= 16; run -= 16) s.put(ac[0xF0], al[0xF0]);
+        const int v = coef_at(row, i);
+        const int n = nbits16(v);
+        const int sym = (run << 4) | n;
+        s.put(ac[sym], al[sym]);
+        s.put(static_cast<uint32_t>(v < 0 ? v - 1 : v) & ((1u << n) - 1u), n);
+    }
+    if (prev < 63) s.put(ac[0], al[0]);
+    if (bi == nblk - 1) {
+        const int pad = (8 - static_cast<int>((bit0 + bits) & 7)) & 7;  // FFmpeg: pad with 1-bits
+        if (pad) s.put((1u << pad) - 1u, pad);
+    }
+    s.finish();
+}
+
+}  // namespace
+
+namespace h2jgpu {  // defined in h2j_kernels.hip: one error slot for the whole C ABI
+extern thread_local char g_err[256];
+int check(hipError_t e, const char* what);
+}  // namespace h2jgpu
+using h2jgpu::check;
+using h2jgpu::g_err;
+
+extern "C" {
+
+int h2j_gpu_histogram(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int tiles = (b->max_mcu * 6 + kTile - 1) / kTile;
+    hipLaunchKernelGGL(h2j_k4d_histogram, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena);
+    return check(hipGetLastError(), "h2j_k4d_histogram");
+}
+
+int h2j_gpu_entropy(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    if (!b->seg || !b->tile_bits || !b->seg_total) {
+        snprintf(g_err, sizeof(g_err), "h2j_gpu_entropy: segment pool / scratch not set");
+        return -1;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int tiles = (b->max_mcu * 6 + kTile - 1) / kTile;
+    hipLaunchKernelGGL(h2j_k5a_tables, dim3(4, b->nframes), dim3(64), 0, s, b->frames, b->arena);
+    int r = check(hipGetLastError(), "h2j_k5a_tables");
+    if (r) return r;
+    hipLaunchKernelGGL(h2j_k5b_tile_bits, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena,
+                       b->tile_bits, tiles);
+    if ((r = check(hipGetLastError(), "h2j_k5b_tile_bits"))) return r;
+    hipLaunchKernelGGL(h2j_k5c_scan_tiles, dim3(b->nframes), dim3(kTile), 0, s, b->frames, b->arena, b->tile_bits,
+                       tiles);
+    if ((r = check(hipGetLastError(), "h2j_k5c_scan_tiles"))) return r;
+    hipLaunchKernelGGL(h2j_k5c_scan_frames, dim3(1), dim3(kTile), 0, s, b->frames, b->nframes, b->arena, b->seg_cap,
+                       b->seg_total);
+    if ((r = check(hipGetLastError(), "h2j_k5c_scan_frames"))) return r;
+    hipLaunchKernelGGL(h2j_k5z_zero, dim3(1024), dim3(256), 0, s, b->seg, b->seg_total);
+    if ((r = check(hipGetLastError(), "h2j_k5z_zero"))) return r;
+    hipLaunchKernelGGL(h2j_k5d_emit, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena, b->tile_bits,
+                       tiles, b->seg);
+    return check(hipGetLastError(), "h2j_k5d_emit");
+}
+
+}  // extern "C"

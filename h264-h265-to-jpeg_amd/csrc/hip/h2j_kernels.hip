@@ -1323,48 +1323,10 @@ __global__ void __launch_bounds__(256) h2j_k4c_fdct_quant(const h2j_frame* frame
     else jpeg_block<uint16_t>(f, arena, bi);
 }
 
-DEVI int nbits16(int v) {
-    const unsigned a = static_cast<unsigned>(v < 0 ? -v : v);
-    return a ? 32 - __clz(a) : 0;
-}
 
-__global__ void __launch_bounds__(256) h2j_k4d_histogram(const h2j_frame* frames, uint8_t* arena) {
-    __shared__ unsigned hist[4][256];
-    for (int i = threadIdx.x; i < 1024; i += 256) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    const h2j_frame& f = frames[blockIdx.y];
-    const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
-    const int bi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (bi < nblk) {
-        const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
-        const int16_t* z = co + static_cast<size_t>(bi) * 64;
-        const int mcu = bi / 6, b = bi % 6;
-        int prev;
-        if (b < 4) prev = b > 0 ? co[static_cast<size_t>(bi - 1) * 64] : (mcu > 0 ? co[static_cast<size_t>(bi - 3) * 64] : 128);
-        else prev = mcu > 0 ? co[static_cast<size_t>(bi - 6) * 64] : 128;
-        const int tab = b < 4 ? 0 : 1;
-        atomicAdd(&hist[tab][nbits16(z[0] - prev)], 1u);
-        int last = 0;
-        for (int i = 63; i >= 1; i--)
-            if (z[i]) { last = i; break; }
-        int run = 0;
-        for (int i = 1; i <= last; i++) {
-            const int v = z[i];
-            if (!v) { run++; continue; }
-            while (run >= 16) { atomicAdd(&hist[2 + tab][0xF0], 1u); run -= 16; }
-            atomicAdd(&hist[2 + tab][(run << 4) | nbits16(v)], 1u);
-            run = 0;
-        }
-        if (last < 63) atomicAdd(&hist[2 + tab][0], 1u);
-    }
-    __syncthreads();
-    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        const unsigned v = (&hist[0][0])[i];
-        if (v) atomicAdd(&js->hist[i >> 8][i & 255], v);
-    }
-}
+}  // namespace
 
+namespace h2jgpu {
 thread_local char g_err[256] = {0};
 
 int check(hipError_t e, const char* what) {
@@ -1372,8 +1334,9 @@ int check(hipError_t e, const char* what) {
     snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
     return -static_cast<int>(e) - 1000;
 }
-
-}  // namespace
+}  // namespace h2jgpu
+using h2jgpu::check;
+using h2jgpu::g_err;
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -1476,8 +1439,7 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     hipLaunchKernelGGL(h2j_k4c_fdct_quant, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
     r = check(hipGetLastError(), "h2j_k4c_fdct_quant");
     if (r) return r;
-    hipLaunchKernelGGL(h2j_k4d_histogram, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
-    return check(hipGetLastError(), "h2j_k4d_histogram");
+    return h2j_gpu_histogram(b, stream);
 }
 
 }  // extern "C"

@@ -1,14 +1,17 @@
-// Batch engine: host entropy threads -> HBM job records -> HIP pixel
-// pipeline -> host Huffman.  One engine per process per GPU; the IDecoder
-// facade and the C ABI (include/h2j.h) both run on it.
+// Batch engine: host entropy threads -> HBM job records -> HIP pixel and
+// JPEG pipeline -> host container assembly.  One engine per process per GPU;
+// the IDecoder facade and the C ABI (include/h2j.h) both run on it.
 //
-// Per batch:
+// A batch is cut into chunks that flow through two slots (HIP stream +
+// device/pinned buffers each), so the host parses chunk c+1 and assembles
+// chunk c-1 while the GPU runs chunk c.  Per chunk:
 //   1. parse      — pool threads run the H.264/H.265 entropy decoders
 //                   (hevc_parser.cpp / h264_parser.cpp) into FrameJobs
 //   2. pack + H2D — job records packed into one pinned staging buffer, one copy
-//   3. GPU        — K1 recon, K2 deblock, K3 SAO, K4 JPEG (h2j_kernels.hip)
-//   4. D2H        — quantised coefficients + per-frame statistics
-//   5. huffman    — pool threads assemble the JPEG files (jpeg_writer.cpp)
+//   3. GPU        — K1 recon, K2 deblock, K3 SAO, K4 JPEG forward path,
+//                   K5 Huffman tables + entropy-coded payload
+//   4. D2H        — per-frame tables (h2j_jstat) and the packed payloads only
+//   5. assemble   — pool threads write the JPEG containers (jpeg_writer.cpp)
 // This is what the reference does per call inside FFmpeg between
 // avcodec_send_packet (/root/reference/src/Decoder.cpp:324) and
 // av_write_frame (/root/reference/src/Encoder.cpp:278).
@@ -17,6 +20,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -157,30 +161,51 @@ int parse_any(const uint8_t* d, size_t n, FrameJob& job) {
 
 }  // namespace
 
-struct Engine {
-    int device = 0;
+// One in-flight chunk: its stream, buffers and layout.
+struct Slot {
     void* stream = nullptr;
-    ThreadPool* pool = nullptr;
-    std::string err;
-    std::vector<FrameJob> jobs;
-    std::vector<int> live;  // indices of successfully parsed jobs
-    std::vector<h2j_frame> frames;
-    DevBuf d_in, d_arena;
-    HostBuf h_in, h_out;
     void* ev[8] = {nullptr};
-    double stats[11] = {0};
-    // layout of the last run
-    size_t zero_bytes = 0, jcoef_base = 0, jcoef_bytes = 0, jstat_base = 0;
+    DevBuf d_in, d_arena, d_seg, d_scratch;
+    HostBuf h_in, h_js, h_seg;
+    std::vector<h2j_frame> frames;
+    std::vector<int> live;  // job index of each frame of the chunk
     h2j_gpu_batch batch{};
+    size_t zero_bytes = 0, jcoef_base = 0, jcoef_bytes = 0, jstat_base = 0, jstat_stride = 0;
+    int stages = 0;
+    bool entropy = false, pending = false;
 
-    ~Engine() {
+    void release() {
         d_in.release();
         d_arena.release();
+        d_seg.release();
+        d_scratch.release();
         h_in.release();
-        h_out.release();
+        h_js.release();
+        h_seg.release();
         for (auto& e : ev)
             if (e) h2j_gpu_event_destroy(e);
         if (stream) h2j_gpu_stream_destroy(stream);
+        stream = nullptr;
+    }
+};
+
+enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
+       ST_ENTROPY, ST_N };
+
+// upper bound of one block's entropy-coded size (code lengths <= 16, values <= 16 bits)
+constexpr size_t kSegBytesPerBlock = 272;
+
+struct Engine {
+    int device = 0;
+    ThreadPool* pool = nullptr;
+    std::string err;
+    std::vector<FrameJob> jobs;
+    Slot slot[2];
+    double stats[ST_N] = {0};
+
+    ~Engine() {
+        slot[0].release();
+        slot[1].release();
         delete pool;
     }
 
@@ -189,19 +214,24 @@ struct Engine {
         return -1;
     }
 
-    // Upload + run the GPU stages on jobs[live]. stages: 1 recon, 2 +deblock,
-    // 3 +sao, 4 +jpeg
-    int run_gpu(int stages, bool fetch_jpeg);
+    // Lay out, pack and enqueue the GPU work of jobs[live] on slot s.
+    // stages: 1 recon, 2 +deblock, 3 +sao, 4 +jpeg forward path; entropy: +K5
+    int enqueue(Slot& s, int stages, bool entropy);
+    // Wait for slot s and copy its payloads down (entropy chunks).
+    int sync(Slot& s);
 };
 
-int Engine::run_gpu(int stages, bool fetch_jpeg) {
-    const int nf = static_cast<int>(live.size());
+int Engine::enqueue(Slot& s, int stages, bool entropy) {
+    const int nf = static_cast<int>(s.live.size());
+    s.stages = stages;
+    s.entropy = entropy;
+    s.pending = false;
     if (nf == 0) return 0;
-    frames.resize(nf);
-    size_t ntu = 0, ncoef = 0, nctb = 0, nslice = 0, nsl = 0;
+    s.frames.resize(nf);
+    size_t ntu = 0, ncoef = 0, nctb = 0, nslice = 0, nsl = 0, nblk = 0;
     int max_w = 0, max_h = 0, max_mcu = 0;
     for (int k = 0; k < nf; k++) {
-        const FrameJob& j = jobs[live[k]];
+        const FrameJob& j = jobs[s.live[k]];
         h2j_frame f = j.hdr;
         f.tu = static_cast<uint32_t>(ntu);
         f.ntu = static_cast<uint32_t>(j.tus.size());
@@ -215,27 +245,30 @@ int Engine::run_gpu(int stages, bool fetch_jpeg) {
         nctb += j.ctbs.size();
         nslice += j.slices.size();
         nsl += j.sl.size();
-        frames[k] = f;
+        s.frames[k] = f;
         max_w = std::max(max_w, f.width);
         max_h = std::max(max_h, f.height);
-        max_mcu = std::max(max_mcu, ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4));
+        const int mcu = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4);
+        max_mcu = std::max(max_mcu, mcu);
+        nblk += static_cast<size_t>(mcu) * 6;
     }
     // arena layout: [zeroed: maps + jstat][pic][pic2][jcoef]
     size_t off = 0;
     for (int k = 0; k < nf; k++) {
-        h2j_frame& f = frames[k];
+        h2j_frame& f = s.frames[k];
         f.maps = off;
         off = align_up(off + static_cast<size_t>(f.mw) * f.mh * 2, 256);
     }
-    jstat_base = off;
+    s.jstat_base = off;
+    s.jstat_stride = align_up(sizeof(h2j_jstat), 256);
     for (int k = 0; k < nf; k++) {
-        frames[k].jstat = off;
-        off = align_up(off + sizeof(h2j_jstat), 256);
+        s.frames[k].jstat = off;
+        off += s.jstat_stride;
     }
-    zero_bytes = off;
+    s.zero_bytes = off;
     for (int pass = 0; pass < 2; pass++)
         for (int k = 0; k < nf; k++) {
-            h2j_frame& f = frames[k];
+            h2j_frame& f = s.frames[k];
             const size_t pel = f.bit_depth > 8 ? 2 : 1;
             const size_t ysz = static_cast<size_t>(f.width) * f.height, csz = ysz / 4;
             f.pic_stride[0] = f.width;
@@ -246,13 +279,13 @@ int Engine::run_gpu(int stages, bool fetch_jpeg) {
             if (pass == 0) f.pic = off; else f.pic2 = off;
             off = align_up(off + (ysz + 2 * csz) * pel, 256);
         }
-    jcoef_base = off;
+    s.jcoef_base = off;
     for (int k = 0; k < nf; k++) {
-        h2j_frame& f = frames[k];
+        h2j_frame& f = s.frames[k];
         f.jcoef = off;
         off = align_up(off + static_cast<size_t>(((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4)) * 6 * 64 * 2, 256);
     }
-    jcoef_bytes = off - jcoef_base;
+    s.jcoef_bytes = off - s.jcoef_base;
     const size_t arena_bytes = off;
     // input staging
     const size_t o_frames = 0;
@@ -262,82 +295,119 @@ int Engine::run_gpu(int stages, bool fetch_jpeg) {
     const size_t o_slices = align_up(o_ctbs + nctb * sizeof(h2j_ctb), 256);
     const size_t o_sl = align_up(o_slices + nslice * sizeof(h2j_slice), 256);
     const size_t in_bytes = align_up(o_sl + nsl + 16, 256);
-    if (!h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
-    if (!d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
-    if (!d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
-    std::memcpy(h_in.p + o_frames, frames.data(), nf * sizeof(h2j_frame));
-    // parallel pack
+    if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
+    if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
+    if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
+    const int tiles = (max_mcu * 6 + 255) / 256;
+    const size_t seg_cap = nblk * kSegBytesPerBlock + 16 * static_cast<size_t>(nf);
+    if (entropy) {
+        if (!s.d_seg.ensure(seg_cap)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
+        if (!s.d_scratch.ensure(static_cast<size_t>(nf) * tiles * 4 + 256))
+            return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
+        if (!s.h_js.ensure(static_cast<size_t>(nf) * s.jstat_stride + 256)) return fail("pinned host allocation failed");
+    }
+    std::memcpy(s.h_in.p + o_frames, s.frames.data(), nf * sizeof(h2j_frame));
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
         for (int k = 0; k < nf; k++) {
-            const FrameJob& j = jobs[live[k]];
+            const FrameJob& j = jobs[s.live[k]];
             bt[k] = a; bc[k] = b; bk[k] = c; bs[k] = d; bl[k] = e;
             a += j.tus.size(); b += j.coefs.size(); c += j.ctbs.size(); d += j.slices.size(); e += j.sl.size();
         }
     }
+    uint8_t* hin = s.h_in.p;
     pool->parallel_for(nf, [&](int k) {
-        const FrameJob& j = jobs[live[k]];
-        if (!j.tus.empty()) std::memcpy(h_in.p + o_tus + bt[k] * sizeof(h2j_tu), j.tus.data(), j.tus.size() * sizeof(h2j_tu));
-        if (!j.coefs.empty()) std::memcpy(h_in.p + o_coefs + bc[k] * sizeof(h2j_coef), j.coefs.data(), j.coefs.size() * sizeof(h2j_coef));
-        if (!j.ctbs.empty()) std::memcpy(h_in.p + o_ctbs + bk[k] * sizeof(h2j_ctb), j.ctbs.data(), j.ctbs.size() * sizeof(h2j_ctb));
-        if (!j.slices.empty()) std::memcpy(h_in.p + o_slices + bs[k] * sizeof(h2j_slice), j.slices.data(), j.slices.size() * sizeof(h2j_slice));
-        if (!j.sl.empty()) std::memcpy(h_in.p + o_sl + bl[k], j.sl.data(), j.sl.size());
+        const FrameJob& j = jobs[s.live[k]];
+        if (!j.tus.empty()) std::memcpy(hin + o_tus + bt[k] * sizeof(h2j_tu), j.tus.data(), j.tus.size() * sizeof(h2j_tu));
+        if (!j.coefs.empty()) std::memcpy(hin + o_coefs + bc[k] * sizeof(h2j_coef), j.coefs.data(), j.coefs.size() * sizeof(h2j_coef));
+        if (!j.ctbs.empty()) std::memcpy(hin + o_ctbs + bk[k] * sizeof(h2j_ctb), j.ctbs.data(), j.ctbs.size() * sizeof(h2j_ctb));
+        if (!j.slices.empty()) std::memcpy(hin + o_slices + bs[k] * sizeof(h2j_slice), j.slices.data(), j.slices.size() * sizeof(h2j_slice));
+        if (!j.sl.empty()) std::memcpy(hin + o_sl + bl[k], j.sl.data(), j.sl.size());
     });
-    uint8_t* din = static_cast<uint8_t*>(d_in.p);
-    batch.nframes = nf;
-    batch.max_w = max_w;
-    batch.max_h = max_h;
-    batch.max_mcu = max_mcu;
-    batch.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
-    batch.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);
-    batch.coefs = reinterpret_cast<const h2j_coef*>(din + o_coefs);
-    batch.ctbs = reinterpret_cast<const h2j_ctb*>(din + o_ctbs);
-    batch.slices = reinterpret_cast<const h2j_slice*>(din + o_slices);
-    batch.sl = din + o_sl;
-    batch.arena = static_cast<uint8_t*>(d_arena.p);
+    uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
+    h2j_gpu_batch& b = s.batch;
+    b.nframes = nf;
+    b.max_w = max_w;
+    b.max_h = max_h;
+    b.max_mcu = max_mcu;
+    b.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
+    b.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);
+    b.coefs = reinterpret_cast<const h2j_coef*>(din + o_coefs);
+    b.ctbs = reinterpret_cast<const h2j_ctb*>(din + o_ctbs);
+    b.slices = reinterpret_cast<const h2j_slice*>(din + o_slices);
+    b.sl = din + o_sl;
+    b.arena = static_cast<uint8_t*>(s.d_arena.p);
+    b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
+    b.seg_cap = entropy ? seg_cap : 0;
+    b.seg_total = entropy ? static_cast<uint64_t*>(s.d_scratch.p) : nullptr;
+    b.tile_bits = entropy ? reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(s.d_scratch.p) + 256) : nullptr;
+    void* st = s.stream;
     int r = 0;
-    r |= h2j_gpu_event_record(ev[0], stream);
-    r |= h2j_gpu_memcpy_h2d(din, h_in.p, in_bytes, stream);
-    r |= h2j_gpu_memset(d_arena.p, 0, zero_bytes, stream);
-    r |= h2j_gpu_event_record(ev[1], stream);
+    r |= h2j_gpu_event_record(s.ev[0], st);
+    r |= h2j_gpu_memcpy_h2d(din, hin, in_bytes, st);
+    r |= h2j_gpu_memset(s.d_arena.p, 0, s.zero_bytes, st);
+    r |= h2j_gpu_event_record(s.ev[1], st);
     if (r) return fail(std::string("upload failed: ") + h2j_gpu_last_error());
-    if (h2j_gpu_recon(&batch, stream)) return fail(h2j_gpu_last_error());
-    h2j_gpu_event_record(ev[2], stream);
-    if (stages >= 2 && h2j_gpu_deblock(&batch, stream)) return fail(h2j_gpu_last_error());
-    h2j_gpu_event_record(ev[3], stream);
-    if (stages >= 3 && h2j_gpu_sao(&batch, stream)) return fail(h2j_gpu_last_error());
-    h2j_gpu_event_record(ev[4], stream);
-    if (stages >= 4 && h2j_gpu_jpeg(&batch, stream)) return fail(h2j_gpu_last_error());
-    h2j_gpu_event_record(ev[5], stream);
-    if (fetch_jpeg) {
-        const size_t out_bytes = jcoef_bytes + (zero_bytes - jstat_base);
-        if (!h_out.ensure(out_bytes)) return fail("pinned host allocation failed");
-        r |= h2j_gpu_memcpy_d2h(h_out.p, static_cast<uint8_t*>(d_arena.p) + jcoef_base, jcoef_bytes, stream);
-        r |= h2j_gpu_memcpy_d2h(h_out.p + jcoef_bytes, static_cast<uint8_t*>(d_arena.p) + jstat_base,
-                                zero_bytes - jstat_base, stream);
+    if (h2j_gpu_recon(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[2], st);
+    if (stages >= 2 && h2j_gpu_deblock(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[3], st);
+    if (stages >= 3 && h2j_gpu_sao(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[4], st);
+    if (stages >= 4 && h2j_gpu_jpeg(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[5], st);
+    if (entropy && h2j_gpu_entropy(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[6], st);
+    if (entropy) {
+        r |= h2j_gpu_memcpy_d2h(s.h_js.p, s.d_scratch.p, 8, st);  // seg_total
+        r |= h2j_gpu_memcpy_d2h(s.h_js.p + 256, static_cast<uint8_t*>(s.d_arena.p) + s.jstat_base,
+                                static_cast<size_t>(nf) * s.jstat_stride, st);
+        if (r) return fail(std::string("download failed: ") + h2j_gpu_last_error());
     }
-    h2j_gpu_event_record(ev[6], stream);
-    if (r) return fail(std::string("download failed: ") + h2j_gpu_last_error());
-    if (h2j_gpu_stream_sync(stream)) return fail(std::string("GPU execution failed: ") + h2j_gpu_last_error());
-    stats[1] = h2j_gpu_event_elapsed_ms(ev[0], ev[1]);
-    stats[2] = h2j_gpu_event_elapsed_ms(ev[1], ev[2]);
-    stats[3] = h2j_gpu_event_elapsed_ms(ev[2], ev[3]);
-    stats[4] = h2j_gpu_event_elapsed_ms(ev[3], ev[4]);
-    stats[5] = h2j_gpu_event_elapsed_ms(ev[4], ev[5]);
-    stats[6] = h2j_gpu_event_elapsed_ms(ev[5], ev[6]);
+    s.pending = true;
     double bytes = 0;
     for (int k = 0; k < nf; k++) {
-        const double S = 1.5 * frames[k].out_w * frames[k].out_h;
-        bytes += S * (4.0 + (frames[k].bit_depth > 8 ? 2.0 : 1.0));
+        const double S = 1.5 * s.frames[k].out_w * s.frames[k].out_h;
+        bytes += S * (4.0 + (s.frames[k].bit_depth > 8 ? 2.0 : 1.0));
     }
-    stats[10] = bytes;
+    stats[ST_BYTES] += bytes;
     return 0;
+}
+
+int Engine::sync(Slot& s) {
+    if (!s.pending) return 0;
+    s.pending = false;
+    if (h2j_gpu_stream_sync(s.stream)) return fail(std::string("GPU execution failed: ") + h2j_gpu_last_error());
+    if (s.entropy) {
+        uint64_t total = 0;
+        std::memcpy(&total, s.h_js.p, 8);
+        if (!s.h_seg.ensure(total + 16)) return fail("pinned host allocation failed");
+        if (total && h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
+            return fail(std::string("download failed: ") + h2j_gpu_last_error());
+    }
+    if (h2j_gpu_event_record(s.ev[7], s.stream) || h2j_gpu_stream_sync(s.stream))
+        return fail(std::string("download failed: ") + h2j_gpu_last_error());
+    stats[ST_H2D] += h2j_gpu_event_elapsed_ms(s.ev[0], s.ev[1]);
+    stats[ST_RECON] += h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[2]);
+    stats[ST_DEBLOCK] += h2j_gpu_event_elapsed_ms(s.ev[2], s.ev[3]);
+    stats[ST_SAO] += h2j_gpu_event_elapsed_ms(s.ev[3], s.ev[4]);
+    stats[ST_JPEG] += h2j_gpu_event_elapsed_ms(s.ev[4], s.ev[5]);
+    stats[ST_ENTROPY] += h2j_gpu_event_elapsed_ms(s.ev[5], s.ev[6]);
+    stats[ST_D2H] += h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[7]);
+    return 0;
+}
+
+int chunk_frames(int n) {
+    const char* e = std::getenv("H2J_CHUNK");
+    if (e && std::atoi(e) > 0) return std::atoi(e);
+    return n;
 }
 
 }  // namespace h2j
 
 using h2j::Engine;
+using h2j::Slot;
 
 struct h2j_engine {
     Engine e;
@@ -345,7 +415,7 @@ struct h2j_engine {
 
 extern "C" {
 
-const char* h2j_version(void) { return "h2j-mi355x 0.1 (gfx950, HIP)"; }
+const char* h2j_version(void) { return "h2j-mi355x 0.2 (gfx950, HIP)"; }
 
 h2j_engine* h2j_engine_create(int device, int host_threads) {
     if (h2j_gpu_device_count() <= 0) return nullptr;
@@ -353,12 +423,14 @@ h2j_engine* h2j_engine_create(int device, int host_threads) {
     h2j_engine* w = new h2j_engine();
     Engine& e = w->e;
     e.device = device;
-    e.stream = h2j_gpu_stream_create();
-    if (!e.stream) {
-        delete w;
-        return nullptr;
+    for (auto& s : e.slot) {
+        s.stream = h2j_gpu_stream_create();
+        if (!s.stream) {
+            delete w;
+            return nullptr;
+        }
+        for (auto& ev : s.ev) ev = h2j_gpu_event_create();
     }
-    for (auto& ev : e.ev) ev = h2j_gpu_event_create();
     int t = host_threads;
     if (t <= 0) {
         t = static_cast<int>(std::thread::hardware_concurrency());
@@ -379,49 +451,80 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     Engine& e = w->e;
     if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
     const double t0 = h2j::now_ms();
+    for (auto& v : e.stats) v = 0;
     if (static_cast<int>(e.jobs.size()) < n) e.jobs.resize(n);
-    e.pool->parallel_for(n, [&](int i) { h2j::parse_any(data[i], sizes[i], e.jobs[i]); });
-    const double t1 = h2j::now_ms();
-    e.live.clear();
     for (int i = 0; i < n; i++) {
-        status[i] = e.jobs[i].error;
         out_len[i] = 0;
         out_off[i] = 0;
-        if (e.jobs[i].error == 0) e.live.push_back(i);
+        status[i] = 0;
     }
-    if (e.run_gpu(4, true)) return -2;
-    const double t2 = h2j::now_ms();
-    // Huffman + assembly per frame into thread-local vectors, then copy out
-    const int nf = static_cast<int>(e.live.size());
-    std::vector<std::vector<uint8_t>> jp(nf);
-    const uint8_t* jc = e.h_out.p;
-    const uint8_t* js = e.h_out.p + e.jcoef_bytes;
-    e.pool->parallel_for(nf, [&](int k) {
-        const h2j_frame& f = e.frames[k];
-        const int16_t* co = reinterpret_cast<const int16_t*>(jc + (f.jcoef - e.jcoef_base));
-        const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + (f.jstat - e.jstat_base));
-        h2j::jpeg_assemble(co, f.out_w, f.out_h, *st, h2j::kLavcIdent, jp[k]);
-    });
+    const int chunk = std::max(1, h2j::chunk_frames(n));
+    const int nchunks = (n + chunk - 1) / chunk;
     size_t pos = 0;
     int rc = 0;
-    for (int k = 0; k < nf; k++) {
-        const int i = e.live[k];
-        if (pos + jp[k].size() > out_cap) {
-            status[i] = -50;
-            rc = -3;
-            continue;
+    // assemble the JPEGs of a finished slot into out (in frame order)
+    auto assemble = [&](Slot& s) -> int {
+        if (e.sync(s)) return -2;
+        const double ta = h2j::now_ms();
+        const int nf = static_cast<int>(s.live.size());
+        const uint8_t* js = s.h_js.p + 256;
+        std::vector<size_t> sz(nf);
+        e.pool->parallel_for(nf, [&](int k) {
+            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            sz[k] = st->seg_off == ~0ull ? 0 : h2j::jpeg_container_size(*st, s.h_seg.p + st->seg_off, h2j::kLavcIdent);
+        });
+        std::vector<size_t> at(nf);
+        for (int k = 0; k < nf; k++) {
+            const int i = s.live[k];
+            if (!sz[k]) {
+                status[i] = -51;  // payload pool overflow
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
+            if (pos + sz[k] > out_cap) {
+                status[i] = -50;
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
+            at[k] = pos;
+            out_off[i] = pos;
+            out_len[i] = sz[k];
+            pos += sz[k];
         }
-        std::memcpy(out + pos, jp[k].data(), jp[k].size());
-        out_off[i] = pos;
-        out_len[i] = jp[k].size();
-        pos += jp[k].size();
+        e.pool->parallel_for(nf, [&](int k) {
+            if (at[k] == ~static_cast<size_t>(0)) return;
+            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            const h2j_frame& f = s.frames[k];
+            h2j::jpeg_write_container(*st, s.h_seg.p + st->seg_off, f.out_w, f.out_h, h2j::kLavcIdent, out + at[k]);
+        });
+        e.stats[h2j::ST_ASSEMBLE] += h2j::now_ms() - ta;
+        e.stats[h2j::ST_FRAMES] += nf;
+        return 0;
+    };
+    for (int c = 0; c < nchunks; c++) {
+        const int i0 = c * chunk, i1 = std::min(n, i0 + chunk);
+        const double tp = h2j::now_ms();
+        e.pool->parallel_for(i1 - i0, [&](int k) { h2j::parse_any(data[i0 + k], sizes[i0 + k], e.jobs[i0 + k]); });
+        e.stats[h2j::ST_PARSE] += h2j::now_ms() - tp;
+        Slot& s = e.slot[c & 1];
+        if (s.pending && assemble(s)) return -2;
+        s.live.clear();
+        for (int i = i0; i < i1; i++) {
+            status[i] = e.jobs[i].error;
+            if (e.jobs[i].error == 0) s.live.push_back(i);
+        }
+        if (e.enqueue(s, 4, true)) return -2;
+        Slot& prev = e.slot[(c + 1) & 1];
+        if (c > 0 && prev.pending && assemble(prev)) return -2;
     }
-    const double t3 = h2j::now_ms();
-    e.stats[0] = t1 - t0;
-    e.stats[7] = t3 - t2;
-    e.stats[8] = t3 - t0;
-    e.stats[9] = nf;
-    if (rc) e.err = "output buffer too small";
+    for (int c = 0; c < 2; c++) {
+        Slot& s = e.slot[(nchunks + c) & 1];
+        if (s.pending && assemble(s)) return -2;
+    }
+    e.stats[h2j::ST_TOTAL] = h2j::now_ms() - t0;
+    if (rc) e.err = "output buffer too small or payload pool overflow";
     return rc;
 }
 
@@ -431,7 +534,7 @@ static int single_job(h2j_engine* w, const uint8_t* data, size_t size) {
     if (e.jobs.empty()) e.jobs.resize(1);
     int r = h2j::parse_any(data, size, e.jobs[0]);
     if (r) return e.fail("parse failed: " + e.jobs[0].message);
-    e.live.assign(1, 0);
+    e.slot[0].live.assign(1, 0);
     return 0;
 }
 
@@ -441,8 +544,9 @@ int h2j_engine_decode(h2j_engine* w, const uint8_t* data, size_t size, int stage
     Engine& e = w->e;
     if (single_job(w, data, size)) return -2;
     const int stages = stage == 1 ? 1 : (stage == 2 ? 2 : 3);
-    if (e.run_gpu(stages, false)) return -3;
-    const h2j_frame& f = e.frames[0];
+    Slot& s = e.slot[0];
+    if (e.enqueue(s, stages, false) || e.sync(s)) return -3;
+    const h2j_frame& f = s.frames[0];
     const int w_ = f.out_w, h_ = f.out_h;
     const size_t need = static_cast<size_t>(w_) * h_ * 3 / 2;
     info[0] = w_;
@@ -453,8 +557,8 @@ int h2j_engine_decode(h2j_engine* w, const uint8_t* data, size_t size, int stage
     const uint64_t base = stage == 0 ? f.pic2 : f.pic;
     const size_t pic_bytes = static_cast<size_t>(f.width) * f.height * 3 / 2 * pel;
     std::vector<uint8_t> tmp(pic_bytes);
-    if (h2j_gpu_memcpy_d2h(tmp.data(), static_cast<uint8_t*>(e.d_arena.p) + base, pic_bytes, e.stream) ||
-        h2j_gpu_stream_sync(e.stream))
+    if (h2j_gpu_memcpy_d2h(tmp.data(), static_cast<uint8_t*>(s.d_arena.p) + base, pic_bytes, s.stream) ||
+        h2j_gpu_stream_sync(s.stream))
         return e.fail(h2j_gpu_last_error());
     size_t o = 0;
     for (int c = 0; c < 3; c++) {
@@ -474,22 +578,27 @@ int h2j_engine_jpeg_coeffs(h2j_engine* w, const uint8_t* data, size_t size, int1
     if (!w) return -1;
     Engine& e = w->e;
     if (single_job(w, data, size)) return -2;
-    if (e.run_gpu(4, true)) return -3;
-    const h2j_frame& f = e.frames[0];
+    Slot& s = e.slot[0];
+    if (e.enqueue(s, 4, false) || e.sync(s)) return -3;
+    const h2j_frame& f = s.frames[0];
     const int nmcu = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4);
-    const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(e.h_out.p + e.jcoef_bytes + (f.jstat - e.jstat_base));
+    h2j_jstat st;
+    if (cap < static_cast<size_t>(nmcu) * 384) return e.fail("output buffer too small");
+    if (h2j_gpu_memcpy_d2h(&st, static_cast<uint8_t*>(s.d_arena.p) + f.jstat, sizeof(st), s.stream) ||
+        h2j_gpu_memcpy_d2h(out, static_cast<uint8_t*>(s.d_arena.p) + f.jcoef, static_cast<size_t>(nmcu) * 384 * 2,
+                           s.stream) ||
+        h2j_gpu_stream_sync(s.stream))
+        return e.fail(h2j_gpu_last_error());
     info[0] = f.out_w;
     info[1] = f.out_h;
-    info[2] = st->qscale;
+    info[2] = st.qscale;
     info[3] = nmcu;
-    if (cap < static_cast<size_t>(nmcu) * 384) return e.fail("output buffer too small");
-    std::memcpy(out, e.h_out.p + (f.jcoef - e.jcoef_base), static_cast<size_t>(nmcu) * 384 * 2);
     return 0;
 }
 
 int h2j_engine_stats(h2j_engine* w, double* out, int n) {
     if (!w) return -1;
-    for (int i = 0; i < n && i < 11; i++) out[i] = w->e.stats[i];
+    for (int i = 0; i < n && i < h2j::ST_N; i++) out[i] = w->e.stats[i];
     return 0;
 }
 

@@ -66,7 +66,7 @@ def _u8(buf: bytes):
 
 
 STAT_KEYS = ["parse_ms", "h2d_ms", "recon_ms", "deblock_ms", "sao_ms", "jpeg_ms", "d2h_ms",
-             "huffman_ms", "total_ms", "frames", "alg_bytes"]
+             "assemble_ms", "total_ms", "frames", "alg_bytes", "entropy_ms"]
 
 
 class Engine:
@@ -150,8 +150,8 @@ class Engine:
         return info[2], out[:nmcu * 384].reshape(nmcu, 6, 64).copy()
 
     def stats(self) -> dict:
-        arr = (ctypes.c_double * 11)()
-        self._lib.h2j_engine_stats(self._h, arr, 11)
+        arr = (ctypes.c_double * len(STAT_KEYS))()
+        self._lib.h2j_engine_stats(self._h, arr, len(STAT_KEYS))
         return {k: arr[i] for i, k in enumerate(STAT_KEYS)}
 
 

@@ -60,6 +60,11 @@ typedef struct {
     const h2j_slice *slices;
     const uint8_t *sl;
     uint8_t *arena;             /* pictures, maps, JPEG coefficients + stats */
+    /* JPEG entropy stage (h2j_gpu_entropy) */
+    uint8_t *seg;               /* entropy-coded segment pool, frames packed at jstat.seg_off */
+    uint64_t seg_cap;           /* pool bytes */
+    uint32_t *tile_bits;        /* scratch: nframes x ceil(max_mcu*6/256) */
+    uint64_t *seg_total;        /* device scalar: pool bytes used (16-byte units x16) */
 } h2j_gpu_batch;
 
 /* K1: dequantisation + inverse transform + intra prediction (HEVC and H.264),
@@ -69,8 +74,15 @@ int h2j_gpu_recon(const h2j_gpu_batch *b, void *stream);
 int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);
 /* K3: SAO frame.pic -> frame.pic2 (copies when SAO is off) */
 int h2j_gpu_sao(const h2j_gpu_batch *b, void *stream);
-/* K4: JPEG forward path on frame.pic2 -> frame.jcoef / frame.jstat */
+/* K4: JPEG forward path on frame.pic2 -> frame.jcoef / frame.jstat
+ * (variance, rate control, FDCT + quantiser + zigzag, symbol histograms) */
 int h2j_gpu_jpeg(const h2j_gpu_batch *b, void *stream);
+/* K4d alone: Huffman symbol histograms of frame.jcoef -> jstat.hist */
+int h2j_gpu_histogram(const h2j_gpu_batch *b, void *stream);
+/* K5: optimal Huffman tables (jstat.bits/val/code/len) and the entropy-coded
+ * payload of every frame, packed into b->seg at jstat.seg_off (jstat.nbytes
+ * bytes, 1-padded, no 0xFF stuffing).  *b->seg_total = bytes used. */
+int h2j_gpu_entropy(const h2j_gpu_batch *b, void *stream);
 
 #ifdef __cplusplus
 }

@@ -116,6 +116,16 @@ typedef struct {
     uint16_t q16[64];       /* quantiser reciprocal (A.5), natural order */
     uint16_t b16[64];       /* quantiser bias (A.5) */
     uint8_t dqt[64];        /* DQT entries, natural order (A.3) */
+    /* optimal Huffman tables (K5a, FFmpeg mjpegenc_huffman.c semantics) */
+    uint8_t bits[4][20];    /* [t][1..16] code counts per length */
+    uint8_t val[4][256];    /* symbols in DHT order */
+    uint8_t len[4][256];    /* code length per symbol */
+    uint16_t code[4][256];  /* code per symbol */
+    uint32_t nval[4];       /* symbols per table */
+    /* entropy-coded segment (K5b-K5d) */
+    uint32_t nbits;         /* payload bits before the 1-padding */
+    uint32_t nbytes;        /* padded payload bytes (no 0xFF stuffing) */
+    uint64_t seg_off;       /* byte offset of the payload in the segment pool */
 } h2j_jstat;
 
 #ifdef __cplusplus
