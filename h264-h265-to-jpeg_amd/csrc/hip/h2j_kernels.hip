@@ -84,270 +84,6 @@ __constant__ int16_t kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,  
                                       -256,  -315,  -390, -482, -630, -910, -1638, -4096, 0};
 __constant__ int8_t kLevelScale[6] = {40, 45, 51, 57, 64, 72};
 
-struct K1Lds {
-    int8_t mat[32][32];
-    int seq[132];
-    int sub[132];
-    int ref[132];
-    int blk[32 * 32];
-    int tmp[32 * 32];
-    int maxx, maxy;
-    int dcsum;
-};
-
-DEVI int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// ---------------------------------------------------------------- K1: HEVC
-template <typename Pel>
-__device__ void hevc_recon_frame(const h2j_frame& f, const h2j_tu* tus, const h2j_coef* coefs,
-                                 const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
-                                 uint8_t* arena, K1Lds& s) {
-    const int lane = threadIdx.x;
-    uint8_t* fmap = arena + f.maps;
-    int8_t* qmap = reinterpret_cast<int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
-    const h2j_tu* T = tus + f.tu;
-    const h2j_coef* CO = coefs + f.coef;
-    for (uint32_t t = 0; t < f.ntu; t++) {
-        const h2j_tu tu = T[t];
-        const int c = tu.c;
-        const int log2n = tu.log2n;
-        const int n = 1 << log2n;
-        const int nn = n * n;
-        const int x0 = tu.x, y0 = tu.y;
-        Pel* P = plane<Pel>(f, arena, f.pic, c);
-        const int st = f.pic_stride[c];
-        const int bd = c ? f.bit_depth_c : f.bit_depth;
-        const int maxv = (1 << bd) - 1;
-        const int shc = c ? 1 : 0;
-        const uint8_t flags = tu.flags;
-
-        if (flags & H2J_TU_PCM) {
-            for (int e = lane; e < tu.ncoef; e += 64) {
-                const uint32_t en = CO[tu.coef + e];
-                const int pos = static_cast<int>(en >> 16);
-                P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<Pel>(static_cast<uint16_t>(en & 0xFFFF));
-            }
-        } else {
-            // ---------------- residual (into s.blk) ----------------
-            const bool cbf = (flags & H2J_TU_CBF) != 0;
-            if (cbf) {
-                for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
-                if (lane == 0) { s.maxx = 0; s.maxy = 0; }
-                __syncthreads();
-                const bool bypass = (flags & H2J_TU_BYPASS) != 0;
-                const int qp = tu.qp;
-                const int bdShift = bd + log2n - 5;
-                const int ls = kLevelScale[qp % 6] << (qp / 6);
-                const uint8_t* slt = nullptr;
-                if (f.scaling_list && !((flags & H2J_TU_TSKIP) && n > 4)) {
-                    const int soff = log2n == 2 ? 0 + c * 16 : (log2n == 3 ? 48 + c * 64 : (log2n == 4 ? 240 + c * 256 : 1008));
-                    slt = sl + f.sl + soff;
-                }
-                int mx = 0, my = 0;
-                for (int e = lane; e < tu.ncoef; e += 64) {
-                    const uint32_t en = CO[tu.coef + e];
-                    const int pos = static_cast<int>(en >> 16);
-                    const int lvl = static_cast<int16_t>(en & 0xFFFF);
-                    int d;
-                    if (bypass) {
-                        d = lvl;
-                    } else {
-                        const int m = slt ? slt[pos] : 16;
-                        long long v = static_cast<long long>(lvl) * m * ls;
-                        v = (v + (1ll << (bdShift - 1))) >> bdShift;
-                        d = static_cast<int>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
-                    }
-                    s.blk[pos] = d;
-                    mx = max(mx, pos & (n - 1));
-                    my = max(my, pos >> log2n);
-                }
-                if (mx) atomicMax(&s.maxx, mx);
-                if (my) atomicMax(&s.maxy, my);
-                __syncthreads();
-                if (!bypass) {
-                    if (flags & H2J_TU_TSKIP) {
-                        const int bdS = 20 - bd;
-                        for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
-                    } else {
-                        const bool dst = (flags & H2J_TU_DST) != 0;
-                        const int mxx = s.maxx, myy = s.maxy;
-                        const int msh = 5 - log2n;
-                        // column pass: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
-                        for (int i = lane; i < nn; i += 64) {
-                            const int x = i & (n - 1), y = i >> log2n;
-                            int acc = 0;
-                            if (x <= mxx) {
-                                for (int j = 0; j <= myy; j++) {
-                                    const int cf = dst ? kDst4[j][y] : s.mat[j << msh][y];
-                                    acc += cf * s.blk[j * n + x];
-                                }
-                            }
-                            s.tmp[i] = clip3(-32768, 32767, (acc + 64) >> 7);
-                        }
-                        __syncthreads();
-                        const int bdS = 20 - bd;
-                        for (int i = lane; i < nn; i += 64) {
-                            const int x = i & (n - 1), y = i >> log2n;
-                            int acc = 0;
-                            for (int j = 0; j <= mxx; j++) {
-                                const int cf = dst ? kDst4[j][x] : s.mat[j << msh][x];
-                                acc += cf * s.tmp[y * n + j];
-                            }
-                            s.blk[i] = (acc + (1 << (bdS - 1))) >> bdS;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            // ---------------- reference samples ----------------
-            const int L = 4 * n + 1;
-            const int xl = x0 << shc, yl = y0 << shc;
-            unsigned long long m0 = 0, m1 = 0, m2 = 0;
-            for (int base = 0; base < L; base += 64) {
-                const int k = base + lane;
-                bool a = false;
-                if (k < L) {
-                    int xn, yn;
-                    if (k < 2 * n) { xn = x0 - 1; yn = y0 + (2 * n - 1 - k); }
-                    else if (k == 2 * n) { xn = x0 - 1; yn = y0 - 1; }
-                    else { xn = x0 + (k - 2 * n - 1); yn = y0 - 1; }
-                    a = avail(f, ctbs, slices, xl, yl, xn << shc, yn << shc);
-                    s.seq[k] = a ? static_cast<int>(P[yn * st + xn]) : 0;
-                }
-                const unsigned long long bal = __ballot(a);
-                if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
-            }
-            __syncthreads();
-            const bool any = (m0 | m1 | m2) != 0;
-            for (int k = lane; k < L; k += 64) {
-                int v;
-                if (!any) {
-                    v = 1 << (bd - 1);
-                } else {
-                    const int ch = k >> 6, bit = k & 63;
-                    const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
-                    if ((mk >> bit) & 1ull) {
-                        v = s.seq[k];
-                    } else {
-                        int j = -1;
-                        const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
-                        if (below) j = (ch << 6) + 63 - __clzll(below);
-                        else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
-                        else if (ch >= 1 && m0) j = 63 - __clzll(m0);
-                        if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
-                                          : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
-                        v = s.seq[j];
-                    }
-                }
-                s.sub[k] = v;
-            }
-            __syncthreads();
-            const int mode = tu.mode;
-            bool filt = false;
-            if (c == 0 && mode != 1 && n != 4) {
-                const int d26 = abs(mode - 26), d10 = abs(mode - 10);
-                const int md = d26 < d10 ? d26 : d10;
-                const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
-                filt = mode == 0 || md > thr;
-            }
-            if (filt) {
-                const int corner = s.sub[2 * n];
-                const bool strong = f.strong_smoothing && n == 32 &&
-                                    abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
-                                    abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
-                for (int k = lane; k < L; k += 64) {
-                    int v;
-                    if (k == 0 || k == 4 * n) v = s.sub[k];
-                    else if (strong) {
-                        if (k == 2 * n) v = corner;
-                        else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
-                        else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
-                    } else {
-                        v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
-                    }
-                    s.ref[k] = v;
-                }
-            } else {
-                for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
-            }
-            __syncthreads();
-            // p(-1,y) = ref[2n-1-y], p(x,-1) = ref[2n+1+x], p(-1,-1) = ref[2n]
-            const int* R = s.ref;
-            int dc = 0;
-            if (mode == 1) {
-                int part = 0;
-                for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
-                dc = (wave_sum(part) + n) >> (log2n + 1);
-            }
-            const int angle = kAngle[mode];
-            const int inv = kInvAngle[mode];
-            for (int i = lane; i < nn; i += 64) {
-                const int x = i & (n - 1), y = i >> log2n;
-                int pv;
-                if (mode == 0) {
-                    pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
-                          (y + 1) * R[n - 1] + n) >> (log2n + 1);
-                } else if (mode == 1) {
-                    pv = dc;
-                    if (c == 0 && n < 32) {
-                        if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
-                        else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                        else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
-                    }
-                } else if (mode >= 18) {
-                    const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
-                    // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
-                    const int k1 = x + idx + 1, k2 = x + idx + 2;
-                    const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
-                    if (fr) {
-                        const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
-                        pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-                    } else {
-                        pv = r1;
-                    }
-                    if (mode == 26 && c == 0 && n < 32 && x == 0)
-                        pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
-                } else {
-                    const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
-                    // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
-                    const int k1 = y + idx + 1, k2 = y + idx + 2;
-                    const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
-                    if (fr) {
-                        const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
-                        pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-                    } else {
-                        pv = r1;
-                    }
-                    if (mode == 10 && c == 0 && n < 32 && y == 0)
-                        pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
-                }
-                const int r = cbf ? s.blk[i] : 0;
-                P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
-            }
-        }
-        // ---------------- deblocking maps (luma TBs) ----------------
-        if (c == 0) {
-            const int nb = n >> 2;
-            for (int i = lane; i < nb * nb; i += 64) {
-                const int bx = i % nb, by = i / nb;
-                const int idx = ((y0 >> 2) + by) * f.mw + (x0 >> 2) + bx;
-                uint8_t fl = 0;
-                if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
-                if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
-                if (flags & H2J_TU_NOFILT) fl |= 4;
-                fmap[idx] = fl;
-                qmap[idx] = tu.qpy;
-            }
-        }
-        __syncthreads();
-    }
-}
-
-
 // ---------------------------------------------------------------- K1: H.264
 // H.264 8.3 (intra prediction), 8.5 (scaling + transforms).  Records: luma
 // log2n 2 (I4x4), 3 (I8x8), 4 (I16x16, DC levels at (4i,4j)); chroma log2n 3
@@ -434,301 +170,664 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
     }
 }
 
-struct H4Lds {
-    int top[40];   // top[0] = corner, top[1 + i] = p[i, -1]
-    int left[20];  // left[0] = corner, left[1 + i] = p[-1, i]
-    int ftop[40], fleft[20];
-    int blk[256];
-    int tmp[256];
+// ---------------------------------------------------------------- K0: per-TU preparation
+// Everything about a transform block that does not depend on reconstructed
+// neighbour samples, for every TU of the batch in parallel: the reference
+// availability mask, the CTB -> TU range, the HEVC deblocking maps, PCM
+// samples, and the residual (dequantisation + inverse transform) into an
+// int16 plane.  K1 then only walks the serial prediction chain.
+constexpr int kK0Tus = 8;    // TUs per K0 wave
+constexpr int kK1Waves = 8;  // waves (CTB rows in flight) per picture in K1
+
+struct K0Lds {
+    int8_t mat[32][32];
+    int blk[32 * 32];
+    int tmp[32 * 32];
     int dc[16];
-    int flags;     // bit0 top, bit1 left, bit2 corner, bit3 top-right
-    int dcv;
+    int maxx, maxy;
 };
 
-template <typename Pel>
-__device__ void h264_recon_frame(const h2j_frame& f, const h2j_tu* tus, const h2j_coef* coefs, const h2j_ctb* mbs,
-                                 const h2j_slice* slices, const uint8_t* sl, uint8_t* arena, H4Lds& s) {
-    const int lane = threadIdx.x;
-    const h2j_tu* T = tus + f.tu;
-    const h2j_coef* CO = coefs + f.coef;
-    for (uint32_t t = 0; t < f.ntu; t++) {
-        const h2j_tu tu = T[t];
-        const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-        const int x0 = tu.x, y0 = tu.y;
-        Pel* P = plane<Pel>(f, arena, f.pic, c);
-        const int st = f.pic_stride[c];
-        const int bd = c ? f.bit_depth_c : f.bit_depth;
-        const int maxv = (1 << bd) - 1;
-        if (tu.flags & H2J_TU_PCM) {
-            for (int e = lane; e < tu.ncoef; e += 64) {
-                const uint32_t en = CO[tu.coef + e];
-                const int pos = static_cast<int>(en >> 16);
-                P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<Pel>(static_cast<uint16_t>(en & 0xFFFF));
-            }
-            __syncthreads();
-            continue;
-        }
-        // ---------------- residual ----------------
-        const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
-        const int qp = tu.qp, qm = qp % 6;
-        const bool i16 = c == 0 && log2n == 4;
-        const bool chroma = c > 0;
-        if (cbf) {
-            for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
-            __syncthreads();
-            for (int e = lane; e < tu.ncoef; e += 64) {
-                const uint32_t en = CO[tu.coef + e];
-                s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
-            }
-            __syncthreads();
-            const uint8_t* w4 = f.scaling_list ? sl + f.sl + c * 16 : nullptr;
-            if (i16 || chroma) {
-                // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
-                const int nb = n >> 2;  // blocks per side: 4 (luma) / 2 (chroma)
-                if (lane < nb * nb) {
-                    const int r = lane / nb, q = lane % nb;
-                    int acc = 0;
-                    for (int i = 0; i < nb; i++)
-                        for (int j = 0; j < nb; j++) {
-                            const int hr = nb == 4 ? ((r == 0 || (r == 1 && i < 2) || (r == 2 && (i == 0 || i == 3)) || (r == 3 && !(i & 1))) ? 1 : -1)
-                                                   : ((r == 0 || i == 0) ? 1 : -1);
-                            const int hc = nb == 4 ? ((q == 0 || (q == 1 && j < 2) || (q == 2 && (j == 0 || j == 3)) || (q == 3 && !(j & 1))) ? 1 : -1)
-                                                   : ((q == 0 || j == 0) ? 1 : -1);
-                            acc += hr * hc * s.blk[(i * 4) * n + j * 4];
-                        }
-                    const int ls0 = (w4 ? w4[0] : 16) * kNorm4[qm][0];
-                    int v;
-                    if (nb == 4) v = qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6);
-                    else v = ((acc * ls0) << (qp / 6)) >> 5;
-                    s.dc[lane] = v;
-                }
-                __syncthreads();
-                for (int i = lane; i < nn; i += 64) {
-                    const int y = i >> log2n, x = i & (n - 1);
-                    const int by = y >> 2, bx = x >> 2, ry = y & 3, rx = x & 3;
-                    if (ry == 0 && rx == 0) s.blk[i] = s.dc[by * (n >> 2) + bx];
-                    else s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[ry * 4 + rx] : 16) * h264_norm4(qm, ry, rx), qp);
-                }
-            } else if (log2n == 2) {
-                for (int i = lane; i < 16; i += 64)
-                    s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[i] : 16) * h264_norm4(qm, i >> 2, i & 3), qp);
-            } else {
-                const uint8_t* w8 = f.scaling_list ? sl + f.sl + 48 : nullptr;
-                for (int i = lane; i < 64; i += 64)
-                    s.blk[i] = h264_scale8(s.blk[i], (w8 ? w8[i] : 16) * h264_norm8(qm, i >> 3, i & 7), qp);
-            }
-            __syncthreads();
-            if (log2n == 3 && !chroma) {
-                // 8x8 inverse transform: rows (lanes 0..7) then columns
-                if (lane < 16) {
-                    const bool rows = lane < 8;
-                    (void)rows;
-                }
-                for (int pass = 0; pass < 2; pass++) {
-                    if (lane < 8) {
-                        int d[8], o[8];
-                        for (int k = 0; k < 8; k++) d[k] = pass == 0 ? s.blk[lane * 8 + k] : s.tmp[k * 8 + lane];
-                        const int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
-                        const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
-                        const int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
-                        const int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
-                        const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
-                        o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
-                        o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
-                        if (pass == 0) for (int k = 0; k < 8; k++) s.tmp[lane * 8 + k] = o[k];
-                        else for (int k = 0; k < 8; k++) s.blk[k * 8 + lane] = (o[k] + 32) >> 6;
-                    }
-                    __syncthreads();
-                }
-            } else {
-                // 4x4 inverse transforms of all 4x4 blocks: lane = block * 4 + row/col
-                const int nb = n >> 2, nblk = nb * nb;
-                for (int pass = 0; pass < 2; pass++) {
-                    for (int id = lane; id < nblk * 4; id += 64) {
-                        const int b = id >> 2, k = id & 3;
-                        const int bx = (b % nb) * 4, by = (b / nb) * 4;
-                        int d0, d1, d2, d3;
-                        if (pass == 0) {
-                            const int* r = &s.blk[(by + k) * n + bx];
-                            d0 = r[0]; d1 = r[1]; d2 = r[2]; d3 = r[3];
-                        } else {
-                            d0 = s.tmp[(by + 0) * n + bx + k]; d1 = s.tmp[(by + 1) * n + bx + k];
-                            d2 = s.tmp[(by + 2) * n + bx + k]; d3 = s.tmp[(by + 3) * n + bx + k];
-                        }
-                        const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
-                        if (pass == 0) {
-                            int* o = &s.tmp[(by + k) * n + bx];
-                            o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
-                        } else {
-                            s.blk[(by + 0) * n + bx + k] = (e0 + e3 + 32) >> 6;
-                            s.blk[(by + 1) * n + bx + k] = (e1 + e2 + 32) >> 6;
-                            s.blk[(by + 2) * n + bx + k] = (e1 - e2 + 32) >> 6;
-                            s.blk[(by + 3) * n + bx + k] = (e0 - e3 + 32) >> 6;
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-        }
-        // ---------------- prediction ----------------
-        const int shc = c ? 1 : 0;
-        const int xl = x0 << shc, yl = y0 << shc;
-        const bool nxn = c == 0 && log2n <= 3;
-        const int ntop = nxn ? 2 * n : n;
-        if (lane == 0) {
-            int fl = 0;
-            if (h264_avail(f, mbs, slices, xl, yl, xl, yl - 1)) fl |= 1;
-            if (h264_avail(f, mbs, slices, xl, yl, xl - 1, yl)) fl |= 2;
-            if (h264_avail(f, mbs, slices, xl, yl, xl - 1, yl - 1)) fl |= 4;
-            if (nxn && h264_avail(f, mbs, slices, xl, yl, xl + n, yl - 1)) fl |= 8;
-            s.flags = fl;
-        }
-        __syncthreads();
-        const int fl = s.flags;
-        for (int i = lane; i <= ntop; i += 64) {
-            int v = 0;
-            if (i == 0) v = (fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0;
-            else if (i - 1 < n) v = (fl & 1) ? P[(y0 - 1) * st + x0 + i - 1] : 0;
-            else v = (fl & 8) ? P[(y0 - 1) * st + x0 + i - 1] : ((fl & 1) ? P[(y0 - 1) * st + x0 + n - 1] : 0);
-            s.top[i] = v;
-        }
-        for (int i = lane; i <= n; i += 64) s.left[i] = i == 0 ? ((fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0)
-                                                               : ((fl & 2) ? P[(y0 + i - 1) * st + x0 - 1] : 0);
-        __syncthreads();
-        const int mode = tu.mode;
-        const int* TT = s.top + 1;
-        const int* LL = s.left + 1;
-        if (nxn && log2n == 3) {
-            // 8.3.2.2.1 reference sample filtering
-            const bool at = fl & 1, al = fl & 2, ad = fl & 4;
-            for (int i = lane; i <= 16; i += 64) {
-                int v = 0;
-                if (i == 0) {
-                    const int C = s.top[0];
-                    if (!ad) v = C;
-                    else if (at && al) v = (TT[0] + 2 * C + LL[0] + 2) >> 2;
-                    else if (at) v = (3 * C + TT[0] + 2) >> 2;
-                    else if (al) v = (3 * C + LL[0] + 2) >> 2;
-                    else v = C;
-                } else if (at) {
-                    const int x = i - 1;
-                    if (x == 0) v = ad ? (s.top[0] + 2 * TT[0] + TT[1] + 2) >> 2 : (3 * TT[0] + TT[1] + 2) >> 2;
-                    else if (x == 15) v = (TT[14] + 3 * TT[15] + 2) >> 2;
-                    else v = (TT[x - 1] + 2 * TT[x] + TT[x + 1] + 2) >> 2;
-                }
-                s.ftop[i] = v;
-            }
-            for (int i = lane; i < 8; i += 64) {
-                int v = 0;
-                if (al) {
-                    if (i == 0) v = ad ? (s.top[0] + 2 * LL[0] + LL[1] + 2) >> 2 : (3 * LL[0] + LL[1] + 2) >> 2;
-                    else if (i == 7) v = (LL[6] + 3 * LL[7] + 2) >> 2;
-                    else v = (LL[i - 1] + 2 * LL[i] + LL[i + 1] + 2) >> 2;
-                }
-                s.fleft[i + 1] = v;
-            }
-            if (lane == 0) s.fleft[0] = 0;
-            __syncthreads();
-            if (lane == 0) s.fleft[0] = s.ftop[0];
-            __syncthreads();
-            TT = s.ftop + 1;
-            LL = s.fleft + 1;
-        }
-        // DC value
-        if (lane == 0) {
-            const bool at = fl & 1, al = fl & 2;
-            int sum = 0, v;
-            if (chroma) {
-                v = 0;  // per-quadrant below
-            } else {
-                const int lg = log2n;
-                if (at && al) {
-                    for (int i = 0; i < n; i++) sum += TT[i] + LL[i];
-                    v = (sum + n) >> (lg + 1);
-                } else if (al) {
-                    for (int i = 0; i < n; i++) sum += LL[i];
-                    v = (sum + (n >> 1)) >> lg;
-                } else if (at) {
-                    for (int i = 0; i < n; i++) sum += TT[i];
-                    v = (sum + (n >> 1)) >> lg;
-                } else {
-                    v = 1 << (bd - 1);
-                }
-            }
-            s.dcv = v;
-        }
-        __syncthreads();
-        const int dcv = s.dcv;
-        for (int i = lane; i < nn; i += 64) {
-            const int x = i & (n - 1), y = i >> log2n;
-            int pv;
-            if (nxn) {
-                pv = h264_pred_nxn(mode, x, y, n, TT, LL, dcv);
-            } else if (!chroma) {  // 16x16
-                if (mode == 0) pv = TT[x];
-                else if (mode == 1) pv = LL[y];
-                else if (mode == 2) pv = dcv;
-                else {
-                    int H = 0, V = 0;
-                    for (int k = 0; k < 8; k++) {
-                        H += (k + 1) * (TT[8 + k] - TT[6 - k]);
-                        V += (k + 1) * (LL[8 + k] - LL[6 - k]);
-                    }
-                    const int a = 16 * (LL[15] + TT[15]), b = (5 * H + 32) >> 6, cc = (5 * V + 32) >> 6;
-                    pv = clip3(0, maxv, (a + b * (x - 7) + cc * (y - 7) + 16) >> 5);
-                }
-            } else {  // chroma 8x8 (mode: 0 DC, 1 horizontal, 2 vertical, 3 plane)
-                if (mode == 1) pv = LL[y];
-                else if (mode == 2) pv = TT[x];
-                else if (mode == 3) {
-                    int H = 0, V = 0;
-                    for (int k = 0; k < 4; k++) {
-                        H += (k + 1) * (TT[4 + k] - TT[2 - k]);
-                        V += (k + 1) * (LL[4 + k] - LL[2 - k]);
-                    }
-                    const int a = 16 * (LL[7] + TT[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
-                    pv = clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
-                } else {
-                    const bool at = fl & 1, al = fl & 2;
-                    const int bx = x >> 2, by = y >> 2;
-                    int st4 = 0, sl4 = 0;
-                    for (int k = 0; k < 4; k++) { st4 += TT[bx * 4 + k]; sl4 += LL[by * 4 + k]; }
-                    if (bx == by) pv = (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1)));
-                    else if (bx) pv = at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1));
-                    else pv = al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
-                }
-            }
-            const int r = cbf ? s.blk[i] : 0;
-            P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
-        }
-        __syncthreads();
-    }
+DEVI int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-__global__ void __launch_bounds__(64) h2j_k1_recon(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
-                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
-                                                  uint8_t* arena) {
-    __shared__ union {
-        K1Lds h5;
-        H4Lds h4;
-    } u;
-    K1Lds& s = u.h5;
-    const h2j_frame& f = frames[blockIdx.x];
-    for (int i = threadIdx.x; i < 1024; i += 64) {
-        const int m = i >> 5, nn = i & 31;
-        int a = ((2 * nn + 1) * m) & 127;
-        if (a > 64) a = 128 - a;
-        s.mat[m][nn] = static_cast<int8_t>(a > 32 ? -kCos33[64 - a] : kCos33[a]);
+// lanes of one wave exchanging data through LDS
+DEVI void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+DEVI uint64_t* tu_masks(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint64_t*>(arena + f.aux); }
+DEVI uint32_t* ctb_ranges(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint32_t*>(arena + f.ctbrng); }
+DEVI int16_t* res_plane(const h2j_frame& f, uint8_t* arena, int c) {
+    return reinterpret_cast<int16_t*>(arena + f.res) + f.pic_off[c];
+}
+DEVI int ctb_of(const h2j_frame& f, const h2j_tu& tu) {
+    const int sh = tu.c ? 1 : 0;
+    return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
+}
+
+// HEVC dequantisation (8.6.2-8.6.3) + inverse transform / transform skip /
+// bypass (8.6.4) of one TB into R (int16, stride rst).
+DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO, const uint8_t* sl, int16_t* R,
+                        int rst, K0Lds& s) {
+    const int lane = threadIdx.x;
+    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const uint8_t flags = tu.flags;
+    for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
+    if (lane == 0) { s.maxx = 0; s.maxy = 0; }
+    __syncthreads();
+    const bool bypass = (flags & H2J_TU_BYPASS) != 0;
+    const int qp = tu.qp;
+    const int bdShift = bd + log2n - 5;
+    const int ls = kLevelScale[qp % 6] << (qp / 6);
+    const uint8_t* slt = nullptr;
+    if (f.scaling_list && !((flags & H2J_TU_TSKIP) && n > 4)) {
+        const int soff = log2n == 2 ? 0 + c * 16 : (log2n == 3 ? 48 + c * 64 : (log2n == 4 ? 240 + c * 256 : 1008));
+        slt = sl + f.sl + soff;
+    }
+    int mx = 0, my = 0;
+    for (int e = lane; e < tu.ncoef; e += 64) {
+        const uint32_t en = CO[tu.coef + e];
+        const int pos = static_cast<int>(en >> 16);
+        const int lvl = static_cast<int16_t>(en & 0xFFFF);
+        int d;
+        if (bypass) {
+            d = lvl;
+        } else {
+            const int m = slt ? slt[pos] : 16;
+            long long v = static_cast<long long>(lvl) * m * ls;
+            v = (v + (1ll << (bdShift - 1))) >> bdShift;
+            d = static_cast<int>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+        }
+        s.blk[pos] = d;
+        mx = max(mx, pos & (n - 1));
+        my = max(my, pos >> log2n);
+    }
+    if (mx) atomicMax(&s.maxx, mx);
+    if (my) atomicMax(&s.maxy, my);
+    __syncthreads();
+    if (!bypass) {
+        if (flags & H2J_TU_TSKIP) {
+            const int bdS = 20 - bd;
+            for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
+        } else {
+            const bool dst = (flags & H2J_TU_DST) != 0;
+            const int mxx = s.maxx, myy = s.maxy;
+            const int msh = 5 - log2n;
+            // column pass: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
+            for (int i = lane; i < nn; i += 64) {
+                const int x = i & (n - 1), y = i >> log2n;
+                int acc = 0;
+                if (x <= mxx) {
+                    for (int j = 0; j <= myy; j++) {
+                        const int cf = dst ? kDst4[j][y] : s.mat[j << msh][y];
+                        acc += cf * s.blk[j * n + x];
+                    }
+                }
+                s.tmp[i] = clip3(-32768, 32767, (acc + 64) >> 7);
+            }
+            __syncthreads();
+            const int bdS = 20 - bd;
+            for (int i = lane; i < nn; i += 64) {
+                const int x = i & (n - 1), y = i >> log2n;
+                int acc = 0;
+                for (int j = 0; j <= mxx; j++) {
+                    const int cf = dst ? kDst4[j][x] : s.mat[j << msh][x];
+                    acc += cf * s.tmp[y * n + j];
+                }
+                s.blk[i] = (acc + (1 << (bdS - 1))) >> bdS;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    __syncthreads();
+}
+
+// H.264 scaling (8.5.9, 8.5.10-8.5.12 DC transforms) + 4x4 / 8x8 inverse
+// transforms (8.5.12.2, 8.5.13) of one record into R.
+DEVI void h264_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO, const uint8_t* sl, int16_t* R,
+                        int rst, K0Lds& s) {
+    const int lane = threadIdx.x;
+    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int qp = tu.qp, qm = qp % 6;
+    const bool i16 = c == 0 && log2n == 4;
+    const bool chroma = c > 0;
+    for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
+    __syncthreads();
+    for (int e = lane; e < tu.ncoef; e += 64) {
+        const uint32_t en = CO[tu.coef + e];
+        s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
+    }
+    __syncthreads();
+    const uint8_t* w4 = f.scaling_list ? sl + f.sl + c * 16 : nullptr;
+    if (i16 || chroma) {
+        // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
+        const int nb = n >> 2;  // blocks per side: 4 (luma) / 2 (chroma)
+        if (lane < nb * nb) {
+            const int r = lane / nb, q = lane % nb;
+            int acc = 0;
+            for (int i = 0; i < nb; i++)
+                for (int j = 0; j < nb; j++) {
+                    const int hr = nb == 4 ? ((r == 0 || (r == 1 && i < 2) || (r == 2 && (i == 0 || i == 3)) || (r == 3 && !(i & 1))) ? 1 : -1)
+                                           : ((r == 0 || i == 0) ? 1 : -1);
+                    const int hc = nb == 4 ? ((q == 0 || (q == 1 && j < 2) || (q == 2 && (j == 0 || j == 3)) || (q == 3 && !(j & 1))) ? 1 : -1)
+                                           : ((q == 0 || j == 0) ? 1 : -1);
+                    acc += hr * hc * s.blk[(i * 4) * n + j * 4];
+                }
+            const int ls0 = (w4 ? w4[0] : 16) * kNorm4[qm][0];
+            int v;
+            if (nb == 4) v = qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+            else v = ((acc * ls0) << (qp / 6)) >> 5;
+            s.dc[lane] = v;
+        }
+        __syncthreads();
+        for (int i = lane; i < nn; i += 64) {
+            const int y = i >> log2n, x = i & (n - 1);
+            const int by = y >> 2, bx = x >> 2, ry = y & 3, rx = x & 3;
+            if (ry == 0 && rx == 0) s.blk[i] = s.dc[by * (n >> 2) + bx];
+            else s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[ry * 4 + rx] : 16) * h264_norm4(qm, ry, rx), qp);
+        }
+    } else if (log2n == 2) {
+        for (int i = lane; i < 16; i += 64)
+            s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[i] : 16) * h264_norm4(qm, i >> 2, i & 3), qp);
+    } else {
+        const uint8_t* w8 = f.scaling_list ? sl + f.sl + 48 : nullptr;
+        for (int i = lane; i < 64; i += 64)
+            s.blk[i] = h264_scale8(s.blk[i], (w8 ? w8[i] : 16) * h264_norm8(qm, i >> 3, i & 7), qp);
+    }
+    __syncthreads();
+    if (log2n == 3 && !chroma) {
+        // 8x8 inverse transform: rows (lanes 0..7) then columns
+        for (int pass = 0; pass < 2; pass++) {
+            if (lane < 8) {
+                int d[8], o[8];
+                for (int k = 0; k < 8; k++) d[k] = pass == 0 ? s.blk[lane * 8 + k] : s.tmp[k * 8 + lane];
+                const int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
+                const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+                const int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
+                const int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
+                const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+                o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
+                o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+                if (pass == 0) for (int k = 0; k < 8; k++) s.tmp[lane * 8 + k] = o[k];
+                else for (int k = 0; k < 8; k++) s.blk[k * 8 + lane] = (o[k] + 32) >> 6;
+            }
+            __syncthreads();
+        }
+    } else {
+        // 4x4 inverse transforms of all 4x4 blocks: lane = block * 4 + row/col
+        const int nb = n >> 2, nblk = nb * nb;
+        for (int pass = 0; pass < 2; pass++) {
+            for (int id = lane; id < nblk * 4; id += 64) {
+                const int b = id >> 2, k = id & 3;
+                const int bx = (b % nb) * 4, by = (b / nb) * 4;
+                int d0, d1, d2, d3;
+                if (pass == 0) {
+                    const int* r = &s.blk[(by + k) * n + bx];
+                    d0 = r[0]; d1 = r[1]; d2 = r[2]; d3 = r[3];
+                } else {
+                    d0 = s.tmp[(by + 0) * n + bx + k]; d1 = s.tmp[(by + 1) * n + bx + k];
+                    d2 = s.tmp[(by + 2) * n + bx + k]; d3 = s.tmp[(by + 3) * n + bx + k];
+                }
+                const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+                if (pass == 0) {
+                    int* o = &s.tmp[(by + k) * n + bx];
+                    o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
+                } else {
+                    s.blk[(by + 0) * n + bx + k] = (e0 + e3 + 32) >> 6;
+                    s.blk[(by + 1) * n + bx + k] = (e1 + e2 + 32) >> 6;
+                    s.blk[(by + 2) * n + bx + k] = (e1 - e2 + 32) >> 6;
+                    s.blk[(by + 3) * n + bx + k] = (e0 - e3 + 32) >> 6;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
+                                                 const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
+                                                 uint8_t* arena) {
+    __shared__ K0Lds s;
+    const h2j_frame& f = frames[blockIdx.y];
+    const uint32_t t0 = blockIdx.x * kK0Tus;
+    if (t0 >= f.ntu) return;
+    const int lane = threadIdx.x;
+    const bool hevc = f.codec == H2J_CODEC_HEVC;
+    if (hevc) {
+        for (int i = lane; i < 1024; i += 64) {
+            const int m = i >> 5, nn = i & 31;
+            int a = ((2 * nn + 1) * m) & 127;
+            if (a > 64) a = 128 - a;
+            s.mat[m][nn] = static_cast<int8_t>(a > 32 ? -kCos33[64 - a] : kCos33[a]);
+        }
     }
     __syncthreads();
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
+    const h2j_tu* T = tus + f.tu;
+    const h2j_coef* CO = coefs + f.coef;
+    uint64_t* masks = tu_masks(f, arena);
+    uint32_t* rng = ctb_ranges(f, arena);
+    uint8_t* fmap = arena + f.maps;
+    int8_t* qmap = reinterpret_cast<int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
+    const uint32_t t1 = min(f.ntu, t0 + kK0Tus);
+    for (uint32_t t = t0; t < t1; t++) {
+        const h2j_tu tu = T[t];
+        const int c = tu.c, log2n = tu.log2n, n = 1 << log2n;
+        const int shc = c ? 1 : 0;
+        const int x0 = tu.x, y0 = tu.y, xl = x0 << shc, yl = y0 << shc;
+        if (lane == 0) {
+            const int cb = ctb_of(f, tu);
+            if (t == 0 || ctb_of(f, T[t - 1]) != cb) rng[2 * cb] = t;
+            if (t + 1 == f.ntu || ctb_of(f, T[t + 1]) != cb) rng[2 * cb + 1] = t + 1;
+        }
+        const uint8_t flags = tu.flags;
+        if (hevc && c == 0) {  // deblocking maps (luma TBs)
+            const int nb = n >> 2;
+            for (int i = lane; i < nb * nb; i += 64) {
+                const int bx = i % nb, by = i / nb;
+                const int idx = ((y0 >> 2) + by) * f.mw + (x0 >> 2) + bx;
+                uint8_t fl = 0;
+                if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
+                if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
+                if (flags & H2J_TU_NOFILT) fl |= 4;
+                fmap[idx] = fl;
+                qmap[idx] = tu.qpy;
+            }
+        }
+        if (flags & H2J_TU_PCM) {
+            const int st = f.pic_stride[c];
+            if (f.bit_depth == 8) {
+                uint8_t* P = plane<uint8_t>(f, arena, f.pic, c);
+                for (int e = lane; e < tu.ncoef; e += 64) {
+                    const uint32_t en = CO[tu.coef + e];
+                    const int pos = static_cast<int>(en >> 16);
+                    P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<uint8_t>(en & 0xFF);
+                }
+            } else {
+                uint16_t* P = plane<uint16_t>(f, arena, f.pic, c);
+                for (int e = lane; e < tu.ncoef; e += 64) {
+                    const uint32_t en = CO[tu.coef + e];
+                    const int pos = static_cast<int>(en >> 16);
+                    P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
+                }
+            }
+            if (lane == 0) masks[t] = 0;
+            continue;
+        }
+        // reference availability mask
+        uint64_t mask;
+        if (hevc) {
+            const int u = c ? 2 : 4, nu = (2 * n) / u;
+            bool a = false;
+            if (lane <= 2 * nu) {
+                int xn, yn;
+                if (lane < nu) { xn = x0 - 1; yn = y0 + 2 * n - 1 - lane * u; }
+                else if (lane == nu) { xn = x0 - 1; yn = y0 - 1; }
+                else { xn = x0 + (lane - nu - 1) * u; yn = y0 - 1; }
+                a = avail(f, C, S, xl, yl, xn << shc, yn << shc);
+            }
+            mask = __ballot(a);
+        } else {
+            const bool nxn = c == 0 && log2n <= 3;
+            bool a = false;
+            if (lane == 0) a = h264_avail(f, C, S, xl, yl, xl, yl - 1);
+            else if (lane == 1) a = h264_avail(f, C, S, xl, yl, xl - 1, yl);
+            else if (lane == 2) a = h264_avail(f, C, S, xl, yl, xl - 1, yl - 1);
+            else if (lane == 3) a = nxn && h264_avail(f, C, S, xl, yl, xl + n, yl - 1);
+            mask = __ballot(a);
+        }
+        if (lane == 0) masks[t] = mask;
+        if (flags & H2J_TU_CBF) {
+            int16_t* R = res_plane(f, arena, c);
+            const int rst = f.pic_stride[c];
+            if (hevc) hevc_residual(f, tu, CO, sl, R, rst, s);
+            else h264_residual(f, tu, CO, sl, R, rst, s);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- K1: intra prediction chain
+// One workgroup per picture, kK1Waves waves; wave w reconstructs CTB rows
+// w, w + kK1Waves, ...  CTB (x, r) starts once row r-1 has finished CTBs
+// 0..x+1 (its left / top-left / top / top-right neighbours: everything intra
+// prediction can reference), tracked by row-tagged progress counters in LDS.
+// Inside a CTB the wave walks the TUs in decoding order: reference gather
+// with K0's availability mask, substitution / filtering, prediction, + K0's
+// residual, clip, store.  (H.265 8.4.4.2; H.264 8.3)
+struct K1WaveLds {  // HEVC
+    int seq[132];
+    int sub[132];
+    int ref[132];
+};
+struct H4WaveLds {  // H.264
+    int top[40];    // top[0] = corner, top[1 + i] = p[i, -1]
+    int left[20];   // left[0] = corner, left[1 + i] = p[-1, i]
+    int ftop[40], fleft[20];
+    int dcv;
+};
+union K1WLds {
+    K1WaveLds h5;
+    H4WaveLds h4;
+};
+
+template <typename Pel>
+DEVI void hevc_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, uint8_t* arena, K1WaveLds& s,
+                          int lane) {
+    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int x0 = tu.x, y0 = tu.y;
+    Pel* P = plane<Pel>(f, arena, f.pic, c);
+    const int16_t* RS = res_plane(f, arena, c);
+    const int st = f.pic_stride[c];
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int maxv = (1 << bd) - 1;
+    const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
+    const int L = 4 * n + 1;
+    const int ush = c ? 1 : 2, nu = (2 * n) >> ush;
+    unsigned long long m0 = 0, m1 = 0, m2 = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int k = base + lane;
+        bool a = false;
+        if (k < L) {
+            int xn, yn, unit;
+            if (k < 2 * n) { xn = x0 - 1; yn = y0 + (2 * n - 1 - k); unit = k >> ush; }
+            else if (k == 2 * n) { xn = x0 - 1; yn = y0 - 1; unit = nu; }
+            else { xn = x0 + (k - 2 * n - 1); yn = y0 - 1; unit = nu + 1 + ((k - 2 * n - 1) >> ush); }
+            a = (mask >> unit) & 1ull;
+            s.seq[k] = a ? static_cast<int>(P[yn * st + xn]) : 0;
+        }
+        const unsigned long long bal = __ballot(a);
+        if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
+    }
+    wave_sync();
+    const bool any = (m0 | m1 | m2) != 0;
+    for (int k = lane; k < L; k += 64) {
+        int v;
+        if (!any) {
+            v = 1 << (bd - 1);
+        } else {
+            const int ch = k >> 6, bit = k & 63;
+            const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
+            if ((mk >> bit) & 1ull) {
+                v = s.seq[k];
+            } else {
+                int j = -1;
+                const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
+                if (below) j = (ch << 6) + 63 - __clzll(below);
+                else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
+                else if (ch >= 1 && m0) j = 63 - __clzll(m0);
+                if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
+                                  : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
+                v = s.seq[j];
+            }
+        }
+        s.sub[k] = v;
+    }
+    wave_sync();
+    const int mode = tu.mode;
+    bool filt = false;
+    if (c == 0 && mode != 1 && n != 4) {
+        const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+        const int md = d26 < d10 ? d26 : d10;
+        const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+        filt = mode == 0 || md > thr;
+    }
+    if (filt) {
+        const int corner = s.sub[2 * n];
+        const bool strong = f.strong_smoothing && n == 32 &&
+                            abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
+                            abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
+        for (int k = lane; k < L; k += 64) {
+            int v;
+            if (k == 0 || k == 4 * n) v = s.sub[k];
+            else if (strong) {
+                if (k == 2 * n) v = corner;
+                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
+                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
+            } else {
+                v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
+            }
+            s.ref[k] = v;
+        }
+    } else {
+        for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
+    }
+    wave_sync();
+    // p(-1,y) = ref[2n-1-y], p(x,-1) = ref[2n+1+x], p(-1,-1) = ref[2n]
+    const int* R = s.ref;
+    int dc = 0;
+    if (mode == 1) {
+        int part = 0;
+        for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
+        dc = (wave_sum(part) + n) >> (log2n + 1);
+    }
+    const int angle = kAngle[mode];
+    const int inv = kInvAngle[mode];
+    for (int i = lane; i < nn; i += 64) {
+        const int x = i & (n - 1), y = i >> log2n;
+        const int r = cbf ? RS[(y0 + y) * st + x0 + x] : 0;
+        int pv;
+        if (mode == 0) {
+            pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
+                  (y + 1) * R[n - 1] + n) >> (log2n + 1);
+        } else if (mode == 1) {
+            pv = dc;
+            if (c == 0 && n < 32) {
+                if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
+                else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+            }
+        } else if (mode >= 18) {
+            const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
+            // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
+            const int k1 = x + idx + 1, k2 = x + idx + 2;
+            const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
+            if (fr) {
+                const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
+                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            } else {
+                pv = r1;
+            }
+            if (mode == 26 && c == 0 && n < 32 && x == 0)
+                pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
+        } else {
+            const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
+            // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
+            const int k1 = y + idx + 1, k2 = y + idx + 2;
+            const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
+            if (fr) {
+                const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
+                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            } else {
+                pv = r1;
+            }
+            if (mode == 10 && c == 0 && n < 32 && y == 0)
+                pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
+        }
+        P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
+    }
+    wave_sync();
+}
+
+template <typename Pel>
+DEVI void h264_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, uint8_t* arena, H4WaveLds& s,
+                          int lane) {
+    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int x0 = tu.x, y0 = tu.y;
+    Pel* P = plane<Pel>(f, arena, f.pic, c);
+    const int16_t* RS = res_plane(f, arena, c);
+    const int st = f.pic_stride[c];
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int maxv = (1 << bd) - 1;
+    const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
+    const bool chroma = c > 0;
+    const bool nxn = c == 0 && log2n <= 3;
+    const int ntop = nxn ? 2 * n : n;
+    // mask bits: 0 top, 1 left, 2 corner, 3 top-right
+    const int fl = static_cast<int>(mask & 15);
+    for (int i = lane; i <= ntop; i += 64) {
+        int v = 0;
+        if (i == 0) v = (fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0;
+        else if (i - 1 < n) v = (fl & 1) ? P[(y0 - 1) * st + x0 + i - 1] : 0;
+        else v = (fl & 8) ? P[(y0 - 1) * st + x0 + i - 1] : ((fl & 1) ? P[(y0 - 1) * st + x0 + n - 1] : 0);
+        s.top[i] = v;
+    }
+    for (int i = lane; i <= n; i += 64) s.left[i] = i == 0 ? ((fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0)
+                                                           : ((fl & 2) ? P[(y0 + i - 1) * st + x0 - 1] : 0);
+    wave_sync();
+    const int mode = tu.mode;
+    const int* TT = s.top + 1;
+    const int* LL = s.left + 1;
+    if (nxn && log2n == 3) {
+        // 8.3.2.2.1 reference sample filtering
+        const bool at = fl & 1, al = fl & 2, ad = fl & 4;
+        for (int i = lane; i <= 16; i += 64) {
+            int v = 0;
+            if (i == 0) {
+                const int C = s.top[0];
+                if (!ad) v = C;
+                else if (at && al) v = (TT[0] + 2 * C + LL[0] + 2) >> 2;
+                else if (at) v = (3 * C + TT[0] + 2) >> 2;
+                else if (al) v = (3 * C + LL[0] + 2) >> 2;
+                else v = C;
+            } else if (at) {
+                const int x = i - 1;
+                if (x == 0) v = ad ? (s.top[0] + 2 * TT[0] + TT[1] + 2) >> 2 : (3 * TT[0] + TT[1] + 2) >> 2;
+                else if (x == 15) v = (TT[14] + 3 * TT[15] + 2) >> 2;
+                else v = (TT[x - 1] + 2 * TT[x] + TT[x + 1] + 2) >> 2;
+            }
+            s.ftop[i] = v;
+        }
+        for (int i = lane; i < 8; i += 64) {
+            int v = 0;
+            if (al) {
+                if (i == 0) v = ad ? (s.top[0] + 2 * LL[0] + LL[1] + 2) >> 2 : (3 * LL[0] + LL[1] + 2) >> 2;
+                else if (i == 7) v = (LL[6] + 3 * LL[7] + 2) >> 2;
+                else v = (LL[i - 1] + 2 * LL[i] + LL[i + 1] + 2) >> 2;
+            }
+            s.fleft[i + 1] = v;
+        }
+        wave_sync();
+        if (lane == 0) s.fleft[0] = s.ftop[0];
+        wave_sync();
+        TT = s.ftop + 1;
+        LL = s.fleft + 1;
+    }
+    // DC value
+    int dcv = 0;
+    if (!chroma) {
+        const bool at = fl & 1, al = fl & 2;
+        int part = 0;
+        for (int i = lane; i < n; i += 64) part += (at ? TT[i] : 0) + (al ? LL[i] : 0);
+        const int sum = wave_sum(part);
+        if (at && al) dcv = (sum + n) >> (log2n + 1);
+        else if (at || al) dcv = (sum + (n >> 1)) >> log2n;
+        else dcv = 1 << (bd - 1);
+    }
+    for (int i = lane; i < nn; i += 64) {
+        const int x = i & (n - 1), y = i >> log2n;
+        const int r = cbf ? RS[(y0 + y) * st + x0 + x] : 0;
+        int pv;
+        if (nxn) {
+            pv = h264_pred_nxn(mode, x, y, n, TT, LL, dcv);
+        } else if (!chroma) {  // 16x16
+            if (mode == 0) pv = TT[x];
+            else if (mode == 1) pv = LL[y];
+            else if (mode == 2) pv = dcv;
+            else {
+                int H = 0, V = 0;
+                for (int k = 0; k < 8; k++) {
+                    H += (k + 1) * (TT[8 + k] - TT[6 - k]);
+                    V += (k + 1) * (LL[8 + k] - LL[6 - k]);
+                }
+                const int a = 16 * (LL[15] + TT[15]), b = (5 * H + 32) >> 6, cc = (5 * V + 32) >> 6;
+                pv = clip3(0, maxv, (a + b * (x - 7) + cc * (y - 7) + 16) >> 5);
+            }
+        } else {  // chroma 8x8 (mode: 0 DC, 1 horizontal, 2 vertical, 3 plane)
+            if (mode == 1) pv = LL[y];
+            else if (mode == 2) pv = TT[x];
+            else if (mode == 3) {
+                int H = 0, V = 0;
+                for (int k = 0; k < 4; k++) {
+                    H += (k + 1) * (TT[4 + k] - TT[2 - k]);
+                    V += (k + 1) * (LL[4 + k] - LL[2 - k]);
+                }
+                const int a = 16 * (LL[7] + TT[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+                pv = clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+            } else {
+                const bool at = fl & 1, al = fl & 2;
+                const int bx = x >> 2, by = y >> 2;
+                int st4 = 0, sl4 = 0;
+                for (int k = 0; k < 4; k++) { st4 += TT[bx * 4 + k]; sl4 += LL[by * 4 + k]; }
+                if (bx == by) pv = (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1)));
+                else if (bx) pv = at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1));
+                else pv = al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
+            }
+        }
+        P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
+    }
+    wave_sync();
+}
+
+template <typename Pel, bool kHevc>
+DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WLds& wl, uint32_t* prog) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t* masks = tu_masks(f, arena);
+    const uint32_t* rng = ctb_ranges(f, arena);
+    constexpr int kSlots = 2 * kK1Waves;
+    for (int row = w; row < f.ctb_h; row += kK1Waves) {
+        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + row % kSlots;
+        uint32_t seen = 0;
+        for (int cx = 0; cx < f.ctb_w; cx++) {
+            if (row > 0) {
+                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(cx + 2, f.ctb_w));
+                if (seen < need) {
+                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                }
+            }
+            const int cb = row * f.ctb_w + cx;
+            const uint32_t a = rng[2 * cb], b = rng[2 * cb + 1];
+            for (uint32_t t = a; t < b; t++) {
+                const h2j_tu tu = T[t];
+                if (tu.flags & H2J_TU_PCM) continue;  // written by K0
+                if (kHevc) hevc_predict_tu<Pel>(f, tu, masks[t], arena, wl.h5, lane);
+                else h264_predict_tu<Pel>(f, tu, masks[t], arena, wl.h4, lane);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon(const h2j_frame* frames, const h2j_tu* tus,
+                                                             uint8_t* arena) {
+    __shared__ K1WLds wl[kK1Waves];
+    __shared__ uint32_t prog[2 * kK1Waves];
+    const h2j_frame& f = frames[blockIdx.x];
+    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
+    __syncthreads();
+    const h2j_tu* T = tus + f.tu;
+    K1WLds& s = wl[threadIdx.x >> 6];
     if (f.codec == H2J_CODEC_HEVC) {
-        if (f.bit_depth == 8) hevc_recon_frame<uint8_t>(f, tus, coefs, C, S, sl, arena, s);
-        else hevc_recon_frame<uint16_t>(f, tus, coefs, C, S, sl, arena, s);
+        if (f.bit_depth == 8) predict_rows<uint8_t, true>(f, T, arena, s, prog);
+        else predict_rows<uint16_t, true>(f, T, arena, s, prog);
     } else if (f.codec == H2J_CODEC_H264) {
-        if (f.bit_depth == 8) h264_recon_frame<uint8_t>(f, tus, coefs, C, S, sl, arena, u.h4);
-        else h264_recon_frame<uint16_t>(f, tus, coefs, C, S, sl, arena, u.h4);
+        if (f.bit_depth == 8) predict_rows<uint8_t, false>(f, T, arena, s, prog);
+        else predict_rows<uint16_t, false>(f, T, arena, s, prog);
     }
 }
 
@@ -1396,8 +1495,14 @@ float h2j_gpu_event_elapsed_ms(void* a, void* b) {
 int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(h2j_k1_recon, dim3(b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
-                       b->slices, b->sl, b->arena);
+    const int waves = (b->max_ntu + kK0Tus - 1) / kK0Tus;
+    if (waves > 0) {
+        hipLaunchKernelGGL(h2j_k0_prep, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
+                           b->slices, b->sl, b->arena);
+        const int r = check(hipGetLastError(), "h2j_k0_prep");
+        if (r) return r;
+    }
+    hipLaunchKernelGGL(h2j_k1_recon, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
     return check(hipGetLastError(), "h2j_k1_recon");
 }
 

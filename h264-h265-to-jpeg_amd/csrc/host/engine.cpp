@@ -229,9 +229,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy) {
     if (nf == 0) return 0;
     s.frames.resize(nf);
     size_t ntu = 0, ncoef = 0, nctb = 0, nslice = 0, nsl = 0, nblk = 0;
-    int max_w = 0, max_h = 0, max_mcu = 0;
+    int max_w = 0, max_h = 0, max_mcu = 0, max_ntu = 0;
     for (int k = 0; k < nf; k++) {
         const FrameJob& j = jobs[s.live[k]];
+        max_ntu = std::max(max_ntu, static_cast<int>(j.tus.size()));
         h2j_frame f = j.hdr;
         f.tu = static_cast<uint32_t>(ntu);
         f.ntu = static_cast<uint32_t>(j.tus.size());
@@ -252,12 +253,14 @@ int Engine::enqueue(Slot& s, int stages, bool entropy) {
         max_mcu = std::max(max_mcu, mcu);
         nblk += static_cast<size_t>(mcu) * 6;
     }
-    // arena layout: [zeroed: maps + jstat][pic][pic2][jcoef]
+    // arena layout: [zeroed: maps + CTB TU ranges + jstat][pic][pic2][jcoef][res][aux]
     size_t off = 0;
     for (int k = 0; k < nf; k++) {
         h2j_frame& f = s.frames[k];
         f.maps = off;
         off = align_up(off + static_cast<size_t>(f.mw) * f.mh * 2, 256);
+        f.ctbrng = off;
+        off = align_up(off + static_cast<size_t>(f.ctb_w) * f.ctb_h * 8, 256);
     }
     s.jstat_base = off;
     s.jstat_stride = align_up(sizeof(h2j_jstat), 256);
@@ -286,6 +289,14 @@ int Engine::enqueue(Slot& s, int stages, bool entropy) {
         off = align_up(off + static_cast<size_t>(((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4)) * 6 * 64 * 2, 256);
     }
     s.jcoef_bytes = off - s.jcoef_base;
+    for (int k = 0; k < nf; k++) {
+        h2j_frame& f = s.frames[k];
+        const size_t ysz = static_cast<size_t>(f.width) * f.height;
+        f.res = off;
+        off = align_up(off + (ysz + ysz / 2) * 2, 256);
+        f.aux = off;
+        off = align_up(off + static_cast<size_t>(f.ntu) * 8, 256);
+    }
     const size_t arena_bytes = off;
     // input staging
     const size_t o_frames = 0;
@@ -331,6 +342,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy) {
     b.max_w = max_w;
     b.max_h = max_h;
     b.max_mcu = max_mcu;
+    b.max_ntu = max_ntu;
     b.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
     b.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);
     b.coefs = reinterpret_cast<const h2j_coef*>(din + o_coefs);

@@ -53,6 +53,7 @@ typedef struct {
     int32_t nframes;
     int32_t max_w, max_h;       /* max coded luma size over the batch */
     int32_t max_mcu;            /* max JPEG MCUs over the batch */
+    int32_t max_ntu;            /* max transform-block records over the batch */
     const h2j_frame *frames;
     const h2j_tu *tus;
     const h2j_coef *coefs;
@@ -67,8 +68,11 @@ typedef struct {
     uint64_t *seg_total;        /* device scalar: pool bytes used (16-byte units x16) */
 } h2j_gpu_batch;
 
-/* K1: dequantisation + inverse transform + intra prediction (HEVC and H.264),
- * writes the pre-loop-filter picture to frame.pic and the deblocking maps. */
+/* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
+ * deblocking maps, PCM samples and residuals (dequantisation + inverse
+ * transform) into frame.res; K1 (CTB-row wavefront, one workgroup per
+ * picture) intra prediction + residual -> the pre-loop-filter picture in
+ * frame.pic.  HEVC and H.264. */
 int h2j_gpu_recon(const h2j_gpu_batch *b, void *stream);
 /* K2: deblocking (vertical edges, then horizontal edges), in place on frame.pic */
 int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);

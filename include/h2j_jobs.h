@@ -101,6 +101,9 @@ typedef struct {
     uint64_t maps;                  /* per-4x4 deblocking maps: flags (u8) then qp (i8) */
     uint64_t jcoef;                 /* JPEG coefficients int16 [mcu][6][64] */
     uint64_t jstat;                 /* JPEG per-frame stats (h2j_jstat) */
+    uint64_t res;                   /* int16 residual planes (K0 -> K1), pic geometry */
+    uint64_t aux;                   /* K0 -> K1: uint64 reference-availability mask per TU */
+    uint64_t ctbrng;                /* K0 -> K1: uint32 [first, end) TU range per CTB (zeroed) */
     int32_t pic_stride[3];          /* elements */
     int32_t pic_off[3];             /* element offset of each plane inside pic / pic2 */
     int32_t mw, mh;                 /* 4x4 map dims */
