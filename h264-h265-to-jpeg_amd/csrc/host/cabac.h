@@ -1,7 +1,5 @@
 // Context-adaptive binary arithmetic decoder (H.264 9.3.3.2 / H.265 9.3.4.3)
-// for the host entropy threads.  Byte-wise refill with a 16-bit value
-// register holding the 9-bit offset plus 7 look-ahead bits, so the common
-// MPS path is one compare and no bitstream access.
+// for the host entropy threads.
 #pragma once
 #include <cstdint>
 
@@ -10,6 +8,9 @@ namespace h2j {
 extern const uint8_t kCabacLps[64][4];
 extern const uint8_t kCabacTransLps[64];
 extern const uint8_t kCabacRenorm[32];
+// next context state ((pStateIdx << 1) | valMps) after an MPS / LPS bin
+extern const uint16_t kCabacNextMps[128];
+extern const uint16_t kCabacNextLps[128];
 
 struct CabacCtx {
     uint8_t state;  // (pStateIdx << 1) | valMps
@@ -26,61 +27,41 @@ inline uint8_t cabac_init_state(int m, int n, int qp) {
     return static_cast<uint8_t>((st << 1) | mps);
 }
 
+// Branch-free on the MPS/LPS decision: the offset lives at the top of a
+// 64-bit window (value = offset << bits | look-ahead), renormalisation is a
+// count-leading-zeros shift of the range and a decrement of `bits`, and the
+// window is refilled 32 bits at a time.
 class Cabac {
 public:
     void init(const uint8_t* p, const uint8_t* end) {
         cur_ = p;
         end_ = end;
         range_ = 510;
-        bits_needed_ = 8;
         value_ = 0;
-        if (cur_ < end_) { value_ = static_cast<uint32_t>(*cur_++) << 8; bits_needed_ -= 8; }
-        if (cur_ < end_) { value_ |= *cur_++; bits_needed_ -= 8; }
+        for (int i = 0; i < 4; i++) value_ = (value_ << 8) | (cur_ < end_ ? *cur_++ : 0u);
+        bits_ = 32 - 9;
     }
-    inline int decision(uint8_t& ctx) {
-        int s = ctx >> 1;
-        int mps = ctx & 1;
-        uint32_t lps = kCabacLps[s][(range_ >> 6) - 4];
-        range_ -= lps;
-        uint32_t scaled = range_ << 7;
-        if (value_ < scaled) {
-            ctx = static_cast<uint8_t>(((s + (s < 62)) << 1) | mps);
-            if (scaled < (256u << 7)) {
-                range_ = scaled >> 6;
-                value_ <<= 1;
-                if (++bits_needed_ == 0) {
-                    bits_needed_ = -8;
-                    if (cur_ < end_) value_ |= *cur_++;
-                }
-            }
-            return mps;
-        }
-        value_ -= scaled;
-        int nb = kCabacRenorm[lps >> 3];
-        value_ <<= nb;
-        range_ = lps << nb;
-        int bin = !mps;
-        if (s == 0) mps = !mps;
-        ctx = static_cast<uint8_t>((kCabacTransLps[s] << 1) | mps);
-        bits_needed_ += nb;
-        if (bits_needed_ >= 0) {
-            if (cur_ < end_) value_ |= static_cast<uint32_t>(*cur_++) << bits_needed_;
-            bits_needed_ -= 8;
-        }
-        return bin;
+    inline int decision(uint16_t& ctx) {
+        const unsigned st = ctx;
+        const uint32_t lps = kCabacLps[st >> 1][(range_ >> 6) & 3];
+        const uint32_t rmps = range_ - lps;
+        const uint64_t scaled = static_cast<uint64_t>(rmps) << bits_;
+        const bool is_lps = value_ >= scaled;
+        value_ -= is_lps ? scaled : 0;
+        const uint32_t r = is_lps ? lps : rmps;
+        ctx = is_lps ? kCabacNextLps[st] : kCabacNextMps[st];
+        const int sh = __builtin_clz(r) - 23;
+        range_ = r << sh;
+        bits_ -= sh;
+        if (bits_ < 0) refill();
+        return static_cast<int>(st & 1) ^ static_cast<int>(is_lps);
     }
     inline int bypass() {
-        value_ <<= 1;
-        if (++bits_needed_ >= 0) {
-            bits_needed_ = -8;
-            if (cur_ < end_) value_ |= *cur_++;
-        }
-        uint32_t scaled = range_ << 7;
-        if (value_ >= scaled) {
-            value_ -= scaled;
-            return 1;
-        }
-        return 0;
+        if (--bits_ < 0) refill();
+        const uint64_t scaled = static_cast<uint64_t>(range_) << bits_;
+        const bool one = value_ >= scaled;
+        value_ -= one ? scaled : 0;
+        return one;
     }
     inline uint32_t bypass_bits(int n) {
         uint32_t v = 0;
@@ -89,30 +70,39 @@ public:
     }
     inline int terminate() {
         range_ -= 2;
-        uint32_t scaled = range_ << 7;
+        const uint64_t scaled = static_cast<uint64_t>(range_) << bits_;
         if (value_ >= scaled) return 1;
-        if (scaled < (256u << 7)) {
-            range_ = scaled >> 6;
-            value_ <<= 1;
-            if (++bits_needed_ == 0) {
-                bits_needed_ = -8;
-                if (cur_ < end_) value_ |= *cur_++;
-            }
+        if (range_ < 256) {
+            range_ <<= 1;
+            if (--bits_ < 0) refill();
         }
         return 0;
     }
-    // After terminate() returned 1 the arithmetic decoder has consumed
-    // exactly through the flush's final '1' bit; the next byte-aligned
-    // syntax (pcm_sample, next substream) starts at cur_.
-    const uint8_t* aligned_pos() const { return cur_; }
-    bool overrun() const { return cur_ >= end_ && bits_needed_ > -8 + 0 && false; }
+    // After terminate() returned 1 the arithmetic decoder (9.3.4.3.5) has
+    // consumed exactly through the flush's final '1' bit; the next
+    // byte-aligned syntax (pcm_sample, next substream) starts at the first
+    // byte boundary after it.
+    const uint8_t* aligned_pos() const { return cur_ - (bits_ >> 3); }
 
 private:
+    void refill() {
+        uint32_t w;
+        if (end_ - cur_ >= 4) {
+            w = (static_cast<uint32_t>(cur_[0]) << 24) | (static_cast<uint32_t>(cur_[1]) << 16) |
+                (static_cast<uint32_t>(cur_[2]) << 8) | cur_[3];
+            cur_ += 4;
+        } else {
+            w = 0;
+            for (int i = 0; i < 4; i++) w = (w << 8) | (cur_ < end_ ? *cur_++ : 0u);
+        }
+        value_ = (value_ << 32) | w;
+        bits_ += 32;
+    }
     const uint8_t* cur_ = nullptr;
     const uint8_t* end_ = nullptr;
+    uint64_t value_ = 0;
     uint32_t range_ = 510;
-    uint32_t value_ = 0;
-    int bits_needed_ = 0;
+    int bits_ = 0;
 };
 
 }  // namespace h2j

@@ -280,7 +280,7 @@ private:
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
-    uint8_t ctx_[460];
+    uint16_t ctx_[460];  // 16-bit: stores must not alias the engine state
     int err_ = 0;
 
     int dec(int c) { return cc_.decision(ctx_[c]); }
@@ -299,9 +299,13 @@ private:
         return (dx == 0 && dy == 0) ? &mb_[mby_ * mbw_ + mbx_] : nb(dx, dy);
     }
     int cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const;
-    int residual_block(int cat, int cbf_inc, int max_num, int* out);
+    // residual_block_cabac (7.3.5.3.3): number of non-zero levels (0: coded_block_flag 0);
+    // scan indices in pos[], levels in lvl[]
+    int residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl);
     void decode_mb();
     void emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos, bool pcm);
+    // sparse record: entries already (pos << 16) | uint16 level
+    void emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n);
 };
 
 int H264Parser::cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const {
@@ -317,63 +321,86 @@ int H264Parser::cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const {
     return 0;
 }
 
-int H264Parser::residual_block(int cat, int cbf_inc, int max_num, int* out) {
+int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl) {
     static const int kCbfOff[5] = {0, 4, 8, 12, 16};
     static const int kSigOff[6] = {0, 15, 29, 44, 47, 0};
     static const int kAbsOff[6] = {0, 10, 20, 30, 39, 0};
-    std::memset(out, 0, sizeof(int) * static_cast<size_t>(max_num));
-    if (cat != 5 && !dec(85 + kCbfOff[cat] + cbf_inc)) return 0;
-    int sig[64], nsig = 0;
+    Cabac cc = cc_;  // engine state in registers for the block
+    uint16_t* const ctx = ctx_;
+    if (cat != 5 && !cc.decision(ctx[85 + kCbfOff[cat] + cbf_inc])) {
+        cc_ = cc;
+        return 0;
+    }
+    int nsig = 0;
     bool last_found = false;
-    for (int i = 0; i < max_num - 1; i++) {
-        int sc, lc;
-        if (cat == 5) {
-            sc = 402 + kSig8x8[i];
-            lc = 417 + kLast8x8[i];
-        } else if (cat == 3) {
+    if (cat == 5) {
+        for (int i = 0; i < max_num - 1; i++)
+            if (cc.decision(ctx[402 + kSig8x8[i]])) {
+                pos[nsig++] = static_cast<uint8_t>(i);
+                if (cc.decision(ctx[417 + kLast8x8[i]])) { last_found = true; break; }
+            }
+    } else if (cat == 3) {
+        for (int i = 0; i < max_num - 1; i++) {
             const int inc = i < 2 ? i : 2;
-            sc = 105 + kSigOff[3] + inc;
-            lc = 166 + kSigOff[3] + inc;
-        } else {
-            sc = 105 + kSigOff[cat] + i;
-            lc = 166 + kSigOff[cat] + i;
-        }
-        if (dec(sc)) {
-            sig[nsig++] = i;
-            if (dec(lc)) {
-                last_found = true;
-                break;
+            if (cc.decision(ctx[105 + kSigOff[3] + inc])) {
+                pos[nsig++] = static_cast<uint8_t>(i);
+                if (cc.decision(ctx[166 + kSigOff[3] + inc])) { last_found = true; break; }
             }
         }
+    } else {
+        uint16_t* const sctx = ctx + 105 + kSigOff[cat];
+        uint16_t* const lctx = ctx + 166 + kSigOff[cat];
+        for (int i = 0; i < max_num - 1; i++)
+            if (cc.decision(sctx[i])) {
+                pos[nsig++] = static_cast<uint8_t>(i);
+                if (cc.decision(lctx[i])) { last_found = true; break; }
+            }
     }
-    if (!last_found) sig[nsig++] = max_num - 1;
+    if (!last_found) pos[nsig++] = static_cast<uint8_t>(max_num - 1);
     int eq1 = 0, gt1 = 0;
-    const int absb = cat == 5 ? 426 : 227 + kAbsOff[cat];
+    uint16_t* const absc = ctx + (cat == 5 ? 426 : 227 + kAbsOff[cat]);
     const int gt_cap = 4 - (cat == 3 ? 1 : 0);
     for (int k = nsig - 1; k >= 0; k--) {
         const int inc = gt1 ? 0 : std::min(4, 1 + eq1);
         int v;
-        if (!dec(absb + inc)) {
+        if (!cc.decision(absc[inc])) {
             v = 1;
+            eq1++;
         } else {
-            const int inc2 = 5 + std::min(gt_cap, gt1);
+            uint16_t& c2 = absc[5 + std::min(gt_cap, gt1)];
             int p = 1;
-            while (p < 14 && dec(absb + inc2)) p++;
+            while (p < 14 && cc.decision(c2)) p++;
             v = p + 1;
             if (p == 14) {
                 int kk = 0;
-                while (cc_.bypass()) {
+                while (cc.bypass()) {
                     v += 1 << kk;
-                    if (++kk > 24) { err_ = -30; return 1; }
+                    if (++kk > 24) { err_ = -30; cc_ = cc; return nsig; }
                 }
-                while (kk--) v += cc_.bypass() << kk;
+                while (kk--) v += cc.bypass() << kk;
             }
+            gt1++;
         }
-        if (v == 1) eq1++;
-        else gt1++;
-        out[sig[k]] = cc_.bypass() ? -v : v;
+        lvl[k] = cc.bypass() ? -v : v;
     }
-    return 1;
+    cc_ = cc;
+    return nsig;
+}
+
+void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n) {
+    h2j_tu t;
+    t.x = static_cast<uint16_t>(x);
+    t.y = static_cast<uint16_t>(y);
+    t.log2n = static_cast<uint8_t>(log2n);
+    t.c = static_cast<uint8_t>(c);
+    t.mode = static_cast<uint8_t>(mode);
+    t.qp = static_cast<int8_t>(qp);
+    t.qpy = static_cast<int8_t>(qp_);
+    t.coef = static_cast<uint32_t>(job_.coefs.size());
+    job_.coefs.insert(job_.coefs.end(), e, e + n);
+    t.ncoef = static_cast<uint16_t>(n);
+    t.flags = n ? H2J_TU_CBF : 0;
+    job_.tus.push_back(t);
 }
 
 void H264Parser::emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos,
@@ -536,36 +563,39 @@ void H264Parser::decode_mb() {
     rec.qp = static_cast<int8_t>(qp_);
     if (m.t8x8) rec.mbflags |= 2;
     const int qpl = qp_ + qpbd_;
-    // ---- residual + record emission ----
-    int coef[64];
-    int mblv[256];
+    // ---- residual + record emission (sparse: (raster pos << 16) | level) ----
+    uint8_t pos[64];
+    int lvl[64];
+    uint32_t mbe[256];  // I16x16: the whole macroblock's levels
+    int nmb = 0;
+    auto entry = [](int p, int v) { return (static_cast<uint32_t>(p) << 16) | static_cast<uint16_t>(v); };
     if (is16) {
-        std::memset(mblv, 0, sizeof(mblv));
         Mb* A = nb(-1, 0);
         Mb* B = nb(0, -1);
-        m.cbf_dc[0] = static_cast<uint8_t>(residual_block(0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, coef));
-        for (int k = 0; k < 16; k++) {
-            const int r = kZz4[k];  // raster index of the DC matrix = 4x4 block position
-            mblv[(r >> 2) * 4 * 16 + (r & 3) * 4] = coef[k];
+        const int n = residual_block(0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, pos, lvl);
+        m.cbf_dc[0] = static_cast<uint8_t>(n != 0);
+        for (int k = 0; k < n; k++) {
+            const int r = kZz4[pos[k]];  // raster index of the DC matrix = 4x4 block position
+            mbe[nmb++] = entry((r >> 2) * 4 * 16 + (r & 3) * 4, lvl[k]);
         }
     }
     for (int b8 = 0; b8 < 4 && !err_; b8++) {
         const bool coded = (m.cbp >> b8) & 1;
         if (m.t8x8) {
-            int lv[64];
-            std::memset(lv, 0, sizeof(lv));
+            uint32_t e[64];
+            int ne = 0;
             if (coded) {
-                residual_block(5, 0, 64, coef);
-                for (int k = 0; k < 64; k++) lv[kZz8[k]] = coef[k];
+                const int n = residual_block(5, 0, 64, pos, lvl);
+                for (int k = 0; k < n; k++) e[ne++] = entry(kZz8[pos[k]], lvl[k]);
                 for (int k = 0; k < 4; k++) m.cbf[b8 * 4 + k] = 1;
             }
-            emit(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], 0, qpl, lv, 64, false);
+            emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
             continue;
         }
         for (int b4 = 0; b4 < 4; b4++) {
             const int blk = b8 * 4 + b4, bx = kBlkX[blk], by = kBlkY[blk];
-            int lv[16];
-            std::memset(lv, 0, sizeof(lv));
+            uint32_t e[16];
+            int ne = 0;
             if (coded) {
                 int nblk;
                 Mb* A = nb_blk(bx - 1, by, &nblk);
@@ -573,31 +603,32 @@ void H264Parser::decode_mb() {
                 Mb* B = nb_blk(bx, by - 1, &nblk);
                 const int cb = cbf_cond(is16 ? 1 : 2, B, nblk, 0);
                 if (is16) {
-                    m.cbf[blk] = static_cast<uint8_t>(residual_block(1, ca + 2 * cb, 15, coef));
-                    for (int k = 0; k < 15; k++) lv[kZz4[k + 1]] = coef[k];
+                    const int n = residual_block(1, ca + 2 * cb, 15, pos, lvl);
+                    m.cbf[blk] = static_cast<uint8_t>(n != 0);
+                    for (int k = 0; k < n; k++) {
+                        const int r = kZz4[pos[k] + 1];
+                        mbe[nmb++] = entry((by * 4 + (r >> 2)) * 16 + bx * 4 + (r & 3), lvl[k]);
+                    }
                 } else {
-                    m.cbf[blk] = static_cast<uint8_t>(residual_block(2, ca + 2 * cb, 16, coef));
-                    for (int k = 0; k < 16; k++) lv[kZz4[k]] = coef[k];
+                    const int n = residual_block(2, ca + 2 * cb, 16, pos, lvl);
+                    m.cbf[blk] = static_cast<uint8_t>(n != 0);
+                    for (int k = 0; k < n; k++) e[ne++] = entry(kZz4[pos[k]], lvl[k]);
                 }
             }
-            if (is16) {
-                for (int i = 1; i < 16; i++) mblv[(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)] = lv[i];
-            } else {
-                emit(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], 0, qpl, lv, 16, false);
-            }
+            if (!is16) emit_sparse(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
         }
     }
-    if (is16) emit(gx, gy, 4, 0, (m.mb_type - 1) % 4, 0, qpl, mblv, 256, false);
+    if (is16) emit_sparse(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
     // chroma
-    int clv[2][64];
-    std::memset(clv, 0, sizeof(clv));
+    uint32_t ce[2][64];
+    int nce[2] = {0, 0};
     if (m.cbp >> 4) {
         for (int c = 0; c < 2; c++) {
             Mb* A = nb(-1, 0);
             Mb* B = nb(0, -1);
-            m.cbf_dc[1 + c] =
-                static_cast<uint8_t>(residual_block(3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, coef));
-            for (int k = 0; k < 4; k++) clv[c][(k >> 1) * 4 * 8 + (k & 1) * 4] = coef[k];
+            const int n = residual_block(3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, pos, lvl);
+            m.cbf_dc[1 + c] = static_cast<uint8_t>(n != 0);
+            for (int k = 0; k < n; k++) ce[c][nce[c]++] = entry((pos[k] >> 1) * 4 * 8 + (pos[k] & 1) * 4, lvl[k]);
         }
     }
     if ((m.cbp >> 4) == 2) {
@@ -606,17 +637,18 @@ void H264Parser::decode_mb() {
                 const int bx = b4 & 1, by = b4 >> 1;
                 const int ca = bx ? m.cbf_c[c][b4 - 1] : cbf_cond(4, nb(-1, 0), b4 + 1, c);
                 const int cb = by ? m.cbf_c[c][b4 - 2] : cbf_cond(4, nb(0, -1), b4 + 2, c);
-                m.cbf_c[c][b4] = static_cast<uint8_t>(residual_block(4, ca + 2 * cb, 15, coef));
-                for (int k = 0; k < 15; k++) {
-                    const int r = kZz4[k + 1];
-                    clv[c][(by * 4 + (r >> 2)) * 8 + bx * 4 + (r & 3)] = coef[k];
+                const int n = residual_block(4, ca + 2 * cb, 15, pos, lvl);
+                m.cbf_c[c][b4] = static_cast<uint8_t>(n != 0);
+                for (int k = 0; k < n; k++) {
+                    const int r = kZz4[pos[k] + 1];
+                    ce[c][nce[c]++] = entry((by * 4 + (r >> 2)) * 8 + bx * 4 + (r & 3), lvl[k]);
                 }
             }
     }
     for (int c = 0; c < 2; c++) {
         const int off = c == 0 ? p_->cqp : p_->cqp2;
         const int qpi = std::max(-qpbd_, std::min(51, qp_ + off));
-        emit(gx / 2, gy / 2, 3, 1 + c, m.cpm, 0, chroma_qp_264(qpi) + qpbd_, clv[c], 64, false);
+        emit_sparse(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
     }
 }
 

@@ -290,6 +290,9 @@ int parse_pps(BitReader& b, Pps* tab) {
 uint8_t g_scan_diag[4][64][2], g_scan_hor[4][64][2], g_scan_ver[4][64][2];
 uint8_t g_diag_pos4[16];  // raster (y*4+x) of 4x4 diag scan
 uint8_t g_diag_pos8[64];
+// context index (C_SIG-relative) of sig_coeff_flag (9.3.4.2.5):
+// [chroma][log2n-2][scanIdx][prevCsbf][subblock != 0][scan pos in subblock]
+uint8_t g_sigctx[2][4][3][4][2][16];
 bool g_scans_ready = false;
 
 void init_scans() {
@@ -322,6 +325,34 @@ void init_scans() {
                 g_scan_ver[l][i][1] = static_cast<uint8_t>(y);
             }
     }
+    for (int c = 0; c < 2; c++)
+        for (int lsb = 0; lsb < 4; lsb++)
+            for (int si = 0; si < 3; si++)
+                for (int pc = 0; pc < 4; pc++)
+                    for (int sb = 0; sb < 2; sb++)
+                        for (int nn = 0; nn < 16; nn++) {
+                            const uint8_t(*sc)[64][2] = si == 0 ? g_scan_diag : (si == 1 ? g_scan_hor : g_scan_ver);
+                            const int log2n = lsb + 2, xp = sc[2][nn][0], yp = sc[2][nn][1];
+                            int sigCtx;
+                            if (log2n == 2) {
+                                static const uint8_t m[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+                                sigCtx = m[(yp << 2) + xp];
+                            } else if (!sb && xp + yp == 0) {
+                                sigCtx = 0;
+                            } else {
+                                if (pc == 0) sigCtx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+                                else if (pc == 1) sigCtx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+                                else if (pc == 2) sigCtx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+                                else sigCtx = 2;
+                                if (c == 0) {
+                                    if (sb) sigCtx += 3;
+                                    sigCtx += (log2n == 3) ? ((si == 0) ? 9 : 15) : 21;
+                                } else {
+                                    sigCtx += (log2n == 3) ? 9 : 12;
+                                }
+                            }
+                            g_sigctx[c][lsb][si][pc][sb][nn] = static_cast<uint8_t>(C_SIG + (c == 0 ? sigCtx : 27 + sigCtx));
+                        }
     for (int i = 0; i < 16; i++) g_diag_pos4[i] = static_cast<uint8_t>(g_scan_diag[2][i][1] * 4 + g_scan_diag[2][i][0]);
     for (int i = 0; i < 64; i++) g_diag_pos8[i] = static_cast<uint8_t>(g_scan_diag[3][i][1] * 8 + g_scan_diag[3][i][0]);
     g_scans_ready = true;
@@ -360,7 +391,7 @@ private:
     int cur_idx_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
-    uint8_t ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];
+    uint16_t ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];  // 16-bit: stores must not alias the engine state
     bool have_ds_ = false;
     int qp_y_ = 0, qg_pred_ = 0, qpd_val_ = 0, last_cu_qp_ = 0;
     bool is_qpd_coded_ = false, first_qg_ = true;
@@ -731,8 +762,13 @@ uint8_t HevcParser::edge_flags(int x0, int y0) const {
 }
 
 void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
+    // hot path: engine state in a local (registers), contexts by pointer,
+    // coefficients into a local buffer appended once per TU
+    Cabac cc = cc_;
+    uint16_t* const ctx = ctx_;
     const int n = 1 << log2n;
-    if (p_->transform_skip && !cu_bypass_ && log2n <= 2 && dec(C_TSKIP + (c ? 1 : 0))) tu.flags |= H2J_TU_TSKIP;
+    if (p_->transform_skip && !cu_bypass_ && log2n <= 2 && cc.decision(ctx[C_TSKIP + (c ? 1 : 0)]))
+        tu.flags |= H2J_TU_TSKIP;
     // last_sig_coeff prefix/suffix
     int off, shift;
     if (c == 0) {
@@ -744,15 +780,15 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     }
     const int maxp = (log2n << 1) - 1;
     int lx = 0, ly = 0;
-    while (lx < maxp && dec(C_LAST_X + off + (lx >> shift))) lx++;
-    while (ly < maxp && dec(C_LAST_Y + off + (ly >> shift))) ly++;
+    while (lx < maxp && cc.decision(ctx[C_LAST_X + off + (lx >> shift)])) lx++;
+    while (ly < maxp && cc.decision(ctx[C_LAST_Y + off + (ly >> shift)])) ly++;
     if (lx > 3) {
         int nb = (lx >> 1) - 1;
-        lx = (1 << nb) * (2 + (lx & 1)) + static_cast<int>(cc_.bypass_bits(nb));
+        lx = (1 << nb) * (2 + (lx & 1)) + static_cast<int>(cc.bypass_bits(nb));
     }
     if (ly > 3) {
         int nb = (ly >> 1) - 1;
-        ly = (1 << nb) * (2 + (ly & 1)) + static_cast<int>(cc_.bypass_bits(nb));
+        ly = (1 << nb) * (2 + (ly & 1)) + static_cast<int>(cc.bypass_bits(nb));
     }
     int scanIdx = 0;
     if (log2n == 2 || (log2n == 3 && c == 0)) {
@@ -760,7 +796,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         else if (pred_mode >= 22 && pred_mode <= 30) scanIdx = 1;
     }
     if (scanIdx == 2) std::swap(lx, ly);
-    if (lx >= n || ly >= n) { err_ = -20; return; }
+    if (lx >= n || ly >= n) { err_ = -20; cc_ = cc; return; }
     const uint8_t(*sc)[64][2] = scanIdx == 0 ? g_scan_diag : (scanIdx == 1 ? g_scan_hor : g_scan_ver);
     const int lsb = log2n - 2;
     // locate last position in scan order
@@ -778,55 +814,41 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     int greater1_ctx = 1;
     const bool sdh = p_->sign_hiding != 0;
     const int sbw = 1 << lsb;
-    const uint32_t base = static_cast<uint32_t>(job_.coefs.size());
+    uint32_t out[32 * 32];
+    int nout = 0;
+    const uint8_t(*const sigtab)[2][16] = g_sigctx[c ? 1 : 0][lsb][scanIdx];
+    uint16_t* const gt1ctx = ctx + C_GT1 + (c ? 16 : 0);
     for (int i = lastSub; i >= 0; i--) {
         const int xs = sc[lsb][i][0], ys = sc[lsb][i][1];
         bool infer_dc = false;
         if (i < lastSub && i > 0) {
             int csr = (xs + 1 < sbw) ? csbf[xs + 1][ys] : 0;
             int csb = (ys + 1 < sbw) ? csbf[xs][ys + 1] : 0;
-            csbf[xs][ys] = static_cast<uint8_t>(dec(C_CSBF + (csr | csb) + (c ? 2 : 0)));
+            csbf[xs][ys] = static_cast<uint8_t>(cc.decision(ctx[C_CSBF + (csr | csb) + (c ? 2 : 0)]));
             infer_dc = true;
         } else {
             csbf[xs][ys] = 1;
         }
-        uint16_t sigmask = 0;  // bit nn
+        unsigned sigmask = 0;  // bit nn
         int nstart = 15;
         if (i == lastSub) {
             nstart = lastPos - 1;
-            sigmask = static_cast<uint16_t>(1u << lastPos);
+            sigmask = 1u << lastPos;
         }
         if (csbf[xs][ys]) {
             int prevCsbf = 0;
             if (xs + 1 < sbw) prevCsbf |= csbf[xs + 1][ys];
             if (ys + 1 < sbw) prevCsbf |= csbf[xs][ys + 1] << 1;
-            for (int nn = nstart; nn >= 0; nn--) {
-                const int xp = sc[2][nn][0], yp = sc[2][nn][1];
-                if (nn > 0 || !infer_dc) {
-                    int sigCtx;
-                    const int xC = (xs << 2) + xp, yC = (ys << 2) + yp;
-                    if (log2n == 2) {
-                        static const uint8_t m[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-                        sigCtx = m[(yC << 2) + xC];
-                    } else if (xC + yC == 0) {
-                        sigCtx = 0;
-                    } else {
-                        if (prevCsbf == 0) sigCtx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-                        else if (prevCsbf == 1) sigCtx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
-                        else if (prevCsbf == 2) sigCtx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
-                        else sigCtx = 2;
-                        if (c == 0) {
-                            if (xs > 0 || ys > 0) sigCtx += 3;
-                            sigCtx += (log2n == 3) ? ((scanIdx == 0) ? 9 : 15) : 21;
-                        } else {
-                            sigCtx += (log2n == 3) ? 9 : 12;
-                        }
-                    }
-                    if (dec(C_SIG + (c == 0 ? sigCtx : 27 + sigCtx))) {
-                        sigmask |= static_cast<uint16_t>(1u << nn);
-                        infer_dc = false;
-                    }
-                } else if (infer_dc) {
+            const uint8_t* sig = sigtab[prevCsbf][(xs | ys) ? 1 : 0];
+            for (int nn = nstart; nn > 0; nn--)
+                if (cc.decision(ctx[sig[nn]])) {
+                    sigmask |= 1u << nn;
+                    infer_dc = false;
+                }
+            if (nstart >= 0) {
+                if (!infer_dc) {
+                    if (cc.decision(ctx[sig[0]])) sigmask |= 1u;
+                } else {
                     sigmask |= 1u;  // nn == 0 inferred
                 }
             }
@@ -836,43 +858,45 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         int ctxSet = (i == 0 || c > 0) ? 0 : 2;
         if (greater1_ctx == 0) ctxSet++;
         greater1_ctx = 1;
-        int g1mask = 0, numG1 = 0, lastG1 = -1, firstSig = 16, lastSig = -1;
-        for (int nn = 15; nn >= 0; nn--) {
-            if (!((sigmask >> nn) & 1)) continue;
-            if (numG1 < 8) {
-                int flag = dec(C_GT1 + ctxSet * 4 + greater1_ctx + (c ? 16 : 0));
-                numG1++;
-                if (flag) {
-                    g1mask |= 1 << nn;
-                    greater1_ctx = 0;
-                    if (lastG1 == -1) lastG1 = nn;
-                } else if (greater1_ctx > 0 && greater1_ctx < 3) {
-                    greater1_ctx++;
-                }
+        unsigned g1mask = 0;
+        int numG1 = 0, lastG1 = -1;
+        const int lastSig = 31 - __builtin_clz(sigmask), firstSig = __builtin_ctz(sigmask);
+        for (unsigned m = sigmask; m && numG1 < 8; numG1++) {
+            const int nn = 31 - __builtin_clz(m);
+            m &= ~(1u << nn);
+            if (cc.decision(gt1ctx[ctxSet * 4 + greater1_ctx])) {
+                g1mask |= 1u << nn;
+                greater1_ctx = 0;
+                if (lastG1 == -1) lastG1 = nn;
+            } else if (greater1_ctx > 0 && greater1_ctx < 3) {
+                greater1_ctx++;
             }
-            if (lastSig == -1) lastSig = nn;
-            firstSig = nn;
         }
         const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
         int g2 = 0;
-        if (lastG1 != -1) g2 = dec(C_GT2 + ctxSet + (c ? 4 : 0));
-        int signs = 0;
-        for (int nn = 15; nn >= 0; nn--)
-            if (((sigmask >> nn) & 1) && (!sdh || !hidden || nn != firstSig)) signs |= cc_.bypass() << nn;
+        if (lastG1 != -1) g2 = cc.decision(ctx[C_GT2 + ctxSet + (c ? 4 : 0)]);
+        unsigned signs = 0;
+        const unsigned signed_mask = (sdh && hidden) ? (sigmask & ~(1u << firstSig)) : sigmask;
+        for (unsigned m = signed_mask; m;) {
+            const int nn = 31 - __builtin_clz(m);
+            m &= ~(1u << nn);
+            signs |= static_cast<unsigned>(cc.bypass()) << nn;
+        }
         int numSig = 0, sumAbs = 0, rice = 0;
-        for (int nn = 15; nn >= 0; nn--) {
-            if (!((sigmask >> nn) & 1)) continue;
+        for (unsigned m = sigmask; m;) {
+            const int nn = 31 - __builtin_clz(m);
+            m &= ~(1u << nn);
             int baseL = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0);
             int lvl = baseL;
             if (baseL == ((numSig < 8) ? ((nn == lastG1) ? 3 : 2) : 1)) {
                 int prefix = 0;
-                while (prefix < 32 && cc_.bypass()) prefix++;
+                while (prefix < 32 && cc.bypass()) prefix++;
                 int rem;
-                if (prefix < 3) rem = (prefix << rice) + static_cast<int>(cc_.bypass_bits(rice));
+                if (prefix < 3) rem = (prefix << rice) + static_cast<int>(cc.bypass_bits(rice));
                 else {
                     int pm3 = prefix - 3;
-                    if (pm3 + rice > 30) { err_ = -21; return; }
-                    rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc_.bypass_bits(pm3 + rice));
+                    if (pm3 + rice > 30) { err_ = -21; cc_ = cc; return; }
+                    rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc.bypass_bits(pm3 + rice));
                 }
                 lvl = baseL + rem;
                 if (lvl > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
@@ -885,12 +909,15 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
             const int xC = (xs << 2) + sc[2][nn][0], yC = (ys << 2) + sc[2][nn][1];
-            job_.coefs.push_back((static_cast<uint32_t>(yC * n + xC) << 16) | static_cast<uint16_t>(v));
+            out[nout++] = (static_cast<uint32_t>(yC * n + xC) << 16) | static_cast<uint16_t>(v);
             numSig++;
         }
     }
+    cc_ = cc;
+    const uint32_t base = static_cast<uint32_t>(job_.coefs.size());
+    job_.coefs.insert(job_.coefs.end(), out, out + nout);
     tu.coef = base - job_.hdr.coef;
-    tu.ncoef = static_cast<uint16_t>(job_.coefs.size() - base);
+    tu.ncoef = static_cast<uint16_t>(nout);
     tu.flags |= H2J_TU_CBF;
 }
 
@@ -1156,10 +1183,10 @@ void HevcParser::ctb_start_contexts(int rs, int ts, bool first) {
         init_contexts(cur_->slice_qp);
     } else if (row_start) {
         const int xr = x0 + ctbs, yr = y0 - ctbs;
-        if (xr < W && yr >= 0 && same_region(x0, y0, xr, yr)) std::memcpy(ctx_, ctx_wpp_, NUM_CTX);
+        if (xr < W && yr >= 0 && same_region(x0, y0, xr, yr)) std::memcpy(ctx_, ctx_wpp_, sizeof(ctx_));
         else init_contexts(cur_->slice_qp);
     } else if (cur_->dependent && have_ds_) {
-        std::memcpy(ctx_, ctx_ds_, NUM_CTX);
+        std::memcpy(ctx_, ctx_ds_, sizeof(ctx_));
     } else {
         init_contexts(cur_->slice_qp);
     }
@@ -1190,7 +1217,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         int endf = cc_.terminate();
         if (p_->wpp) {
             for (size_t i = 0; i + 1 < col_bd_.size(); i++)
-                if (rx == col_bd_[i] + 1 && col_bd_[i] + 1 < col_bd_[i + 1]) std::memcpy(ctx_wpp_, ctx_, NUM_CTX);
+                if (rx == col_bd_[i] + 1 && col_bd_[i] + 1 < col_bd_[i + 1]) std::memcpy(ctx_wpp_, ctx_, sizeof(ctx_));
         }
         ts++;
         if (endf) break;
@@ -1207,7 +1234,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         }
         rs = nrs;
     }
-    std::memcpy(ctx_ds_, ctx_, NUM_CTX);
+    std::memcpy(ctx_ds_, ctx_, sizeof(ctx_));
     have_ds_ = true;
     return 0;
 }
