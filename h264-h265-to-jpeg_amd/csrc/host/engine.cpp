@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -215,13 +216,14 @@ struct Engine {
     }
 
     // Lay out, pack and enqueue the GPU work of jobs[live] on slot s.
-    // stages: 1 recon, 2 +deblock, 3 +sao, 4 +jpeg forward path; entropy: +K5
-    int enqueue(Slot& s, int stages, bool entropy);
+    // stages: 1 recon, 2 +deblock, 3 +sao, 4 +jpeg forward path; entropy: +K5.
+    // pool_free: the thread pool may be used for packing (not busy parsing).
+    int enqueue(Slot& s, int stages, bool entropy, bool pool_free = true);
     // Wait for slot s and copy its payloads down (entropy chunks).
     int sync(Slot& s);
 };
 
-int Engine::enqueue(Slot& s, int stages, bool entropy) {
+int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const int nf = static_cast<int>(s.live.size());
     s.stages = stages;
     s.entropy = entropy;
@@ -328,14 +330,16 @@ int Engine::enqueue(Slot& s, int stages, bool entropy) {
         }
     }
     uint8_t* hin = s.h_in.p;
-    pool->parallel_for(nf, [&](int k) {
+    auto pack = [&](int k) {
         const FrameJob& j = jobs[s.live[k]];
         if (!j.tus.empty()) std::memcpy(hin + o_tus + bt[k] * sizeof(h2j_tu), j.tus.data(), j.tus.size() * sizeof(h2j_tu));
         if (!j.coefs.empty()) std::memcpy(hin + o_coefs + bc[k] * sizeof(h2j_coef), j.coefs.data(), j.coefs.size() * sizeof(h2j_coef));
         if (!j.ctbs.empty()) std::memcpy(hin + o_ctbs + bk[k] * sizeof(h2j_ctb), j.ctbs.data(), j.ctbs.size() * sizeof(h2j_ctb));
         if (!j.slices.empty()) std::memcpy(hin + o_slices + bs[k] * sizeof(h2j_slice), j.slices.data(), j.slices.size() * sizeof(h2j_slice));
         if (!j.sl.empty()) std::memcpy(hin + o_sl + bl[k], j.sl.data(), j.sl.size());
-    });
+    };
+    if (pool_free) pool->parallel_for(nf, pack);
+    else for (int k = 0; k < nf; k++) pack(k);
     uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
     h2j_gpu_batch& b = s.batch;
     b.nframes = nf;
@@ -410,10 +414,12 @@ int Engine::sync(Slot& s) {
     return 0;
 }
 
+// Frames per pipeline chunk: large enough to fill the GPU (K1 runs one
+// workgroup per picture), small enough that parse / GPU / assembly overlap.
 int chunk_frames(int n) {
     const char* e = std::getenv("H2J_CHUNK");
     if (e && std::atoi(e) > 0) return std::atoi(e);
-    return n;
+    return n >= 512 ? 256 : n;
 }
 
 }  // namespace h2j
@@ -474,6 +480,27 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     const int nchunks = (n + chunk - 1) / chunk;
     size_t pos = 0;
     int rc = 0;
+    // Parsing runs ahead on the pool (frames claimed in order), so chunk c+1
+    // parses while the GPU runs chunk c and the host assembles chunk c-1.
+    const bool overlap = nchunks > 1;
+    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[nchunks]);
+    for (int c = 0; c < nchunks; c++) left[c] = std::min(n, (c + 1) * chunk) - c * chunk;
+    std::mutex mu;
+    std::condition_variable cv;
+    double t_parsed = t0;
+    auto parse_all = [&]() {
+        e.pool->parallel_for(n, [&](int i) {
+            h2j::parse_any(data[i], sizes[i], e.jobs[i]);
+            if (left[i / chunk].fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> g(mu);
+                cv.notify_all();
+            }
+        });
+        t_parsed = h2j::now_ms();
+    };
+    std::thread producer;
+    if (overlap) producer = std::thread(parse_all);
+    else parse_all();
     // assemble the JPEGs of a finished slot into out (in frame order)
     auto assemble = [&](Slot& s) -> int {
         if (e.sync(s)) return -2;
@@ -481,10 +508,12 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
         const int nf = static_cast<int>(s.live.size());
         const uint8_t* js = s.h_js.p + 256;
         std::vector<size_t> sz(nf);
-        e.pool->parallel_for(nf, [&](int k) {
+        auto size_of = [&](int k) {
             const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
             sz[k] = st->seg_off == ~0ull ? 0 : h2j::jpeg_container_size(*st, s.h_seg.p + st->seg_off, h2j::kLavcIdent);
-        });
+        };
+        if (overlap) for (int k = 0; k < nf; k++) size_of(k);
+        else e.pool->parallel_for(nf, size_of);
         std::vector<size_t> at(nf);
         for (int k = 0; k < nf; k++) {
             const int i = s.live[k];
@@ -505,35 +534,46 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
             out_len[i] = sz[k];
             pos += sz[k];
         }
-        e.pool->parallel_for(nf, [&](int k) {
+        auto write = [&](int k) {
             if (at[k] == ~static_cast<size_t>(0)) return;
             const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
             const h2j_frame& f = s.frames[k];
             h2j::jpeg_write_container(*st, s.h_seg.p + st->seg_off, f.out_w, f.out_h, h2j::kLavcIdent, out + at[k]);
-        });
+        };
+        if (overlap) for (int k = 0; k < nf; k++) write(k);
+        else e.pool->parallel_for(nf, write);
         e.stats[h2j::ST_ASSEMBLE] += h2j::now_ms() - ta;
         e.stats[h2j::ST_FRAMES] += nf;
         return 0;
     };
-    for (int c = 0; c < nchunks; c++) {
+    int fail = 0;
+    for (int c = 0; c < nchunks && !fail; c++) {
         const int i0 = c * chunk, i1 = std::min(n, i0 + chunk);
-        const double tp = h2j::now_ms();
-        e.pool->parallel_for(i1 - i0, [&](int k) { h2j::parse_any(data[i0 + k], sizes[i0 + k], e.jobs[i0 + k]); });
-        e.stats[h2j::ST_PARSE] += h2j::now_ms() - tp;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return left[c].load() == 0; });
+        }
         Slot& s = e.slot[c & 1];
-        if (s.pending && assemble(s)) return -2;
+        if (s.pending && assemble(s)) { fail = 1; break; }
         s.live.clear();
         for (int i = i0; i < i1; i++) {
             status[i] = e.jobs[i].error;
             if (e.jobs[i].error == 0) s.live.push_back(i);
         }
-        if (e.enqueue(s, 4, true)) return -2;
+        if (e.enqueue(s, 4, true, !overlap)) { fail = 1; break; }
         Slot& prev = e.slot[(c + 1) & 1];
-        if (c > 0 && prev.pending && assemble(prev)) return -2;
+        if (c > 0 && prev.pending && assemble(prev)) { fail = 1; break; }
     }
-    for (int c = 0; c < 2; c++) {
+    for (int c = 0; c < 2 && !fail; c++) {
         Slot& s = e.slot[(nchunks + c) & 1];
-        if (s.pending && assemble(s)) return -2;
+        if (s.pending && assemble(s)) fail = 1;
+    }
+    if (producer.joinable()) producer.join();
+    e.stats[h2j::ST_PARSE] = t_parsed - t0;
+    if (fail) {
+        for (auto& s : e.slot)
+            if (s.pending) e.sync(s);
+        return -2;
     }
     e.stats[h2j::ST_TOTAL] = h2j::now_ms() - t0;
     if (rc) e.err = "output buffer too small or payload pool overflow";
