@@ -509,16 +509,22 @@ struct K1WaveLds {  // HEVC
     int sub[132];
     int ref[132];
 };
-struct H4WaveLds {  // H.264
+// H.264: one macroblock plus its top line and left column, per wave.
+// Window coordinates: (x - mb_x + 1, y - mb_y + 1); row 0 is the line
+// above (luma incl. the 8 top-right samples), column 0 the left column.
+constexpr int kH4MaxTus = 24;
+struct H4WaveLds {
+    uint16_t wy[17][25];
+    uint16_t wc[2][9][9];
+    int16_t ry[16][16];   // residual (K0)
+    int16_t rc[2][8][8];
+    h2j_tu tus[kH4MaxTus];
+    uint64_t masks[kH4MaxTus];
     int top[40];    // top[0] = corner, top[1 + i] = p[i, -1]
     int left[20];   // left[0] = corner, left[1 + i] = p[-1, i]
     int ftop[40], fleft[20];
-    int dcv;
 };
-union K1WLds {
-    K1WaveLds h5;
-    H4WaveLds h4;
-};
+
 
 template <typename Pel>
 DEVI void hevc_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, uint8_t* arena, K1WaveLds& s,
@@ -658,31 +664,29 @@ DEVI void hevc_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, u
     wave_sync();
 }
 
-template <typename Pel>
-DEVI void h264_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, uint8_t* arena, H4WaveLds& s,
-                          int lane) {
+// One H.264 prediction block (I4x4 / I8x8 / I16x16 / chroma) inside the
+// wave's macroblock window; all sample traffic is LDS.
+DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int bd, H4WaveLds& s, int lane) {
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-    const int x0 = tu.x, y0 = tu.y;
-    Pel* P = plane<Pel>(f, arena, f.pic, c);
-    const int16_t* RS = res_plane(f, arena, c);
-    const int st = f.pic_stride[c];
-    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int ox = c ? tu.x - mbx * 8 : tu.x - mbx * 16;   // block origin inside the macroblock
+    const int oy = c ? tu.y - mby * 8 : tu.y - mby * 16;
     const int maxv = (1 << bd) - 1;
     const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
     const bool chroma = c > 0;
     const bool nxn = c == 0 && log2n <= 3;
     const int ntop = nxn ? 2 * n : n;
+    // window accessors (dx, dy relative to the block origin; -1 = neighbour)
+#define WIN(dx, dy) (chroma ? s.wc[c - 1][oy + (dy) + 1][ox + (dx) + 1] : s.wy[oy + (dy) + 1][ox + (dx) + 1])
     // mask bits: 0 top, 1 left, 2 corner, 3 top-right
     const int fl = static_cast<int>(mask & 15);
     for (int i = lane; i <= ntop; i += 64) {
         int v = 0;
-        if (i == 0) v = (fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0;
-        else if (i - 1 < n) v = (fl & 1) ? P[(y0 - 1) * st + x0 + i - 1] : 0;
-        else v = (fl & 8) ? P[(y0 - 1) * st + x0 + i - 1] : ((fl & 1) ? P[(y0 - 1) * st + x0 + n - 1] : 0);
+        if (i == 0) v = (fl & 4) ? WIN(-1, -1) : 0;
+        else if (i - 1 < n) v = (fl & 1) ? WIN(i - 1, -1) : 0;
+        else v = (fl & 8) ? WIN(i - 1, -1) : ((fl & 1) ? WIN(n - 1, -1) : 0);
         s.top[i] = v;
     }
-    for (int i = lane; i <= n; i += 64) s.left[i] = i == 0 ? ((fl & 4) ? P[(y0 - 1) * st + x0 - 1] : 0)
-                                                           : ((fl & 2) ? P[(y0 + i - 1) * st + x0 - 1] : 0);
+    for (int i = lane; i <= n; i += 64) s.left[i] = i == 0 ? ((fl & 4) ? WIN(-1, -1) : 0) : ((fl & 2) ? WIN(-1, i - 1) : 0);
     wave_sync();
     const int mode = tu.mode;
     const int* TT = s.top + 1;
@@ -735,7 +739,7 @@ DEVI void h264_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, u
     }
     for (int i = lane; i < nn; i += 64) {
         const int x = i & (n - 1), y = i >> log2n;
-        const int r = cbf ? RS[(y0 + y) * st + x0 + x] : 0;
+        const int r = cbf ? (chroma ? s.rc[c - 1][oy + y][ox + x] : s.ry[oy + y][ox + x]) : 0;
         int pv;
         if (nxn) {
             pv = h264_pred_nxn(mode, x, y, n, TT, LL, dcv);
@@ -773,13 +777,109 @@ DEVI void h264_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, u
                 else pv = al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
             }
         }
-        P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
+        WIN(x, y) = static_cast<uint16_t>(clip3(0, maxv, pv + r));
     }
+#undef WIN
     wave_sync();
 }
 
-template <typename Pel, bool kHevc>
-DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WLds& wl, uint32_t* prog) {
+// H.264 macroblock rows: per MB one batched round trip (TU records, masks,
+// top line, residual), the prediction chain in LDS, one store of the MB.
+template <typename Pel>
+DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t* masks = tu_masks(f, arena);
+    const uint32_t* rng = ctb_ranges(f, arena);
+    constexpr int kSlots = 2 * kK1Waves;
+    Pel* PY = plane<Pel>(f, arena, f.pic, 0);
+    Pel* PC[2] = {plane<Pel>(f, arena, f.pic, 1), plane<Pel>(f, arena, f.pic, 2)};
+    const int16_t* RY = res_plane(f, arena, 0);
+    const int16_t* RC[2] = {res_plane(f, arena, 1), res_plane(f, arena, 2)};
+    const int sty = f.pic_stride[0], stc = f.pic_stride[1];
+    const int W = f.width, Wc = f.width >> 1;
+    for (int row = w; row < f.ctb_h; row += kK1Waves) {
+        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + row % kSlots;
+        uint32_t seen = 0;
+        const int gy = row * 16, cy = row * 8;
+        for (int mx = 0; mx < f.ctb_w; mx++) {
+            const int gx = mx * 16, cx = mx * 8;
+            if (row > 0) {
+                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, f.ctb_w));
+                if (seen < need) {
+                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+            }
+            const int cb = row * f.ctb_w + mx;
+            const uint32_t a = rng[2 * cb], ntu = min(rng[2 * cb + 1] - a, static_cast<uint32_t>(kH4MaxTus));
+            // ---- batched loads: records, masks, top line, left column (first MB), residual
+            if (lane < static_cast<int>(ntu)) {
+                s.tus[lane] = T[a + lane];
+                s.masks[lane] = masks[a + lane];
+            }
+            if (lane < 25) {
+                const int x = gx - 1 + lane;
+                s.wy[0][lane] = (row > 0 && x >= 0 && x < W) ? static_cast<uint16_t>(PY[(gy - 1) * sty + x]) : 0;
+            } else if (lane < 43) {
+                const int k = lane - 25, c = k / 9, i = k % 9, x = cx - 1 + i;
+                s.wc[c][0][i] = (row > 0 && x >= 0 && x < Wc) ? static_cast<uint16_t>(PC[c][(cy - 1) * stc + x]) : 0;
+            }
+            if (mx == 0) {  // left of the picture: never available
+                if (lane < 16) s.wy[lane + 1][0] = 0;
+                else if (lane < 32) s.wc[(lane - 16) >> 3][((lane - 16) & 7) + 1][0] = 0;
+            }
+            {
+                const int r = lane >> 2, c4 = (lane & 3) * 4;  // luma residual: 4 per lane
+                const uint2 v = *reinterpret_cast<const uint2*>(RY + (gy + r) * sty + gx + c4);
+                *reinterpret_cast<uint2*>(&s.ry[r][c4]) = v;
+                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;  // chroma: 2 per lane
+                const uint32_t u = *reinterpret_cast<const uint32_t*>(RC[c] + (cy + rr) * stc + cx + c2);
+                *reinterpret_cast<uint32_t*>(&s.rc[c][rr][c2]) = u;
+            }
+            wave_sync();
+            const bool pcm = ntu > 0 && (s.tus[0].flags & H2J_TU_PCM);
+            if (pcm) {  // samples written by K0: pull them into the window
+                for (int i = lane; i < 256; i += 64) s.wy[(i >> 4) + 1][(i & 15) + 1] = PY[(gy + (i >> 4)) * sty + gx + (i & 15)];
+                for (int i = lane; i < 128; i += 64) {
+                    const int c = i >> 6, k = i & 63;
+                    s.wc[c][(k >> 3) + 1][(k & 7) + 1] = PC[c][(cy + (k >> 3)) * stc + cx + (k & 7)];
+                }
+                wave_sync();
+            } else {
+                for (uint32_t t = 0; t < ntu; t++) {
+                    const h2j_tu tu = s.tus[t];
+                    h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? f.bit_depth_c : f.bit_depth, s, lane);
+                }
+                // ---- store the macroblock
+                {
+                    const int r = lane >> 2, c4 = (lane & 3) * 4;
+                    Pel* d = PY + (gy + r) * sty + gx + c4;
+                    for (int k = 0; k < 4; k++) d[k] = static_cast<Pel>(s.wy[r + 1][c4 + k + 1]);
+                    const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
+                    Pel* e = PC[c] + (cy + rr) * stc + cx + c2;
+                    e[0] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 1]);
+                    e[1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
+                }
+            }
+            // right column becomes the next MB's left column
+            if (lane < 16) s.wy[lane + 1][0] = s.wy[lane + 1][16];
+            else if (lane < 32) {
+                const int c = (lane - 16) >> 3, i = ((lane - 16) & 7) + 1;
+                s.wc[c][i][0] = s.wc[c][i][8];
+            }
+            wave_sync();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+template <typename Pel>
+DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WaveLds& wl, uint32_t* prog) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t* masks = tu_masks(f, arena);
     const uint32_t* rng = ctb_ranges(f, arena);
@@ -794,7 +894,7 @@ DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WL
                 if (seen < need) {
                     while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
                         __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
             }
             const int cb = row * f.ctb_w + cx;
@@ -802,10 +902,9 @@ DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WL
             for (uint32_t t = a; t < b; t++) {
                 const h2j_tu tu = T[t];
                 if (tu.flags & H2J_TU_PCM) continue;  // written by K0
-                if (kHevc) hevc_predict_tu<Pel>(f, tu, masks[t], arena, wl.h5, lane);
-                else h264_predict_tu<Pel>(f, tu, masks[t], arena, wl.h4, lane);
+                hevc_predict_tu<Pel>(f, tu, masks[t], arena, wl, lane);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0)
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -813,22 +912,32 @@ DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WL
     }
 }
 
-__global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon(const h2j_frame* frames, const h2j_tu* tus,
-                                                             uint8_t* arena) {
-    __shared__ K1WLds wl[kK1Waves];
+// Separate kernels per codec so each gets its own register budget; a mixed
+// batch launches both and each skips the other codec's pictures.
+__global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
+                                                                  uint8_t* arena) {
+    __shared__ K1WaveLds wl[kK1Waves];
     __shared__ uint32_t prog[2 * kK1Waves];
     const h2j_frame& f = frames[blockIdx.x];
+    if (f.codec != H2J_CODEC_HEVC) return;
     if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
     __syncthreads();
-    const h2j_tu* T = tus + f.tu;
-    K1WLds& s = wl[threadIdx.x >> 6];
-    if (f.codec == H2J_CODEC_HEVC) {
-        if (f.bit_depth == 8) predict_rows<uint8_t, true>(f, T, arena, s, prog);
-        else predict_rows<uint16_t, true>(f, T, arena, s, prog);
-    } else if (f.codec == H2J_CODEC_H264) {
-        if (f.bit_depth == 8) predict_rows<uint8_t, false>(f, T, arena, s, prog);
-        else predict_rows<uint16_t, false>(f, T, arena, s, prog);
-    }
+    K1WaveLds& s = wl[threadIdx.x >> 6];
+    if (f.bit_depth == 8) predict_rows<uint8_t>(f, tus + f.tu, arena, s, prog);
+    else predict_rows<uint16_t>(f, tus + f.tu, arena, s, prog);
+}
+
+__global__ void __launch_bounds__(64 * kK1Waves, 6) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
+                                                                  uint8_t* arena) {
+    __shared__ H4WaveLds wl[kK1Waves];
+    __shared__ uint32_t prog[2 * kK1Waves];
+    const h2j_frame& f = frames[blockIdx.x];
+    if (f.codec != H2J_CODEC_H264) return;
+    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
+    __syncthreads();
+    H4WaveLds& s = wl[threadIdx.x >> 6];
+    if (f.bit_depth == 8) h264_rows<uint8_t>(f, tus + f.tu, arena, s, prog);
+    else h264_rows<uint16_t>(f, tus + f.tu, arena, s, prog);
 }
 
 // ---------------------------------------------------------------- K2: deblocking
@@ -1502,8 +1611,16 @@ int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
         const int r = check(hipGetLastError(), "h2j_k0_prep");
         if (r) return r;
     }
-    hipLaunchKernelGGL(h2j_k1_recon, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
-    return check(hipGetLastError(), "h2j_k1_recon");
+    if (b->has_hevc) {
+        hipLaunchKernelGGL(h2j_k1_recon_hevc, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
+        const int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
+        if (r) return r;
+    }
+    if (b->has_h264) {
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
+        return check(hipGetLastError(), "h2j_k1_recon_h264");
+    }
+    return 0;
 }
 
 int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {

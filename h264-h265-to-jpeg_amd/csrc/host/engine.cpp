@@ -347,6 +347,12 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.max_h = max_h;
     b.max_mcu = max_mcu;
     b.max_ntu = max_ntu;
+    b.has_hevc = 0;
+    b.has_h264 = 0;
+    for (int k = 0; k < nf; k++) {
+        if (s.frames[k].codec == H2J_CODEC_HEVC) b.has_hevc = 1;
+        if (s.frames[k].codec == H2J_CODEC_H264) b.has_h264 = 1;
+    }
     b.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
     b.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);
     b.coefs = reinterpret_cast<const h2j_coef*>(din + o_coefs);
