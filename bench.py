@@ -54,16 +54,44 @@ def load_streams(pattern):
     return [open(f, "rb").read() for f in files]
 
 
-def pmc_traffic():
-    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_k1.json")
+def pmc_traffic(workload):
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_k1_<workload>.json, written by tools/prof_summary.py), if any."""
+    path = os.path.join(ROOT, "profiles", f"pmc_k1_{workload}.json")
     if os.path.exists(path):
         try:
-            d = json.load(open(path))
-            return d.get("hbm_bytes_per_launch")
-        except Exception:
+            return json.load(open(path)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             return None
     return None
+
+
+def reduce_over_ranks(dist, elapsed, frames, local_rank=0):
+    """The run's only collectives: MAX of the timed region, SUM of the frames
+    (RCCL over xGMI on GPUs, gloo on CPU).  Returns (elapsed, total_frames)."""
+    if dist is None:
+        return elapsed, frames
+    import torch
+    use_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+    dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([frames], dtype=torch.int64, device=dev)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(c.item())
+
+
+def shard_lpt(costs, world):
+    """Size-balanced LPT partition of independent stills over `world` GPUs
+    (SURVEY.md §8e, config 5): returns one index list per rank."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    loads = [0.0] * world
+    parts = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (loads[k], k))
+        parts[r].append(i)
+        loads[r] += costs[i]
+    return [sorted(p) for p in parts]
 
 
 def cpu_baseline(streams, budget_s=12.0):
@@ -150,27 +178,21 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([n * args.steps], dtype=torch.int64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        total_frames = int(c.item())
-    else:
-        total_frames = n * args.steps
+    elapsed, total_frames = reduce_over_ranks(dist, elapsed, n * args.steps, local)
 
     if rank == 0:
         steps = args.steps
         per = {k: v / steps for k, v in stage_sum.items()}
-        recon_ms = per["recon_ms"]
-        gpu_ms = (per["h2d_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"]
-                  + per["entropy_ms"] + per["d2h_ms"])
-        alg_bytes = alg_bytes_per_frame(wl) * n
-        achieved = alg_bytes / (recon_ms / 1e3) / 1e9
-        traffic = pmc_traffic() if args.workload == "hevc1080" else None
+        # dominant kernel: K1 (intra prediction chain), one launch per chunk
+        chunks = max(1, round(per["chunks"]))
+        k1_ms = per["recon_ms"] / chunks
+        frames_per_launch = n / chunks
+        alg_bytes = alg_bytes_per_frame(wl) * frames_per_launch
+        achieved = alg_bytes / (k1_ms / 1e3) / 1e9
+        gpu_ms = (per["h2d_ms"] + per["prep_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"]
+                  + per["jpeg_ms"] + per["entropy_ms"] + per["d2h_ms"])
+        k1_name = "h2j_k1_recon_h264" if args.workload.startswith("avc") else "h2j_k1_recon_hevc"
+        traffic = pmc_traffic(args.workload)
         res = {
             "metric": METRIC,
             "value": total_frames / elapsed,
@@ -187,9 +209,10 @@ def main():
             "config": {"workload": wl["desc"], "workload_key": args.workload,
                        "frames_per_gpu": n, "global_batch": n * world, "host_threads_per_gpu": args.threads,
                        "parallelism": f"independent replicas x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "h2j_k1_recon", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+            "roofline": {"bound": "hbm", "kernel": k1_name, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": recon_ms},
+                         "alg_bytes_per_launch": alg_bytes, "frames_per_launch": frames_per_launch,
+                         "avg_launch_ms": k1_ms},
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }

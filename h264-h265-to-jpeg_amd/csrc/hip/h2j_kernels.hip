@@ -1601,16 +1601,19 @@ float h2j_gpu_event_elapsed_ms(void* a, void* b) {
     return ms;
 }
 
-int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
+int h2j_gpu_prep(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int waves = (b->max_ntu + kK0Tus - 1) / kK0Tus;
-    if (waves > 0) {
-        hipLaunchKernelGGL(h2j_k0_prep, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
-                           b->slices, b->sl, b->arena);
-        const int r = check(hipGetLastError(), "h2j_k0_prep");
-        if (r) return r;
-    }
+    if (waves <= 0) return 0;
+    hipLaunchKernelGGL(h2j_k0_prep, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
+                       b->slices, b->sl, b->arena);
+    return check(hipGetLastError(), "h2j_k0_prep");
+}
+
+int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
+    if (!b || b->nframes <= 0) return 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
     if (b->has_hevc) {
         hipLaunchKernelGGL(h2j_k1_recon_hevc, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
         const int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
@@ -1621,6 +1624,11 @@ int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;
+}
+
+int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
+    const int r = h2j_gpu_prep(b, stream);
+    return r ? r : h2j_gpu_predict(b, stream);
 }
 
 int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {

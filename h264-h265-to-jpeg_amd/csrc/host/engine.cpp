@@ -165,7 +165,7 @@ int parse_any(const uint8_t* d, size_t n, FrameJob& job) {
 // One in-flight chunk: its stream, buffers and layout.
 struct Slot {
     void* stream = nullptr;
-    void* ev[8] = {nullptr};
+    void* ev[9] = {nullptr};
     DevBuf d_in, d_arena, d_seg, d_scratch;
     HostBuf h_in, h_js, h_seg;
     std::vector<h2j_frame> frames;
@@ -190,8 +190,9 @@ struct Slot {
     }
 };
 
+// stats slots (h2j_engine_stats): times in ms summed over chunks; ST_RECON is K1 only, ST_PREP is K0
 enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
-       ST_ENTROPY, ST_N };
+       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_N };
 
 // upper bound of one block's entropy-coded size (code lengths <= 16, values <= 16 bits)
 constexpr size_t kSegBytesPerBlock = 272;
@@ -371,7 +372,9 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     r |= h2j_gpu_memset(s.d_arena.p, 0, s.zero_bytes, st);
     r |= h2j_gpu_event_record(s.ev[1], st);
     if (r) return fail(std::string("upload failed: ") + h2j_gpu_last_error());
-    if (h2j_gpu_recon(&b, st)) return fail(h2j_gpu_last_error());
+    if (h2j_gpu_prep(&b, st)) return fail(h2j_gpu_last_error());
+    h2j_gpu_event_record(s.ev[8], st);
+    if (h2j_gpu_predict(&b, st)) return fail(h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[2], st);
     if (stages >= 2 && h2j_gpu_deblock(&b, st)) return fail(h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[3], st);
@@ -411,7 +414,9 @@ int Engine::sync(Slot& s) {
     if (h2j_gpu_event_record(s.ev[7], s.stream) || h2j_gpu_stream_sync(s.stream))
         return fail(std::string("download failed: ") + h2j_gpu_last_error());
     stats[ST_H2D] += h2j_gpu_event_elapsed_ms(s.ev[0], s.ev[1]);
-    stats[ST_RECON] += h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[2]);
+    stats[ST_PREP] += h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[8]);
+    stats[ST_RECON] += h2j_gpu_event_elapsed_ms(s.ev[8], s.ev[2]);
+    stats[ST_CHUNKS] += 1;
     stats[ST_DEBLOCK] += h2j_gpu_event_elapsed_ms(s.ev[2], s.ev[3]);
     stats[ST_SAO] += h2j_gpu_event_elapsed_ms(s.ev[3], s.ev[4]);
     stats[ST_JPEG] += h2j_gpu_event_elapsed_ms(s.ev[4], s.ev[5]);

@@ -75,6 +75,9 @@ typedef struct {
  * picture) intra prediction + residual -> the pre-loop-filter picture in
  * frame.pic.  HEVC and H.264. */
 int h2j_gpu_recon(const h2j_gpu_batch *b, void *stream);
+/* the two halves of h2j_gpu_recon: K0 alone, then K1 alone */
+int h2j_gpu_prep(const h2j_gpu_batch *b, void *stream);
+int h2j_gpu_predict(const h2j_gpu_batch *b, void *stream);
 /* K2: deblocking (vertical edges, then horizontal edges), in place on frame.pic */
 int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);
 /* K3: SAO frame.pic -> frame.pic2 (copies when SAO is off) */
