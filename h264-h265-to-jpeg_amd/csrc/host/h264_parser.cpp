@@ -17,6 +17,7 @@
 
 #include "bitstream.h"
 #include "cabac.h"
+#include "cavlc_tables.h"
 #include "job.h"
 
 namespace h2j {
@@ -261,7 +262,113 @@ struct Mb {
     uint8_t cbf[16];
     uint8_t cbf_c[2][4];
     uint8_t cbf_dc[3];
+    uint8_t tc[16];     // CAVLC TotalCoeff per luma 4x4 block (I16x16: AC block)
+    uint8_t tcc[2][4];  // CAVLC TotalCoeff per chroma AC block
 };
+
+// MSB-first reader over one slice's RBSP for CAVLC: 64-bit window, peek/skip.
+class VlcBits {
+public:
+    void init(const uint8_t* p, size_t n, size_t bitpos) {
+        p_ = p;
+        n_ = n;
+        pos_ = bitpos;
+    }
+    inline uint32_t peek32() const {
+        const size_t byte = pos_ >> 3;
+        uint64_t w = 0;
+        if (byte + 8 <= n_) {
+            for (int i = 0; i < 8; i++) w = (w << 8) | p_[byte + i];
+        } else {
+            for (int i = 0; i < 8; i++) w = (w << 8) | (byte + i < n_ ? p_[byte + i] : 0u);
+        }
+        return static_cast<uint32_t>((w << (pos_ & 7)) >> 32);
+    }
+    inline void skip(int n) { pos_ += static_cast<size_t>(n); }
+    inline uint32_t u(int n) {
+        if (!n) return 0;
+        const uint32_t v = peek32() >> (32 - n);
+        pos_ += static_cast<size_t>(n);
+        return v;
+    }
+    inline uint32_t ue() {
+        const uint32_t w = peek32();
+        if (!w) { pos_ = n_ * 8 + 1; return 0; }
+        const int lz = __builtin_clz(w);
+        if (lz > 15) {  // long code: two steps
+            pos_ += static_cast<size_t>(lz + 1);
+            return ((1u << lz) - 1u) + u(lz);
+        }
+        pos_ += static_cast<size_t>(2 * lz + 1);
+        return (w >> (31 - 2 * lz)) - 1u;
+    }
+    inline int32_t se() {
+        const uint32_t k = ue();
+        return (k & 1) ? static_cast<int32_t>((k + 1) >> 1) : -static_cast<int32_t>(k >> 1);
+    }
+    void align() { pos_ = (pos_ + 7) & ~static_cast<size_t>(7); }
+    size_t pos() const { return pos_; }
+    size_t byte_pos() const { return pos_ >> 3; }
+    bool overrun() const { return pos_ > n_ * 8; }
+    // more_rbsp_data(): anything before the rbsp_stop_one_bit
+    bool more_rbsp_data(size_t stop_bit) const { return pos_ < stop_bit; }
+
+private:
+    const uint8_t* p_ = nullptr;
+    size_t n_ = 0;
+    size_t pos_ = 0;
+};
+
+// Direct-lookup decoders for the CAVLC VLC tables (built once).
+struct CavlcLut {
+    // coeff_token: [nC class 0..3][16-bit prefix] -> (len << 10) | (t1 << 5) | tc, 0 = invalid
+    std::vector<uint16_t> ct[4];
+    uint8_t tz[15][512];    // total_zeros: (len << 4) | value, 9-bit prefix
+    uint8_t tzdc[3][8];     // chroma DC total_zeros, 3-bit prefix
+    uint8_t rb[7][2048];    // run_before: (len << 4) | run, 11-bit prefix
+    CavlcLut() {
+        for (int col = 0; col < 4; col++) {
+            ct[col].assign(65536, 0);
+            for (int t1 = 0; t1 < 4; t1++)
+                for (int tc = 0; tc <= 16; tc++) {
+                    const int len = kCoeffTokenLen[col][t1][tc];
+                    if (!len) continue;
+                    const uint32_t base = static_cast<uint32_t>(kCoeffTokenCode[col][t1][tc]) << (16 - len);
+                    for (uint32_t k = 0; k < (1u << (16 - len)); k++)
+                        ct[col][base + k] = static_cast<uint16_t>((len << 10) | (t1 << 5) | tc);
+                }
+        }
+        std::memset(tz, 0, sizeof(tz));
+        for (int t = 0; t < 15; t++)
+            for (int z = 0; z < 16; z++) {
+                const int len = kTotalZerosLen[t][z];
+                if (!len) continue;
+                const uint32_t base = static_cast<uint32_t>(kTotalZerosCode[t][z]) << (9 - len);
+                for (uint32_t k = 0; k < (1u << (9 - len)); k++) tz[t][base + k] = static_cast<uint8_t>((len << 4) | z);
+            }
+        std::memset(tzdc, 0, sizeof(tzdc));
+        for (int t = 0; t < 3; t++)
+            for (int z = 0; z < 4; z++) {
+                const int len = kTotalZerosDcLen[t][z];
+                if (!len) continue;
+                const uint32_t base = static_cast<uint32_t>(kTotalZerosDcCode[t][z]) << (3 - len);
+                for (uint32_t k = 0; k < (1u << (3 - len)); k++) tzdc[t][base + k] = static_cast<uint8_t>((len << 4) | z);
+            }
+        std::memset(rb, 0, sizeof(rb));
+        for (int z = 0; z < 7; z++)
+            for (int r = 0; r < 15; r++) {
+                const int len = kRunBeforeLen[z][r];
+                if (!len) continue;
+                const uint32_t base = static_cast<uint32_t>(kRunBeforeCode[z][r]) << (11 - len);
+                for (uint32_t k = 0; k < (1u << (11 - len)); k++) rb[z][base + k] = static_cast<uint8_t>((len << 4) | r);
+            }
+    }
+};
+
+const CavlcLut& cavlc_lut() {
+    static const CavlcLut lut;  // C++11 thread-safe initialisation
+    return lut;
+}
 
 class H264Parser {
 public:
@@ -283,7 +390,14 @@ private:
     uint16_t ctx_[460];  // 16-bit: stores must not alias the engine state
     int err_ = 0;
 
+    VlcBits vb_;  // CAVLC slice data
+    size_t stop_bit_ = 0;
     int dec(int c) { return cc_.decision(ctx_[c]); }
+    // CAVLC (7.3.5.3.2 / 9.2)
+    int cavlc_block(int nC, int maxnum, uint8_t* pos, int* lvl);
+    int nc_luma(int blk);
+    int nc_chroma(const Mb& m, int c, int b4);
+    void decode_mb_cavlc();
     Mb* nb(int dx, int dy) {
         const int x = mbx_ + dx, y = mby_ + dy;
         if (x < 0 || y < 0 || x >= mbw_) return nullptr;
@@ -652,6 +766,271 @@ void H264Parser::decode_mb() {
     }
 }
 
+// ---------------------------------------------------------------- CAVLC
+// residual_block_cavlc: number of non-zero levels; scan indices in pos[] and
+// levels in lvl[]; -1 on a malformed block.
+int H264Parser::cavlc_block(int nC, int maxnum, uint8_t* pos, int* lvl) {
+    const CavlcLut& L = cavlc_lut();
+    int tc, t1;
+    if (nC >= 8) {
+        const int v = static_cast<int>(vb_.u(6));
+        if (v == 3) return 0;
+        tc = (v >> 2) + 1;
+        t1 = v & 3;
+        if (t1 > tc) return -1;
+    } else {
+        const int col = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+        const uint16_t e = L.ct[col][vb_.peek32() >> 16];
+        if (!e) return -1;
+        vb_.skip(e >> 10);
+        tc = e & 31;
+        t1 = (e >> 5) & 3;
+    }
+    if (tc == 0) return 0;
+    if (tc > maxnum) return -1;
+    int level[16], run[16];
+    if (t1) {
+        const uint32_t sgn = vb_.u(t1);
+        for (int i = 0; i < t1; i++) level[i] = ((sgn >> (t1 - 1 - i)) & 1) ? -1 : 1;
+    }
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int i = t1; i < tc; i++) {
+        const uint32_t w = vb_.peek32();
+        if (!w) return -1;
+        const int prefix = __builtin_clz(w);
+        vb_.skip(prefix + 1);
+        int code = (prefix < 15 ? prefix : 15) << sl;
+        const int sz = (prefix == 14 && sl == 0) ? 4 : (prefix >= 15 ? prefix - 3 : sl);
+        if (sz > 0) code += static_cast<int>(vb_.u(sz));
+        if (prefix >= 15 && sl == 0) code += 15;
+        if (prefix >= 16) code += (1 << (prefix - 3)) - 4096;
+        if (i == t1 && t1 < 3) code += 2;
+        level[i] = (code & 1) ? (-code - 1) >> 1 : (code + 2) >> 1;
+        if (sl == 0) sl = 1;
+        if (std::abs(level[i]) > (3 << (sl - 1)) && sl < 6) sl++;
+    }
+    int zeros = 0;
+    if (tc < maxnum) {
+        uint8_t e;
+        if (maxnum == 4) e = L.tzdc[tc - 1][vb_.peek32() >> 29];
+        else e = L.tz[tc - 1][vb_.peek32() >> 23];
+        if (!e) return -1;
+        vb_.skip(e >> 4);
+        zeros = e & 15;
+        if (zeros > maxnum - tc) return -1;
+    }
+    for (int i = 0; i < tc - 1; i++) {
+        if (zeros > 0) {
+            const int zl = zeros < 7 ? zeros : 7;
+            const uint8_t e = L.rb[zl - 1][vb_.peek32() >> 21];
+            if (!e) return -1;
+            vb_.skip(e >> 4);
+            const int r = e & 15;
+            if (r > zeros) return -1;
+            run[i] = r;
+            zeros -= r;
+        } else {
+            run[i] = 0;
+        }
+    }
+    run[tc - 1] = zeros;
+    int coeff = -1;
+    for (int i = tc - 1, k = 0; i >= 0; i--, k++) {
+        coeff += run[i] + 1;
+        pos[k] = static_cast<uint8_t>(coeff);
+        lvl[k] = level[i];
+    }
+    return tc;
+}
+
+// nC (9.2.1): average of the neighbours' TotalCoeff, I_PCM counts 16
+int H264Parser::nc_luma(int blk) {
+    int nblk, cnt_a = 0, cnt_b = 0;
+    Mb* A = nb_blk(kBlkX[blk] - 1, kBlkY[blk], &nblk);
+    if (A) cnt_a = A->mb_type == 25 ? 16 : A->tc[nblk];
+    Mb* B = nb_blk(kBlkX[blk], kBlkY[blk] - 1, &nblk);
+    if (B) cnt_b = B->mb_type == 25 ? 16 : B->tc[nblk];
+    if (A && B) return (cnt_a + cnt_b + 1) >> 1;
+    return A ? cnt_a : (B ? cnt_b : 0);
+}
+
+int H264Parser::nc_chroma(const Mb& m, int c, int b4) {
+    const int bx = b4 & 1, by = b4 >> 1;
+    int cnt_a = 0, cnt_b = 0;
+    bool aa = true, ab = true;
+    if (bx) {
+        cnt_a = m.tcc[c][b4 - 1];
+    } else {
+        Mb* A = nb(-1, 0);
+        if (!A) aa = false;
+        else cnt_a = A->mb_type == 25 ? 16 : A->tcc[c][b4 + 1];
+    }
+    if (by) {
+        cnt_b = m.tcc[c][b4 - 2];
+    } else {
+        Mb* B = nb(0, -1);
+        if (!B) ab = false;
+        else cnt_b = B->mb_type == 25 ? 16 : B->tcc[c][b4 + 2];
+    }
+    if (aa && ab) return (cnt_a + cnt_b + 1) >> 1;
+    return aa ? cnt_a : (ab ? cnt_b : 0);
+}
+
+void H264Parser::decode_mb_cavlc() {
+    Mb& m = mb_[mby_ * mbw_ + mbx_];
+    m = Mb();
+    m.slice = cur_slice_;
+    const int gx = mbx_ * 16, gy = mby_ * 16;
+    h2j_ctb& rec = job_.ctbs[mby_ * mbw_ + mbx_];
+    rec.slice = static_cast<uint8_t>(cur_slice_);
+    rec.mbflags = 4;
+    const uint32_t mbt = vb_.ue();
+    if (mbt > 25) { err_ = -40; return; }
+    m.mb_type = static_cast<int>(mbt);
+    if (m.mb_type == 25) {
+        vb_.align();
+        int lv[256];
+        for (int i = 0; i < 256; i++) lv[i] = static_cast<int>(vb_.u(s_->bit_depth));
+        emit(gx, gy, 4, 0, 0, H2J_TU_PCM, 0, lv, 256, true);
+        for (int c = 1; c < 3; c++) {
+            for (int i = 0; i < 64; i++) lv[i] = static_cast<int>(vb_.u(s_->bit_depth_c));
+            emit(gx / 2, gy / 2, 3, c, 0, H2J_TU_PCM, 0, lv, 64, true);
+        }
+        m.qp = qp_;
+        m.cbp = 0x2F;
+        std::memset(m.tc, 16, sizeof(m.tc));
+        std::memset(m.tcc, 16, sizeof(m.tcc));
+        for (int i = 0; i < 16; i++) m.ipm[i] = 2;
+        rec.qp = static_cast<int8_t>(qp_);
+        rec.mbflags |= 1;
+        return;
+    }
+    const bool is16 = m.mb_type >= 1 && m.mb_type <= 24;
+    if (m.mb_type == 0 && p_->transform_8x8) m.t8x8 = static_cast<int>(vb_.u(1));
+    if (m.mb_type == 0) {
+        const int n = m.t8x8 ? 4 : 16;
+        for (int i = 0; i < n; i++) {
+            const int blk = m.t8x8 ? i * 4 : i;
+            const int prev = static_cast<int>(vb_.u(1));
+            const int rem = prev ? 0 : static_cast<int>(vb_.u(3));
+            int nblk;
+            const int bx = kBlkX[blk], by = kBlkY[blk];
+            Mb* A = nb_blk(bx - 1, by, &nblk);
+            const int ma = !A ? -1 : (A->mb_type != 0 ? 2 : A->ipm[nblk]);
+            Mb* B = nb_blk(bx, by - 1, &nblk);
+            const int mb = !B ? -1 : (B->mb_type != 0 ? 2 : B->ipm[nblk]);
+            const int pm = (ma < 0 || mb < 0) ? 2 : std::min(ma, mb);
+            const int mode = prev ? pm : (rem < pm ? rem : rem + 1);
+            if (m.t8x8) {
+                for (int k = 0; k < 4; k++) m.ipm[blk + k] = static_cast<uint8_t>(mode);
+            } else {
+                m.ipm[blk] = static_cast<uint8_t>(mode);
+            }
+        }
+    } else {
+        for (int i = 0; i < 16; i++) m.ipm[i] = 2;
+    }
+    const uint32_t cpm = vb_.ue();
+    if (cpm > 3) { err_ = -41; return; }
+    m.cpm = static_cast<int>(cpm);
+    if (is16) {
+        const int t = m.mb_type - 1;
+        m.cbp = (((t / 4) % 3) << 4) | (t >= 12 ? 15 : 0);
+    } else {
+        const uint32_t cn = vb_.ue();
+        if (cn > 47) { err_ = -42; return; }
+        m.cbp = kCbpIntra[cn];
+    }
+    if ((m.cbp & 15) || (m.cbp >> 4) || is16) {
+        const int qpd = vb_.se();
+        if (qpd < -(26 + qpbd_ / 2) || qpd > 25 + qpbd_ / 2) { err_ = -43; return; }
+        qp_ = ((qp_ + qpd + 52 + 2 * qpbd_) % (52 + qpbd_)) - qpbd_;
+    }
+    m.qp = qp_;
+    rec.qp = static_cast<int8_t>(qp_);
+    if (m.t8x8) rec.mbflags |= 2;
+    const int qpl = qp_ + qpbd_;
+    uint8_t pos[16];
+    int lvl[16];
+    uint32_t mbe[256];
+    int nmb = 0;
+    auto entry = [](int p, int v) { return (static_cast<uint32_t>(p) << 16) | static_cast<uint16_t>(v); };
+    if (is16) {
+        const int n = cavlc_block(nc_luma(0), 16, pos, lvl);
+        if (n < 0) { err_ = -44; return; }
+        for (int k = 0; k < n; k++) {
+            const int r = kZz4[pos[k]];
+            mbe[nmb++] = entry((r >> 2) * 4 * 16 + (r & 3) * 4, lvl[k]);
+        }
+    }
+    for (int b8 = 0; b8 < 4; b8++) {
+        const bool coded = (m.cbp >> b8) & 1;
+        if (m.t8x8) {
+            uint32_t e[64];
+            int ne = 0;
+            if (coded) {
+                for (int i4 = 0; i4 < 4; i4++) {
+                    const int blk = b8 * 4 + i4;
+                    const int n = cavlc_block(nc_luma(blk), 16, pos, lvl);
+                    if (n < 0) { err_ = -44; return; }
+                    m.tc[blk] = static_cast<uint8_t>(n);
+                    for (int k = 0; k < n; k++) e[ne++] = entry(kZz8[4 * pos[k] + i4], lvl[k]);
+                }
+            }
+            emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
+            continue;
+        }
+        for (int b4 = 0; b4 < 4; b4++) {
+            const int blk = b8 * 4 + b4, bx = kBlkX[blk], by = kBlkY[blk];
+            uint32_t e[16];
+            int ne = 0;
+            if (coded) {
+                const int n = cavlc_block(nc_luma(blk), is16 ? 15 : 16, pos, lvl);
+                if (n < 0) { err_ = -44; return; }
+                m.tc[blk] = static_cast<uint8_t>(n);
+                for (int k = 0; k < n; k++) {
+                    if (is16) {
+                        const int r = kZz4[pos[k] + 1];
+                        mbe[nmb++] = entry((by * 4 + (r >> 2)) * 16 + bx * 4 + (r & 3), lvl[k]);
+                    } else {
+                        e[ne++] = entry(kZz4[pos[k]], lvl[k]);
+                    }
+                }
+            }
+            if (!is16) emit_sparse(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
+        }
+    }
+    if (is16) emit_sparse(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
+    uint32_t ce[2][64];
+    int nce[2] = {0, 0};
+    if (m.cbp >> 4) {
+        for (int c = 0; c < 2; c++) {
+            const int n = cavlc_block(-1, 4, pos, lvl);
+            if (n < 0) { err_ = -44; return; }
+            for (int k = 0; k < n; k++) ce[c][nce[c]++] = entry((pos[k] >> 1) * 4 * 8 + (pos[k] & 1) * 4, lvl[k]);
+        }
+    }
+    if ((m.cbp >> 4) == 2) {
+        for (int c = 0; c < 2; c++)
+            for (int b4 = 0; b4 < 4; b4++) {
+                const int bx = b4 & 1, by = b4 >> 1;
+                const int n = cavlc_block(nc_chroma(m, c, b4), 15, pos, lvl);
+                if (n < 0) { err_ = -44; return; }
+                m.tcc[c][b4] = static_cast<uint8_t>(n);
+                for (int k = 0; k < n; k++) {
+                    const int r = kZz4[pos[k] + 1];
+                    ce[c][nce[c]++] = entry((by * 4 + (r >> 2)) * 8 + bx * 4 + (r & 3), lvl[k]);
+                }
+            }
+    }
+    for (int c = 0; c < 2; c++) {
+        const int off = c == 0 ? p_->cqp : p_->cqp2;
+        const int qpi = std::max(-qpbd_, std::min(51, qp_ + off));
+        emit_sparse(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
+    }
+    if (vb_.overrun()) err_ = -45;
+}
+
 int H264Parser::run(const uint8_t* data, size_t size) {
     std::vector<Nal> nals;
     split_annexb(data, size, nals);
@@ -685,7 +1064,6 @@ int H264Parser::run(const uint8_t* data, size_t size) {
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
             if (slice_type % 5 != 2) { job_.message = "first picture is not intra (P/B slices unsupported)"; return -5; }
-            if (!p.cabac) { job_.message = "CAVLC entropy coding not supported yet"; return -20; }
             if (type == 5) b.ue();
             if (s.poc_type == 0) {
                 b.u(s.log2_max_poc_lsb);
@@ -765,28 +1143,46 @@ int H264Parser::run(const uint8_t* data, size_t size) {
                 job_.message = "scaling matrices changed inside the picture";
                 return -6;
             }
-            b.align();  // cabac_alignment_one_bit
-            const size_t off = b.byte_pos();
-            if (off > rn) { job_.message = "truncated slice"; return -6; }
-            keep.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
-            keep.resize(keep.size() + 8, 0);
-            end_ = keep.data() + (rn - off);
-            cc_.init(keep.data(), end_);
             cur_slice_ = nslice;
             job_.slices.push_back(srec);
             qp_ = p.init_qp + qpd;
             if (qp_ < -qpbd_ || qp_ > 51) { job_.message = "invalid slice QP"; return -6; }
-            for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_state(kInitI[i][0], kInitI[i][1], qp_);
             prev_qpd_nz_ = 0;
             int addr = first_mb;
-            for (;;) {
-                if (addr >= mbw_ * mbh_) { job_.message = "slice overruns the picture"; return -7; }
-                mbx_ = addr % mbw_;
-                mby_ = addr / mbw_;
-                decode_mb();
-                if (err_) { job_.message = "macroblock decode error"; return -7; }
-                if (cc_.terminate()) break;
-                addr++;
+            if (p.cabac) {
+                b.align();  // cabac_alignment_one_bit
+                const size_t off = b.byte_pos();
+                if (off > rn) { job_.message = "truncated slice"; return -6; }
+                keep.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
+                keep.resize(keep.size() + 8, 0);
+                end_ = keep.data() + (rn - off);
+                cc_.init(keep.data(), end_);
+                for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_state(kInitI[i][0], kInitI[i][1], qp_);
+                for (;;) {
+                    if (addr >= mbw_ * mbh_) { job_.message = "slice overruns the picture"; return -7; }
+                    mbx_ = addr % mbw_;
+                    mby_ = addr / mbw_;
+                    decode_mb();
+                    if (err_) { job_.message = "macroblock decode error"; return -7; }
+                    if (cc_.terminate()) break;
+                    addr++;
+                }
+            } else {
+                // CAVLC: macroblocks until the rbsp_stop_one_bit
+                size_t last = rn;
+                while (last > 0 && rbsp_[last - 1] == 0) last--;
+                if (!last) { job_.message = "empty slice data"; return -6; }
+                stop_bit_ = (last - 1) * 8 + 7 - static_cast<size_t>(__builtin_ctz(rbsp_[last - 1]));
+                vb_.init(rbsp_.data(), rn, b.bit_pos());
+                for (;;) {
+                    if (addr >= mbw_ * mbh_) { job_.message = "slice overruns the picture"; return -7; }
+                    mbx_ = addr % mbw_;
+                    mby_ = addr / mbw_;
+                    decode_mb_cavlc();
+                    if (err_) { job_.message = "macroblock decode error"; return -7; }
+                    if (!vb_.more_rbsp_data(stop_bit_)) break;
+                    addr++;
+                }
             }
             if (++nslice >= 255) { job_.message = "too many slices"; return -8; }
         } else if (type == 9 && have) {

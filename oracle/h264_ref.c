@@ -13,7 +13,7 @@
  * test/img/img01.h264, Main profile CABAC) and by img01.h264.jpeg.
  * The 8x8 transform / 8x8 CABAC contexts (High profile) are exercised only by
  * generated vectors: parity for those is pinned to this restatement.
- * CAVLC is not implemented in this round (returns -20).
+ * CAVLC (7.3.5.3.2 / 9.2) with the VLC tables of tools/gen_cavlc_tables.py.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -22,6 +22,7 @@
 
 #include "bits.h"
 #include "cabac_tables.h"
+#include "cavlc_tables.h"
 #include "oracle.h"
 
 /* ------------------------------------------------------------ CABAC init (I slices) */
@@ -308,6 +309,8 @@ typedef struct {
     uint8_t cbf[16];    /* luma 4x4 coded_block_flag (8x8: replicated) */
     uint8_t cbf_c[2][4];/* chroma AC */
     uint8_t cbf_dc[3];  /* luma DC (I16x16), Cb DC, Cr DC */
+    uint8_t tc[16];     /* CAVLC: TotalCoeff of each luma 4x4 block (I16x16: AC block) */
+    uint8_t tcc[2][4];  /* CAVLC: TotalCoeff of each chroma AC block */
 } MbInfo;
 
 typedef struct {
@@ -920,6 +923,101 @@ static int pred_mode_nb(H4Dec *d, int blk, int is8x8, int dir /* 0 A left, 1 B t
     return N->ipm[nblk];
 }
 
+/* ---- reconstruction of one macroblock from the parsed levels (8.3, 8.5) ---- */
+static int recon_mb(H4Dec *d, MbInfo *m) {
+    const int gx = d->mbx * 16, gy = d->mby * 16;
+    /* ---- reconstruction ---- */
+    const int qp = d->qp + d->qpbd; /* QP'Y */
+    const int qm = qp % 6, qd = qp / 6;
+    int pred[256], res[64];
+    if (m->mb_type == MB_I_NXN && !m->t8x8) {
+        const uint8_t *w = d->p->sl4[0];
+        for (int blk = 0; blk < 16; blk++) {
+            pred4x4(d, blk, m->ipm[blk], pred);
+            int r[16];
+            for (int i = 0; i < 16; i++) {
+                int ls = ws4(w, i) * norm4(qm, i >> 2, i & 3);
+                r[i] = qp >= 24 ? (d->lvl4[blk][i] * ls) << (qd - 4) : (d->lvl4[blk][i] * ls + (1 << (3 - qd))) >> (4 - qd);
+            }
+            idct4(r);
+            put_block(d, 0, gx + k_blk_x[blk] * 4, gy + k_blk_y[blk] * 4, 4, pred, r);
+        }
+    } else if (m->mb_type == MB_I_NXN) {
+        const uint8_t *w = d->p->sl8[0];
+        for (int b8 = 0; b8 < 4; b8++) {
+            pred8x8(d, b8, m->ipm[b8 * 4], pred);
+            for (int i = 0; i < 64; i++) {
+                int ls = ws8(w, i) * norm8(qm, i >> 3, i & 7);
+                res[i] = qp >= 36 ? (d->lvl8[b8][i] * ls) << (qd - 6) : (d->lvl8[b8][i] * ls + (1 << (5 - qd))) >> (6 - qd);
+            }
+            idct8(res);
+            put_block(d, 0, gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 8, pred, res);
+        }
+    } else {
+        pred16x16(d, (m->mb_type - 1) % 4, pred);
+        const uint8_t *w = d->p->sl4[0];
+        /* luma DC: Hadamard then scale */
+        int f[16], c4[16];
+        memcpy(c4, d->dc_l, sizeof(c4));
+        for (int i = 0; i < 4; i++) { /* rows */
+            int *r = c4 + i * 4;
+            int a = r[0] + r[1], b = r[0] - r[1], cc = r[2] + r[3], dd = r[2] - r[3];
+            f[i * 4 + 0] = a + cc; f[i * 4 + 1] = a - cc; f[i * 4 + 2] = b - dd; f[i * 4 + 3] = b + dd;
+        }
+        int g[16];
+        for (int j = 0; j < 4; j++) {
+            int a = f[j] + f[4 + j], b = f[j] - f[4 + j], cc = f[8 + j] + f[12 + j], dd = f[8 + j] - f[12 + j];
+            g[j] = a + cc; g[4 + j] = a - cc; g[8 + j] = b - dd; g[12 + j] = b + dd;
+        }
+        int ls0 = ws4(w, 0) * norm4(qm, 0, 0);
+        int dcs[16];
+        for (int i = 0; i < 16; i++)
+            dcs[i] = qp >= 36 ? (g[i] * ls0) << (qd - 6) : (g[i] * ls0 + (1 << (5 - qd))) >> (6 - qd);
+        for (int blk = 0; blk < 16; blk++) {
+            int bx = k_blk_x[blk], by = k_blk_y[blk];
+            int r[16];
+            for (int i = 0; i < 16; i++) {
+                int ls = ws4(w, i) * norm4(qm, i >> 2, i & 3);
+                r[i] = qp >= 24 ? (d->lvl4[blk][i] * ls) << (qd - 4) : (d->lvl4[blk][i] * ls + (1 << (3 - qd))) >> (4 - qd);
+            }
+            r[0] = dcs[by * 4 + bx];
+            idct4(r);
+            int p4[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) p4[y * 4 + x] = pred[(by * 4 + y) * 16 + bx * 4 + x];
+            put_block(d, 0, gx + bx * 4, gy + by * 4, 4, p4, r);
+        }
+    }
+    /* chroma */
+    for (int c = 0; c < 2; c++) {
+        int off = c == 0 ? d->p->chroma_qp_offset : d->p->chroma_qp_offset2;
+        int qpc = chroma_qp(clip3(-d->qpbdc, 51, d->qp + off)) + d->qpbdc;
+        int cm = qpc % 6, cd = qpc / 6;
+        const uint8_t *w = d->p->sl4[1 + c];
+        pred_chroma(d, 1 + c, m->cpm, pred);
+        int *dc = d->dc_c[c];
+        int f0 = dc[0] + dc[1] + dc[2] + dc[3], f1 = dc[0] - dc[1] + dc[2] - dc[3];
+        int f2 = dc[0] + dc[1] - dc[2] - dc[3], f3 = dc[0] - dc[1] - dc[2] + dc[3];
+        int fc[4] = {f0, f1, f2, f3};
+        int ls0 = ws4(w, 0) * norm4(cm, 0, 0);
+        for (int b4 = 0; b4 < 4; b4++) {
+            int r[16];
+            for (int i = 0; i < 16; i++) {
+                int ls = ws4(w, i) * norm4(cm, i >> 2, i & 3);
+                r[i] = qpc >= 24 ? (d->ac_c[c][b4][i] * ls) << (cd - 4) : (d->ac_c[c][b4][i] * ls + (1 << (3 - cd))) >> (4 - cd);
+            }
+            r[0] = ((fc[b4] * ls0) << cd) >> 5;
+            idct4(r);
+            int bx = b4 & 1, by = b4 >> 1;
+            int p4[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) p4[y * 4 + x] = pred[(by * 4 + y) * 8 + bx * 4 + x];
+            put_block(d, 1 + c, gx / 2 + bx * 4, gy / 2 + by * 4, 4, p4, r);
+        }
+    }
+    return 0;
+}
+
 static int decode_mb(H4Dec *d, int slice_idx) {
     MbInfo *m = &d->mb[d->mby * d->mbw + d->mbx];
     memset(m, 0, sizeof(*m));
@@ -1041,96 +1139,230 @@ static int decode_mb(H4Dec *d, int slice_idx) {
                 for (int k = 0; k < 15; k++) d->ac_c[c][b4][k_zz4[k + 1]] = coef[k];
             }
     }
-    /* ---- reconstruction ---- */
-    const int qp = d->qp + d->qpbd; /* QP'Y */
-    const int qm = qp % 6, qd = qp / 6;
-    int pred[256], res[64];
-    if (m->mb_type == MB_I_NXN && !m->t8x8) {
-        const uint8_t *w = d->p->sl4[0];
-        for (int blk = 0; blk < 16; blk++) {
-            pred4x4(d, blk, m->ipm[blk], pred);
-            int r[16];
-            for (int i = 0; i < 16; i++) {
-                int ls = ws4(w, i) * norm4(qm, i >> 2, i & 3);
-                r[i] = qp >= 24 ? (d->lvl4[blk][i] * ls) << (qd - 4) : (d->lvl4[blk][i] * ls + (1 << (3 - qd))) >> (4 - qd);
-            }
-            idct4(r);
-            put_block(d, 0, gx + k_blk_x[blk] * 4, gy + k_blk_y[blk] * 4, 4, pred, r);
+    return recon_mb(d, m);
+}
+
+/* ------------------------------------------------------------ CAVLC (7.3.5.3.2, 9.2) */
+static int vlc_read(OraBits *b, const uint8_t *lens, const void *codes, int wide, int n) {
+    uint32_t code = 0;
+    for (int len = 1; len <= 16; len++) {
+        code = (code << 1) | (uint32_t)ob_bit(b);
+        for (int i = 0; i < n; i++) {
+            uint32_t c = wide ? ((const uint16_t *)codes)[i] : ((const uint8_t *)codes)[i];
+            if (lens[i] == len && c == code) return i;
         }
-    } else if (m->mb_type == MB_I_NXN) {
-        const uint8_t *w = d->p->sl8[0];
-        for (int b8 = 0; b8 < 4; b8++) {
-            pred8x8(d, b8, m->ipm[b8 * 4], pred);
-            for (int i = 0; i < 64; i++) {
-                int ls = ws8(w, i) * norm8(qm, i >> 3, i & 7);
-                res[i] = qp >= 36 ? (d->lvl8[b8][i] * ls) << (qd - 6) : (d->lvl8[b8][i] * ls + (1 << (5 - qd))) >> (6 - qd);
-            }
-            idct8(res);
-            put_block(d, 0, gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 8, pred, res);
+    }
+    return -1;
+}
+
+/* coeff_token (9.2.1): returns TotalCoeff, *t1 = TrailingOnes; -1 on error */
+static int cavlc_coeff_token(OraBits *b, int nC, int *t1) {
+    if (nC >= 8) {
+        int v = (int)ob_u(b, 6);
+        if (v == 3) { *t1 = 0; return 0; }
+        *t1 = v & 3;
+        if ((v >> 2) + 1 < *t1) return -1;
+        return (v >> 2) + 1;
+    }
+    int col = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+    uint32_t code = 0;
+    for (int len = 1; len <= 16; len++) {
+        code = (code << 1) | (uint32_t)ob_bit(b);
+        for (int t = 0; t < 4; t++)
+            for (int tc = 0; tc <= 16; tc++)
+                if (kCoeffTokenLen[col][t][tc] == len && kCoeffTokenCode[col][t][tc] == code) {
+                    *t1 = t;
+                    return tc;
+                }
+    }
+    return -1;
+}
+
+/* residual_block_cavlc: coeffLevel[0..maxNum-1] in scan order; returns TotalCoeff (-1 error) */
+static int cavlc_block(H4Dec *d, int nC, int maxNum, int *out) {
+    OraBits *b = &d->bits;
+    memset(out, 0, sizeof(int) * maxNum);
+    int t1, tc = cavlc_coeff_token(b, nC, &t1);
+    if (tc < 0 || tc > maxNum) return -1;
+    if (tc == 0) return 0;
+    int level[16], run[16];
+    int suffixLength = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int i = 0; i < tc; i++) {
+        if (i < t1) {
+            level[i] = ob_bit(b) ? -1 : 1;
+            continue;
+        }
+        int prefix = 0;
+        while (!ob_bit(b)) {
+            if (++prefix > 32) return -1;
+        }
+        int levelCode = (prefix < 15 ? prefix : 15) << suffixLength;
+        int sz = (prefix == 14 && suffixLength == 0) ? 4 : (prefix >= 15 ? prefix - 3 : suffixLength);
+        if (sz > 0) levelCode += (int)ob_u(b, sz);
+        if (prefix >= 15 && suffixLength == 0) levelCode += 15;
+        if (prefix >= 16) levelCode += (1 << (prefix - 3)) - 4096;
+        if (i == t1 && t1 < 3) levelCode += 2;
+        level[i] = (levelCode % 2 == 0) ? (levelCode + 2) >> 1 : (-levelCode - 1) >> 1;
+        if (suffixLength == 0) suffixLength = 1;
+        if (abs(level[i]) > (3 << (suffixLength - 1)) && suffixLength < 6) suffixLength++;
+    }
+    int zerosLeft = 0;
+    if (tc < maxNum) {
+        if (maxNum == 4) zerosLeft = vlc_read(b, kTotalZerosDcLen[tc - 1], kTotalZerosDcCode[tc - 1], 0, 5 - tc);
+        else zerosLeft = vlc_read(b, kTotalZerosLen[tc - 1], kTotalZerosCode[tc - 1], 0, 17 - tc);
+        if (zerosLeft < 0 || zerosLeft > maxNum - tc) return -1;
+    }
+    for (int i = 0; i < tc - 1; i++) {
+        if (zerosLeft > 0) {
+            int zl = zerosLeft < 7 ? zerosLeft : 7;
+            int r = vlc_read(b, kRunBeforeLen[zl - 1], kRunBeforeCode[zl - 1], 1, zl < 7 ? zl + 1 : 15);
+            if (r < 0 || r > zerosLeft) return -1;
+            run[i] = r;
+            zerosLeft -= r;
+        } else {
+            run[i] = 0;
+        }
+    }
+    run[tc - 1] = zerosLeft;
+    int coeffNum = -1;
+    for (int i = tc - 1; i >= 0; i--) {
+        coeffNum += run[i] + 1;
+        out[coeffNum] = level[i];
+    }
+    return tc;
+}
+
+/* nC for a luma 4x4 block (9.2.1): neighbours' TotalCoeff, I_PCM = 16 */
+static int cavlc_nc_luma(H4Dec *d, int blk) {
+    int bx = k_blk_x[blk], by = k_blk_y[blk], na = 0, nb = 0, nblk;
+    MbInfo *A = nb_blk(d, bx - 1, by, &nblk);
+    if (A) na = A->mb_type == MB_I_PCM ? 16 : A->tc[nblk];
+    MbInfo *B = nb_blk(d, bx, by - 1, &nblk);
+    if (B) nb = B->mb_type == MB_I_PCM ? 16 : B->tc[nblk];
+    if (A && B) return (na + nb + 1) >> 1;
+    return A ? na : (B ? nb : 0);
+}
+static int cavlc_nc_chroma(H4Dec *d, MbInfo *m, int c, int b4) {
+    int bx = b4 & 1, by = b4 >> 1, na = 0, nb = 0, aa = 1, ab = 1;
+    if (bx) na = m->tcc[c][b4 - 1];
+    else {
+        MbInfo *A = nb_mb(d, -1, 0);
+        if (!A) aa = 0;
+        else na = A->mb_type == MB_I_PCM ? 16 : A->tcc[c][b4 + 1];
+    }
+    if (by) nb = m->tcc[c][b4 - 2];
+    else {
+        MbInfo *B = nb_mb(d, 0, -1);
+        if (!B) ab = 0;
+        else nb = B->mb_type == MB_I_PCM ? 16 : B->tcc[c][b4 + 2];
+    }
+    if (aa && ab) return (na + nb + 1) >> 1;
+    return aa ? na : (ab ? nb : 0);
+}
+
+static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
+    MbInfo *m = &d->mb[d->mby * d->mbw + d->mbx];
+    memset(m, 0, sizeof(*m));
+    m->slice = slice_idx;
+    OraBits *b = &d->bits;
+    uint32_t mbt = ob_ue(b);
+    if (mbt > 25) return -1;
+    m->mb_type = (int)mbt;
+    const int gx = d->mbx * 16, gy = d->mby * 16;
+    if (m->mb_type == MB_I_PCM) {
+        b->pos = (b->pos + 7) & ~7L;
+        for (int y = 0; y < 16; y++)
+            for (int x = 0; x < 16; x++) d->pl[0][(gy + y) * d->st[0] + gx + x] = (uint16_t)ob_u(b, d->bd);
+        for (int c = 1; c < 3; c++)
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) d->pl[c][(gy / 2 + y) * d->st[c] + gx / 2 + x] = (uint16_t)ob_u(b, d->bdc);
+        m->qp = d->qp;
+        m->cbp = 0x2F;
+        memset(m->tc, 16, sizeof(m->tc));
+        memset(m->tcc, 16, sizeof(m->tcc));
+        for (int i = 0; i < 16; i++) m->ipm[i] = 2;
+        return 0;
+    }
+    int is16 = m->mb_type >= 1 && m->mb_type <= 24;
+    if (m->mb_type == MB_I_NXN && d->p->transform_8x8) m->t8x8 = ob_bit(b);
+    if (m->mb_type == MB_I_NXN) {
+        int nb = m->t8x8 ? 4 : 16;
+        for (int i = 0; i < nb; i++) {
+            int blk = m->t8x8 ? i * 4 : i;
+            int prev = ob_bit(b);
+            int rem = prev ? 0 : (int)ob_u(b, 3);
+            int a = pred_mode_nb(d, blk, m->t8x8, 0), bb = pred_mode_nb(d, blk, m->t8x8, 1);
+            int pm = (a < 0 || bb < 0) ? 2 : (a < bb ? a : bb);
+            int mode = prev ? pm : (rem < pm ? rem : rem + 1);
+            if (m->t8x8) for (int k = 0; k < 4; k++) m->ipm[blk + k] = (uint8_t)mode;
+            else m->ipm[blk] = (uint8_t)mode;
         }
     } else {
-        pred16x16(d, (m->mb_type - 1) % 4, pred);
-        const uint8_t *w = d->p->sl4[0];
-        /* luma DC: Hadamard then scale */
-        int f[16], c4[16];
-        memcpy(c4, d->dc_l, sizeof(c4));
-        for (int i = 0; i < 4; i++) { /* rows */
-            int *r = c4 + i * 4;
-            int a = r[0] + r[1], b = r[0] - r[1], cc = r[2] + r[3], dd = r[2] - r[3];
-            f[i * 4 + 0] = a + cc; f[i * 4 + 1] = a - cc; f[i * 4 + 2] = b - dd; f[i * 4 + 3] = b + dd;
-        }
-        int g[16];
-        for (int j = 0; j < 4; j++) {
-            int a = f[j] + f[4 + j], b = f[j] - f[4 + j], cc = f[8 + j] + f[12 + j], dd = f[8 + j] - f[12 + j];
-            g[j] = a + cc; g[4 + j] = a - cc; g[8 + j] = b - dd; g[12 + j] = b + dd;
-        }
-        int ls0 = ws4(w, 0) * norm4(qm, 0, 0);
-        int dcs[16];
-        for (int i = 0; i < 16; i++)
-            dcs[i] = qp >= 36 ? (g[i] * ls0) << (qd - 6) : (g[i] * ls0 + (1 << (5 - qd))) >> (6 - qd);
-        for (int blk = 0; blk < 16; blk++) {
-            int bx = k_blk_x[blk], by = k_blk_y[blk];
-            int r[16];
-            for (int i = 0; i < 16; i++) {
-                int ls = ws4(w, i) * norm4(qm, i >> 2, i & 3);
-                r[i] = qp >= 24 ? (d->lvl4[blk][i] * ls) << (qd - 4) : (d->lvl4[blk][i] * ls + (1 << (3 - qd))) >> (4 - qd);
-            }
-            r[0] = dcs[by * 4 + bx];
-            idct4(r);
-            int p4[16];
-            for (int y = 0; y < 4; y++)
-                for (int x = 0; x < 4; x++) p4[y * 4 + x] = pred[(by * 4 + y) * 16 + bx * 4 + x];
-            put_block(d, 0, gx + bx * 4, gy + by * 4, 4, p4, r);
-        }
+        for (int i = 0; i < 16; i++) m->ipm[i] = 2;
     }
-    /* chroma */
-    for (int c = 0; c < 2; c++) {
-        int off = c == 0 ? d->p->chroma_qp_offset : d->p->chroma_qp_offset2;
-        int qpc = chroma_qp(clip3(-d->qpbdc, 51, d->qp + off)) + d->qpbdc;
-        int cm = qpc % 6, cd = qpc / 6;
-        const uint8_t *w = d->p->sl4[1 + c];
-        pred_chroma(d, 1 + c, m->cpm, pred);
-        int *dc = d->dc_c[c];
-        int f0 = dc[0] + dc[1] + dc[2] + dc[3], f1 = dc[0] - dc[1] + dc[2] - dc[3];
-        int f2 = dc[0] + dc[1] - dc[2] - dc[3], f3 = dc[0] - dc[1] - dc[2] + dc[3];
-        int fc[4] = {f0, f1, f2, f3};
-        int ls0 = ws4(w, 0) * norm4(cm, 0, 0);
+    uint32_t cpm = ob_ue(b);
+    if (cpm > 3) return -1;
+    m->cpm = (int)cpm;
+    if (is16) {
+        int t = m->mb_type - 1;
+        m->cbp = ((t / 4) % 3) << 4 | (t >= 12 ? 15 : 0);
+    } else {
+        uint32_t cn = ob_ue(b);
+        if (cn > 47) return -1;
+        m->cbp = kCbpIntra[cn];
+    }
+    if ((m->cbp & 15) || (m->cbp >> 4) || is16) {
+        int qpd = ob_se(b);
+        d->qp = ((d->qp + qpd + 52 + 2 * d->qpbd) % (52 + d->qpbd)) - d->qpbd;
+    }
+    m->qp = d->qp;
+    int coef[64];
+    memset(d->lvl4, 0, sizeof(d->lvl4));
+    memset(d->lvl8, 0, sizeof(d->lvl8));
+    memset(d->dc_l, 0, sizeof(d->dc_l));
+    memset(d->dc_c, 0, sizeof(d->dc_c));
+    memset(d->ac_c, 0, sizeof(d->ac_c));
+    if (is16) {
+        if (cavlc_block(d, cavlc_nc_luma(d, 0), 16, coef) < 0) return -1;
+        for (int k = 0; k < 16; k++) d->dc_l[k_zz4[k]] = coef[k];
+    }
+    for (int b8 = 0; b8 < 4; b8++) {
+        if (!((m->cbp >> b8) & 1)) continue;
+        if (m->t8x8) {
+            for (int i4 = 0; i4 < 4; i4++) {
+                int blk = b8 * 4 + i4;
+                int tc = cavlc_block(d, cavlc_nc_luma(d, blk), 16, coef);
+                if (tc < 0) return -1;
+                m->tc[blk] = (uint8_t)tc;
+                for (int k = 0; k < 16; k++) d->lvl8[b8][k_zz8[4 * k + i4]] = coef[k];
+            }
+            continue;
+        }
         for (int b4 = 0; b4 < 4; b4++) {
-            int r[16];
-            for (int i = 0; i < 16; i++) {
-                int ls = ws4(w, i) * norm4(cm, i >> 2, i & 3);
-                r[i] = qpc >= 24 ? (d->ac_c[c][b4][i] * ls) << (cd - 4) : (d->ac_c[c][b4][i] * ls + (1 << (3 - cd))) >> (4 - cd);
-            }
-            r[0] = ((fc[b4] * ls0) << cd) >> 5;
-            idct4(r);
-            int bx = b4 & 1, by = b4 >> 1;
-            int p4[16];
-            for (int y = 0; y < 4; y++)
-                for (int x = 0; x < 4; x++) p4[y * 4 + x] = pred[(by * 4 + y) * 8 + bx * 4 + x];
-            put_block(d, 1 + c, gx / 2 + bx * 4, gy / 2 + by * 4, 4, p4, r);
+            int blk = b8 * 4 + b4;
+            int tc = cavlc_block(d, cavlc_nc_luma(d, blk), is16 ? 15 : 16, coef);
+            if (tc < 0) return -1;
+            m->tc[blk] = (uint8_t)tc;
+            if (is16) for (int k = 0; k < 15; k++) d->lvl4[blk][k_zz4[k + 1]] = coef[k];
+            else for (int k = 0; k < 16; k++) d->lvl4[blk][k_zz4[k]] = coef[k];
         }
     }
-    return 0;
+    if (m->cbp >> 4) {
+        for (int c = 0; c < 2; c++) {
+            if (cavlc_block(d, -1, 4, coef) < 0) return -1;
+            for (int k = 0; k < 4; k++) d->dc_c[c][k] = coef[k];
+        }
+    }
+    if ((m->cbp >> 4) == 2) {
+        for (int c = 0; c < 2; c++)
+            for (int b4 = 0; b4 < 4; b4++) {
+                int tc = cavlc_block(d, cavlc_nc_chroma(d, m, c, b4), 15, coef);
+                if (tc < 0) return -1;
+                m->tcc[c][b4] = (uint8_t)tc;
+                for (int k = 0; k < 15; k++) d->ac_c[c][b4][k_zz4[k + 1]] = coef[k];
+            }
+    }
+    return recon_mb(d, m);
 }
 
 /* ------------------------------------------------------------ deblocking (8.7) */
@@ -1276,7 +1508,6 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             int frame_num = (int)ob_u(&b, s->log2_max_frame_num);
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
             if (slice_type % 5 != 2) { ret = -5; goto done; } /* P/B: the first picture must be intra */
-            if (!p->cabac) { ret = -20; goto done; }          /* CAVLC: not in this round */
             if (type == 5) ob_ue(&b);                          /* idr_pic_id */
             if (s->poc_type == 0) {
                 ob_u(&b, s->log2_max_poc_lsb);
@@ -1334,22 +1565,35 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 first_idr = type == 5;
             }
             d->p = p;
-            /* cabac_alignment_one_bit */
-            while (b.pos & 7) ob_u(&b, 1);
-            d->bits = b;
-            oc_init(&d->cc, &d->bits);
             d->qp = p->init_qp + qpd;
-            init_ctx(d, d->qp);
             d->prev_qpd_nz = 0;
             int mbaddr = first_mb;
-            for (;;) {
-                if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
-                d->mbx = mbaddr % d->mbw;
-                d->mby = mbaddr / d->mbw;
-                d->mb[mbaddr].slice = d->nslice;
-                decode_mb(d, d->nslice);
-                if (oc_terminate(&d->cc)) break;
-                mbaddr++;
+            if (p->cabac) {
+                /* cabac_alignment_one_bit */
+                while (b.pos & 7) ob_u(&b, 1);
+                d->bits = b;
+                oc_init(&d->cc, &d->bits);
+                init_ctx(d, d->qp);
+                for (;;) {
+                    if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
+                    d->mbx = mbaddr % d->mbw;
+                    d->mby = mbaddr / d->mbw;
+                    d->mb[mbaddr].slice = d->nslice;
+                    decode_mb(d, d->nslice);
+                    if (oc_terminate(&d->cc)) break;
+                    mbaddr++;
+                }
+            } else {
+                d->bits = b;
+                for (;;) {
+                    if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
+                    d->mbx = mbaddr % d->mbw;
+                    d->mby = mbaddr / d->mbw;
+                    d->mb[mbaddr].slice = d->nslice;
+                    if (decode_mb_cavlc(d, d->nslice) < 0) { ret = -21; goto done_free; }
+                    if (!ob_more_rbsp(&d->bits)) break;
+                    mbaddr++;
+                }
             }
             d->nslice++;
             if (d->nslice >= 256) { ret = -8; goto done_free; }

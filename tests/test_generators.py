@@ -1,0 +1,73 @@
+"""CPU: the test-vector encoders (tools/hevcgen, tools/h264gen) and the oracle
+agree bit-for-bit on the pre-loop-filter reconstruction, across the coding
+tools the parity vectors exercise (incl. H.264 CAVLC, which has no reference
+fixture: parity for it is pinned only by this round trip and the spec-table
+structure checks of tools/gen_cavlc_tables.py)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _build(name):
+    src = os.path.join(ROOT, "tools", name, name + ".c")
+    exe = os.path.join(ROOT, "tools", name, name)
+    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O2", "-o", exe, src, "-lm"])
+    return exe
+
+
+def _roundtrip(tmp_path, gen, codec, W, H, bd, qp, seed, opts):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W]
+    maxv = (1 << bd) - 1
+    base = (np.sin(xx / 7.0) * 0.3 + np.cos(yy / 11.0) * 0.3 + 0.5) * maxv
+    planes = [np.clip(base + rng.normal(0, 0.04 * maxv, base.shape), 0, maxv)]
+    for c in range(2):
+        planes.append(np.clip(base[::2, ::2] * (0.6 + 0.2 * c) + rng.normal(0, 0.02 * maxv, (H // 2, W // 2)), 0, maxv))
+    dt = np.uint8 if bd == 8 else np.dtype("<u2")
+    yuv, out, rec = tmp_path / "in.yuv", tmp_path / "out.bin", tmp_path / "rec.yuv"
+    with open(yuv, "wb") as f:
+        for p in planes:
+            f.write(np.rint(p).astype(dt).tobytes())
+    subprocess.check_call([gen, str(yuv), str(W), str(H), str(bd), str(qp), str(seed), str(out), "--recon", str(rec)] + opts)
+    y, u, v, obd = O.decode(open(out, "rb").read(), codec, skip_loop_filter=True)
+    r = np.fromfile(rec, dtype=dt).astype(np.int32)
+    ys, cs = W * H, (W // 2) * (H // 2)
+    assert obd == bd
+    assert np.array_equal(y, r[:ys].reshape(H, W))
+    assert np.array_equal(u, r[ys:ys + cs].reshape(H // 2, W // 2))
+    assert np.array_equal(v, r[ys + cs:].reshape(H // 2, W // 2))
+
+
+H264_CASES = [
+    ("cabac_main", 96, 64, 8, 28, ["--t8x8", "0"]),
+    ("cabac_high_pcm_slices", 128, 96, 8, 20, ["--pcm", "1", "--slices", "2"]),
+    ("cabac_10bit", 96, 64, 10, 16, []),
+    ("cavlc_main", 96, 64, 8, 28, ["--cavlc", "1", "--t8x8", "0"]),
+    ("cavlc_high8x8_pcm", 128, 96, 8, 18, ["--cavlc", "1", "--pcm", "1"]),
+    ("cavlc_q0_big_levels", 64, 64, 8, 0, ["--cavlc", "1"]),
+    ("cavlc_10bit_slices", 128, 64, 10, 10, ["--cavlc", "1", "--slices", "2", "--cqp", "-3"]),
+]
+
+
+@pytest.mark.parametrize("name,W,H,bd,qp,opts", H264_CASES, ids=[c[0] for c in H264_CASES])
+def test_h264gen_oracle_roundtrip(tmp_path, name, W, H, bd, qp, opts):
+    _roundtrip(tmp_path, _build("h264gen"), 264, W, H, bd, qp, 7, opts)
+
+
+HEVC_CASES = [
+    ("default", 96, 64, 8, 27, []),
+    ("pcm_bypass_slices", 128, 96, 8, 22, ["--pcm", "1", "--bypass", "1", "--slices", "1"]),
+    ("ctb16_10bit", 96, 64, 10, 12, ["--ctb", "16"]),
+]
+
+
+@pytest.mark.parametrize("name,W,H,bd,qp,opts", HEVC_CASES, ids=[c[0] for c in HEVC_CASES])
+def test_hevcgen_oracle_roundtrip(tmp_path, name, W, H, bd, qp, opts):
+    _roundtrip(tmp_path, _build("hevcgen"), 265, W, H, bd, qp, 5, opts)

@@ -16,7 +16,7 @@
  *
  * usage: h264gen in.yuv W H bitdepth qp seed out.h264 [options]
  *   --t8x8 0|1 --pcm 0|1 --qpdelta 0|1 --slices N(MB rows, 0 = one)
- *   --alpha A --beta B (div2 offsets) --dbidc 0|1|2 --cqp N --cqp2 N --recon out.yuv
+ *   --alpha A --beta B (div2 offsets) --dbidc 0|1|2 --cqp N --cqp2 N --cavlc 0|1 --recon out.yuv
  */
 #include <math.h>
 #include <stdint.h>
@@ -26,6 +26,7 @@
 
 #include "../../oracle/bits.h"
 #include "../../oracle/cabac_tables.h"
+#include "cavlc_tables.h"
 
 static uint64_t g_rng = 1;
 static uint32_t rnd(void) {
@@ -167,10 +168,11 @@ static const uint8_t k_blk_of[4][4] = {{0, 1, 4, 5}, {2, 3, 6, 7}, {8, 9, 12, 13
 typedef struct {
     int slice, mb_type, t8x8, cbp, qp, cpm;
     uint8_t ipm[16], cbf[16], cbf_c[2][4], cbf_dc[3];
+    uint8_t tc[16], tcc[2][4];  /* CAVLC TotalCoeff per luma / chroma AC 4x4 block */
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc;
     uint16_t *src[3], *rec[3];
     int st[3];
     Mb *mb;
@@ -467,6 +469,77 @@ static void quantize(const Basis *B, const int *x, int *lv, int maxlev) {
 /* ------------------------------------------------------------ CABAC syntax */
 static int bin(G *g, int ctx, int v) { ce_bin(&g->ce, &g->ctx[ctx], v); return v; }
 
+/* ------------------------------------------------------------ CAVLC (9.2) */
+static int cavlc_nc(int na, int aa, int nb_, int ab) {
+    if (aa && ab) return (na + nb_ + 1) >> 1;
+    return aa ? na : (ab ? nb_ : 0);
+}
+/* residual_block_cavlc for coefficients co[0..maxnum-1] in scan order; returns TotalCoeff */
+static int enc_block_cavlc(G *g, int nC, int maxnum, const int *co) {
+    BW *b = g->ce.bw;
+    int idx[16], lv[16], tc = 0;
+    for (int i = maxnum - 1; i >= 0; i--)
+        if (co[i]) { idx[tc] = i; lv[tc] = co[i]; tc++; }  /* highest frequency first */
+    int t1 = 0;
+    while (t1 < tc && t1 < 3 && abs(lv[t1]) == 1) t1++;
+    if (nC >= 8) {
+        bw_put(b, tc ? (uint32_t)(((tc - 1) << 2) | t1) : 3u, 6);
+    } else {
+        int col = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+        bw_put(b, kCoeffTokenCode[col][t1][tc], kCoeffTokenLen[col][t1][tc]);
+    }
+    if (!tc) return 0;
+    for (int i = 0; i < t1; i++) bw_put(b, lv[i] < 0, 1);
+    int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (int i = t1; i < tc; i++) {
+        int code = lv[i] > 0 ? 2 * lv[i] - 2 : -2 * lv[i] - 1;
+        if (i == t1 && t1 < 3) code -= 2;
+        int prefix, ssz, suffix;
+        if (sl == 0) {
+            if (code < 14) { prefix = code; ssz = 0; suffix = 0; }
+            else if (code < 30) { prefix = 14; ssz = 4; suffix = code - 14; }
+            else { prefix = 15; ssz = 12; suffix = code - 30; }
+        } else if (code < (15 << sl)) {
+            prefix = code >> sl; ssz = sl; suffix = code & ((1 << sl) - 1);
+        } else {
+            prefix = 15; ssz = 12; suffix = code - (15 << sl);
+        }
+        if (suffix >= 4096) { fprintf(stderr, "level out of CAVLC range\n"); exit(3); }
+        bw_put(b, 1, prefix + 1);  /* prefix zeros then 1 */
+        if (ssz) bw_put(b, (uint32_t)suffix, ssz);
+        if (sl == 0) sl = 1;
+        if (abs(lv[i]) > (3 << (sl - 1)) && sl < 6) sl++;
+    }
+    int zeros = idx[0] + 1 - tc;
+    if (tc < maxnum) {
+        if (maxnum == 4) bw_put(b, kTotalZerosDcCode[tc - 1][zeros], kTotalZerosDcLen[tc - 1][zeros]);
+        else bw_put(b, kTotalZerosCode[tc - 1][zeros], kTotalZerosLen[tc - 1][zeros]);
+    }
+    for (int i = 0; i < tc - 1 && zeros > 0; i++) {
+        int run = idx[i] - idx[i + 1] - 1;
+        int zl = zeros < 7 ? zeros : 7;
+        bw_put(b, kRunBeforeCode[zl - 1][run], kRunBeforeLen[zl - 1][run]);
+        zeros -= run;
+    }
+    return tc;
+}
+static int nc_luma(G *g, int blk) {
+    int nblk, va = 0, vb = 0;
+    Mb *A = nb_blk(g, k_blk_x[blk] - 1, k_blk_y[blk], &nblk);
+    if (A) va = A->mb_type == 25 ? 16 : A->tc[nblk];
+    Mb *B = nb_blk(g, k_blk_x[blk], k_blk_y[blk] - 1, &nblk);
+    if (B) vb = B->mb_type == 25 ? 16 : B->tc[nblk];
+    return cavlc_nc(va, A != NULL, vb, B != NULL);
+}
+static int nc_chroma(G *g, Mb *m, int c, int b4) {
+    int bx = b4 & 1, by = b4 >> 1, va = 0, vb = 0, aa = 1, ab = 1;
+    if (bx) va = m->tcc[c][b4 - 1];
+    else { Mb *A = nb(g, -1, 0); if (!A) aa = 0; else va = A->mb_type == 25 ? 16 : A->tcc[c][b4 + 1]; }
+    if (by) vb = m->tcc[c][b4 - 2];
+    else { Mb *B = nb(g, 0, -1); if (!B) ab = 0; else vb = B->mb_type == 25 ? 16 : B->tcc[c][b4 + 2]; }
+    return cavlc_nc(va, aa, vb, ab);
+}
+
 static int cbf_cond(int cat, Mb *N, int nblk, int icbcr) {
     if (!N) return 1;
     if (N->mb_type == 25) return 1;
@@ -557,10 +630,14 @@ static void encode_mb(G *g) {
     int new_qp = g->cur_qp;
     if (g->qpdelta && rndn(4) == 0) new_qp = clip3(-6 * (g->bd - 8), 51, g->qp + rndn(7) - 3);
     if (pcm) {
-        bin(g, 3 + ctx, 1);
-        ce_term(&g->ce, 1);
-        ce_finish(&g->ce);
-        bw_put(g->ce.bw, 1, 1);
+        if (g->cavlc) {
+            bw_ue(g->ce.bw, 25);
+        } else {
+            bin(g, 3 + ctx, 1);
+            ce_term(&g->ce, 1);
+            ce_finish(&g->ce);
+            bw_put(g->ce.bw, 1, 1);
+        }
         bw_align_zero(g->ce.bw);
         for (int y = 0; y < 16; y++) for (int x = 0; x < 16; x++) {
             int s = g->src[0][(gy + y) * g->st[0] + gx + x];
@@ -572,8 +649,9 @@ static void encode_mb(G *g) {
             bw_put(g->ce.bw, (uint32_t)s, g->bd);
             g->rec[c][(gy / 2 + y) * g->st[c] + gx / 2 + x] = (uint16_t)s;
         }
-        { BW *bw = g->ce.bw; ce_start(&g->ce, bw); }
+        if (!g->cavlc) { BW *bw = g->ce.bw; ce_start(&g->ce, bw); }
         m->mb_type = 25; m->qp = g->cur_qp; m->cbp = 0x2F;
+        memset(m->tc, 16, sizeof(m->tc)); memset(m->tcc, 16, sizeof(m->tcc));
         memset(m->cbf, 1, 16); memset(m->cbf_c, 1, sizeof(m->cbf_c)); memset(m->cbf_dc, 1, 3);
         for (int i = 0; i < 16; i++) m->ipm[i] = 2;
         g->prev_qpd_nz = 0;
@@ -626,19 +704,28 @@ static void encode_mb(G *g) {
         if (!ac) for (int i = 0; i < 256; i++) if ((i & 3) || ((i >> 4) & 3)) lv16[i] = 0;
         m->mb_type = 1 + mode16 + 4 * cbp_c + (ac ? 12 : 0);
         m->cbp = (cbp_c << 4) | (ac ? 15 : 0);
-        bin(g, 3 + ctx, 1);
-        ce_term(&g->ce, 0);
-        bin(g, 6, ac);
-        bin(g, 7, cbp_c != 0);
-        if (cbp_c) bin(g, 8, cbp_c == 2);
-        bin(g, 9, mode16 >> 1);
-        bin(g, 10, mode16 & 1);
+        if (g->cavlc) {
+            bw_ue(g->ce.bw, (uint32_t)m->mb_type);
+        } else {
+            bin(g, 3 + ctx, 1);
+            ce_term(&g->ce, 0);
+            bin(g, 6, ac);
+            bin(g, 7, cbp_c != 0);
+            if (cbp_c) bin(g, 8, cbp_c == 2);
+            bin(g, 9, mode16 >> 1);
+            bin(g, 10, mode16 & 1);
+        }
     } else {
         m->mb_type = 0;
-        bin(g, 3 + ctx, 0);
-        if (g->t8x8) {
-            int c8 = (A && A->t8x8) + (B && B->t8x8);
-            bin(g, 399 + c8, t8);
+        if (g->cavlc) {
+            bw_ue(g->ce.bw, 0);
+            if (g->t8x8) bw_put(g->ce.bw, (uint32_t)t8, 1);
+        } else {
+            bin(g, 3 + ctx, 0);
+            if (g->t8x8) {
+                int c8 = (A && A->t8x8) + (B && B->t8x8);
+                bin(g, 399 + c8, t8);
+            }
         }
         m->t8x8 = t8;
     }
@@ -670,10 +757,15 @@ static void encode_mb(G *g) {
             Mb *NB = nb_blk(g, k_blk_x[blk], k_blk_y[blk] - 1, &nblkB);
             int mb2 = !NB ? -1 : (NB->mb_type != 0 ? 2 : NB->ipm[nblkB]);
             int pm = (ma < 0 || mb2 < 0) ? 2 : (ma < mb2 ? ma : mb2);
-            bin(g, 68, bm == pm);
-            if (bm != pm) {
-                int rem = bm < pm ? bm : bm - 1;
-                bin(g, 69, rem & 1); bin(g, 69, (rem >> 1) & 1); bin(g, 69, (rem >> 2) & 1);
+            if (g->cavlc) {
+                bw_put(g->ce.bw, bm == pm, 1);
+                if (bm != pm) bw_put(g->ce.bw, (uint32_t)(bm < pm ? bm : bm - 1), 3);
+            } else {
+                bin(g, 68, bm == pm);
+                if (bm != pm) {
+                    int rem = bm < pm ? bm : bm - 1;
+                    bin(g, 69, rem & 1); bin(g, 69, (rem >> 1) & 1); bin(g, 69, (rem >> 2) & 1);
+                }
             }
             if (t8) for (int k = 0; k < 4; k++) m->ipm[blk + k] = (uint8_t)bm;
             else m->ipm[blk] = (uint8_t)bm;
@@ -703,11 +795,19 @@ static void encode_mb(G *g) {
     /* chroma pred mode */
     {
         int c2 = (A && A->mb_type != 25 && A->cpm != 0) + (B && B->mb_type != 25 && B->cpm != 0);
-        bin(g, 64 + c2, cpm != 0);
-        if (cpm) { bin(g, 67, cpm > 1); if (cpm > 1) bin(g, 67, cpm > 2); }
+        if (g->cavlc) {
+            bw_ue(g->ce.bw, (uint32_t)cpm);
+        } else {
+            bin(g, 64 + c2, cpm != 0);
+            if (cpm) { bin(g, 67, cpm > 1); if (cpm > 1) bin(g, 67, cpm > 2); }
+        }
         m->cpm = cpm;
     }
-    if (!is16) {
+    if (!is16 && g->cavlc) {
+        int cn = 0;
+        while (kCbpIntra[cn] != m->cbp) cn++;
+        bw_ue(g->ce.bw, (uint32_t)cn);
+    } else if (!is16) {
         int cbp = m->cbp;
         for (int b8 = 0; b8 < 4; b8++) {
             int bx = b8 & 1, by = b8 >> 1, ca, cb;
@@ -728,10 +828,14 @@ static void encode_mb(G *g) {
         qpd = qp_use - g->cur_qp;
         int k = qpd > 0 ? 2 * qpd - 1 : -2 * qpd;
         int c0 = g->prev_qpd_nz ? 1 : 0;
-        bin(g, 60 + c0, k > 0);
-        if (k > 0) {
-            for (int i = 1; i < k; i++) bin(g, 60 + (i == 1 ? 2 : 3), 1);
-            bin(g, 60 + (k == 1 ? 2 : 3), 0);
+        if (g->cavlc) {
+            bw_se(g->ce.bw, qpd);
+        } else {
+            bin(g, 60 + c0, k > 0);
+            if (k > 0) {
+                for (int i = 1; i < k; i++) bin(g, 60 + (i == 1 ? 2 : 3), 1);
+                bin(g, 60 + (k == 1 ? 2 : 3), 0);
+            }
         }
         g->cur_qp = qp_use;
     } else if (qp_use != g->cur_qp) {
@@ -743,10 +847,18 @@ static void encode_mb(G *g) {
     int co[64];
     if (is16) {
         for (int k = 0; k < 16; k++) { int rr = k_zz4[k]; co[k] = lv16[(rr >> 2) * 4 * 16 + (rr & 3) * 4]; }
-        m->cbf_dc[0] = (uint8_t)enc_block(g, 0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, co);
+        if (g->cavlc) enc_block_cavlc(g, nc_luma(g, 0), 16, co);
+        else m->cbf_dc[0] = (uint8_t)enc_block(g, 0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, co);
     }
     for (int b8 = 0; b8 < 4; b8++) {
         if (!((m->cbp >> b8) & 1)) continue;
+        if (t8 && g->cavlc) {
+            for (int i4 = 0; i4 < 4; i4++) {
+                for (int k = 0; k < 16; k++) co[k] = lv8[b8][k_zz8[4 * k + i4]];
+                m->tc[b8 * 4 + i4] = (uint8_t)enc_block_cavlc(g, nc_luma(g, b8 * 4 + i4), 16, co);
+            }
+            continue;
+        }
         if (t8) {
             for (int k = 0; k < 64; k++) co[k] = lv8[b8][k_zz8[k]];
             enc_block(g, 5, 0, 64, co);
@@ -761,17 +873,20 @@ static void encode_mb(G *g) {
             int cb = cbf_cond(is16 ? 1 : 2, NB, nb1, 0);
             if (is16) {
                 for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lv16[(by * 4 + (rr >> 2)) * 16 + bx * 4 + (rr & 3)]; }
-                m->cbf[blk] = (uint8_t)enc_block(g, 1, ca + 2 * cb, 15, co);
+                if (g->cavlc) m->tc[blk] = (uint8_t)enc_block_cavlc(g, nc_luma(g, blk), 15, co);
+                else m->cbf[blk] = (uint8_t)enc_block(g, 1, ca + 2 * cb, 15, co);
             } else {
                 for (int k = 0; k < 16; k++) co[k] = lv4[blk][k_zz4[k]];
-                m->cbf[blk] = (uint8_t)enc_block(g, 2, ca + 2 * cb, 16, co);
+                if (g->cavlc) m->tc[blk] = (uint8_t)enc_block_cavlc(g, nc_luma(g, blk), 16, co);
+                else m->cbf[blk] = (uint8_t)enc_block(g, 2, ca + 2 * cb, 16, co);
             }
         }
     }
     if (m->cbp >> 4) {
         for (int c = 0; c < 2; c++) {
             for (int k = 0; k < 4; k++) co[k] = lvc[c][(k >> 1) * 4 * 8 + (k & 1) * 4];
-            m->cbf_dc[1 + c] = (uint8_t)enc_block(g, 3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, co);
+            if (g->cavlc) enc_block_cavlc(g, -1, 4, co);
+            else m->cbf_dc[1 + c] = (uint8_t)enc_block(g, 3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, co);
         }
     }
     if ((m->cbp >> 4) == 2) {
@@ -781,7 +896,8 @@ static void encode_mb(G *g) {
                 int ca = bx ? m->cbf_c[c][b4 - 1] : cbf_cond(4, A, b4 + 1, c);
                 int cb = by ? m->cbf_c[c][b4 - 2] : cbf_cond(4, B, b4 + 2, c);
                 for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lvc[c][(by * 4 + (rr >> 2)) * 8 + bx * 4 + (rr & 3)]; }
-                m->cbf_c[c][b4] = (uint8_t)enc_block(g, 4, ca + 2 * cb, 15, co);
+                if (g->cavlc) m->tcc[c][b4] = (uint8_t)enc_block_cavlc(g, nc_chroma(g, m, c, b4), 15, co);
+                else m->cbf_c[c][b4] = (uint8_t)enc_block(g, 4, ca + 2 * cb, 15, co);
             }
     }
     /* reconstruction of I16x16 luma and chroma */
@@ -832,7 +948,7 @@ static void write_sps(FILE *f, G *g, int profile) {
 static void write_pps(FILE *f, G *g, int high) {
     BW b; bw_init(&b);
     bw_ue(&b, 0); bw_ue(&b, 0);
-    bw_put(&b, 1, 1); /* CABAC */
+    bw_put(&b, (uint32_t)!g->cavlc, 1); /* entropy_coding_mode_flag */
     bw_put(&b, 0, 1);
     bw_ue(&b, 0);     /* slice groups */
     bw_ue(&b, 0); bw_ue(&b, 0);
@@ -870,6 +986,7 @@ int main(int argc, char **argv) {
     g->dbidc = opt_int(argc, argv, "--dbidc", 0);
     g->cqp = opt_int(argc, argv, "--cqp", 0);
     g->cqp2 = opt_int(argc, argv, "--cqp2", g->cqp);
+    g->cavlc = opt_int(argc, argv, "--cavlc", 0);
     int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp ? 100 : 77));
     g->W = (g->outW + 15) & ~15; g->H = (g->outH + 15) & ~15;
     g->mbw = g->W / 16; g->mbh = g->H / 16;
@@ -908,7 +1025,7 @@ int main(int argc, char **argv) {
         int idc = g->dbidc;
         bw_ue(&b, (uint32_t)idc);
         if (idc != 1) { bw_se(&b, g->alpha); bw_se(&b, g->beta); }
-        while (b.nb) bw_put(&b, 1, 1);        /* cabac_alignment_one_bit */
+        if (!g->cavlc) while (b.nb) bw_put(&b, 1, 1);  /* cabac_alignment_one_bit */
         for (int i = 0; i < 460; i++) {
             int mm = k_init_I[i][0], nn = k_init_I[i][1];
             int pre = clip3(1, 126, ((mm * clip3(0, 51, sqp)) >> 4) + nn), mps = pre <= 63 ? 0 : 1;
@@ -924,9 +1041,9 @@ int main(int argc, char **argv) {
                 g->mbx = mx; g->mby = my;
                 g->mb[my * g->mbw + mx].slice = nslice;
                 encode_mb(g);
-                ce_term(&g->ce, my == r1 - 1 && mx == g->mbw - 1);
+                if (!g->cavlc) ce_term(&g->ce, my == r1 - 1 && mx == g->mbw - 1);
             }
-        ce_finish(&g->ce);
+        if (!g->cavlc) ce_finish(&g->ce);
         bw_put(&b, 1, 1);
         bw_align_zero(&b);
         write_nal(fo, 3, 5, b.buf, b.n);

@@ -153,6 +153,13 @@ PARITY264 = [
     ("a11_64x64_tiny", 64, 64, 8, 26, 41, 2, []),
     ("a12_72x40_odd_crop", 72, 40, 8, 20, 42, 5, ["--pcm", "1"]),
     ("a13_320x180_10bit_q0", 320, 180, 10, 0, 43, 4, ["--t8x8", "0", "--cqp", "-5"]),
+    # CAVLC (entropy_coding_mode_flag 0)
+    ("a14_416x240_cavlc_main", 416, 240, 8, 26, 44, 2, ["--cavlc", "1", "--t8x8", "0"]),
+    ("a15_352x288_cavlc_high8x8_pcm", 352, 288, 8, 20, 45, 4, ["--cavlc", "1", "--pcm", "1"]),
+    ("a16_320x176_cavlc_10bit", 320, 176, 10, 12, 46, 6, ["--cavlc", "1"]),
+    ("a17_256x144_cavlc_q0_noise", 256, 144, 8, 0, 47, 20, ["--cavlc", "1", "--t8x8", "1"]),
+    ("a18_480x272_cavlc_slices_offsets", 480, 272, 8, 33, 48, 2,
+     ["--cavlc", "1", "--slices", "2", "--cqp", "2", "--alpha", "1", "--beta", "-1"]),
 ]
 
 
@@ -171,7 +178,8 @@ def parity264():
 
 
 def bench264(n=16):
-    """Config 3: 1080p H.264 High (8x8 transform) I-frames."""
+    """Config 3: 1080p H.264 High (8x8 transform) I-frames; streams 7 and 15
+    are CAVLC (2/16 = 12.5 %, SURVEY.md §8d asks for a ~10 % CAVLC mix)."""
     out_dir = os.path.join(ROOT, "tests/golden/bench264")
     os.makedirs(out_dir, exist_ok=True)
     planes = source_planes()
@@ -182,7 +190,8 @@ def bench264(n=16):
         qp, sigma = qps[i % 4], sigmas[(i // 4) % 3]
         content = make_content(planes, 1920, 1080, 200 + i, sigma, 8)
         path = os.path.join(out_dir, f"avc1080_{i:02d}.h264")
-        nb = encode(content, 1920, 1080, 8, qp, 200 + i, path, ["--t8x8", "1"], codec=264)
+        opts = ["--t8x8", "1"] + (["--cavlc", "1"] if i % 8 == 7 else [])
+        nb = encode(content, 1920, 1080, 8, qp, 200 + i, path, opts, codec=264)
         total += nb
         print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
     print("total", total)
