@@ -509,6 +509,17 @@ struct K1WaveLds {  // HEVC
     int sub[132];
     int ref[132];
 };
+
+// HEVC: one CTB (up to 64x64 luma) plus the line above it (incl. the
+// top-right reach of the largest TB) and the left column, per wave.
+template <typename Pel>
+struct HWin {
+    Pel top[3][132];     // y = -1: x = -1 .. 130 (index x + 1)
+    Pel left[3][64];     // x = -1: y = 0 .. S-1
+    Pel by[64 * 64];     // CTB body, row-major, stride = CTB size of the component
+    Pel bc[2][32 * 32];
+    K1WaveLds k;
+};
 // H.264: one macroblock plus its top line and left column, per wave.
 // Window coordinates: (x - mb_x + 1, y - mb_y + 1); row 0 is the line
 // above (luma incl. the 8 top-right samples), column 0 the left column.
@@ -878,6 +889,271 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     }
 }
 
+// One HEVC TB predicted inside the wave's CTB window (all sample traffic LDS;
+// the K0 residual is loaded from HBM up front so it overlaps the chain).
+template <typename Pel>
+DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, int cx0, int cy0, const int16_t* RSc,
+                              HWin<Pel>& w, int lane) {
+    K1WaveLds& s = w.k;
+    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int shc = c ? 1 : 0;
+    const int S = (1 << f.log2ctb) >> shc;               // CTB size in this component
+    const int ox = tu.x - (cx0 >> shc), oy = tu.y - (cy0 >> shc);  // TB origin in the CTB
+    Pel* body = c == 0 ? w.by : w.bc[c - 1];
+    const Pel* top = w.top[c];
+    const Pel* left = w.left[c];
+    const int st = f.pic_stride[c];
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int maxv = (1 << bd) - 1;
+    const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
+    // residual prefetch (independent of the chain)
+    int rr[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int i = lane + 64 * k;
+        rr[k] = (cbf && i < nn) ? RSc[(tu.y + (i >> log2n)) * st + tu.x + (i & (n - 1))] : 0;
+    }
+    auto sample = [&](int x, int y) -> int {  // CTB-relative, x,y >= -1
+        if (y < 0) return top[x + 1];
+        if (x < 0) return left[y];
+        return body[y * S + x];
+    };
+    const int L = 4 * n + 1;
+    const int ush = c ? 1 : 2, nu = (2 * n) >> ush;
+    unsigned long long m0 = 0, m1 = 0, m2 = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int k = base + lane;
+        bool a = false;
+        if (k < L) {
+            int xn, yn, unit;
+            if (k < 2 * n) { xn = ox - 1; yn = oy + (2 * n - 1 - k); unit = k >> ush; }
+            else if (k == 2 * n) { xn = ox - 1; yn = oy - 1; unit = nu; }
+            else { xn = ox + (k - 2 * n - 1); yn = oy - 1; unit = nu + 1 + ((k - 2 * n - 1) >> ush); }
+            a = (mask >> unit) & 1ull;
+            s.seq[k] = a ? sample(xn, yn) : 0;
+        }
+        const unsigned long long bal = __ballot(a);
+        if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
+    }
+    wave_sync();
+    const bool any = (m0 | m1 | m2) != 0;
+    for (int k = lane; k < L; k += 64) {
+        int v;
+        if (!any) {
+            v = 1 << (bd - 1);
+        } else {
+            const int ch = k >> 6, bit = k & 63;
+            const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
+            if ((mk >> bit) & 1ull) {
+                v = s.seq[k];
+            } else {
+                int j = -1;
+                const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
+                if (below) j = (ch << 6) + 63 - __clzll(below);
+                else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
+                else if (ch >= 1 && m0) j = 63 - __clzll(m0);
+                if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
+                                  : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
+                v = s.seq[j];
+            }
+        }
+        s.sub[k] = v;
+    }
+    wave_sync();
+    const int mode = tu.mode;
+    bool filt = false;
+    if (c == 0 && mode != 1 && n != 4) {
+        const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+        const int md = d26 < d10 ? d26 : d10;
+        const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+        filt = mode == 0 || md > thr;
+    }
+    if (filt) {
+        const int corner = s.sub[2 * n];
+        const bool strong = f.strong_smoothing && n == 32 &&
+                            abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
+                            abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
+        for (int k = lane; k < L; k += 64) {
+            int v;
+            if (k == 0 || k == 4 * n) v = s.sub[k];
+            else if (strong) {
+                if (k == 2 * n) v = corner;
+                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
+                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
+            } else {
+                v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
+            }
+            s.ref[k] = v;
+        }
+    } else {
+        for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
+    }
+    wave_sync();
+    const int* R = s.ref;
+    int dc = 0;
+    if (mode == 1) {
+        int part = 0;
+        for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
+        dc = (wave_sum(part) + n) >> (log2n + 1);
+    }
+    const int angle = kAngle[mode];
+    const int inv = kInvAngle[mode];
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) {
+        const int i = lane + 64 * kk;
+        if (i >= nn) break;
+        const int x = i & (n - 1), y = i >> log2n;
+        int pv;
+        if (mode == 0) {
+            pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
+                  (y + 1) * R[n - 1] + n) >> (log2n + 1);
+        } else if (mode == 1) {
+            pv = dc;
+            if (c == 0 && n < 32) {
+                if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
+                else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+            }
+        } else if (mode >= 18) {
+            const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
+            const int k1 = x + idx + 1, k2 = x + idx + 2;
+            const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
+            if (fr) {
+                const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
+                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            } else {
+                pv = r1;
+            }
+            if (mode == 26 && c == 0 && n < 32 && x == 0)
+                pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
+        } else {
+            const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
+            const int k1 = y + idx + 1, k2 = y + idx + 2;
+            const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
+            if (fr) {
+                const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
+                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            } else {
+                pv = r1;
+            }
+            if (mode == 10 && c == 0 && n < 32 && y == 0)
+                pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
+        }
+        body[(oy + y) * S + ox + x] = static_cast<Pel>(clip3(0, maxv, pv + rr[kk]));
+    }
+    wave_sync();
+}
+
+// Copy a CTB window body to / from the picture (only the part inside it).
+template <typename Pel, bool kStore>
+DEVI void hevc_ctb_io(const h2j_frame& f, uint8_t* arena, int cx0, int cy0, HWin<Pel>& w, int lane) {
+    for (int c = 0; c < 3; c++) {
+        const int shc = c ? 1 : 0;
+        const int S = (1 << f.log2ctb) >> shc;
+        const int x0 = cx0 >> shc, y0 = cy0 >> shc;
+        const int wc = min(S, (f.width >> shc) - x0), hc = min(S, (f.height >> shc) - y0);
+        Pel* P = plane<Pel>(f, arena, f.pic, c);
+        Pel* body = c == 0 ? w.by : w.bc[c - 1];
+        const int st = f.pic_stride[c];
+        const int per_row = wc >> 1;  // 2 samples per lane step (widths are multiples of 2 samples)
+        for (int i = lane; i < hc * per_row; i += 64) {
+            const int y = i / per_row, x = (i - y * per_row) * 2;
+            if (kStore) {
+                P[(y0 + y) * st + x0 + x] = body[y * S + x];
+                P[(y0 + y) * st + x0 + x + 1] = body[y * S + x + 1];
+            } else {
+                body[y * S + x] = P[(y0 + y) * st + x0 + x];
+                body[y * S + x + 1] = P[(y0 + y) * st + x0 + x + 1];
+            }
+        }
+    }
+}
+
+template <typename Pel>
+DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HWin<Pel>& w, uint32_t* prog) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t* masks = tu_masks(f, arena);
+    const uint32_t* rng = ctb_ranges(f, arena);
+    constexpr int kSlots = 2 * kK1Waves;
+    const int CS = 1 << f.log2ctb;
+    const int16_t* RS[3] = {res_plane(f, arena, 0), res_plane(f, arena, 1), res_plane(f, arena, 2)};
+    for (int row = wv; row < f.ctb_h; row += kK1Waves) {
+        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + row % kSlots;
+        uint32_t seen = 0;
+        const int cy0 = row * CS;
+        for (int cx = 0; cx < f.ctb_w; cx++) {
+            const int cx0 = cx * CS;
+            if (row > 0) {
+                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(cx + 2, f.ctb_w));
+                if (seen < need) {
+                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+            }
+            // line above (incl. top-right reach) from the picture; left column from the previous CTB
+            for (int c = 0; c < 3; c++) {
+                const int shc = c ? 1 : 0, S = CS >> shc, x0 = cx0 >> shc, y0 = cy0 >> shc;
+                const int Wc = f.width >> shc;
+                const Pel* P = plane<Pel>(f, arena, f.pic, c);
+                const int st = f.pic_stride[c];
+                const int reach = min(2 * S, S + 32) + 1;  // corner + CTB width + top-right of the largest TB
+                for (int i = lane; i < reach; i += 64) {
+                    const int x = x0 - 1 + i;
+                    w.top[c][i] = (row > 0 && x >= 0 && x < Wc) ? P[(y0 - 1) * st + x] : Pel(0);
+                }
+                if (cx == 0)
+                    for (int i = lane; i < S; i += 64) w.left[c][i] = Pel(0);
+            }
+            wave_sync();
+            const int cb = row * f.ctb_w + cx;
+            const uint32_t a = rng[2 * cb], b = rng[2 * cb + 1];
+            bool pcm_seen = false;
+            if (a < b) {
+                h2j_tu cur = T[a];
+                uint64_t cm = masks[a];
+                for (uint32_t t = a; t < b; t++) {
+                    h2j_tu nxt = cur;
+                    uint64_t nm = 0;
+                    if (t + 1 < b) {  // prefetch the next record
+                        nxt = T[t + 1];
+                        nm = masks[t + 1];
+                    }
+                    if (cur.flags & H2J_TU_PCM) {
+                        pcm_seen = true;  // samples written by K0: pull that block into the window
+                        const int shc = cur.c ? 1 : 0, S = CS >> shc, n = 1 << cur.log2n;
+                        const int ox = cur.x - (cx0 >> shc), oy = cur.y - (cy0 >> shc);
+                        const Pel* P = plane<Pel>(f, arena, f.pic, cur.c);
+                        Pel* body = cur.c == 0 ? w.by : w.bc[cur.c - 1];
+                        for (int i = lane; i < n * n; i += 64)
+                            body[(oy + i / n) * S + ox + (i % n)] =
+                                P[(cur.y + i / n) * f.pic_stride[cur.c] + cur.x + (i % n)];
+                        wave_sync();
+                    } else {
+                        hevc_predict_tu_win<Pel>(f, cur, cm, cx0, cy0, RS[cur.c], w, lane);
+                    }
+                    cur = nxt;
+                    cm = nm;
+                }
+            }
+            (void)pcm_seen;
+            hevc_ctb_io<Pel, true>(f, arena, cx0, cy0, w, lane);
+            // right column becomes the next CTB's left column
+            for (int c = 0; c < 3; c++) {
+                const int S = CS >> (c ? 1 : 0);
+                const Pel* body = c == 0 ? w.by : w.bc[c - 1];
+                for (int i = lane; i < S; i += 64) w.left[c][i] = body[i * S + S - 1];
+            }
+            wave_sync();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
 template <typename Pel>
 DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WaveLds& wl, uint32_t* prog) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -914,17 +1190,16 @@ DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1Wa
 
 // Separate kernels per codec so each gets its own register budget; a mixed
 // batch launches both and each skips the other codec's pictures.
+template <typename Pel>
 __global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
                                                                   uint8_t* arena) {
-    __shared__ K1WaveLds wl[kK1Waves];
+    __shared__ HWin<Pel> wl[kK1Waves];
     __shared__ uint32_t prog[2 * kK1Waves];
     const h2j_frame& f = frames[blockIdx.x];
-    if (f.codec != H2J_CODEC_HEVC) return;
+    if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
     if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
     __syncthreads();
-    K1WaveLds& s = wl[threadIdx.x >> 6];
-    if (f.bit_depth == 8) predict_rows<uint8_t>(f, tus + f.tu, arena, s, prog);
-    else predict_rows<uint16_t>(f, tus + f.tu, arena, s, prog);
+    hevc_rows<Pel>(f, tus + f.tu, arena, wl[threadIdx.x >> 6], prog);
 }
 
 __global__ void __launch_bounds__(64 * kK1Waves, 6) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
@@ -1615,8 +1890,13 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (b->has_hevc) {
-        hipLaunchKernelGGL(h2j_k1_recon_hevc, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
-        const int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
+        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint8_t>, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus,
+                           b->arena);
+        int r = check(hipGetLastError(), "h2j_k1_recon_hevc<u8>");
+        if (r) return r;
+        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint16_t>, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus,
+                           b->arena);
+        r = check(hipGetLastError(), "h2j_k1_recon_hevc<u16>");
         if (r) return r;
     }
     if (b->has_h264) {

@@ -425,12 +425,26 @@ int Engine::sync(Slot& s) {
     return 0;
 }
 
-// Frames per pipeline chunk: large enough to fill the GPU (K1 runs one
-// workgroup per picture), small enough that parse / GPU / assembly overlap.
-int chunk_frames(int n) {
+// Chunk boundaries: chunks large enough to fill the GPU (K1 runs one
+// workgroup per picture), small enough that parse / GPU / assembly overlap;
+// the last quarter is split into shrinking chunks so that the GPU work left
+// after the last picture is parsed (the pipeline's tail) is short.
+std::vector<int> chunk_plan(int n) {
+    int chunk = n >= 512 ? 256 : n;
     const char* e = std::getenv("H2J_CHUNK");
-    if (e && std::atoi(e) > 0) return std::atoi(e);
-    return n >= 512 ? 256 : n;
+    if (e && std::atoi(e) > 0) chunk = std::atoi(e);
+    chunk = std::max(1, chunk);
+    std::vector<int> starts;
+    int i = 0;
+    while (i < n) {
+        starts.push_back(i);
+        int c = chunk;
+        const int left = n - i;
+        if (left <= chunk && left > 64 && chunk >= 128) c = left / 2;  // tail: halve
+        i += std::min(c, left);
+    }
+    starts.push_back(n);
+    return starts;
 }
 
 }  // namespace h2j
@@ -487,22 +501,25 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
         out_off[i] = 0;
         status[i] = 0;
     }
-    const int chunk = std::max(1, h2j::chunk_frames(n));
-    const int nchunks = (n + chunk - 1) / chunk;
+    const std::vector<int> bounds = h2j::chunk_plan(n);
+    const int nchunks = static_cast<int>(bounds.size()) - 1;
+    std::vector<int> chunk_of(n);
+    for (int c = 0; c < nchunks; c++)
+        for (int i = bounds[c]; i < bounds[c + 1]; i++) chunk_of[i] = c;
     size_t pos = 0;
     int rc = 0;
     // Parsing runs ahead on the pool (frames claimed in order), so chunk c+1
     // parses while the GPU runs chunk c and the host assembles chunk c-1.
     const bool overlap = nchunks > 1;
     std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[nchunks]);
-    for (int c = 0; c < nchunks; c++) left[c] = std::min(n, (c + 1) * chunk) - c * chunk;
+    for (int c = 0; c < nchunks; c++) left[c] = bounds[c + 1] - bounds[c];
     std::mutex mu;
     std::condition_variable cv;
     double t_parsed = t0;
     auto parse_all = [&]() {
         e.pool->parallel_for(n, [&](int i) {
             h2j::parse_any(data[i], sizes[i], e.jobs[i]);
-            if (left[i / chunk].fetch_sub(1) == 1) {
+            if (left[chunk_of[i]].fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> g(mu);
                 cv.notify_all();
             }
@@ -559,7 +576,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     };
     int fail = 0;
     for (int c = 0; c < nchunks && !fail; c++) {
-        const int i0 = c * chunk, i1 = std::min(n, i0 + chunk);
+        const int i0 = bounds[c], i1 = bounds[c + 1];
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return left[c].load() == 0; });
