@@ -40,11 +40,43 @@ WORKLOADS = {
     "hevc2160": dict(streams="tests/golden/bench4k/hevc2160_10b_*.h265", w=3840, h=2160, bps=2,
                      desc="configs[3]: 4K H.265 Main10 I-frames, 10-bit decode -> 8-bit JPEG per GPU",
                      data="4 hevcgen 2160p HEVC Main10 I-frame streams (tests/golden/bench4k)"),
+    "mixed": dict(streams=None, w=None, h=None, bps=None,
+                  desc="configs[4]: mixed 720p/1080p/4K (40/40/20 by count) x H.264/H.265 (50/50) stills, "
+                       "LPT-sharded over the GPUs (frames = per-GPU share of the global list)",
+                  data="tests/golden/{mixed,bench,bench264,bench4k} generator streams"),
+}
+
+# configs[4] ingredients: (size class, codec) -> (glob, w, h, bytes/sample)
+MIXED_SETS = {
+    ("720", 265): ("tests/golden/mixed/hevc720_*.h265", 1280, 720, 1),
+    ("720", 264): ("tests/golden/mixed/avc720_*.h264", 1280, 720, 1),
+    ("1080", 265): ("tests/golden/bench/hevc1080_*.h265", 1920, 1080, 1),
+    ("1080", 264): ("tests/golden/bench264/avc1080_*.h264", 1920, 1080, 1),
+    ("2160", 265): ("tests/golden/bench4k/hevc2160_10b_*.h265", 3840, 2160, 2),
+    ("2160", 264): ("tests/golden/mixed/avc2160_*.h264", 3840, 2160, 1),
 }
 
 
+def alg_bytes(w, h, bps):
+    """B = 2S (int16 residual in) + bps*S (picture out) + 2S (int16 JPEG coefficients out)."""
+    return (4 + bps) * (w * h * 3 // 2)
+
+
 def alg_bytes_per_frame(wl):
-    return 5 * (wl["w"] * wl["h"] * 3 // 2) * wl["bps"]
+    return alg_bytes(wl["w"], wl["h"], wl["bps"])
+
+
+def mixed_list(total):
+    """Deterministic configs[4] list: index g -> size class by g % 10 (0-3 720p,
+    4-7 1080p, 8-9 4K), codec by (g // 10) % 2, stream by (g // 20)."""
+    sets = {k: (load_streams(v[0]), v[1], v[2], v[3]) for k, v in MIXED_SETS.items()}
+    items = []
+    for g in range(total):
+        cls = "720" if g % 10 < 4 else ("1080" if g % 10 < 8 else "2160")
+        codec = 265 if (g // 10) % 2 == 0 else 264
+        streams, w, h, bps = sets[(cls, codec)]
+        items.append((streams[(g // 20) % len(streams)], alg_bytes(w, h, bps), w * h))
+    return items
 
 
 def load_streams(pattern):
@@ -118,7 +150,7 @@ def main():
     ap.add_argument("--frames", type=int, default=1024, help="frames per GPU per step")
     ap.add_argument("--threads", type=int, default=16, help="host entropy/Huffman threads per GPU")
     ap.add_argument("--workload", default="hevc1080", choices=sorted(WORKLOADS),
-                    help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]")
+                    help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]/[4]")
     ap.add_argument("--streams", default=None, help="override the workload's stream glob")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -138,16 +170,27 @@ def main():
 
     import h2j
     wl = WORKLOADS[args.workload]
-    streams = load_streams(args.streams or wl["streams"])
     n = args.frames
-    batch = [streams[i % len(streams)] for i in range(n)]
+    if args.workload == "mixed":
+        items = mixed_list(n * world)
+        # cost model for the LPT shard: bitstream bytes (host CABAC/CAVLC) + pixels (GPU)
+        mine = shard_lpt([len(b) + 0.02 * px for b, _, px in items], world)[rank]
+        batch = [items[i][0] for i in mine]
+        frame_bytes = [items[i][1] for i in mine]
+        streams = sorted({id(b): b for b in batch}.values(), key=len)
+        n = len(batch)
+    else:
+        streams = load_streams(args.streams or wl["streams"])
+        batch = [streams[i % len(streams)] for i in range(n)]
+        frame_bytes = [alg_bytes_per_frame(wl)] * n
     eng = h2j.Engine(local, args.threads)
 
     # pre-built ctypes arguments: nothing but the C call inside the timed region
     bufs = [(ctypes.c_uint8 * len(s)).from_buffer_copy(s) for s in batch]
     ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
     sizes = (ctypes.c_size_t * n)(*[len(s) for s in batch])
-    cap = n * (2 << 20)
+    # output capacity: 2 MiB per picture or one byte per luma pixel, whichever is larger
+    cap = sum(max(2 << 20, fb // 6) for fb in frame_bytes)
     out = (ctypes.c_uint8 * cap)()
     offs = (ctypes.c_size_t * n)()
     lens = (ctypes.c_size_t * n)()
@@ -187,11 +230,12 @@ def main():
         chunks = max(1, round(per["chunks"]))
         k1_ms = per["recon_ms"] / chunks
         frames_per_launch = n / chunks
-        alg_bytes = alg_bytes_per_frame(wl) * frames_per_launch
-        achieved = alg_bytes / (k1_ms / 1e3) / 1e9
+        alg_bytes_launch = sum(frame_bytes) / chunks
+        achieved = alg_bytes_launch / (k1_ms / 1e3) / 1e9
         gpu_ms = (per["h2d_ms"] + per["prep_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"]
                   + per["jpeg_ms"] + per["entropy_ms"] + per["d2h_ms"])
-        k1_name = "h2j_k1_recon_h264" if args.workload.startswith("avc") else "h2j_k1_recon_hevc"
+        k1_name = {"avc1080": "h2j_k1_recon_h264", "mixed": "h2j_k1_recon_hevc+h2j_k1_recon_h264"}.get(
+            args.workload, "h2j_k1_recon_hevc")
         traffic = pmc_traffic(args.workload)
         res = {
             "metric": METRIC,
@@ -211,7 +255,7 @@ def main():
                        "parallelism": f"independent replicas x{world}"},
             "roofline": {"bound": "hbm", "kernel": k1_name, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "frames_per_launch": frames_per_launch,
+                         "alg_bytes_per_launch": alg_bytes_launch, "frames_per_launch": frames_per_launch,
                          "avg_launch_ms": k1_ms},
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},

@@ -12,6 +12,7 @@ reconstruction bit-for-bit.
   python tools/make_streams.py 4k      -> tests/golden/bench4k/hevc2160_10b_XX.h265
   python tools/make_streams.py parity264 -> tests/golden/h264/*.h264 + manifest.json (tools/h264gen)
   python tools/make_streams.py bench264  -> tests/golden/bench264/avc1080_XX.h264 (16 streams, High 8x8)
+  python tools/make_streams.py mixed     -> tests/golden/mixed/ (720p H.265/H.264, 4K H.264) for configs[4]
 """
 import json
 import os
@@ -197,6 +198,26 @@ def bench264(n=16):
     print("total", total)
 
 
+def mixed():
+    """configs[4] ingredients: 720p H.265 + H.264, 4K H.264 (1080p and 4K H.265
+    come from the bench / bench4k sets)."""
+    out_dir = os.path.join(ROOT, "tests/golden/mixed")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    for i, qp in enumerate([22, 27, 32, 37]):
+        content = make_content(planes, 1280, 720, 300 + i, 2, 8)
+        nb = encode(content, 1280, 720, 8, qp, 300 + i, os.path.join(out_dir, f"hevc720_{i:02d}.h265"))
+        print(f"hevc720_{i:02d}: {nb} B", flush=True)
+        opts = ["--t8x8", "1"] + (["--cavlc", "1"] if i == 3 else [])
+        nb = encode(content, 1280, 720, 8, qp, 310 + i, os.path.join(out_dir, f"avc720_{i:02d}.h264"), opts, codec=264)
+        print(f"avc720_{i:02d}: {nb} B", flush=True)
+    for i, qp in enumerate([27, 32]):
+        content = make_content(planes, 3840, 2160, 320 + i, 2, 8, upsample=2)
+        nb = encode(content, 3840, 2160, 8, qp, 320 + i, os.path.join(out_dir, f"avc2160_{i:02d}.h264"), ["--t8x8", "1"],
+                    codec=264)
+        print(f"avc2160_{i:02d}: {nb} B", flush=True)
+
+
 def fourk(n=4):
     out_dir = os.path.join(ROOT, "tests/golden/bench4k")
     os.makedirs(out_dir, exist_ok=True)
@@ -212,4 +233,5 @@ def fourk(n=4):
 if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
-    {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264}[what]()
+    {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
+     "mixed": mixed}[what]()
