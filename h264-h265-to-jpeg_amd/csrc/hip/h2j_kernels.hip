@@ -76,10 +76,10 @@ DEVI bool avail(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices
 __constant__ int8_t kCos33[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
                                   61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
 __constant__ int8_t kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
-__constant__ int8_t kAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
+__constant__ int kAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
                                   -5,  -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
                                   -5,  -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
-__constant__ int16_t kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,    0,    0,
+__constant__ int kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,    0,    0,
                                       0,     0,     -4096, -1638, -910, -630, -482, -390, -315,
                                       -256,  -315,  -390, -482, -630, -910, -1638, -4096, 0};
 __constant__ int8_t kLevelScale[6] = {40, 45, 51, 57, 64, 72};
@@ -199,6 +199,26 @@ DEVI void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// Optional K1 cycle accounting (build with -DH2J_PROF: `make prof`), read via h2j_gpu_prof().
+#ifdef H2J_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_T() __builtin_amdgcn_s_memtime()
+#define PROF_ADD(i, v) (pacc[i] += (v))
+#define PROF_DECL unsigned long long pacc[16] = {0}; unsigned long long pt0 = PROF_T(), pt1
+#define PROF_LAP(i) (pt1 = PROF_T(), PROF_ADD(i, pt1 - pt0), pt0 = pt1)
+#define PROF_LAPK(k) do { pt1 = PROF_T(); const unsigned long long d_ = pt1 - pt0; pt0 = pt1; \
+    switch (k) { case 0: pacc[8] += d_; break; case 1: pacc[9] += d_; break; case 2: pacc[10] += d_; break; \
+    case 3: pacc[11] += d_; break; case 4: pacc[12] += d_; break; case 5: pacc[13] += d_; break; \
+    case 6: pacc[14] += d_; break; default: pacc[15] += d_; break; } } while (0)
+#define PROF_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd(&g_prof[q_], pacc[q_]); } while (0)
+#else
+#define PROF_DECL
+#define PROF_ADD(i, v)
+#define PROF_LAP(i)
+#define PROF_LAPK(k)
+#define PROF_FLUSH()
+#endif
 
 DEVI uint64_t* tu_masks(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint64_t*>(arena + f.aux); }
 DEVI uint32_t* ctb_ranges(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint32_t*>(arena + f.ctbrng); }
@@ -510,16 +530,6 @@ struct K1WaveLds {  // HEVC
     int ref[132];
 };
 
-// HEVC: one CTB (up to 64x64 luma) plus the line above it (incl. the
-// top-right reach of the largest TB) and the left column, per wave.
-template <typename Pel>
-struct HWin {
-    Pel top[3][132];     // y = -1: x = -1 .. 130 (index x + 1)
-    Pel left[3][64];     // x = -1: y = 0 .. S-1
-    Pel by[64 * 64];     // CTB body, row-major, stride = CTB size of the component
-    Pel bc[2][32 * 32];
-    K1WaveLds k;
-};
 // H.264: one macroblock plus its top line and left column, per wave.
 // Window coordinates: (x - mb_x + 1, y - mb_y + 1); row 0 is the line
 // above (luma incl. the 8 top-right samples), column 0 the left column.
@@ -536,144 +546,6 @@ struct H4WaveLds {
     int ftop[40], fleft[20];
 };
 
-
-template <typename Pel>
-DEVI void hevc_predict_tu(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, uint8_t* arena, K1WaveLds& s,
-                          int lane) {
-    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-    const int x0 = tu.x, y0 = tu.y;
-    Pel* P = plane<Pel>(f, arena, f.pic, c);
-    const int16_t* RS = res_plane(f, arena, c);
-    const int st = f.pic_stride[c];
-    const int bd = c ? f.bit_depth_c : f.bit_depth;
-    const int maxv = (1 << bd) - 1;
-    const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
-    const int L = 4 * n + 1;
-    const int ush = c ? 1 : 2, nu = (2 * n) >> ush;
-    unsigned long long m0 = 0, m1 = 0, m2 = 0;
-    for (int base = 0; base < L; base += 64) {
-        const int k = base + lane;
-        bool a = false;
-        if (k < L) {
-            int xn, yn, unit;
-            if (k < 2 * n) { xn = x0 - 1; yn = y0 + (2 * n - 1 - k); unit = k >> ush; }
-            else if (k == 2 * n) { xn = x0 - 1; yn = y0 - 1; unit = nu; }
-            else { xn = x0 + (k - 2 * n - 1); yn = y0 - 1; unit = nu + 1 + ((k - 2 * n - 1) >> ush); }
-            a = (mask >> unit) & 1ull;
-            s.seq[k] = a ? static_cast<int>(P[yn * st + xn]) : 0;
-        }
-        const unsigned long long bal = __ballot(a);
-        if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
-    }
-    wave_sync();
-    const bool any = (m0 | m1 | m2) != 0;
-    for (int k = lane; k < L; k += 64) {
-        int v;
-        if (!any) {
-            v = 1 << (bd - 1);
-        } else {
-            const int ch = k >> 6, bit = k & 63;
-            const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
-            if ((mk >> bit) & 1ull) {
-                v = s.seq[k];
-            } else {
-                int j = -1;
-                const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
-                if (below) j = (ch << 6) + 63 - __clzll(below);
-                else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
-                else if (ch >= 1 && m0) j = 63 - __clzll(m0);
-                if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
-                                  : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
-                v = s.seq[j];
-            }
-        }
-        s.sub[k] = v;
-    }
-    wave_sync();
-    const int mode = tu.mode;
-    bool filt = false;
-    if (c == 0 && mode != 1 && n != 4) {
-        const int d26 = abs(mode - 26), d10 = abs(mode - 10);
-        const int md = d26 < d10 ? d26 : d10;
-        const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
-        filt = mode == 0 || md > thr;
-    }
-    if (filt) {
-        const int corner = s.sub[2 * n];
-        const bool strong = f.strong_smoothing && n == 32 &&
-                            abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
-                            abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
-        for (int k = lane; k < L; k += 64) {
-            int v;
-            if (k == 0 || k == 4 * n) v = s.sub[k];
-            else if (strong) {
-                if (k == 2 * n) v = corner;
-                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
-                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
-            } else {
-                v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
-            }
-            s.ref[k] = v;
-        }
-    } else {
-        for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
-    }
-    wave_sync();
-    // p(-1,y) = ref[2n-1-y], p(x,-1) = ref[2n+1+x], p(-1,-1) = ref[2n]
-    const int* R = s.ref;
-    int dc = 0;
-    if (mode == 1) {
-        int part = 0;
-        for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
-        dc = (wave_sum(part) + n) >> (log2n + 1);
-    }
-    const int angle = kAngle[mode];
-    const int inv = kInvAngle[mode];
-    for (int i = lane; i < nn; i += 64) {
-        const int x = i & (n - 1), y = i >> log2n;
-        const int r = cbf ? RS[(y0 + y) * st + x0 + x] : 0;
-        int pv;
-        if (mode == 0) {
-            pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
-                  (y + 1) * R[n - 1] + n) >> (log2n + 1);
-        } else if (mode == 1) {
-            pv = dc;
-            if (c == 0 && n < 32) {
-                if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
-                else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
-            }
-        } else if (mode >= 18) {
-            const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
-            // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
-            const int k1 = x + idx + 1, k2 = x + idx + 2;
-            const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
-            if (fr) {
-                const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
-                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-            } else {
-                pv = r1;
-            }
-            if (mode == 26 && c == 0 && n < 32 && x == 0)
-                pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
-        } else {
-            const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
-            // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
-            const int k1 = y + idx + 1, k2 = y + idx + 2;
-            const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
-            if (fr) {
-                const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
-                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-            } else {
-                pv = r1;
-            }
-            if (mode == 10 && c == 0 && n < 32 && y == 0)
-                pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
-        }
-        P[(y0 + y) * st + x0 + x] = static_cast<Pel>(clip3(0, maxv, pv + r));
-    }
-    wave_sync();
-}
 
 // One H.264 prediction block (I4x4 / I8x8 / I16x16 / chroma) inside the
 // wave's macroblock window; all sample traffic is LDS.
@@ -889,30 +761,54 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     }
 }
 
-// One HEVC TB predicted inside the wave's CTB window (all sample traffic LDS;
-// the K0 residual is loaded from HBM up front so it overlaps the chain).
-template <typename Pel>
-DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, int cx0, int cy0, const int16_t* RSc,
-                              HWin<Pel>& w, int lane) {
-    K1WaveLds& s = w.k;
+// HEVC K1: each wave owns an int16 CTB window in LDS.  The K0 residual of the
+// whole CTB is prefetched into registers one CTB ahead and dropped into the
+// window when the CTB starts; every TB then reads its residual and writes its
+// reconstruction in place (a TB only ever reads neighbours that are already
+// reconstructed, so the two never alias).  The line above comes from an LDS
+// line buffer shared by the picture's waves (each row leaves its bottom line
+// there), the left column and the top-left corner are carried from the
+// previous CTB, and the TU records stream in 64-record batches held one per
+// lane (readlane).  HBM is touched only by the prefetches and the CTB store.
+constexpr int kLineMax = 4096;  // widest picture whose line above is served from LDS
+
+struct HWinLds {
+    int16_t body[64 * 64 + 2 * 32 * 32];  // Y | Cb | Cr, row stride = CTB size of the component
+    int16_t top[3][132];                  // y = -1: x = -1 .. 130 (index x + 1)
+    int16_t left[3][64];                  // x = -1
+    int16_t corner[4];                    // carried top-left sample of the next CTB
+    K1WaveLds k;
+};
+struct HevcK1Lds {
+    HWinLds w[kK1Waves];
+    int16_t line[2 * kLineMax];  // bottom line of the last finished CTB per column: Y | Cb | Cr
+    uint32_t prog[2 * kK1Waves];
+};
+DEVI int hwin_base(int c) { return c == 0 ? 0 : 64 * 64 + (c - 1) * 32 * 32; }
+DEVI int line_base(int c) { return c == 0 ? 0 : kLineMax + (c - 1) * (kLineMax / 2); }
+
+DEVI h2j_tu tu_from_lanes(const uint4& r, int l) {
+    uint32_t w[4];
+    w[0] = __builtin_amdgcn_readlane(r.x, l);
+    w[1] = __builtin_amdgcn_readlane(r.y, l);
+    w[2] = __builtin_amdgcn_readlane(r.z, l);
+    w[3] = __builtin_amdgcn_readlane(r.w, l);
+    h2j_tu t;
+    memcpy(&t, w, sizeof(t));
+    return t;
+}
+DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
+    return static_cast<uint64_t>(__builtin_amdgcn_readlane(m.x, l)) |
+           (static_cast<uint64_t>(__builtin_amdgcn_readlane(m.y, l)) << 32);
+}
+
+// One HEVC TB predicted + reconstructed inside the wave's CTB window.
+DEVI void hevc_predict_tb(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
+                          const int16_t* top, const int16_t* left, K1WaveLds& s, int lane) {
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-    const int shc = c ? 1 : 0;
-    const int S = (1 << f.log2ctb) >> shc;               // CTB size in this component
-    const int ox = tu.x - (cx0 >> shc), oy = tu.y - (cy0 >> shc);  // TB origin in the CTB
-    Pel* body = c == 0 ? w.by : w.bc[c - 1];
-    const Pel* top = w.top[c];
-    const Pel* left = w.left[c];
-    const int st = f.pic_stride[c];
     const int bd = c ? f.bit_depth_c : f.bit_depth;
     const int maxv = (1 << bd) - 1;
     const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
-    // residual prefetch (independent of the chain)
-    int rr[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int i = lane + 64 * k;
-        rr[k] = (cbf && i < nn) ? RSc[(tu.y + (i >> log2n)) * st + tu.x + (i & (n - 1))] : 0;
-    }
     auto sample = [&](int x, int y) -> int {  // CTB-relative, x,y >= -1
         if (y < 0) return top[x + 1];
         if (x < 0) return left[y];
@@ -985,11 +881,10 @@ DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mas
             }
             s.ref[k] = v;
         }
-    } else {
-        for (int k = lane; k < L; k += 64) s.ref[k] = s.sub[k];
+        wave_sync();
     }
-    wave_sync();
-    const int* R = s.ref;
+    // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
+    const int* R = filt ? s.ref : s.sub;
     int dc = 0;
     if (mode == 1) {
         int part = 0;
@@ -998,10 +893,7 @@ DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mas
     }
     const int angle = kAngle[mode];
     const int inv = kInvAngle[mode];
-#pragma unroll
-    for (int kk = 0; kk < 16; kk++) {
-        const int i = lane + 64 * kk;
-        if (i >= nn) break;
+    for (int i = lane; i < nn; i += 64) {
         const int x = i & (n - 1), y = i >> log2n;
         int pv;
         if (mode == 0) {
@@ -1016,6 +908,7 @@ DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mas
             }
         } else if (mode >= 18) {
             const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
+            // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
             const int k1 = x + idx + 1, k2 = x + idx + 2;
             const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
             if (fr) {
@@ -1028,6 +921,7 @@ DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mas
                 pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
         } else {
             const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
+            // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
             const int k1 = y + idx + 1, k2 = y + idx + 2;
             const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
             if (fr) {
@@ -1039,47 +933,85 @@ DEVI void hevc_predict_tu_win(const h2j_frame& f, const h2j_tu& tu, uint64_t mas
             if (mode == 10 && c == 0 && n < 32 && y == 0)
                 pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
         }
-        body[(oy + y) * S + ox + x] = static_cast<Pel>(clip3(0, maxv, pv + rr[kk]));
+        int16_t* d = body + (oy + y) * S + ox + x;
+        const int r = cbf ? *d : 0;  // K0 residual, replaced in place by the reconstruction
+        *d = static_cast<int16_t>(clip3(0, maxv, pv + r));
     }
     wave_sync();
 }
 
-// Copy a CTB window body to / from the picture (only the part inside it).
-template <typename Pel, bool kStore>
-DEVI void hevc_ctb_io(const h2j_frame& f, uint8_t* arena, int cx0, int cy0, HWin<Pel>& w, int lane) {
-    for (int c = 0; c < 3; c++) {
-        const int shc = c ? 1 : 0;
-        const int S = (1 << f.log2ctb) >> shc;
-        const int x0 = cx0 >> shc, y0 = cy0 >> shc;
-        const int wc = min(S, (f.width >> shc) - x0), hc = min(S, (f.height >> shc) - y0);
-        Pel* P = plane<Pel>(f, arena, f.pic, c);
-        Pel* body = c == 0 ? w.by : w.bc[c - 1];
-        const int st = f.pic_stride[c];
-        const int per_row = wc >> 1;  // 2 samples per lane step (widths are multiples of 2 samples)
-        for (int i = lane; i < hc * per_row; i += 64) {
-            const int y = i / per_row, x = (i - y * per_row) * 2;
-            if (kStore) {
-                P[(y0 + y) * st + x0 + x] = body[y * S + x];
-                P[(y0 + y) * st + x0 + x + 1] = body[y * S + x + 1];
-            } else {
-                body[y * S + x] = P[(y0 + y) * st + x0 + x];
-                body[y * S + x + 1] = P[(y0 + y) * st + x0 + x + 1];
-            }
+// K0 residual of one CTB -> registers (16 B luma / 8 B chroma per load; all
+// loads issued back to back, consumed one CTB later).
+struct HRes {
+    uint4 y[8];
+    uint2 c[2][4];
+};
+DEVI void hevc_res_fetch(const h2j_frame& f, uint8_t* arena, int row, int cx, HRes& r, int lane) {
+    const int CS = 1 << f.log2ctb;
+    {
+        const int16_t* R = res_plane(f, arena, 0);
+        const int x0 = cx * CS, y0 = row * CS, cpr = CS >> 3, st = f.pic_stride[0];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 8;
+            // branch-free: clamp the address of an out-of-CTB/picture chunk, then select zero
+            const bool ok = yy < CS && y0 + yy < f.height && x0 + xx < f.width;
+            const uint4 v = *reinterpret_cast<const uint4*>(R + (ok ? (y0 + yy) * st + x0 + xx : 0));
+            r.y[j] = ok ? v : make_uint4(0, 0, 0, 0);
+        }
+    }
+    const int S = CS >> 1, x0 = cx * S, y0 = row * S, cpr = S >> 2;
+    const int Wc = f.width >> 1, Hc = f.height >> 1, st = f.pic_stride[1];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int16_t* R = res_plane(f, arena, c + 1);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 4;
+            const bool ok = yy < S && y0 + yy < Hc && x0 + xx < Wc;
+            const uint2 v = *reinterpret_cast<const uint2*>(R + (ok ? (y0 + yy) * st + x0 + xx : 0));
+            r.c[c][j] = ok ? v : make_uint2(0, 0);
         }
     }
 }
+DEVI void hevc_res_put(const h2j_frame& f, const HRes& r, int16_t* body, int lane) {
+    const int CS = 1 << f.log2ctb, cpr = CS >> 3;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int idx = lane + 64 * j;
+        if (idx < CS * cpr) *reinterpret_cast<uint4*>(body + idx * 8) = r.y[j];
+    }
+    const int S = CS >> 1, cpr2 = S >> 2;
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = lane + 64 * j;
+            if (idx < S * cpr2) *reinterpret_cast<uint2*>(body + hwin_base(c + 1) + idx * 4) = r.c[c][j];
+        }
+}
 
 template <typename Pel>
-DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HWin<Pel>& w, uint32_t* prog) {
+DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HevcK1Lds& L) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    HWinLds& w = L.w[wv];
     const uint64_t* masks = tu_masks(f, arena);
     const uint32_t* rng = ctb_ranges(f, arena);
     constexpr int kSlots = 2 * kK1Waves;
     const int CS = 1 << f.log2ctb;
-    const int16_t* RS[3] = {res_plane(f, arena, 0), res_plane(f, arena, 1), res_plane(f, arena, 2)};
+    const bool lds_line = f.width <= kLineMax;
+    if (wv >= f.ctb_h) return;
+    PROF_DECL;
+    // prefetch state for the wave's first CTB
+    HRes res;
+    hevc_res_fetch(f, arena, wv, 0, res, lane);
+    uint32_t na = rng[2 * (wv * f.ctb_w)], nb = rng[2 * (wv * f.ctb_w) + 1];
+    // record batches: lane l holds record a + l (clamped loads, no branches)
+    uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
+    uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
     for (int row = wv; row < f.ctb_h; row += kK1Waves) {
-        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
-        uint32_t* mine = prog + row % kSlots;
+        uint32_t* above = L.prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = L.prog + row % kSlots;
         uint32_t seen = 0;
         const int cy0 = row * CS;
         for (int cx = 0; cx < f.ctb_w; cx++) {
@@ -1092,57 +1024,95 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HWin<Pe
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
             }
-            // line above (incl. top-right reach) from the picture; left column from the previous CTB
+            PROF_LAP(0);
+            // line above (incl. the top-right reach of the largest TB); corner carried
             for (int c = 0; c < 3; c++) {
                 const int shc = c ? 1 : 0, S = CS >> shc, x0 = cx0 >> shc, y0 = cy0 >> shc;
                 const int Wc = f.width >> shc;
+                const int reach = min(2 * S, S + 32) + 1;
                 const Pel* P = plane<Pel>(f, arena, f.pic, c);
                 const int st = f.pic_stride[c];
-                const int reach = min(2 * S, S + 32) + 1;  // corner + CTB width + top-right of the largest TB
                 for (int i = lane; i < reach; i += 64) {
                     const int x = x0 - 1 + i;
-                    w.top[c][i] = (row > 0 && x >= 0 && x < Wc) ? P[(y0 - 1) * st + x] : Pel(0);
+                    int16_t v = 0;
+                    if (row > 0 && x >= 0 && x < Wc) {
+                        if (i == 0) v = w.corner[c];
+                        else v = lds_line ? L.line[line_base(c) + x] : static_cast<int16_t>(P[(y0 - 1) * st + x]);
+                    }
+                    w.top[c][i] = v;
                 }
                 if (cx == 0)
-                    for (int i = lane; i < S; i += 64) w.left[c][i] = Pel(0);
+                    for (int i = lane; i < S; i += 64) w.left[c][i] = 0;
             }
-            wave_sync();
-            const int cb = row * f.ctb_w + cx;
-            const uint32_t a = rng[2 * cb], b = rng[2 * cb + 1];
-            bool pcm_seen = false;
-            if (a < b) {
-                h2j_tu cur = T[a];
-                uint64_t cm = masks[a];
-                for (uint32_t t = a; t < b; t++) {
-                    h2j_tu nxt = cur;
-                    uint64_t nm = 0;
-                    if (t + 1 < b) {  // prefetch the next record
-                        nxt = T[t + 1];
-                        nm = masks[t + 1];
-                    }
-                    if (cur.flags & H2J_TU_PCM) {
-                        pcm_seen = true;  // samples written by K0: pull that block into the window
-                        const int shc = cur.c ? 1 : 0, S = CS >> shc, n = 1 << cur.log2n;
-                        const int ox = cur.x - (cx0 >> shc), oy = cur.y - (cy0 >> shc);
-                        const Pel* P = plane<Pel>(f, arena, f.pic, cur.c);
-                        Pel* body = cur.c == 0 ? w.by : w.bc[cur.c - 1];
-                        for (int i = lane; i < n * n; i += 64)
-                            body[(oy + i / n) * S + ox + (i % n)] =
-                                P[(cur.y + i / n) * f.pic_stride[cur.c] + cur.x + (i % n)];
-                        wave_sync();
-                    } else {
-                        hevc_predict_tu_win<Pel>(f, cur, cm, cx0, cy0, RS[cur.c], w, lane);
-                    }
-                    cur = nxt;
-                    cm = nm;
+            const uint32_t a = na, b = nb;
+            uint4 rec = nrec;
+            uint2 msk = nmsk;
+            hevc_res_put(f, res, w.body, lane);
+            // prefetch the wave's next CTB (residual + first record batch)
+            {
+                int nrow = row, ncx = cx + 1;
+                if (ncx == f.ctb_w) { ncx = 0; nrow += kK1Waves; }
+                if (nrow < f.ctb_h) {
+                    const int ncb = nrow * f.ctb_w + ncx;
+                    hevc_res_fetch(f, arena, nrow, ncx, res, lane);
+                    na = rng[2 * ncb];
+                    nb = rng[2 * ncb + 1];
+                    nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
+                    nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
                 }
             }
-            (void)pcm_seen;
-            hevc_ctb_io<Pel, true>(f, arena, cx0, cy0, w, lane);
-            // right column becomes the next CTB's left column
+            wave_sync();
+            PROF_LAP(1);
+            PROF_ADD(5, b - a);
+            PROF_ADD(6, 1);
+            for (uint32_t t = a; t < b; t++) {
+                const int l = static_cast<int>((t - a) & 63);
+                if (l == 0 && t != a) {  // next 64-record batch of a large CTB
+                    rec = reinterpret_cast<const uint4*>(T)[min(t + lane, b - 1)];
+                    msk = reinterpret_cast<const uint2*>(masks)[min(t + lane, b - 1)];
+                }
+                const h2j_tu tu = tu_from_lanes(rec, l);
+                const int c = tu.c, shc = c ? 1 : 0, S = CS >> shc;
+                const int ox = tu.x - (cx0 >> shc), oy = tu.y - (cy0 >> shc);
+                int16_t* body = w.body + hwin_base(c);
+                if (tu.flags & H2J_TU_PCM) {  // samples written by K0: pull that block into the window
+                    const int n = 1 << tu.log2n;
+                    const Pel* P = plane<Pel>(f, arena, f.pic, c);
+                    for (int i = lane; i < n * n; i += 64)
+                        body[(oy + i / n) * S + ox + (i % n)] =
+                            static_cast<int16_t>(P[(tu.y + i / n) * f.pic_stride[c] + tu.x + (i % n)]);
+                    wave_sync();
+                } else {
+                    hevc_predict_tb(f, tu, mask_from_lanes(msk, l), ox, oy, S, body, w.top[c], w.left[c], w.k, lane);
+                }
+                PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
+            }
+            PROF_LAP(2);
+            // store the CTB; leave its bottom line for the row below, carry the right column + corner
+            const bool below = row + 1 < f.ctb_h;
             for (int c = 0; c < 3; c++) {
-                const int S = CS >> (c ? 1 : 0);
-                const Pel* body = c == 0 ? w.by : w.bc[c - 1];
+                const int shc = c ? 1 : 0;
+                const int S = CS >> shc;
+                const int x0 = cx0 >> shc, y0 = cy0 >> shc;
+                const int wc = min(S, (f.width >> shc) - x0), hc = min(S, (f.height >> shc) - y0);
+                Pel* P = plane<Pel>(f, arena, f.pic, c);
+                const int16_t* body = w.body + hwin_base(c);
+                const int st = f.pic_stride[c];
+                const int q = wc >> 2;  // 4 samples per lane step (component widths are multiples of 4)
+                for (int i = lane; i < hc * q; i += 64) {
+                    const int y = i / q, x = (i - y * q) * 4;
+                    const uint2 v = *reinterpret_cast<const uint2*>(body + y * S + x);
+                    Pel* d = P + (y0 + y) * st + x0 + x;
+                    if (sizeof(Pel) == 1) {
+                        const uint32_t p = (v.x & 0xFF) | ((v.x >> 8) & 0xFF00) | ((v.y & 0xFF) << 16) | ((v.y >> 16) << 24);
+                        *reinterpret_cast<uint32_t*>(d) = p;
+                    } else {
+                        *reinterpret_cast<uint2*>(d) = v;
+                    }
+                }
+                if (below && lds_line)
+                    for (int i = lane; i < wc; i += 64) L.line[line_base(c) + x0 + i] = body[(S - 1) * S + i];
+                if (lane == 0) w.corner[c] = w.top[c][S];
                 for (int i = lane; i < S; i += 64) w.left[c][i] = body[i * S + S - 1];
             }
             wave_sync();
@@ -1150,42 +1120,10 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HWin<Pe
             if (lane == 0)
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            PROF_LAP(3);
         }
     }
-}
-
-template <typename Pel>
-DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1WaveLds& wl, uint32_t* prog) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t* masks = tu_masks(f, arena);
-    const uint32_t* rng = ctb_ranges(f, arena);
-    constexpr int kSlots = 2 * kK1Waves;
-    for (int row = w; row < f.ctb_h; row += kK1Waves) {
-        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
-        uint32_t* mine = prog + row % kSlots;
-        uint32_t seen = 0;
-        for (int cx = 0; cx < f.ctb_w; cx++) {
-            if (row > 0) {
-                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(cx + 2, f.ctb_w));
-                if (seen < need) {
-                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                        __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
-            }
-            const int cb = row * f.ctb_w + cx;
-            const uint32_t a = rng[2 * cb], b = rng[2 * cb + 1];
-            for (uint32_t t = a; t < b; t++) {
-                const h2j_tu tu = T[t];
-                if (tu.flags & H2J_TU_PCM) continue;  // written by K0
-                hevc_predict_tu<Pel>(f, tu, masks[t], arena, wl, lane);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0)
-                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
+    PROF_FLUSH();
 }
 
 // Separate kernels per codec so each gets its own register budget; a mixed
@@ -1193,13 +1131,12 @@ DEVI void predict_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, K1Wa
 template <typename Pel>
 __global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
                                                                   uint8_t* arena) {
-    __shared__ HWin<Pel> wl[kK1Waves];
-    __shared__ uint32_t prog[2 * kK1Waves];
+    __shared__ HevcK1Lds lds;
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
-    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kK1Waves) lds.prog[threadIdx.x] = 0;
     __syncthreads();
-    hevc_rows<Pel>(f, tus + f.tu, arena, wl[threadIdx.x >> 6], prog);
+    hevc_rows<Pel>(f, tus + f.tu, arena, lds);
 }
 
 __global__ void __launch_bounds__(64 * kK1Waves, 6) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
@@ -1884,6 +1821,24 @@ int h2j_gpu_prep(const h2j_gpu_batch* b, void* stream) {
     hipLaunchKernelGGL(h2j_k0_prep, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
                        b->slices, b->sl, b->arena);
     return check(hipGetLastError(), "h2j_k0_prep");
+}
+
+// K1 cycle accounting (only in -DH2J_PROF builds): copies 16 counters, optionally resets them.
+int h2j_gpu_prof(unsigned long long* out, int n, int reset) {
+#ifdef H2J_PROF
+    unsigned long long h[16] = {0};
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < 16; i++) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+#else
+    (void)out; (void)n; (void)reset;
+    return -1;
+#endif
 }
 
 int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {

@@ -20,7 +20,8 @@ _lib = None
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, _LIB_NAME)
+    # H2J_LIB_DIR selects an alternative build of the same libraries (e.g. build/prof)
+    return os.path.join(os.environ.get("H2J_LIB_DIR", _HERE), _LIB_NAME)
 
 
 def load_library() -> ctypes.CDLL:

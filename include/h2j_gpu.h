@@ -78,6 +78,8 @@ int h2j_gpu_recon(const h2j_gpu_batch *b, void *stream);
 /* the two halves of h2j_gpu_recon: K0 alone, then K1 alone */
 int h2j_gpu_prep(const h2j_gpu_batch *b, void *stream);
 int h2j_gpu_predict(const h2j_gpu_batch *b, void *stream);
+/* Diagnostics: K1 cycle counters of a -DH2J_PROF build (`make prof`); -1 otherwise. */
+int h2j_gpu_prof(unsigned long long *out, int n, int reset);
 /* K2: deblocking (vertical edges, then horizontal edges), in place on frame.pic */
 int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);
 /* K3: SAO frame.pic -> frame.pic2 (copies when SAO is off) */

@@ -1,0 +1,35 @@
+"""K1 cycle accounting: run N frames of a stream through the -DH2J_PROF build
+and print where the K1 waves spend their cycles (s_memtime, shader clock).
+  make -C h264-h265-to-jpeg_amd prof && python tools/k1prof.py tests/golden/bench/hevc1080_00.h265 256"""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
+os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", "prof")
+sys.path.insert(0, PKG)
+import h2j
+files = [a for a in sys.argv[1:] if not a.isdigit()]
+n = int([a for a in sys.argv[1:] if a.isdigit()][0]) if any(a.isdigit() for a in sys.argv[1:]) else 256
+eng = h2j.Engine(0)
+hip = ctypes.CDLL(os.path.join(os.environ["H2J_LIB_DIR"], "libh2j_hip.so"))
+buf = (ctypes.c_ulonglong * 16)()
+for path in files:
+    data = open(path, "rb").read()
+    eng.transcode([data] * 8)
+    hip.h2j_gpu_prof(buf, 16, 1)
+    outs = eng.transcode([data] * n)
+    assert all(o is not None for o in outs)
+    st = eng.stats()
+    if hip.h2j_gpu_prof(buf, 16, 1) != 0:
+        raise SystemExit("not a -DH2J_PROF build")
+    v = list(buf)
+    waves = None
+    tot = sum(v[0:4]) + sum(v[8:16])
+    ntu, nctb = v[5], v[6]
+    print(f"{os.path.basename(path)}: {n} frames, K1 {st['recon_ms']:.2f} ms, TUs {ntu}, CTBs {nctb}")
+    names = ["wait", "setup", "-", "store"]
+    for i, nm in enumerate(names):
+        if i != 2:
+            print(f"  {nm:8s} {v[i] / max(1, nctb):10.0f} cyc/CTB  {100 * v[i] / tot:5.1f}%")
+    for k in range(8):
+        print(f"  {'YC'[k // 4]} {4 << (k % 4):2d}x{4 << (k % 4):<2d} {v[8 + k] / max(1, nctb):10.0f} cyc/CTB  {100 * v[8 + k] / tot:5.1f}%")
+    print(f"  TU loop {sum(v[8:16]) / max(1, ntu):.0f} cyc/TU")
