@@ -177,7 +177,8 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
 constexpr int kK0Tus = 8;    // TUs per K0 wave
-constexpr int kK1Waves = 8;  // waves (CTB rows in flight) per picture in K1
+constexpr int kK1Waves = 8;    // HEVC K1: waves (CTB rows in flight) per picture
+constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
 struct K0Lds {
     int8_t mat[32][32];
@@ -524,10 +525,9 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
 // Inside a CTB the wave walks the TUs in decoding order: reference gather
 // with K0's availability mask, substitution / filtering, prediction, + K0's
 // residual, clip, store.  (H.265 8.4.4.2; H.264 8.3)
-struct K1WaveLds {  // HEVC
-    int seq[132];
-    int sub[132];
-    int ref[132];
+struct K1WaveLds {  // HEVC reference arrays (4n + 1 <= 129 samples)
+    int16_t sub[132];
+    int16_t ref[132];
 };
 
 // H.264: one macroblock plus its top line and left column, per wave.
@@ -673,14 +673,14 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t* masks = tu_masks(f, arena);
     const uint32_t* rng = ctb_ranges(f, arena);
-    constexpr int kSlots = 2 * kK1Waves;
+    constexpr int kSlots = 2 * kAvcWaves;
     Pel* PY = plane<Pel>(f, arena, f.pic, 0);
     Pel* PC[2] = {plane<Pel>(f, arena, f.pic, 1), plane<Pel>(f, arena, f.pic, 2)};
     const int16_t* RY = res_plane(f, arena, 0);
     const int16_t* RC[2] = {res_plane(f, arena, 1), res_plane(f, arena, 2)};
     const int sty = f.pic_stride[0], stc = f.pic_stride[1];
     const int W = f.width, Wc = f.width >> 1;
-    for (int row = w; row < f.ctb_h; row += kK1Waves) {
+    for (int row = w; row < f.ctb_h; row += kAvcWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
@@ -761,31 +761,78 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     }
 }
 
-// HEVC K1: each wave owns an int16 CTB window in LDS.  The K0 residual of the
-// whole CTB is prefetched into registers one CTB ahead and dropped into the
-// window when the CTB starts; every TB then reads its residual and writes its
-// reconstruction in place (a TB only ever reads neighbours that are already
-// reconstructed, so the two never alias).  The line above comes from an LDS
-// line buffer shared by the picture's waves (each row leaves its bottom line
-// there), the left column and the top-left corner are carried from the
-// previous CTB, and the TU records stream in 64-record batches held one per
-// lane (readlane).  HBM is touched only by the prefetches and the CTB store.
-constexpr int kLineMax = 4096;  // widest picture whose line above is served from LDS
+// HEVC K1.  Per picture, two workgroups run side by side: group 0 walks the
+// luma TB chain, group 1 the Cb/Cr chains (intra prediction never crosses
+// components, H.265 8.4.4.2.1), halving the dependent chain each one walks.
+// Wave w of a group reconstructs CTB rows w, w + kK1Waves, ... one 32x32
+// quadrant (16x16 chroma) at a time — the z-scan visits quadrants in order and
+// no TB is larger than 32x32 — in a small int16 LDS window, so a group needs
+// ~36 KB of LDS and several pictures share a CU.  The quadrant's K0 residual
+// is prefetched into registers one quadrant ahead and dropped into the window
+// when the quadrant starts; every TB reads its residual and writes its
+// reconstruction in place (a TB only reads neighbours that are already
+// reconstructed, so the two never alias).  Neighbours come from LDS only: the
+// line above from a per-group line buffer (each CTB row leaves its bottom line
+// there), the rest from carries (previous CTB's right column, the top
+// quadrants' bottom rows, the left quadrant's right column, the next CTB's
+// top-left corner).  TU records stream in 64-record batches held one per lane
+// (readlane).  HBM is touched only by the prefetches and the quadrant stores.
+// Frame fields the K1 loops use, read once into scalar registers.  Reading
+// them through the h2j_frame reference inside the loops made the compiler
+// re-load them from global memory after every fence, each time waiting for
+// every outstanding load and store of the wave (vmcnt(0)).  Per-component
+// values are selected, never indexed, so nothing lands in scratch.
+DEVI uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+DEVI uint64_t ufl64(uint64_t v) {
+    return (static_cast<uint64_t>(ufl(static_cast<uint32_t>(v >> 32))) << 32) | ufl(static_cast<uint32_t>(v));
+}
+// (pointers stay `arena + uniform offset`, so the compiler keeps them global
+// and emits global_load, not flat_load — flat ops would also hold lgkmcnt)
+struct FU {
+    int width, height, log2ctb, ctb_w, ctb_h, bd, bdc, strong, sty, stc;
+    uint8_t* pic;     // plane 0 base (bytes); planes 1/2 at off1/off2 elements
+    int16_t* res;     // residual plane 0; planes 1/2 at the same element offsets
+    int off1, off2;
+    DEVI int st(int c) const { return c ? stc : sty; }
+    DEVI int off(int c) const { return c == 0 ? 0 : (c == 1 ? off1 : off2); }
+    template <typename Pel>
+    DEVI Pel* plane(int c) const { return reinterpret_cast<Pel*>(pic) + off(c); }
+    DEVI const int16_t* rplane(int c) const { return res + off(c); }
+};
+DEVI FU make_fu(const h2j_frame& f, uint8_t* arena) {
+    FU u;
+    u.width = ufl(f.width);
+    u.height = ufl(f.height);
+    u.log2ctb = ufl(f.log2ctb);
+    u.ctb_w = ufl(f.ctb_w);
+    u.ctb_h = ufl(f.ctb_h);
+    u.bd = ufl(f.bit_depth);
+    u.bdc = ufl(f.bit_depth_c);
+    u.strong = ufl(f.strong_smoothing);
+    u.sty = ufl(f.pic_stride[0]);
+    u.stc = ufl(f.pic_stride[1]);
+    u.off1 = ufl(f.pic_off[1]);
+    u.off2 = ufl(f.pic_off[2]);
+    u.pic = arena + ufl64(f.pic);
+    u.res = reinterpret_cast<int16_t*>(arena + ufl64(f.res));
+    return u;
+}
 
-struct HWinLds {
-    int16_t body[64 * 64 + 2 * 32 * 32];  // Y | Cb | Cr, row stride = CTB size of the component
-    int16_t top[3][132];                  // y = -1: x = -1 .. 130 (index x + 1)
-    int16_t left[3][64];                  // x = -1
-    int16_t corner[4];                    // carried top-left sample of the next CTB
+struct QComp {              // one component's carried neighbours (quadrant size Qc <= 32, CTB size Sc <= 64)
+    int16_t top[68];        // y = -1: x = -1 .. 2Qc-1 (index x + 1)
+    int16_t left[64];       // x = -1: y = 0 .. 2Qc-1
+    int16_t prevR[2][64];   // right column of the previous CTB (double-buffered by CTB parity)
+    int16_t qbot[64];       // bottom rows of the top quadrant row (TL | TR)
+    int16_t qright[32];     // right column of the left quadrant (TL for TR, BL for BR)
+    int16_t corner, pad;    // top-left sample of the next CTB
+};
+struct QWave {
+    int16_t body[32 * 32];  // luma quadrant | Cb at 0 and Cr at 256 (16x16 each)
+    QComp cs[2];            // luma: cs[0]; chroma: Cb cs[0], Cr cs[1]
     K1WaveLds k;
 };
-struct HevcK1Lds {
-    HWinLds w[kK1Waves];
-    int16_t line[2 * kLineMax];  // bottom line of the last finished CTB per column: Y | Cb | Cr
-    uint32_t prog[2 * kK1Waves];
-};
-DEVI int hwin_base(int c) { return c == 0 ? 0 : 64 * 64 + (c - 1) * 32 * 32; }
-DEVI int line_base(int c) { return c == 0 ? 0 : kLineMax + (c - 1) * (kLineMax / 2); }
+// dynamic LDS of one K1 group: QWave[kK1Waves], prog[2 * kK1Waves], line[2 * max width] (int16)
+constexpr size_t kK1FixedLds = sizeof(QWave) * kK1Waves + 2 * kK1Waves * sizeof(uint32_t);
 
 DEVI h2j_tu tu_from_lanes(const uint4& r, int l) {
     uint32_t w[4];
@@ -802,60 +849,67 @@ DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
            (static_cast<uint64_t>(__builtin_amdgcn_readlane(m.y, l)) << 32);
 }
 
-// One HEVC TB predicted + reconstructed inside the wave's CTB window.
-DEVI void hevc_predict_tb(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
+// Wave-wide integer sum with DPP row shifts + row broadcasts (no LDS trip);
+// call with all 64 lanes active.
+DEVI int wave_sum_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+// One HEVC TB predicted + reconstructed inside the wave's CTB window
+// (H.265 8.4.4.2.2 substitution, 8.4.4.2.3 filtering, 8.4.4.2.4-6 planar / DC /
+// angular).  Reference index k: 0 .. 2n-1 = p(-1, 2n-1-k), 2n = p(-1,-1),
+// 2n+1 .. 4n = p(k-2n-1, -1).  Each lane first resolves which sample its
+// (possibly substituted) reference comes from using only the availability
+// ballots, then reads it with one LDS load.
+DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
                           const int16_t* top, const int16_t* left, K1WaveLds& s, int lane) {
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int bd = c ? u.bdc : u.bd;
     const int maxv = (1 << bd) - 1;
     const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
-    auto sample = [&](int x, int y) -> int {  // CTB-relative, x,y >= -1
-        if (y < 0) return top[x + 1];
-        if (x < 0) return left[y];
-        return body[y * S + x];
-    };
     const int L = 4 * n + 1;
     const int ush = c ? 1 : 2, nu = (2 * n) >> ush;
-    unsigned long long m0 = 0, m1 = 0, m2 = 0;
-    for (int base = 0; base < L; base += 64) {
-        const int k = base + lane;
-        bool a = false;
-        if (k < L) {
-            int xn, yn, unit;
-            if (k < 2 * n) { xn = ox - 1; yn = oy + (2 * n - 1 - k); unit = k >> ush; }
-            else if (k == 2 * n) { xn = ox - 1; yn = oy - 1; unit = nu; }
-            else { xn = ox + (k - 2 * n - 1); yn = oy - 1; unit = nu + 1 + ((k - 2 * n - 1) >> ush); }
-            a = (mask >> unit) & 1ull;
-            s.seq[k] = a ? sample(xn, yn) : 0;
+    const int nch = (L + 63) >> 6;  // 1 (n <= 8 luma / n <= 8 chroma), 2 (n = 16), 3 (n = 32)
+    // availability ballots (unit = 4 luma / 2 chroma samples; bit nu = corner)
+    unsigned long long m[3] = {0, 0, 0};
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        if (ch < nch) {
+            const int k = lane + 64 * ch;
+            const int unit = k < 2 * n ? (k >> ush) : (k == 2 * n ? nu : nu + 1 + ((k - 2 * n - 1) >> ush));
+            const bool a = k < L && ((mask >> unit) & 1ull);
+            m[ch] = __ballot(a);
         }
-        const unsigned long long bal = __ballot(a);
-        if (base == 0) m0 = bal; else if (base == 64) m1 = bal; else m2 = bal;
     }
-    wave_sync();
-    const bool any = (m0 | m1 | m2) != 0;
-    for (int k = lane; k < L; k += 64) {
-        int v;
-        if (!any) {
-            v = 1 << (bd - 1);
-        } else {
-            const int ch = k >> 6, bit = k & 63;
-            const unsigned long long mk = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
-            if ((mk >> bit) & 1ull) {
-                v = s.seq[k];
-            } else {
-                int j = -1;
-                const unsigned long long below = bit ? (mk & ((1ull << bit) - 1)) : 0ull;
-                if (below) j = (ch << 6) + 63 - __clzll(below);
-                else if (ch >= 2 && m1) j = 64 + 63 - __clzll(m1);
-                else if (ch >= 1 && m0) j = 63 - __clzll(m0);
-                if (j < 0) j = m0 ? __ffsll(static_cast<long long>(m0)) - 1
-                                  : (m1 ? 64 + __ffsll(static_cast<long long>(m1)) - 1 : 128);
-                v = s.seq[j];
-            }
+    const bool any = (m[0] | m[1] | m[2]) != 0;
+    const int first = m[0] ? __ffsll(static_cast<long long>(m[0])) - 1
+                           : (m[1] ? 64 + __ffsll(static_cast<long long>(m[1])) - 1 : 128);
+    int dcpart = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        if (ch < nch) {
+            const int k = lane + 64 * ch;
+            // last available index <= k, else the first available one (8.4.4.2.2)
+            const unsigned long long le = m[ch] & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+            int j = le ? 64 * ch + 63 - __clzll(le) : -1;
+            if (j < 0 && ch >= 2 && m[1]) j = 64 + 63 - __clzll(m[1]);
+            if (j < 0 && ch >= 1 && m[0]) j = 63 - __clzll(m[0]);
+            if (j < 0) j = first;
+            const int xn = j <= 2 * n ? ox - 1 : ox + (j - 2 * n - 1);
+            const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
+            const int16_t* src = yn < 0 ? top + (xn + 1) : (xn < 0 ? left + yn : body + yn * S + xn);
+            int v = any ? static_cast<int>(*src) : (1 << (bd - 1));
+            if (k < L) s.sub[k] = v;
+            // DC: p(-1, 0..n-1) = k in [n, 2n), p(0..n-1, -1) = k in [2n+1, 3n]
+            dcpart += (k >= n && k <= 3 * n && k != 2 * n) ? v : 0;
         }
-        s.sub[k] = v;
     }
-    wave_sync();
     const int mode = tu.mode;
     bool filt = false;
     if (c == 0 && mode != 1 && n != 4) {
@@ -864,263 +918,294 @@ DEVI void hevc_predict_tb(const h2j_frame& f, const h2j_tu& tu, uint64_t mask, i
         const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
         filt = mode == 0 || md > thr;
     }
+    int dc = 0;
+    if (mode == 1) dc = (wave_sum_dpp(dcpart) + n) >> (log2n + 1);
+    wave_sync();
     if (filt) {
         const int corner = s.sub[2 * n];
-        const bool strong = f.strong_smoothing && n == 32 &&
+        const bool strong = u.strong && n == 32 &&
                             abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
                             abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
-        for (int k = lane; k < L; k += 64) {
-            int v;
-            if (k == 0 || k == 4 * n) v = s.sub[k];
-            else if (strong) {
-                if (k == 2 * n) v = corner;
-                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * s.sub[0] + 32) >> 6; }
-                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * s.sub[4 * n] + 32) >> 6; }
-            } else {
-                v = (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
+        if (strong) {
+            const int bl = s.sub[0], tr = s.sub[4 * n];
+            for (int k = lane; k < L; k += 64) {
+                int v;
+                if (k == 0 || k == 4 * n || k == 2 * n) v = s.sub[k];
+                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * bl + 32) >> 6; }
+                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * tr + 32) >> 6; }
+                s.ref[k] = v;
             }
-            s.ref[k] = v;
+        } else {
+            for (int k = lane; k < L; k += 64) {
+                const int v = (k == 0 || k == 4 * n) ? s.sub[k] : (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
+                s.ref[k] = v;
+            }
         }
         wave_sync();
     }
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
-    const int* R = filt ? s.ref : s.sub;
-    int dc = 0;
-    if (mode == 1) {
-        int part = 0;
-        for (int k = lane; k < n; k += 64) part += R[2 * n - 1 - k] + R[2 * n + 1 + k];
-        dc = (wave_sum(part) + n) >> (log2n + 1);
-    }
-    const int angle = kAngle[mode];
-    const int inv = kInvAngle[mode];
-    for (int i = lane; i < nn; i += 64) {
-        const int x = i & (n - 1), y = i >> log2n;
-        int pv;
-        if (mode == 0) {
-            pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * R[3 * n + 1] + (n - 1 - y) * R[2 * n + 1 + x] +
-                  (y + 1) * R[n - 1] + n) >> (log2n + 1);
-        } else if (mode == 1) {
-            pv = dc;
-            if (c == 0 && n < 32) {
+    const int16_t* R = filt ? s.ref : s.sub;
+    const int edge = c == 0 && n < 32;  // DC / pure horizontal / pure vertical boundary smoothing
+    if (mode == 0) {
+        const int tr = R[3 * n + 1], bl = R[n - 1];
+        for (int i = lane; i < nn; i += 64) {
+            const int x = i & (n - 1), y = i >> log2n;
+            const int pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * tr + (n - 1 - y) * R[2 * n + 1 + x] +
+                            (y + 1) * bl + n) >> (log2n + 1);
+            int16_t* d = body + (oy + y) * S + ox + x;
+            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+        }
+    } else if (mode == 1) {
+        for (int i = lane; i < nn; i += 64) {
+            const int x = i & (n - 1), y = i >> log2n;
+            int pv = dc;
+            if (edge && (x == 0 || y == 0)) {
                 if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
                 else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                else if (x == 0) pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                else pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
             }
-        } else if (mode >= 18) {
-            const int idx = ((y + 1) * angle) >> 5, fr = ((y + 1) * angle) & 31;
-            // refV(k): k>=0 -> p(k-1,-1) ; k<0 -> p(-1, ((k*inv+128)>>8)-1)
-            const int k1 = x + idx + 1, k2 = x + idx + 2;
-            const int r1 = k1 >= 0 ? R[2 * n + k1] : R[2 * n - ((k1 * inv + 128) >> 8)];
-            if (fr) {
-                const int r2 = k2 >= 0 ? R[2 * n + k2] : R[2 * n - ((k2 * inv + 128) >> 8)];
-                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-            } else {
-                pv = r1;
-            }
-            if (mode == 26 && c == 0 && n < 32 && x == 0)
-                pv = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - 1 - y] - R[2 * n]) >> 1));
-        } else {
-            const int idx = ((x + 1) * angle) >> 5, fr = ((x + 1) * angle) & 31;
-            // refH(k): k>=0 -> p(-1,k-1) ; k<0 -> p(((k*inv+128)>>8)-1, -1)
-            const int k1 = y + idx + 1, k2 = y + idx + 2;
-            const int r1 = k1 >= 0 ? R[2 * n - k1] : R[2 * n + ((k1 * inv + 128) >> 8)];
-            if (fr) {
-                const int r2 = k2 >= 0 ? R[2 * n - k2] : R[2 * n + ((k2 * inv + 128) >> 8)];
-                pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
-            } else {
-                pv = r1;
-            }
-            if (mode == 10 && c == 0 && n < 32 && y == 0)
-                pv = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + 1 + x] - R[2 * n]) >> 1));
+            int16_t* d = body + (oy + y) * S + ox + x;
+            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
-        int16_t* d = body + (oy + y) * S + ox + x;
-        const int r = cbf ? *d : 0;  // K0 residual, replaced in place by the reconstruction
-        *d = static_cast<int16_t>(clip3(0, maxv, pv + r));
+    } else {
+        const int angle = kAngle[mode], inv = kInvAngle[mode];
+        const bool vert = mode >= 18;
+        // vertical: main = top row (refV(k) = R[2n + k], k < 0 projected from the left column);
+        // horizontal: main = left column (refH(k) = R[2n - k], k < 0 projected from the top row)
+        const int sgn = vert ? 1 : -1;
+        const bool bnd = edge && (mode == 26 || mode == 10);
+        for (int i = lane; i < nn; i += 64) {
+            const int x = i & (n - 1), y = i >> log2n;
+            const int a = vert ? y : x, b = vert ? x : y;  // a: distance from the main reference, b: position along it
+            const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+            const int k1 = b + idx + 1, k2 = k1 + 1;
+            const int i1 = k1 >= 0 ? 2 * n + sgn * k1 : 2 * n - sgn * ((k1 * inv + 128) >> 8);
+            const int i2 = k2 >= 0 ? 2 * n + sgn * k2 : 2 * n - sgn * ((k2 * inv + 128) >> 8);
+            int pv = ((32 - fr) * R[i1] + fr * R[i2] + 16) >> 5;
+            if (bnd && b == 0) pv = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n - sgn * (a + 1)] - R[2 * n]) >> 1));
+            int16_t* d = body + (oy + y) * S + ox + x;
+            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+        }
     }
     wave_sync();
 }
 
-// K0 residual of one CTB -> registers (16 B luma / 8 B chroma per load; all
-// loads issued back to back, consumed one CTB later).
-struct HRes {
-    uint4 y[8];
-    uint2 c[2][4];
-};
-DEVI void hevc_res_fetch(const h2j_frame& f, uint8_t* arena, int row, int cx, HRes& r, int lane) {
-    const int CS = 1 << f.log2ctb;
-    {
-        const int16_t* R = res_plane(f, arena, 0);
-        const int x0 = cx * CS, y0 = row * CS, cpr = CS >> 3, st = f.pic_stride[0];
+// K0 residual of one quadrant -> registers.  Luma: 2 x 16 B chunks per lane
+// (32x32 int16); chroma: one 8 B chunk of Cb in .xy and of Cr in .zw.
+DEVI void hevc_qres_fetch(const FU& u, int grp, int X0, int Y0, int Qc, uint4 (&r)[2], int lane) {
+    if (grp == 0) {
+        const int16_t* R = u.rplane(0);
+        const int cpr = Qc >> 3;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 2; j++) {
             const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 8;
-            // branch-free: clamp the address of an out-of-CTB/picture chunk, then select zero
-            const bool ok = yy < CS && y0 + yy < f.height && x0 + xx < f.width;
-            const uint4 v = *reinterpret_cast<const uint4*>(R + (ok ? (y0 + yy) * st + x0 + xx : 0));
-            r.y[j] = ok ? v : make_uint4(0, 0, 0, 0);
+            const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
+            const uint4 v = *reinterpret_cast<const uint4*>(R + (ok ? (Y0 + yy) * u.sty + X0 + xx : 0));
+            r[j] = ok ? v : make_uint4(0, 0, 0, 0);
         }
-    }
-    const int S = CS >> 1, x0 = cx * S, y0 = row * S, cpr = S >> 2;
-    const int Wc = f.width >> 1, Hc = f.height >> 1, st = f.pic_stride[1];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-        const int16_t* R = res_plane(f, arena, c + 1);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 4;
-            const bool ok = yy < S && y0 + yy < Hc && x0 + xx < Wc;
-            const uint2 v = *reinterpret_cast<const uint2*>(R + (ok ? (y0 + yy) * st + x0 + xx : 0));
-            r.c[c][j] = ok ? v : make_uint2(0, 0);
-        }
+    } else {
+        const int cpr = Qc >> 2, yy = lane / cpr, xx = (lane - yy * cpr) * 4;
+        const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
+        const int o = ok ? (Y0 + yy) * u.stc + X0 + xx : 0;
+        const uint2 b = *reinterpret_cast<const uint2*>(u.rplane(1) + o);
+        const uint2 c = *reinterpret_cast<const uint2*>(u.rplane(2) + o);
+        r[0] = ok ? make_uint4(b.x, b.y, c.x, c.y) : make_uint4(0, 0, 0, 0);
     }
 }
-DEVI void hevc_res_put(const h2j_frame& f, const HRes& r, int16_t* body, int lane) {
-    const int CS = 1 << f.log2ctb, cpr = CS >> 3;
+DEVI void hevc_qres_put(int grp, int Qc, const uint4 (&r)[2], int16_t* body, int lane) {
+    if (grp == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const int idx = lane + 64 * j;
-        if (idx < CS * cpr) *reinterpret_cast<uint4*>(body + idx * 8) = r.y[j];
-    }
-    const int S = CS >> 1, cpr2 = S >> 2;
-#pragma unroll
-    for (int c = 0; c < 2; c++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < 2; j++) {
             const int idx = lane + 64 * j;
-            if (idx < S * cpr2) *reinterpret_cast<uint2*>(body + hwin_base(c + 1) + idx * 4) = r.c[c][j];
+            if (idx < Qc * (Qc >> 3)) *reinterpret_cast<uint4*>(body + idx * 8) = r[j];
         }
+    } else if (lane < Qc * (Qc >> 2)) {
+        *reinterpret_cast<uint2*>(body + lane * 4) = make_uint2(r[0].x, r[0].y);
+        *reinterpret_cast<uint2*>(body + 256 + lane * 4) = make_uint2(r[0].z, r[0].w);
+    }
 }
 
 template <typename Pel>
-DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HevcK1Lds& L) {
+DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
+                    int16_t* line) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    HWinLds& w = L.w[wv];
-    const uint64_t* masks = tu_masks(f, arena);
-    const uint32_t* rng = ctb_ranges(f, arena);
+    QWave& w = W[wv];
+    const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
     constexpr int kSlots = 2 * kK1Waves;
-    const int CS = 1 << f.log2ctb;
-    const bool lds_line = f.width <= kLineMax;
-    if (wv >= f.ctb_h) return;
+    const FU u = make_fu(f, arena);
+    if (wv >= u.ctb_h) return;
+    const int shc = grp ? 1 : 0;                 // component subsampling of this group
+    const int CS = 1 << u.log2ctb;               // luma CTB size
+    const int Sc = CS >> shc;                    // CTB size in this group's components
+    const int Q = CS == 64 ? 32 : CS;            // luma quadrant size
+    const int Qc = Q >> shc;
+    const int nqs = CS / Q;                      // quadrants per side (2 or 1)
+    const int Wc = u.width >> shc, Hc = u.height >> shc;
+    const int ncomp = grp ? 2 : 1;
     PROF_DECL;
-    // prefetch state for the wave's first CTB
-    HRes res;
-    hevc_res_fetch(f, arena, wv, 0, res, lane);
-    uint32_t na = rng[2 * (wv * f.ctb_w)], nb = rng[2 * (wv * f.ctb_w) + 1];
-    // record batches: lane l holds record a + l (clamped loads, no branches)
+    // the wave's quadrant sequence: rows wv, wv + kK1Waves, ..., CTBs left to right, z-order
+    // quadrants, skipping quadrants outside the picture
+    auto q_inside = [&](int row, int cx, int q) {
+        return cx * Sc + (q & 1) * Qc < Wc && row * Sc + (q >> 1) * Qc < Hc;
+    };
+    auto q_next = [&](int& row, int& cx, int& q) {  // advance to the next quadrant inside the picture
+        do {
+            if (++q == nqs * nqs) {
+                q = 0;
+                if (++cx == u.ctb_w) { cx = 0; row += kK1Waves; }
+            }
+        } while (row < u.ctb_h && !q_inside(row, cx, q));
+    };
+    uint4 res[2];
+    hevc_qres_fetch(u, grp, 0, wv * Sc, Qc, res, lane);
+    uint32_t na = rng[2 * (wv * u.ctb_w)], nb = rng[2 * (wv * u.ctb_w) + 1];
     uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
     uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
-    for (int row = wv; row < f.ctb_h; row += kK1Waves) {
-        uint32_t* above = L.prog + (row + kSlots - 1) % kSlots;
-        uint32_t* mine = L.prog + row % kSlots;
+    for (int row = wv; row < u.ctb_h; row += kK1Waves) {
+        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
-        const int cy0 = row * CS;
-        for (int cx = 0; cx < f.ctb_w; cx++) {
-            const int cx0 = cx * CS;
-            if (row > 0) {
-                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(cx + 2, f.ctb_w));
-                if (seen < need) {
-                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                        __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
-            }
-            PROF_LAP(0);
-            // line above (incl. the top-right reach of the largest TB); corner carried
-            for (int c = 0; c < 3; c++) {
-                const int shc = c ? 1 : 0, S = CS >> shc, x0 = cx0 >> shc, y0 = cy0 >> shc;
-                const int Wc = f.width >> shc;
-                const int reach = min(2 * S, S + 32) + 1;
-                const Pel* P = plane<Pel>(f, arena, f.pic, c);
-                const int st = f.pic_stride[c];
-                for (int i = lane; i < reach; i += 64) {
-                    const int x = x0 - 1 + i;
-                    int16_t v = 0;
-                    if (row > 0 && x >= 0 && x < Wc) {
-                        if (i == 0) v = w.corner[c];
-                        else v = lds_line ? L.line[line_base(c) + x] : static_cast<int16_t>(P[(y0 - 1) * st + x]);
-                    }
-                    w.top[c][i] = v;
-                }
-                if (cx == 0)
-                    for (int i = lane; i < S; i += 64) w.left[c][i] = 0;
-            }
+        const bool below = row + 1 < u.ctb_h;
+        for (int cx = 0; cx < u.ctb_w; cx++) {
+            const int CX0 = cx * Sc, CY0 = row * Sc;
+            const int pin = cx & 1, pprev = pin ^ 1;   // prevR slot written by this CTB / read from the previous
+            // this CTB's record range + first batch (prefetched); prefetch the next CTB's
             const uint32_t a = na, b = nb;
+            uint32_t t = a, tb = a;
             uint4 rec = nrec;
             uint2 msk = nmsk;
-            hevc_res_put(f, res, w.body, lane);
-            // prefetch the wave's next CTB (residual + first record batch)
             {
                 int nrow = row, ncx = cx + 1;
-                if (ncx == f.ctb_w) { ncx = 0; nrow += kK1Waves; }
-                if (nrow < f.ctb_h) {
-                    const int ncb = nrow * f.ctb_w + ncx;
-                    hevc_res_fetch(f, arena, nrow, ncx, res, lane);
+                if (ncx == u.ctb_w) { ncx = 0; nrow += kK1Waves; }
+                if (nrow < u.ctb_h) {
+                    const int ncb = nrow * u.ctb_w + ncx;
                     na = rng[2 * ncb];
                     nb = rng[2 * ncb + 1];
                     nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
                     nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
                 }
             }
-            wave_sync();
-            PROF_LAP(1);
-            PROF_ADD(5, b - a);
-            PROF_ADD(6, 1);
-            for (uint32_t t = a; t < b; t++) {
-                const int l = static_cast<int>((t - a) & 63);
-                if (l == 0 && t != a) {  // next 64-record batch of a large CTB
-                    rec = reinterpret_cast<const uint4*>(T)[min(t + lane, b - 1)];
-                    msk = reinterpret_cast<const uint2*>(masks)[min(t + lane, b - 1)];
-                }
-                const h2j_tu tu = tu_from_lanes(rec, l);
-                const int c = tu.c, shc = c ? 1 : 0, S = CS >> shc;
-                const int ox = tu.x - (cx0 >> shc), oy = tu.y - (cy0 >> shc);
-                int16_t* body = w.body + hwin_base(c);
-                if (tu.flags & H2J_TU_PCM) {  // samples written by K0: pull that block into the window
-                    const int n = 1 << tu.log2n;
-                    const Pel* P = plane<Pel>(f, arena, f.pic, c);
-                    for (int i = lane; i < n * n; i += 64)
-                        body[(oy + i / n) * S + ox + (i % n)] =
-                            static_cast<int16_t>(P[(tu.y + i / n) * f.pic_stride[c] + tu.x + (i % n)]);
-                    wave_sync();
-                } else {
-                    hevc_predict_tb(f, tu, mask_from_lanes(msk, l), ox, oy, S, body, w.top[c], w.left[c], w.k, lane);
-                }
-                PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
-            }
-            PROF_LAP(2);
-            // store the CTB; leave its bottom line for the row below, carry the right column + corner
-            const bool below = row + 1 < f.ctb_h;
-            for (int c = 0; c < 3; c++) {
-                const int shc = c ? 1 : 0;
-                const int S = CS >> shc;
-                const int x0 = cx0 >> shc, y0 = cy0 >> shc;
-                const int wc = min(S, (f.width >> shc) - x0), hc = min(S, (f.height >> shc) - y0);
-                Pel* P = plane<Pel>(f, arena, f.pic, c);
-                const int16_t* body = w.body + hwin_base(c);
-                const int st = f.pic_stride[c];
-                const int q = wc >> 2;  // 4 samples per lane step (component widths are multiples of 4)
-                for (int i = lane; i < hc * q; i += 64) {
-                    const int y = i / q, x = (i - y * q) * 4;
-                    const uint2 v = *reinterpret_cast<const uint2*>(body + y * S + x);
-                    Pel* d = P + (y0 + y) * st + x0 + x;
-                    if (sizeof(Pel) == 1) {
-                        const uint32_t p = (v.x & 0xFF) | ((v.x >> 8) & 0xFF00) | ((v.y & 0xFF) << 16) | ((v.y >> 16) << 24);
-                        *reinterpret_cast<uint32_t*>(d) = p;
-                    } else {
-                        *reinterpret_cast<uint2*>(d) = v;
+            for (int q = 0; q < nqs * nqs; q++) {
+                if (!q_inside(row, cx, q)) continue;
+                const int qx = q & 1, qy = q >> 1;
+                const int X0 = CX0 + qx * Qc, Y0 = CY0 + qy * Qc;
+                // top quadrants need the row above: TL up to this CTB, TR up to the next one
+                if (row > 0 && qy == 0) {
+                    const uint32_t need = (static_cast<uint32_t>(row) << 16) |
+                                          static_cast<uint32_t>(min(cx + 1 + (qx == nqs - 1 ? 1 : 0), u.ctb_w));
+                    if (seen < need) {
+                        while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                            __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                     }
                 }
-                if (below && lds_line)
-                    for (int i = lane; i < wc; i += 64) L.line[line_base(c) + x0 + i] = body[(S - 1) * S + i];
-                if (lane == 0) w.corner[c] = w.top[c][S];
-                for (int i = lane; i < S; i += 64) w.left[c][i] = body[i * S + S - 1];
+                PROF_LAP(0);
+                // neighbour arrays of the quadrant
+                for (int ci = 0; ci < ncomp; ci++) {
+                    QComp& C = w.cs[ci];
+                    const int16_t* ln = line + ci * (Wc + 64);
+                    for (int i = lane; i <= 2 * Qc; i += 64) {  // top, x = i - 1
+                        const int x = i - 1;
+                        int16_t v = 0;
+                        if (qy == 0) {
+                            if (row > 0 && X0 + x >= 0 && X0 + x < Wc)
+                                v = (x < 0 && qx == 0) ? C.corner : ln[X0 + x];
+                        } else if (x < 0) {
+                            v = qx == 0 ? (cx > 0 ? C.prevR[pprev][Qc - 1] : int16_t(0)) : C.qbot[Qc - 1];
+                        } else if (qx * Qc + x < 2 * Qc) {
+                            v = C.qbot[qx * Qc + x];
+                        }
+                        C.top[i] = v;
+                    }
+                    for (int y = lane; y < 2 * Qc; y += 64) {  // left column
+                        int16_t v = 0;
+                        if (qx == 0) {
+                            if (cx > 0 && qy * Qc + y < Sc) v = C.prevR[pprev][qy * Qc + y];
+                        } else if (y < Qc) {
+                            v = C.qright[y];
+                        }
+                        C.left[y] = v;
+                    }
+                }
+                hevc_qres_put(grp, Qc, res, w.body, lane);
+                {  // prefetch the next quadrant's residual
+                    int nr = row, nc = cx, nq = q;
+                    q_next(nr, nc, nq);
+                    if (nr < u.ctb_h)
+                        hevc_qres_fetch(u, grp, nc * Sc + (nq & 1) * Qc, nr * Sc + (nq >> 1) * Qc, Qc, res, lane);
+                }
+                wave_sync();
+                PROF_LAP(1);
+                // this group's TBs of quadrant q (records are in z-scan order)
+                while (t < b) {
+                    if (t - tb >= 64) {  // next 64-record batch
+                        tb = t;
+                        rec = reinterpret_cast<const uint4*>(T)[min(t + lane, b - 1)];
+                        msk = reinterpret_cast<const uint2*>(masks)[min(t + lane, b - 1)];
+                    }
+                    const int l = static_cast<int>(t - tb);
+                    const h2j_tu tu = tu_from_lanes(rec, l);
+                    const int c = tu.c;
+                    if ((c > 0) != (grp > 0)) { t++; continue; }
+                    const int ox = tu.x - X0, oy = tu.y - Y0;
+                    if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
+                    const int ci = c == 2 ? 1 : 0;
+                    int16_t* body = w.body + ci * 256;
+                    if (tu.flags & H2J_TU_PCM) {  // samples written by K0: pull that block into the window
+                        const int n = 1 << tu.log2n;
+                        const Pel* P = u.plane<Pel>(c);
+                        for (int i = lane; i < n * n; i += 64)
+                            body[(oy + i / n) * Qc + ox + (i % n)] =
+                                static_cast<int16_t>(P[(tu.y + i / n) * u.st(c) + tu.x + (i % n)]);
+                        wave_sync();
+                    } else {
+                        hevc_predict_tb(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top,
+                                        w.cs[ci].left, w.k, lane);
+                    }
+                    PROF_ADD(5, 1);
+                    PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
+                    t++;
+                }
+                // store the quadrant and update the carries
+                const int wq = min(Qc, Wc - X0), hq = min(Qc, Hc - Y0);
+                for (int ci = 0; ci < ncomp; ci++) {
+                    const int c = grp ? ci + 1 : 0;
+                    QComp& C = w.cs[ci];
+                    const int16_t* body = w.body + ci * 256;
+                    Pel* P = u.plane<Pel>(c);
+                    const int st = u.st(c);
+                    const int qn = wq >> 2;  // 4 samples per lane step (component widths are multiples of 4)
+                    for (int i = lane; i < hq * qn; i += 64) {
+                        const int y = i / qn, x = (i - y * qn) * 4;
+                        const uint2 v = *reinterpret_cast<const uint2*>(body + y * Qc + x);
+                        Pel* d = P + (Y0 + y) * st + X0 + x;
+                        if (sizeof(Pel) == 1) {
+                            *reinterpret_cast<uint32_t*>(d) =
+                                (v.x & 0xFF) | ((v.x >> 8) & 0xFF00) | ((v.y & 0xFF) << 16) | ((v.y >> 16) << 24);
+                        } else {
+                            *reinterpret_cast<uint2*>(d) = v;
+                        }
+                    }
+                    if (qy == nqs - 1 && below)  // bottom line for the CTB row below
+                        for (int i = lane; i < wq; i += 64) line[ci * (Wc + 64) + X0 + i] = body[(Qc - 1) * Qc + i];
+                    if (qy == 0 && nqs == 2)
+                        for (int i = lane; i < Qc; i += 64) C.qbot[qx * Qc + i] = body[(Qc - 1) * Qc + i];
+                    if (qx == 0 && nqs == 2)
+                        for (int i = lane; i < Qc; i += 64) C.qright[i] = body[i * Qc + Qc - 1];
+                    if (qx == nqs - 1) {
+                        for (int i = lane; i < Qc; i += 64) C.prevR[pin][qy * Qc + i] = body[i * Qc + Qc - 1];
+                        if (qy == 0 && lane == 0) C.corner = C.top[Qc];
+                    }
+                }
+                wave_sync();
+                PROF_LAP(3);
             }
-            wave_sync();
+            PROF_ADD(6, 1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0)
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            PROF_LAP(3);
         }
     }
     PROF_FLUSH();
@@ -1128,24 +1213,28 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, HevcK1L
 
 // Separate kernels per codec so each gets its own register budget; a mixed
 // batch launches both and each skips the other codec's pictures.
+// grid (pictures, 2): blockIdx.y = 0 luma chain, 1 chroma chains.
 template <typename Pel>
 __global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
                                                                   uint8_t* arena) {
-    __shared__ HevcK1Lds lds;
+    extern __shared__ __align__(16) uint8_t k1lds[];
+    QWave* W = reinterpret_cast<QWave*>(k1lds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(k1lds + sizeof(QWave) * kK1Waves);
+    int16_t* line = reinterpret_cast<int16_t*>(k1lds + kK1FixedLds);
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
-    if (threadIdx.x < 2 * kK1Waves) lds.prog[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
     __syncthreads();
-    hevc_rows<Pel>(f, tus + f.tu, arena, lds);
+    hevc_rows<Pel>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line);
 }
 
-__global__ void __launch_bounds__(64 * kK1Waves, 6) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
+__global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
                                                                   uint8_t* arena) {
-    __shared__ H4WaveLds wl[kK1Waves];
-    __shared__ uint32_t prog[2 * kK1Waves];
+    __shared__ H4WaveLds wl[kAvcWaves];
+    __shared__ uint32_t prog[2 * kAvcWaves];
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_H264) return;
-    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
     if (f.bit_depth == 8) h264_rows<uint8_t>(f, tus + f.tu, arena, s, prog);
@@ -1845,17 +1934,18 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (b->has_hevc) {
-        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint8_t>, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus,
-                           b->arena);
+        const size_t lds = kK1FixedLds + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
+        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint8_t>, dim3(b->nframes, 2), dim3(64 * kK1Waves), lds, s, b->frames,
+                           b->tus, b->arena);
         int r = check(hipGetLastError(), "h2j_k1_recon_hevc<u8>");
         if (r) return r;
-        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint16_t>, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus,
-                           b->arena);
+        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint16_t>, dim3(b->nframes, 2), dim3(64 * kK1Waves), lds, s, b->frames,
+                           b->tus, b->arena);
         r = check(hipGetLastError(), "h2j_k1_recon_hevc<u16>");
         if (r) return r;
     }
     if (b->has_h264) {
-        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kK1Waves), 0, s, b->frames, b->tus, b->arena);
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kAvcWaves), 0, s, b->frames, b->tus, b->arena);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;

@@ -1,10 +1,15 @@
 // Host-only timing of the entropy decoders (no GPU): parses every stream of
-// a directory N times on one thread and prints ms/frame and TUs/frame.
-//   g++ -O2 -std=c++11 -I../../include -I../../h264-h265-to-jpeg_amd/csrc/host parse_bench.cpp \
+// the argument list `reps` times on T threads (each with its own FrameJob,
+// streams dealt round-robin) and prints ms/frame (wall / frames, and per
+// thread) and TUs/frame.
+//   g++ -O2 -std=c++11 -pthread -I../../include -I../../h264-h265-to-jpeg_amd/csrc/host parse_bench.cpp \
 //       ../../h264-h265-to-jpeg_amd/csrc/host/{bitstream,cabac_tables,hevc_parser,h264_parser}.cpp
+#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bitstream.h"
@@ -12,15 +17,19 @@
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: parse_bench file... [-r reps]\n");
+        std::fprintf(stderr, "usage: parse_bench file... [-r reps] [-t threads]\n");
         return 2;
     }
-    int reps = 3;
+    int reps = 3, threads = 1;
     std::vector<std::vector<uint8_t>> streams;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "-r" && i + 1 < argc) {
             reps = std::atoi(argv[++i]);
+            continue;
+        }
+        if (a == "-t" && i + 1 < argc) {
+            threads = std::atoi(argv[++i]);
             continue;
         }
         FILE* f = std::fopen(argv[i], "rb");
@@ -32,25 +41,38 @@ int main(int argc, char** argv) {
         std::fclose(f);
         streams.push_back(d);
     }
-    h2j::FrameJob job;
-    size_t tus = 0, coefs = 0, bytes = 0;
-    auto t0 = std::chrono::steady_clock::now();
-    for (int r = 0; r < reps; r++)
-        for (auto& s : streams) {
+    const int total = reps * static_cast<int>(streams.size());
+    std::atomic<int> next(0), failed(0);
+    std::atomic<size_t> tus(0), coefs(0), bytes(0);
+    auto worker = [&]() {
+        h2j::FrameJob job;
+        size_t t = 0, c = 0, b = 0;
+        for (int i = next++; i < total; i = next++) {
+            const auto& s = streams[i % streams.size()];
             const int codec = h2j::detect_codec(s.data(), s.size());
             const int rc = codec == 265 ? h2j::hevc_parse_picture(s.data(), s.size(), job)
                                         : h2j::h264_parse_picture(s.data(), s.size(), job);
             if (rc) {
                 std::fprintf(stderr, "parse error %d: %s\n", rc, job.message.c_str());
-                return 1;
+                failed++;
+                return;
             }
-            tus += job.tus.size();
-            coefs += job.coefs.size();
-            bytes += s.size();
+            t += job.tus.size();
+            c += job.coefs.size();
+            b += s.size();
         }
+        tus += t;
+        coefs += c;
+        bytes += b;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int k = 0; k < threads; k++) pool.emplace_back(worker);
+    for (auto& th : pool) th.join();
+    if (failed) return 1;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    const double nf = static_cast<double>(reps) * streams.size();
-    std::printf("%.3f ms/frame  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s\n", ms / nf, tus / nf, coefs / nf,
-                bytes / (ms / 1e3) / 1e6);
+    const double nf = total;
+    std::printf("%d thr: %.3f ms/frame wall, %.3f ms/frame/thread  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s\n",
+                threads, ms / nf, ms * threads / nf, tus / nf, coefs / nf, bytes / (ms / 1e3) / 1e6);
     return 0;
 }
