@@ -11,7 +11,8 @@
 //                        (H.265 8.4.4.2, 8.6.2-8.6.4; H.264 8.3, 8.5)
 //   K2 h2j_k2_deblock  — one thread per 4-line edge segment, vertical pass
 //                        then horizontal pass (H.265 8.7.2, H.264 8.7)
-//   K3 h2j_k3_sao      — one thread per 4 samples, band/edge offsets
+//   K3 h2j_k3_sao      — one workgroup per (CTB, component), LDS tile + border,
+//                        band/edge offsets
 //                        (H.265 8.7.3)
 //   K4 h2j_k4_*        — JPEG forward path of FFmpeg's mjpeg encoder as
 //                        restated in SURVEY.md Appendix A: MB variance ->
@@ -206,13 +207,13 @@ DEVI void wave_sync() {
 __device__ unsigned long long g_prof[16];
 #define PROF_T() __builtin_amdgcn_s_memtime()
 #define PROF_ADD(i, v) (pacc[i] += (v))
-#define PROF_DECL unsigned long long pacc[16] = {0}; unsigned long long pt0 = PROF_T(), pt1
+#define PROF_DECL unsigned long long pacc[16] = {0}; unsigned long long pt0 = PROF_T(), pt1, prt0 = __builtin_amdgcn_s_memrealtime(), pmt0 = pt0
 #define PROF_LAP(i) (pt1 = PROF_T(), PROF_ADD(i, pt1 - pt0), pt0 = pt1)
 #define PROF_LAPK(k) do { pt1 = PROF_T(); const unsigned long long d_ = pt1 - pt0; pt0 = pt1; \
     switch (k) { case 0: pacc[8] += d_; break; case 1: pacc[9] += d_; break; case 2: pacc[10] += d_; break; \
     case 3: pacc[11] += d_; break; case 4: pacc[12] += d_; break; case 5: pacc[13] += d_; break; \
     case 6: pacc[14] += d_; break; default: pacc[15] += d_; break; } } while (0)
-#define PROF_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd(&g_prof[q_], pacc[q_]); } while (0)
+#define PROF_FLUSH() do { pacc[4] = __builtin_amdgcn_s_memrealtime() - prt0; pacc[7] = PROF_T() - pmt0; if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd(&g_prof[q_], pacc[q_]); } while (0)
 #else
 #define PROF_DECL
 #define PROF_ADD(i, v)
@@ -1536,101 +1537,132 @@ __global__ void __launch_bounds__(512) h2j_k2_deblock264(const h2j_frame* frames
 }
 
 // ---------------------------------------------------------------- K3: SAO
-DEVI int zscan_luma(const h2j_frame& f, const h2j_ctb* ctbs, int x, int y) {
-    const int l2 = f.log2ctb;
-    const int ctb = (y >> l2) * f.ctb_w + (x >> l2);
-    const int m = (1 << l2) - 1;
-    const int ax = (x & m) >> 2, ay = (y & m) >> 2;
-    int z = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) z |= (((ax >> i) & 1) << (2 * i)) | (((ay >> i) & 1) << (2 * i + 1));
-    return static_cast<int>(ctbs[ctb].ts << (2 * (l2 - 2))) + z;
-}
+// K3 SAO (H.265 8.7.3): one 256-thread workgroup per (CTB, component).  The
+// CTB's deblocked samples plus a one-sample border are staged in LDS (int16,
+// -1 = outside the picture), the CTB's SAO parameters and the usability of
+// its 8 neighbour CTBs across slice / tile boundaries are resolved once per
+// workgroup, then every thread filters 4 horizontally adjacent samples and
+// writes them with one store.  Pictures without SAO alias pic2 = pic and are
+// skipped (the host lays them out that way).
+constexpr int kSaoTile = 66 * 66;
 
 template <typename Pel>
-DEVI void sao_sample(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, const Pel* src, Pel* dst,
-                     int st, int pw, int ph, int c, int x, int y, const uint8_t* fmap) {
+DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, int ctb, int c,
+                  int16_t* tile, int* nbok) {
+    const int tid = threadIdx.x;
     const int shc = c ? 1 : 0;
-    const int xl = x << shc, yl = y << shc;
-    const int ctb = (yl >> f.log2ctb) * f.ctb_w + (xl >> f.log2ctb);
-    const h2j_ctb& C = ctbs[ctb];
-    const h2j_slice& S = slices[C.slice];
-    int v = src[y * st + x];
-    const int type = C.type[c];
-    const bool on = type != 0 && (c == 0 ? S.sao_luma : S.sao_chroma) && !(fmap[(yl >> 2) * f.mw + (xl >> 2)] & 4);
-    if (on) {
-        const int bd = c ? f.bit_depth_c : f.bit_depth;
-        int off = 0;
-        if (type == 1) {
-            const int k = ((v >> (bd - 5)) - C.band_pos[c]) & 31;
-            if (k < 4) off = C.off[c][k];
-        } else {
-            const int cls = C.eo_class[c];
-            const int hx0 = cls == 0 ? -1 : (cls == 1 ? 0 : (cls == 2 ? -1 : 1));
-            const int vy0 = cls == 0 ? 0 : -1;
-            const int xa = x + hx0, ya = y + vy0, xb = x - hx0, yb = y - vy0;
-            bool ok = xa >= 0 && ya >= 0 && xa < pw && ya < ph && xb >= 0 && yb >= 0 && xb < pw && yb < ph;
-            if (ok) {
-                // slice / tile boundary restrictions (8.7.3.2)
-                const int nx[2] = {xa, xb}, ny[2] = {ya, yb};
-#pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    const int xnl = nx[k] << shc, ynl = ny[k] << shc;
-                    const int cn = (ynl >> f.log2ctb) * f.ctb_w + (xnl >> f.log2ctb);
-                    if (cn != ctb) {
-                        const h2j_ctb& N = ctbs[cn];
-                        const h2j_slice& SN = slices[N.slice];
-                        if (SN.slice_addr_rs != S.slice_addr_rs) {
-                            const int zn = zscan_luma(f, ctbs, xnl, ynl), zc = zscan_luma(f, ctbs, xl, yl);
-                            if (zn < zc && !S.lf_across_slices) ok = false;
-                            if (zc < zn && !SN.lf_across_slices) ok = false;
-                        }
-                        if (!f.lf_across_tiles && N.tile != C.tile) ok = false;
-                    }
-                }
-            }
-            if (ok) {
-                const int a = src[ya * st + xa], b = src[yb * st + xb];
-                int e = 2 + ((v > a) - (v < a)) + ((v > b) - (v < b));
-                e = e == 0 ? 1 : (e == 1 ? 2 : (e == 2 ? 0 : e));
-                if (e) off = C.off[c][e - 1];
-            }
-        }
-        v = clip3(0, (1 << bd) - 1, v + off);
-    }
-    dst[y * st + x] = static_cast<Pel>(v);
-}
-
-template <typename Pel>
-DEVI void sao_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, uint8_t* arena, int idx) {
-    // 4 horizontal samples per thread; luma then Cb then Cr index ranges
-    const int W = f.width, H = f.height;
-    const int lq = (W >> 2) * H;
-    const int cq = (W >> 3) * (H >> 1);
-    int c, x, y;
-    if (idx < lq) { c = 0; y = idx / (W >> 2); x = (idx % (W >> 2)) * 4; }
-    else if (idx < lq + cq) { c = 1; idx -= lq; y = idx / (W >> 3); x = (idx % (W >> 3)) * 4; }
-    else if (idx < lq + 2 * cq) { c = 2; idx -= lq + cq; y = idx / (W >> 3); x = (idx % (W >> 3)) * 4; }
-    else return;
+    const int S = (1 << f.log2ctb) >> shc;
+    const int cxi = ctb % f.ctb_w, cyi = ctb / f.ctb_w;
+    const int x0 = cxi * S, y0 = cyi * S;
+    const int pw = f.width >> shc, ph = f.height >> shc;
+    const int w = min(S, pw - x0), h = min(S, ph - y0);
     const Pel* src = plane<Pel>(f, arena, f.pic, c);
     Pel* dst = plane<Pel>(f, arena, f.pic2, c);
     const int st = f.pic_stride[c];
-    const int pw = c ? W >> 1 : W, ph = c ? H >> 1 : H;
+    const h2j_ctb& cc = C[ctb];
+    const h2j_slice& sc = SL[cc.slice];
+    const int type = cc.type[c];
+    const bool on = type != 0 && (c == 0 ? sc.sao_luma : sc.sao_chroma);
+    if (!on) {  // plain copy, 4 samples per thread step
+        const int q = w >> 2;
+        for (int i = tid; i < h * q; i += 256) {
+            const int y = i / q, x = (i - y * q) * 4;
+            const Pel* s = src + (y0 + y) * st + x0 + x;
+            Pel* d = dst + (y0 + y) * st + x0 + x;
+            if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
+            else *reinterpret_cast<uint2*>(d) = *reinterpret_cast<const uint2*>(s);
+        }
+        return;
+    }
+    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int maxv = (1 << bd) - 1;
+    const int cls = cc.eo_class[c];
+    if (type == 2) {
+        // stage the tile + border; -1 marks samples outside the picture
+        const int tw = w + 2, th = h + 2;
+        for (int i = tid; i < tw * th; i += 256) {
+            const int ty = i / tw, tx = i - ty * tw;
+            const int x = x0 + tx - 1, y = y0 + ty - 1;
+            tile[ty * 66 + tx] = (x >= 0 && y >= 0 && x < pw && y < ph) ? static_cast<int16_t>(src[y * st + x]) : -1;
+        }
+        if (tid < 9) {  // neighbour CTB (dx, dy) usable across slice / tile boundaries (8.7.3.2)
+            const int dx = tid % 3 - 1, dy = tid / 3 - 1;
+            const int nx = cxi + dx, ny = cyi + dy;
+            int ok = 1;
+            if (nx >= 0 && ny >= 0 && nx < f.ctb_w && ny < f.ctb_h && (dx || dy)) {
+                const h2j_ctb& nc = C[ny * f.ctb_w + nx];
+                const h2j_slice& sn = SL[nc.slice];
+                if (sn.slice_addr_rs != sc.slice_addr_rs) {
+                    if (nc.ts < cc.ts && !sc.lf_across_slices) ok = 0;
+                    if (cc.ts < nc.ts && !sn.lf_across_slices) ok = 0;
+                }
+                if (!f.lf_across_tiles && nc.tile != cc.tile) ok = 0;
+            }
+            nbok[tid] = ok;
+        }
+        __syncthreads();
+    }
+    const int hx = cls == 0 ? -1 : (cls == 1 ? 0 : (cls == 2 ? -1 : 1));
+    const int vy = cls == 0 ? 0 : -1;
     const uint8_t* fmap = arena + f.maps;
-    for (int k = 0; k < 4 && x + k < pw; k++) {
-        if (f.sao_enabled) sao_sample<Pel>(f, ctbs, slices, src, dst, st, pw, ph, c, x + k, y, fmap);
-        else dst[y * st + x + k] = src[y * st + x + k];
+    const int q = w >> 2;
+    for (int i = tid; i < h * q; i += 256) {
+        const int y = i / q, x = (i - y * q) * 4;
+        const Pel* s = src + (y0 + y) * st + x0 + x;
+        int v[4];
+        if (type == 2) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = tile[(y + 1) * 66 + x + k + 1];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = s[k];
+        }
+        // samples of pcm (loop filter off) / transquant-bypass blocks stay untouched
+        const bool keep = (fmap[(((y0 + y) << shc) >> 2) * f.mw + (((x0 + x) << shc) >> 2)] & 4) != 0;
+        int o[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            int off = 0;
+            if (type == 1) {
+                const int b = ((v[k] >> (bd - 5)) - cc.band_pos[c]) & 31;
+                if (b < 4) off = cc.off[c][b];
+            } else {
+                const int xa = x + k + hx, ya = y + vy, xb = x + k - hx, yb = y - vy;
+                const int a = tile[(ya + 1) * 66 + xa + 1], bb = tile[(yb + 1) * 66 + xb + 1];
+                const int na = ((ya < 0 ? 0 : (ya >= S ? 2 : 1)) * 3) + (xa < 0 ? 0 : (xa >= S ? 2 : 1));
+                const int nb = ((yb < 0 ? 0 : (yb >= S ? 2 : 1)) * 3) + (xb < 0 ? 0 : (xb >= S ? 2 : 1));
+                if (a >= 0 && bb >= 0 && nbok[na] && nbok[nb]) {
+                    int e = 2 + ((v[k] > a) - (v[k] < a)) + ((v[k] > bb) - (v[k] < bb));
+                    e = e == 0 ? 1 : (e == 1 ? 2 : (e == 2 ? 0 : e));
+                    if (e) off = cc.off[c][e - 1];
+                }
+            }
+            o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
+        }
+        Pel* d = dst + (y0 + y) * st + x0 + x;
+        if (sizeof(Pel) == 1) {
+            *reinterpret_cast<uint32_t*>(d) = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 8) |
+                                              (static_cast<uint32_t>(o[2]) << 16) | (static_cast<uint32_t>(o[3]) << 24);
+        } else {
+            *reinterpret_cast<uint2*>(d) = make_uint2(static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 16),
+                                                      static_cast<uint32_t>(o[2]) | (static_cast<uint32_t>(o[3]) << 16));
+        }
     }
 }
 
+// grid (ctbs * 3, pictures): blockIdx.x = ctb * 3 + component
 __global__ void __launch_bounds__(256) h2j_k3_sao(const h2j_frame* frames, const h2j_ctb* ctbs,
                                                  const h2j_slice* slices, uint8_t* arena) {
+    __shared__ int16_t tile[kSaoTile];
+    __shared__ int nbok[9];
     const h2j_frame& f = frames[blockIdx.y];
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f.codec != H2J_CODEC_HEVC || f.pic2 == f.pic) return;
+    const int ctb = blockIdx.x / 3, c = blockIdx.x - ctb * 3;
+    if (ctb >= f.ctb_w * f.ctb_h) return;
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) sao_thread<uint8_t>(f, C, S, arena, idx);
-    else sao_thread<uint16_t>(f, C, S, arena, idx);
+    if (f.bit_depth == 8) sao_ctb<uint8_t>(f, C, S, arena, ctb, c, tile, nbok);
+    else sao_ctb<uint16_t>(f, C, S, arena, ctb, c, tile, nbok);
 }
 
 // ---------------------------------------------------------------- K4: JPEG
@@ -1972,10 +2004,10 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
 }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
-    if (!b || b->nframes <= 0) return 0;
+    if (!b || b->nframes <= 0 || !b->has_hevc) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int items = (b->max_w >> 2) * b->max_h + 2 * (b->max_w >> 3) * (b->max_h >> 1);
-    dim3 grid((items + 255) / 256, b->nframes);
+    // CTB grid of the largest picture at the smallest CTB size present is bounded by max_ctbs
+    dim3 grid(static_cast<unsigned>(b->max_ctbs) * 3, b->nframes);
     hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena);
     return check(hipGetLastError(), "h2j_k3_sao");
 }

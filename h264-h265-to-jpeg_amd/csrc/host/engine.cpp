@@ -232,7 +232,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     if (nf == 0) return 0;
     s.frames.resize(nf);
     size_t ntu = 0, ncoef = 0, nctb = 0, nslice = 0, nsl = 0, nblk = 0;
-    int max_w = 0, max_h = 0, max_mcu = 0, max_ntu = 0;
+    int max_w = 0, max_h = 0, max_mcu = 0, max_ntu = 0, max_ctbs = 0;
     for (int k = 0; k < nf; k++) {
         const FrameJob& j = jobs[s.live[k]];
         max_ntu = std::max(max_ntu, static_cast<int>(j.tus.size()));
@@ -251,6 +251,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         nsl += j.sl.size();
         s.frames[k] = f;
         max_w = std::max(max_w, f.width);
+        max_ctbs = std::max(max_ctbs, f.ctb_w * f.ctb_h);
         max_h = std::max(max_h, f.height);
         const int mcu = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4);
         max_mcu = std::max(max_mcu, mcu);
@@ -282,6 +283,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
             f.pic_off[0] = 0;
             f.pic_off[1] = static_cast<int32_t>(ysz);
             f.pic_off[2] = static_cast<int32_t>(ysz + csz);
+            if (pass == 1 && (f.codec != H2J_CODEC_HEVC || !f.sao_enabled)) {
+                f.pic2 = f.pic;  // no SAO: the deblocked picture is the decoded picture (K3 skips it)
+                continue;
+            }
             if (pass == 0) f.pic = off; else f.pic2 = off;
             off = align_up(off + (ysz + 2 * csz) * pel, 256);
         }
@@ -348,6 +353,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.max_h = max_h;
     b.max_mcu = max_mcu;
     b.max_ntu = max_ntu;
+    b.max_ctbs = max_ctbs;
     b.has_hevc = 0;
     b.has_h264 = 0;
     for (int k = 0; k < nf; k++) {

@@ -55,6 +55,7 @@ typedef struct {
     int32_t max_mcu;            /* max JPEG MCUs over the batch */
     int32_t max_ntu;            /* max transform-block records over the batch */
     int32_t has_hevc, has_h264; /* codecs present in the batch */
+    int32_t max_ctbs;           /* max CTBs (H.264: macroblocks) of one picture over the batch */
     const h2j_frame *frames;
     const h2j_tu *tus;
     const h2j_coef *coefs;

@@ -33,3 +33,5 @@ for path in files:
     for k in range(8):
         print(f"  {'YC'[k // 4]} {4 << (k % 4):2d}x{4 << (k % 4):<2d} {v[8 + k] / max(1, nctb):10.0f} cyc/CTB  {100 * v[8 + k] / tot:5.1f}%")
     print(f"  TU loop {sum(v[8:16]) / max(1, ntu):.0f} cyc/TU")
+    if v[4]:
+        print(f"  s_memtime rate vs 100 MHz s_memrealtime: {100.0 * v[7] / v[4]:.0f} MHz (shader clock)")
