@@ -1249,12 +1249,8 @@ __constant__ uint8_t kBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,
 __constant__ uint8_t kTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,  1,  1,  1,  1, 1,
                                 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
 
-DEVI int chroma_qp_tab(int qpi) {
-    if (qpi < 30) return qpi;
-    if (qpi > 43) return qpi - 6;
-    const int t[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
-    return t[qpi - 30];
-}
+__constant__ int kChromaQp265[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+DEVI int chroma_qp_tab(int qpi) { return qpi < 30 ? qpi : (qpi > 43 ? qpi - 6 : kChromaQp265[qpi - 30]); }
 
 template <typename Pel>
 DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fmap, const int8_t* qmap,
@@ -1392,13 +1388,13 @@ __global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* frames, c
 // HEVC.  One workgroup per picture walks the anti-diagonals d = mx + 2*my
 // (all dependencies of an MB lie on earlier diagonals); 16 lanes per MB,
 // one lane per line across each edge phase.
-__constant__ uint8_t kAlpha264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
+__constant__ int kAlpha264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
                                       5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22, 25,  28,  32,  36,  40,  45,
                                       50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
-__constant__ uint8_t kBeta264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
+__constant__ int kBeta264[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
                                      2,  3,  3,  3,  3,  4,  4,  4,  6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
                                      11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
-__constant__ uint8_t kTc0_264[52][3] = {
+__constant__ int kTc0_264[52][3] = {
     {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
     {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
     {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
@@ -1406,11 +1402,8 @@ __constant__ uint8_t kTc0_264[52][3] = {
     {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
     {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
 
-DEVI int chroma_qp_264(int qpi) {
-    if (qpi < 30) return qpi;
-    const int t[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
-    return t[qpi - 30];
-}
+__constant__ int kChromaQp264[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+DEVI int chroma_qp_264(int qpi) { return qpi < 30 ? qpi : kChromaQp264[qpi - 30]; }
 
 template <typename Pel>
 DEVI void h264_filt_line(Pel* q, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
@@ -1458,82 +1451,266 @@ DEVI void h264_filt_line(Pel* q, int step, int bs, int alpha, int beta, int tc0,
 }
 
 // one phase (vertical or horizontal edges) of one MB, one lane = one line
+// H.264 K2 (8.7): one workgroup per picture; wave w deblocks macroblock rows
+// w, w + kAvcDbWaves, ... in raster order.  MB (x, y) starts once row y-1
+// has finished MBs 0..x+1: its top edge reads and modifies row y-1's bottom
+// rows, which MB (x+1, y-1)'s left edge modifies too.  Each wave filters its
+// MB inside an LDS window (the MB, 4 luma / 2 chroma rows above it, 4 / 2
+// columns left of it); the rows above come from a per-picture LDS line
+// buffer that every row leaves behind, the columns on the left are carried
+// from the previous MB, and the MB's own samples (K1 output, not touched by
+// anyone else before) are prefetched into registers one MB ahead.  After the
+// 8 luma + 4 chroma edge passes the window is written back once.
+constexpr int kAvcDbWaves = 16;
+struct DbWin {
+    uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
+    uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
+};
+
 template <typename Pel>
-DEVI void h264_mb_phase(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, int mx,
-                        int my, bool vert, int l) {
-    const h2j_ctb& m = mbs[my * f.ctb_w + mx];
-    if (!(m.mbflags & 4)) return;
+struct DbPrefetch {  // one MB: luma 4 samples + chroma 2 samples per lane
+    Pel y[4];
+    Pel c[2];
+};
+
+template <typename Pel>
+DEVI void db264_fetch(const Pel* PY, const Pel* const* PC, int sty, int stc, int mx, int my, DbPrefetch<Pel>& r,
+                      int lane) {
+    const Pel* s = PY + (my * 16 + (lane >> 2)) * sty + mx * 16 + (lane & 3) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.y[k] = s[k];
+    const int c = lane >> 5, k = lane & 31;
+    const Pel* t = PC[c] + (my * 8 + (k >> 2)) * stc + mx * 8 + (k & 3) * 2;
+    r.c[0] = t[0];
+    r.c[1] = t[1];
+}
+
+// Deblocking parameters of one MB and of its top neighbour (loaded one MB ahead)
+struct DbInfo {
+    int mf, qp, saddr, dd, tco, beo, cq0, cq1;  // MB flags, QPY, slice first MB, disable idc, offsets
+    int tmf, tqp, tsaddr;                        // top neighbour (tmf = 0: none)
+};
+DEVI DbInfo db264_info(const h2j_ctb* mbs, const h2j_slice* slices, int mbw, int mx, int my) {
+    DbInfo d;
+    const h2j_ctb& m = mbs[my * mbw + mx];
     const h2j_slice& sl = slices[m.slice];
-    if (sl.deblock_disabled == 1) return;
-    const h2j_ctb* n = nullptr;
-    if (vert && mx > 0) n = &mbs[my * f.ctb_w + mx - 1];
-    if (!vert && my > 0) n = &mbs[(my - 1) * f.ctb_w + mx];
-    bool mb_edge = n != nullptr && (n->mbflags & 4);
-    if (mb_edge && sl.deblock_disabled == 2 && slices[n->slice].slice_addr_rs != sl.slice_addr_rs) mb_edge = false;
-    const int bd = f.bit_depth, bdc = f.bit_depth_c;
-    const int qm = (m.mbflags & 1) ? 0 : m.qp;
-    for (int e = 0; e < 4; e++) {
-        if (e == 0 && !mb_edge) continue;
-        if ((e & 1) && (m.mbflags & 2)) continue;
-        const int bs = e == 0 ? 4 : 3;
-        const int qn = e == 0 ? ((n->mbflags & 1) ? 0 : n->qp) : qm;
-        if (l < 16) {
-            const int qpav = (qn + qm + 1) >> 1;
-            const int ia = clip3(0, 51, qpav + sl.tc_offset), ib = clip3(0, 51, qpav + sl.beta_offset);
-            const int alpha = kAlpha264[ia] << (bd - 8), beta = kBeta264[ib] << (bd - 8);
-            const int tc0 = bs < 4 ? kTc0_264[ia][bs - 1] << (bd - 8) : 0;
-            Pel* Y = plane<Pel>(f, arena, f.pic, 0);
-            const int st = f.pic_stride[0];
-            Pel* q = vert ? &Y[(my * 16 + l) * st + mx * 16 + e * 4] : &Y[(my * 16 + e * 4) * st + mx * 16 + l];
-            h264_filt_line<Pel>(q, vert ? 1 : st, bs, alpha, beta, tc0, false, (1 << bd) - 1);
-        }
-        if ((e == 0 || e == 2)) {
-            const int c = l < 8 ? 1 : 2, k = l & 7;
-            const int off = sl.cqp_offset[c - 1];
-            const int qpp = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qn + off));
-            const int qpq = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qm + off));
-            const int qa = (qpp + qpq + 1) >> 1;
-            const int ia = clip3(0, 51, qa + sl.tc_offset), ib = clip3(0, 51, qa + sl.beta_offset);
-            const int alpha = kAlpha264[ia] << (bdc - 8), beta = kBeta264[ib] << (bdc - 8);
-            const int tc0 = bs < 4 ? kTc0_264[ia][bs - 1] << (bdc - 8) : 0;
-            Pel* C = plane<Pel>(f, arena, f.pic, c);
-            const int st = f.pic_stride[c];
-            Pel* q = vert ? &C[(my * 8 + k) * st + mx * 8 + e * 2] : &C[(my * 8 + e * 2) * st + mx * 8 + k];
-            h264_filt_line<Pel>(q, vert ? 1 : st, bs, alpha, beta, tc0, true, (1 << bdc) - 1);
-        }
+    d.mf = m.mbflags;
+    d.qp = m.qp;
+    d.saddr = sl.slice_addr_rs;
+    d.dd = sl.deblock_disabled;
+    d.tco = sl.tc_offset;
+    d.beo = sl.beta_offset;
+    d.cq0 = sl.cqp_offset[0];
+    d.cq1 = sl.cqp_offset[1];
+    d.tmf = 0;
+    d.tqp = 0;
+    d.tsaddr = -1;
+    if (my > 0) {
+        const h2j_ctb& t = mbs[(my - 1) * mbw + mx];
+        d.tmf = t.mbflags;
+        d.tqp = t.qp;
+        d.tsaddr = slices[t.slice].slice_addr_rs;
     }
+    return d;
 }
 
 template <typename Pel>
-__device__ void h264_deblock_frame(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena) {
-    const int mbw = f.ctb_w, mbh = f.ctb_h;
-    const int ndiag = mbw + 2 * (mbh - 1);
-    const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
-    const int groups = blockDim.x >> 4;
-    for (int d = 0; d < ndiag; d++) {
-        const int ylo = d - mbw + 1 > 0 ? (d - mbw + 2) / 2 : 0;
-        const int yhi = min(mbh - 1, d / 2);
-        const int count = yhi - ylo + 1;
-        for (int base = 0; base < count; base += groups) {
-            const int k = base + g;
-            const int my = ylo + k, mx = d - 2 * my;
-            const bool act = k < count && mx >= 0 && mx < mbw;
-            if (act) h264_mb_phase<Pel>(f, mbs, slices, arena, mx, my, true, l);
-            __syncthreads();
-            if (act) h264_mb_phase<Pel>(f, mbs, slices, arena, mx, my, false, l);
-            __syncthreads();
+DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
+                       uint32_t* prog, uint16_t* line) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    DbWin& w = W[wv];
+    const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
+    const int bd = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
+    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
+    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
+    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
+    uint16_t* LY = line;                  // [4][width]: rows 12..15 of the MB row above
+    uint16_t* LC = line + 4 * width;      // [2 comps][2 rows][width / 2]: chroma rows 6..7
+    const int cw = width >> 1;
+    constexpr int kSlots = 2 * kAvcDbWaves;
+    if (wv >= mbh) return;
+    PROF_DECL;
+    DbPrefetch<Pel> pf;
+    db264_fetch<Pel>(PY, PC, sty, stc, 0, wv, pf, lane);
+    DbInfo ninfo = db264_info(mbs, slices, mbw, 0, wv);
+    int lmf = 0, lqp = 0, lsaddr = -1;  // left neighbour (previous MB of the row)
+    for (int row = wv; row < mbh; row += kAvcDbWaves) {
+        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + row % kSlots;
+        uint32_t seen = 0;
+        for (int mx = 0; mx < mbw; mx++) {
+            if (row > 0) {
+                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
+                if (seen < need) {
+                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+            }
+            PROF_LAP(0);
+            // window: MB body (prefetched), rows above (line buffer); the left columns are carried
+            {
+                const int r = lane >> 2, c4 = (lane & 3) * 4;
+#pragma unroll
+                for (int k = 0; k < 4; k++) w.y[r + 4][c4 + k + 4] = pf.y[k];
+                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
+                w.c[c][rr + 2][c2 + 2] = pf.c[0];
+                w.c[c][rr + 2][c2 + 3] = pf.c[1];
+                if (row > 0) {
+                    const int tr = lane >> 4, tc = lane & 15;  // 4 rows x 16 luma columns
+                    w.y[tr][tc + 4] = LY[tr * width + mx * 16 + tc];
+                    if (lane < 32) {  // 2 comps x 2 rows x 8 columns
+                        const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
+                        w.c[cc][cr][ck + 2] = LC[(cc * 2 + cr) * cw + mx * 8 + ck];
+                    }
+                }
+            }
+            {  // prefetch the next MB of this wave
+                int nx = mx + 1, ny = row;
+                if (nx == mbw) { nx = 0; ny += kAvcDbWaves; }
+                if (ny < mbh) db264_fetch<Pel>(PY, PC, sty, stc, nx, ny, pf, lane);
+            }
+            wave_sync();
+            PROF_LAP(1);
+            const DbInfo cur = ninfo;
+            {  // parameters of the wave's next MB
+                int nx = mx + 1, ny = row;
+                if (nx == mbw) { nx = 0; ny += kAvcDbWaves; }
+                if (ny < mbh) ninfo = db264_info(mbs, slices, mbw, nx, ny);
+            }
+            const int mf = ufl(cur.mf);
+            PROF_LAP(2);
+            const bool active = (mf & 4) && ufl(cur.dd) != 1;
+            if (active) {
+                const int qm = (mf & 1) ? 0 : ufl(cur.qp);
+                const int tco = ufl(cur.tco), beo = ufl(cur.beo);
+                const int cqo[2] = {static_cast<int>(ufl(cur.cq0)), static_cast<int>(ufl(cur.cq1))};
+                const int saddr = ufl(cur.saddr), dd = ufl(cur.dd);
+                for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
+                    const bool vert = dir == 0;
+                    // left neighbour = the previous MB of this row (carried), top neighbour from DbInfo
+                    const int nmf = vert ? (mx > 0 ? lmf : 0) : ufl(cur.tmf);
+                    bool mb_edge = (nmf & 4) != 0;
+                    if (mb_edge && dd == 2 && (vert ? lsaddr : static_cast<int>(ufl(cur.tsaddr))) != saddr) mb_edge = false;
+                    const int qn = (nmf & 1) ? 0 : (vert ? lqp : static_cast<int>(ufl(cur.tqp)));
+                    for (int e = 0; e < 4; e++) {
+                        if (e == 0 && !mb_edge) continue;
+                        const int bs = e == 0 ? 4 : 3;
+                        const int qp = e == 0 ? qn : qm;
+                        // thresholds, computed once per edge (scalar)
+                        const int qpav = (qp + qm + 1) >> 1;
+                        const int ia = clip3(0, 51, qpav + tco), ib = clip3(0, 51, qpav + beo);
+                        const int la = kAlpha264[ia] << (bd - 8), lb = kBeta264[ib] << (bd - 8);
+                        const int lt = bs < 4 ? kTc0_264[ia][bs - 1] << (bd - 8) : 0;
+                        int ca[2] = {0, 0}, cb[2] = {0, 0}, ct[2] = {0, 0};
+                        const bool chroma_edge = e == 0 || e == 2;
+                        if (chroma_edge) {
+#pragma unroll
+                            for (int c = 0; c < 2; c++) {
+                                const int qpp = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qp + cqo[c]));
+                                const int qpq = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qm + cqo[c]));
+                                const int qa = (qpp + qpq + 1) >> 1;
+                                const int ja = clip3(0, 51, qa + tco), jb = clip3(0, 51, qa + beo);
+                                ca[c] = kAlpha264[ja] << (bdc - 8);
+                                cb[c] = kBeta264[jb] << (bdc - 8);
+                                ct[c] = bs < 4 ? kTc0_264[ja][bs - 1] << (bdc - 8) : 0;
+                            }
+                        }
+                        if (lane < 16 && !((e & 1) && (mf & 2))) {  // luma line `lane`
+                            uint16_t* q = vert ? &w.y[lane + 4][e * 4 + 4] : &w.y[e * 4 + 4][lane + 4];
+                            h264_filt_line<uint16_t>(q, vert ? 1 : 20, bs, la, lb, lt, false, (1 << bd) - 1);
+                        } else if (lane >= 32 && lane < 48 && chroma_edge) {  // chroma line
+                            const int c = (lane - 32) >> 3, k = lane & 7;
+                            uint16_t* q = vert ? &w.c[c][k + 2][e * 2 + 2] : &w.c[c][e * 2 + 2][k + 2];
+                            h264_filt_line<uint16_t>(q, vert ? 1 : 10, bs, c ? ca[1] : ca[0], c ? cb[1] : cb[0],
+                                                     c ? ct[1] : ct[0], true, (1 << bdc) - 1);
+                        }
+                        wave_sync();
+                        PROF_LAPK(dir * 4 + e);
+                    }
+                }
+            }
+            lmf = mf;
+            lqp = ufl(cur.qp);
+            lsaddr = ufl(cur.saddr);
+            // write back: left columns (MB x-1), rows above (MB row y-1), the MB itself
+            {
+                const int r = lane >> 2, c4 = (lane & 3) * 4;
+                Pel* d = PY + (row * 16 + r) * sty + mx * 16 + c4;
+#pragma unroll
+                for (int k = 0; k < 4; k++) d[k] = static_cast<Pel>(w.y[r + 4][c4 + k + 4]);
+                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
+                Pel* e = PC[c] + (row * 8 + rr) * stc + mx * 8 + c2;
+                e[0] = static_cast<Pel>(w.c[c][rr + 2][c2 + 2]);
+                e[1] = static_cast<Pel>(w.c[c][rr + 2][c2 + 3]);
+                if (active && mx > 0) {
+                    if (lane < 48) {  // luma columns -3..-1, rows 0..15
+                        const int lr = lane / 3, lc = lane - lr * 3 + 1;
+                        PY[(row * 16 + lr) * sty + mx * 16 + lc - 4] = static_cast<Pel>(w.y[lr + 4][lc]);
+                    } else {  // chroma column -1, rows 0..7, both comps
+                        const int cc = (lane - 48) >> 3, cr = lane & 7;
+                        PC[cc][(row * 8 + cr) * stc + mx * 8 - 1] = static_cast<Pel>(w.c[cc][cr + 2][1]);
+                    }
+                }
+                if (active && row > 0) {
+                    if (lane < 48) {  // luma rows -3..-1, columns 0..15
+                        const int tr = lane >> 4, tc = lane & 15;
+                        PY[(row * 16 - 3 + tr) * sty + mx * 16 + tc] = static_cast<Pel>(w.y[tr + 1][tc + 4]);
+                    } else {  // chroma row -1, columns 0..7, both comps
+                        const int cc = (lane - 48) >> 3, ck = lane & 7;
+                        PC[cc][(row * 8 - 1) * stc + mx * 8 + ck] = static_cast<Pel>(w.c[cc][1][ck + 2]);
+                    }
+                }
+            }
+            // line buffer for the row below: the MB's bottom rows (columns final so far) and
+            // the previous MB's last columns, which this MB's left edge has just finished
+            if (row + 1 < mbh) {
+                const bool last = mx == mbw - 1;
+                const int tr = lane >> 4, tc = lane & 15;  // rows 12..15 of this MB
+                if (tc < 12 || last) LY[tr * width + mx * 16 + tc] = w.y[tr + 16][tc + 4];
+                if (mx > 0 && tc < 4) LY[tr * width + mx * 16 - 4 + tc] = w.y[tr + 16][tc];
+                if (lane < 32) {  // chroma rows 6..7
+                    const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
+                    if (ck < 6 || last) LC[(cc * 2 + cr) * cw + mx * 8 + ck] = w.c[cc][cr + 8][ck + 2];
+                    if (mx > 0 && ck < 2) LC[(cc * 2 + cr) * cw + mx * 8 - 2 + ck] = w.c[cc][cr + 8][ck];
+                }
+            }
+            wave_sync();
+            // carry the last columns into the next MB's left strip
+            if (lane < 64) {
+                const int r = lane >> 2, k = lane & 3;
+                w.y[r + 4][k] = w.y[r + 4][k + 16];
+            }
+            if (lane < 32) {
+                const int cc = lane >> 4, r = (lane >> 1) & 7, k = lane & 1;
+                w.c[cc][r + 2][k] = w.c[cc][r + 2][k + 8];
+            }
+            wave_sync();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            PROF_LAP(3);
+            PROF_ADD(6, 1);
         }
     }
+    PROF_FLUSH();
 }
 
-__global__ void __launch_bounds__(512) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
-                                                        const h2j_slice* slices, uint8_t* arena) {
+__global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                                    const h2j_slice* slices, uint8_t* arena) {
+    extern __shared__ __align__(16) uint8_t dblds[];
+    DbWin* W = reinterpret_cast<DbWin*>(dblds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * kAvcDbWaves);
+    uint16_t* line = reinterpret_cast<uint16_t*>(dblds + sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4);
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_H264) return;
+    if (threadIdx.x < 2 * kAvcDbWaves) prog[threadIdx.x] = 0;
+    __syncthreads();
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) h264_deblock_frame<uint8_t>(f, C, S, arena);
-    else h264_deblock_frame<uint16_t>(f, C, S, arena);
+    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line);
+    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line);
 }
 
 // ---------------------------------------------------------------- K3: SAO
@@ -1991,15 +2168,26 @@ int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {
 int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int maps = ((b->max_w + 3) >> 2) * ((b->max_h + 3) >> 2);
-    dim3 grid((maps + 255) / 256, b->nframes);
-    hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
-    int r = check(hipGetLastError(), "h2j_k2_deblock(v)");
-    if (r) return r;
-    hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
-    r = check(hipGetLastError(), "h2j_k2_deblock(h)");
-    if (r) return r;
-    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->nframes), dim3(512), 0, s, b->frames, b->ctbs, b->slices, b->arena);
+    if (b->has_hevc) {
+        const int maps = ((b->max_w + 3) >> 2) * ((b->max_h + 3) >> 2);
+        dim3 grid((maps + 255) / 256, b->nframes);
+        hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
+        int r = check(hipGetLastError(), "h2j_k2_deblock(v)");
+        if (r) return r;
+        hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
+        r = check(hipGetLastError(), "h2j_k2_deblock(h)");
+        if (r) return r;
+    }
+    if (!b->has_h264) return 0;
+    const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + 12 * static_cast<size_t>(b->max_w);
+    static bool attr = false;
+    if (!attr) {  // line buffers of pictures wider than ~3.6K need more than the 64 KB default
+        hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k2_deblock264),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->nframes), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
+                       b->slices, b->arena);
     return check(hipGetLastError(), "h2j_k2_deblock264");
 }
 

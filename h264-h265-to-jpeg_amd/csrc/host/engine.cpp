@@ -165,7 +165,7 @@ int parse_any(const uint8_t* d, size_t n, FrameJob& job) {
 // One in-flight chunk: its stream, buffers and layout.
 struct Slot {
     void* stream = nullptr;
-    void* ev[9] = {nullptr};
+    void* ev[11] = {nullptr};  // 9: after the stats D2H, 10: before the payload D2H
     DevBuf d_in, d_arena, d_seg, d_scratch;
     HostBuf h_in, h_js, h_seg;
     std::vector<h2j_frame> frames;
@@ -396,6 +396,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
                                 static_cast<size_t>(nf) * s.jstat_stride, st);
         if (r) return fail(std::string("download failed: ") + h2j_gpu_last_error());
     }
+    h2j_gpu_event_record(s.ev[9], st);
     s.pending = true;
     double bytes = 0;
     for (int k = 0; k < nf; k++) {
@@ -414,6 +415,7 @@ int Engine::sync(Slot& s) {
         uint64_t total = 0;
         std::memcpy(&total, s.h_js.p, 8);
         if (!s.h_seg.ensure(total + 16)) return fail("pinned host allocation failed");
+        h2j_gpu_event_record(s.ev[10], s.stream);
         if (total && h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
             return fail(std::string("download failed: ") + h2j_gpu_last_error());
     }
@@ -427,7 +429,9 @@ int Engine::sync(Slot& s) {
     stats[ST_SAO] += h2j_gpu_event_elapsed_ms(s.ev[3], s.ev[4]);
     stats[ST_JPEG] += h2j_gpu_event_elapsed_ms(s.ev[4], s.ev[5]);
     stats[ST_ENTROPY] += h2j_gpu_event_elapsed_ms(s.ev[5], s.ev[6]);
-    stats[ST_D2H] += h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[7]);
+    // copies only (the payload copy is enqueued once the host has read the sizes)
+    stats[ST_D2H] += h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]) +
+                     (s.entropy ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[7]) : 0.0f);
     return 0;
 }
 
