@@ -83,28 +83,31 @@ __constant__ int kAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,
 __constant__ int kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,    0,    0,
                                       0,     0,     -4096, -1638, -910, -630, -482, -390, -315,
                                       -256,  -315,  -390, -482, -630, -910, -1638, -4096, 0};
-__constant__ int8_t kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+__constant__ int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
 
 // ---------------------------------------------------------------- K1: H.264
 // H.264 8.3 (intra prediction), 8.5 (scaling + transforms).  Records: luma
 // log2n 2 (I4x4), 3 (I8x8), 4 (I16x16, DC levels at (4i,4j)); chroma log2n 3
 // (DC levels at (4i,4j)); PCM.  Macroblocks are the "CTB" records (log2ctb 4).
-__constant__ uint8_t kNorm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
-__constant__ uint8_t kNorm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+__constant__ int kNorm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+__constant__ int kNorm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
                                      {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
 
+// m (= qP % 6) is uniform: the table row is read with scalar loads, the
+// position class is selected per lane
 DEVI int h264_norm4(int m, int i, int j) {
-    if (!(i & 1) && !(j & 1)) return kNorm4[m][0];
-    if ((i & 1) && (j & 1)) return kNorm4[m][1];
-    return kNorm4[m][2];
+    const int n0 = kNorm4[m][0], n1 = kNorm4[m][1], n2 = kNorm4[m][2];
+    return (!(i & 1) && !(j & 1)) ? n0 : (((i & 1) && (j & 1)) ? n1 : n2);
 }
 DEVI int h264_norm8(int m, int i, int j) {
-    if (!(i & 3) && !(j & 3)) return kNorm8[m][0];
-    if ((i & 1) && (j & 1)) return kNorm8[m][1];
-    if ((i & 3) == 2 && (j & 3) == 2) return kNorm8[m][2];
-    if ((!(i & 3) && (j & 1)) || ((i & 1) && !(j & 3))) return kNorm8[m][3];
-    if ((!(i & 3) && (j & 3) == 2) || ((i & 3) == 2 && !(j & 3))) return kNorm8[m][4];
-    return kNorm8[m][5];
+    const int n0 = kNorm8[m][0], n1 = kNorm8[m][1], n2 = kNorm8[m][2], n3 = kNorm8[m][3], n4 = kNorm8[m][4],
+              n5 = kNorm8[m][5];
+    if (!(i & 3) && !(j & 3)) return n0;
+    if ((i & 1) && (j & 1)) return n1;
+    if ((i & 3) == 2 && (j & 3) == 2) return n2;
+    if ((!(i & 3) && (j & 1)) || ((i & 1) && !(j & 3))) return n3;
+    if ((!(i & 3) && (j & 3) == 2) || ((i & 3) == 2 && !(j & 3))) return n4;
+    return n5;
 }
 DEVI int h264_scale4(int lvl, int ls, int qp) {
     return qp >= 24 ? (lvl * ls) << (qp / 6 - 4) : (lvl * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
@@ -177,12 +180,13 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // availability mask, the CTB -> TU range, the HEVC deblocking maps, PCM
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
-constexpr int kK0Tus = 8;    // TUs per K0 wave
+constexpr int kK0Tus = 16;   // TUs per K0 wave (records held one per lane)
 constexpr int kK1Waves = 8;    // HEVC K1: waves (CTB rows in flight) per picture
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
 struct K0Lds {
     int8_t mat[32][32];
+    int8_t dst[4][4];
     int blk[32 * 32];
     int tmp[32 * 32];
     int dc[16];
@@ -222,6 +226,28 @@ __device__ unsigned long long g_prof[16];
 #define PROF_FLUSH()
 #endif
 
+// uniform values into scalar registers; records held one per lane, read with readlane
+DEVI uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+DEVI uint64_t ufl64(uint64_t v) {
+    return (static_cast<uint64_t>(ufl(static_cast<uint32_t>(v >> 32))) << 32) | ufl(static_cast<uint32_t>(v));
+}
+
+DEVI h2j_tu tu_from_lanes(const uint4& r, int l) {
+    uint32_t w[4];
+    w[0] = __builtin_amdgcn_readlane(r.x, l);
+    w[1] = __builtin_amdgcn_readlane(r.y, l);
+    w[2] = __builtin_amdgcn_readlane(r.z, l);
+    w[3] = __builtin_amdgcn_readlane(r.w, l);
+    h2j_tu t;
+    memcpy(&t, w, sizeof(t));
+    return t;
+}
+
+DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
+    return static_cast<uint64_t>(__builtin_amdgcn_readlane(m.x, l)) |
+           (static_cast<uint64_t>(__builtin_amdgcn_readlane(m.y, l)) << 32);
+}
+
 DEVI uint64_t* tu_masks(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint64_t*>(arena + f.aux); }
 DEVI uint32_t* ctb_ranges(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint32_t*>(arena + f.ctbrng); }
 DEVI int16_t* res_plane(const h2j_frame& f, uint8_t* arena, int c) {
@@ -234,11 +260,15 @@ DEVI int ctb_of(const h2j_frame& f, const h2j_tu& tu) {
 
 // HEVC dequantisation (8.6.2-8.6.3) + inverse transform / transform skip /
 // bypass (8.6.4) of one TB into R (int16, stride rst).
-DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO, const uint8_t* sl, int16_t* R,
-                        int rst, K0Lds& s) {
+struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
+    int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo;
+    uint32_t sl;
+};
+DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
+                        int16_t* R, int rst, K0Lds& s) {
     const int lane = threadIdx.x;
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
-    const int bd = c ? f.bit_depth_c : f.bit_depth;
+    const int bd = c ? f.bdc : f.bd;
     const uint8_t flags = tu.flags;
     for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
     if (lane == 0) { s.maxx = 0; s.maxy = 0; }
@@ -248,13 +278,13 @@ DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
     const int bdShift = bd + log2n - 5;
     const int ls = kLevelScale[qp % 6] << (qp / 6);
     const uint8_t* slt = nullptr;
-    if (f.scaling_list && !((flags & H2J_TU_TSKIP) && n > 4)) {
+    if (f.slist && !((flags & H2J_TU_TSKIP) && n > 4)) {
         const int soff = log2n == 2 ? 0 + c * 16 : (log2n == 3 ? 48 + c * 64 : (log2n == 4 ? 240 + c * 256 : 1008));
         slt = sl + f.sl + soff;
     }
     int mx = 0, my = 0;
     for (int e = lane; e < tu.ncoef; e += 64) {
-        const uint32_t en = CO[tu.coef + e];
+        const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];  // first 64 entries prefetched
         const int pos = static_cast<int>(en >> 16);
         const int lvl = static_cast<int16_t>(en & 0xFFFF);
         int d;
@@ -287,7 +317,7 @@ DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
                 int acc = 0;
                 if (x <= mxx) {
                     for (int j = 0; j <= myy; j++) {
-                        const int cf = dst ? kDst4[j][y] : s.mat[j << msh][y];
+                        const int cf = dst ? s.dst[j][y] : s.mat[j << msh][y];
                         acc += cf * s.blk[j * n + x];
                     }
                 }
@@ -299,7 +329,7 @@ DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
                 const int x = i & (n - 1), y = i >> log2n;
                 int acc = 0;
                 for (int j = 0; j <= mxx; j++) {
-                    const int cf = dst ? kDst4[j][x] : s.mat[j << msh][x];
+                    const int cf = dst ? s.dst[j][x] : s.mat[j << msh][x];
                     acc += cf * s.tmp[y * n + j];
                 }
                 s.blk[i] = (acc + (1 << (bdS - 1))) >> bdS;
@@ -313,8 +343,8 @@ DEVI void hevc_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
 
 // H.264 scaling (8.5.9, 8.5.10-8.5.12 DC transforms) + 4x4 / 8x8 inverse
 // transforms (8.5.12.2, 8.5.13) of one record into R.
-DEVI void h264_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO, const uint8_t* sl, int16_t* R,
-                        int rst, K0Lds& s) {
+DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
+                        int16_t* R, int rst, K0Lds& s) {
     const int lane = threadIdx.x;
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
     const int qp = tu.qp, qm = qp % 6;
@@ -323,11 +353,11 @@ DEVI void h264_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
     for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
     __syncthreads();
     for (int e = lane; e < tu.ncoef; e += 64) {
-        const uint32_t en = CO[tu.coef + e];
+        const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
         s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
     }
     __syncthreads();
-    const uint8_t* w4 = f.scaling_list ? sl + f.sl + c * 16 : nullptr;
+    const uint8_t* w4 = f.slist ? sl + f.sl + c * 16 : nullptr;
     if (i16 || chroma) {
         // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
         const int nb = n >> 2;  // blocks per side: 4 (luma) / 2 (chroma)
@@ -359,7 +389,7 @@ DEVI void h264_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
         for (int i = lane; i < 16; i += 64)
             s.blk[i] = h264_scale4(s.blk[i], (w4 ? w4[i] : 16) * h264_norm4(qm, i >> 2, i & 3), qp);
     } else {
-        const uint8_t* w8 = f.scaling_list ? sl + f.sl + 48 : nullptr;
+        const uint8_t* w8 = f.slist ? sl + f.sl + 48 : nullptr;
         for (int i = lane; i < 64; i += 64)
             s.blk[i] = h264_scale8(s.blk[i], (w8 ? w8[i] : 16) * h264_norm8(qm, i >> 3, i & 7), qp);
     }
@@ -415,15 +445,57 @@ DEVI void h264_residual(const h2j_frame& f, const h2j_tu& tu, const h2j_coef* CO
     __syncthreads();
 }
 
+// position of a 4x4 block inside its CTB in z-scan order (6.5.2)
+DEVI int zorder4(int ax, int ay) {
+    int z = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) z |= (((ax >> i) & 1) << (2 * i)) | (((ay >> i) & 1) << (2 * i + 1));
+    return z;
+}
+
 __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
                                                  uint8_t* arena) {
     __shared__ K0Lds s;
-    const h2j_frame& f = frames[blockIdx.y];
+    const h2j_frame& fr = frames[blockIdx.y];
+    const uint32_t ntu = ufl(fr.ntu);
     const uint32_t t0 = blockIdx.x * kK0Tus;
-    if (t0 >= f.ntu) return;
+    if (t0 >= ntu) return;
     const int lane = threadIdx.x;
-    const bool hevc = f.codec == H2J_CODEC_HEVC;
+    const bool hevc = ufl(fr.codec) == H2J_CODEC_HEVC;
+    K0F f;
+    f.bd = ufl(fr.bit_depth);
+    f.bdc = ufl(fr.bit_depth_c);
+    f.slist = ufl(fr.scaling_list);
+    f.sl = ufl(fr.sl);
+    f.log2ctb = ufl(fr.log2ctb);
+    f.ctb_w = ufl(fr.ctb_w);
+    f.width = ufl(fr.width);
+    f.height = ufl(fr.height);
+    f.mw = ufl(fr.mw);
+    f.topo = ufl(fr.topo);
+    const h2j_ctb* C = ctbs + ufl(fr.ctb);
+    const h2j_slice* S = slices + ufl(fr.slice);
+    const h2j_tu* T = tus + ufl(fr.tu);
+    const h2j_coef* CO = coefs + ufl(fr.coef);
+    uint64_t* masks = reinterpret_cast<uint64_t*>(arena + ufl64(fr.aux));
+    uint32_t* rng = reinterpret_cast<uint32_t*>(arena + ufl64(fr.ctbrng));
+    uint8_t* fmap = arena + ufl64(fr.maps);
+    int8_t* qmap = reinterpret_cast<int8_t*>(fmap + static_cast<size_t>(f.mw) * ufl(fr.mh));
+    uint8_t* pic = arena + ufl64(fr.pic);
+    int16_t* res = reinterpret_cast<int16_t*>(arena + ufl64(fr.res));
+    const int st0 = ufl(fr.pic_stride[0]), st1 = ufl(fr.pic_stride[1]);
+    const int off1 = ufl(fr.pic_off[1]), off2 = ufl(fr.pic_off[2]);
+    // this workgroup's records (lane k: record t0 + k) and the two neighbours of the range
+    const uint32_t t1 = min(ntu, t0 + kK0Tus);
+    const int nrec = static_cast<int>(t1 - t0);
+    uint4 rec = make_uint4(0, 0, 0, 0);
+    {
+        int ri = static_cast<int>(t0) + lane;
+        if (lane == kK0Tus) ri = static_cast<int>(t0) - 1;
+        if (lane == kK0Tus + 1) ri = static_cast<int>(t1);
+        if (lane <= kK0Tus + 1 && ri >= 0 && ri < static_cast<int>(ntu)) rec = reinterpret_cast<const uint4*>(T)[ri];
+    }
     if (hevc) {
         for (int i = lane; i < 1024; i += 64) {
             const int m = i >> 5, nn = i & 31;
@@ -431,26 +503,35 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
             if (a > 64) a = 128 - a;
             s.mat[m][nn] = static_cast<int8_t>(a > 32 ? -kCos33[64 - a] : kCos33[a]);
         }
+        if (lane < 16) s.dst[lane >> 2][lane & 3] = kDst4[lane >> 2][lane & 3];
     }
     __syncthreads();
-    const h2j_ctb* C = ctbs + f.ctb;
-    const h2j_slice* S = slices + f.slice;
-    const h2j_tu* T = tus + f.tu;
-    const h2j_coef* CO = coefs + f.coef;
-    uint64_t* masks = tu_masks(f, arena);
-    uint32_t* rng = ctb_ranges(f, arena);
-    uint8_t* fmap = arena + f.maps;
-    int8_t* qmap = reinterpret_cast<int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
-    const uint32_t t1 = min(f.ntu, t0 + kK0Tus);
-    for (uint32_t t = t0; t < t1; t++) {
-        const h2j_tu tu = T[t];
+    auto ctb_of_tu = [&](const h2j_tu& tu) {
+        const int sh = tu.c ? 1 : 0;
+        return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
+    };
+    const int prev_cb = t0 > 0 ? ctb_of_tu(tu_from_lanes(rec, kK0Tus)) : -1;
+    const int next_cb = t1 < ntu ? ctb_of_tu(tu_from_lanes(rec, kK0Tus + 1)) : -1;
+    // coefficient entries of the current TU (lane e < 64), prefetched one TU ahead
+    auto fetch_co = [&](const h2j_tu& v) -> uint32_t {
+        const uint32_t e = min(static_cast<uint32_t>(lane), max(static_cast<uint32_t>(v.ncoef), 1u) - 1);
+        return v.ncoef ? CO[v.coef + e] : 0u;
+    };
+    uint32_t nco = fetch_co(tu_from_lanes(rec, 0));
+    for (int k = 0; k < nrec; k++) {
+        const uint32_t t = t0 + k;
+        const h2j_tu tu = tu_from_lanes(rec, k);
+        const uint32_t co0 = nco;
+        if (k + 1 < nrec) nco = fetch_co(tu_from_lanes(rec, k + 1));
         const int c = tu.c, log2n = tu.log2n, n = 1 << log2n;
         const int shc = c ? 1 : 0;
         const int x0 = tu.x, y0 = tu.y, xl = x0 << shc, yl = y0 << shc;
+        const int cb = ctb_of_tu(tu);
         if (lane == 0) {
-            const int cb = ctb_of(f, tu);
-            if (t == 0 || ctb_of(f, T[t - 1]) != cb) rng[2 * cb] = t;
-            if (t + 1 == f.ntu || ctb_of(f, T[t + 1]) != cb) rng[2 * cb + 1] = t + 1;
+            const int pcb = k > 0 ? ctb_of_tu(tu_from_lanes(rec, k - 1)) : prev_cb;
+            const int ncb = k + 1 < nrec ? ctb_of_tu(tu_from_lanes(rec, k + 1)) : next_cb;
+            if (pcb != cb) rng[2 * cb] = t;
+            if (ncb != cb) rng[2 * cb + 1] = t + 1;
         }
         const uint8_t flags = tu.flags;
         if (hevc && c == 0) {  // deblocking maps (luma TBs)
@@ -466,27 +547,29 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                 qmap[idx] = tu.qpy;
             }
         }
+        const int stc = c ? st1 : st0;
+        const int offc = c == 0 ? 0 : (c == 1 ? off1 : off2);
         if (flags & H2J_TU_PCM) {
-            const int st = f.pic_stride[c];
-            if (f.bit_depth == 8) {
-                uint8_t* P = plane<uint8_t>(f, arena, f.pic, c);
+            if (f.bd == 8) {
+                uint8_t* P = pic + offc;
                 for (int e = lane; e < tu.ncoef; e += 64) {
-                    const uint32_t en = CO[tu.coef + e];
+                    const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
                     const int pos = static_cast<int>(en >> 16);
-                    P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<uint8_t>(en & 0xFF);
+                    P[(y0 + (pos >> log2n)) * stc + x0 + (pos & (n - 1))] = static_cast<uint8_t>(en & 0xFF);
                 }
             } else {
-                uint16_t* P = plane<uint16_t>(f, arena, f.pic, c);
+                uint16_t* P = reinterpret_cast<uint16_t*>(pic) + offc;
                 for (int e = lane; e < tu.ncoef; e += 64) {
-                    const uint32_t en = CO[tu.coef + e];
+                    const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
                     const int pos = static_cast<int>(en >> 16);
-                    P[(y0 + (pos >> log2n)) * st + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
+                    P[(y0 + (pos >> log2n)) * stc + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
                 }
             }
             if (lane == 0) masks[t] = 0;
             continue;
         }
-        // reference availability mask
+        // reference availability mask; without several slices / tiles it is pure
+        // geometry: inside the picture and earlier in decoding (z-scan / raster) order
         uint64_t mask;
         if (hevc) {
             const int u = c ? 2 : 4, nu = (2 * n) / u;
@@ -496,24 +579,47 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                 if (lane < nu) { xn = x0 - 1; yn = y0 + 2 * n - 1 - lane * u; }
                 else if (lane == nu) { xn = x0 - 1; yn = y0 - 1; }
                 else { xn = x0 + (lane - nu - 1) * u; yn = y0 - 1; }
-                a = avail(f, C, S, xl, yl, xn << shc, yn << shc);
+                const int xnl = xn << shc, ynl = yn << shc;
+                if (f.topo) {
+                    a = avail(fr, C, S, xl, yl, xnl, ynl);
+                } else if (xnl >= 0 && ynl >= 0 && xnl < f.width && ynl < f.height) {
+                    const int l2 = f.log2ctb, m = (1 << l2) - 1;
+                    const int cn = (ynl >> l2) * f.ctb_w + (xnl >> l2);
+                    a = cn == cb ? zorder4((xnl & m) >> 2, (ynl & m) >> 2) <= zorder4((xl & m) >> 2, (yl & m) >> 2)
+                                 : cn < cb;
+                }
             }
             mask = __ballot(a);
         } else {
             const bool nxn = c == 0 && log2n <= 3;
+            int xn = xl, yn = yl;
+            bool use = lane < 4;
+            if (lane == 0) yn = yl - 1;
+            else if (lane == 1) xn = xl - 1;
+            else if (lane == 2) { xn = xl - 1; yn = yl - 1; }
+            else if (lane == 3) { xn = xl + n; yn = yl - 1; use = nxn; }
             bool a = false;
-            if (lane == 0) a = h264_avail(f, C, S, xl, yl, xl, yl - 1);
-            else if (lane == 1) a = h264_avail(f, C, S, xl, yl, xl - 1, yl);
-            else if (lane == 2) a = h264_avail(f, C, S, xl, yl, xl - 1, yl - 1);
-            else if (lane == 3) a = nxn && h264_avail(f, C, S, xl, yl, xl + n, yl - 1);
+            if (use) {
+                if (f.topo) {
+                    a = h264_avail(fr, C, S, xl, yl, xn, yn);
+                } else if (xn >= 0 && yn >= 0 && xn < f.width && yn < f.height) {
+                    const int cn = (yn >> 4) * f.ctb_w + (xn >> 4), cc = (yl >> 4) * f.ctb_w + (xl >> 4);
+                    if (cn == cc) {
+                        const int ax = (xn & 15) >> 2, ay = (yn & 15) >> 2, bx = (xl & 15) >> 2, by = (yl & 15) >> 2;
+                        a = ((ax & 1) | ((ay & 1) << 1) | ((ax & 2) << 1) | ((ay & 2) << 2)) <
+                            ((bx & 1) | ((by & 1) << 1) | ((bx & 2) << 1) | ((by & 2) << 2));
+                    } else {
+                        a = cn < cc;
+                    }
+                }
+            }
             mask = __ballot(a);
         }
         if (lane == 0) masks[t] = mask;
         if (flags & H2J_TU_CBF) {
-            int16_t* R = res_plane(f, arena, c);
-            const int rst = f.pic_stride[c];
-            if (hevc) hevc_residual(f, tu, CO, sl, R, rst, s);
-            else h264_residual(f, tu, CO, sl, R, rst, s);
+            int16_t* R = res + offc;
+            if (hevc) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
+            else h264_residual(f, tu, CO, co0, sl, R, stc, s);
         }
     }
 }
@@ -783,10 +889,6 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
 // re-load them from global memory after every fence, each time waiting for
 // every outstanding load and store of the wave (vmcnt(0)).  Per-component
 // values are selected, never indexed, so nothing lands in scratch.
-DEVI uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-DEVI uint64_t ufl64(uint64_t v) {
-    return (static_cast<uint64_t>(ufl(static_cast<uint32_t>(v >> 32))) << 32) | ufl(static_cast<uint32_t>(v));
-}
 // (pointers stay `arena + uniform offset`, so the compiler keeps them global
 // and emits global_load, not flat_load — flat ops would also hold lgkmcnt)
 struct FU {
@@ -835,20 +937,6 @@ struct QWave {
 // dynamic LDS of one K1 group: QWave[kK1Waves], prog[2 * kK1Waves], line[2 * max width] (int16)
 constexpr size_t kK1FixedLds = sizeof(QWave) * kK1Waves + 2 * kK1Waves * sizeof(uint32_t);
 
-DEVI h2j_tu tu_from_lanes(const uint4& r, int l) {
-    uint32_t w[4];
-    w[0] = __builtin_amdgcn_readlane(r.x, l);
-    w[1] = __builtin_amdgcn_readlane(r.y, l);
-    w[2] = __builtin_amdgcn_readlane(r.z, l);
-    w[3] = __builtin_amdgcn_readlane(r.w, l);
-    h2j_tu t;
-    memcpy(&t, w, sizeof(t));
-    return t;
-}
-DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
-    return static_cast<uint64_t>(__builtin_amdgcn_readlane(m.x, l)) |
-           (static_cast<uint64_t>(__builtin_amdgcn_readlane(m.y, l)) << 32);
-}
 
 // Wave-wide integer sum with DPP row shifts + row broadcasts (no LDS trip);
 // call with all 64 lanes active.

@@ -1191,6 +1191,7 @@ int H264Parser::run(const uint8_t* data, size_t size) {
     }
     if (!have) { job_.message = "no picture found"; return -9; }
     job_.hdr.nslice = static_cast<uint32_t>(job_.slices.size());
+    job_.hdr.topo = (job_.slices.size() != 1 || job_.slices[0].slice_addr_rs != 0) ? 1u : 0u;
     job_.hdr.ntu = static_cast<uint32_t>(job_.tus.size());
     return 0;
 }

@@ -1303,6 +1303,11 @@ int HevcParser::run(const uint8_t* data, size_t size) {
     }
     if (!have_pic) { job_.message = "no picture found"; return -8; }
     job_.hdr.nslice = static_cast<uint32_t>(job_.slices.size());
+    {
+        bool multi = job_.slices.size() != 1 || job_.slices[0].slice_addr_rs != 0;
+        for (size_t i = 0; i < tile_id_.size() && !multi; i++) multi = tile_id_[i] != 0;
+        job_.hdr.topo = multi ? 1u : 0u;
+    }
     job_.hdr.ntu = static_cast<uint32_t>(job_.tus.size());
     return 0;
 }

@@ -94,7 +94,7 @@ typedef struct {
     uint32_t ctb;                   /* h2j_ctb base (ctb_w * ctb_h records) */
     uint32_t slice, nslice;         /* h2j_slice range */
     uint32_t sl;                    /* uint8 scaling factor tables: [sizeId 0..3][c 0..2][32*32]... see DESIGN.md */
-    uint32_t pad0;
+    uint32_t topo;                  /* 1: several slices / tiles, or not starting at CTB 0 (availability needs the CTB records) */
     /* device arena offsets (bytes), filled by the pipeline */
     uint64_t pic;                   /* reconstruction / deblocking planes */
     uint64_t pic2;                  /* SAO output planes (final decoded picture) */
