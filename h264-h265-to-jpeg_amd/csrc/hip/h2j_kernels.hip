@@ -511,6 +511,7 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
     };
     const int prev_cb = t0 > 0 ? ctb_of_tu(tu_from_lanes(rec, kK0Tus)) : -1;
+    const int prev_c = t0 > 0 ? tu_from_lanes(rec, kK0Tus).c : 0;
     const int next_cb = t1 < ntu ? ctb_of_tu(tu_from_lanes(rec, kK0Tus + 1)) : -1;
     // coefficient entries of the current TU (lane e < 64), prefetched one TU ahead
     auto fetch_co = [&](const h2j_tu& v) -> uint32_t {
@@ -530,8 +531,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         if (lane == 0) {
             const int pcb = k > 0 ? ctb_of_tu(tu_from_lanes(rec, k - 1)) : prev_cb;
             const int ncb = k + 1 < nrec ? ctb_of_tu(tu_from_lanes(rec, k + 1)) : next_cb;
-            if (pcb != cb) rng[2 * cb] = t;
-            if (ncb != cb) rng[2 * cb + 1] = t + 1;
+            if (pcb != cb) rng[4 * cb] = t;
+            if (ncb != cb) rng[4 * cb + 2] = t + 1;
+            // first chroma record of the CTB (HEVC records are luma first, then chroma)
+            if (c > 0 && (pcb != cb || (k > 0 ? tu_from_lanes(rec, k - 1).c : prev_c) == 0)) rng[4 * cb + 1] = t;
         }
         const uint8_t flags = tu.flags;
         if (hevc && c == 0) {  // deblocking maps (luma TBs)
@@ -803,7 +806,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 }
             }
             const int cb = row * f.ctb_w + mx;
-            const uint32_t a = rng[2 * cb], ntu = min(rng[2 * cb + 1] - a, static_cast<uint32_t>(kH4MaxTus));
+            const uint32_t a = rng[4 * cb], ntu = min(rng[4 * cb + 2] - a, static_cast<uint32_t>(kH4MaxTus));
             // ---- batched loads: records, masks, top line, left column (first MB), residual
             if (lane < static_cast<int>(ntu)) {
                 s.tus[lane] = T[a + lane];
@@ -938,6 +941,23 @@ struct QWave {
 constexpr size_t kK1FixedLds = sizeof(QWave) * kK1Waves + 2 * kK1Waves * sizeof(uint32_t);
 
 
+// intraPredAngle / invAngle (H.265 Tables 8-4, 8-5) from the mode with scalar
+// arithmetic on packed constants (no memory round trip per TB):
+// d = m - 26 (vertical) or 10 - m (horizontal), angle = sign(d) * mag[|d|].
+DEVI int hevc_angle(int m) {
+    const int d = m >= 18 ? m - 26 : 10 - m;
+    const int k = d < 0 ? -d : d;
+    const int mag = k == 8 ? 32 : static_cast<int>((0x1A15110D09050200ull >> (8 * k)) & 0xFF);
+    return d < 0 ? -mag : mag;
+}
+DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / |angle|)
+    const int k = angle == -2 ? 1 : angle == -5 ? 2 : angle == -9 ? 3 : angle == -13 ? 4 : angle == -17 ? 5
+                : angle == -21 ? 6 : angle == -26 ? 7 : 8;
+    const int v = k <= 4 ? static_cast<int>((0x0276038E06661000ull >> (16 * (k - 1))) & 0xFFFF)
+                         : static_cast<int>((0x0100013B018601E2ull >> (16 * (k - 5))) & 0xFFFF);
+    return -v;
+}
+
 // Wave-wide integer sum with DPP row shifts + row broadcasts (no LDS trip);
 // call with all 64 lanes active.
 DEVI int wave_sum_dpp(int x) {
@@ -1032,6 +1052,9 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         }
         wave_sync();
     }
+#if defined(H2J_EXP) && H2J_EXP == 2  // timing experiment: reference samples only
+    return;
+#endif
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
     const int16_t* R = filt ? s.ref : s.sub;
     const int edge = c == 0 && n < 32;  // DC / pure horizontal / pure vertical boundary smoothing
@@ -1057,7 +1080,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
     } else {
-        const int angle = kAngle[mode], inv = kInvAngle[mode];
+        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
         const bool vert = mode >= 18;
         // vertical: main = top row (refV(k) = R[2n + k], k < 0 projected from the left column);
         // horizontal: main = left column (refH(k) = R[2n - k], k < 0 projected from the top row)
@@ -1148,7 +1171,15 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     };
     uint4 res[2];
     hevc_qres_fetch(u, grp, 0, wv * Sc, Qc, res, lane);
-    uint32_t na = rng[2 * (wv * u.ctb_w)], nb = rng[2 * (wv * u.ctb_w) + 1];
+    // this group's record range of a CTB: luma [first, first chroma), chroma [first chroma, end)
+    auto grange = [&](int cbi, uint32_t& ra, uint32_t& rb) {
+        const uint4 r = reinterpret_cast<const uint4*>(rng)[cbi];
+        const uint32_t mid = (r.y > r.x && r.y <= r.z) ? r.y : r.z;
+        ra = grp ? mid : r.x;
+        rb = grp ? r.z : mid;
+    };
+    uint32_t na, nb;
+    grange(wv * u.ctb_w, na, nb);
     uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
     uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
     for (int row = wv; row < u.ctb_h; row += kK1Waves) {
@@ -1169,8 +1200,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                 if (ncx == u.ctb_w) { ncx = 0; nrow += kK1Waves; }
                 if (nrow < u.ctb_h) {
                     const int ncb = nrow * u.ctb_w + ncx;
-                    na = rng[2 * ncb];
-                    nb = rng[2 * ncb + 1];
+                    grange(ncb, na, nb);
                     nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
                     nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
                 }
@@ -1236,7 +1266,6 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     const int l = static_cast<int>(t - tb);
                     const h2j_tu tu = tu_from_lanes(rec, l);
                     const int c = tu.c;
-                    if ((c > 0) != (grp > 0)) { t++; continue; }
                     const int ox = tu.x - X0, oy = tu.y - Y0;
                     if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
                     const int ci = c == 2 ? 1 : 0;
@@ -1249,8 +1278,12 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                                 static_cast<int16_t>(P[(tu.y + i / n) * u.st(c) + tu.x + (i % n)]);
                         wave_sync();
                     } else {
+#if defined(H2J_EXP) && H2J_EXP == 1  // timing experiment: no TB work at all
+                        (void)ox;
+#else
                         hevc_predict_tb(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top,
                                         w.cs[ci].left, w.k, lane);
+#endif
                     }
                     PROF_ADD(5, 1);
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));

@@ -264,7 +264,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         f.maps = off;
         off = align_up(off + static_cast<size_t>(f.mw) * f.mh * 2, 256);
         f.ctbrng = off;
-        off = align_up(off + static_cast<size_t>(f.ctb_w) * f.ctb_h * 8, 256);
+        off = align_up(off + static_cast<size_t>(f.ctb_w) * f.ctb_h * 16, 256);  // [first, first chroma, end, -]
     }
     s.jstat_base = off;
     s.jstat_stride = align_up(sizeof(h2j_jstat), 256);

@@ -427,6 +427,8 @@ private:
                         int cbf_cr, int cm, int cux, int cuy, int log2cb);
     void residual(int log2n, int c, int mode, h2j_tu& tu);
     void emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int pred_mode_for_scan);
+    void split_ctb_records(size_t first);
+    std::vector<h2j_tu> chroma_tmp_;
     uint8_t edge_flags(int x0, int y0) const;
     void pcm_sample(int x0, int y0, int log2cb);
     void set_map(std::vector<uint8_t>& m, int x0, int y0, int n, uint8_t v) {
@@ -921,6 +923,17 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     tu.flags |= H2J_TU_CBF;
 }
 
+void HevcParser::split_ctb_records(size_t first) {
+    std::vector<h2j_tu>& v = job_.tus;
+    chroma_tmp_.clear();
+    size_t w = first;
+    for (size_t i = first; i < v.size(); i++) {
+        if (v[i].c == 0) v[w++] = v[i];
+        else chroma_tmp_.push_back(v[i]);
+    }
+    std::copy(chroma_tmp_.begin(), chroma_tmp_.end(), v.begin() + static_cast<long>(w));
+}
+
 void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int) {
     h2j_tu tu;
     tu.x = static_cast<uint16_t>(x);
@@ -1212,8 +1225,12 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         ctb_start_contexts(rs, ts, first);
         first = false;
         parse_sao(rx, ry);
+        const size_t first_tu = job_.tus.size();
         coding_quadtree(rx << log2ctb, ry << log2ctb, log2ctb, 0);
         if (err_) return err_;
+        // the CTB's luma TBs first, then its chroma TBs, each in z-scan order: the GPU
+        // reconstructs the luma and the chroma chains in separate workgroups
+        split_ctb_records(first_tu);
         int endf = cc_.terminate();
         if (p_->wpp) {
             for (size_t i = 0; i + 1 < col_bd_.size(); i++)

@@ -3,7 +3,7 @@ one stream; see the PROF_LAP / PROF_LAPK calls in h2j_kernels.hip for the bucket
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
-os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", "prof")
+os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", os.environ.get("H2J_PROF_VARIANT", "prof"))
 sys.path.insert(0, PKG)
 import h2j
 path, n = sys.argv[1], int(sys.argv[2])

@@ -4,7 +4,7 @@ and print where the K1 waves spend their cycles (s_memtime, shader clock).
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
-os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", "prof")
+os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", os.environ.get("H2J_PROF_VARIANT", "prof"))
 sys.path.insert(0, PKG)
 import h2j
 files = [a for a in sys.argv[1:] if not a.isdigit()]
