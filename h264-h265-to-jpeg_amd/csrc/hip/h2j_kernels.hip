@@ -991,30 +991,34 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     for (int ch = 0; ch < 3; ch++) {
         if (ch < nch) {
             const int k = lane + 64 * ch;
-            const int unit = k < 2 * n ? (k >> ush) : (k == 2 * n ? nu : nu + 1 + ((k - 2 * n - 1) >> ush));
+            const int unit = k < 2 * n ? (k >> ush) : nu + ((k - 2 * n + (1 << ush) - 1) >> ush);
             const bool a = k < L && ((mask >> unit) & 1ull);
             m[ch] = __ballot(a);
         }
     }
     const bool any = (m[0] | m[1] | m[2]) != 0;
+    // substitution (8.4.4.2.2): sample k takes the last available index <= k, or the
+    // first available one; per chunk the "nothing below in this chunk" case is uniform
     const int first = m[0] ? __ffsll(static_cast<long long>(m[0])) - 1
                            : (m[1] ? 64 + __ffsll(static_cast<long long>(m[1])) - 1 : 128);
+    const int last0 = m[0] ? 63 - __clzll(m[0]) : first;
+    const int fb[3] = {first, last0, m[1] ? 127 - __clzll(m[1]) : last0};
+    // neighbour sample -> element index relative to `body` (top / left sit at fixed offsets)
+    const int topo = static_cast<int>(top - body), lefto = static_cast<int>(left - body);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
     int dcpart = 0;
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
         if (ch < nch) {
             const int k = lane + 64 * ch;
-            // last available index <= k, else the first available one (8.4.4.2.2)
-            const unsigned long long le = m[ch] & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-            int j = le ? 64 * ch + 63 - __clzll(le) : -1;
-            if (j < 0 && ch >= 2 && m[1]) j = 64 + 63 - __clzll(m[1]);
-            if (j < 0 && ch >= 1 && m[0]) j = 63 - __clzll(m[0]);
-            if (j < 0) j = first;
-            const int xn = j <= 2 * n ? ox - 1 : ox + (j - 2 * n - 1);
+            const unsigned long long le = m[ch] & upto;
+            const int j = le ? 64 * ch + 63 - static_cast<int>(__clzll(le)) : fb[ch];
+            const int xn = j > 2 * n ? ox + (j - 2 * n - 1) : ox - 1;
             const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
-            const int16_t* src = yn < 0 ? top + (xn + 1) : (xn < 0 ? left + yn : body + yn * S + xn);
-            int v = any ? static_cast<int>(*src) : (1 << (bd - 1));
-            if (k < L) s.sub[k] = v;
+            const int idx = yn < 0 ? topo + xn + 1 : (xn < 0 ? lefto + yn : yn * S + xn);
+            const int raw = body[idx];  // unconditional: idx stays inside the wave's window
+            const int v = any ? raw : (1 << (bd - 1));
+            s.sub[k < L ? k : 131] = static_cast<int16_t>(v);
             // DC: p(-1, 0..n-1) = k in [n, 2n), p(0..n-1, -1) = k in [2n+1, 3n]
             dcpart += (k >= n && k <= 3 * n && k != 2 * n) ? v : 0;
         }
@@ -1220,31 +1224,41 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     }
                 }
                 PROF_LAP(0);
-                // neighbour arrays of the quadrant
-                for (int ci = 0; ci < ncomp; ci++) {
-                    QComp& C = w.cs[ci];
-                    const int16_t* ln = line + ci * (Wc + 64);
-                    for (int i = lane; i <= 2 * Qc; i += 64) {  // top, x = i - 1
-                        const int x = i - 1;
-                        int16_t v = 0;
-                        if (qy == 0) {
-                            if (row > 0 && X0 + x >= 0 && X0 + x < Wc)
-                                v = (x < 0 && qx == 0) ? C.corner : ln[X0 + x];
-                        } else if (x < 0) {
-                            v = qx == 0 ? (cx > 0 ? C.prevR[pprev][Qc - 1] : int16_t(0)) : C.qbot[Qc - 1];
-                        } else if (qx * Qc + x < 2 * Qc) {
-                            v = C.qbot[qx * Qc + x];
+                // neighbour arrays of the quadrant: one pass, lane = x of the line above and y of
+                // the column on the left; sources picked by uniform element offsets from the
+                // start of the group's LDS, one unconditional load each
+                {
+                    int16_t* base = reinterpret_cast<int16_t*>(W);
+                    for (int ci = 0; ci < ncomp; ci++) {
+                        QComp& C = w.cs[ci];
+                        const int o_line = static_cast<int>(line + ci * (Wc + 64) - base);
+                        const int o_qbot = static_cast<int>(C.qbot - base);
+                        const int o_prev = static_cast<int>(C.prevR[pprev] - base);
+                        const int o_qr = static_cast<int>(C.qright - base);
+                        const int x = lane, y = lane;
+                        bool ta;
+                        int to;
+                        if (qy == 0) { ta = row > 0 && X0 + x < Wc; to = o_line + X0 + x; }
+                        else { ta = qx * Qc + x < 2 * Qc; to = o_qbot + qx * Qc + x; }
+                        bool la;
+                        int lo;
+                        if (qx == 0) { la = cx > 0 && qy * Qc + y < Sc; lo = o_prev + qy * Qc + y; }
+                        else { la = y < Qc; lo = o_qr + y; }
+                        const int16_t tv = base[ta ? to : o_qbot];
+                        const int16_t lv = base[la ? lo : o_qbot];
+                        if (lane < 2 * Qc) {
+                            C.top[lane + 1] = ta ? tv : int16_t(0);
+                            C.left[lane] = la ? lv : int16_t(0);
                         }
-                        C.top[i] = v;
-                    }
-                    for (int y = lane; y < 2 * Qc; y += 64) {  // left column
-                        int16_t v = 0;
-                        if (qx == 0) {
-                            if (cx > 0 && qy * Qc + y < Sc) v = C.prevR[pprev][qy * Qc + y];
-                        } else if (y < Qc) {
-                            v = C.qright[y];
+                        if (lane == 0) {  // top-left corner
+                            int16_t cv = 0;
+                            if (qy == 0) {
+                                if (row > 0 && X0 > 0) cv = qx == 0 ? C.corner : line[ci * (Wc + 64) + X0 - 1];
+                            } else {
+                                cv = qx == 0 ? (cx > 0 ? C.prevR[pprev][Qc - 1] : int16_t(0)) : C.qbot[Qc - 1];
+                            }
+                            C.top[0] = cv;
                         }
-                        C.left[y] = v;
                     }
                 }
                 hevc_qres_put(grp, Qc, res, w.body, lane);
