@@ -77,12 +77,6 @@ DEVI bool avail(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices
 __constant__ int8_t kCos33[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
                                   61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
 __constant__ int8_t kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
-__constant__ int kAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
-                                  -5,  -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
-                                  -5,  -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
-__constant__ int kInvAngle[35] = {0,     0,     0,    0,    0,    0,    0,    0,    0,
-                                      0,     0,     -4096, -1638, -910, -630, -482, -390, -315,
-                                      -256,  -315,  -390, -482, -630, -910, -1638, -4096, 0};
 __constant__ int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
 
 // ---------------------------------------------------------------- K1: H.264
@@ -181,7 +175,8 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
 constexpr int kK0Tus = 16;   // TUs per K0 wave (records held one per lane)
-constexpr int kK1Waves = 8;    // HEVC K1: waves (CTB rows in flight) per picture
+constexpr int kK1Waves = 8;       // HEVC K1: waves (CTB rows in flight) per group, launches of > 128 pictures
+constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
 struct K0Lds {
@@ -252,10 +247,6 @@ DEVI uint64_t* tu_masks(const h2j_frame& f, uint8_t* arena) { return reinterpret
 DEVI uint32_t* ctb_ranges(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint32_t*>(arena + f.ctbrng); }
 DEVI int16_t* res_plane(const h2j_frame& f, uint8_t* arena, int c) {
     return reinterpret_cast<int16_t*>(arena + f.res) + f.pic_off[c];
-}
-DEVI int ctb_of(const h2j_frame& f, const h2j_tu& tu) {
-    const int sh = tu.c ? 1 : 0;
-    return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
 }
 
 // HEVC dequantisation (8.6.2-8.6.3) + inverse transform / transform skip /
@@ -938,7 +929,7 @@ struct QWave {
     K1WaveLds k;
 };
 // dynamic LDS of one K1 group: QWave[kK1Waves], prog[2 * kK1Waves], line[2 * max width] (int16)
-constexpr size_t kK1FixedLds = sizeof(QWave) * kK1Waves + 2 * kK1Waves * sizeof(uint32_t);
+__host__ __device__ constexpr size_t k1_fixed_lds(int waves) { return sizeof(QWave) * waves + 2 * waves * sizeof(uint32_t); }
 
 
 // intraPredAngle / invAngle (H.265 Tables 8-4, 8-5) from the mode with scalar
@@ -1141,14 +1132,14 @@ DEVI void hevc_qres_put(int grp, int Qc, const uint4 (&r)[2], int16_t* body, int
     }
 }
 
-template <typename Pel>
+template <typename Pel, int W_>
 DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
                     int16_t* line) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     QWave& w = W[wv];
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
-    constexpr int kSlots = 2 * kK1Waves;
+    constexpr int kSlots = 2 * W_;
     const FU u = make_fu(f, arena);
     if (wv >= u.ctb_h) return;
     const int shc = grp ? 1 : 0;                 // component subsampling of this group
@@ -1160,7 +1151,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     const int Wc = u.width >> shc, Hc = u.height >> shc;
     const int ncomp = grp ? 2 : 1;
     PROF_DECL;
-    // the wave's quadrant sequence: rows wv, wv + kK1Waves, ..., CTBs left to right, z-order
+    // the wave's quadrant sequence: rows wv, wv + W_, ..., CTBs left to right, z-order
     // quadrants, skipping quadrants outside the picture
     auto q_inside = [&](int row, int cx, int q) {
         return cx * Sc + (q & 1) * Qc < Wc && row * Sc + (q >> 1) * Qc < Hc;
@@ -1169,7 +1160,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
         do {
             if (++q == nqs * nqs) {
                 q = 0;
-                if (++cx == u.ctb_w) { cx = 0; row += kK1Waves; }
+                if (++cx == u.ctb_w) { cx = 0; row += W_; }
             }
         } while (row < u.ctb_h && !q_inside(row, cx, q));
     };
@@ -1186,7 +1177,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     grange(wv * u.ctb_w, na, nb);
     uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
     uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
-    for (int row = wv; row < u.ctb_h; row += kK1Waves) {
+    for (int row = wv; row < u.ctb_h; row += W_) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
@@ -1201,7 +1192,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
             uint2 msk = nmsk;
             {
                 int nrow = row, ncx = cx + 1;
-                if (ncx == u.ctb_w) { ncx = 0; nrow += kK1Waves; }
+                if (ncx == u.ctb_w) { ncx = 0; nrow += W_; }
                 if (nrow < u.ctb_h) {
                     const int ncb = nrow * u.ctb_w + ncx;
                     grange(ncb, na, nb);
@@ -1350,18 +1341,18 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
 // Separate kernels per codec so each gets its own register budget; a mixed
 // batch launches both and each skips the other codec's pictures.
 // grid (pictures, 2): blockIdx.y = 0 luma chain, 1 chroma chains.
-template <typename Pel>
-__global__ void __launch_bounds__(64 * kK1Waves) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
-                                                                  uint8_t* arena) {
+template <typename Pel, int W_>
+__global__ void __launch_bounds__(64 * W_) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
+                                                            uint8_t* arena) {
     extern __shared__ __align__(16) uint8_t k1lds[];
     QWave* W = reinterpret_cast<QWave*>(k1lds);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(k1lds + sizeof(QWave) * kK1Waves);
-    int16_t* line = reinterpret_cast<int16_t*>(k1lds + kK1FixedLds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(k1lds + sizeof(QWave) * W_);
+    int16_t* line = reinterpret_cast<int16_t*>(k1lds + k1_fixed_lds(W_));
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
-    if (threadIdx.x < 2 * kK1Waves) prog[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * W_) prog[threadIdx.x] = 0;
     __syncthreads();
-    hevc_rows<Pel>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line);
+    hevc_rows<Pel, W_>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line);
 }
 
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
@@ -2278,14 +2269,33 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (b->has_hevc) {
-        const size_t lds = kK1FixedLds + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint8_t>, dim3(b->nframes, 2), dim3(64 * kK1Waves), lds, s, b->frames,
-                           b->tus, b->arena);
-        int r = check(hipGetLastError(), "h2j_k1_recon_hevc<u8>");
-        if (r) return r;
-        hipLaunchKernelGGL(h2j_k1_recon_hevc<uint16_t>, dim3(b->nframes, 2), dim3(64 * kK1Waves), lds, s, b->frames,
-                           b->tus, b->arena);
-        r = check(hipGetLastError(), "h2j_k1_recon_hevc<u16>");
+        // two workgroups per picture (luma, chroma).  Up to 128 pictures every group gets a CU
+        // of its own and runs kK1WavesWide waves (rows in flight); beyond that two groups share
+        // a CU and run kK1Waves each (VGPR-bound occupancy).
+        const bool wide = b->nframes <= 128;
+        const int wv = wide ? kK1WavesWide : kK1Waves;
+        const size_t lds = k1_fixed_lds(wv) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1WavesWide>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1Waves>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1Waves>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+        const dim3 grid(b->nframes, 2), block(64 * wv);
+        if (wide) {
+            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
+        } else {
+            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
+        }
+        int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
         if (r) return r;
     }
     if (b->has_h264) {
@@ -2317,7 +2327,7 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
     const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + 12 * static_cast<size_t>(b->max_w);
     static bool attr = false;
     if (!attr) {  // line buffers of pictures wider than ~3.6K need more than the 64 KB default
-        hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k2_deblock264),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k2_deblock264),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }

@@ -444,13 +444,15 @@ std::vector<int> chunk_plan(int n) {
     const char* e = std::getenv("H2J_CHUNK");
     if (e && std::atoi(e) > 0) chunk = std::atoi(e);
     chunk = std::max(1, chunk);
+    const char* tail = std::getenv("H2J_TAIL");  // "0": no shrinking tail chunks
+    const bool shrink = !(tail && tail[0] == '0');
     std::vector<int> starts;
     int i = 0;
     while (i < n) {
         starts.push_back(i);
         int c = chunk;
         const int left = n - i;
-        if (left <= chunk && left > 64 && chunk >= 128) c = left / 2;  // tail: halve
+        if (shrink && left <= chunk && left > 64 && chunk >= 128) c = left / 2;  // tail: halve
         i += std::min(c, left);
     }
     starts.push_back(n);
