@@ -232,8 +232,9 @@ def main():
         frames_per_launch = n / chunks
         alg_bytes_launch = sum(frame_bytes) / chunks
         achieved = alg_bytes_launch / (k1_ms / 1e3) / 1e9
-        gpu_ms = (per["h2d_ms"] + per["prep_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"]
-                  + per["jpeg_ms"] + per["entropy_ms"] + per["d2h_ms"])
+        kern_ms = (per["prep_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"]
+                   + per["entropy_ms"])
+        gpu_ms = kern_ms + per["h2d_ms"] + per["d2h_ms"]
         k1_name = {"avc1080": "h2j_k1_recon_h264", "mixed": "h2j_k1_recon_hevc+h2j_k1_recon_h264"}.get(
             args.workload, "h2j_k1_recon_hevc")
         traffic = pmc_traffic(args.workload)
@@ -257,6 +258,11 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes_launch, "frames_per_launch": frames_per_launch,
                          "avg_launch_ms": k1_ms},
+            # value is end to end: host CABAC/CAVLC (north_star keeps entropy decoding on host
+            # threads) + PCIe + K0-K5 + container.  With the job records already in HBM the
+            # GPU kernels alone sustain hbm_resident_fps; gpu_pipeline_fps adds the PCIe copies.
+            "timed_region": "bitstreams in host memory -> JPEG bytes in host memory (host entropy decode inside)",
+            "hbm_resident_fps": n / (kern_ms / 1e3),
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
