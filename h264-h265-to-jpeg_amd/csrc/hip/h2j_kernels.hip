@@ -243,11 +243,6 @@ DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
            (static_cast<uint64_t>(__builtin_amdgcn_readlane(m.y, l)) << 32);
 }
 
-DEVI uint64_t* tu_masks(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint64_t*>(arena + f.aux); }
-DEVI uint32_t* ctb_ranges(const h2j_frame& f, uint8_t* arena) { return reinterpret_cast<uint32_t*>(arena + f.ctbrng); }
-DEVI int16_t* res_plane(const h2j_frame& f, uint8_t* arena, int c) {
-    return reinterpret_cast<int16_t*>(arena + f.res) + f.pic_off[c];
-}
 
 // HEVC dequantisation (8.6.2-8.6.3) + inverse transform / transform skip /
 // bypass (8.6.4) of one TB into R (int16, stride rst).
@@ -767,62 +762,118 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
     wave_sync();
 }
 
-// H.264 macroblock rows: per MB one batched round trip (TU records, masks,
-// top line, residual), the prediction chain in LDS, one store of the MB.
+// H.264 macroblock rows.  Per MB: the records (held one per lane, prefetched
+// while the previous MB runs: in raster order the next MB's records start
+// where this MB's end), the K0 residual (registers, one MB ahead), the line
+// above from a per-picture LDS line buffer (each row leaves its unfiltered
+// bottom samples there; the top-left corner is carried), the prediction
+// chain in the LDS window, one store of the MB.
+struct H4Pre {      // one MB's prefetched inputs
+    uint4 rec;      // lane t < 24: record t
+    uint2 msk;
+    uint2 ry;       // luma residual: 4 per lane
+    uint32_t rc;    // chroma residual: 2 per lane
+};
+
 template <typename Pel>
-DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog) {
+DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog,
+                    uint16_t* line) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t* masks = tu_masks(f, arena);
-    const uint32_t* rng = ctb_ranges(f, arena);
+    const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
     constexpr int kSlots = 2 * kAvcWaves;
-    Pel* PY = plane<Pel>(f, arena, f.pic, 0);
-    Pel* PC[2] = {plane<Pel>(f, arena, f.pic, 1), plane<Pel>(f, arena, f.pic, 2)};
-    const int16_t* RY = res_plane(f, arena, 0);
-    const int16_t* RC[2] = {res_plane(f, arena, 1), res_plane(f, arena, 2)};
-    const int sty = f.pic_stride[0], stc = f.pic_stride[1];
-    const int W = f.width, Wc = f.width >> 1;
-    for (int row = w; row < f.ctb_h; row += kAvcWaves) {
+    const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h);
+    const int W = ufl(f.width), Wc = W >> 1;
+    const int bdy = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
+    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
+    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
+    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
+    const int16_t* RY = reinterpret_cast<const int16_t*>(arena + ufl64(f.res));
+    const int16_t* RC[2] = {RY + ufl(f.pic_off[1]), RY + ufl(f.pic_off[2])};
+    uint16_t* LY = line;            // [W]: bottom luma row of the MB row above
+    uint16_t* LC = line + W;        // [2][Wc]
+    const uint32_t ntot = ufl(f.ntu);
+    if (w >= mbh) return;
+    auto fetch = [&](int mx, int my, uint32_t a, H4Pre& p) {
+        const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
+        p.rec = reinterpret_cast<const uint4*>(T)[ri];
+        p.msk = reinterpret_cast<const uint2*>(masks)[ri];
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        p.ry = *reinterpret_cast<const uint2*>(RY + (my * 16 + r) * sty + mx * 16 + c4);
+        const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
+        p.rc = *reinterpret_cast<const uint32_t*>(RC[c] + (my * 8 + rr) * stc + mx * 8 + c2);
+    };
+    H4Pre pre;
+    uint32_t pre_a = rng[4 * (w * mbw)];  // first record the prefetch assumed
+    fetch(0, w, pre_a, pre);
+    uint16_t cy_corner = 0, cc_corner[2] = {0, 0};  // carried top-left samples (luma, Cb, Cr)
+    for (int row = w; row < mbh; row += kAvcWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
         const int gy = row * 16, cy = row * 8;
-        for (int mx = 0; mx < f.ctb_w; mx++) {
+        for (int mx = 0; mx < mbw; mx++) {
             const int gx = mx * 16, cx = mx * 8;
+            const int cb = row * mbw + mx;
+            const uint4 rg = reinterpret_cast<const uint4*>(rng)[cb];
+            const uint32_t a = rg.x, ntu = min(rg.z - rg.x, static_cast<uint32_t>(kH4MaxTus));
             if (row > 0) {
-                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, f.ctb_w));
+                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
                 if (seen < need) {
                     while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
                         __builtin_amdgcn_s_sleep(1);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
             }
-            const int cb = row * f.ctb_w + mx;
-            const uint32_t a = rng[4 * cb], ntu = min(rng[4 * cb + 2] - a, static_cast<uint32_t>(kH4MaxTus));
-            // ---- batched loads: records, masks, top line, left column (first MB), residual
-            if (lane < static_cast<int>(ntu)) {
-                s.tus[lane] = T[a + lane];
-                s.masks[lane] = masks[a + lane];
+            // ---- window: prefetched records / residual, line above from LDS, left column carried
+            if (pre_a != a) {  // an MB without records before this one: reload the records
+                const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
+                pre.rec = reinterpret_cast<const uint4*>(T)[ri];
+                pre.msk = reinterpret_cast<const uint2*>(masks)[ri];
             }
-            if (lane < 25) {
+            if (lane < static_cast<int>(ntu)) {
+                memcpy(&s.tus[lane], &pre.rec, sizeof(h2j_tu));
+                s.masks[lane] = static_cast<uint64_t>(pre.msk.x) | (static_cast<uint64_t>(pre.msk.y) << 32);
+            }
+            {
+                const int r = lane >> 2, c4 = (lane & 3) * 4;
+                *reinterpret_cast<uint2*>(&s.ry[r][c4]) = pre.ry;
+                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
+                *reinterpret_cast<uint32_t*>(&s.rc[c][rr][c2]) = pre.rc;
+            }
+            if (lane < 25) {  // luma x = gx - 1 .. gx + 23
                 const int x = gx - 1 + lane;
-                s.wy[0][lane] = (row > 0 && x >= 0 && x < W) ? static_cast<uint16_t>(PY[(gy - 1) * sty + x]) : 0;
+                uint16_t v = 0;
+                if (row > 0 && x >= 0 && x < W) v = lane == 0 ? cy_corner : LY[x];
+                s.wy[0][lane] = v;
             } else if (lane < 43) {
                 const int k = lane - 25, c = k / 9, i = k % 9, x = cx - 1 + i;
-                s.wc[c][0][i] = (row > 0 && x >= 0 && x < Wc) ? static_cast<uint16_t>(PC[c][(cy - 1) * stc + x]) : 0;
+                uint16_t v = 0;
+                if (row > 0 && x >= 0 && x < Wc) v = i == 0 ? (c ? cc_corner[1] : cc_corner[0]) : LC[c * Wc + x];
+                s.wc[c][0][i] = v;
             }
             if (mx == 0) {  // left of the picture: never available
                 if (lane < 16) s.wy[lane + 1][0] = 0;
                 else if (lane < 32) s.wc[(lane - 16) >> 3][((lane - 16) & 7) + 1][0] = 0;
             }
-            {
-                const int r = lane >> 2, c4 = (lane & 3) * 4;  // luma residual: 4 per lane
-                const uint2 v = *reinterpret_cast<const uint2*>(RY + (gy + r) * sty + gx + c4);
-                *reinterpret_cast<uint2*>(&s.ry[r][c4]) = v;
-                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;  // chroma: 2 per lane
-                const uint32_t u = *reinterpret_cast<const uint32_t*>(RC[c] + (cy + rr) * stc + cx + c2);
-                *reinterpret_cast<uint32_t*>(&s.rc[c][rr][c2]) = u;
+            {  // prefetch the wave's next MB (its records follow this MB's in raster order)
+                int nx = mx + 1, ny = row;
+                uint32_t na = rg.z;
+                if (nx == mbw) {
+                    nx = 0;
+                    ny += kAvcWaves;
+                    na = ny < mbh ? rng[4 * (ny * mbw)] : 0;
+                }
+                if (ny < mbh) {
+                    fetch(nx, ny, na, pre);
+                    pre_a = na;
+                }
             }
             wave_sync();
+            // the next MB's top-left corners = this MB's top line end (about to be overwritten)
+            cy_corner = s.wy[0][16];
+            cc_corner[0] = s.wc[0][0][8];
+            cc_corner[1] = s.wc[1][0][8];
             const bool pcm = ntu > 0 && (s.tus[0].flags & H2J_TU_PCM);
             if (pcm) {  // samples written by K0: pull them into the window
                 for (int i = lane; i < 256; i += 64) s.wy[(i >> 4) + 1][(i & 15) + 1] = PY[(gy + (i >> 4)) * sty + gx + (i & 15)];
@@ -834,7 +885,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             } else {
                 for (uint32_t t = 0; t < ntu; t++) {
                     const h2j_tu tu = s.tus[t];
-                    h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? f.bit_depth_c : f.bit_depth, s, lane);
+                    h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? bdc : bdy, s, lane);
                 }
                 // ---- store the macroblock
                 {
@@ -847,7 +898,14 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     e[1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
                 }
             }
-            // right column becomes the next MB's left column
+            // bottom row for the MB row below; right column becomes the next MB's left column
+            if (row + 1 < mbh) {
+                if (lane < 16) LY[gx + lane] = s.wy[16][lane + 1];
+                else if (lane < 32) {
+                    const int c = (lane - 16) >> 3, i = (lane - 16) & 7;
+                    LC[c * Wc + cx + i] = s.wc[c][8][i + 1];
+                }
+            }
             if (lane < 16) s.wy[lane + 1][0] = s.wy[lane + 1][16];
             else if (lane < 32) {
                 const int c = (lane - 16) >> 3, i = ((lane - 16) & 7) + 1;
@@ -1357,15 +1415,18 @@ __global__ void __launch_bounds__(64 * W_) h2j_k1_recon_hevc(const h2j_frame* fr
 
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
                                                                   uint8_t* arena) {
-    __shared__ H4WaveLds wl[kAvcWaves];
-    __shared__ uint32_t prog[2 * kAvcWaves];
+    extern __shared__ __align__(16) uint8_t h4lds[];
+    H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(h4lds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves);
+    uint16_t* line = reinterpret_cast<uint16_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4);
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_H264) return;
     if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
-    if (f.bit_depth == 8) h264_rows<uint8_t>(f, tus + f.tu, arena, s, prog);
-    else h264_rows<uint16_t>(f, tus + f.tu, arena, s, prog);
+    const h2j_tu* T = tus + ufl(f.tu);
+    if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line);
+    else h264_rows<uint16_t>(f, T, arena, s, prog, line);
 }
 
 // ---------------------------------------------------------------- K2: deblocking
@@ -2299,7 +2360,16 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         if (r) return r;
     }
     if (b->has_h264) {
-        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kAvcWaves), 0, s, b->frames, b->tus, b->arena);
+        // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
+        const size_t lds = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4 + 4 * static_cast<size_t>(b->max_w);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_h264),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
+                           b->arena);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;
