@@ -63,10 +63,28 @@ public:
         value_ -= one ? scaled : 0;
         return one;
     }
+    // k (1..24) bypass bins at once, first bin in the MSB.  Decoding bypass bins
+    // (9.3.4.3.4) is long division of the offset, extended by one look-ahead bit
+    // per bin, by the range: the bins are the k-bit quotient, the new offset the
+    // remainder.
+    inline uint32_t bypass_batch(int k) {
+        if (bits_ < k) refill();
+        const int sh = bits_ - k;
+        const uint64_t v = value_ >> sh;
+        const uint32_t q = static_cast<uint32_t>(v / range_);
+        value_ -= (static_cast<uint64_t>(q) * range_) << sh;
+        bits_ = sh;
+        return q;
+    }
     inline uint32_t bypass_bits(int n) {
-        uint32_t v = 0;
-        for (int i = 0; i < n; i++) v = (v << 1) | static_cast<uint32_t>(bypass());
-        return v;
+        if (n <= 2) {
+            uint32_t v = 0;
+            for (int i = 0; i < n; i++) v = (v << 1) | static_cast<uint32_t>(bypass());
+            return v;
+        }
+        if (n <= 24) return bypass_batch(n);
+        const uint32_t hi = bypass_batch(n - 16);
+        return (hi << 16) | bypass_batch(16);
     }
     inline int terminate() {
         range_ -= 2;

@@ -288,6 +288,7 @@ int parse_pps(BitReader& b, Pps* tab) {
 }
 
 uint8_t g_scan_diag[4][64][2], g_scan_hor[4][64][2], g_scan_ver[4][64][2];
+uint8_t g_scan_inv[3][4][64];  // [scanIdx][log2 size][y * size + x] -> scan position
 uint8_t g_diag_pos4[16];  // raster (y*4+x) of 4x4 diag scan
 uint8_t g_diag_pos8[64];
 // context index (C_SIG-relative) of sig_coeff_flag (9.3.4.2.5):
@@ -325,6 +326,12 @@ void init_scans() {
                 g_scan_ver[l][i][1] = static_cast<uint8_t>(y);
             }
     }
+    for (int si = 0; si < 3; si++)
+        for (int l = 0; l < 4; l++) {
+            const uint8_t(*sc)[64][2] = si == 0 ? g_scan_diag : (si == 1 ? g_scan_hor : g_scan_ver);
+            for (int i = 0; i < (1 << (2 * l)); i++)
+                g_scan_inv[si][l][sc[l][i][1] * (1 << l) + sc[l][i][0]] = static_cast<uint8_t>(i);
+        }
     for (int c = 0; c < 2; c++)
         for (int lsb = 0; lsb < 4; lsb++)
             for (int si = 0; si < 3; si++)
@@ -802,15 +809,8 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     const uint8_t(*sc)[64][2] = scanIdx == 0 ? g_scan_diag : (scanIdx == 1 ? g_scan_hor : g_scan_ver);
     const int lsb = log2n - 2;
     // locate last position in scan order
-    int lastSub = -1, lastPos = -1;
-    {
-        int xs = lx >> 2, ys = ly >> 2, xp = lx & 3, yp = ly & 3;
-        const int nsb = 1 << (2 * lsb);
-        for (int i = 0; i < nsb; i++)
-            if (sc[lsb][i][0] == xs && sc[lsb][i][1] == ys) { lastSub = i; break; }
-        for (int k = 0; k < 16; k++)
-            if (sc[2][k][0] == xp && sc[2][k][1] == yp) { lastPos = k; break; }
-    }
+    const int lastSub = g_scan_inv[scanIdx][lsb][((ly >> 2) << lsb) + (lx >> 2)];
+    const int lastPos = g_scan_inv[scanIdx][2][((ly & 3) << 2) + (lx & 3)];
     uint8_t csbf[8][8];
     std::memset(csbf, 0, sizeof(csbf));
     int greater1_ctx = 1;
@@ -879,10 +879,16 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         if (lastG1 != -1) g2 = cc.decision(ctx[C_GT2 + ctxSet + (c ? 4 : 0)]);
         unsigned signs = 0;
         const unsigned signed_mask = (sdh && hidden) ? (sigmask & ~(1u << firstSig)) : sigmask;
-        for (unsigned m = signed_mask; m;) {
-            const int nn = 31 - __builtin_clz(m);
-            m &= ~(1u << nn);
-            signs |= static_cast<unsigned>(cc.bypass()) << nn;
+        {
+            // all sign bins at once; bin i (MSB first) belongs to the i-th highest position
+            const int ns = __builtin_popcount(signed_mask);
+            uint32_t q = ns > 1 ? cc.bypass_batch(ns) : (ns ? static_cast<uint32_t>(cc.bypass()) : 0u);
+            for (unsigned m = signed_mask; m;) {
+                const int nn = __builtin_ctz(m);  // lowest position takes the last bin
+                m &= m - 1;
+                signs |= (q & 1u) << nn;
+                q >>= 1;
+            }
         }
         int numSig = 0, sumAbs = 0, rice = 0;
         for (unsigned m = sigmask; m;) {

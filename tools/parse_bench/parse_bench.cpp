@@ -17,15 +17,20 @@
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: parse_bench file... [-r reps] [-t threads]\n");
+        std::fprintf(stderr, "usage: parse_bench file... [-r reps] [-t threads] [-d (output digest)]\n");
         return 2;
     }
     int reps = 3, threads = 1;
+    bool want_digest = false;
     std::vector<std::vector<uint8_t>> streams;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "-r" && i + 1 < argc) {
             reps = std::atoi(argv[++i]);
+            continue;
+        }
+        if (a == "-d") {
+            want_digest = true;
             continue;
         }
         if (a == "-t" && i + 1 < argc) {
@@ -44,6 +49,7 @@ int main(int argc, char** argv) {
     const int total = reps * static_cast<int>(streams.size());
     std::atomic<int> next(0), failed(0);
     std::atomic<size_t> tus(0), coefs(0), bytes(0);
+    std::atomic<unsigned long long> digest(0);  // order-independent checksum of all parse outputs
     auto worker = [&]() {
         h2j::FrameJob job;
         size_t t = 0, c = 0, b = 0;
@@ -60,6 +66,16 @@ int main(int argc, char** argv) {
             t += job.tus.size();
             c += job.coefs.size();
             b += s.size();
+            if (!want_digest) continue;
+            unsigned long long hsh = 1469598103934665603ull;
+            auto mix = [&](const void* p, size_t n) {
+                const unsigned char* q = static_cast<const unsigned char*>(p);
+                for (size_t j = 0; j < n; j++) hsh = (hsh ^ q[j]) * 1099511628211ull;
+            };
+            mix(job.tus.data(), job.tus.size() * sizeof(h2j_tu));
+            mix(job.coefs.data(), job.coefs.size() * sizeof(h2j_coef));
+            mix(job.ctbs.data(), job.ctbs.size() * sizeof(h2j_ctb));
+            digest += hsh;
         }
         tus += t;
         coefs += c;
@@ -72,7 +88,8 @@ int main(int argc, char** argv) {
     if (failed) return 1;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const double nf = total;
-    std::printf("%d thr: %.3f ms/frame wall, %.3f ms/frame/thread  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s\n",
-                threads, ms / nf, ms * threads / nf, tus / nf, coefs / nf, bytes / (ms / 1e3) / 1e6);
+    std::printf("%d thr: %.3f ms/frame wall, %.3f ms/frame/thread  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s  digest %016llx\n",
+                threads, ms / nf, ms * threads / nf, tus / nf, coefs / nf, bytes / (ms / 1e3) / 1e6,
+                static_cast<unsigned long long>(digest));
     return 0;
 }
