@@ -1144,10 +1144,15 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             const int a = vert ? y : x, b = vert ? x : y;  // a: distance from the main reference, b: position along it
             const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
             const int k1 = b + idx + 1, k2 = k1 + 1;
-            const int i1 = k1 >= 0 ? 2 * n + sgn * k1 : 2 * n - sgn * ((k1 * inv + 128) >> 8);
-            const int i2 = k2 >= 0 ? 2 * n + sgn * k2 : 2 * n - sgn * ((k2 * inv + 128) >> 8);
-            int pv = ((32 - fr) * R[i1] + fr * R[i2] + 16) >> 5;
-            if (bnd && b == 0) pv = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n - sgn * (a + 1)] - R[2 * n]) >> 1));
+            // negative k projects onto the side reference through invAngle; both forms are
+            // computed and selected (no divergent branch)
+            const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
+            const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
+            int pv = ((32 - fr) * R[2 * n + sgn * o1] + fr * R[2 * n + sgn * o2] + 16) >> 5;
+            if (bnd) {
+                const int e = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n - sgn * (a + 1)] - R[2 * n]) >> 1));
+                pv = b == 0 ? e : pv;
+            }
             int16_t* d = body + (oy + y) * S + ox + x;
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
