@@ -8,12 +8,15 @@
 // src/Encoder.cpp:29), decoder-delay streams are handled (the first picture
 // is decoded directly), 10-bit input is converted with
 // v8 = min(255, (v + 2) >> 2) instead of producing a corrupted JPEG.
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <ctime>
+#include <deque>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "IDecoder.h"
@@ -36,13 +39,89 @@ void LOG(const char* format, ...) {
 
 namespace {
 
-// One engine per process (per GPU 0); IDecoder instances are cheap handles.
-std::mutex g_engine_mu;
+// One engine per process (GPU 0); IDecoder instances are cheap handles.
+// Concurrent H265ToJpeg calls are batched: callers queue their bitstreams and
+// whichever caller finds the engine idle runs everything queued as one
+// h2j_engine_transcode batch (host entropy decoding fans out over the engine's
+// thread pool, the GPU sees one launch per stage), then hands every caller its
+// JPEG.  A lone caller simply runs a batch of one.
+struct Request {
+    const uint8_t* data = nullptr;
+    size_t size = 0;
+    std::vector<uint8_t> jpeg;
+    int status = 0;
+    std::string error;
+    bool done = false;
+};
+
+std::mutex g_mu;
+std::condition_variable g_cv;
+std::deque<Request*> g_queue;
+bool g_busy = false;
 h2j_engine* g_engine = nullptr;
 
-h2j_engine* shared_engine() {
-    if (!g_engine) g_engine = h2j_engine_create(0, 0);
-    return g_engine;
+// run one batch (caller holds no lock); fills jpeg / status / error of each request
+void run_batch(h2j_engine* e, std::vector<Request*>& batch) {
+    const int n = static_cast<int>(batch.size());
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<size_t> sizes(n), off(n), len(n);
+    std::vector<int> status(n);
+    size_t cap = 8u << 20;
+    for (int i = 0; i < n; i++) {
+        ptrs[i] = batch[i]->data;
+        sizes[i] = batch[i]->size;
+        cap += batch[i]->size * 4 + (2u << 20);
+    }
+    std::vector<uint8_t> out;
+    int r = -1;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        out.resize(cap);
+        r = h2j_engine_transcode(e, n, ptrs.data(), sizes.data(), out.data(), cap, off.data(), len.data(),
+                                 status.data());
+        bool small = false;
+        for (int i = 0; i < n; i++) small = small || status[i] == -50;
+        if (!small) break;
+        cap *= 4;
+    }
+    for (int i = 0; i < n; i++) {
+        Request* q = batch[i];
+        q->status = status[i];
+        if (r != 0 && status[i] == 0) q->status = r;
+        if (q->status == 0) q->jpeg.assign(out.begin() + static_cast<long>(off[i]),
+                                           out.begin() + static_cast<long>(off[i] + len[i]));
+        else q->error = h2j_engine_error(e);
+    }
+}
+
+// transcode one picture through the shared, batching engine
+bool transcode_shared(Request& req) {
+    std::unique_lock<std::mutex> lk(g_mu);
+    g_queue.push_back(&req);
+    while (!req.done) {
+        if (g_busy) {
+            g_cv.wait(lk);
+            continue;
+        }
+        g_busy = true;
+        if (!g_engine) g_engine = h2j_engine_create(0, 0);
+        h2j_engine* e = g_engine;
+        std::vector<Request*> batch(g_queue.begin(), g_queue.end());
+        g_queue.clear();
+        lk.unlock();
+        if (e) {
+            run_batch(e, batch);
+        } else {
+            for (Request* q : batch) {
+                q->status = -1;
+                q->error = "no HIP device available: the MI355X pipeline cannot run";
+            }
+        }
+        lk.lock();
+        for (Request* q : batch) q->done = true;
+        g_busy = false;
+        g_cv.notify_all();
+    }
+    return req.status == 0;
 }
 
 bool read_file(const char* path, std::vector<uint8_t>& buf) {
@@ -75,31 +154,14 @@ bool Decoder::H265ToJpeg(const char* const in, const char* const out) {
         LOG("cannot open input file: %s", in);
         return false;
     }
-    std::vector<uint8_t> jpeg;
-    {
-        std::lock_guard<std::mutex> g(g_engine_mu);
-        h2j_engine* e = shared_engine();
-        if (!e) {
-            LOG("no HIP device available: the MI355X pipeline cannot run");
-            return false;
-        }
-        const uint8_t* d = data.data();
-        size_t sz = data.size(), off = 0, len = 0;
-        int status = 0;
-        size_t cap = 1 << 20;
-        for (int attempt = 0; attempt < 2; attempt++) {
-            cap = std::max(cap, sz * 4 + (8u << 20));
-            jpeg.resize(cap);
-            int r = h2j_engine_transcode(e, 1, &d, &sz, jpeg.data(), cap, &off, &len, &status);
-            if (r == 0 && status == 0) break;
-            if (status == -50) { cap *= 4; continue; }
-            LOG("transcode failed (%d/%d): %s", r, status, h2j_engine_error(e));
-            return false;
-        }
-        if (status != 0) return false;
-        jpeg.erase(jpeg.begin(), jpeg.begin() + static_cast<long>(off));
-        jpeg.resize(len);
+    Request req;
+    req.data = data.data();
+    req.size = data.size();
+    if (!transcode_shared(req)) {
+        LOG("transcode failed (%d): %s", req.status, req.error.c_str());
+        return false;
     }
+    const std::vector<uint8_t>& jpeg = req.jpeg;
     FILE* f = fopen(out, "wb+");
     if (!f) {
         LOG("failed to encode Yuv to Jpeg: cannot open %s", out);
