@@ -126,6 +126,25 @@ def shard_lpt(costs, world):
     return [sorted(p) for p in parts]
 
 
+def host_cpu_share(local_rank, local_world, requested=0, cap=16):
+    """Host entropy threads for this rank: its slice of the CPUs the job may use
+    (sched_getaffinity, not os.cpu_count, which reports the whole machine), at
+    most `cap`.  With several ranks per node each rank is pinned to a disjoint
+    slice so the ranks' parse pools do not fight over the same cores."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = list(range(os.cpu_count() or 1))
+    per = max(1, len(cpus) // max(1, local_world))
+    if local_world > 1 and len(cpus) >= local_world:
+        mine = cpus[local_rank * per:(local_rank + 1) * per]
+        try:
+            os.sched_setaffinity(0, mine)
+        except (AttributeError, OSError):
+            pass
+    return requested if requested > 0 else max(1, min(cap, per))
+
+
 def cpu_baseline(streams, budget_s=12.0):
     """Oracle (CPU restatement of the reference path) on 1 host core, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -148,7 +167,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=1024, help="frames per GPU per step")
-    ap.add_argument("--threads", type=int, default=16, help="host entropy/Huffman threads per GPU")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host entropy/Huffman threads per GPU (default: this rank's share of the CPUs, at most 16)")
     ap.add_argument("--workload", default="hevc1080", choices=sorted(WORKLOADS),
                     help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]/[4]")
     ap.add_argument("--streams", default=None, help="override the workload's stream glob")
@@ -183,6 +203,7 @@ def main():
         streams = load_streams(args.streams or wl["streams"])
         batch = [streams[i % len(streams)] for i in range(n)]
         frame_bytes = [alg_bytes_per_frame(wl)] * n
+    args.threads = host_cpu_share(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))), args.threads)
     eng = h2j.Engine(local, args.threads)
 
     # pre-built ctypes arguments: nothing but the C call inside the timed region

@@ -57,3 +57,17 @@ def test_shard_lpt_balanced_and_complete(world):
     assert sorted(i for p in parts for i in p) == list(range(1000))
     loads = [sum(costs[i] for i in p) for p in parts]
     assert max(loads) - min(loads) <= max(costs)
+
+
+def test_host_cpu_share_slices_affinity():
+    # run in a child: the helper pins the calling process when local_world > 1
+    import subprocess, sys, os
+    code = ("import sys, os; sys.path.insert(0, %r); import bench; "
+            "n = len(os.sched_getaffinity(0)); a = bench.host_cpu_share(0, 1); "
+            "b = bench.host_cpu_share(1, 2); m = len(os.sched_getaffinity(0)); "
+            "print(n, a, b, m)") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.check_output([sys.executable, "-c", code], text=True).split()
+    n, a, b, m = map(int, out)
+    assert a == min(16, n)
+    if n >= 2:
+        assert b == min(16, n // 2) and m == n // 2
