@@ -777,7 +777,7 @@ struct H4Pre {      // one MB's prefetched inputs
 
 template <typename Pel>
 DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog,
-                    uint16_t* line) {
+                    uint16_t* line, int band, int nbands) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
@@ -793,7 +793,13 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     uint16_t* LY = line;            // [W]: bottom luma row of the MB row above
     uint16_t* LC = line + W;        // [2][Wc]
     const uint32_t ntot = ufl(f.ntu);
-    if (w >= mbh) return;
+    // this workgroup's rows: one band of 16 MB rows (one per wave; tall pictures run on several
+    // workgroups, see h2j_frame.k1bands) or, unbanded, rows w, w + 16, ...
+    const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
+    // band hand-off: per-row progress words (4th word of the row's first CTB range, zeroed) and
+    // the boundary rows, both accessed with agent-scope atomics (coherent across CUs / XCDs)
+    const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
+    if (rbeg + w >= rend) return;
     auto fetch = [&](int mx, int my, uint32_t a, H4Pre& p) {
         const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
         p.rec = reinterpret_cast<const uint4*>(T)[ri];
@@ -804,20 +810,39 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
         p.rc = *reinterpret_cast<const uint32_t*>(RC[c] + (my * 8 + rr) * stc + mx * 8 + c2);
     };
     H4Pre pre;
-    uint32_t pre_a = rng[4 * (w * mbw)];  // first record the prefetch assumed
-    fetch(0, w, pre_a, pre);
+    uint32_t pre_a = rng[4 * ((rbeg + w) * mbw)];  // first record the prefetch assumed
+    fetch(0, rbeg + w, pre_a, pre);
     uint16_t cy_corner = 0, cc_corner[2] = {0, 0};  // carried top-left samples (luma, Cb, Cr)
-    for (int row = w; row < mbh; row += kAvcWaves) {
+    for (int row = rbeg + w; row < rend; row += kAvcWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
+        const bool from_band = nbands > 1 && band > 0 && row == rbeg;             // line above from the band above
+        const bool to_band = nbands > 1 && band < nbands - 1 && row == rend - 1;  // bottom row to the band below
+        // boundary b (between bands b and b + 1): W dwords = 2W uint16 (luma W, then Cb, Cr Wc each)
+        const uint64_t o_xin = o_xl + 4ull * (band - 1) * W, o_xout = o_xl + 4ull * band * W;
         const int gy = row * 16, cy = row * 8;
         for (int mx = 0; mx < mbw; mx++) {
             const int gx = mx * 16, cx = mx * 8;
             const int cb = row * mbw + mx;
             const uint4 rg = reinterpret_cast<const uint4*>(rng)[cb];
             const uint32_t a = rg.x, ntu = min(rg.z - rg.x, static_cast<uint32_t>(kH4MaxTus));
-            if (row > 0) {
+            if (from_band) {  // the row above belongs to another workgroup: bounded wait on its global word
+                const uint32_t need = static_cast<uint32_t>(min(mx + 2, mbw));
+                if (seen < need) {
+                    uint32_t it = 0;
+                    uint32_t* fl = reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * ((row - 1) * mbw);
+                    while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
+                            uint32_t* err = reinterpret_cast<uint32_t*>(arena + ufl64(f.jstat) + offsetof(h2j_jstat, dev_error));
+                            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            seen = static_cast<uint32_t>(mbw);
+                            break;
+                        }
+                    }
+                }
+            } else if (row > rbeg || (row > 0 && nbands <= 1)) {
                 const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
                 if (seen < need) {
                     while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
@@ -841,7 +866,16 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
                 *reinterpret_cast<uint32_t*>(&s.rc[c][rr][c2]) = pre.rc;
             }
-            if (lane < 25) {  // luma x = gx - 1 .. gx + 23
+            if (from_band) {  // boundary row of the band above (uint16 pairs in dwords, agent-scope loads)
+                int x = -1, e = 0;
+                if (lane < 25) { x = gx - 1 + lane; e = x; }
+                else if (lane < 43) { const int k = lane - 25, c = k / 9; x = cx - 1 + k % 9; e = W + c * Wc + x; }
+                const bool ok = x >= 0 && (lane < 25 ? x < W : x < Wc);
+                const uint32_t d = ok ? __hip_atomic_load(reinterpret_cast<const uint32_t*>(arena + o_xin) + (e >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                const uint16_t v = ok ? static_cast<uint16_t>((e & 1) ? (d >> 16) : (d & 0xFFFF)) : 0;
+                if (lane < 25) s.wy[0][lane] = v;
+                else if (lane < 43) { const int k = lane - 25; s.wc[k / 9][0][k % 9] = v; }
+            } else if (lane < 25) {  // luma x = gx - 1 .. gx + 23
                 const int x = gx - 1 + lane;
                 uint16_t v = 0;
                 if (row > 0 && x >= 0 && x < W) v = lane == 0 ? cy_corner : LY[x];
@@ -899,7 +933,22 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 }
             }
             // bottom row for the MB row below; right column becomes the next MB's left column
-            if (row + 1 < mbh) {
+            if (to_band) {  // hand the bottom row to the band below: data, wait for completion, then progress
+                if (lane < 16) {
+                    int e0, v0, v1;
+                    if (lane < 8) { e0 = gx + 2 * lane; v0 = s.wy[16][2 * lane + 1]; v1 = s.wy[16][2 * lane + 2]; }
+                    else { const int c = (lane - 8) >> 2, i = ((lane - 8) & 3) * 2; e0 = W + c * Wc + cx + i;
+                           v0 = s.wc[c][8][i + 1]; v1 = s.wc[c][8][i + 2]; }
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(arena + o_xout) + (e0 >> 1), static_cast<uint32_t>(v0) | (static_cast<uint32_t>(v1) << 16),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the boundary stores have completed
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0)
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * (row * mbw), static_cast<uint32_t>(mx + 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else if (row + 1 < mbh) {
                 if (lane < 16) LY[gx + lane] = s.wy[16][lane + 1];
                 else if (lane < 32) {
                     const int c = (lane - 16) >> 3, i = (lane - 16) & 7;
@@ -1418,20 +1467,25 @@ __global__ void __launch_bounds__(64 * W_) h2j_k1_recon_hevc(const h2j_frame* fr
     hevc_rows<Pel, W_>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line);
 }
 
+// grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
+// picture in order, so a band only ever waits on an earlier workgroup)
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
-                                                                  uint8_t* arena) {
+                                                                  uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t h4lds[];
     H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(h4lds);
     uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves);
     uint16_t* line = reinterpret_cast<uint16_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4);
-    const h2j_frame& f = frames[blockIdx.x];
+    const uint32_t me = map[blockIdx.x];
+    const h2j_frame& f = frames[me >> 8];
+    const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264) return;
+    const int nbands = ufl(f.k1bands);
     if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
     const h2j_tu* T = tus + ufl(f.tu);
-    if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line);
-    else h264_rows<uint16_t>(f, T, arena, s, prog, line);
+    if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
+    else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
 }
 
 // ---------------------------------------------------------------- K2: deblocking
@@ -2373,8 +2427,9 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;
         }
-        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->nframes), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
-                           b->arena);
+        if (b->k1wgs > 0)
+            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
+                               b->arena, b->k1map);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;

@@ -192,7 +192,10 @@ struct Slot {
 
 // stats slots (h2j_engine_stats): times in ms summed over chunks; ST_RECON is K1 only, ST_PREP is K0
 enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
-       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_N };
+       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_N };  // ST_PACK: host time packing records into staging
+
+// H.264 pictures with more MB rows than this are reconstructed by several K1 workgroups
+constexpr int kK1BandRows = 68;
 
 // upper bound of one block's entropy-coded size (code lengths <= 16, values <= 16 bits)
 constexpr size_t kSegBytesPerBlock = 272;
@@ -249,6 +252,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         nctb += j.ctbs.size();
         nslice += j.slices.size();
         nsl += j.sl.size();
+        // H.264 K1: pictures taller than 1080p run on one workgroup per 16 MB rows
+        // (a single 16-wave workgroup would walk 5+ rows per wave)
+        f.k1bands = (f.codec == H2J_CODEC_H264 && f.ctb_h > kK1BandRows) ? (f.ctb_h + 15) / 16 : 1;
+        f.xline = 0;
         s.frames[k] = f;
         max_w = std::max(max_w, f.width);
         max_ctbs = std::max(max_ctbs, f.ctb_w * f.ctb_h);
@@ -304,6 +311,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         off = align_up(off + (ysz + ysz / 2) * 2, 256);
         f.aux = off;
         off = align_up(off + static_cast<size_t>(f.ntu) * 8, 256);
+        if (f.k1bands > 1) {  // one luma + two chroma bottom rows (uint16) per band boundary
+            f.xline = off;
+            off = align_up(off + static_cast<size_t>(f.k1bands - 1) * 2 * f.width * 2, 256);
+        }
     }
     const size_t arena_bytes = off;
     // input staging
@@ -313,7 +324,16 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const size_t o_ctbs = align_up(o_coefs + ncoef * sizeof(h2j_coef), 256);
     const size_t o_slices = align_up(o_ctbs + nctb * sizeof(h2j_ctb), 256);
     const size_t o_sl = align_up(o_slices + nslice * sizeof(h2j_slice), 256);
-    const size_t in_bytes = align_up(o_sl + nsl + 16, 256);
+    // H.264 K1 workgroup map: banded pictures first (their long chains start early), bands in order
+    std::vector<uint32_t> k1map;
+    for (int pass = 0; pass < 2; pass++)
+        for (int k = 0; k < nf; k++) {
+            const h2j_frame& f = s.frames[k];
+            if (f.codec != H2J_CODEC_H264 || (f.k1bands > 1) != (pass == 0)) continue;
+            for (int bnd = 0; bnd < f.k1bands; bnd++) k1map.push_back((static_cast<uint32_t>(k) << 8) | bnd);
+        }
+    const size_t o_map = align_up(o_sl + nsl + 16, 256);
+    const size_t in_bytes = align_up(o_map + k1map.size() * 4 + 16, 256);
     if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
     if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
     if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
@@ -326,6 +346,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         if (!s.h_js.ensure(static_cast<size_t>(nf) * s.jstat_stride + 256)) return fail("pinned host allocation failed");
     }
     std::memcpy(s.h_in.p + o_frames, s.frames.data(), nf * sizeof(h2j_frame));
+    if (!k1map.empty()) std::memcpy(s.h_in.p + o_map, k1map.data(), k1map.size() * 4);
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -344,8 +365,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         if (!j.slices.empty()) std::memcpy(hin + o_slices + bs[k] * sizeof(h2j_slice), j.slices.data(), j.slices.size() * sizeof(h2j_slice));
         if (!j.sl.empty()) std::memcpy(hin + o_sl + bl[k], j.sl.data(), j.sl.size());
     };
+    const double tp = now_ms();
     if (pool_free) pool->parallel_for(nf, pack);
     else for (int k = 0; k < nf; k++) pack(k);
+    stats[ST_PACK] += now_ms() - tp;
     uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
     h2j_gpu_batch& b = s.batch;
     b.nframes = nf;
@@ -366,6 +389,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.ctbs = reinterpret_cast<const h2j_ctb*>(din + o_ctbs);
     b.slices = reinterpret_cast<const h2j_slice*>(din + o_slices);
     b.sl = din + o_sl;
+    b.k1map = reinterpret_cast<const uint32_t*>(din + o_map);
+    b.k1wgs = static_cast<int32_t>(k1map.size());
     b.arena = static_cast<uint8_t*>(s.d_arena.p);
     b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
     b.seg_cap = entropy ? seg_cap : 0;
@@ -446,13 +471,15 @@ std::vector<int> chunk_plan(int n) {
     chunk = std::max(1, chunk);
     const char* tail = std::getenv("H2J_TAIL");  // "0": no shrinking tail chunks
     const bool shrink = !(tail && tail[0] == '0');
+    const char* tmin = std::getenv("H2J_TAIL_MIN");  // smallest tail chunk (default 64)
+    const int tail_min = tmin && std::atoi(tmin) > 0 ? std::atoi(tmin) : 64;
     std::vector<int> starts;
     int i = 0;
     while (i < n) {
         starts.push_back(i);
         int c = chunk;
         const int left = n - i;
-        if (shrink && left <= chunk && left > 64 && chunk >= 128) c = left / 2;  // tail: halve
+        if (shrink && left <= chunk && left > tail_min && chunk >= 128) c = left / 2;  // tail: halve
         i += std::min(c, left);
     }
     starts.push_back(n);
@@ -557,6 +584,13 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
         std::vector<size_t> at(nf);
         for (int k = 0; k < nf; k++) {
             const int i = s.live[k];
+            const h2j_jstat* stk = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            if (stk->dev_error) {  // a device-side failure (e.g. a K1 band hand-off timed out)
+                status[i] = -52;
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
             if (!sz[k]) {
                 status[i] = -51;  // payload pool overflow
                 rc = -3;

@@ -56,6 +56,8 @@ typedef struct {
     int32_t max_ntu;            /* max transform-block records over the batch */
     int32_t has_hevc, has_h264; /* codecs present in the batch */
     int32_t max_ctbs;           /* max CTBs (H.264: macroblocks) of one picture over the batch */
+    int32_t k1wgs;              /* H.264 K1 workgroups (sum of h2j_frame.k1bands over H.264 pictures) */
+    const uint32_t *k1map;      /* H.264 K1 workgroup -> (frame << 8) | band, dependency order */
     const h2j_frame *frames;
     const h2j_tu *tus;
     const h2j_coef *coefs;

@@ -108,7 +108,8 @@ typedef struct {
     int32_t pic_off[3];             /* element offset of each plane inside pic / pic2 */
     int32_t mw, mh;                 /* 4x4 map dims */
     int32_t status;                 /* device-side error code */
-    int32_t pad1;
+    int32_t k1bands;                /* H.264 K1: workgroups (16-row bands) this picture runs on */
+    uint64_t xline;                 /* H.264 K1 band boundaries: bottom rows handed to the next band (uint16) */
 } h2j_frame;
 
 /* per-frame JPEG statistics written by the GPU */
@@ -129,6 +130,8 @@ typedef struct {
     uint32_t nbits;         /* payload bits before the 1-padding */
     uint32_t nbytes;        /* padded payload bytes (no 0xFF stuffing) */
     uint64_t seg_off;       /* byte offset of the payload in the segment pool */
+    uint32_t dev_error;     /* device-side failure flags (bit 0: K1 band hand-off timed out) */
+    uint32_t pad_e;
 } h2j_jstat;
 
 #ifdef __cplusplus

@@ -67,3 +67,23 @@ def test_h264_bench_streams_sample(engine):
     outs = engine.transcode(streams)
     for s, o, p in zip(streams, outs, paths):
         assert o == O.transcode(s), p
+
+
+def test_h264_tall_picture_banded(engine):
+    """configs[4] 3840x2160 H.264: 135 MB rows run on 9 K1 workgroups of 16 rows
+    (the last band 7 rows) handing boundary rows across workgroups."""
+    s = read(golden("mixed/avc2160_00.h264"))
+    for stage, skip in ((1, True), (0, False)):
+        gy, gu, gv, bd = engine.decode(s, stage=stage)
+        oy, ou, ov, obd = O.decode(s, 264, skip_loop_filter=skip)
+        assert bd == obd
+        _cmp((gy, gu, gv), (oy, ou, ov), f"stage {stage}")
+
+
+def test_mixed_workload_batch(engine):
+    """configs[4] sample: 720p H.264/H.265 and banded 2160p H.264 in one batch."""
+    paths = sorted(glob.glob(os.path.join(golden("mixed"), "*")))
+    streams = [read(p) for p in paths]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, paths):
+        assert o == O.transcode(s), p
