@@ -20,6 +20,7 @@ import argparse
 import ctypes
 import glob
 import json
+import resource
 import os
 import sys
 import time
@@ -233,6 +234,7 @@ def main():
         step()
     barrier()
     stage_sum = {}
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -240,8 +242,11 @@ def main():
         for k, v in st.items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
     t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
     barrier()
     elapsed = t1 - t0
+    # host CPU time of this process (all threads) over the timed region, in busy cores
+    host_cores = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / max(elapsed, 1e-9)
     elapsed, total_frames = reduce_over_ranks(dist, elapsed, n * args.steps, local)
 
     if rank == 0:
@@ -285,6 +290,7 @@ def main():
             "timed_region": "bitstreams in host memory -> JPEG bytes in host memory (host entropy decode inside)",
             "hbm_resident_fps": n / (kern_ms / 1e3),
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
+            "host_cpu_busy_cores": round(host_cores, 2),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
         if not args.no_cpu_baseline:

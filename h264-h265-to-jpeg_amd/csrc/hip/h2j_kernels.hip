@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "h2j_gpu.h"
@@ -1762,7 +1763,7 @@ DEVI DbInfo db264_info(const h2j_ctb* mbs, const h2j_slice* slices, int mbw, int
 
 template <typename Pel>
 DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
-                       uint32_t* prog, uint16_t* line) {
+                       uint32_t* prog, uint16_t* line, int band, int nbands) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     DbWin& w = W[wv];
     const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
@@ -1774,18 +1775,47 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
     uint16_t* LC = line + 4 * width;      // [2 comps][2 rows][width / 2]: chroma rows 6..7
     const int cw = width >> 1;
     constexpr int kSlots = 2 * kAvcDbWaves;
-    if (wv >= mbh) return;
+    // rows of this workgroup: the K1 banding (h2j_frame.k1bands); across a band boundary the line
+    // buffer lives in frame.xline (3W dwords per boundary) and progress in the row's 4th CTB-range
+    // word, which K1 left at mbw (K2 counts on from there), both with agent-scope atomics
+    const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
+    const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
+    if (rbeg + wv >= rend) return;
     PROF_DECL;
     DbPrefetch<Pel> pf;
-    db264_fetch<Pel>(PY, PC, sty, stc, 0, wv, pf, lane);
-    DbInfo ninfo = db264_info(mbs, slices, mbw, 0, wv);
+    db264_fetch<Pel>(PY, PC, sty, stc, 0, rbeg + wv, pf, lane);
+    DbInfo ninfo = db264_info(mbs, slices, mbw, 0, rbeg + wv);
     int lmf = 0, lqp = 0, lsaddr = -1;  // left neighbour (previous MB of the row)
-    for (int row = wv; row < mbh; row += kAvcDbWaves) {
+    for (int row = rbeg + wv; row < rend; row += kAvcDbWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
+        const bool from_band = nbands > 1 && band > 0 && row == rbeg;
+        const bool to_band = nbands > 1 && band < nbands - 1 && row == rend - 1;
+        const uint64_t o_xin = o_xl + 12ull * (band - 1) * width, o_xout = o_xl + 12ull * band * width;
+        // stores of a boundary row go through to the coherence point (the band below writes the
+        // same bottom rows once its top edges are filtered, possibly from another XCD)
+        auto put = [&](Pel* p, Pel v) {
+            if (to_band) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else *p = v;
+        };
         for (int mx = 0; mx < mbw; mx++) {
-            if (row > 0) {
+            if (from_band) {
+                const uint32_t need = static_cast<uint32_t>(mbw + min(mx + 2, mbw));
+                if (seen < need) {
+                    uint32_t it = 0;
+                    uint32_t* fl = reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * ((row - 1) * mbw);
+                    while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
+                            uint32_t* err = reinterpret_cast<uint32_t*>(arena + ufl64(f.jstat) + offsetof(h2j_jstat, dev_error));
+                            if (lane == 0) __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            seen = 2u * mbw;
+                            break;
+                        }
+                    }
+                }
+            } else if (row > rbeg || (row > 0 && nbands <= 1)) {
                 const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
                 if (seen < need) {
                     while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
@@ -1802,7 +1832,16 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                 const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
                 w.c[c][rr + 2][c2 + 2] = pf.c[0];
                 w.c[c][rr + 2][c2 + 3] = pf.c[1];
-                if (row > 0) {
+                if (from_band) {
+                    const uint16_t* X = reinterpret_cast<const uint16_t*>(arena + o_xin);
+                    const int tr = lane >> 4, tc = lane & 15;
+                    w.y[tr][tc + 4] = __hip_atomic_load(X + tr * width + mx * 16 + tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane < 32) {
+                        const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
+                        w.c[cc][cr][ck + 2] = __hip_atomic_load(X + 4 * width + (cc * 2 + cr) * cw + mx * 8 + ck,
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else if (row > 0) {
                     const int tr = lane >> 4, tc = lane & 15;  // 4 rows x 16 luma columns
                     w.y[tr][tc + 4] = LY[tr * width + mx * 16 + tc];
                     if (lane < 32) {  // 2 comps x 2 rows x 8 columns
@@ -1884,18 +1923,18 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                 const int r = lane >> 2, c4 = (lane & 3) * 4;
                 Pel* d = PY + (row * 16 + r) * sty + mx * 16 + c4;
 #pragma unroll
-                for (int k = 0; k < 4; k++) d[k] = static_cast<Pel>(w.y[r + 4][c4 + k + 4]);
+                for (int k = 0; k < 4; k++) put(d + k, static_cast<Pel>(w.y[r + 4][c4 + k + 4]));
                 const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
                 Pel* e = PC[c] + (row * 8 + rr) * stc + mx * 8 + c2;
-                e[0] = static_cast<Pel>(w.c[c][rr + 2][c2 + 2]);
-                e[1] = static_cast<Pel>(w.c[c][rr + 2][c2 + 3]);
+                put(e, static_cast<Pel>(w.c[c][rr + 2][c2 + 2]));
+                put(e + 1, static_cast<Pel>(w.c[c][rr + 2][c2 + 3]));
                 if (active && mx > 0) {
                     if (lane < 48) {  // luma columns -3..-1, rows 0..15
                         const int lr = lane / 3, lc = lane - lr * 3 + 1;
-                        PY[(row * 16 + lr) * sty + mx * 16 + lc - 4] = static_cast<Pel>(w.y[lr + 4][lc]);
+                        put(PY + (row * 16 + lr) * sty + mx * 16 + lc - 4, static_cast<Pel>(w.y[lr + 4][lc]));
                     } else {  // chroma column -1, rows 0..7, both comps
                         const int cc = (lane - 48) >> 3, cr = lane & 7;
-                        PC[cc][(row * 8 + cr) * stc + mx * 8 - 1] = static_cast<Pel>(w.c[cc][cr + 2][1]);
+                        put(PC[cc] + (row * 8 + cr) * stc + mx * 8 - 1, static_cast<Pel>(w.c[cc][cr + 2][1]));
                     }
                 }
                 if (active && row > 0) {
@@ -1910,7 +1949,29 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
             }
             // line buffer for the row below: the MB's bottom rows (columns final so far) and
             // the previous MB's last columns, which this MB's left edge has just finished
-            if (row + 1 < mbh) {
+            if (to_band) {  // the same, into the boundary buffer of the band below
+                uint16_t* X = reinterpret_cast<uint16_t*>(arena + o_xout);
+                const bool last = mx == mbw - 1;
+                const int tr = lane >> 4, tc = lane & 15;
+                if (tc < 12 || last)
+                    __hip_atomic_store(X + tr * width + mx * 16 + tc, w.y[tr + 16][tc + 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (mx > 0 && tc < 4)
+                    __hip_atomic_store(X + tr * width + mx * 16 - 4 + tc, w.y[tr + 16][tc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane < 32) {
+                    const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
+                    uint16_t* XC = X + 4 * width + (cc * 2 + cr) * cw + mx * 8;
+                    if (ck < 6 || last)
+                        __hip_atomic_store(XC + ck, w.c[cc][cr + 8][ck + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (mx > 0 && ck < 2)
+                        __hip_atomic_store(XC - 2 + ck, w.c[cc][cr + 8][ck], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): picture and boundary stores have completed
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0)
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * (row * mbw),
+                                       static_cast<uint32_t>(mbw + mx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (row + 1 < mbh) {
                 const bool last = mx == mbw - 1;
                 const int tr = lane >> 4, tc = lane & 15;  // rows 12..15 of this MB
                 if (tc < 12 || last) LY[tr * width + mx * 16 + tc] = w.y[tr + 16][tc + 4];
@@ -1944,19 +2005,23 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
 }
 
 __global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
-                                                                    const h2j_slice* slices, uint8_t* arena) {
+                                                                    const h2j_slice* slices, uint8_t* arena,
+                                                                    const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t dblds[];
     DbWin* W = reinterpret_cast<DbWin*>(dblds);
     uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * kAvcDbWaves);
     uint16_t* line = reinterpret_cast<uint16_t*>(dblds + sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4);
-    const h2j_frame& f = frames[blockIdx.x];
+    const uint32_t me = map[blockIdx.x];  // same (picture, band) map as K1
+    const h2j_frame& f = frames[me >> 8];
+    const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264) return;
+    const int nbands = ufl(f.k1bands);
     if (threadIdx.x < 2 * kAvcDbWaves) prog[threadIdx.x] = 0;
     __syncthreads();
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line);
-    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line);
+    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line, band, nbands);
+    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line, band, nbands);
 }
 
 // ---------------------------------------------------------------- K3: SAO
@@ -2331,7 +2396,23 @@ void* h2j_gpu_stream_create(void) {
     return s;
 }
 int h2j_gpu_stream_destroy(void* s) { return check(hipStreamDestroy(static_cast<hipStream_t>(s)), "hipStreamDestroy"); }
-int h2j_gpu_stream_sync(void* s) { return check(hipStreamSynchronize(static_cast<hipStream_t>(s)), "hipStreamSynchronize"); }
+// hipStreamSynchronize (HIP yields while it waits: the host CPU use of the bench is the
+// same as with blocking waits).  H2J_SYNC=block waits on a blocking-sync event instead.
+int h2j_gpu_stream_sync(void* s) {
+    static const bool spin = [] {
+        const char* e = std::getenv("H2J_SYNC");
+        return !(e && std::strcmp(e, "block") == 0);
+    }();
+    hipStream_t st = static_cast<hipStream_t>(s);
+    if (spin) return check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    hipEvent_t ev = nullptr;
+    int r = check(hipEventCreateWithFlags(&ev, hipEventBlockingSync | hipEventDisableTiming), "hipEventCreateWithFlags");
+    if (r) return r;
+    r = check(hipEventRecord(ev, st), "hipEventRecord");
+    if (!r) r = check(hipEventSynchronize(ev), "hipEventSynchronize");
+    (void)hipEventDestroy(ev);
+    return r;
+}
 int h2j_gpu_memcpy_h2d(void* dst, const void* src, size_t n, void* s) {
     return check(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, static_cast<hipStream_t>(s)), "hipMemcpyH2D");
 }
@@ -2461,8 +2542,9 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->nframes), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
-                       b->slices, b->arena);
+    if (b->k1wgs <= 0) return 0;
+    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->k1wgs), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
+                       b->slices, b->arena, b->k1map);
     return check(hipGetLastError(), "h2j_k2_deblock264");
 }
 

@@ -311,9 +311,9 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         off = align_up(off + (ysz + ysz / 2) * 2, 256);
         f.aux = off;
         off = align_up(off + static_cast<size_t>(f.ntu) * 8, 256);
-        if (f.k1bands > 1) {  // one luma + two chroma bottom rows (uint16) per band boundary
+        if (f.k1bands > 1) {  // per band boundary: K1 1 luma + 2 chroma rows, K2 4 luma + 2x2 chroma rows (uint16)
             f.xline = off;
-            off = align_up(off + static_cast<size_t>(f.k1bands - 1) * 2 * f.width * 2, 256);
+            off = align_up(off + static_cast<size_t>(f.k1bands - 1) * 6 * f.width * 2, 256);
         }
     }
     const size_t arena_bytes = off;
