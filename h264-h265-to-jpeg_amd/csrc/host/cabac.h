@@ -5,6 +5,13 @@
 
 namespace h2j {
 
+#ifdef H2J_CABAC_COUNT  // diagnostics (tools/parse_bench): bins decoded by this thread
+extern thread_local unsigned long long g_bins_ctx, g_bins_byp;
+#define H2J_COUNT(v, n) (v += (n))
+#else
+#define H2J_COUNT(v, n) ((void)0)
+#endif
+
 extern const uint8_t kCabacLps[64][4];
 extern const uint8_t kCabacTransLps[64];
 extern const uint8_t kCabacRenorm[32];
@@ -42,6 +49,7 @@ public:
         bits_ = 32 - 9;
     }
     inline int decision(uint16_t& ctx) {
+        H2J_COUNT(g_bins_ctx, 1);
         const unsigned st = ctx;
         const uint32_t lps = kCabacLps[st >> 1][(range_ >> 6) & 3];
         const uint32_t rmps = range_ - lps;
@@ -57,6 +65,7 @@ public:
         return static_cast<int>(st & 1) ^ static_cast<int>(is_lps);
     }
     inline int bypass() {
+        H2J_COUNT(g_bins_byp, 1);
         if (--bits_ < 0) refill();
         const uint64_t scaled = static_cast<uint64_t>(range_) << bits_;
         const bool one = value_ >= scaled;
@@ -68,6 +77,7 @@ public:
     // per bin, by the range: the bins are the k-bit quotient, the new offset the
     // remainder.
     inline uint32_t bypass_batch(int k) {
+        H2J_COUNT(g_bins_byp, k);
         if (bits_ < k) refill();
         const int sh = bits_ - k;
         const uint64_t v = value_ >> sh;

@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <deque>
@@ -93,11 +94,17 @@ void run_batch(h2j_engine* e, std::vector<Request*>& batch) {
     }
 }
 
-// transcode one picture through the shared, batching engine
-bool transcode_shared(Request& req) {
+// transcode pictures through the shared, batching engine (all of `reqs` join the same queue,
+// so a caller's own batch runs as one engine batch together with whatever else is queued)
+void transcode_shared_many(const std::vector<Request*>& reqs) {
     std::unique_lock<std::mutex> lk(g_mu);
-    g_queue.push_back(&req);
-    while (!req.done) {
+    for (Request* r : reqs) g_queue.push_back(r);
+    auto all_done = [&] {
+        for (Request* r : reqs)
+            if (!r->done) return false;
+        return true;
+    };
+    while (!all_done()) {
         if (g_busy) {
             g_cv.wait(lk);
             continue;
@@ -121,6 +128,10 @@ bool transcode_shared(Request& req) {
         g_busy = false;
         g_cv.notify_all();
     }
+}
+
+bool transcode_shared(Request& req) {
+    transcode_shared_many(std::vector<Request*>{&req});
     return req.status == 0;
 }
 
@@ -180,3 +191,74 @@ bool Decoder::H265ToJpeg(const char* const in, const char* const out) {
 }  // namespace
 
 std::shared_ptr<IDecoder> IDecoder::getInstance() { return std::make_shared<Decoder>(); }
+
+// ---- in-memory and batch entry points beside IDecoder
+
+extern "C" int h2j_h265_to_jpeg_mem(const uint8_t* data, size_t size, uint8_t** jpeg, size_t* jpeg_len) {
+    if (!jpeg || !jpeg_len) return -1;
+    *jpeg = nullptr;
+    *jpeg_len = 0;
+    if (!data || size == 0) return -1;
+    Request req;
+    req.data = data;
+    req.size = size;
+    if (!transcode_shared(req)) {
+        LOG("transcode failed (%d): %s", req.status, req.error.c_str());
+        return req.status ? req.status : -1;
+    }
+    uint8_t* p = static_cast<uint8_t*>(malloc(req.jpeg.size()));
+    if (!p) return -1;
+    std::memcpy(p, req.jpeg.data(), req.jpeg.size());
+    *jpeg = p;
+    *jpeg_len = req.jpeg.size();
+    return 0;
+}
+
+extern "C" void h2j_free(void* p) { free(p); }
+
+extern "C" int h2j_h265_to_jpeg_batch(const char* const* in_paths, const char* const* out_paths, int n, int* ok) {
+    if (n <= 0 || !in_paths || !out_paths) return 0;
+    std::vector<std::vector<uint8_t>> data(static_cast<size_t>(n));
+    std::vector<Request> reqs(static_cast<size_t>(n));
+    std::vector<Request*> live;
+    for (int i = 0; i < n; i++) {
+        if (ok) ok[i] = 0;
+        const char* in = in_paths[i];
+        const char* out = out_paths[i];
+        if (!in || !out || !*in || !*out) {
+            LOG("input or output path is empty: input:%s, output:%s", in ? in : "(null)", out ? out : "(null)");
+            continue;
+        }
+        if (!read_file(in, data[i])) {
+            LOG("cannot open input file: %s", in);
+            continue;
+        }
+        reqs[i].data = data[i].data();
+        reqs[i].size = data[i].size();
+        live.push_back(&reqs[i]);
+    }
+    if (!live.empty()) transcode_shared_many(live);
+    int good = 0;
+    for (int i = 0; i < n; i++) {
+        const Request& q = reqs[i];
+        if (!q.done) continue;
+        if (q.status != 0) {
+            LOG("transcode failed (%d) for %s: %s", q.status, in_paths[i], q.error.c_str());
+            continue;
+        }
+        FILE* f = fopen(out_paths[i], "wb+");
+        if (!f) {
+            LOG("failed to encode Yuv to Jpeg: cannot open %s", out_paths[i]);
+            continue;
+        }
+        const size_t w = fwrite(q.jpeg.data(), 1, q.jpeg.size(), f);
+        fclose(f);
+        if (w != q.jpeg.size()) {
+            LOG("failed to write Jpeg file %s", out_paths[i]);
+            continue;
+        }
+        if (ok) ok[i] = 1;
+        good++;
+    }
+    return good;
+}

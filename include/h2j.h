@@ -54,6 +54,20 @@ int h2j_engine_jpeg_coeffs(h2j_engine *e, const uint8_t *data, size_t size, int1
  * [9] frames  [10] algorithmic bytes of the GPU pixel path. */
 int h2j_engine_stats(h2j_engine *e, double *out, int n);
 
+/* In-memory and batch entry points beside IDecoder (the reference has only the
+ * file-path call, /root/reference/export_inc/IDecoder.h:29).
+ * Both go through the same process-wide batching engine as IDecoder, so
+ * concurrent callers share GPU batches.
+ * h2j_h265_to_jpeg_mem: one Annex-B still (H.264 or H.265) -> JPEG bytes in
+ *   *jpeg (malloc'ed, release with h2j_free), 0 on success, < 0 on failure.
+ * h2j_h265_to_jpeg_batch: n (input, output) file pairs transcoded as one
+ *   batch; ok[i] = 1 where output i was written (may be NULL); returns the
+ *   number written.  Per-file behaviour (empty paths, unreadable input, LOG
+ *   lines) is that of IDecoder::H265ToJpeg. */
+int h2j_h265_to_jpeg_mem(const uint8_t *data, size_t size, uint8_t **jpeg, size_t *jpeg_len);
+int h2j_h265_to_jpeg_batch(const char *const *in_paths, const char *const *out_paths, int n, int *ok);
+void h2j_free(void *p);
+
 /* Library self-description (version, arch, build). */
 const char *h2j_version(void);
 

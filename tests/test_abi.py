@@ -44,6 +44,9 @@ def test_host_abi_exports(built):
     # reference C++ / JNI surface
     assert "_ZN8IDecoder11getInstanceEv" in ex
     assert "Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decode" in ex
+    # in-memory / batch JNI variants beside it
+    assert "Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBytes" in ex
+    assert "Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBatch" in ex
 
 
 def test_library_loads(built):

@@ -120,3 +120,116 @@ def test_jni_export_with_stub_env(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     import oracle_py as O
     assert out.read_bytes() == O.transcode(read(golden("img01.h265")))
+
+
+MEM_BATCH_DRIVER = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "h2j.h"
+/* argv: in265 in264 outdir -> mem transcode of in265 to outdir/m.jpg, batch of
+ * (in265, in264, missing, "") to outdir/b0..b3.jpg */
+int main(int argc, char** argv) {
+    FILE* f = fopen(argv[1], "rb");
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    rewind(f);
+    unsigned char* d = (unsigned char*)malloc(n);
+    if (fread(d, 1, n, f) != (size_t)n) return 5;
+    fclose(f);
+    unsigned char* jpeg = 0;
+    size_t len = 0;
+    if (h2j_h265_to_jpeg_mem(d, n, &jpeg, &len) != 0 || !jpeg) return 2;
+    char p[4096];
+    snprintf(p, sizeof p, "%s/m.jpg", argv[3]);
+    f = fopen(p, "wb");
+    fwrite(jpeg, 1, len, f);
+    fclose(f);
+    h2j_free(jpeg);
+    if (h2j_h265_to_jpeg_mem(d, 16, &jpeg, &len) == 0 || jpeg) return 3; /* truncated input fails */
+    const char* in[4] = {argv[1], argv[2], "/nonexistent/x.h265", ""};
+    char outs[4][4096];
+    const char* out[4];
+    for (int i = 0; i < 4; i++) { snprintf(outs[i], sizeof outs[i], "%s/b%d.jpg", argv[3], i); out[i] = outs[i]; }
+    int ok[4] = {9, 9, 9, 9};
+    int good = h2j_h265_to_jpeg_batch(in, out, 4, ok);
+    printf("good=%d ok=%d%d%d%d\n", good, ok[0], ok[1], ok[2], ok[3]);
+    return good == 2 && ok[0] == 1 && ok[1] == 1 && ok[2] == 0 && ok[3] == 0 ? 0 : 4;
+}
+'''
+
+
+def test_mem_and_batch_entry_points(tmp_path):
+    src = tmp_path / "mb.c"
+    src.write_text(MEM_BATCH_DRIVER)
+    exe = tmp_path / "mb"
+    subprocess.check_call(["gcc", "-O1", str(src), "-I", os.path.join(ROOT, "include"), "-L", PKG, "-lH265ToJpeg",
+                           f"-Wl,-rpath,{PKG}", "-o", str(exe)])
+    r = subprocess.run([str(exe), golden("img01.h265"), golden("img01.h264"), str(tmp_path)], capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    import oracle_py as O
+    w265 = O.transcode(read(golden("img01.h265")))
+    assert (tmp_path / "m.jpg").read_bytes() == w265
+    assert (tmp_path / "b0.jpg").read_bytes() == w265
+    assert (tmp_path / "b1.jpg").read_bytes() == O.transcode(read(golden("img01.h264")))
+    assert not (tmp_path / "b2.jpg").exists() and not (tmp_path / "b3.jpg").exists()
+
+
+JNI_ARRAYS_DRIVER = r'''
+/* decodeBytes / decodeBatch driven through a stub JNIEnv: a jbyteArray is a
+ * {len, bytes} struct, a String[] a {len, char**} struct, a boolean[] a
+ * {len, bytes} struct (JNINativeInterface_ slots 169-176, 200, 207, 208). */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+typedef unsigned char jboolean;
+typedef struct { int len; unsigned char* b; } Arr;
+typedef struct { int len; const char** s; } SArr;
+static const char* get_utf(void* e, void* s, jboolean* c) { (void)e; if (c) *c = 0; return (const char*)s; }
+static void rel_utf(void* e, void* s, const char* c) { (void)e; (void)s; (void)c; }
+static int arr_len(void* e, void* a) { (void)e; return ((Arr*)a)->len; }
+static void* obj_elem(void* e, void* a, int i) { (void)e; return (void*)((SArr*)a)->s[i]; }
+static void* new_arr(void* e, int n) { (void)e; Arr* a = malloc(sizeof(Arr)); a->len = n; a->b = calloc(n + 1, 1); return a; }
+static void get_region(void* e, void* a, int s, int n, signed char* d) { (void)e; memcpy(d, ((Arr*)a)->b + s, n); }
+static void set_region(void* e, void* a, int s, int n, const void* d) { (void)e; memcpy(((Arr*)a)->b + s, d, n); }
+extern void* Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBytes(void*, void*, void*);
+extern void* Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBatch(void*, void*, void*, void*);
+int main(int argc, char** argv) {
+    void* table[232];
+    memset(table, 0, sizeof(table));
+    table[169] = (void*)get_utf; table[170] = (void*)rel_utf; table[171] = (void*)arr_len;
+    table[173] = (void*)obj_elem; table[175] = (void*)new_arr; table[176] = (void*)new_arr;
+    table[200] = (void*)get_region; table[207] = (void*)set_region; table[208] = (void*)set_region;
+    void** env = table;
+    FILE* f = fopen(argv[1], "rb");
+    fseek(f, 0, SEEK_END);
+    Arr in; in.len = (int)ftell(f); rewind(f); in.b = malloc(in.len);
+    if (fread(in.b, 1, in.len, f) != (size_t)in.len) return 5;
+    fclose(f);
+    Arr* out = Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBytes(&env, 0, &in);
+    if (!out) return 2;
+    f = fopen(argv[3], "wb"); fwrite(out->b, 1, out->len, f); fclose(f);
+    const char* ins[2] = {argv[1], "/nonexistent.h265"};
+    const char* outs[2] = {argv[4], argv[5]};
+    SArr si = {2, ins}, so = {2, outs};
+    Arr* ok = Java_com_autonavi_socol_occtiltedserver_service_H265DecodeService_decodeBatch(&env, 0, &si, &so);
+    if (!ok || ok->len != 2) return 3;
+    printf("ok=%d%d\n", ok->b[0], ok->b[1]);
+    return ok->b[0] == 1 && ok->b[1] == 0 ? 0 : 4;
+}
+'''
+
+
+def test_jni_bytes_and_batch_with_stub_env(tmp_path):
+    src = tmp_path / "jarr.c"
+    src.write_text(JNI_ARRAYS_DRIVER)
+    exe = tmp_path / "jarr"
+    subprocess.check_call(["gcc", "-O1", str(src), "-L", PKG, "-lH265ToJpeg", f"-Wl,-rpath,{PKG}", "-o", str(exe)])
+    o1, o2, o3 = tmp_path / "bytes.jpg", tmp_path / "batch0.jpg", tmp_path / "batch1.jpg"
+    r = subprocess.run([str(exe), golden("img01.h264"), "unused", str(o1), str(o2), str(o3)], capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    import oracle_py as O
+    want = O.transcode(read(golden("img01.h264")))
+    assert o1.read_bytes() == want and o2.read_bytes() == want and not o3.exists()

@@ -13,7 +13,14 @@
 #include <vector>
 
 #include "bitstream.h"
+#include "cabac.h"
 #include "job.h"
+
+#ifdef H2J_CABAC_COUNT
+namespace h2j {
+thread_local unsigned long long g_bins_ctx = 0, g_bins_byp = 0;
+}
+#endif
 
 int main(int argc, char** argv) {
     if (argc < 2) {
@@ -49,6 +56,7 @@ int main(int argc, char** argv) {
     const int total = reps * static_cast<int>(streams.size());
     std::atomic<int> next(0), failed(0);
     std::atomic<size_t> tus(0), coefs(0), bytes(0);
+    std::atomic<unsigned long long> bins_ctx(0), bins_byp(0);
     std::atomic<unsigned long long> digest(0);  // order-independent checksum of all parse outputs
     auto worker = [&]() {
         h2j::FrameJob job;
@@ -80,6 +88,10 @@ int main(int argc, char** argv) {
         tus += t;
         coefs += c;
         bytes += b;
+#ifdef H2J_CABAC_COUNT
+        bins_ctx += h2j::g_bins_ctx;
+        bins_byp += h2j::g_bins_byp;
+#endif
     };
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
@@ -91,5 +103,8 @@ int main(int argc, char** argv) {
     std::printf("%d thr: %.3f ms/frame wall, %.3f ms/frame/thread  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s  digest %016llx\n",
                 threads, ms / nf, ms * threads / nf, tus / nf, coefs / nf, bytes / (ms / 1e3) / 1e6,
                 static_cast<unsigned long long>(digest));
+    if (bins_ctx + bins_byp)
+        std::printf("bins/frame: %.0f context-coded, %.0f bypass; %.2f ns per bin\n", bins_ctx / nf, bins_byp / nf,
+                    ms * 1e6 * threads / static_cast<double>(bins_ctx + bins_byp));
     return 0;
 }
