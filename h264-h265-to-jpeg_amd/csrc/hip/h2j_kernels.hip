@@ -1032,7 +1032,7 @@ struct QComp {              // one component's carried neighbours (quadrant size
     int16_t corner, pad;    // top-left sample of the next CTB
 };
 struct QWave {
-    int16_t body[32 * 32];  // luma quadrant | Cb at 0 and Cr at 256 (16x16 each)
+    int16_t body[2][32 * 32];  // quadrant windows (ping-pong): luma | Cb at 0 and Cr at 256 (16x16 each)
     QComp cs[2];            // luma: cs[0]; chroma: Cb cs[0], Cr cs[1]
     K1WaveLds k;
 };
@@ -1210,9 +1210,31 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     wave_sync();
 }
 
-// K0 residual of one quadrant -> registers.  Luma: 2 x 16 B chunks per lane
-// (32x32 int16); chroma: one 8 B chunk of Cb in .xy and of Cr in .zw.
-DEVI void hevc_qres_fetch(const FU& u, int grp, int X0, int Y0, int Qc, uint4 (&r)[2], int lane) {
+// Asynchronous global -> LDS copies (LDS-DMA): lane i's bytes land at lds + i * size, with no
+// VGPR destination.  M0 carries the wave-uniform LDS byte address (set and restored inside the
+// statement, the compiler reserves M0).  Issued as asm, so the compiler does not track them:
+// every use of the data waits vmcnt(0) explicitly (lds_dma_wait).
+DEVI void lds_dma16(const void* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+DEVI void lds_dma4(const void* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+DEVI void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+DEVI void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+DEVI uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
+}
+
+// K0 residual of one quadrant -> a quadrant window in LDS by LDS-DMA (no registers held while
+// it is in flight; the register prefetch it replaces spilled to scratch at this kernel's VGPR
+// budget).  Luma: 2 x 16 B per lane, row-major Qc x Qc; chroma: 4 B per lane, Cb at element 0
+// and Cr at 256, Qc x Qc each.  Lanes outside the picture write zeros instead.
+DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* body, int lane) {
     if (grp == 0) {
         const int16_t* R = u.rplane(0);
         const int cpr = Qc >> 3;
@@ -1220,28 +1242,18 @@ DEVI void hevc_qres_fetch(const FU& u, int grp, int X0, int Y0, int Qc, uint4 (&
         for (int j = 0; j < 2; j++) {
             const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 8;
             const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
-            const uint4 v = *reinterpret_cast<const uint4*>(R + (ok ? (Y0 + yy) * u.sty + X0 + xx : 0));
-            r[j] = ok ? v : make_uint4(0, 0, 0, 0);
+            if (ok) lds_dma16(R + (Y0 + yy) * u.sty + X0 + xx, lds_addr(body + 512 * j));
+            else *reinterpret_cast<uint4*>(body + idx * 8) = make_uint4(0, 0, 0, 0);
         }
     } else {
-        const int cpr = Qc >> 2, yy = lane / cpr, xx = (lane - yy * cpr) * 4;
-        const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
-        const int o = ok ? (Y0 + yy) * u.stc + X0 + xx : 0;
-        const uint2 b = *reinterpret_cast<const uint2*>(u.rplane(1) + o);
-        const uint2 c = *reinterpret_cast<const uint2*>(u.rplane(2) + o);
-        r[0] = ok ? make_uint4(b.x, b.y, c.x, c.y) : make_uint4(0, 0, 0, 0);
-    }
-}
-DEVI void hevc_qres_put(int grp, int Qc, const uint4 (&r)[2], int16_t* body, int lane) {
-    if (grp == 0) {
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int idx = lane + 64 * j;
-            if (idx < Qc * (Qc >> 3)) *reinterpret_cast<uint4*>(body + idx * 8) = r[j];
+        for (int k = 0; k < 4; k++) {  // (plane, half): 64 lanes x 2 samples
+            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e / Qc, xx = e - yy * Qc;
+            const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
+            int16_t* dst = body + c * 256 + (k & 1) * 128;
+            if (ok) lds_dma4(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx, lds_addr(dst));
+            else *reinterpret_cast<uint32_t*>(dst + lane * 2) = 0u;
         }
-    } else if (lane < Qc * (Qc >> 2)) {
-        *reinterpret_cast<uint2*>(body + lane * 4) = make_uint2(r[0].x, r[0].y);
-        *reinterpret_cast<uint2*>(body + 256 + lane * 4) = make_uint2(r[0].z, r[0].w);
     }
 }
 
@@ -1277,8 +1289,9 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
             }
         } while (row < u.ctb_h && !q_inside(row, cx, q));
     };
-    uint4 res[2];
-    hevc_qres_fetch(u, grp, 0, wv * Sc, Qc, res, lane);
+    int cur = 0;  // quadrant window in use (the other one is being filled for the next quadrant)
+    hevc_qres_dma(u, grp, 0, wv * Sc, Qc, w.body[0], lane);
+    lds_dma_wait();
     // this group's record range of a CTB: luma [first, first chroma), chroma [first chroma, end)
     auto grange = [&](int cbi, uint32_t& ra, uint32_t& rb) {
         const uint4 r = reinterpret_cast<const uint4*>(rng)[cbi];
@@ -1365,12 +1378,13 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                         }
                     }
                 }
-                hevc_qres_put(grp, Qc, res, w.body, lane);
-                {  // prefetch the next quadrant's residual
+                {  // prefetch the next quadrant's residual into the other window (its last reader,
+                   // the previous quadrant's store, has finished reading it)
                     int nr = row, nc = cx, nq = q;
                     q_next(nr, nc, nq);
+                    lds_reads_done();
                     if (nr < u.ctb_h)
-                        hevc_qres_fetch(u, grp, nc * Sc + (nq & 1) * Qc, nr * Sc + (nq >> 1) * Qc, Qc, res, lane);
+                        hevc_qres_dma(u, grp, nc * Sc + (nq & 1) * Qc, nr * Sc + (nq >> 1) * Qc, Qc, w.body[cur ^ 1], lane);
                 }
                 wave_sync();
                 PROF_LAP(1);
@@ -1387,7 +1401,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     const int ox = tu.x - X0, oy = tu.y - Y0;
                     if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
                     const int ci = c == 2 ? 1 : 0;
-                    int16_t* body = w.body + ci * 256;
+                    int16_t* body = w.body[cur] + ci * 256;
                     if (tu.flags & H2J_TU_PCM) {  // samples written by K0: pull that block into the window
                         const int n = 1 << tu.log2n;
                         const Pel* P = u.plane<Pel>(c);
@@ -1407,12 +1421,14 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
                     t++;
                 }
-                // store the quadrant and update the carries
+                // store the quadrant and update the carries; the next quadrant's window has
+                // landed by now (issued a whole quadrant ago), retire it before the stores
+                lds_dma_wait();
                 const int wq = min(Qc, Wc - X0), hq = min(Qc, Hc - Y0);
                 for (int ci = 0; ci < ncomp; ci++) {
                     const int c = grp ? ci + 1 : 0;
                     QComp& C = w.cs[ci];
-                    const int16_t* body = w.body + ci * 256;
+                    const int16_t* body = w.body[cur] + ci * 256;
                     Pel* P = u.plane<Pel>(c);
                     const int st = u.st(c);
                     const int qn = wq >> 2;  // 4 samples per lane step (component widths are multiples of 4)
@@ -1439,6 +1455,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     }
                 }
                 wave_sync();
+                cur ^= 1;
                 PROF_LAP(3);
             }
             PROF_ADD(6, 1);

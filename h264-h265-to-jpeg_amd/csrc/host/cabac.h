@@ -18,6 +18,10 @@ extern const uint8_t kCabacRenorm[32];
 // next context state ((pStateIdx << 1) | valMps) after an MPS / LPS bin
 extern const uint16_t kCabacNextMps[128];
 extern const uint16_t kCabacNextLps[128];
+// the same, merged for branch-free decoding: [(state << 1) | bin_was_lps]
+extern const uint16_t kCabacNext[256];
+// rangeTabLps by (state, range >> 6): [(pStateIdx << 1) | valMps][8], columns 4..7 used
+extern const uint8_t kCabacLpsByState[128][8];
 
 struct CabacCtx {
     uint8_t state;  // (pStateIdx << 1) | valMps
@@ -51,7 +55,7 @@ public:
     inline int decision(uint16_t& ctx) {
         H2J_COUNT(g_bins_ctx, 1);
         const unsigned st = ctx;
-        const uint32_t lps = kCabacLps[st >> 1][(range_ >> 6) & 3];
+        const uint32_t lps = kCabacLpsByState[st][range_ >> 6];
         const uint32_t rmps = range_ - lps;
         const uint64_t scaled = static_cast<uint64_t>(rmps) << bits_;
         const bool is_lps = value_ >= scaled;
@@ -63,6 +67,26 @@ public:
         bits_ -= sh;
         if (bits_ < 0) refill();
         return static_cast<int>(st & 1) ^ static_cast<int>(is_lps);
+    }
+    // The same with the MPS/LPS outcome as a mask, never a branch.  For contexts near 50 %
+    // (significance flags) a branch mispredicts on every other bin; for skewed contexts the
+    // predicted branch is faster (the next bin starts speculatively), so decision() keeps it.
+    inline int decision_bf(uint16_t& ctx) {
+        H2J_COUNT(g_bins_ctx, 1);
+        const unsigned st = ctx;
+        const uint32_t lps = kCabacLpsByState[st][range_ >> 6];
+        const uint32_t rmps = range_ - lps;
+        const uint64_t scaled = static_cast<uint64_t>(rmps) << bits_;
+        const uint32_t is_lps = value_ >= scaled ? 1u : 0u;
+        const uint64_t m = 0 - static_cast<uint64_t>(is_lps);
+        value_ -= scaled & m;
+        const uint32_t r = rmps ^ ((rmps ^ lps) & static_cast<uint32_t>(m));
+        ctx = kCabacNext[(st << 1) | is_lps];
+        const int sh = __builtin_clz(r) - 23;
+        range_ = r << sh;
+        bits_ -= sh;
+        if (bits_ < 0) refill();
+        return static_cast<int>((st & 1) ^ is_lps);
     }
     inline int bypass() {
         H2J_COUNT(g_bins_byp, 1);

@@ -842,11 +842,11 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             if (xs + 1 < sbw) prevCsbf |= csbf[xs + 1][ys];
             if (ys + 1 < sbw) prevCsbf |= csbf[xs][ys + 1] << 1;
             const uint8_t* sig = sigtab[prevCsbf][(xs | ys) ? 1 : 0];
-            for (int nn = nstart; nn > 0; nn--)
-                if (cc.decision(ctx[sig[nn]])) {
-                    sigmask |= 1u << nn;
-                    infer_dc = false;
-                }
+            // bins feed the mask arithmetically (no data-dependent branch per bin)
+            unsigned got = 0;
+            for (int nn = nstart; nn > 0; nn--) got |= static_cast<unsigned>(cc.decision_bf(ctx[sig[nn]])) << nn;
+            sigmask |= got;
+            infer_dc = infer_dc && got == 0;
             if (nstart >= 0) {
                 if (!infer_dc) {
                     if (cc.decision(ctx[sig[0]])) sigmask |= 1u;
@@ -863,17 +863,17 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         unsigned g1mask = 0;
         int numG1 = 0, lastG1 = -1;
         const int lastSig = 31 - __builtin_clz(sigmask), firstSig = __builtin_ctz(sigmask);
+        uint16_t* const g1c = gt1ctx + ctxSet * 4;
         for (unsigned m = sigmask; m && numG1 < 8; numG1++) {
             const int nn = 31 - __builtin_clz(m);
             m &= ~(1u << nn);
-            if (cc.decision(gt1ctx[ctxSet * 4 + greater1_ctx])) {
-                g1mask |= 1u << nn;
-                greater1_ctx = 0;
-                if (lastG1 == -1) lastG1 = nn;
-            } else if (greater1_ctx > 0 && greater1_ctx < 3) {
-                greater1_ctx++;
-            }
+            const unsigned d = static_cast<unsigned>(cc.decision(g1c[greater1_ctx]));
+            g1mask |= d << nn;
+            // greater1Ctx: 0 once a bin was 1, else 1 -> 2 -> 3 (saturating), as a mask select
+            const int inc = greater1_ctx + ((greater1_ctx > 0) & (greater1_ctx < 3));
+            greater1_ctx = inc & (static_cast<int>(d) - 1);
         }
+        if (g1mask) lastG1 = 31 - __builtin_clz(g1mask);
         const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
         int g2 = 0;
         if (lastG1 != -1) g2 = cc.decision(ctx[C_GT2 + ctxSet + (c ? 4 : 0)]);

@@ -23,7 +23,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "hevc1080"
-k1_base = "h2j_k1_recon_h264" if workload.startswith("avc") else "h2j_k1_recon_hevc"
+k1_base = {"avc1080": "h2j_k1_recon_h264", "mixed": "h2j_k1_recon_"}.get(workload, "h2j_k1_recon_hevc")
+
+
+def k1_group(k):  # dispatches of one group happen once per chunk (width variants alternate)
+    return "h264" if "h264" in k else ("hevc_u16" if "unsigned short" in k else "hevc_u8")
 out = os.path.join(ROOT, "gpurun_out")
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -61,20 +65,20 @@ for r in stats:
                  f"{fa if fa is None else round(fa)} | {wa if wa is None else round(wa)} | "
                  f"{hbm if hbm is None else round(hbm, 3)} |")
     if k.startswith(k1_base):
-        pel = "u16" if "unsigned short" in k else "u8"
+        pel = k1_group(k)
         k1_time_ns += float(r["TotalDurationNs"])
         k1_calls_by_pel[pel] += int(r["Calls"])
         k1_time_by_pel[pel] += float(r["TotalDurationNs"])
 if k1_calls_by_pel:
-    main_pel = max(k1_time_by_pel, key=k1_time_by_pel.get)
+    main_pel = max(k1_calls_by_pel, key=k1_calls_by_pel.get)
     chunks = k1_calls_by_pel[main_pel]
     # PMC passes ran their own (shorter) bench; normalise by their own chunk count
     pm_f = [v for k, d in pmc.items() if k.startswith(k1_base) for v in d.get("FETCH_SIZE", [])]
     pm_w = [v for k, d in pmc.items() if k.startswith(k1_base) for v in d.get("WRITE_SIZE", [])]
     pm_chunks_f = sum(len(d.get("FETCH_SIZE", [])) for k, d in pmc.items()
-                      if k.startswith(k1_base) and (("unsigned short" in k) == (main_pel == "u16")))
+                      if k.startswith(k1_base) and k1_group(k) == main_pel)
     pm_chunks_w = sum(len(d.get("WRITE_SIZE", [])) for k, d in pmc.items()
-                      if k.startswith(k1_base) and (("unsigned short" in k) == (main_pel == "u16")))
+                      if k.startswith(k1_base) and k1_group(k) == main_pel)
     fa = sum(pm_f) / pm_chunks_f if pm_chunks_f else None
     wa = sum(pm_w) / pm_chunks_w if pm_chunks_w else None
     hbm = (2 * fa + wa) * 1024 if fa is not None and wa is not None else None
