@@ -24,6 +24,7 @@
 // /root/reference/src/Encoder.cpp:250 (avcodec_send_frame, mjpeg).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -259,7 +260,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     const uint8_t flags = tu.flags;
     for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
     if (lane == 0) { s.maxx = 0; s.maxy = 0; }
-    __syncthreads();
+    wave_sync();
     const bool bypass = (flags & H2J_TU_BYPASS) != 0;
     const int qp = tu.qp;
     const int bdShift = bd + log2n - 5;
@@ -289,7 +290,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     }
     if (mx) atomicMax(&s.maxx, mx);
     if (my) atomicMax(&s.maxy, my);
-    __syncthreads();
+    wave_sync();
     if (!bypass) {
         if (flags & H2J_TU_TSKIP) {
             const int bdS = 20 - bd;
@@ -310,7 +311,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
                 }
                 s.tmp[i] = clip3(-32768, 32767, (acc + 64) >> 7);
             }
-            __syncthreads();
+            wave_sync();
             const int bdS = 20 - bd;
             for (int i = lane; i < nn; i += 64) {
                 const int x = i & (n - 1), y = i >> log2n;
@@ -323,9 +324,9 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
-    __syncthreads();
+    wave_sync();
 }
 
 // H.264 scaling (8.5.9, 8.5.10-8.5.12 DC transforms) + 4x4 / 8x8 inverse
@@ -338,12 +339,12 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     const bool i16 = c == 0 && log2n == 4;
     const bool chroma = c > 0;
     for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
-    __syncthreads();
+    wave_sync();
     for (int e = lane; e < tu.ncoef; e += 64) {
         const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
         s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
     }
-    __syncthreads();
+    wave_sync();
     const uint8_t* w4 = f.slist ? sl + f.sl + c * 16 : nullptr;
     if (i16 || chroma) {
         // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
@@ -365,7 +366,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
             else v = ((acc * ls0) << (qp / 6)) >> 5;
             s.dc[lane] = v;
         }
-        __syncthreads();
+        wave_sync();
         for (int i = lane; i < nn; i += 64) {
             const int y = i >> log2n, x = i & (n - 1);
             const int by = y >> 2, bx = x >> 2, ry = y & 3, rx = x & 3;
@@ -380,7 +381,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
         for (int i = lane; i < 64; i += 64)
             s.blk[i] = h264_scale8(s.blk[i], (w8 ? w8[i] : 16) * h264_norm8(qm, i >> 3, i & 7), qp);
     }
-    __syncthreads();
+    wave_sync();
     if (log2n == 3 && !chroma) {
         // 8x8 inverse transform: rows (lanes 0..7) then columns
         for (int pass = 0; pass < 2; pass++) {
@@ -397,7 +398,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
                 if (pass == 0) for (int k = 0; k < 8; k++) s.tmp[lane * 8 + k] = o[k];
                 else for (int k = 0; k < 8; k++) s.blk[k * 8 + lane] = (o[k] + 32) >> 6;
             }
-            __syncthreads();
+            wave_sync();
         }
     } else {
         // 4x4 inverse transforms of all 4x4 blocks: lane = block * 4 + row/col
@@ -425,11 +426,11 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
                     s.blk[(by + 3) * n + bx + k] = (e0 - e3 + 32) >> 6;
                 }
             }
-            __syncthreads();
+            wave_sync();
         }
     }
     for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
-    __syncthreads();
+    wave_sync();
 }
 
 // position of a 4x4 block inside its CTB in z-scan order (6.5.2)
@@ -492,8 +493,8 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         }
         if (lane < 16) s.dst[lane >> 2][lane & 3] = kDst4[lane >> 2][lane & 3];
     }
-    __syncthreads();
-    auto ctb_of_tu = [&](const h2j_tu& tu) {
+    wave_sync();
+    auto ctb_of_tu = [&](const h2j_tu& tu) __attribute__((always_inline)) {
         const int sh = tu.c ? 1 : 0;
         return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
     };
@@ -501,7 +502,7 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     const int prev_c = t0 > 0 ? tu_from_lanes(rec, kK0Tus).c : 0;
     const int next_cb = t1 < ntu ? ctb_of_tu(tu_from_lanes(rec, kK0Tus + 1)) : -1;
     // coefficient entries of the current TU (lane e < 64), prefetched one TU ahead
-    auto fetch_co = [&](const h2j_tu& v) -> uint32_t {
+    auto fetch_co = [&](const h2j_tu& v) __attribute__((always_inline)) -> uint32_t {
         const uint32_t e = min(static_cast<uint32_t>(lane), max(static_cast<uint32_t>(v.ncoef), 1u) - 1);
         return v.ncoef ? CO[v.coef + e] : 0u;
     };
@@ -801,7 +802,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     // the boundary rows, both accessed with agent-scope atomics (coherent across CUs / XCDs)
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
     if (rbeg + w >= rend) return;
-    auto fetch = [&](int mx, int my, uint32_t a, H4Pre& p) {
+    auto fetch = [&](int mx, int my, uint32_t a, H4Pre& p) __attribute__((always_inline)) {
         const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
         p.rec = reinterpret_cast<const uint4*>(T)[ri];
         p.msk = reinterpret_cast<const uint2*>(masks)[ri];
@@ -1259,8 +1260,8 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
 
 template <typename Pel, int W_>
 DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
-                    int16_t* line) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+                    int16_t* line, int wv) {
+    const int lane = threadIdx.x & 63;
     QWave& w = W[wv];
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
@@ -1278,10 +1279,10 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     PROF_DECL;
     // the wave's quadrant sequence: rows wv, wv + W_, ..., CTBs left to right, z-order
     // quadrants, skipping quadrants outside the picture
-    auto q_inside = [&](int row, int cx, int q) {
+    auto q_inside = [&](int row, int cx, int q) __attribute__((always_inline)) {
         return cx * Sc + (q & 1) * Qc < Wc && row * Sc + (q >> 1) * Qc < Hc;
     };
-    auto q_next = [&](int& row, int& cx, int& q) {  // advance to the next quadrant inside the picture
+    auto q_next = [&](int& row, int& cx, int& q) __attribute__((always_inline)) {  // advance to the next quadrant inside the picture
         do {
             if (++q == nqs * nqs) {
                 q = 0;
@@ -1293,7 +1294,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     hevc_qres_dma(u, grp, 0, wv * Sc, Qc, w.body[0], lane);
     lds_dma_wait();
     // this group's record range of a CTB: luma [first, first chroma), chroma [first chroma, end)
-    auto grange = [&](int cbi, uint32_t& ra, uint32_t& rb) {
+    auto grange = [&](int cbi, uint32_t& ra, uint32_t& rb) __attribute__((always_inline)) {
         const uint4 r = reinterpret_cast<const uint4*>(rng)[cbi];
         const uint32_t mid = (r.y > r.x && r.y <= r.z) ? r.y : r.z;
         ra = grp ? mid : r.x;
@@ -1472,7 +1473,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
 // batch launches both and each skips the other codec's pictures.
 // grid (pictures, 2): blockIdx.y = 0 luma chain, 1 chroma chains.
 template <typename Pel, int W_>
-__global__ void __launch_bounds__(64 * W_) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
+__global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame* frames, const h2j_tu* tus,
                                                             uint8_t* arena) {
     extern __shared__ __align__(16) uint8_t k1lds[];
     QWave* W = reinterpret_cast<QWave*>(k1lds);
@@ -1480,9 +1481,13 @@ __global__ void __launch_bounds__(64 * W_) h2j_k1_recon_hevc(const h2j_frame* fr
     int16_t* line = reinterpret_cast<int16_t*>(k1lds + k1_fixed_lds(W_));
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
+#if defined(H2J_EXP) && (H2J_EXP == 3 || H2J_EXP == 4)  // timing experiment: one chain only (3: chroma, 4: luma)
+    if (static_cast<int>(blockIdx.y) == (H2J_EXP == 3 ? 0 : 1)) return;
+#endif
     if (threadIdx.x < 2 * W_) prog[threadIdx.x] = 0;
     __syncthreads();
-    hevc_rows<Pel, W_>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line);
+    hevc_rows<Pel, W_>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line,
+                       static_cast<int>(threadIdx.x >> 6));
 }
 
 // grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
@@ -1504,6 +1509,45 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
     const h2j_tu* T = tus + ufl(f.tu);
     if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
     else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
+}
+
+// K1 for batches mixing HEVC 8-bit, HEVC high bit depth and H.264 pictures (configs[4]): one
+// launch instead of three back-to-back ones, so the pictures' chains run side by side (each
+// launch alone is one long chain per picture and leaves most of the GPU idle).  Workgroups of
+// 16 waves: an HEVC picture's luma group (waves 0-7) and chroma group (waves 8-15) share one
+// workgroup; an H.264 workgroup is one band as in h2j_k1_recon_h264.  `map`: the host's list,
+// longest chains first; bit 31 marks HEVC entries.  `gbytes`: LDS bytes of one HEVC group.
+__global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_frame* frames, const h2j_tu* tus,
+                                                                 uint8_t* arena, const uint32_t* map,
+                                                                 uint32_t gbytes) {
+    static_assert(2 * kK1Waves == kAvcWaves, "an HEVC picture's two groups fill one H.264-sized workgroup");
+    extern __shared__ __align__(16) uint8_t anylds[];
+    const uint32_t me = map[blockIdx.x];
+    const h2j_frame& f = frames[(me >> 8) & 0x7FFFFFu];
+    const h2j_tu* T = tus + ufl(f.tu);
+    if (me & 0x80000000u) {
+        const int grp = static_cast<int>(threadIdx.x >> 9);
+        uint8_t* gb = anylds + grp * gbytes;
+        QWave* W = reinterpret_cast<QWave*>(gb);
+        uint32_t* prog = reinterpret_cast<uint32_t*>(gb + sizeof(QWave) * kK1Waves);
+        int16_t* line = reinterpret_cast<int16_t*>(gb + k1_fixed_lds(kK1Waves));
+        if ((threadIdx.x & 511) < 2 * kK1Waves) prog[threadIdx.x & 511] = 0;
+        __syncthreads();
+        const int wv = static_cast<int>((threadIdx.x >> 6) & (kK1Waves - 1));
+        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t, kK1Waves>(f, T, arena, grp, W, prog, line, wv);
+        else hevc_rows<uint16_t, kK1Waves>(f, T, arena, grp, W, prog, line, wv);
+    } else {
+        H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(anylds);
+        uint32_t* prog = reinterpret_cast<uint32_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves);
+        uint16_t* line = reinterpret_cast<uint16_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4);
+        const int band = static_cast<int>(me & 0xFF);
+        const int nbands = ufl(f.k1bands);
+        if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
+        __syncthreads();
+        H4WaveLds& s = wl[threadIdx.x >> 6];
+        if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
+        else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
+    }
 }
 
 // ---------------------------------------------------------------- K2: deblocking
@@ -1812,7 +1856,7 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
         const uint64_t o_xin = o_xl + 12ull * (band - 1) * width, o_xout = o_xl + 12ull * band * width;
         // stores of a boundary row go through to the coherence point (the band below writes the
         // same bottom rows once its top edges are filtered, possibly from another XCD)
-        auto put = [&](Pel* p, Pel v) {
+        auto put = [&](Pel* p, Pel v) __attribute__((always_inline)) {
             if (to_band) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else *p = v;
         };
@@ -2486,47 +2530,58 @@ int h2j_gpu_prof(unsigned long long* out, int n, int reset) {
 int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    // two workgroups per HEVC picture (luma, chroma).  Up to 128 pictures every group gets a CU
+    // of its own and runs kK1WavesWide waves (rows in flight); beyond that two groups share
+    // a CU and run kK1Waves each (VGPR-bound occupancy).
+    const bool wide = b->nframes <= 128;
+    const int pels = b->hevc_pels;  // bit 0: 8-bit HEVC pictures, bit 1: high bit depth
+    const int kinds = ((pels & 1) ? 1 : 0) + ((pels & 2) ? 1 : 0) + (b->has_h264 && b->k1wgs > 0 ? 1 : 0);
+    const size_t lds264 = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4 + 4 * static_cast<size_t>(b->max_w);
+    static bool attr = false;
+    if (!attr) {
+        const void* fns[] = {reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1WavesWide>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1Waves>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1Waves>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_h264),
+                             reinterpret_cast<const void*>(h2j_k1_recon_any)};
+        for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    static const bool merge = [] {  // H2J_K1_MERGE=0: separate launches per kind (A/B timing)
+        const char* e = std::getenv("H2J_K1_MERGE");
+        return !(e && e[0] == '0');
+    }();
+    if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0) {  // one launch for every kind of picture
+        const size_t gbytes = (k1_fixed_lds(kK1Waves) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t) + 15) & ~size_t(15);
+        const size_t lds = std::max(2 * gbytes, lds264);
+        if (lds > 160 * 1024) {
+            snprintf(g_err, sizeof(g_err), "h2j_k1_recon_any: %zu B of LDS per workgroup (max 160 KB)", lds);
+            return -1;
+        }
+        hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
+                           b->arena, b->k1all, static_cast<uint32_t>(gbytes));
+        return check(hipGetLastError(), "h2j_k1_recon_any");
+    }
     if (b->has_hevc) {
-        // two workgroups per picture (luma, chroma).  Up to 128 pictures every group gets a CU
-        // of its own and runs kK1WavesWide waves (rows in flight); beyond that two groups share
-        // a CU and run kK1Waves each (VGPR-bound occupancy).
-        const bool wide = b->nframes <= 128;
         const int wv = wide ? kK1WavesWide : kK1Waves;
         const size_t lds = k1_fixed_lds(wv) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1WavesWide>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1Waves>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1Waves>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
         const dim3 grid(b->nframes, 2), block(64 * wv);
+        const bool p8 = pels == 0 || (pels & 1), p16 = pels == 0 || (pels & 2);
         if (wide) {
-            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
-            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
         } else {
-            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
-            hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
         }
         int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
         if (r) return r;
     }
     if (b->has_h264) {
         // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
-        const size_t lds = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4 + 4 * static_cast<size_t>(b->max_w);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k1_recon_h264),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
         if (b->k1wgs > 0)
-            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
+            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, s, b->frames, b->tus,
                                b->arena, b->k1map);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }

@@ -332,8 +332,27 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
             if (f.codec != H2J_CODEC_H264 || (f.k1bands > 1) != (pass == 0)) continue;
             for (int bnd = 0; bnd < f.k1bands; bnd++) k1map.push_back((static_cast<uint32_t>(k) << 8) | bnd);
         }
+    // mixed-batch K1 map (h2j_k1_recon_any): every HEVC picture and H.264 band, tallest first so
+    // the longest chains start first; bands of one picture stay in order
+    std::vector<uint32_t> k1all;
+    {
+        std::vector<std::pair<int, uint32_t>> e;
+        for (int k = 0; k < nf; k++) {
+            const h2j_frame& f = s.frames[k];
+            const int rows = f.codec == H2J_CODEC_H264 ? std::min(f.ctb_h, 16) : f.ctb_h << (f.log2ctb - 4);
+            if (f.codec == H2J_CODEC_HEVC) e.emplace_back(-rows, (1u << 31) | (static_cast<uint32_t>(k) << 8));
+        }
+        for (uint32_t m : k1map) {
+            const h2j_frame& f = s.frames[m >> 8];
+            e.emplace_back(-std::min(f.ctb_h, 16) - (f.k1bands > 1 ? 1000 : 0), m);
+        }
+        std::stable_sort(e.begin(), e.end(),
+                         [](const std::pair<int, uint32_t>& a, const std::pair<int, uint32_t>& b) { return a.first < b.first; });
+        for (const auto& x : e) k1all.push_back(x.second);
+    }
     const size_t o_map = align_up(o_sl + nsl + 16, 256);
-    const size_t in_bytes = align_up(o_map + k1map.size() * 4 + 16, 256);
+    const size_t o_all = align_up(o_map + k1map.size() * 4 + 16, 256);
+    const size_t in_bytes = align_up(o_all + k1all.size() * 4 + 16, 256);
     if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
     if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
     if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
@@ -347,6 +366,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     }
     std::memcpy(s.h_in.p + o_frames, s.frames.data(), nf * sizeof(h2j_frame));
     if (!k1map.empty()) std::memcpy(s.h_in.p + o_map, k1map.data(), k1map.size() * 4);
+    if (!k1all.empty()) std::memcpy(s.h_in.p + o_all, k1all.data(), k1all.size() * 4);
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -391,6 +411,11 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.sl = din + o_sl;
     b.k1map = reinterpret_cast<const uint32_t*>(din + o_map);
     b.k1wgs = static_cast<int32_t>(k1map.size());
+    b.k1all = reinterpret_cast<const uint32_t*>(din + o_all);
+    b.k1all_n = static_cast<int32_t>(k1all.size());
+    b.hevc_pels = 0;
+    for (int k = 0; k < nf; k++)
+        if (s.frames[k].codec == H2J_CODEC_HEVC) b.hevc_pels |= (s.frames[k].bit_depth > 8 || s.frames[k].bit_depth_c > 8) ? 2 : 1;
     b.arena = static_cast<uint8_t*>(s.d_arena.p);
     b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
     b.seg_cap = entropy ? seg_cap : 0;

@@ -58,6 +58,10 @@ typedef struct {
     int32_t max_ctbs;           /* max CTBs (H.264: macroblocks) of one picture over the batch */
     int32_t k1wgs;              /* H.264 K1 workgroups (sum of h2j_frame.k1bands over H.264 pictures) */
     const uint32_t *k1map;      /* H.264 K1 workgroup -> (frame << 8) | band, dependency order */
+    int32_t hevc_pels;          /* HEVC sample types present: bit 0 8-bit, bit 1 high bit depth */
+    int32_t k1all_n;            /* entries of k1all */
+    const uint32_t *k1all;      /* mixed-batch K1 workgroups, longest chains first: HEVC pictures
+                                   (1u << 31) | (frame << 8), then H.264 (frame << 8) | band */
     const h2j_frame *frames;
     const h2j_tu *tus;
     const h2j_coef *coefs;

@@ -87,3 +87,16 @@ def test_mixed_workload_batch(engine):
     outs = engine.transcode(streams)
     for s, o, p in zip(streams, outs, paths):
         assert o == O.transcode(s), p
+
+
+def test_merged_k1_launch_mixed_kinds(engine):
+    """A batch of more than 128 pictures mixing HEVC 8-bit, HEVC 10-bit and H.264
+    runs K1 as one merged launch (h2j_k1_recon_any); every JPEG byte-exact."""
+    hevc = sorted(glob.glob(os.path.join(golden("hevc"), "*.h265")))
+    kinds = [read(p) for p in PARITY264 + hevc]
+    assert any("10bit" in p for p in hevc)
+    streams = [kinds[i % len(kinds)] for i in range(160)]
+    want = {i: O.transcode(s) for i, s in enumerate(kinds)}
+    outs = engine.transcode(streams)
+    for i, o in enumerate(outs):
+        assert o == want[i % len(kinds)], i

@@ -28,7 +28,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     int reps = 3, threads = 1;
-    bool want_digest = false;
+    bool want_digest = false, want_hist = false;
     std::vector<std::vector<uint8_t>> streams;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -38,6 +38,10 @@ int main(int argc, char** argv) {
         }
         if (a == "-d") {
             want_digest = true;
+            continue;
+        }
+        if (a == "-s") {  // transform-block histogram by (component, size, cbf)
+            want_hist = true;
             continue;
         }
         if (a == "-t" && i + 1 < argc) {
@@ -58,6 +62,8 @@ int main(int argc, char** argv) {
     std::atomic<size_t> tus(0), coefs(0), bytes(0);
     std::atomic<unsigned long long> bins_ctx(0), bins_byp(0);
     std::atomic<unsigned long long> digest(0);  // order-independent checksum of all parse outputs
+    std::atomic<unsigned long long> hist[2][4][2];
+    for (auto& a : hist) for (auto& b : a) for (auto& c : b) c = 0;
     auto worker = [&]() {
         h2j::FrameJob job;
         size_t t = 0, c = 0, b = 0;
@@ -72,6 +78,9 @@ int main(int argc, char** argv) {
                 return;
             }
             t += job.tus.size();
+            if (want_hist)
+                for (const h2j_tu& u : job.tus)
+                    if (u.log2n >= 2 && u.log2n <= 5) hist[u.c ? 1 : 0][u.log2n - 2][(u.flags & H2J_TU_CBF) ? 1 : 0]++;
             c += job.coefs.size();
             b += s.size();
             if (!want_digest) continue;
@@ -103,6 +112,11 @@ int main(int argc, char** argv) {
     std::printf("%d thr: %.3f ms/frame wall, %.3f ms/frame/thread  %.0f TUs/frame  %.0f coefs/frame  %.1f MB/s  digest %016llx\n",
                 threads, ms / nf, ms * threads / nf, tus / nf, coefs / nf, bytes / (ms / 1e3) / 1e6,
                 static_cast<unsigned long long>(digest));
+    if (want_hist)
+        for (int c = 0; c < 2; c++)
+            for (int l = 0; l < 4; l++)
+                std::printf("%s %2dx%-2d: %8.0f TBs/frame, %8.0f with residual\n", c ? "chroma" : "luma  ", 4 << l, 4 << l,
+                            (hist[c][l][0] + hist[c][l][1]) / nf, hist[c][l][1] / nf);
     if (bins_ctx + bins_byp)
         std::printf("bins/frame: %.0f context-coded, %.0f bypass; %.2f ns per bin\n", bins_ctx / nf, bins_byp / nf,
                     ms * 1e6 * threads / static_cast<double>(bins_ctx + bins_byp));
