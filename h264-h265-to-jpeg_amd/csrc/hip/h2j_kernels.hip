@@ -76,10 +76,26 @@ DEVI bool avail(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices
 }
 
 // HEVC 32x32 inverse transform matrix entries from the 33 distinct cosines
-__constant__ int8_t kCos33[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
-                                  61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
-__constant__ int8_t kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
 __constant__ int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+// the 32x32 HEVC DCT matrix (8.6.4.2, transMatrix), built at compile time from the 33 cosines
+// above; an N-point transform uses rows j * 32 / N.  int32 entries: rows load into scalar registers.
+struct DctMat {
+    int v[32][32];
+};
+constexpr DctMat make_dct32() {
+    constexpr int c[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                           61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+    DctMat t{};
+    for (int m = 0; m < 32; m++)
+        for (int k = 0; k < 32; k++) {
+            int a = ((2 * k + 1) * m) & 127;
+            if (a > 64) a = 128 - a;
+            t.v[m][k] = a > 32 ? -c[64 - a] : c[a];
+        }
+    return t;
+}
+__constant__ DctMat kDct32 = make_dct32();
+__constant__ int kDst4i[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
 
 // ---------------------------------------------------------------- K1: H.264
 // H.264 8.3 (intra prediction), 8.5 (scaling + transforms).  Records: luma
@@ -176,14 +192,13 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // availability mask, the CTB -> TU range, the HEVC deblocking maps, PCM
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
-constexpr int kK0Tus = 16;   // TUs per K0 wave (records held one per lane)
+constexpr int kK0Tus = 16;      // H.264 TUs per K0 wave (records held one per lane)
+constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
 constexpr int kK1Waves = 8;       // HEVC K1: waves (CTB rows in flight) per group, launches of > 128 pictures
 constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
 struct K0Lds {
-    int8_t mat[32][32];
-    int8_t dst[4][4];
     int blk[32 * 32];
     int tmp[32 * 32];
     int dc[16];
@@ -246,8 +261,8 @@ DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
 }
 
 
-// HEVC dequantisation (8.6.2-8.6.3) + inverse transform / transform skip /
-// bypass (8.6.4) of one TB into R (int16, stride rst).
+// HEVC dequantisation (8.6.2-8.6.3) + transform skip / bypass (8.6.4) of one TB
+// into R (int16, stride rst); regular transforms: hevc_residual_group.
 struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
     int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo;
     uint32_t sl;
@@ -291,41 +306,116 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     if (mx) atomicMax(&s.maxx, mx);
     if (my) atomicMax(&s.maxy, my);
     wave_sync();
-    if (!bypass) {
-        if (flags & H2J_TU_TSKIP) {
-            const int bdS = 20 - bd;
-            for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
-        } else {
-            const bool dst = (flags & H2J_TU_DST) != 0;
-            const int mxx = s.maxx, myy = s.maxy;
-            const int msh = 5 - log2n;
-            // column pass: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
-            for (int i = lane; i < nn; i += 64) {
-                const int x = i & (n - 1), y = i >> log2n;
-                int acc = 0;
-                if (x <= mxx) {
-                    for (int j = 0; j <= myy; j++) {
-                        const int cf = dst ? s.dst[j][y] : s.mat[j << msh][y];
-                        acc += cf * s.blk[j * n + x];
-                    }
-                }
-                s.tmp[i] = clip3(-32768, 32767, (acc + 64) >> 7);
-            }
-            wave_sync();
-            const int bdS = 20 - bd;
-            for (int i = lane; i < nn; i += 64) {
-                const int x = i & (n - 1), y = i >> log2n;
-                int acc = 0;
-                for (int j = 0; j <= mxx; j++) {
-                    const int cf = dst ? s.dst[j][x] : s.mat[j << msh][x];
-                    acc += cf * s.tmp[y * n + j];
-                }
-                s.blk[i] = (acc + (1 << (bdS - 1))) >> bdS;
-            }
-        }
+    if (!bypass) {  // transform skip (regular transforms run batched: hevc_residual_group)
+        const int bdS = 20 - bd;
+        for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
     }
     wave_sync();
     for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    wave_sync();
+}
+
+// HEVC dequantisation + inverse DCT/DST (8.6.2-8.6.4) of up to 64 / N same-size TBs of one wave
+// at once: lane = (TB slot, column) in the column pass, (TB slot, row) in the row pass, so no lane
+// idles on small TBs.  Each lane keeps its N partial sums in registers and walks the non-zero
+// input rows / columns (bounded by the group's largest coefficient position); the matrix row of a
+// step is uniform (scalar loads).  The intermediate goes through LDS (int16), the result straight
+// to the residual plane.  `gm`: record lanes of the group's G TBs (slot g = g-th set bit).
+// Transform-skip and bypass TBs are not batched (hevc_residual).
+template <int LOG2N>
+DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
+                              const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0Lds& s) {
+    constexpr int N = 1 << LOG2N, NN = N * N, MSH = 5 - LOG2N;
+    const int lane = threadIdx.x;
+    int16_t* blk = reinterpret_cast<int16_t*>(s.blk);  // [G][N][N] dequantised coefficients
+    int16_t* tmp = reinterpret_cast<int16_t*>(s.tmp);  // [G][N][N] after the column pass (row-major)
+    for (int i = lane * 8; i < G * NN; i += 512) *reinterpret_cast<uint4*>(blk + i) = make_uint4(0, 0, 0, 0);
+    wave_sync();
+    int mx = 0, my = 0;
+    uint64_t mm = gm;
+    for (int g = 0; g < G; g++) {
+        const int kg = __ffsll(static_cast<long long>(mm)) - 1;
+        mm &= mm - 1;
+        const h2j_tu tu = tu_from_lanes(rec, kg);
+        const int c = tu.c, bd = c ? f.bdc : f.bd, qp = tu.qp;
+        const int bdShift = bd + LOG2N - 5;
+        const long long ls = static_cast<long long>(kLevelScale[qp % 6] << (qp / 6));
+        const uint8_t* slt = f.slist ? sl + f.sl + (LOG2N == 2 ? c * 16 : LOG2N == 3 ? 48 + c * 64 : LOG2N == 4 ? 240 + c * 256 : 1008)
+                                     : nullptr;
+        for (int e = lane; e < tu.ncoef; e += 64) {
+            const uint32_t en = CO[tu.coef + e];
+            const int pos = static_cast<int>(en >> 16);
+            const int lvl = static_cast<int16_t>(en & 0xFFFF);
+            const int m = slt ? slt[pos] : 16;
+            long long v = static_cast<long long>(lvl) * m * ls;
+            v = (v + (1ll << (bdShift - 1))) >> bdShift;
+            blk[g * NN + pos] = static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+            mx = max(mx, pos & (N - 1));
+            my = max(my, pos >> LOG2N);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, __shfl_xor(mx, o, 64));
+        my = max(my, __shfl_xor(my, o, 64));
+    }
+    const int mxx = ufl(mx), myy = ufl(my);
+    wave_sync();
+    // this lane's TB: its record lives in lane k of `rec`
+    const int g = lane >> LOG2N, q = lane & (N - 1);
+    const bool act = g < G;
+    uint64_t ml = gm;
+    for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+    const int k = __ffsll(static_cast<long long>(ml)) - 1;
+    const uint32_t w0 = __shfl(rec.x, k, 64), w1 = __shfl(rec.y, k, 64), w2 = __shfl(rec.z, k, 64);
+    uint32_t wq[4] = {w0, w1, w2, 0};
+    h2j_tu mine;
+    memcpy(&mine, wq, sizeof(mine));
+    const bool dst = LOG2N == 2 && (mine.flags & H2J_TU_DST) != 0;
+    auto coef = [&](int j, int i) __attribute__((always_inline)) {
+        const int cv = kDct32.v[j << MSH][i];
+        if (LOG2N != 2) return cv;
+        return dst ? kDst4i[j][i] : cv;
+    };
+    if (act) {  // columns: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
+        int acc[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) acc[i] = 0;
+        for (int j = 0; j <= myy; j++) {
+            const int v = blk[g * NN + j * N + q];
+#pragma unroll
+            for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
+        }
+#pragma unroll
+        for (int i = 0; i < N; i++) tmp[g * NN + i * N + q] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
+    }
+    wave_sync();
+    if (act) {  // rows: r[y][x] = (sum_j M[j][x] * tmp[y][j] + rnd) >> (20 - bitDepth)
+        int acc[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) acc[i] = 0;
+        for (int j = 0; j <= mxx; j++) {
+            const int v = tmp[g * NN + q * N + j];
+#pragma unroll
+            for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
+        }
+        const int bdS = 20 - (mine.c ? f.bdc : f.bd);
+        const int c = mine.c;
+        int16_t* R = res + (c == 0 ? 0 : (c == 1 ? off1 : off2)) + (mine.y + q) * (c ? st1 : st0) + mine.x;
+        uint32_t packed[N / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; i++) {
+            const int a = (acc[2 * i] + (1 << (bdS - 1))) >> bdS, b = (acc[2 * i + 1] + (1 << (bdS - 1))) >> bdS;
+            packed[i] = (static_cast<uint32_t>(a) & 0xFFFF) | (static_cast<uint32_t>(b) << 16);
+        }
+        if (N == 4) {
+            *reinterpret_cast<uint2*>(R) = make_uint2(packed[0], packed[1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < N / 8; i++)
+                reinterpret_cast<uint4*>(R)[i] = make_uint4(packed[4 * i], packed[4 * i + 1], packed[4 * i + 2], packed[4 * i + 3]);
+        }
+    }
     wave_sync();
 }
 
@@ -441,16 +531,21 @@ DEVI int zorder4(int ax, int ay) {
     return z;
 }
 
+// One kernel per codec (HEVC: batched transforms, more records per wave; each gets its own
+// register budget), each skipping the other codec's pictures.
+template <bool HEVC>
 __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
                                                  uint8_t* arena) {
+    constexpr int kTus = HEVC ? kK0TusHevc : kK0Tus;
     __shared__ K0Lds s;
     const h2j_frame& fr = frames[blockIdx.y];
+    if ((ufl(fr.codec) == H2J_CODEC_HEVC) != HEVC) return;
     const uint32_t ntu = ufl(fr.ntu);
-    const uint32_t t0 = blockIdx.x * kK0Tus;
+    const uint32_t t0 = blockIdx.x * kTus;
     if (t0 >= ntu) return;
     const int lane = threadIdx.x;
-    const bool hevc = ufl(fr.codec) == H2J_CODEC_HEVC;
+    constexpr bool hevc = HEVC;
     K0F f;
     f.bd = ufl(fr.bit_depth);
     f.bdc = ufl(fr.bit_depth_c);
@@ -475,43 +570,39 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     const int st0 = ufl(fr.pic_stride[0]), st1 = ufl(fr.pic_stride[1]);
     const int off1 = ufl(fr.pic_off[1]), off2 = ufl(fr.pic_off[2]);
     // this workgroup's records (lane k: record t0 + k) and the two neighbours of the range
-    const uint32_t t1 = min(ntu, t0 + kK0Tus);
+    const uint32_t t1 = min(ntu, t0 + kTus);
     const int nrec = static_cast<int>(t1 - t0);
     uint4 rec = make_uint4(0, 0, 0, 0);
     {
         int ri = static_cast<int>(t0) + lane;
-        if (lane == kK0Tus) ri = static_cast<int>(t0) - 1;
-        if (lane == kK0Tus + 1) ri = static_cast<int>(t1);
-        if (lane <= kK0Tus + 1 && ri >= 0 && ri < static_cast<int>(ntu)) rec = reinterpret_cast<const uint4*>(T)[ri];
+        if (lane == kTus) ri = static_cast<int>(t0) - 1;
+        if (lane == kTus + 1) ri = static_cast<int>(t1);
+        if (lane <= kTus + 1 && ri >= 0 && ri < static_cast<int>(ntu)) rec = reinterpret_cast<const uint4*>(T)[ri];
     }
-    if (hevc) {
-        for (int i = lane; i < 1024; i += 64) {
-            const int m = i >> 5, nn = i & 31;
-            int a = ((2 * nn + 1) * m) & 127;
-            if (a > 64) a = 128 - a;
-            s.mat[m][nn] = static_cast<int8_t>(a > 32 ? -kCos33[64 - a] : kCos33[a]);
-        }
-        if (lane < 16) s.dst[lane >> 2][lane & 3] = kDst4[lane >> 2][lane & 3];
-    }
+    // (the HEVC matrices are constants: kDct32 / kDst4i; transform-skip and bypass TBs use none)
     wave_sync();
     auto ctb_of_tu = [&](const h2j_tu& tu) __attribute__((always_inline)) {
         const int sh = tu.c ? 1 : 0;
         return ((tu.y << sh) >> f.log2ctb) * f.ctb_w + ((tu.x << sh) >> f.log2ctb);
     };
-    const int prev_cb = t0 > 0 ? ctb_of_tu(tu_from_lanes(rec, kK0Tus)) : -1;
-    const int prev_c = t0 > 0 ? tu_from_lanes(rec, kK0Tus).c : 0;
-    const int next_cb = t1 < ntu ? ctb_of_tu(tu_from_lanes(rec, kK0Tus + 1)) : -1;
+    const int prev_cb = t0 > 0 ? ctb_of_tu(tu_from_lanes(rec, kTus)) : -1;
+    const int prev_c = t0 > 0 ? tu_from_lanes(rec, kTus).c : 0;
+    const int next_cb = t1 < ntu ? ctb_of_tu(tu_from_lanes(rec, kTus + 1)) : -1;
     // coefficient entries of the current TU (lane e < 64), prefetched one TU ahead
     auto fetch_co = [&](const h2j_tu& v) __attribute__((always_inline)) -> uint32_t {
         const uint32_t e = min(static_cast<uint32_t>(lane), max(static_cast<uint32_t>(v.ncoef), 1u) - 1);
         return v.ncoef ? CO[v.coef + e] : 0u;
     };
-    uint32_t nco = fetch_co(tu_from_lanes(rec, 0));
+    // H.264: coefficients of the next record prefetched one record ahead.  HEVC: no load in the
+    // loop (its wait would stall every record); the rare per-record paths (PCM, transform skip,
+    // bypass) load their own, regular transforms run batched after the loop.
+    uint32_t nco = hevc ? 0u : fetch_co(tu_from_lanes(rec, 0));
     for (int k = 0; k < nrec; k++) {
         const uint32_t t = t0 + k;
         const h2j_tu tu = tu_from_lanes(rec, k);
-        const uint32_t co0 = nco;
-        if (k + 1 < nrec) nco = fetch_co(tu_from_lanes(rec, k + 1));
+        uint32_t co0 = nco;
+        if (!hevc && k + 1 < nrec) nco = fetch_co(tu_from_lanes(rec, k + 1));
+        if (hevc && (tu.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS))) co0 = fetch_co(tu);
         const int c = tu.c, log2n = tu.log2n, n = 1 << log2n;
         const int shc = c ? 1 : 0;
         const int x0 = tu.x, y0 = tu.y, xl = x0 << shc, yl = y0 << shc;
@@ -609,8 +700,40 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         if (lane == 0) masks[t] = mask;
         if (flags & H2J_TU_CBF) {
             int16_t* R = res + offc;
-            if (hevc) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
-            else h264_residual(f, tu, CO, co0, sl, R, stc, s);
+            if (hevc) {
+                if (flags & (H2J_TU_TSKIP | H2J_TU_BYPASS)) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
+                // regular HEVC transforms: batched by size below
+            } else {
+                h264_residual(f, tu, CO, co0, sl, R, stc, s);
+            }
+        }
+    }
+    if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
+        h2j_tu own;
+        {
+            uint32_t w[4] = {rec.x, rec.y, rec.z, rec.w};
+            memcpy(&own, w, sizeof(own));
+        }
+        const bool batch = lane < nrec && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS));
+#pragma unroll
+        for (int l2 = 2; l2 <= 5; l2++) {
+            uint64_t m = __ballot(batch && own.log2n == l2);
+            const int G = 64 >> l2;  // 16, 8, 4, 2 TBs per pass
+            while (m) {
+                uint64_t gm = 0;  // the next (up to) G TBs of this size
+                int cnt = 0;
+                while (m && cnt < G) {
+                    gm |= m & (0 - m);
+                    m &= m - 1;
+                    cnt++;
+                }
+                switch (l2) {
+                    case 2: hevc_residual_group<2>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
+                    case 3: hevc_residual_group<3>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
+                    case 4: hevc_residual_group<4>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
+                    default: hevc_residual_group<5>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
+                }
+            }
         }
     }
 }
@@ -2502,11 +2625,21 @@ float h2j_gpu_event_elapsed_ms(void* a, void* b) {
 int h2j_gpu_prep(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int waves = (b->max_ntu + kK0Tus - 1) / kK0Tus;
-    if (waves <= 0) return 0;
-    hipLaunchKernelGGL(h2j_k0_prep, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs, b->ctbs,
-                       b->slices, b->sl, b->arena);
-    return check(hipGetLastError(), "h2j_k0_prep");
+    if (b->max_ntu <= 0) return 0;
+    if (b->has_hevc) {
+        const int waves = (b->max_ntu + kK0TusHevc - 1) / kK0TusHevc;
+        hipLaunchKernelGGL(h2j_k0_prep<true>, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs,
+                           b->ctbs, b->slices, b->sl, b->arena);
+        const int r = check(hipGetLastError(), "h2j_k0_prep<hevc>");
+        if (r) return r;
+    }
+    if (b->has_h264) {
+        const int waves = (b->max_ntu + kK0Tus - 1) / kK0Tus;
+        hipLaunchKernelGGL(h2j_k0_prep<false>, dim3(waves, b->nframes), dim3(64), 0, s, b->frames, b->tus, b->coefs,
+                           b->ctbs, b->slices, b->sl, b->arena);
+        return check(hipGetLastError(), "h2j_k0_prep<h264>");
+    }
+    return 0;
 }
 
 // K1 cycle accounting (only in -DH2J_PROF builds): copies 16 counters, optionally resets them.
