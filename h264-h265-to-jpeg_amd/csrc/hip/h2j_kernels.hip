@@ -1834,7 +1834,6 @@ __constant__ int kTc0_264[52][3] = {
     {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
 
 __constant__ int kChromaQp264[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
-DEVI int chroma_qp_264(int qpi) { return qpi < 30 ? qpi : kChromaQp264[qpi - 30]; }
 
 template <typename Pel>
 DEVI void h264_filt_line(Pel* q, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
@@ -1916,38 +1915,30 @@ DEVI void db264_fetch(const Pel* PY, const Pel* const* PC, int sty, int stc, int
     r.c[1] = t[1];
 }
 
-// Deblocking parameters of one MB and of its top neighbour (loaded one MB ahead)
-struct DbInfo {
-    int mf, qp, saddr, dd, tco, beo, cq0, cq1;  // MB flags, QPY, slice first MB, disable idc, offsets
-    int tmf, tqp, tsaddr;                        // top neighbour (tmf = 0: none)
-};
-DEVI DbInfo db264_info(const h2j_ctb* mbs, const h2j_slice* slices, int mbw, int mx, int my) {
-    DbInfo d;
-    const h2j_ctb& m = mbs[my * mbw + mx];
-    const h2j_slice& sl = slices[m.slice];
-    d.mf = m.mbflags;
-    d.qp = m.qp;
-    d.saddr = sl.slice_addr_rs;
-    d.dd = sl.deblock_disabled;
-    d.tco = sl.tc_offset;
-    d.beo = sl.beta_offset;
-    d.cq0 = sl.cqp_offset[0];
-    d.cq1 = sl.cqp_offset[1];
-    d.tmf = 0;
-    d.tqp = 0;
-    d.tsaddr = -1;
-    if (my > 0) {
-        const h2j_ctb& t = mbs[(my - 1) * mbw + mx];
-        d.tmf = t.mbflags;
-        d.tqp = t.qp;
-        d.tsaddr = slices[t.slice].slice_addr_rs;
-    }
-    return d;
+// Deblocking parameters of one MB and of its top neighbour, loaded one MB ahead with VECTOR
+// loads (lane 0/1: the MB's dwords 2 and 9, lane 2/3: the top MB's): scalar loads would be
+// waited with lgkmcnt(0), which also drains every LDS access in between (the old form cost
+// ~2k cycles per MB).  Fields: slice = byte 9, qp = byte 36, mbflags = byte 37.
+static_assert(offsetof(h2j_ctb, slice) == 9 && offsetof(h2j_ctb, qp) == 36 && offsetof(h2j_ctb, mbflags) == 37 &&
+                  sizeof(h2j_ctb) % 4 == 0,
+              "h2j_ctb layout assumed by db264_info_raw");
+DEVI uint32_t db264_info_raw(const h2j_ctb* mbs, int mbw, int mx, int my, int lane) {
+    const int top = my > 0 ? (my - 1) * mbw + mx : my * mbw + mx;
+    const int idx = (lane & 2) ? top : my * mbw + mx;
+    return reinterpret_cast<const uint32_t*>(mbs + idx)[(lane & 1) ? 9 : 2];
 }
+// LDS copies of the H.264 deblocking tables (per-lane lookups, no scalar-load chains)
+constexpr int kDbSlices = 64;  // slices cached in LDS; more are read from global memory
+static_assert(sizeof(h2j_slice) % 4 == 0, "slice records are copied to LDS as dwords");
+struct DbTables {
+    int alpha[52], beta[52], tc0[52];  // tc0: bS 3 column (intra internal edges)
+    int cqp[22];                       // chroma QP map above 29
+    h2j_slice sl[kDbSlices];
+};
 
 template <typename Pel>
 DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
-                       uint32_t* prog, uint16_t* line, int band, int nbands) {
+                       uint32_t* prog, uint16_t* line, int band, int nbands, const DbTables& TB) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     DbWin& w = W[wv];
     const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
@@ -1968,7 +1959,7 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
     PROF_DECL;
     DbPrefetch<Pel> pf;
     db264_fetch<Pel>(PY, PC, sty, stc, 0, rbeg + wv, pf, lane);
-    DbInfo ninfo = db264_info(mbs, slices, mbw, 0, rbeg + wv);
+    uint32_t ninfo = db264_info_raw(mbs, mbw, 0, rbeg + wv, lane);
     int lmf = 0, lqp = 0, lsaddr = -1;  // left neighbour (previous MB of the row)
     for (int row = rbeg + wv; row < rend; row += kAvcDbWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
@@ -2041,48 +2032,73 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
             }
             wave_sync();
             PROF_LAP(1);
-            const DbInfo cur = ninfo;
+            const uint32_t cur = ninfo;
             {  // parameters of the wave's next MB
                 int nx = mx + 1, ny = row;
                 if (nx == mbw) { nx = 0; ny += kAvcDbWaves; }
-                if (ny < mbh) ninfo = db264_info(mbs, slices, mbw, nx, ny);
+                if (ny < mbh) ninfo = db264_info_raw(mbs, mbw, nx, ny, lane);
             }
-            const int mf = ufl(cur.mf);
+            const uint32_t r0 = __builtin_amdgcn_readlane(cur, 0), r1 = __builtin_amdgcn_readlane(cur, 1);
+            const uint32_t r2 = __builtin_amdgcn_readlane(cur, 2), r3 = __builtin_amdgcn_readlane(cur, 3);
+            const int mf = static_cast<int>((r1 >> 8) & 0xFF), mqp = static_cast<int8_t>(r1 & 0xFF);
+            const int csl = static_cast<int>((r0 >> 8) & 0xFF), tsl = static_cast<int>((r2 >> 8) & 0xFF);
+            const int tmf = row > 0 ? static_cast<int>((r3 >> 8) & 0xFF) : 0, tqp = static_cast<int8_t>(r3 & 0xFF);
+            const h2j_slice* SC = csl < kDbSlices ? &TB.sl[csl] : slices + csl;
+            const int dd = ufl(SC->deblock_disabled);
             PROF_LAP(2);
-            const bool active = (mf & 4) && ufl(cur.dd) != 1;
+            const bool active = (mf & 4) && dd != 1;
             if (active) {
-                const int qm = (mf & 1) ? 0 : ufl(cur.qp);
-                const int tco = ufl(cur.tco), beo = ufl(cur.beo);
-                const int cqo[2] = {static_cast<int>(ufl(cur.cq0)), static_cast<int>(ufl(cur.cq1))};
-                const int saddr = ufl(cur.saddr), dd = ufl(cur.dd);
+                const int qm = (mf & 1) ? 0 : mqp;
+                const int tco = static_cast<int>(ufl(static_cast<uint32_t>(SC->tc_offset)));
+                const int beo = static_cast<int>(ufl(static_cast<uint32_t>(SC->beta_offset)));
+                const int cq0 = static_cast<int>(ufl(static_cast<uint32_t>(SC->cqp_offset[0])));
+                const int cq1 = static_cast<int>(ufl(static_cast<uint32_t>(SC->cqp_offset[1])));
+                const int saddr = static_cast<int>(ufl(static_cast<uint32_t>(SC->slice_addr_rs)));
+                const int tsaddr = row > 0 ? static_cast<int>(ufl(static_cast<uint32_t>(
+                                                 (tsl < kDbSlices ? TB.sl[tsl] : slices[tsl]).slice_addr_rs)))
+                                           : -1;
+                // the MB's nine threshold sets, one per lane, from the LDS tables in one pass:
+                // lane = 3 * component + (0 left MB edge, 1 top MB edge, 2 internal edges)
+                int ta = 0, tb = 0, tt = 0;
+                if (lane < 9) {
+                    const int kind = lane % 3, comp = lane / 3;
+                    const int qleft = (lmf & 1) ? 0 : lqp, qtop = (tmf & 1) ? 0 : tqp;
+                    const int qn = kind == 0 ? qleft : (kind == 1 ? qtop : qm);
+                    int qa;
+                    if (comp == 0) {
+                        qa = (qn + qm + 1) >> 1;
+                    } else {
+                        const int off = comp == 1 ? cq0 : cq1, lo = -6 * (bdc - 8);
+                        const int a = clip3(lo, 51, qn + off), b = clip3(lo, 51, qm + off);
+                        const int qpp = a < 30 ? a : TB.cqp[a - 30], qpq = b < 30 ? b : TB.cqp[b - 30];
+                        qa = (qpp + qpq + 1) >> 1;
+                    }
+                    const int ia = clip3(0, 51, qa + tco), ib = clip3(0, 51, qa + beo);
+                    const int sh = comp ? bdc - 8 : bd - 8;
+                    ta = TB.alpha[ia] << sh;
+                    tb = TB.beta[ib] << sh;
+                    tt = TB.tc0[ia] << sh;
+                }
                 for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
                     const bool vert = dir == 0;
-                    // left neighbour = the previous MB of this row (carried), top neighbour from DbInfo
-                    const int nmf = vert ? (mx > 0 ? lmf : 0) : ufl(cur.tmf);
+                    // left neighbour = the previous MB of this row (carried), top neighbour loaded
+                    const int nmf = vert ? (mx > 0 ? lmf : 0) : tmf;
                     bool mb_edge = (nmf & 4) != 0;
-                    if (mb_edge && dd == 2 && (vert ? lsaddr : static_cast<int>(ufl(cur.tsaddr))) != saddr) mb_edge = false;
-                    const int qn = (nmf & 1) ? 0 : (vert ? lqp : static_cast<int>(ufl(cur.tqp)));
+                    if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
                     for (int e = 0; e < 4; e++) {
                         if (e == 0 && !mb_edge) continue;
                         const int bs = e == 0 ? 4 : 3;
-                        const int qp = e == 0 ? qn : qm;
-                        // thresholds, computed once per edge (scalar)
-                        const int qpav = (qp + qm + 1) >> 1;
-                        const int ia = clip3(0, 51, qpav + tco), ib = clip3(0, 51, qpav + beo);
-                        const int la = kAlpha264[ia] << (bd - 8), lb = kBeta264[ib] << (bd - 8);
-                        const int lt = bs < 4 ? kTc0_264[ia][bs - 1] << (bd - 8) : 0;
+                        const int set = e == 0 ? dir : 2;
+                        const int la = __builtin_amdgcn_readlane(ta, set), lb = __builtin_amdgcn_readlane(tb, set);
+                        const int lt = bs < 4 ? __builtin_amdgcn_readlane(tt, set) : 0;
                         int ca[2] = {0, 0}, cb[2] = {0, 0}, ct[2] = {0, 0};
                         const bool chroma_edge = e == 0 || e == 2;
                         if (chroma_edge) {
 #pragma unroll
                             for (int c = 0; c < 2; c++) {
-                                const int qpp = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qp + cqo[c]));
-                                const int qpq = chroma_qp_264(clip3(-6 * (bdc - 8), 51, qm + cqo[c]));
-                                const int qa = (qpp + qpq + 1) >> 1;
-                                const int ja = clip3(0, 51, qa + tco), jb = clip3(0, 51, qa + beo);
-                                ca[c] = kAlpha264[ja] << (bdc - 8);
-                                cb[c] = kBeta264[jb] << (bdc - 8);
-                                ct[c] = bs < 4 ? kTc0_264[ja][bs - 1] << (bdc - 8) : 0;
+                                ca[c] = __builtin_amdgcn_readlane(ta, 3 + 3 * c + set);
+                                cb[c] = __builtin_amdgcn_readlane(tb, 3 + 3 * c + set);
+                                ct[c] = bs < 4 ? __builtin_amdgcn_readlane(tt, 3 + 3 * c + set) : 0;
                             }
                         }
                         if (lane < 16 && !((e & 1) && (mf & 2))) {  // luma line `lane`
@@ -2100,8 +2116,8 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                 }
             }
             lmf = mf;
-            lqp = ufl(cur.qp);
-            lsaddr = ufl(cur.saddr);
+            lqp = mqp;
+            lsaddr = static_cast<int>(ufl(static_cast<uint32_t>(SC->slice_addr_rs)));
             // write back: left columns (MB x-1), rows above (MB row y-1), the MB itself
             {
                 const int r = lane >> 2, c4 = (lane & 3) * 4;
@@ -2191,21 +2207,33 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
 __global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
                                                                     const h2j_slice* slices, uint8_t* arena,
                                                                     const uint32_t* map) {
+    // LDS: windows | progress | tables | line buffer (db264_lds_bytes)
     extern __shared__ __align__(16) uint8_t dblds[];
     DbWin* W = reinterpret_cast<DbWin*>(dblds);
     uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * kAvcDbWaves);
-    uint16_t* line = reinterpret_cast<uint16_t*>(dblds + sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4);
+    DbTables& TB = *reinterpret_cast<DbTables*>(dblds + sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4);
+    uint16_t* line = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(&TB) + sizeof(DbTables));
     const uint32_t me = map[blockIdx.x];  // same (picture, band) map as K1
     const h2j_frame& f = frames[me >> 8];
     const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264) return;
     const int nbands = ufl(f.k1bands);
-    if (threadIdx.x < 2 * kAvcDbWaves) prog[threadIdx.x] = 0;
-    __syncthreads();
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line, band, nbands);
-    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line, band, nbands);
+    const int t = threadIdx.x;
+    if (t < 2 * kAvcDbWaves) prog[t] = 0;
+    if (t < 52) {
+        TB.alpha[t] = kAlpha264[t];
+        TB.beta[t] = kBeta264[t];
+        TB.tc0[t] = kTc0_264[t][2];
+    }
+    if (t < 22) TB.cqp[t] = kChromaQp264[t];
+    const int nsl = min(static_cast<int>(ufl(f.nslice)), kDbSlices);
+    if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
+        reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
+    __syncthreads();
+    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line, band, nbands, TB);
+    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line, band, nbands, TB);
 }
 
 // ---------------------------------------------------------------- K3: SAO
@@ -2740,7 +2768,7 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         if (r) return r;
     }
     if (!b->has_h264) return 0;
-    const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + 12 * static_cast<size_t>(b->max_w);
+    const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + sizeof(DbTables) + 12 * static_cast<size_t>(b->max_w);
     static bool attr = false;
     if (!attr) {  // line buffers of pictures wider than ~3.6K need more than the 64 KB default
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k2_deblock264),
