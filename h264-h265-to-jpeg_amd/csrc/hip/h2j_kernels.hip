@@ -1835,48 +1835,56 @@ __constant__ int kTc0_264[52][3] = {
 
 __constant__ int kChromaQp264[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
 
-template <typename Pel>
-DEVI void h264_filt_line(Pel* q, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
-    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
-    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-    if (chroma) {
+// H.264 edge filter (8.7.2.3-8.7.2.4) on a line held in registers: the edge lies between
+// v[E - 1] and v[E]; `on` false leaves the line as is.  Selects only (lanes diverge on data).
+template <int E, bool CHROMA, int LEN>
+DEVI void h264_filt_reg(int (&v)[LEN], bool on, int bs, int alpha, int beta, int tc0, int maxv) {
+    static_assert(E >= (CHROMA ? 2 : 4) && E + (CHROMA ? 2 : 4) <= LEN, "edge taps inside the line");
+    const int p0 = v[E - 1], p1 = v[E - 2], q0 = v[E], q1 = v[E + 1];
+    const bool f = on && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta;
+    if constexpr (CHROMA) {
+        int np0, nq0;
         if (bs < 4) {
             const int tc = tc0 + 1;
             const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
-            q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
-            q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
+            np0 = clip3(0, maxv, p0 + dl);
+            nq0 = clip3(0, maxv, q0 - dl);
         } else {
-            q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
-            q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
+            np0 = (2 * p1 + p0 + q1 + 2) >> 2;
+            nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
         }
-        return;
-    }
-    const int p2 = q[-3 * step], q2 = q[2 * step];
+        v[E - 1] = f ? np0 : p0;
+        v[E] = f ? nq0 : q0;
+    } else {
+    const int p2 = v[E - 3], q2 = v[E + 2];
     const int ap = abs(p2 - p0), aq = abs(q2 - q0);
     if (bs < 4) {
         const int tc = tc0 + (ap < beta) + (aq < beta);
         const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
-        q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
-        q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
-        if (ap < beta) q[-2 * step] = static_cast<Pel>(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1));
-        if (aq < beta) q[step] = static_cast<Pel>(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1));
+        const int avg = (p0 + q0 + 1) >> 1;
+        const int np1 = ap < beta ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 * 2)) >> 1) : p1;
+        const int nq1 = aq < beta ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 * 2)) >> 1) : q1;
+        v[E - 1] = f ? clip3(0, maxv, p0 + dl) : p0;
+        v[E] = f ? clip3(0, maxv, q0 - dl) : q0;
+        v[E - 2] = f ? np1 : p1;
+        v[E + 1] = f ? nq1 : q1;
     } else {
-        const int p3 = q[-4 * step], q3 = q[3 * step];
+        const int p3 = v[E - 4], q3 = v[E + 3];
         const bool sm = abs(p0 - q0) < ((alpha >> 2) + 2);
-        if (ap < beta && sm) {
-            q[-step] = static_cast<Pel>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            q[-2 * step] = static_cast<Pel>((p2 + p1 + p0 + q0 + 2) >> 2);
-            q[-3 * step] = static_cast<Pel>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else {
-            q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
-        }
-        if (aq < beta && sm) {
-            q[0] = static_cast<Pel>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            q[step] = static_cast<Pel>((p0 + q0 + q1 + q2 + 2) >> 2);
-            q[2 * step] = static_cast<Pel>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else {
-            q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
-        }
+        const bool sp = ap < beta && sm, sq = aq < beta && sm;
+        const int np0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
+        const int np1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
+        const int np2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
+        const int nq0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
+        const int nq1 = sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1;
+        const int nq2 = sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
+        v[E - 1] = f ? np0 : p0;
+        v[E - 2] = f ? np1 : p1;
+        v[E - 3] = f ? np2 : p2;
+        v[E] = f ? nq0 : q0;
+        v[E + 1] = f ? nq1 : q1;
+        v[E + 2] = f ? nq2 : q2;
+    }
     }
 }
 
@@ -2079,40 +2087,57 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                     tb = TB.beta[ib] << sh;
                     tt = TB.tc0[ia] << sh;
                 }
+                // Each lane filters a whole line through all edges of a direction in registers
+                // (lanes 0-15: luma rows / columns, 32-47: chroma rows / columns), one LDS
+                // round trip per direction instead of one per edge.  Edge e of a direction: the MB
+                // edge (e = 0, bS 4, if filtered at all) or internal (bS 3; luma e = 1, 3 not in
+                // 8x8-transform MBs; chroma only e = 0, 2).
+                const bool t8 = (mf & 2) != 0;
+                const bool luma_lane = lane < 16, chroma_lane = lane >= 32 && lane < 48;
+                const int cc = (lane - 32) >> 3, ck = lane & 7;  // chroma lanes: component, line
+                const int maxy = (1 << bd) - 1, maxc = (1 << bdc) - 1;
                 for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
                     const bool vert = dir == 0;
                     // left neighbour = the previous MB of this row (carried), top neighbour loaded
                     const int nmf = vert ? (mx > 0 ? lmf : 0) : tmf;
                     bool mb_edge = (nmf & 4) != 0;
                     if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
-                    for (int e = 0; e < 4; e++) {
-                        if (e == 0 && !mb_edge) continue;
-                        const int bs = e == 0 ? 4 : 3;
-                        const int set = e == 0 ? dir : 2;
-                        const int la = __builtin_amdgcn_readlane(ta, set), lb = __builtin_amdgcn_readlane(tb, set);
-                        const int lt = bs < 4 ? __builtin_amdgcn_readlane(tt, set) : 0;
-                        int ca[2] = {0, 0}, cb[2] = {0, 0}, ct[2] = {0, 0};
-                        const bool chroma_edge = e == 0 || e == 2;
-                        if (chroma_edge) {
+                    const int la0 = __builtin_amdgcn_readlane(ta, dir), lb0 = __builtin_amdgcn_readlane(tb, dir);
+                    const int la1 = __builtin_amdgcn_readlane(ta, 2), lb1 = __builtin_amdgcn_readlane(tb, 2);
+                    const int lt1 = __builtin_amdgcn_readlane(tt, 2);
+                    if (luma_lane) {
+                        int v[20];
+                        const int stp = vert ? 1 : 20;
+                        const uint16_t* src = vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4];
 #pragma unroll
-                            for (int c = 0; c < 2; c++) {
-                                ca[c] = __builtin_amdgcn_readlane(ta, 3 + 3 * c + set);
-                                cb[c] = __builtin_amdgcn_readlane(tb, 3 + 3 * c + set);
-                                ct[c] = bs < 4 ? __builtin_amdgcn_readlane(tt, 3 + 3 * c + set) : 0;
-                            }
-                        }
-                        if (lane < 16 && !((e & 1) && (mf & 2))) {  // luma line `lane`
-                            uint16_t* q = vert ? &w.y[lane + 4][e * 4 + 4] : &w.y[e * 4 + 4][lane + 4];
-                            h264_filt_line<uint16_t>(q, vert ? 1 : 20, bs, la, lb, lt, false, (1 << bd) - 1);
-                        } else if (lane >= 32 && lane < 48 && chroma_edge) {  // chroma line
-                            const int c = (lane - 32) >> 3, k = lane & 7;
-                            uint16_t* q = vert ? &w.c[c][k + 2][e * 2 + 2] : &w.c[c][e * 2 + 2][k + 2];
-                            h264_filt_line<uint16_t>(q, vert ? 1 : 10, bs, c ? ca[1] : ca[0], c ? cb[1] : cb[0],
-                                                     c ? ct[1] : ct[0], true, (1 << bdc) - 1);
-                        }
-                        wave_sync();
-                        PROF_LAPK(dir * 4 + e);
+                        for (int i = 0; i < 20; i++) v[i] = src[i * stp];
+                        h264_filt_reg<4, false>(v, mb_edge, 4, la0, lb0, 0, maxy);
+                        h264_filt_reg<8, false>(v, !t8, 3, la1, lb1, lt1, maxy);
+                        h264_filt_reg<12, false>(v, true, 3, la1, lb1, lt1, maxy);
+                        h264_filt_reg<16, false>(v, !t8, 3, la1, lb1, lt1, maxy);
+                        uint16_t* dst = vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4];
+#pragma unroll
+                        for (int i = 1; i < 19; i++) dst[i * stp] = static_cast<uint16_t>(v[i]);
+                    } else if (chroma_lane) {
+                        // Cb sets 3..5, Cr sets 6..8: fetch both, select per lane
+                        const int a0 = __builtin_amdgcn_readlane(ta, 3 + dir), a3 = __builtin_amdgcn_readlane(ta, 6 + dir);
+                        const int b0 = __builtin_amdgcn_readlane(tb, 3 + dir), b3 = __builtin_amdgcn_readlane(tb, 6 + dir);
+                        const int a1 = __builtin_amdgcn_readlane(ta, 5), a4 = __builtin_amdgcn_readlane(ta, 8);
+                        const int b1 = __builtin_amdgcn_readlane(tb, 5), b4 = __builtin_amdgcn_readlane(tb, 8);
+                        const int t1 = __builtin_amdgcn_readlane(tt, 5), t4 = __builtin_amdgcn_readlane(tt, 8);
+                        int v[10];
+                        const int stp = vert ? 1 : 10;
+                        const uint16_t* src = vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) v[i] = src[i * stp];
+                        h264_filt_reg<2, true>(v, mb_edge, 4, cc ? a3 : a0, cc ? b3 : b0, 0, maxc);
+                        h264_filt_reg<6, true>(v, true, 3, cc ? a4 : a1, cc ? b4 : b1, cc ? t4 : t1, maxc);
+                        uint16_t* dst = vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2];
+#pragma unroll
+                        for (int i = 1; i < 7; i++) dst[i * stp] = static_cast<uint16_t>(v[i]);
                     }
+                    wave_sync();
+                    PROF_LAPK(dir * 4);
                 }
             }
             lmf = mf;
