@@ -1229,7 +1229,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     // neighbour sample -> element index relative to `body` (top / left sit at fixed offsets)
     const int topo = static_cast<int>(top - body), lefto = static_cast<int>(left - body);
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    int dcpart = 0;
+    int dcpart = 0, v0 = 0;
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
         if (ch < nch) {
@@ -1241,7 +1241,8 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             const int idx = yn < 0 ? topo + xn + 1 : (xn < 0 ? lefto + yn : yn * S + xn);
             const int raw = body[idx];  // unconditional: idx stays inside the wave's window
             const int v = any ? raw : (1 << (bd - 1));
-            s.sub[k < L ? k : 131] = static_cast<int16_t>(v);
+            if (ch == 0) v0 = v;
+            if (nch > 1) s.sub[k < L ? k : 131] = static_cast<int16_t>(v);
             // DC: p(-1, 0..n-1) = k in [n, 2n), p(0..n-1, -1) = k in [2n+1, 3n]
             dcpart += (k >= n && k <= 3 * n && k != 2 * n) ? v : 0;
         }
@@ -1256,6 +1257,56 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     }
     int dc = 0;
     if (mode == 1) dc = (wave_sum_dpp(dcpart) + n) >> (log2n + 1);
+    const int edge = c == 0 && n < 32;  // DC / pure horizontal / pure vertical boundary smoothing
+    if (nch == 1) {
+        // L <= 64 (n <= 8 luma, chroma <= 8): lane k keeps reference k in a register; the
+        // filter and the prediction read neighbours by ds_bpermute (__shfl) instead of an LDS
+        // write, a barrier and LDS reads.  Only luma 8x8 is ever filtered here (no strong filter).
+        int r = v0;
+        if (filt) {
+            const int vl = __shfl(v0, lane - 1, 64), vr = __shfl(v0, lane + 1, 64);
+            r = (lane == 0 || lane == 4 * n) ? v0 : (vl + 2 * v0 + vr + 2) >> 2;
+        }
+        const int i = lane, x = i & (n - 1), y = i >> log2n;
+        int pv;
+        if (mode == 0) {
+            const int tr = __builtin_amdgcn_readlane(r, 3 * n + 1), bl = __builtin_amdgcn_readlane(r, n - 1);
+            const int left = __shfl(r, 2 * n - 1 - y, 64), above = __shfl(r, 2 * n + 1 + x, 64);
+            pv = ((n - 1 - x) * left + (x + 1) * tr + (n - 1 - y) * above + (y + 1) * bl + n) >> (log2n + 1);
+        } else if (mode == 1) {
+            const int above = __shfl(r, 2 * n + 1 + x, 64), left = __shfl(r, 2 * n - 1 - y, 64);
+            pv = dc;
+            if (edge && (x == 0 || y == 0)) {
+                if (x == 0 && y == 0) pv = (left + 2 * dc + above + 2) >> 2;
+                else if (y == 0) pv = (above + 3 * dc + 2) >> 2;
+                else pv = (left + 3 * dc + 2) >> 2;
+            }
+        } else {
+            const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+            const bool vert = mode >= 18;
+            const int sgn = vert ? 1 : -1;
+            const bool bnd = edge && (mode == 26 || mode == 10);
+            const int a = vert ? y : x, b = vert ? x : y;
+            const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+            const int k1 = b + idx + 1, k2 = k1 + 1;
+            const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
+            const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
+            const int r1 = __shfl(r, 2 * n + sgn * o1, 64), r2 = __shfl(r, 2 * n + sgn * o2, 64);
+            pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            if (bnd) {
+                const int side = __shfl(r, 2 * n - sgn * (a + 1), 64);
+                const int e = clip3(0, maxv, __builtin_amdgcn_readlane(r, 2 * n + sgn) +
+                                                 ((side - __builtin_amdgcn_readlane(r, 2 * n)) >> 1));
+                pv = b == 0 ? e : pv;
+            }
+        }
+        if (i < nn) {
+            int16_t* d = body + (oy + y) * S + ox + x;
+            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+        }
+        wave_sync();
+        return;
+    }
     wave_sync();
     if (filt) {
         const int corner = s.sub[2 * n];
@@ -1284,7 +1335,6 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
 #endif
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
     const int16_t* R = filt ? s.ref : s.sub;
-    const int edge = c == 0 && n < 32;  // DC / pure horizontal / pure vertical boundary smoothing
     if (mode == 0) {
         const int tr = R[3 * n + 1], bl = R[n - 1];
         for (int i = lane; i < nn; i += 64) {
