@@ -1688,17 +1688,30 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
 // launch instead of three back-to-back ones, so the pictures' chains run side by side (each
 // launch alone is one long chain per picture and leaves most of the GPU idle).  Workgroups of
 // 16 waves: an HEVC picture's luma group (waves 0-7) and chroma group (waves 8-15) share one
-// workgroup; an H.264 workgroup is one band as in h2j_k1_recon_h264.  `map`: the host's list,
-// longest chains first; bit 31 marks HEVC entries.  `gbytes`: LDS bytes of one HEVC group.
+// workgroup; an H.264 workgroup is one band as in h2j_k1_recon_h264.  Tall HEVC pictures (the
+// longest chains of such a batch) instead get one 16-wave workgroup per component group, twice
+// the rows in flight.  `map`: the host's list, longest chains first; bit 31 marks HEVC entries,
+// bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).  `gbytes`: LDS bytes of one 8-wave HEVC
+// group.
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_frame* frames, const h2j_tu* tus,
                                                                  uint8_t* arena, const uint32_t* map,
                                                                  uint32_t gbytes) {
     static_assert(2 * kK1Waves == kAvcWaves, "an HEVC picture's two groups fill one H.264-sized workgroup");
     extern __shared__ __align__(16) uint8_t anylds[];
     const uint32_t me = map[blockIdx.x];
-    const h2j_frame& f = frames[(me >> 8) & 0x7FFFFFu];
+    const h2j_frame& f = frames[(me >> 8) & 0x3FFFFFu];
     const h2j_tu* T = tus + ufl(f.tu);
-    if (me & 0x80000000u) {
+    if ((me & 0xC0000000u) == 0xC0000000u) {  // one 16-wave HEVC group
+        const int grp = static_cast<int>(me & 1);
+        QWave* W = reinterpret_cast<QWave*>(anylds);
+        uint32_t* prog = reinterpret_cast<uint32_t*>(anylds + sizeof(QWave) * kK1WavesWide);
+        int16_t* line = reinterpret_cast<int16_t*>(anylds + k1_fixed_lds(kK1WavesWide));
+        if (threadIdx.x < 2 * kK1WavesWide) prog[threadIdx.x] = 0;
+        __syncthreads();
+        const int wv = static_cast<int>(threadIdx.x >> 6);
+        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t, kK1WavesWide>(f, T, arena, grp, W, prog, line, wv);
+        else hevc_rows<uint16_t, kK1WavesWide>(f, T, arena, grp, W, prog, line, wv);
+    } else if (me & 0x80000000u) {
         const int grp = static_cast<int>(threadIdx.x >> 9);
         uint8_t* gb = anylds + grp * gbytes;
         QWave* W = reinterpret_cast<QWave*>(gb);
@@ -2790,7 +2803,8 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     }();
     if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0) {  // one launch for every kind of picture
         const size_t gbytes = (k1_fixed_lds(kK1Waves) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t) + 15) & ~size_t(15);
-        const size_t lds = std::max(2 * gbytes, lds264);
+        const size_t wbytes = k1_fixed_lds(kK1WavesWide) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
+        const size_t lds = std::max(std::max(2 * gbytes, lds264), wbytes);
         if (lds > 160 * 1024) {
             snprintf(g_err, sizeof(g_err), "h2j_k1_recon_any: %zu B of LDS per workgroup (max 160 KB)", lds);
             return -1;

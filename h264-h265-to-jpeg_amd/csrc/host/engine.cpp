@@ -339,8 +339,14 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         std::vector<std::pair<int, uint32_t>> e;
         for (int k = 0; k < nf; k++) {
             const h2j_frame& f = s.frames[k];
-            const int rows = f.codec == H2J_CODEC_H264 ? std::min(f.ctb_h, 16) : f.ctb_h << (f.log2ctb - 4);
-            if (f.codec == H2J_CODEC_HEVC) e.emplace_back(-rows, (1u << 31) | (static_cast<uint32_t>(k) << 8));
+            if (f.codec != H2J_CODEC_HEVC) continue;
+            const int rows = f.ctb_h << (f.log2ctb - 4);  // in 16-sample rows
+            if (rows > kK1BandRows) {  // taller than 1088: a 16-wave workgroup per component group
+                e.emplace_back(-2000 - rows, (3u << 30) | (static_cast<uint32_t>(k) << 8) | 0u);
+                e.emplace_back(-2000 - rows, (3u << 30) | (static_cast<uint32_t>(k) << 8) | 1u);
+            } else {
+                e.emplace_back(-rows, (1u << 31) | (static_cast<uint32_t>(k) << 8));
+            }
         }
         for (uint32_t m : k1map) {
             const h2j_frame& f = s.frames[m >> 8];

@@ -90,10 +90,12 @@ def test_mixed_workload_batch(engine):
 
 
 def test_merged_k1_launch_mixed_kinds(engine):
-    """A batch of more than 128 pictures mixing HEVC 8-bit, HEVC 10-bit and H.264
-    runs K1 as one merged launch (h2j_k1_recon_any); every JPEG byte-exact."""
+    """A batch of more than 128 pictures mixing HEVC 8-bit, HEVC 10-bit (incl. a 4K
+    picture on 16-wave groups) and H.264 (incl. a banded 4K picture) runs K1 as one
+    merged launch (h2j_k1_recon_any); every JPEG byte-exact."""
     hevc = sorted(glob.glob(os.path.join(golden("hevc"), "*.h265")))
-    kinds = [read(p) for p in PARITY264 + hevc]
+    tall = [sorted(glob.glob(os.path.join(golden("bench4k"), "*.h265")))[0], golden("mixed/avc2160_00.h264")]
+    kinds = [read(p) for p in tall + PARITY264 + hevc]  # 4K HEVC: 16-wave groups; 4K H.264: bands
     assert any("10bit" in p for p in hevc)
     streams = [kinds[i % len(kinds)] for i in range(160)]
     want = {i: O.transcode(s) for i, s in enumerate(kinds)}
