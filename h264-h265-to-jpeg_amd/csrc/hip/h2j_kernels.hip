@@ -2801,14 +2801,13 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         const char* e = std::getenv("H2J_K1_MERGE");
         return !(e && e[0] == '0');
     }();
-    if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0) {  // one launch for every kind of picture
-        const size_t gbytes = (k1_fixed_lds(kK1Waves) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t) + 15) & ~size_t(15);
-        const size_t wbytes = k1_fixed_lds(kK1WavesWide) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-        const size_t lds = std::max(std::max(2 * gbytes, lds264), wbytes);
-        if (lds > 160 * 1024) {
-            snprintf(g_err, sizeof(g_err), "h2j_k1_recon_any: %zu B of LDS per workgroup (max 160 KB)", lds);
-            return -1;
-        }
+    const size_t gbytes = (k1_fixed_lds(kK1Waves) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t) + 15) & ~size_t(15);
+    const size_t wbytes = k1_fixed_lds(kK1WavesWide) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
+    const size_t lds_any = std::max(std::max(2 * gbytes, lds264), wbytes);
+    // one launch for every kind of picture (unless the widest picture's line buffers would not
+    // fit one workgroup's LDS: then the per-kind launches below)
+    if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
+        const size_t lds = lds_any;
         hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
                            b->arena, b->k1all, static_cast<uint32_t>(gbytes));
         return check(hipGetLastError(), "h2j_k1_recon_any");
