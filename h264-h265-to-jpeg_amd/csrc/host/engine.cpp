@@ -586,8 +586,12 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     std::mutex mu;
     std::condition_variable cv;
     double t_parsed = t0;
+    // batches smaller than the thread pool (a lone IDecoder call): pictures with several
+    // independent slices parse them on several threads
+    const int slice_threads = std::max(1, (e.pool->size() + 1) / std::max(1, n));
     auto parse_all = [&]() {
         e.pool->parallel_for(n, [&](int i) {
+            e.jobs[i].threads = slice_threads;
             h2j::parse_any(data[i], sizes[i], e.jobs[i]);
             if (left[chunk_of[i]].fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> g(mu);
@@ -689,6 +693,7 @@ static int single_job(h2j_engine* w, const uint8_t* data, size_t size) {
     Engine& e = w->e;
     if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
     if (e.jobs.empty()) e.jobs.resize(1);
+    e.jobs[0].threads = e.pool->size() + 1;  // independent slices on several threads
     int r = h2j::parse_any(data, size, e.jobs[0]);
     if (r) return e.fail("parse failed: " + e.jobs[0].message);
     e.slot[0].live.assign(1, 0);

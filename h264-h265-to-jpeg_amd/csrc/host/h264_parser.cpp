@@ -12,6 +12,9 @@
 // Macroblocks reuse the h2j_ctb record (log2ctb 4): slice, address, QPY,
 // I_PCM / transform_size_8x8 flags for intra availability and deblocking.
 #include <algorithm>
+#include <atomic>
+#include <memory>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 
@@ -370,13 +373,27 @@ const CavlcLut& cavlc_lut() {
     return lut;
 }
 
+// slice data kept for the decode pass (after all slice headers of the picture are read)
+struct SliceWork {
+    bool cabac = true;
+    std::vector<uint8_t> data;  // CABAC: bytes after the header (+8 zero bytes); CAVLC: the whole RBSP
+    size_t nbytes = 0;          // valid bytes of data
+    size_t bitpos = 0;          // CAVLC: first bit of the slice data
+    size_t stop_bit = 0;        // CAVLC: position of the rbsp_stop_one_bit
+    int qp = 0, first_mb = 0, index = 0, pps_id = 0;
+};
+
 class H264Parser {
 public:
-    explicit H264Parser(FrameJob& job) : job_(job) {}
-    int run(const uint8_t* data, size_t size);
+    explicit H264Parser(FrameJob& job) : job_(&job) {}
+    // a worker for other slices of the same picture: picture state copied, its own outputs
+    H264Parser(const H264Parser& proto, FrameJob& job) : H264Parser(proto) { job_ = &job; }
+    int run(const uint8_t* data, size_t size, int threads);
 
 private:
-    FrameJob& job_;
+    H264Parser(const H264Parser&) = default;
+    int decode_slice(const SliceWork& w);
+    FrameJob* job_;
     Sps sps_[32];
     Pps pps_[256];
     const Sps* s_ = nullptr;
@@ -510,11 +527,11 @@ void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, c
     t.mode = static_cast<uint8_t>(mode);
     t.qp = static_cast<int8_t>(qp);
     t.qpy = static_cast<int8_t>(qp_);
-    t.coef = static_cast<uint32_t>(job_.coefs.size());
-    job_.coefs.insert(job_.coefs.end(), e, e + n);
+    t.coef = static_cast<uint32_t>(job_->coefs.size());
+    job_->coefs.insert(job_->coefs.end(), e, e + n);
     t.ncoef = static_cast<uint16_t>(n);
     t.flags = n ? H2J_TU_CBF : 0;
-    job_.tus.push_back(t);
+    job_->tus.push_back(t);
 }
 
 void H264Parser::emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos,
@@ -527,12 +544,12 @@ void H264Parser::emit(int x, int y, int log2n, int c, int mode, uint8_t flags, i
     t.mode = static_cast<uint8_t>(mode);
     t.qp = static_cast<int8_t>(qp);
     t.qpy = static_cast<int8_t>(qp_);
-    t.coef = static_cast<uint32_t>(job_.coefs.size());
+    t.coef = static_cast<uint32_t>(job_->coefs.size());
     for (int i = 0; i < npos; i++)
-        if (lv[i] || pcm) job_.coefs.push_back((static_cast<uint32_t>(i) << 16) | static_cast<uint16_t>(lv[i]));
-    t.ncoef = static_cast<uint16_t>(job_.coefs.size() - t.coef);
+        if (lv[i] || pcm) job_->coefs.push_back((static_cast<uint32_t>(i) << 16) | static_cast<uint16_t>(lv[i]));
+    t.ncoef = static_cast<uint16_t>(job_->coefs.size() - t.coef);
     t.flags = flags | (t.ncoef ? H2J_TU_CBF : 0);
-    job_.tus.push_back(t);
+    job_->tus.push_back(t);
 }
 
 int chroma_qp_264(int qpi) {
@@ -545,7 +562,7 @@ void H264Parser::decode_mb() {
     m = Mb();
     m.slice = cur_slice_;
     const int gx = mbx_ * 16, gy = mby_ * 16;
-    h2j_ctb& rec = job_.ctbs[mby_ * mbw_ + mbx_];
+    h2j_ctb& rec = job_->ctbs[mby_ * mbw_ + mbx_];
     rec.slice = static_cast<uint8_t>(cur_slice_);
     rec.mbflags = 4;
     // mb_type (I slice)
@@ -881,7 +898,7 @@ void H264Parser::decode_mb_cavlc() {
     m = Mb();
     m.slice = cur_slice_;
     const int gx = mbx_ * 16, gy = mby_ * 16;
-    h2j_ctb& rec = job_.ctbs[mby_ * mbw_ + mbx_];
+    h2j_ctb& rec = job_->ctbs[mby_ * mbw_ + mbx_];
     rec.slice = static_cast<uint8_t>(cur_slice_);
     rec.mbflags = 4;
     const uint32_t mbt = vb_.ue();
@@ -1031,14 +1048,14 @@ void H264Parser::decode_mb_cavlc() {
     if (vb_.overrun()) err_ = -45;
 }
 
-int H264Parser::run(const uint8_t* data, size_t size) {
+int H264Parser::run(const uint8_t* data, size_t size, int threads) {
     std::vector<Nal> nals;
     split_annexb(data, size, nals);
     rbsp_.resize(size + 16);
     bool have = false;
     int first_frame_num = -1, first_idr = -1;
     int nslice = 0;
-    std::vector<uint8_t> keep;
+    std::vector<SliceWork> works;
     for (const Nal& nal : nals) {
         if (nal.n < 1) continue;
         const int nal_ref_idc = (nal.p[0] >> 5) & 3;
@@ -1047,23 +1064,23 @@ int H264Parser::run(const uint8_t* data, size_t size) {
         BitReader b(rbsp_.data(), rn);
         if (type == 7) {
             if (have) break;
-            if (parse_sps(b, sps_) < 0) { job_.message = "unsupported or invalid SPS"; return -2; }
+            if (parse_sps(b, sps_) < 0) { job_->message = "unsupported or invalid SPS"; return -2; }
         } else if (type == 8) {
             if (have) break;
-            if (parse_pps(b, pps_, sps_) < 0) { job_.message = "unsupported or invalid PPS"; return -3; }
+            if (parse_pps(b, pps_, sps_) < 0) { job_->message = "unsupported or invalid PPS"; return -3; }
         } else if (type == 1 || type == 5) {
             const int first_mb = static_cast<int>(b.ue());
             const int slice_type = static_cast<int>(b.ue());
             const uint32_t pps_id = b.ue();
             if (pps_id > 255 || !pps_[pps_id].valid || !sps_[pps_[pps_id].sps_id].valid) {
-                job_.message = "slice references a missing parameter set";
+                job_->message = "slice references a missing parameter set";
                 return -4;
             }
             const Pps& p = pps_[pps_id];
             const Sps& s = sps_[p.sps_id];
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
-            if (slice_type % 5 != 2) { job_.message = "first picture is not intra (P/B slices unsupported)"; return -5; }
+            if (slice_type % 5 != 2) { job_->message = "first picture is not intra (P/B slices unsupported)"; return -5; }
             if (type == 5) b.ue();
             if (s.poc_type == 0) {
                 b.u(s.log2_max_poc_lsb);
@@ -1106,11 +1123,11 @@ int H264Parser::run(const uint8_t* data, size_t size) {
                 mbh_ = s.mb_h;
                 qpbd_ = 6 * (s.bit_depth - 8);
                 mb_.assign(static_cast<size_t>(mbw_) * mbh_, Mb());
-                job_.ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
-                for (int i = 0; i < mbw_ * mbh_; i++) job_.ctbs[i].ts = static_cast<uint32_t>(i);
-                job_.tus.reserve(static_cast<size_t>(mbw_) * mbh_ * 10);
-                job_.coefs.reserve(static_cast<size_t>(mbw_) * mbh_ * 64);
-                h2j_frame& f = job_.hdr;
+                job_->ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
+                for (int i = 0; i < mbw_ * mbh_; i++) job_->ctbs[i].ts = static_cast<uint32_t>(i);
+                job_->tus.reserve(static_cast<size_t>(mbw_) * mbh_ * 10);
+                job_->coefs.reserve(static_cast<size_t>(mbw_) * mbh_ * 64);
+                h2j_frame& f = job_->hdr;
                 f.codec = H2J_CODEC_H264;
                 f.width = mbw_ * 16;
                 f.height = mbh_ * 16;
@@ -1128,10 +1145,10 @@ int H264Parser::run(const uint8_t* data, size_t size) {
                 f.lf_across_tiles = 1;
                 if (s.scaling_present || p.transform_8x8) {
                     // weight scale tables (raster), used by K1 for every H.264 frame with this flag
-                    job_.sl.assign(H2J_SL264_BYTES, 16);
+                    job_->sl.assign(H2J_SL264_BYTES, 16);
                     for (int c = 0; c < 3; c++)
-                        for (int k = 0; k < 16; k++) job_.sl[H2J_SL264_4 + c * 16 + kZz4[k]] = p.sl4[c][k];
-                    for (int k = 0; k < 64; k++) job_.sl[H2J_SL264_8 + kZz8[k]] = p.sl8[0][k];
+                        for (int k = 0; k < 16; k++) job_->sl[H2J_SL264_4 + c * 16 + kZz4[k]] = p.sl4[c][k];
+                    for (int k = 0; k < 64; k++) job_->sl[H2J_SL264_8 + kZz8[k]] = p.sl8[0][k];
                     f.scaling_list = 1;
                 }
                 have = true;
@@ -1139,60 +1156,121 @@ int H264Parser::run(const uint8_t* data, size_t size) {
                 first_idr = type == 5;
             }
             p_ = &p;
-            if (job_.hdr.scaling_list == 0 && (p.transform_8x8 || s.scaling_present)) {
-                job_.message = "scaling matrices changed inside the picture";
+            if (job_->hdr.scaling_list == 0 && (p.transform_8x8 || s.scaling_present)) {
+                job_->message = "scaling matrices changed inside the picture";
                 return -6;
             }
-            cur_slice_ = nslice;
-            job_.slices.push_back(srec);
-            qp_ = p.init_qp + qpd;
-            if (qp_ < -qpbd_ || qp_ > 51) { job_.message = "invalid slice QP"; return -6; }
-            prev_qpd_nz_ = 0;
-            int addr = first_mb;
-            if (p.cabac) {
+            job_->slices.push_back(srec);
+            works.emplace_back();
+            SliceWork& w = works.back();
+            w.index = nslice;
+            w.pps_id = static_cast<int>(pps_id);
+            w.first_mb = first_mb;
+            w.qp = p.init_qp + qpd;
+            if (w.qp < -qpbd_ || w.qp > 51) { job_->message = "invalid slice QP"; return -6; }
+            w.cabac = p.cabac != 0;
+            if (w.cabac) {
                 b.align();  // cabac_alignment_one_bit
                 const size_t off = b.byte_pos();
-                if (off > rn) { job_.message = "truncated slice"; return -6; }
-                keep.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
-                keep.resize(keep.size() + 8, 0);
-                end_ = keep.data() + (rn - off);
-                cc_.init(keep.data(), end_);
-                for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_state(kInitI[i][0], kInitI[i][1], qp_);
-                for (;;) {
-                    if (addr >= mbw_ * mbh_) { job_.message = "slice overruns the picture"; return -7; }
-                    mbx_ = addr % mbw_;
-                    mby_ = addr / mbw_;
-                    decode_mb();
-                    if (err_) { job_.message = "macroblock decode error"; return -7; }
-                    if (cc_.terminate()) break;
-                    addr++;
-                }
+                if (off > rn) { job_->message = "truncated slice"; return -6; }
+                w.data.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
+                w.nbytes = rn - off;
+                w.data.resize(w.nbytes + 8, 0);
             } else {
                 // CAVLC: macroblocks until the rbsp_stop_one_bit
                 size_t last = rn;
                 while (last > 0 && rbsp_[last - 1] == 0) last--;
-                if (!last) { job_.message = "empty slice data"; return -6; }
-                stop_bit_ = (last - 1) * 8 + 7 - static_cast<size_t>(__builtin_ctz(rbsp_[last - 1]));
-                vb_.init(rbsp_.data(), rn, b.bit_pos());
-                for (;;) {
-                    if (addr >= mbw_ * mbh_) { job_.message = "slice overruns the picture"; return -7; }
-                    mbx_ = addr % mbw_;
-                    mby_ = addr / mbw_;
-                    decode_mb_cavlc();
-                    if (err_) { job_.message = "macroblock decode error"; return -7; }
-                    if (!vb_.more_rbsp_data(stop_bit_)) break;
-                    addr++;
-                }
+                if (!last) { job_->message = "empty slice data"; return -6; }
+                w.stop_bit = (last - 1) * 8 + 7 - static_cast<size_t>(__builtin_ctz(rbsp_[last - 1]));
+                w.data.assign(rbsp_.begin(), rbsp_.begin() + static_cast<long>(rn));
+                w.nbytes = rn;
+                w.bitpos = b.bit_pos();
+                w.data.resize(rn + 8, 0);
             }
-            if (++nslice >= 255) { job_.message = "too many slices"; return -8; }
+            if (++nslice >= 255) { job_->message = "too many slices"; return -8; }
         } else if (type == 9 && have) {
             break;
         }
     }
-    if (!have) { job_.message = "no picture found"; return -9; }
-    job_.hdr.nslice = static_cast<uint32_t>(job_.slices.size());
-    job_.hdr.topo = (job_.slices.size() != 1 || job_.slices[0].slice_addr_rs != 0) ? 1u : 0u;
-    job_.hdr.ntu = static_cast<uint32_t>(job_.tus.size());
+    if (!have) { job_->message = "no picture found"; return -9; }
+    // Slices share nothing for parsing (CABAC / CAVLC restart, neighbours in other slices are
+    // unavailable): with threads > 1 they decode side by side, slice 0 into this job, the
+    // others into their own jobs, appended in decoding order.
+    const int ns = static_cast<int>(works.size());
+    if (threads <= 1 || ns <= 1) {
+        for (int k = 0; k < ns; k++) {
+            const int e = decode_slice(works[k]);
+            if (e) return e;
+        }
+    } else {
+        std::vector<FrameJob> part(ns);
+        std::vector<std::unique_ptr<H264Parser>> wk(ns);
+        for (int k = 1; k < ns; k++) {  // clones first: slice 0 then mutates this parser's state
+            part[k].ctbs = job_->ctbs;
+            wk[k].reset(new H264Parser(*this, part[k]));
+        }
+        std::vector<int> rc(ns, 0);
+        std::atomic<int> next(1);
+        auto work = [&]() {
+            for (int k = next++; k < ns; k = next++) rc[k] = wk[k]->decode_slice(works[k]);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < std::min(threads, ns); t++) pool.emplace_back(work);
+        rc[0] = decode_slice(works[0]);
+        work();
+        for (auto& t : pool) t.join();
+        for (int k = 1; k < ns; k++)
+            if (rc[k]) { job_->message = part[k].message; return rc[k]; }
+        if (rc[0]) return rc[0];
+        for (int k = 1; k < ns; k++) {
+            const uint32_t cbase = static_cast<uint32_t>(job_->coefs.size());
+            for (h2j_tu t : part[k].tus) {
+                t.coef += cbase;  // (every record carries its position in the coefficient stream)
+                job_->tus.push_back(t);
+            }
+            job_->coefs.insert(job_->coefs.end(), part[k].coefs.begin(), part[k].coefs.end());
+            for (size_t m = 0; m < wk[k]->mb_.size(); m++)
+                if (wk[k]->mb_[m].slice == k) job_->ctbs[m] = part[k].ctbs[m];
+        }
+    }
+    job_->hdr.nslice = static_cast<uint32_t>(job_->slices.size());
+    job_->hdr.topo = (job_->slices.size() != 1 || job_->slices[0].slice_addr_rs != 0) ? 1u : 0u;
+    job_->hdr.ntu = static_cast<uint32_t>(job_->tus.size());
+    return 0;
+}
+
+int H264Parser::decode_slice(const SliceWork& w) {
+    p_ = &pps_[w.pps_id];  // this parser's own copy of the parameter sets
+    cur_slice_ = w.index;
+    qp_ = w.qp;
+    prev_qpd_nz_ = 0;
+    int addr = w.first_mb;
+    if (w.cabac) {
+        end_ = w.data.data() + w.nbytes;
+        cc_.init(w.data.data(), end_);
+        for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_state(kInitI[i][0], kInitI[i][1], qp_);
+        for (;;) {
+            if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
+            mbx_ = addr % mbw_;
+            mby_ = addr / mbw_;
+            decode_mb();
+            if (err_) { job_->message = "macroblock decode error"; return -7; }
+            if (cc_.terminate()) break;
+            addr++;
+        }
+    } else {
+        stop_bit_ = w.stop_bit;
+        vb_.init(w.data.data(), w.nbytes, w.bitpos);
+        for (;;) {
+            if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
+            mbx_ = addr % mbw_;
+            mby_ = addr / mbw_;
+            decode_mb_cavlc();
+            if (err_) { job_->message = "macroblock decode error"; return -7; }
+            if (!vb_.more_rbsp_data(stop_bit_)) break;
+            addr++;
+        }
+    }
     return 0;
 }
 
@@ -1200,8 +1278,8 @@ int H264Parser::run(const uint8_t* data, size_t size) {
 
 int h264_parse_picture(const uint8_t* data, size_t size, FrameJob& job) {
     job.clear();
-    H264Parser p(job);
-    const int r = p.run(data, size);
+    std::unique_ptr<H264Parser> p(new H264Parser(job));  // large (parameter-set tables): heap
+    const int r = p->run(data, size, job.threads);
     job.error = r;
     return r;
 }

@@ -9,8 +9,12 @@
 // (include/h2j_jobs.h); dequantisation, transforms, intra prediction and
 // the loop filters run on the GPU.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
 
 #include "bitstream.h"
 #include "cabac.h"
@@ -374,11 +378,15 @@ int chroma_qp_table(int qpi) {
 
 class HevcParser {
 public:
-    explicit HevcParser(FrameJob& job) : job_(job) {}
-    int run(const uint8_t* data, size_t size);
+    explicit HevcParser(FrameJob& job) : job_(&job) {}
+    // a worker for one slice group of the same picture: the picture state (parameter sets,
+    // geometry, maps, slice headers) copied, its own outputs
+    HevcParser(const HevcParser& proto, FrameJob& job) : HevcParser(proto) { job_ = &job; }
+    int run(const uint8_t* data, size_t size, int threads);
 
 private:
-    FrameJob& job_;
+    HevcParser(const HevcParser&) = default;
+    FrameJob* job_;
     Sps sps_[16];
     Pps pps_[64];
     const Sps* s_ = nullptr;
@@ -567,14 +575,14 @@ void HevcParser::setup_picture() {
     ts2rs_.assign(nctb, 0);
     tile_id_.assign(nctb, 0);
     setup_tiles();
-    job_.ctbs.assign(nctb, h2j_ctb());
+    job_->ctbs.assign(nctb, h2j_ctb());
     for (int rs = 0; rs < nctb; rs++) {
-        job_.ctbs[rs].ts = static_cast<uint32_t>(rs2ts_[rs]);
-        job_.ctbs[rs].tile = static_cast<uint16_t>(tile_id_[rs2ts_[rs]]);
+        job_->ctbs[rs].ts = static_cast<uint32_t>(rs2ts_[rs]);
+        job_->ctbs[rs].tile = static_cast<uint16_t>(tile_id_[rs2ts_[rs]]);
     }
-    job_.tus.reserve(static_cast<size_t>(W) * H / 24);
-    job_.coefs.reserve(static_cast<size_t>(W) * H / 8);
-    h2j_frame& f = job_.hdr;
+    job_->tus.reserve(static_cast<size_t>(W) * H / 24);
+    job_->coefs.reserve(static_cast<size_t>(W) * H / 8);
+    h2j_frame& f = job_->hdr;
     f.codec = H2J_CODEC_HEVC;
     f.width = W;
     f.height = H;
@@ -598,13 +606,13 @@ void HevcParser::setup_picture() {
         // ScalingFactor tables (7.4.5): [sizeId][matrixId(c)][y*n+x]
         const uint8_t(*sl)[6][64] = p_->sl_present ? p_->sl : s_->sl;
         const uint8_t(*dc)[6] = p_->sl_present ? p_->sl_dc : s_->sl_dc;
-        job_.sl.assign(H2J_SL_BYTES, 16);
+        job_->sl.assign(H2J_SL_BYTES, 16);
         for (int c = 0; c < 3; c++)
-            for (int i = 0; i < 16; i++) job_.sl[H2J_SL_S0 + c * 16 + g_diag_pos4[i]] = sl[0][c][i];
+            for (int i = 0; i < 16; i++) job_->sl[H2J_SL_S0 + c * 16 + g_diag_pos4[i]] = sl[0][c][i];
         for (int c = 0; c < 3; c++)
-            for (int i = 0; i < 64; i++) job_.sl[H2J_SL_S1 + c * 64 + g_diag_pos8[i]] = sl[1][c][i];
+            for (int i = 0; i < 64; i++) job_->sl[H2J_SL_S1 + c * 64 + g_diag_pos8[i]] = sl[1][c][i];
         for (int c = 0; c < 3; c++) {
-            uint8_t* t = &job_.sl[H2J_SL_S2 + c * 256];
+            uint8_t* t = &job_->sl[H2J_SL_S2 + c * 256];
             for (int y = 0; y < 16; y++)
                 for (int x = 0; x < 16; x++) {
                     int k = 0;
@@ -613,7 +621,7 @@ void HevcParser::setup_picture() {
                 }
             t[0] = dc[2][c];
         }
-        uint8_t* t = &job_.sl[H2J_SL_S3];
+        uint8_t* t = &job_->sl[H2J_SL_S3];
         for (int y = 0; y < 32; y++)
             for (int x = 0; x < 32; x++) {
                 int k = 0;
@@ -682,7 +690,7 @@ void HevcParser::qg_start(int xq, int yq) {
 
 void HevcParser::parse_sao(int rx, int ry) {
     int ctb = ry * ctbW + rx;
-    h2j_ctb& r = job_.ctbs[ctb];
+    h2j_ctb& r = job_->ctbs[ctb];
     uint32_t ts = r.ts;
     uint16_t tile = r.tile;
     std::memset(&r, 0, sizeof(r));
@@ -691,7 +699,7 @@ void HevcParser::parse_sao(int rx, int ry) {
     r.slice = static_cast<uint8_t>(cur_idx_);
     if (!cur_->sao_luma && !cur_->sao_chroma) return;
     auto copy_from = [&](int src) {
-        const h2j_ctb& o = job_.ctbs[src];
+        const h2j_ctb& o = job_->ctbs[src];
         std::memcpy(r.type, o.type, 3);
         std::memcpy(r.band_pos, o.band_pos, 3);
         std::memcpy(r.eo_class, o.eo_class, 3);
@@ -922,15 +930,15 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         }
     }
     cc_ = cc;
-    const uint32_t base = static_cast<uint32_t>(job_.coefs.size());
-    job_.coefs.insert(job_.coefs.end(), out, out + nout);
-    tu.coef = base - job_.hdr.coef;
+    const uint32_t base = static_cast<uint32_t>(job_->coefs.size());
+    job_->coefs.insert(job_->coefs.end(), out, out + nout);
+    tu.coef = base - job_->hdr.coef;
     tu.ncoef = static_cast<uint16_t>(nout);
     tu.flags |= H2J_TU_CBF;
 }
 
 void HevcParser::split_ctb_records(size_t first) {
-    std::vector<h2j_tu>& v = job_.tus;
+    std::vector<h2j_tu>& v = job_->tus;
     chroma_tmp_.clear();
     size_t w = first;
     for (size_t i = first; i < v.size(); i++) {
@@ -953,7 +961,7 @@ void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags
     tu.ncoef = 0;
     tu.coef = 0;
     if (cbf) residual(log2n, c, mode, tu);
-    job_.tus.push_back(tu);
+    job_->tus.push_back(tu);
 }
 
 void HevcParser::transform_unit(int x0, int y0, int xb, int yb, int log2n, int blk, int cbf_l, int cbf_cb,
@@ -982,7 +990,7 @@ void HevcParser::transform_unit(int x0, int y0, int xb, int yb, int log2n, int b
     uint8_t lfl = fl;
     if (log2n == 2) lfl |= H2J_TU_DST;
     emit_tu(x0, y0, log2n, 0, lmode, lfl, cbf_l != 0, lmode);
-    if ((job_.tus.back().flags & (H2J_TU_TSKIP | H2J_TU_BYPASS)) != 0) job_.tus.back().flags &= ~H2J_TU_DST;
+    if ((job_->tus.back().flags & (H2J_TU_TSKIP | H2J_TU_BYPASS)) != 0) job_->tus.back().flags &= ~H2J_TU_DST;
     if (err_) return;
     uint8_t cfl = cu_bypass_ ? (H2J_TU_BYPASS | H2J_TU_NOFILT) : 0;
     if (log2n > 2) {
@@ -1054,15 +1062,15 @@ void HevcParser::pcm_sample(int x0, int y0, int log2cb) {
                 }
                 t.qp = 0;
                 t.qpy = 0;
-                t.coef = static_cast<uint32_t>(job_.coefs.size()) - job_.hdr.coef;
+                t.coef = static_cast<uint32_t>(job_->coefs.size()) - job_->hdr.coef;
                 t.ncoef = static_cast<uint16_t>(sub * sub);
-                job_.tus.push_back(t);
-                for (int k = 0; k < sub * sub; k++) job_.coefs.push_back(0);
+                job_->tus.push_back(t);
+                for (int k = 0; k < sub * sub; k++) job_->coefs.push_back(0);
             }
     }
     // samples are stored in raster order of the whole CU per component: fill
     // the records just pushed in bitstream order
-    size_t tu_end = job_.tus.size();
+    size_t tu_end = job_->tus.size();
     int recs_y = (n > 32) ? 4 : 1;
     size_t first = tu_end - static_cast<size_t>(recs_y + 2);
     for (int c = 0; c < 3; c++) {
@@ -1073,9 +1081,9 @@ void HevcParser::pcm_sample(int x0, int y0, int log2cb) {
             for (int x = 0; x < cn; x++) {
                 int v = static_cast<int>(b.u(pbd)) << (bd - pbd);
                 size_t rec = first + (c == 0 ? static_cast<size_t>((y / sub) * (cn / sub) + x / sub) : static_cast<size_t>(recs_y + c - 1));
-                const h2j_tu& t = job_.tus[rec];
+                const h2j_tu& t = job_->tus[rec];
                 int pos = (y % sub) * sub + (x % sub);
-                job_.coefs[job_.hdr.coef + t.coef + pos] = (static_cast<uint32_t>(pos) << 16) | static_cast<uint16_t>(v);
+                job_->coefs[job_->hdr.coef + t.coef + pos] = (static_cast<uint32_t>(pos) << 16) | static_cast<uint16_t>(v);
             }
     }
     cc_.init(p + b.byte_pos(), end_);
@@ -1083,7 +1091,7 @@ void HevcParser::pcm_sample(int x0, int y0, int log2cb) {
 
 void HevcParser::coding_unit(int x0, int y0, int log2cb) {
     const int n = 1 << log2cb;
-    cu_tu_begin_ = static_cast<int>(job_.tus.size());
+    cu_tu_begin_ = static_cast<int>(job_->tus.size());
     cu_bypass_ = 0;
     if (p_->transquant_bypass) cu_bypass_ = dec(C_TQ_BYPASS);
     int part_nxn = 0;
@@ -1155,8 +1163,8 @@ void HevcParser::coding_unit(int x0, int y0, int log2cb) {
         if (qpi > 57) qpi = 57;
         qpc[k] = chroma_qp_table(qpi) + qpbd;
     }
-    for (size_t t = static_cast<size_t>(cu_tu_begin_); t < job_.tus.size(); t++) {
-        h2j_tu& tu = job_.tus[t];
+    for (size_t t = static_cast<size_t>(cu_tu_begin_); t < job_->tus.size(); t++) {
+        h2j_tu& tu = job_->tus[t];
         tu.qpy = static_cast<int8_t>(qp_y_);
         tu.qp = static_cast<int8_t>(tu.c == 0 ? qpy : qpc[tu.c - 1]);
     }
@@ -1231,7 +1239,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         ctb_start_contexts(rs, ts, first);
         first = false;
         parse_sao(rx, ry);
-        const size_t first_tu = job_.tus.size();
+        const size_t first_tu = job_->tus.size();
         coding_quadtree(rx << log2ctb, ry << log2ctb, log2ctb, 0);
         if (err_) return err_;
         // the CTB's luma TBs first, then its chroma TBs, each in z-scan order: the GPU
@@ -1262,7 +1270,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
     return 0;
 }
 
-int HevcParser::run(const uint8_t* data, size_t size) {
+int HevcParser::run(const uint8_t* data, size_t size, int threads) {
     init_scans();
     std::vector<Nal> nals;
     split_annexb(data, size, nals);
@@ -1270,6 +1278,7 @@ int HevcParser::run(const uint8_t* data, size_t size) {
     bool have_pic = false;
     const SliceHdr* prev = nullptr;
     sh_.reserve(256);
+    std::vector<std::vector<uint8_t>> seg;  // per slice segment: its slice data (+8 zero bytes)
     for (const Nal& nal : nals) {
         if (nal.n < 2) continue;
         const int type = (nal.p[0] >> 1) & 63;
@@ -1277,21 +1286,21 @@ int HevcParser::run(const uint8_t* data, size_t size) {
         BitReader b(rbsp_.data(), rn);
         if (type == 33) {
             if (have_pic) break;
-            if (parse_sps(b, sps_) < 0) { job_.message = "unsupported or invalid SPS"; return -2; }
+            if (parse_sps(b, sps_) < 0) { job_->message = "unsupported or invalid SPS"; return -2; }
         } else if (type == 34) {
             if (have_pic) break;
-            if (parse_pps(b, pps_) < 0) { job_.message = "invalid PPS"; return -3; }
+            if (parse_pps(b, pps_) < 0) { job_->message = "invalid PPS"; return -3; }
         } else if (type <= 21) {
             if (type >= 10 && type <= 15) continue;
             const int first = (rbsp_[0] >> 7) & 1;
             if (first && have_pic) break;
             if (!first && !have_pic) continue;
-            if (sh_.size() >= 255) { job_.message = "too many slices"; return -4; }
+            if (sh_.size() >= 255) { job_->message = "too many slices"; return -4; }
             sh_.push_back(SliceHdr());
             SliceHdr& sh = sh_.back();
             int r = parse_slice_header(b, type, sh, prev);
             if (r < 0) {
-                job_.message = r == -2 ? "non-intra first picture (P/B slices) unsupported" : "invalid slice header";
+                job_->message = r == -2 ? "non-intra first picture (P/B slices) unsupported" : "invalid slice header";
                 return r == -2 ? -5 : -6;
             }
             if (!have_pic) {
@@ -1301,13 +1310,12 @@ int HevcParser::run(const uint8_t* data, size_t size) {
                 have_pic = true;
             }
             p_ = &pps_[sh.pps_id];
-            if (&sps_[p_->sps_id] != s_) { job_.message = "SPS change inside picture"; return -6; }
-            // slice data: the RBSP after the header; copy so it stays valid
+            if (&sps_[p_->sps_id] != s_) { job_->message = "SPS change inside picture"; return -6; }
+            // slice data: the RBSP after the header, kept for the decode pass
             const size_t off = b.byte_pos();
-            if (off > rn) { job_.message = "truncated slice"; return -6; }
-            std::vector<uint8_t>& keep = slice_data_;
-            keep.assign(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
-            keep.resize(keep.size() + 8, 0);
+            if (off > rn) { job_->message = "truncated slice"; return -6; }
+            seg.emplace_back(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
+            seg.back().resize(seg.back().size() + 8, 0);
             h2j_slice rec{};
             rec.beta_offset = static_cast<int8_t>(sh.beta_offset);
             rec.tc_offset = static_cast<int8_t>(sh.tc_offset);
@@ -1316,22 +1324,72 @@ int HevcParser::run(const uint8_t* data, size_t size) {
             rec.lf_across_slices = static_cast<uint8_t>(sh.lf_across_slices);
             rec.deblock_disabled = static_cast<uint8_t>(sh.deblock_disabled);
             rec.slice_addr_rs = sh.slice_addr_rs;
-            job_.slices.push_back(rec);
-            int e = decode_slice_data(static_cast<int>(sh_.size() - 1), keep.data(), keep.data() + (rn - off));
-            if (e < 0) { job_.message = "slice data decode error"; return -7; }
+            job_->slices.push_back(rec);
             prev = &sh_.back();
         } else if (type == 35 && have_pic) {
             break;
         }
     }
-    if (!have_pic) { job_.message = "no picture found"; return -8; }
-    job_.hdr.nslice = static_cast<uint32_t>(job_.slices.size());
-    {
-        bool multi = job_.slices.size() != 1 || job_.slices[0].slice_addr_rs != 0;
-        for (size_t i = 0; i < tile_id_.size() && !multi; i++) multi = tile_id_[i] != 0;
-        job_.hdr.topo = multi ? 1u : 0u;
+    if (!have_pic) { job_->message = "no picture found"; return -8; }
+    // Slice groups: an independent slice segment and the dependent segments that continue it.
+    // Groups share nothing for parsing (CABAC restarts, neighbours in other slices are
+    // unavailable, 6.4.1), so with threads > 1 they decode side by side: group 0 into this
+    // job, the others into their own jobs, appended in decoding order.
+    std::vector<int> gs;
+    for (size_t i = 0; i < sh_.size(); i++)
+        if (i == 0 || !sh_[i].dependent) gs.push_back(static_cast<int>(i));
+    gs.push_back(static_cast<int>(sh_.size()));
+    const int ng = static_cast<int>(gs.size()) - 1;
+    auto decode_group = [&](HevcParser& P, int g) -> int {
+        for (int i = gs[g]; i < gs[g + 1]; i++) {
+            const std::vector<uint8_t>& d = seg[i];
+            P.p_ = &P.pps_[P.sh_[i].pps_id];  // this parser's own copies of the parameter sets
+            P.s_ = &P.sps_[P.p_->sps_id];
+            const int e = P.decode_slice_data(i, d.data(), d.data() + (d.size() - 8));
+            if (e < 0) return e;
+        }
+        return 0;
+    };
+    if (threads <= 1 || ng <= 1) {
+        for (int g = 0; g < ng; g++)
+            if (decode_group(*this, g) < 0) { job_->message = "slice data decode error"; return -7; }
+    } else {
+        std::vector<FrameJob> part(ng);
+        std::vector<std::unique_ptr<HevcParser>> wk(ng);
+        for (int g = 1; g < ng; g++) {  // clones first: group 0 then mutates this parser's maps
+            part[g].ctbs = job_->ctbs;
+            wk[g].reset(new HevcParser(*this, part[g]));
+        }
+        std::vector<int> rc(ng, 0);
+        std::atomic<int> next(1);
+        auto work = [&]() {
+            for (int g = next++; g < ng; g = next++) rc[g] = decode_group(*wk[g], g);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < std::min(threads, ng); t++) pool.emplace_back(work);
+        rc[0] = decode_group(*this, 0);
+        work();
+        for (auto& t : pool) t.join();
+        for (int g = 0; g < ng; g++)
+            if (rc[g] < 0) { job_->message = "slice data decode error"; return -7; }
+        for (int g = 1; g < ng; g++) {
+            const uint32_t cbase = static_cast<uint32_t>(job_->coefs.size());
+            for (h2j_tu t : part[g].tus) {
+                if (t.ncoef) t.coef += cbase;  // (records without coefficients keep coef 0)
+                job_->tus.push_back(t);
+            }
+            job_->coefs.insert(job_->coefs.end(), part[g].coefs.begin(), part[g].coefs.end());
+            for (int rs = 0; rs < nctb; rs++)
+                if (wk[g]->ctb_slice_[rs] >= gs[g] && wk[g]->ctb_slice_[rs] < gs[g + 1]) job_->ctbs[rs] = part[g].ctbs[rs];
+        }
     }
-    job_.hdr.ntu = static_cast<uint32_t>(job_.tus.size());
+    job_->hdr.nslice = static_cast<uint32_t>(job_->slices.size());
+    {
+        bool multi = job_->slices.size() != 1 || job_->slices[0].slice_addr_rs != 0;
+        for (size_t i = 0; i < tile_id_.size() && !multi; i++) multi = tile_id_[i] != 0;
+        job_->hdr.topo = multi ? 1u : 0u;
+    }
+    job_->hdr.ntu = static_cast<uint32_t>(job_->tus.size());
     return 0;
 }
 
@@ -1339,8 +1397,8 @@ int HevcParser::run(const uint8_t* data, size_t size) {
 
 int hevc_parse_picture(const uint8_t* data, size_t size, FrameJob& job) {
     job.clear();
-    HevcParser p(job);
-    int r = p.run(data, size);
+    std::unique_ptr<HevcParser> p(new HevcParser(job));  // large (parameter-set tables): heap
+    int r = p->run(data, size, job.threads);
     job.error = r;
     return r;
 }

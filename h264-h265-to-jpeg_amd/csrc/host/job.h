@@ -17,6 +17,7 @@ struct FrameJob {
     std::vector<uint8_t> sl;  // scaling factors (2032 B) when hdr.scaling_list
     int error = 0;            // 0 ok, <0 parse error
     std::string message;
+    int threads = 1;          // threads the parser may use inside this picture (independent slices)
 
     void clear() {
         hdr = h2j_frame{};

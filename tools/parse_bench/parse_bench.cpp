@@ -27,7 +27,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "usage: parse_bench file... [-r reps] [-t threads] [-d (output digest)]\n");
         return 2;
     }
-    int reps = 3, threads = 1;
+    int reps = 3, threads = 1, pthreads = 1;
     bool want_digest = false, want_hist = false;
     std::vector<std::vector<uint8_t>> streams;
     for (int i = 1; i < argc; i++) {
@@ -42,6 +42,10 @@ int main(int argc, char** argv) {
         }
         if (a == "-s") {  // transform-block histogram by (component, size, cbf)
             want_hist = true;
+            continue;
+        }
+        if (a == "-p" && i + 1 < argc) {  // threads inside one picture (independent slices)
+            pthreads = std::atoi(argv[++i]);
             continue;
         }
         if (a == "-t" && i + 1 < argc) {
@@ -66,6 +70,7 @@ int main(int argc, char** argv) {
     for (auto& a : hist) for (auto& b : a) for (auto& c : b) c = 0;
     auto worker = [&]() {
         h2j::FrameJob job;
+        job.threads = pthreads;
         size_t t = 0, c = 0, b = 0;
         for (int i = next++; i < total; i = next++) {
             const auto& s = streams[i % streams.size()];
@@ -92,6 +97,8 @@ int main(int argc, char** argv) {
             mix(job.tus.data(), job.tus.size() * sizeof(h2j_tu));
             mix(job.coefs.data(), job.coefs.size() * sizeof(h2j_coef));
             mix(job.ctbs.data(), job.ctbs.size() * sizeof(h2j_ctb));
+            mix(job.slices.data(), job.slices.size() * sizeof(h2j_slice));
+            mix(&job.hdr, sizeof(job.hdr));
             digest += hsh;
         }
         tus += t;
