@@ -194,7 +194,10 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // int16 plane.  K1 then only walks the serial prediction chain.
 constexpr int kK0Tus = 16;      // H.264 TUs per K0 wave (records held one per lane)
 constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
-constexpr int kK1Waves = 8;       // HEVC K1: waves (CTB rows in flight) per group, launches of > 128 pictures
+// HEVC K1: launches of > 128 pictures run one 16-wave workgroup per picture split unevenly: the Cb/Cr chain processes each Cb/Cr TB
+// pair in one pass (about 2/3 of a luma row's time), so 9 luma + 7 chroma waves finish a 17-row
+// 1080p picture in 2 luma rounds instead of 3 (8 + 8)
+constexpr int kYWaves = 9, kCWaves = 7;
 constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
@@ -1384,6 +1387,75 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     wave_sync();
 }
 
+// A Cb TB and the Cr TB at the same place (n <= 8: at most 33 references) in one pass: both
+// components share geometry, availability and the intra mode (chroma is never filtered, no
+// boundary smoothing), so the substitution indices, the reference gathers and the prediction
+// indices are computed once and applied to two register sets (lane k: Cb and Cr reference k).
+DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, uint64_t mask, int ox, int oy,
+                                   int S, int16_t* bcb, int16_t* bcr, const int16_t* tcb, const int16_t* lcb,
+                                   const int16_t* tcr, const int16_t* lcr, int lane) {
+    const int log2n = tb.log2n, n = 1 << log2n, nn = n * n;
+    const int maxv = (1 << u.bdc) - 1;
+    const bool cbf_cb = (tb.flags & H2J_TU_CBF) != 0;
+    const int L = 4 * n + 1, nu = n;  // unit = 2 chroma samples
+    const int k = lane;
+    const int unit = k < 2 * n ? (k >> 1) : nu + ((k - 2 * n + 1) >> 1);
+    const unsigned long long m = __ballot(k < L && ((mask >> unit) & 1ull));
+    const bool any = m != 0;
+    const int first = m ? __ffsll(static_cast<long long>(m)) - 1 : 0;
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const unsigned long long le = m & upto;
+    const int j = le ? 63 - static_cast<int>(__clzll(le)) : first;
+    const int xn = j > 2 * n ? ox + (j - 2 * n - 1) : ox - 1;
+    const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
+    const int top_cb = static_cast<int>(tcb - bcb), left_cb = static_cast<int>(lcb - bcb);
+    const int top_cr = static_cast<int>(tcr - bcr), left_cr = static_cast<int>(lcr - bcr);
+    const int in = yn * S + xn;
+    const int icb = yn < 0 ? top_cb + xn + 1 : (xn < 0 ? left_cb + yn : in);
+    const int icr = yn < 0 ? top_cr + xn + 1 : (xn < 0 ? left_cr + yn : in);
+    const int half = 1 << (u.bdc - 1);
+    const int rb = any ? bcb[icb] : half, rr = any ? bcr[icr] : half;
+    const int mode = tb.mode;
+    int dcb = 0, dcr = 0;
+    if (mode == 1) {
+        const bool dk = k >= n && k <= 3 * n && k != 2 * n;
+        dcb = (wave_sum_dpp(dk ? rb : 0) + n) >> (log2n + 1);
+        dcr = (wave_sum_dpp(dk ? rr : 0) + n) >> (log2n + 1);
+    }
+    const int i = lane, x = i & (n - 1), y = i >> log2n;
+    int pb, pr;
+    if (mode == 0) {
+        const int trb = __builtin_amdgcn_readlane(rb, 3 * n + 1), blb = __builtin_amdgcn_readlane(rb, n - 1);
+        const int trr = __builtin_amdgcn_readlane(rr, 3 * n + 1), blr = __builtin_amdgcn_readlane(rr, n - 1);
+        const int il = 2 * n - 1 - y, ia = 2 * n + 1 + x;
+        const int lb = __shfl(rb, il, 64), ab = __shfl(rb, ia, 64), lr = __shfl(rr, il, 64), ar = __shfl(rr, ia, 64);
+        pb = ((n - 1 - x) * lb + (x + 1) * trb + (n - 1 - y) * ab + (y + 1) * blb + n) >> (log2n + 1);
+        pr = ((n - 1 - x) * lr + (x + 1) * trr + (n - 1 - y) * ar + (y + 1) * blr + n) >> (log2n + 1);
+    } else if (mode == 1) {
+        pb = dcb;
+        pr = dcr;
+    } else {
+        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+        const bool vert = mode >= 18;
+        const int sgn = vert ? 1 : -1;
+        const int a = vert ? y : x, b = vert ? x : y;
+        const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+        const int k1 = b + idx + 1, k2 = k1 + 1;
+        const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
+        const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
+        const int i1 = 2 * n + sgn * o1, i2 = 2 * n + sgn * o2;
+        pb = ((32 - fr) * __shfl(rb, i1, 64) + fr * __shfl(rb, i2, 64) + 16) >> 5;
+        pr = ((32 - fr) * __shfl(rr, i1, 64) + fr * __shfl(rr, i2, 64) + 16) >> 5;
+    }
+    if (i < nn) {
+        int16_t* db = bcb + (oy + y) * S + ox + x;
+        int16_t* dr = bcr + (oy + y) * S + ox + x;
+        *db = static_cast<int16_t>(clip3(0, maxv, pb + (cbf_cb ? *db : 0)));
+        *dr = static_cast<int16_t>(clip3(0, maxv, pr + (cbf_cr ? *dr : 0)));
+    }
+    wave_sync();
+}
+
 // Asynchronous global -> LDS copies (LDS-DMA): lane i's bytes land at lds + i * size, with no
 // VGPR destination.  M0 carries the wave-uniform LDS byte address (set and restored inside the
 // statement, the compiler reserves M0).  Issued as asm, so the compiler does not track them:
@@ -1431,14 +1503,14 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
     }
 }
 
-template <typename Pel, int W_>
+template <typename Pel>
 DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
-                    int16_t* line, int wv) {
+                    int16_t* line, int wv, const int W_) {
     const int lane = threadIdx.x & 63;
     QWave& w = W[wv];
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
-    constexpr int kSlots = 2 * W_;
+    const int kSlots = 2 * W_;  // (W_: waves of this group, a runtime value: one code copy per sample type)
     const FU u = make_fu(f, arena);
     if (wv >= u.ctb_h) return;
     const int shc = grp ? 1 : 0;                 // component subsampling of this group
@@ -1576,6 +1648,19 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                     if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
                     const int ci = c == 2 ? 1 : 0;
                     int16_t* body = w.body[cur] + ci * 256;
+                    if (c == 1 && tu.log2n <= 3 && l + 1 < 64 && t + 1 < b && !(tu.flags & H2J_TU_PCM)) {
+                        // Cb TB followed by the Cr TB at the same place: one pass for both
+                        const h2j_tu tr = tu_from_lanes(rec, l + 1);
+                        if (tr.c == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2n == tu.log2n && !(tr.flags & H2J_TU_PCM)) {
+                            hevc_predict_chroma_pair(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
+                                                     body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
+                                                     w.cs[1].left, lane);
+                            PROF_ADD(5, 2);
+                            PROF_LAPK(tu.log2n - 2 + 4);
+                            t += 2;
+                            continue;
+                        }
+                    }
                     if (tu.flags & H2J_TU_PCM) {  // samples written by K0: pull that block into the window
                         const int n = 1 << tu.log2n;
                         const Pel* P = u.plane<Pel>(c);
@@ -1659,8 +1744,8 @@ __global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame*
 #endif
     if (threadIdx.x < 2 * W_) prog[threadIdx.x] = 0;
     __syncthreads();
-    hevc_rows<Pel, W_>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line,
-                       static_cast<int>(threadIdx.x >> 6));
+    hevc_rows<Pel>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line,
+                       static_cast<int>(threadIdx.x >> 6), W_);
 }
 
 // grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
@@ -1684,6 +1769,33 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
     else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
 }
 
+// One HEVC picture in one 16-wave workgroup: waves 0..kYWaves-1 the luma chain, the rest the
+// Cb/Cr chain, each group with its own LDS region (luma first, `ybytes` long).
+template <typename Pel>
+DEVI void hevc_picture_groups(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, uint8_t* lds, uint32_t ybytes) {
+    const int wave = static_cast<int>(threadIdx.x >> 6);
+    const int grp = wave < kYWaves ? 0 : 1;
+    const int nw = grp ? kCWaves : kYWaves;
+    uint8_t* gb = lds + (grp ? ybytes : 0);
+    QWave* W = reinterpret_cast<QWave*>(gb);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(gb + sizeof(QWave) * nw);
+    int16_t* line = reinterpret_cast<int16_t*>(gb + k1_fixed_lds(nw));
+    const int tl = static_cast<int>(threadIdx.x) - (grp ? 64 * kYWaves : 0);
+    if (tl < 2 * nw) prog[tl] = 0;
+    __syncthreads();
+    if (grp == 0) hevc_rows<Pel>(f, T, arena, 0, W, prog, line, wave, kYWaves);  // one specialised copy per group
+    else hevc_rows<Pel>(f, T, arena, 1, W, prog, line, wave - kYWaves, kCWaves);
+}
+// launches of > 128 pictures: one workgroup per picture (see kYWaves)
+template <typename Pel>
+__global__ void __launch_bounds__(64 * (kYWaves + kCWaves)) h2j_k1_recon_hevc_pic(const h2j_frame* frames, const h2j_tu* tus,
+                                                                                uint8_t* arena, uint32_t ybytes) {
+    extern __shared__ __align__(16) uint8_t k1lds[];
+    const h2j_frame& f = frames[blockIdx.x];
+    if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
+    hevc_picture_groups<Pel>(f, tus + ufl(f.tu), arena, k1lds, ybytes);
+}
+
 // K1 for batches mixing HEVC 8-bit, HEVC high bit depth and H.264 pictures (configs[4]): one
 // launch instead of three back-to-back ones, so the pictures' chains run side by side (each
 // launch alone is one long chain per picture and leaves most of the GPU idle).  Workgroups of
@@ -1691,12 +1803,12 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
 // workgroup; an H.264 workgroup is one band as in h2j_k1_recon_h264.  Tall HEVC pictures (the
 // longest chains of such a batch) instead get one 16-wave workgroup per component group, twice
 // the rows in flight.  `map`: the host's list, longest chains first; bit 31 marks HEVC entries,
-// bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).  `gbytes`: LDS bytes of one 8-wave HEVC
-// group.
+// bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).  `ybytes`: LDS bytes of the luma group of a
+// picture workgroup (hevc_picture_groups).
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_frame* frames, const h2j_tu* tus,
                                                                  uint8_t* arena, const uint32_t* map,
-                                                                 uint32_t gbytes) {
-    static_assert(2 * kK1Waves == kAvcWaves, "an HEVC picture's two groups fill one H.264-sized workgroup");
+                                                                 uint32_t ybytes) {
+    static_assert(kYWaves + kCWaves == kAvcWaves, "an HEVC picture's two groups fill one H.264-sized workgroup");
     extern __shared__ __align__(16) uint8_t anylds[];
     const uint32_t me = map[blockIdx.x];
     const h2j_frame& f = frames[(me >> 8) & 0x3FFFFFu];
@@ -1709,19 +1821,11 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
         if (threadIdx.x < 2 * kK1WavesWide) prog[threadIdx.x] = 0;
         __syncthreads();
         const int wv = static_cast<int>(threadIdx.x >> 6);
-        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t, kK1WavesWide>(f, T, arena, grp, W, prog, line, wv);
-        else hevc_rows<uint16_t, kK1WavesWide>(f, T, arena, grp, W, prog, line, wv);
+        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t>(f, T, arena, grp, W, prog, line, wv, kK1WavesWide);
+        else hevc_rows<uint16_t>(f, T, arena, grp, W, prog, line, wv, kK1WavesWide);
     } else if (me & 0x80000000u) {
-        const int grp = static_cast<int>(threadIdx.x >> 9);
-        uint8_t* gb = anylds + grp * gbytes;
-        QWave* W = reinterpret_cast<QWave*>(gb);
-        uint32_t* prog = reinterpret_cast<uint32_t*>(gb + sizeof(QWave) * kK1Waves);
-        int16_t* line = reinterpret_cast<int16_t*>(gb + k1_fixed_lds(kK1Waves));
-        if ((threadIdx.x & 511) < 2 * kK1Waves) prog[threadIdx.x & 511] = 0;
-        __syncthreads();
-        const int wv = static_cast<int>((threadIdx.x >> 6) & (kK1Waves - 1));
-        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t, kK1Waves>(f, T, arena, grp, W, prog, line, wv);
-        else hevc_rows<uint16_t, kK1Waves>(f, T, arena, grp, W, prog, line, wv);
+        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_picture_groups<uint8_t>(f, T, arena, anylds, ybytes);
+        else hevc_picture_groups<uint16_t>(f, T, arena, anylds, ybytes);
     } else {
         H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(anylds);
         uint32_t* prog = reinterpret_cast<uint32_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves);
@@ -2790,8 +2894,8 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!attr) {
         const void* fns[] = {reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1WavesWide>),
-                             reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1Waves>),
-                             reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1Waves>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint8_t>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint16_t>),
                              reinterpret_cast<const void*>(h2j_k1_recon_h264),
                              reinterpret_cast<const void*>(h2j_k1_recon_any)};
         for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2801,28 +2905,35 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         const char* e = std::getenv("H2J_K1_MERGE");
         return !(e && e[0] == '0');
     }();
-    const size_t gbytes = (k1_fixed_lds(kK1Waves) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t) + 15) & ~size_t(15);
-    const size_t wbytes = k1_fixed_lds(kK1WavesWide) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-    const size_t lds_any = std::max(std::max(2 * gbytes, lds264), wbytes);
+    const size_t line_bytes = 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
+    const size_t ybytes = (k1_fixed_lds(kYWaves) + line_bytes + 15) & ~size_t(15);   // luma group of a picture workgroup
+    const size_t pbytes = ybytes + k1_fixed_lds(kCWaves) + line_bytes;                 // the whole picture workgroup
+    const size_t wbytes = k1_fixed_lds(kK1WavesWide) + line_bytes;
+    const size_t lds_any = std::max(std::max(pbytes, lds264), wbytes);
     // one launch for every kind of picture (unless the widest picture's line buffers would not
     // fit one workgroup's LDS: then the per-kind launches below)
     if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
-        const size_t lds = lds_any;
-        hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus,
-                           b->arena, b->k1all, static_cast<uint32_t>(gbytes));
+        hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
+                           b->arena, b->k1all, static_cast<uint32_t>(ybytes));
         return check(hipGetLastError(), "h2j_k1_recon_any");
     }
     if (b->has_hevc) {
-        const int wv = wide ? kK1WavesWide : kK1Waves;
-        const size_t lds = k1_fixed_lds(wv) + 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-        const dim3 grid(b->nframes, 2), block(64 * wv);
         const bool p8 = pels == 0 || (pels & 1), p16 = pels == 0 || (pels & 2);
         if (wide) {
+            const size_t lds = wbytes;
+            const dim3 grid(b->nframes, 2), block(64 * kK1WavesWide);
             if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
             if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
         } else {
-            if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
-            if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1Waves>), grid, block, lds, s, b->frames, b->tus, b->arena);
+            if (pbytes > 160 * 1024) {
+                snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pic: %zu B of LDS per workgroup (max 160 KB)", pbytes);
+                return -1;
+            }
+            const dim3 grid(b->nframes), block(64 * (kYWaves + kCWaves));
+            if (p8) hipLaunchKernelGGL(h2j_k1_recon_hevc_pic<uint8_t>, grid, block, pbytes, s, b->frames, b->tus, b->arena,
+                                       static_cast<uint32_t>(ybytes));
+            if (p16) hipLaunchKernelGGL(h2j_k1_recon_hevc_pic<uint16_t>, grid, block, pbytes, s, b->frames, b->tus, b->arena,
+                                        static_cast<uint32_t>(ybytes));
         }
         int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
         if (r) return r;
