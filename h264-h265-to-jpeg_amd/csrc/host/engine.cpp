@@ -586,6 +586,10 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     std::mutex mu;
     std::condition_variable cv;
     double t_parsed = t0;
+    // once every picture is parsed the pool is idle: the pipeline's tail (packing, assembly)
+    // then fans out over it instead of running on this thread alone
+    std::atomic<bool> parsed(false);
+    auto pool_idle = [&]() { return !overlap || parsed.load(std::memory_order_acquire); };
     // batches smaller than the thread pool (a lone IDecoder call): pictures with several
     // independent slices parse them on several threads
     const int slice_threads = std::max(1, (e.pool->size() + 1) / std::max(1, n));
@@ -599,6 +603,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
             }
         });
         t_parsed = h2j::now_ms();
+        parsed.store(true, std::memory_order_release);
     };
     std::thread producer;
     if (overlap) producer = std::thread(parse_all);
@@ -614,7 +619,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
             const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
             sz[k] = st->seg_off == ~0ull ? 0 : h2j::jpeg_container_size(*st, s.h_seg.p + st->seg_off, h2j::kLavcIdent);
         };
-        if (overlap) for (int k = 0; k < nf; k++) size_of(k);
+        if (!pool_idle()) for (int k = 0; k < nf; k++) size_of(k);
         else e.pool->parallel_for(nf, size_of);
         std::vector<size_t> at(nf);
         for (int k = 0; k < nf; k++) {
@@ -649,7 +654,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
             const h2j_frame& f = s.frames[k];
             h2j::jpeg_write_container(*st, s.h_seg.p + st->seg_off, f.out_w, f.out_h, h2j::kLavcIdent, out + at[k]);
         };
-        if (overlap) for (int k = 0; k < nf; k++) write(k);
+        if (!pool_idle()) for (int k = 0; k < nf; k++) write(k);
         else e.pool->parallel_for(nf, write);
         e.stats[h2j::ST_ASSEMBLE] += h2j::now_ms() - ta;
         e.stats[h2j::ST_FRAMES] += nf;
@@ -669,7 +674,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
             status[i] = e.jobs[i].error;
             if (e.jobs[i].error == 0) s.live.push_back(i);
         }
-        if (e.enqueue(s, 4, true, !overlap)) { fail = 1; break; }
+        if (e.enqueue(s, 4, true, pool_idle())) { fail = 1; break; }
         Slot& prev = e.slot[(c + 1) & 1];
         if (c > 0 && prev.pending && assemble(prev)) { fail = 1; break; }
     }
