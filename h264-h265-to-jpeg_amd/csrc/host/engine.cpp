@@ -502,8 +502,8 @@ std::vector<int> chunk_plan(int n) {
     chunk = std::max(1, chunk);
     const char* tail = std::getenv("H2J_TAIL");  // "0": no shrinking tail chunks
     const bool shrink = !(tail && tail[0] == '0');
-    const char* tmin = std::getenv("H2J_TAIL_MIN");  // smallest tail chunk (default 64)
-    const int tail_min = tmin && std::atoi(tmin) > 0 ? std::atoi(tmin) : 64;
+    const char* tmin = std::getenv("H2J_TAIL_MIN");  // smallest tail chunk (default 128: 256,256,256,128,128 for 1024)
+    const int tail_min = tmin && std::atoi(tmin) > 0 ? std::atoi(tmin) : 128;
     std::vector<int> starts;
     int i = 0;
     while (i < n) {
