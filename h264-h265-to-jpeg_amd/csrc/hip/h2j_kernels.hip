@@ -596,42 +596,112 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         const uint32_t e = min(static_cast<uint32_t>(lane), max(static_cast<uint32_t>(v.ncoef), 1u) - 1);
         return v.ncoef ? CO[v.coef + e] : 0u;
     };
-    // H.264: coefficients of the next record prefetched one record ahead.  HEVC: no load in the
-    // loop (its wait would stall every record); the rare per-record paths (PCM, transform skip,
-    // bypass) load their own, regular transforms run batched after the loop.
-    uint32_t nco = hevc ? 0u : fetch_co(tu_from_lanes(rec, 0));
-    for (int k = 0; k < nrec; k++) {
-        const uint32_t t = t0 + k;
+    // ---- per-record metadata, one lane per record: CTB ranges, deblocking maps (HEVC luma),
+    // availability masks.  (The neighbours of the range sit in lanes kTus, kTus + 1.)
+    h2j_tu own;
+    {
+        uint32_t w4[4] = {rec.x, rec.y, rec.z, rec.w};
+        memcpy(&own, w4, sizeof(own));
+    }
+    const bool mine = lane < nrec;
+    {
+        const int oc = own.c, on = 1 << own.log2n, oshc = oc ? 1 : 0;
+        const int ox0 = own.x, oy0 = own.y, oxl = ox0 << oshc, oyl = oy0 << oshc;
+        const int ocb = (oyl >> f.log2ctb) * f.ctb_w + (oxl >> f.log2ctb);
+        const int lcb = __shfl(ocb, lane > 0 ? lane - 1 : 0, 64), lcc = __shfl(oc, lane > 0 ? lane - 1 : 0, 64);
+        const int rcb = __shfl(ocb, lane < 63 ? lane + 1 : 63, 64);
+        const int pcb = lane == 0 ? prev_cb : lcb, pc = lane == 0 ? prev_c : lcc;
+        const int ncb = lane == nrec - 1 ? next_cb : rcb;
+        if (mine) {
+            const uint32_t t = t0 + lane;
+            if (pcb != ocb) rng[4 * ocb] = t;
+            if (ncb != ocb) rng[4 * ocb + 2] = t + 1;
+            // first chroma record of the CTB (HEVC records are luma first, then chroma)
+            if (oc > 0 && (pcb != ocb || pc == 0)) rng[4 * ocb + 1] = t;
+            const uint8_t flags = own.flags;
+            if (hevc && oc == 0) {  // deblocking maps (luma TBs)
+                const int nb = on >> 2;
+                for (int q = 0; q < nb * nb; q++) {
+                    const int bx = q % nb, by = q / nb;
+                    const int idx = ((oy0 >> 2) + by) * f.mw + (ox0 >> 2) + bx;
+                    uint8_t fl = 0;
+                    if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
+                    if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
+                    if (flags & H2J_TU_NOFILT) fl |= 4;
+                    fmap[idx] = fl;
+                    qmap[idx] = own.qpy;
+                }
+            }
+            // reference availability mask; without several slices / tiles it is pure
+            // geometry: inside the picture and earlier in decoding (z-scan / raster) order
+            uint64_t mask = 0;
+            if (!(flags & H2J_TU_PCM)) {
+                if (hevc) {
+                    const int u = oc ? 2 : 4, nu = (2 * on) / u;
+                    const int l2 = f.log2ctb, m = (1 << l2) - 1;
+                    const int zc = zorder4((oxl & m) >> 2, (oyl & m) >> 2);
+                    for (int q = 0; q <= 2 * nu; q++) {
+                        int xn, yn;
+                        if (q < nu) { xn = ox0 - 1; yn = oy0 + 2 * on - 1 - q * u; }
+                        else if (q == nu) { xn = ox0 - 1; yn = oy0 - 1; }
+                        else { xn = ox0 + (q - nu - 1) * u; yn = oy0 - 1; }
+                        const int xnl = xn << oshc, ynl = yn << oshc;
+                        bool a = false;
+                        if (f.topo) {
+                            a = avail(fr, C, S, oxl, oyl, xnl, ynl);
+                        } else if (xnl >= 0 && ynl >= 0 && xnl < f.width && ynl < f.height) {
+                            const int cn = (ynl >> l2) * f.ctb_w + (xnl >> l2);
+                            a = cn == ocb ? zorder4((xnl & m) >> 2, (ynl & m) >> 2) <= zc : cn < ocb;
+                        }
+                        mask |= static_cast<uint64_t>(a) << q;
+                    }
+                } else {
+                    const bool nxn = oc == 0 && own.log2n <= 3;
+                    for (int q = 0; q < 4; q++) {
+                        int xn = oxl, yn = oyl;
+                        bool use = true;
+                        if (q == 0) yn = oyl - 1;
+                        else if (q == 1) xn = oxl - 1;
+                        else if (q == 2) { xn = oxl - 1; yn = oyl - 1; }
+                        else { xn = oxl + on; yn = oyl - 1; use = nxn; }
+                        bool a = false;
+                        if (use) {
+                            if (f.topo) {
+                                a = h264_avail(fr, C, S, oxl, oyl, xn, yn);
+                            } else if (xn >= 0 && yn >= 0 && xn < f.width && yn < f.height) {
+                                const int cn = (yn >> 4) * f.ctb_w + (xn >> 4), cc = (oyl >> 4) * f.ctb_w + (oxl >> 4);
+                                if (cn == cc) {
+                                    const int ax = (xn & 15) >> 2, ay = (yn & 15) >> 2, bx = (oxl & 15) >> 2, by = (oyl & 15) >> 2;
+                                    a = ((ax & 1) | ((ay & 1) << 1) | ((ax & 2) << 1) | ((ay & 2) << 2)) <
+                                        ((bx & 1) | ((by & 1) << 1) | ((bx & 2) << 1) | ((by & 2) << 2));
+                                } else {
+                                    a = cn < cc;
+                                }
+                            }
+                        }
+                        mask |= static_cast<uint64_t>(a) << q;
+                    }
+                }
+            }
+            masks[t] = mask;
+        }
+    }
+    // ---- records with per-record work, one after another: PCM samples, H.264 residuals, HEVC
+    // transform-skip / bypass residuals (regular HEVC transforms run batched below).  H.264:
+    // the next such record's coefficients prefetched one record ahead.
+    uint64_t work = __ballot(mine && ((own.flags & H2J_TU_PCM) ||
+                                      ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
+    uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
+    while (work) {
+        const int k = __ffsll(static_cast<long long>(work)) - 1;
+        work &= work - 1;
         const h2j_tu tu = tu_from_lanes(rec, k);
         uint32_t co0 = nco;
-        if (!hevc && k + 1 < nrec) nco = fetch_co(tu_from_lanes(rec, k + 1));
-        if (hevc && (tu.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS))) co0 = fetch_co(tu);
+        if (!hevc && work) nco = fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1));
+        if (hevc) co0 = fetch_co(tu);
         const int c = tu.c, log2n = tu.log2n, n = 1 << log2n;
-        const int shc = c ? 1 : 0;
-        const int x0 = tu.x, y0 = tu.y, xl = x0 << shc, yl = y0 << shc;
-        const int cb = ctb_of_tu(tu);
-        if (lane == 0) {
-            const int pcb = k > 0 ? ctb_of_tu(tu_from_lanes(rec, k - 1)) : prev_cb;
-            const int ncb = k + 1 < nrec ? ctb_of_tu(tu_from_lanes(rec, k + 1)) : next_cb;
-            if (pcb != cb) rng[4 * cb] = t;
-            if (ncb != cb) rng[4 * cb + 2] = t + 1;
-            // first chroma record of the CTB (HEVC records are luma first, then chroma)
-            if (c > 0 && (pcb != cb || (k > 0 ? tu_from_lanes(rec, k - 1).c : prev_c) == 0)) rng[4 * cb + 1] = t;
-        }
+        const int x0 = tu.x, y0 = tu.y;
         const uint8_t flags = tu.flags;
-        if (hevc && c == 0) {  // deblocking maps (luma TBs)
-            const int nb = n >> 2;
-            for (int i = lane; i < nb * nb; i += 64) {
-                const int bx = i % nb, by = i / nb;
-                const int idx = ((y0 >> 2) + by) * f.mw + (x0 >> 2) + bx;
-                uint8_t fl = 0;
-                if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
-                if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
-                if (flags & H2J_TU_NOFILT) fl |= 4;
-                fmap[idx] = fl;
-                qmap[idx] = tu.qpy;
-            }
-        }
         const int stc = c ? st1 : st0;
         const int offc = c == 0 ? 0 : (c == 1 ? off1 : off2);
         if (flags & H2J_TU_PCM) {
@@ -650,73 +720,13 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                     P[(y0 + (pos >> log2n)) * stc + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
                 }
             }
-            if (lane == 0) masks[t] = 0;
             continue;
         }
-        // reference availability mask; without several slices / tiles it is pure
-        // geometry: inside the picture and earlier in decoding (z-scan / raster) order
-        uint64_t mask;
-        if (hevc) {
-            const int u = c ? 2 : 4, nu = (2 * n) / u;
-            bool a = false;
-            if (lane <= 2 * nu) {
-                int xn, yn;
-                if (lane < nu) { xn = x0 - 1; yn = y0 + 2 * n - 1 - lane * u; }
-                else if (lane == nu) { xn = x0 - 1; yn = y0 - 1; }
-                else { xn = x0 + (lane - nu - 1) * u; yn = y0 - 1; }
-                const int xnl = xn << shc, ynl = yn << shc;
-                if (f.topo) {
-                    a = avail(fr, C, S, xl, yl, xnl, ynl);
-                } else if (xnl >= 0 && ynl >= 0 && xnl < f.width && ynl < f.height) {
-                    const int l2 = f.log2ctb, m = (1 << l2) - 1;
-                    const int cn = (ynl >> l2) * f.ctb_w + (xnl >> l2);
-                    a = cn == cb ? zorder4((xnl & m) >> 2, (ynl & m) >> 2) <= zorder4((xl & m) >> 2, (yl & m) >> 2)
-                                 : cn < cb;
-                }
-            }
-            mask = __ballot(a);
-        } else {
-            const bool nxn = c == 0 && log2n <= 3;
-            int xn = xl, yn = yl;
-            bool use = lane < 4;
-            if (lane == 0) yn = yl - 1;
-            else if (lane == 1) xn = xl - 1;
-            else if (lane == 2) { xn = xl - 1; yn = yl - 1; }
-            else if (lane == 3) { xn = xl + n; yn = yl - 1; use = nxn; }
-            bool a = false;
-            if (use) {
-                if (f.topo) {
-                    a = h264_avail(fr, C, S, xl, yl, xn, yn);
-                } else if (xn >= 0 && yn >= 0 && xn < f.width && yn < f.height) {
-                    const int cn = (yn >> 4) * f.ctb_w + (xn >> 4), cc = (yl >> 4) * f.ctb_w + (xl >> 4);
-                    if (cn == cc) {
-                        const int ax = (xn & 15) >> 2, ay = (yn & 15) >> 2, bx = (xl & 15) >> 2, by = (yl & 15) >> 2;
-                        a = ((ax & 1) | ((ay & 1) << 1) | ((ax & 2) << 1) | ((ay & 2) << 2)) <
-                            ((bx & 1) | ((by & 1) << 1) | ((bx & 2) << 1) | ((by & 2) << 2));
-                    } else {
-                        a = cn < cc;
-                    }
-                }
-            }
-            mask = __ballot(a);
-        }
-        if (lane == 0) masks[t] = mask;
-        if (flags & H2J_TU_CBF) {
-            int16_t* R = res + offc;
-            if (hevc) {
-                if (flags & (H2J_TU_TSKIP | H2J_TU_BYPASS)) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
-                // regular HEVC transforms: batched by size below
-            } else {
-                h264_residual(f, tu, CO, co0, sl, R, stc, s);
-            }
-        }
+        int16_t* R = res + offc;
+        if (hevc) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
+        else h264_residual(f, tu, CO, co0, sl, R, stc, s);
     }
     if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
-        h2j_tu own;
-        {
-            uint32_t w[4] = {rec.x, rec.y, rec.z, rec.w};
-            memcpy(&own, w, sizeof(own));
-        }
         const bool batch = lane < nrec && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS));
 #pragma unroll
         for (int l2 = 2; l2 <= 5; l2++) {
