@@ -205,7 +205,6 @@ struct K0Lds {
     int blk[32 * 32];
     int tmp[32 * 32];
     int dc[16];
-    int maxx, maxy;
 };
 
 DEVI int wave_sum(int v) {
@@ -277,7 +276,6 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     const int bd = c ? f.bdc : f.bd;
     const uint8_t flags = tu.flags;
     for (int i = lane; i < nn; i += 64) s.blk[i] = 0;
-    if (lane == 0) { s.maxx = 0; s.maxy = 0; }
     wave_sync();
     const bool bypass = (flags & H2J_TU_BYPASS) != 0;
     const int qp = tu.qp;
@@ -288,7 +286,6 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
         const int soff = log2n == 2 ? 0 + c * 16 : (log2n == 3 ? 48 + c * 64 : (log2n == 4 ? 240 + c * 256 : 1008));
         slt = sl + f.sl + soff;
     }
-    int mx = 0, my = 0;
     for (int e = lane; e < tu.ncoef; e += 64) {
         const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];  // first 64 entries prefetched
         const int pos = static_cast<int>(en >> 16);
@@ -303,11 +300,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
             d = static_cast<int>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
         }
         s.blk[pos] = d;
-        mx = max(mx, pos & (n - 1));
-        my = max(my, pos >> log2n);
     }
-    if (mx) atomicMax(&s.maxx, mx);
-    if (my) atomicMax(&s.maxy, my);
     wave_sync();
     if (!bypass) {  // transform skip (regular transforms run batched: hevc_residual_group)
         const int bdS = 20 - bd;
