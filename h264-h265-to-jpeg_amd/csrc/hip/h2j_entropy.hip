@@ -132,6 +132,7 @@ struct HuffLds {
     int nb[260];              // code length per symbol
     int hc[256], hl[256];     // (symbol, length) pairs
     int stk[64][2];
+    unsigned hist[256];       // the table's symbol counts, staged by all lanes
 };
 
 // libavutil/qsort.h AV_QSORT on index range [0, num) (unstable: tie order
@@ -201,10 +202,14 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
     const h2j_frame& f = frames[blockIdx.y];
     h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
     const int t = blockIdx.x;
+    // the counts through LDS (one wide pass by every lane; a serial loop of global loads
+    // would wait for each of them)
+    for (int i = threadIdx.x; i < 256; i += 64) s.hist[i] = js->hist[t][i];
+    __syncthreads();
     if (threadIdx.x != 0) return;  // serial by construction (AV_QSORT tie order)
     int nval = 0;
     for (int i = 0; i < 256; i++) {
-        const unsigned c = js->hist[t][i];
+        const unsigned c = s.hist[i];
         if (c) {
             s.pv[nval] = i;
             s.pp[nval] = static_cast<int>(c);
