@@ -9,6 +9,7 @@
 // (include/h2j_jobs.h); dequantisation, transforms, intra prediction and
 // the loop filters run on the GPU.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -78,6 +79,7 @@ struct SliceHdr {
     int first_in_pic = 0, dependent = 0, address = 0, slice_addr_rs = 0, pps_id = 0, type = 0;
     int sao_luma = 0, sao_chroma = 0, qp_delta = 0, cb_qp_offset = 0, cr_qp_offset = 0;
     int deblock_disabled = 0, beta_offset = 0, tc_offset = 0, lf_across_slices = 0, slice_qp = 26;
+    std::vector<uint32_t> entry;  // entry_point_offset_minus1[i] + 1 (bytes, emulation prevention included)
 };
 
 const uint8_t kSlIntra[64] = {
@@ -378,15 +380,27 @@ int chroma_qp_table(int qpi) {
 
 class HevcParser {
 public:
-    explicit HevcParser(FrameJob& job) : job_(&job) {}
+    explicit HevcParser(FrameJob& job) : job_(&job), ctbs_(&job.ctbs) {}
     // a worker for one slice group of the same picture: the picture state (parameter sets,
     // geometry, maps, slice headers) copied, its own outputs
-    HevcParser(const HevcParser& proto, FrameJob& job) : HevcParser(proto) { job_ = &job; }
+    HevcParser(const HevcParser& proto, FrameJob& job) : HevcParser(proto) {
+        job_ = &job;
+        ctbs_ = &job.ctbs;
+        bind_maps();
+    }
+    // a worker for the CTB rows of one WPP slice: the picture maps and CTB records are the
+    // prototype's (rows write disjoint parts; a row reads the row above only behind its
+    // progress counter), the TB records its own
+    HevcParser(const HevcParser& proto, bool share_maps) : HevcParser(proto) {
+        (void)share_maps;
+        ctbs_ = proto.ctbs_;
+    }
     int run(const uint8_t* data, size_t size, int threads);
 
 private:
     HevcParser(const HevcParser&) = default;
     FrameJob* job_;
+    std::vector<h2j_ctb>* ctbs_;  // CTB records (SAO parameters; read back by sao_merge_left/up)
     Sps sps_[16];
     Pps pps_[64];
     const Sps* s_ = nullptr;
@@ -397,10 +411,22 @@ private:
     // picture geometry
     int W = 0, H = 0, log2ctb = 0, ctbs = 0, ctbW = 0, ctbH = 0, nctb = 0, mw = 0, mh = 0;
     int qpbd = 0;
-    // maps (4x4 granularity)
-    std::vector<int8_t> qp_;
-    std::vector<uint8_t> ipm_, ctd_;
-    std::vector<int> ctb_addr_rs_, ctb_slice_, rs2ts_, ts2rs_, tile_id_, col_bd_;
+    // maps (4x4 granularity): storage, and the pointers decoding uses (own storage, or the
+    // prototype's for WPP row workers)
+    std::vector<int8_t> qp_store_;
+    std::vector<uint8_t> ipm_store_, ctd_store_;
+    std::vector<int> addr_store_, slice_store_;
+    int8_t* qp_ = nullptr;
+    uint8_t *ipm_ = nullptr, *ctd_ = nullptr;
+    int *ctb_addr_rs_ = nullptr, *ctb_slice_ = nullptr;
+    void bind_maps() {
+        qp_ = qp_store_.data();
+        ipm_ = ipm_store_.data();
+        ctd_ = ctd_store_.data();
+        ctb_addr_rs_ = addr_store_.data();
+        ctb_slice_ = slice_store_.data();
+    }
+    std::vector<int> rs2ts_, ts2rs_, tile_id_, col_bd_;
     // slice decode state
     const SliceHdr* cur_ = nullptr;
     int cur_idx_ = 0;
@@ -418,6 +444,9 @@ private:
     void setup_picture();
     void setup_tiles();
     int decode_slice_data(int shi, const uint8_t* p, const uint8_t* end);
+    struct WppRows;
+    int decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t* end, WppRows& w);
+    int run_wpp(const std::vector<uint8_t>& seg, const std::vector<uint32_t>& sub, int threads);
     void ctb_start_contexts(int rs, int ts, bool first);
     void init_contexts(int qp) {
         for (int i = 0; i < NUM_CTX; i++) {
@@ -446,7 +475,7 @@ private:
     std::vector<h2j_tu> chroma_tmp_;
     uint8_t edge_flags(int x0, int y0) const;
     void pcm_sample(int x0, int y0, int log2cb);
-    void set_map(std::vector<uint8_t>& m, int x0, int y0, int n, uint8_t v) {
+    void set_map(uint8_t* m, int x0, int y0, int n, uint8_t v) {
         int ye = std::min((y0 + n) >> 2, mh), xe = std::min((x0 + n) >> 2, mw);
         for (int y = y0 >> 2; y < ye; y++) std::memset(&m[y * mw + (x0 >> 2)], v, static_cast<size_t>(xe - (x0 >> 2)));
     }
@@ -543,7 +572,7 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
         if (ne > 0) {
             int len = static_cast<int>(b.ue()) + 1;
             if (len > 32) return -1;
-            for (int i = 0; i < ne; i++) b.u(len);
+            for (int i = 0; i < ne; i++) sh.entry.push_back(b.u(len) + 1u);
         }
     }
     if (p.slice_header_ext) {
@@ -566,11 +595,12 @@ void HevcParser::setup_picture() {
     mw = (W + 3) >> 2;
     mh = (H + 3) >> 2;
     qpbd = 6 * (s_->bit_depth - 8);
-    qp_.assign(static_cast<size_t>(mw) * mh, 0);
-    ipm_.assign(static_cast<size_t>(mw) * mh, 1);
-    ctd_.assign(static_cast<size_t>(mw) * mh, 0);
-    ctb_addr_rs_.assign(nctb, -1);
-    ctb_slice_.assign(nctb, -1);
+    qp_store_.assign(static_cast<size_t>(mw) * mh, 0);
+    ipm_store_.assign(static_cast<size_t>(mw) * mh, 1);
+    ctd_store_.assign(static_cast<size_t>(mw) * mh, 0);
+    addr_store_.assign(nctb, -1);
+    slice_store_.assign(nctb, -1);
+    bind_maps();
     rs2ts_.assign(nctb, 0);
     ts2rs_.assign(nctb, 0);
     tile_id_.assign(nctb, 0);
@@ -690,7 +720,7 @@ void HevcParser::qg_start(int xq, int yq) {
 
 void HevcParser::parse_sao(int rx, int ry) {
     int ctb = ry * ctbW + rx;
-    h2j_ctb& r = job_->ctbs[ctb];
+    h2j_ctb& r = (*ctbs_)[ctb];
     uint32_t ts = r.ts;
     uint16_t tile = r.tile;
     std::memset(&r, 0, sizeof(r));
@@ -699,7 +729,7 @@ void HevcParser::parse_sao(int rx, int ry) {
     r.slice = static_cast<uint8_t>(cur_idx_);
     if (!cur_->sao_luma && !cur_->sao_chroma) return;
     auto copy_from = [&](int src) {
-        const h2j_ctb& o = job_->ctbs[src];
+        const h2j_ctb& o = (*ctbs_)[src];
         std::memcpy(r.type, o.type, 3);
         std::memcpy(r.band_pos, o.band_pos, 3);
         std::memcpy(r.eo_class, o.eo_class, 3);
@@ -1217,7 +1247,12 @@ void HevcParser::ctb_start_contexts(int rs, int ts, bool first) {
     } else {
         init_contexts(cur_->slice_qp);
     }
-    if (tile_start || row_start) first_qg_ = true;
+    // qPY_PREV = SliceQpY for the first QG of a tile / of a CTB row under WPP (8.6.1), also
+    // when qg_start runs again for a QG smaller than the CTB
+    if (tile_start || row_start) {
+        first_qg_ = true;
+        last_cu_qp_ = cur_->slice_qp;
+    }
 }
 
 int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end) {
@@ -1270,6 +1305,97 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
     return 0;
 }
 
+// WPP (entropy_coding_sync) rows of one slice decoded side by side: row r may parse CTB x
+// once row r-1 has finished CTB x+1 (its contexts after CTB 1 seed row r, 9.3.1 / 9.3.2.4;
+// split-flag, availability and SAO-merge neighbours lie at most one CTB up and to the right).
+struct HevcParser::WppRows {
+    std::unique_ptr<std::atomic<int>[]> done;      // per row: CTBs finished
+    std::vector<std::array<uint16_t, NUM_CTX>> ctx;  // per row: contexts after its 2nd CTB
+    std::atomic<bool> failed{false};
+};
+
+int HevcParser::decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t* end, WppRows& w) {
+    const SliceHdr& sh = sh_[shi];
+    cur_ = &sh;
+    cur_idx_ = shi;
+    end_ = end;
+    cc_.init(p, end);
+    first_qg_ = true;  // qPY_PREV = SliceQpY at a WPP row start (8.6.1)
+    last_cu_qp_ = sh.slice_qp;
+    for (int rx = 0; rx < ctbW; rx++) {
+        const int rs = row * ctbW + rx;
+        if (row > 0) {
+            const int need = std::min(rx + 2, ctbW);
+            for (int spin = 0; w.done[row - 1].load(std::memory_order_acquire) < need; spin++) {
+                if (w.failed.load(std::memory_order_relaxed)) return -31;
+                if (spin > 64) std::this_thread::yield();
+            }
+        }
+        ctb_slice_[rs] = shi;
+        ctb_addr_rs_[rs] = sh.slice_addr_rs;
+        if (rx == 0) {
+            if (row > 0 && ctbW > 1) std::memcpy(ctx_, w.ctx[row - 1].data(), sizeof(ctx_));
+            else init_contexts(sh.slice_qp);
+        }
+        parse_sao(rx, row);
+        const size_t first_tu = job_->tus.size();
+        coding_quadtree(rx << log2ctb, row << log2ctb, log2ctb, 0);
+        if (err_) return err_;
+        split_ctb_records(first_tu);
+        const int endf = cc_.terminate();
+        if (rx == 1) std::memcpy(w.ctx[row].data(), ctx_, sizeof(ctx_));
+        w.done[row].store(rx + 1, std::memory_order_release);
+        if (endf != (row == ctbH - 1 && rx == ctbW - 1)) return -30;
+    }
+    return 0;
+}
+
+// seg: the slice's data; sub: each row's substream start in it (from the entry points)
+int HevcParser::run_wpp(const std::vector<uint8_t>& seg, const std::vector<uint32_t>& sub, int threads) {
+    WppRows w;
+    w.done.reset(new std::atomic<int>[ctbH]);
+    for (int r = 0; r < ctbH; r++) w.done[r].store(0);
+    w.ctx.resize(ctbH);
+    std::vector<FrameJob> part(ctbH);
+    const int nt = std::min(threads, ctbH);
+    std::vector<std::unique_ptr<HevcParser>> wk(nt);
+    for (int t = 0; t < nt; t++) {
+        wk[t].reset(new HevcParser(*this, true));
+        wk[t]->p_ = &wk[t]->pps_[sh_[0].pps_id];
+        wk[t]->s_ = &wk[t]->sps_[wk[t]->p_->sps_id];
+    }
+    const uint8_t* end = seg.data() + (seg.size() - 8);
+    std::vector<int> rc(ctbH, 0);
+    std::atomic<int> next(0);
+    // rows are claimed in order, so every row waited on is already being decoded
+    auto work = [&](HevcParser& P) {
+        for (int r = next++; r < ctbH; r = next++) {
+            P.job_ = &part[r];
+            P.err_ = 0;
+            rc[r] = P.decode_wpp_row(0, r, seg.data() + sub[r], end, w);
+            if (rc[r] < 0) {
+                w.failed.store(true);
+                w.done[r].store(ctbW, std::memory_order_release);
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work, std::ref(*wk[t]));
+    work(*wk[0]);
+    for (auto& t : pool) t.join();
+    for (int r = 0; r < ctbH; r++)
+        if (rc[r] < 0) return rc[r];
+    for (int r = 0; r < ctbH; r++) {
+        const uint32_t cbase = static_cast<uint32_t>(job_->coefs.size());
+        for (h2j_tu t : part[r].tus) {
+            if (t.ncoef) t.coef += cbase;  // (records without coefficients keep coef 0)
+            job_->tus.push_back(t);
+        }
+        job_->coefs.insert(job_->coefs.end(), part[r].coefs.begin(), part[r].coefs.end());
+    }
+    return 0;
+}
+
 int HevcParser::run(const uint8_t* data, size_t size, int threads) {
     init_scans();
     std::vector<Nal> nals;
@@ -1279,6 +1405,7 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
     const SliceHdr* prev = nullptr;
     sh_.reserve(256);
     std::vector<std::vector<uint8_t>> seg;  // per slice segment: its slice data (+8 zero bytes)
+    std::vector<std::vector<uint32_t>> seg_sub;  // per slice segment: substream starts in it
     for (const Nal& nal : nals) {
         if (nal.n < 2) continue;
         const int type = (nal.p[0] >> 1) & 63;
@@ -1316,6 +1443,32 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
             if (off > rn) { job_->message = "truncated slice"; return -6; }
             seg.emplace_back(rbsp_.begin() + static_cast<long>(off), rbsp_.begin() + static_cast<long>(rn));
             seg.back().resize(seg.back().size() + 8, 0);
+            seg_sub.emplace_back();
+            if (!sh.entry.empty()) {
+                // entry points count escaped bytes: map them into the unescaped slice data
+                const uint8_t* src = nal.p + 2;
+                std::vector<size_t> epb;  // escaped positions of emulation-prevention bytes
+                int zeros = 0;
+                for (size_t i = 0; i < nal.n - 2; i++) {
+                    if (zeros >= 2 && src[i] == 3) {
+                        epb.push_back(i);
+                        zeros = 0;
+                        continue;
+                    }
+                    zeros = src[i] == 0 ? zeros + 1 : 0;
+                }
+                size_t e = off, j = 0;
+                while (j < epb.size() && epb[j] <= e) { e++; j++; }
+                std::vector<uint32_t>& su = seg_sub.back();
+                su.push_back(0);
+                for (uint32_t len : sh.entry) {
+                    e += len;
+                    while (j < epb.size() && epb[j] < e) j++;
+                    const size_t u = e - j - off;
+                    if (u >= rn - off) { su.clear(); break; }  // inconsistent: decode sequentially
+                    su.push_back(static_cast<uint32_t>(u));
+                }
+            }
             h2j_slice rec{};
             rec.beta_offset = static_cast<int8_t>(sh.beta_offset);
             rec.tc_offset = static_cast<int8_t>(sh.tc_offset);
@@ -1350,7 +1503,11 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
         }
         return 0;
     };
-    if (threads <= 1 || ng <= 1) {
+    if (threads > 1 && ng == 1 && sh_.size() == 1 && p_->wpp && !p_->tiles && sh_[0].address == 0 && ctbH > 1 &&
+        seg_sub[0].size() == static_cast<size_t>(ctbH)) {
+        // one WPP slice (the usual single-slice x265 picture): its CTB rows in parallel
+        if (run_wpp(seg[0], seg_sub[0], threads) < 0) { job_->message = "slice data decode error"; return -7; }
+    } else if (threads <= 1 || ng <= 1) {
         for (int g = 0; g < ng; g++)
             if (decode_group(*this, g) < 0) { job_->message = "slice data decode error"; return -7; }
     } else {

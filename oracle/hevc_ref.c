@@ -1383,7 +1383,9 @@ static void ctb_start_contexts(Dec *d, SliceHdr *sh, int ctbAddrRs, int ctbAddrT
     } else {
         init_contexts(d, sh->slice_qp);
     }
-    if (tile_start || row_start) d->first_qg = 1;
+    /* qPY_PREV = SliceQpY for the first QG of a tile / of a CTB row under WPP (8.6.1): also for
+     * the QG-size call that follows the CTB-level one (FFmpeg hevcdec first_qp_group) */
+    if (tile_start || row_start) { d->first_qg = 1; d->last_cu_qp = d->cur->slice_qp; }
 }
 
 static int decode_slice_data(Dec *d, int shi) {

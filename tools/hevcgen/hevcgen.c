@@ -203,7 +203,7 @@ typedef struct {
     int outW, outH;
     int bd;
     int qp;
-    int sdh, tskip, qpdelta, sao, pcm, bypass, slice_rows, depth, log2ctb, beta, tc, cbqp, crqp;
+    int sdh, tskip, qpdelta, sao, pcm, bypass, slice_rows, depth, log2ctb, beta, tc, cbqp, crqp, wpp;
     int strong;
     int log2maxtb;
 } Opt;
@@ -1171,7 +1171,7 @@ static void write_pps(FILE *f, const Opt *o) {
     bw_put(&b, 0, 1); bw_put(&b, 0, 1);
     bw_put(&b, (uint32_t)o->bypass, 1);
     bw_put(&b, 0, 1);  /* tiles */
-    bw_put(&b, 0, 1);  /* wpp */
+    bw_put(&b, (uint32_t)o->wpp, 1);  /* entropy_coding_sync (WPP) */
     bw_put(&b, 1, 1);  /* loop filter across slices */
     int dfc = o->beta != 0 || o->tc != 0;
     bw_put(&b, (uint32_t)dfc, 1);
@@ -1220,6 +1220,7 @@ int main(int argc, char **argv) {
     o->tc = opt_int(argc, argv, "--tc", 0);
     o->cbqp = opt_int(argc, argv, "--cbqp", 0);
     o->crqp = opt_int(argc, argv, "--crqp", 0);
+    o->wpp = opt_int(argc, argv, "--wpp", 0);
     o->strong = 1;
     int ctb = opt_int(argc, argv, "--ctb", 64);
     o->log2ctb = ctb == 16 ? 4 : (ctb == 32 ? 5 : 6);
@@ -1292,24 +1293,74 @@ int main(int argc, char **argv) {
         bw_se(&b, g->slice_qp - 26);
         /* pps_loop_filter_across_slices_enabled: signal slice flag */
         if (1) bw_put(&b, (uint32_t)(nslice % 2 == 0), 1);
-        bw_put(&b, 1, 1);      /* byte_alignment */
-        bw_align_zero(&b);
+        /* slice data: one substream per CTB row with WPP (7.3.8.1 end_of_subset_one_bit +
+         * byte_alignment; contexts stored after the row's 2nd CTB, 9.3.2.4, and synchronised
+         * at the next row's start, 9.3.1), else one */
+        int r1 = r0 + rows_per_slice < g->ctbH ? r0 + rows_per_slice : g->ctbH;
+        int nsub = o->wpp ? r1 - r0 : 1, ks = 0;
+        BW *sub = (BW *)calloc((size_t)nsub, sizeof(BW));
+        uint8_t wpp_ctx[NUM_CTX];
+        bw_init(&sub[0]);
         init_contexts(g, g->slice_qp);
-        ce_start(&g->ce, &b);
+        ce_start(&g->ce, &sub[0]);
         g->first_qg = 1;
         g->last_cu_qp = g->slice_qp;
-        int r1 = r0 + rows_per_slice < g->ctbH ? r0 + rows_per_slice : g->ctbH;
-        for (int ry = r0; ry < r1; ry++)
+        for (int ry = r0; ry < r1; ry++) {
+            if (o->wpp && ry > r0) {
+                if (g->ctbW > 1) memcpy(g->ctx, wpp_ctx, NUM_CTX);
+                else init_contexts(g, g->slice_qp);
+                g->first_qg = 1;
+                g->last_cu_qp = g->slice_qp; /* qPY_PREV of the row's first QG (8.6.1) */
+            }
             for (int rx = 0; rx < g->ctbW; rx++) {
                 g->ctb_slice[ry * g->ctbW + rx] = nslice;
                 if (o->sao) write_sao(g, rx, ry, sao);
                 coding_quadtree(g, rx << o->log2ctb, ry << o->log2ctb, o->log2ctb, 0, log2qg);
+                if (o->wpp && rx == 1) memcpy(wpp_ctx, g->ctx, NUM_CTX);
                 int last = ry == r1 - 1 && rx == g->ctbW - 1;
                 ce_term(&g->ce, last);
+                if (!last && o->wpp && rx == g->ctbW - 1) {
+                    ce_term(&g->ce, 1); /* end_of_subset_one_bit */
+                    ce_finish(&g->ce);
+                    bw_put(&sub[ks], 1, 1);
+                    bw_align_zero(&sub[ks]);
+                    bw_init(&sub[++ks]);
+                    ce_start(&g->ce, &sub[ks]);
+                }
             }
+        }
         ce_finish(&g->ce);
-        bw_put(&b, 1, 1);
+        bw_put(&sub[ks], 1, 1);
+        bw_align_zero(&sub[ks]);
+        if (o->wpp) {
+            /* entry points: substream sizes with their emulation-prevention bytes (every
+             * substream ends in a non-zero byte, so each one's escaping is self-contained) */
+            uint32_t mx = 1, *sz = (uint32_t *)calloc((size_t)nsub, 4);
+            for (int k = 0; k < nsub; k++) {
+                int zeros = 0;
+                sz[k] = (uint32_t)sub[k].n;
+                for (size_t i = 0; i < sub[k].n; i++) {
+                    if (zeros >= 2 && sub[k].buf[i] <= 3) { sz[k]++; zeros = 0; }
+                    zeros = sub[k].buf[i] == 0 ? zeros + 1 : 0;
+                }
+                if (k < nsub - 1 && sz[k] > mx) mx = sz[k];
+            }
+            bw_ue(&b, (uint32_t)(nsub - 1));
+            if (nsub > 1) {
+                int len = 1;
+                while ((1u << len) < mx) len++; /* offsets - 1 fit in len bits */
+                bw_ue(&b, (uint32_t)(len - 1));
+                for (int k = 0; k < nsub - 1; k++) bw_put(&b, sz[k] - 1, len);
+            }
+            free(sz);
+        }
+        bw_put(&b, 1, 1); /* byte_alignment */
         bw_align_zero(&b);
+        for (int k = 0; k < nsub; k++) {
+            for (size_t i = 0; i < sub[k].n; i++) bw_put(&b, sub[k].buf[i], 8);
+            free(sub[k].buf);
+        }
+        free(sub);
         write_nal(fo, 19, b.buf, b.n); /* IDR_W_RADL */
         free(b.buf);
     }

@@ -122,6 +122,12 @@ PARITY = [
     ("p10_480x272_slices2", 480, 272, 8, 31, 20, 1, ["--slices", "2", "--bypass", "1"]),
     ("p11_64x64_tiny", 64, 64, 8, 26, 21, 2, []),
     ("p12_72x40_odd_crop", 72, 40, 8, 26, 22, 2, ["--ctb", "16"]),
+    ("p13_416x240_wpp", 416, 240, 8, 27, 23, 2, ["--wpp", "1"]),
+    ("p14_480x272_wpp_slices_ctb32", 480, 272, 8, 30, 24, 2, ["--wpp", "1", "--slices", "2", "--ctb", "32"]),
+    ("p15_48x200_wpp_narrow", 48, 200, 8, 26, 25, 2, ["--wpp", "1"]),
+    ("p16_1280x720_wpp_ctb32", 1280, 720, 8, 24, 26, 3, ["--wpp", "1", "--ctb", "32"]),
+    # black top third: PCM samples of 0 put emulation-prevention bytes inside WPP substreams
+    ("p17_416x240_10bit_wpp_pcm_black", 416, 240, 10, 30, 28, 0, ["--wpp", "1", "--pcm", "1", "--ctb", "32"]),
 ]
 
 
@@ -132,6 +138,8 @@ def parity():
     manifest = []
     for name, W, H, bd, qp, seed, sigma, opts in PARITY:
         content = make_content(planes, W, H, seed, sigma, bd)
+        if "black" in name:
+            content[0][: H // 3] = 0
         path = os.path.join(out_dir, name + ".h265")
         nb = encode(content, W, H, bd, qp, seed, path, opts)
         manifest.append({"file": name + ".h265", "w": W, "h": H, "bit_depth": bd, "qp": qp, "options": opts})
