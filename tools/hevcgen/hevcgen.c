@@ -204,6 +204,7 @@ typedef struct {
     int bd;
     int qp;
     int sdh, tskip, qpdelta, sao, pcm, bypass, slice_rows, depth, log2ctb, beta, tc, cbqp, crqp, wpp;
+    int tile_cols, tile_rows, lf_tiles; /* uniform tile grid (1 x 1 = no tiles) */
     int strong;
     int log2maxtb;
 } Opt;
@@ -217,6 +218,7 @@ typedef struct {
     int8_t *qpm;
     uint8_t *ipm, *ctd;
     int *ctb_slice; /* slice index per CTB (-1 = not coded) */
+    int *rs2ts, *ts2rs, *tile_id, *col_bd; /* tile scan (6.5.1); identity without tiles */
     /* state */
     uint8_t ctx[NUM_CTX];
     Enc ce;
@@ -243,13 +245,14 @@ static int zs(G *g, int x, int y) {
     int ctb = (y >> g->o.log2ctb) * g->ctbW + (x >> g->o.log2ctb);
     int xi = (x & (g->ctbs - 1)) >> 2, yi = (y & (g->ctbs - 1)) >> 2, z = 0;
     for (int i = 0; i < 5; i++) z |= (((xi >> i) & 1) << (2 * i)) | (((yi >> i) & 1) << (2 * i + 1));
-    return (ctb << (2 * (g->o.log2ctb - 2))) + z;
+    return (g->rs2ts[ctb] << (2 * (g->o.log2ctb - 2))) + z; /* decoding order */
 }
 static int avail(G *g, int xc, int yc, int xn, int yn) {
     if (xn < 0 || yn < 0 || xn >= g->o.CW || yn >= g->o.CH) return 0;
     int cn = (yn >> g->o.log2ctb) * g->ctbW + (xn >> g->o.log2ctb);
     int cc = (yc >> g->o.log2ctb) * g->ctbW + (xc >> g->o.log2ctb);
     if (g->ctb_slice[cn] < 0 || g->ctb_slice[cn] != g->ctb_slice[cc]) return 0;
+    if (g->tile_id[cn] != g->tile_id[cc]) return 0;
     return zs(g, xn, yn) <= zs(g, xc, yc);
 }
 
@@ -1044,12 +1047,12 @@ static void write_sao(G *g, int rx, int ry, Sao *tab) {
     Sao *s = &tab[ctb];
     memset(s, 0, sizeof(*s));
     int bd = g->o.bd, cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
-    if (rx > 0 && g->ctb_slice[ctb - 1] == g->ctb_slice[ctb]) {
+    if (rx > 0 && g->ctb_slice[ctb - 1] == g->ctb_slice[ctb] && g->tile_id[ctb - 1] == g->tile_id[ctb]) {
         int m = rndn(4) == 0;
         ce_bin(&g->ce, &g->ctx[C_SAO_MERGE], m);
         if (m) { *s = tab[ctb - 1]; return; }
     }
-    if (ry > 0 && g->ctb_slice[ctb - g->ctbW] == g->ctb_slice[ctb]) {
+    if (ry > 0 && g->ctb_slice[ctb - g->ctbW] == g->ctb_slice[ctb] && g->tile_id[ctb - g->ctbW] == g->tile_id[ctb]) {
         int m = rndn(4) == 0;
         ce_bin(&g->ce, &g->ctx[C_SAO_MERGE], m);
         if (m) { *s = tab[ctb - g->ctbW]; return; }
@@ -1170,8 +1173,15 @@ static void write_pps(FILE *f, const Opt *o) {
     bw_put(&b, 0, 1);  /* slice chroma qp offsets present */
     bw_put(&b, 0, 1); bw_put(&b, 0, 1);
     bw_put(&b, (uint32_t)o->bypass, 1);
-    bw_put(&b, 0, 1);  /* tiles */
+    int tiles = o->tile_cols > 1 || o->tile_rows > 1;
+    bw_put(&b, (uint32_t)tiles, 1);
     bw_put(&b, (uint32_t)o->wpp, 1);  /* entropy_coding_sync (WPP) */
+    if (tiles) {
+        bw_ue(&b, (uint32_t)(o->tile_cols - 1));
+        bw_ue(&b, (uint32_t)(o->tile_rows - 1));
+        bw_put(&b, 1, 1); /* uniform_spacing */
+        bw_put(&b, (uint32_t)o->lf_tiles, 1);
+    }
     bw_put(&b, 1, 1);  /* loop filter across slices */
     int dfc = o->beta != 0 || o->tc != 0;
     bw_put(&b, (uint32_t)dfc, 1);
@@ -1221,6 +1231,9 @@ int main(int argc, char **argv) {
     o->cbqp = opt_int(argc, argv, "--cbqp", 0);
     o->crqp = opt_int(argc, argv, "--crqp", 0);
     o->wpp = opt_int(argc, argv, "--wpp", 0);
+    o->tile_cols = opt_int(argc, argv, "--tilecols", 1);
+    o->tile_rows = opt_int(argc, argv, "--tilerows", 1);
+    o->lf_tiles = opt_int(argc, argv, "--lftiles", 1);
     o->strong = 1;
     int ctb = opt_int(argc, argv, "--ctb", 64);
     o->log2ctb = ctb == 16 ? 4 : (ctb == 32 ? 5 : 6);
@@ -1264,6 +1277,31 @@ int main(int argc, char **argv) {
     int nctb = g->ctbW * g->ctbH;
     g->ctb_slice = (int *)malloc(sizeof(int) * nctb);
     for (int i = 0; i < nctb; i++) g->ctb_slice[i] = -1;
+    /* tile scan: uniform column / row boundaries (6.5.1), tiles in raster order, CTBs in
+     * raster order inside each tile */
+    if (o->tile_cols > g->ctbW) o->tile_cols = g->ctbW;
+    if (o->tile_rows > g->ctbH) o->tile_rows = g->ctbH;
+    if ((o->tile_cols > 1 || o->tile_rows > 1) && o->slice_rows) { fprintf(stderr, "tiles with --slices unsupported\n"); return 2; }
+    g->rs2ts = (int *)malloc(sizeof(int) * nctb);
+    g->ts2rs = (int *)malloc(sizeof(int) * nctb);
+    g->tile_id = (int *)malloc(sizeof(int) * nctb);
+    g->col_bd = (int *)malloc(sizeof(int) * (o->tile_cols + 1));
+    {
+        int *row_bd = (int *)malloc(sizeof(int) * (o->tile_rows + 1));
+        for (int i = 0; i <= o->tile_cols; i++) g->col_bd[i] = i * g->ctbW / o->tile_cols;
+        for (int i = 0; i <= o->tile_rows; i++) row_bd[i] = i * g->ctbH / o->tile_rows;
+        int ts = 0;
+        for (int ty = 0; ty < o->tile_rows; ty++)
+            for (int tx = 0; tx < o->tile_cols; tx++)
+                for (int y = row_bd[ty]; y < row_bd[ty + 1]; y++)
+                    for (int x = g->col_bd[tx]; x < g->col_bd[tx + 1]; x++) {
+                        int rs = y * g->ctbW + x;
+                        g->rs2ts[rs] = ts;
+                        g->ts2rs[ts++] = rs;
+                        g->tile_id[rs] = ty * o->tile_cols + tx;
+                    }
+        free(row_bd);
+    }
     g_nodes = (TNode *)malloc(sizeof(TNode) * 128);
     Sao *sao = (Sao *)calloc((size_t)nctb, sizeof(Sao));
 
@@ -1297,7 +1335,15 @@ int main(int argc, char **argv) {
          * byte_alignment; contexts stored after the row's 2nd CTB, 9.3.2.4, and synchronised
          * at the next row's start, 9.3.1), else one */
         int r1 = r0 + rows_per_slice < g->ctbH ? r0 + rows_per_slice : g->ctbH;
-        int nsub = o->wpp ? r1 - r0 : 1, ks = 0;
+        /* CTBs of the slice in decoding (tile-scan) order; a new substream at every tile
+         * start and, with WPP, at every CTB row of a tile */
+        const int ts0 = r0 * g->ctbW, ts1 = r1 * g->ctbW;
+        int nsub = 1, ks = 0;
+        for (int ts = ts0 + 1; ts < ts1; ts++) {
+            int rs = g->ts2rs[ts], rx = rs % g->ctbW, tc = 0;
+            while (rx >= g->col_bd[tc + 1]) tc++;
+            if (g->tile_id[rs] != g->tile_id[g->ts2rs[ts - 1]] || (o->wpp && rx == g->col_bd[tc])) nsub++;
+        }
         BW *sub = (BW *)calloc((size_t)nsub, sizeof(BW));
         uint8_t wpp_ctx[NUM_CTX];
         bw_init(&sub[0]);
@@ -1305,34 +1351,37 @@ int main(int argc, char **argv) {
         ce_start(&g->ce, &sub[0]);
         g->first_qg = 1;
         g->last_cu_qp = g->slice_qp;
-        for (int ry = r0; ry < r1; ry++) {
-            if (o->wpp && ry > r0) {
-                if (g->ctbW > 1) memcpy(g->ctx, wpp_ctx, NUM_CTX);
+        for (int ts = ts0; ts < ts1; ts++) {
+            const int rs = g->ts2rs[ts], rx = rs % g->ctbW, ry = rs / g->ctbW;
+            int tc = 0;
+            while (rx >= g->col_bd[tc + 1]) tc++;
+            const int tile_start = ts > ts0 && g->tile_id[rs] != g->tile_id[g->ts2rs[ts - 1]];
+            const int row_start = ts > ts0 && o->wpp && rx == g->col_bd[tc];
+            if (tile_start || row_start) {
+                ce_term(&g->ce, 1); /* end_of_subset_one_bit */
+                ce_finish(&g->ce);
+                bw_put(&sub[ks], 1, 1);
+                bw_align_zero(&sub[ks]);
+                bw_init(&sub[++ks]);
+                ce_start(&g->ce, &sub[ks]);
+                /* 9.3.1: initialise at a tile start; at a WPP row start synchronise with the
+                 * contexts after the 2nd CTB of the row above when that CTB is available */
+                if (!tile_start && ry > 0 && rx + 1 < g->col_bd[tc + 1] && g->ctb_slice[rs - g->ctbW + 1] == nslice)
+                    memcpy(g->ctx, wpp_ctx, NUM_CTX);
                 else init_contexts(g, g->slice_qp);
                 g->first_qg = 1;
-                g->last_cu_qp = g->slice_qp; /* qPY_PREV of the row's first QG (8.6.1) */
+                g->last_cu_qp = g->slice_qp; /* qPY_PREV of the first QG (8.6.1) */
             }
-            for (int rx = 0; rx < g->ctbW; rx++) {
-                g->ctb_slice[ry * g->ctbW + rx] = nslice;
-                if (o->sao) write_sao(g, rx, ry, sao);
-                coding_quadtree(g, rx << o->log2ctb, ry << o->log2ctb, o->log2ctb, 0, log2qg);
-                if (o->wpp && rx == 1) memcpy(wpp_ctx, g->ctx, NUM_CTX);
-                int last = ry == r1 - 1 && rx == g->ctbW - 1;
-                ce_term(&g->ce, last);
-                if (!last && o->wpp && rx == g->ctbW - 1) {
-                    ce_term(&g->ce, 1); /* end_of_subset_one_bit */
-                    ce_finish(&g->ce);
-                    bw_put(&sub[ks], 1, 1);
-                    bw_align_zero(&sub[ks]);
-                    bw_init(&sub[++ks]);
-                    ce_start(&g->ce, &sub[ks]);
-                }
-            }
+            g->ctb_slice[rs] = nslice;
+            if (o->sao) write_sao(g, rx, ry, sao);
+            coding_quadtree(g, rx << o->log2ctb, ry << o->log2ctb, o->log2ctb, 0, log2qg);
+            if (o->wpp && rx == g->col_bd[tc] + 1) memcpy(wpp_ctx, g->ctx, NUM_CTX);
+            ce_term(&g->ce, ts == ts1 - 1); /* end_of_slice_segment_flag */
         }
         ce_finish(&g->ce);
         bw_put(&sub[ks], 1, 1);
         bw_align_zero(&sub[ks]);
-        if (o->wpp) {
+        if (o->wpp || o->tile_cols > 1 || o->tile_rows > 1) {
             /* entry points: substream sizes with their emulation-prevention bytes (every
              * substream ends in a non-zero byte, so each one's escaping is self-contained) */
             uint32_t mx = 1, *sz = (uint32_t *)calloc((size_t)nsub, 4);

@@ -128,6 +128,9 @@ PARITY = [
     ("p16_1280x720_wpp_ctb32", 1280, 720, 8, 24, 26, 3, ["--wpp", "1", "--ctb", "32"]),
     # black top third: PCM samples of 0 put emulation-prevention bytes inside WPP substreams
     ("p17_416x240_10bit_wpp_pcm_black", 416, 240, 10, 30, 28, 0, ["--wpp", "1", "--pcm", "1", "--ctb", "32"]),
+    ("p18_416x240_tiles3x2_ctb32", 416, 240, 8, 28, 29, 2, ["--ctb", "32", "--tilecols", "3", "--tilerows", "2"]),
+    ("p19_480x272_tiles2x2_wpp_nolf", 480, 272, 8, 30, 30, 2, ["--ctb", "32", "--tilecols", "2", "--tilerows", "2", "--wpp", "1", "--lftiles", "0"]),
+    ("p20_80x96_tiles5x3_wpp_narrow", 80, 96, 8, 26, 31, 2, ["--ctb", "16", "--tilecols", "5", "--tilerows", "3", "--wpp", "1"]),
 ]
 
 
