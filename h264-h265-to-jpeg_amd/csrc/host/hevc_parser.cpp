@@ -447,6 +447,9 @@ private:
     struct WppRows;
     int decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t* end, WppRows& w);
     int run_wpp(const std::vector<uint8_t>& seg, const std::vector<uint32_t>& sub, int threads);
+    int decode_tile(int shi, int ts0, int ts1, bool last, const uint8_t* p, const uint8_t* end);
+    int run_tiles(const std::vector<uint8_t>& seg, const std::vector<uint32_t>& sub, int threads);
+    void merge_parts(const std::vector<FrameJob>& part);
     void ctb_start_contexts(int rs, int ts, bool first);
     void init_contexts(int qp) {
         for (int i = 0; i < NUM_CTX; i++) {
@@ -458,8 +461,8 @@ private:
         if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
         int cn = (yn >> log2ctb) * ctbW + (xn >> log2ctb);
         int cc = (yc >> log2ctb) * ctbW + (xc >> log2ctb);
-        if (ctb_slice_[cn] < 0) return false;
-        return ctb_addr_rs_[cn] == ctb_addr_rs_[cc] && tile_id_[rs2ts_[cn]] == tile_id_[rs2ts_[cc]];
+        if (tile_id_[rs2ts_[cn]] != tile_id_[rs2ts_[cc]] || ctb_slice_[cn] < 0) return false;
+        return ctb_addr_rs_[cn] == ctb_addr_rs_[cc];
     }
     void qg_start(int xq, int yq);
     void parse_sao(int rx, int ry);
@@ -737,13 +740,13 @@ void HevcParser::parse_sao(int rx, int ry) {
     };
     if (rx > 0) {
         int l = ctb - 1;
-        if (ctb_slice_[l] >= 0 && ctb_addr_rs_[l] == ctb_addr_rs_[ctb] && tile_id_[rs2ts_[l]] == tile_id_[rs2ts_[ctb]]) {
+        if (tile_id_[rs2ts_[l]] == tile_id_[rs2ts_[ctb]] && ctb_slice_[l] >= 0 && ctb_addr_rs_[l] == ctb_addr_rs_[ctb]) {
             if (dec(C_SAO_MERGE)) { copy_from(l); return; }
         }
     }
     if (ry > 0) {
         int u = ctb - ctbW;
-        if (ctb_slice_[u] >= 0 && ctb_addr_rs_[u] == ctb_addr_rs_[ctb] && tile_id_[rs2ts_[u]] == tile_id_[rs2ts_[ctb]]) {
+        if (tile_id_[rs2ts_[u]] == tile_id_[rs2ts_[ctb]] && ctb_slice_[u] >= 0 && ctb_addr_rs_[u] == ctb_addr_rs_[ctb]) {
             if (dec(C_SAO_MERGE)) { copy_from(u); return; }
         }
     }
@@ -1385,14 +1388,82 @@ int HevcParser::run_wpp(const std::vector<uint8_t>& seg, const std::vector<uint3
     for (auto& t : pool) t.join();
     for (int r = 0; r < ctbH; r++)
         if (rc[r] < 0) return rc[r];
-    for (int r = 0; r < ctbH; r++) {
+    merge_parts(part);
+    return 0;
+}
+
+// records of the parts appended in decoding order
+void HevcParser::merge_parts(const std::vector<FrameJob>& part) {
+    for (const FrameJob& pj : part) {
         const uint32_t cbase = static_cast<uint32_t>(job_->coefs.size());
-        for (h2j_tu t : part[r].tus) {
+        for (h2j_tu t : pj.tus) {
             if (t.ncoef) t.coef += cbase;  // (records without coefficients keep coef 0)
             job_->tus.push_back(t);
         }
-        job_->coefs.insert(job_->coefs.end(), part[r].coefs.begin(), part[r].coefs.end());
+        job_->coefs.insert(job_->coefs.end(), pj.coefs.begin(), pj.coefs.end());
     }
+}
+
+// One tile of a slice (CTBs ts0..ts1-1 in tile scan): no parsing dependency on any other
+// tile (contexts initialised at the tile start, neighbours across tiles unavailable, 6.4.1).
+int HevcParser::decode_tile(int shi, int ts0, int ts1, bool last, const uint8_t* p, const uint8_t* end) {
+    const SliceHdr& sh = sh_[shi];
+    cur_ = &sh;
+    cur_idx_ = shi;
+    end_ = end;
+    cc_.init(p, end);
+    init_contexts(sh.slice_qp);
+    first_qg_ = true;
+    last_cu_qp_ = sh.slice_qp;
+    for (int ts = ts0; ts < ts1; ts++) {
+        const int rs = ts2rs_[ts];
+        parse_sao(rs % ctbW, rs / ctbW);
+        const size_t first_tu = job_->tus.size();
+        coding_quadtree((rs % ctbW) << log2ctb, (rs / ctbW) << log2ctb, log2ctb, 0);
+        if (err_) return err_;
+        split_ctb_records(first_tu);
+        if (cc_.terminate() != (last && ts == ts1 - 1)) return -30;
+    }
+    return 0;
+}
+
+// A single slice split into tiles (no WPP): its tiles in parallel from the entry points.
+int HevcParser::run_tiles(const std::vector<uint8_t>& seg, const std::vector<uint32_t>& sub, int threads) {
+    const int nt = static_cast<int>(sub.size());
+    std::vector<int> t0(nt + 1, nctb);
+    for (int ts = 0, t = 0; ts < nctb; ts++)
+        if (ts == 0 || tile_id_[ts] != tile_id_[ts - 1]) t0[t++] = ts;
+    // the slice covers the picture: its CTB ownership is known up front (deblocking-edge
+    // flags compare slice addresses across tile borders)
+    for (int rs = 0; rs < nctb; rs++) {
+        ctb_slice_[rs] = 0;
+        ctb_addr_rs_[rs] = sh_[0].slice_addr_rs;
+    }
+    std::vector<FrameJob> part(nt);
+    const int nw = std::min(threads, nt);
+    std::vector<std::unique_ptr<HevcParser>> wk(nw);
+    for (int w = 0; w < nw; w++) {
+        wk[w].reset(new HevcParser(*this, true));
+        wk[w]->p_ = &wk[w]->pps_[sh_[0].pps_id];
+        wk[w]->s_ = &wk[w]->sps_[wk[w]->p_->sps_id];
+    }
+    const uint8_t* end = seg.data() + (seg.size() - 8);
+    std::vector<int> rc(nt, 0);
+    std::atomic<int> next(0);
+    auto work = [&](HevcParser& P) {
+        for (int t = next++; t < nt; t = next++) {
+            P.job_ = &part[t];
+            P.err_ = 0;
+            rc[t] = P.decode_tile(0, t0[t], t0[t + 1], t == nt - 1, seg.data() + sub[t], end);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nw; w++) pool.emplace_back(work, std::ref(*wk[w]));
+    work(*wk[0]);
+    for (auto& t : pool) t.join();
+    for (int t = 0; t < nt; t++)
+        if (rc[t] < 0) return rc[t];
+    merge_parts(part);
     return 0;
 }
 
@@ -1507,6 +1578,10 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
         seg_sub[0].size() == static_cast<size_t>(ctbH)) {
         // one WPP slice (the usual single-slice x265 picture): its CTB rows in parallel
         if (run_wpp(seg[0], seg_sub[0], threads) < 0) { job_->message = "slice data decode error"; return -7; }
+    } else if (threads > 1 && ng == 1 && sh_.size() == 1 && p_->tiles && !p_->wpp && sh_[0].address == 0 &&
+               !seg_sub[0].empty() && seg_sub[0].size() == static_cast<size_t>(tile_id_[nctb - 1] + 1)) {
+        // one slice of several tiles: the tiles in parallel
+        if (run_tiles(seg[0], seg_sub[0], threads) < 0) { job_->message = "slice data decode error"; return -7; }
     } else if (threads <= 1 || ng <= 1) {
         for (int g = 0; g < ng; g++)
             if (decode_group(*this, g) < 0) { job_->message = "slice data decode error"; return -7; }

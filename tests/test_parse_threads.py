@@ -1,7 +1,7 @@
 """Intra-picture parallel parsing: pictures with several
 independent slices decode them on several host threads, and a single WPP
 (entropy_coding_sync) slice decodes its CTB rows side by side from the entry
-points; the records must be identical to a single-threaded parse (parse_bench
+points, and a single tiled slice its tiles; the records must be identical to a single-threaded parse (parse_bench
 output digest)."""
 import glob
 import os
@@ -30,12 +30,13 @@ def _digest(exe, path, threads):
 
 MULTI = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "h264", "*slices*.h264")) +
                glob.glob(os.path.join(ROOT, "tests", "golden", "hevc", "*slices*.h265")) +
-               glob.glob(os.path.join(ROOT, "tests", "golden", "hevc", "*wpp*.h265")))
+               glob.glob(os.path.join(ROOT, "tests", "golden", "hevc", "*wpp*.h265")) +
+               glob.glob(os.path.join(ROOT, "tests", "golden", "hevc", "p18_*tiles*.h265")))
 
 
 @pytest.mark.parametrize("path", MULTI, ids=[os.path.basename(p) for p in MULTI])
 def test_slice_parallel_parse_is_identical(parse_bench, path):
-    assert len(MULTI) >= 9
+    assert len(MULTI) >= 12
     one = _digest(parse_bench, path, 1)
     assert _digest(parse_bench, path, 8) == one
     assert _digest(parse_bench, path, 2) == one
