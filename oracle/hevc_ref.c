@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 
 #include "bits.h"
 #include "cabac_tables.h"
@@ -1758,9 +1759,14 @@ static void apply_sao(Dec *d) {
 }
 
 /* ------------------------------------------------------------ top level */
-int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture *out) {
+static void init_tables(void) {
     init_scans();
     init_tm();
+}
+static pthread_once_t tables_once = PTHREAD_ONCE_INIT; /* the CPU baseline calls from several threads */
+
+int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture *out) {
+    pthread_once(&tables_once, init_tables);
     memset(out, 0, sizeof(*out));
     int maxnal = 4096;
     OraNal *nals = (OraNal *)malloc(sizeof(OraNal) * maxnal);

@@ -312,7 +312,7 @@ DEFINE_QSORT(qsort_hufflen, HuffLen, cmp_len)
 
 /* package-merge, max length 16 (FFmpeg mjpegenc_huffman.c) */
 static void compute_bits(PTable *prob, HuffLen *distincts, int size, int max_length) {
-    static PMList la, lb; /* oracle is single-threaded per call site */
+    static __thread PMList la, lb; /* per thread: the CPU baseline runs several transcodes at once */
     PMList *to = &la, *from = &lb, *t;
     int nbits[257] = {0};
     int i = 0, j, k;
