@@ -155,6 +155,11 @@ def cpu_baseline(streams, threads, budget_s=12.0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py  # test infrastructure: only the cpu_baseline leg uses it
     oracle_py.transcode(streams[0])  # one-time table set-up outside the clock
+    lat = []
+    for _ in range(3):  # single-call latency on one core (the reference's own per-call figure)
+        t = time.perf_counter()
+        oracle_py.transcode(streams[0])
+        lat.append((time.perf_counter() - t) * 1e3)
     lock = threading.Lock()
     state = {"next": 0, "done": 0}
     t0 = time.perf_counter()
@@ -176,8 +181,39 @@ def cpu_baseline(streams, threads, budget_s=12.0):
     dt = time.perf_counter() - t0
     n = state["done"]
     return {"value": n / dt, "unit": "frames/s", "cores": max(1, threads), "kind": "port",
+            "single_call_ms": round(sorted(lat)[1], 2),
             "sample": f"{n} transcodes of the {len(streams)} distinct benchmark streams (round-robin, "
                       f"~{budget_s:.0f} s), oracle decode+JPEG, {max(1, threads)} threads"}
+
+
+def single_call_latency(streams, calls=9):
+    """configs[0]: one still per call through the in-memory IDecoder entry point
+    (h2j_h265_to_jpeg_mem, the same process-wide engine IDecoder::H265ToJpeg uses, minus the
+    file I/O).  Median wall ms per call after two warm-up calls; a lone call gets the whole
+    host pool for its slices / WPP rows / tiles."""
+    import h2j
+    lib = h2j.load_library()
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    lib.h2j_h265_to_jpeg_mem.restype = ctypes.c_int
+    lib.h2j_h265_to_jpeg_mem.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+    lib.h2j_free.argtypes = [ctypes.c_void_p]
+    res = {}
+    for name, s in streams:
+        buf = (ctypes.c_uint8 * len(s)).from_buffer_copy(s)
+        ms = []
+        for i in range(calls + 2):
+            jp = u8p()
+            jl = ctypes.c_size_t()
+            t = time.perf_counter()
+            rc = lib.h2j_h265_to_jpeg_mem(buf, len(s), ctypes.byref(jp), ctypes.byref(jl))
+            dt = (time.perf_counter() - t) * 1e3
+            if rc != 0:
+                raise RuntimeError(f"h2j_h265_to_jpeg_mem failed rc={rc} on {name}")
+            lib.h2j_free(jp)
+            if i >= 2:
+                ms.append(dt)
+        res[name] = round(sorted(ms)[len(ms) // 2], 2)
+    return res
 
 
 def main():
@@ -311,6 +347,10 @@ def main():
             "host_cpu_busy_cores": round(host_cores, 2),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
+        # configs[0]-style single calls: the reference fixture and one stream of this workload
+        with open(os.path.join(ROOT, "tests", "golden", "img01.h265"), "rb") as fx:
+            fixture = fx.read()
+        res["single_call_ms"] = single_call_latency([("img01.h265", fixture), ("workload_stream0", streams[0])])
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(streams, args.threads)
         print(json.dumps(res), flush=True)
