@@ -1522,6 +1522,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     const int Q = CS == 64 ? 32 : CS;            // luma quadrant size
     const int Qc = Q >> shc;
     const int nqs = CS / Q;                      // quadrants per side (2 or 1)
+    const int nq = nqs * nqs;                    // quadrants per CTB (units of the row progress words)
     const int Wc = u.width >> shc, Hc = u.height >> shc;
     const int ncomp = grp ? 2 : 1;
     PROF_DECL;
@@ -1579,10 +1580,13 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                 if (!q_inside(row, cx, q)) continue;
                 const int qx = q & 1, qy = q >> 1;
                 const int X0 = CX0 + qx * Qc, Y0 = CY0 + qy * Qc;
-                // top quadrants need the row above: TL up to this CTB, TR up to the next one
+                // top quadrants need the row above (progress counts its quadrants, nq per CTB):
+                // the left one up to this CTB, the right one also the next CTB's bottom-left
+                // quadrant (whose top line is the right one's above-right reference)
                 if (row > 0 && qy == 0) {
-                    const uint32_t need = (static_cast<uint32_t>(row) << 16) |
-                                          static_cast<uint32_t>(min(cx + 1 + (qx == nqs - 1 ? 1 : 0), u.ctb_w));
+                    int cnt = nq * (cx + 1);
+                    if (qx == nqs - 1 && cx + 1 < u.ctb_w) cnt += nqs == 2 ? 3 : 1;
+                    const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(cnt);
                     if (seen < need) {
                         while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
                             __builtin_amdgcn_s_sleep(1);
@@ -1719,11 +1723,17 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                 wave_sync();
                 cur ^= 1;
                 PROF_LAP(3);
+                if (nqs == 2 && q == 2 && below) {  // bottom-left quadrant: its bottom line is in `line`
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0)
+                        __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(nq * cx + 3),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
             PROF_ADD(6, 1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0)
-                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(cx + 1),
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(nq * (cx + 1)),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
