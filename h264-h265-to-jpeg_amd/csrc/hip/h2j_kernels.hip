@@ -417,6 +417,17 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
 
 // H.264 scaling (8.5.9, 8.5.10-8.5.12 DC transforms) + 4x4 / 8x8 inverse
 // transforms (8.5.12.2, 8.5.13) of one record into R.
+// 8-point H.264 inverse transform butterfly (8.5.13.2), one row or column
+DEVI void h264_idct8_1d(const int (&d)[8], int (&o)[8]) {
+    const int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
+    const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    const int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
+    const int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
+    const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
+    o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+}
+
 DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
                         int16_t* R, int rst, K0Lds& s) {
     const int lane = threadIdx.x;
@@ -474,13 +485,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
             if (lane < 8) {
                 int d[8], o[8];
                 for (int k = 0; k < 8; k++) d[k] = pass == 0 ? s.blk[lane * 8 + k] : s.tmp[k * 8 + lane];
-                const int a0 = d[0] + d[4], a4 = d[0] - d[4], a2 = (d[2] >> 1) - d[6], a6 = d[2] + (d[6] >> 1);
-                const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
-                const int a1 = -d[3] + d[5] - d[7] - (d[7] >> 1), a3 = d[1] + d[7] - d[3] - (d[3] >> 1);
-                const int a5 = -d[1] + d[7] + d[5] + (d[5] >> 1), a7 = d[3] + d[5] + d[1] + (d[1] >> 1);
-                const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
-                o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
-                o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+                h264_idct8_1d(d, o);
                 if (pass == 0) for (int k = 0; k < 8; k++) s.tmp[lane * 8 + k] = o[k];
                 else for (int k = 0; k < 8; k++) s.blk[k * 8 + lane] = (o[k] + 32) >> 6;
             }
@@ -516,6 +521,99 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
         }
     }
     for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    wave_sync();
+}
+
+// H.264 luma 4x4 / 8x8 residuals without a DC transform (I4x4, I8x8 TBs), 64 / N TBs per pass
+// like hevc_residual_group: lane = (TB, row) dequantises its row and runs the row butterfly in
+// registers, then lane = (TB, column) the column butterfly; one packed store per row.  Same
+// arithmetic as h264_residual (8.5.12, 8.5.13): int intermediates, (x + 32) >> 6 at the end.
+template <int LOG2N>
+DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
+                              const uint8_t* sl, int16_t* res, int st0, K0Lds& s) {
+    constexpr int N = 1 << LOG2N, NN = N * N, GMAX = 64 / N;
+    const int lane = threadIdx.x;
+    int* blk = s.blk;  // [G][N][N] levels, then the final residual
+    int* tmp = s.tmp;  // [G][N][N] after the row pass
+    for (int i = lane; i < G * NN; i += 64) blk[i] = 0;
+    // coefficient entries of all TBs of the group first (independent loads), then the scatter
+    uint32_t en[GMAX];
+    int ncf[GMAX];
+    {
+        uint64_t mm = gm;
+#pragma unroll
+        for (int g = 0; g < GMAX; g++) {
+            en[g] = 0;
+            ncf[g] = 0;
+            if (g < G) {
+                const int kg = __ffsll(static_cast<long long>(mm)) - 1;
+                mm &= mm - 1;
+                const h2j_tu tu = tu_from_lanes(rec, kg);
+                ncf[g] = tu.ncoef;
+                if (lane < tu.ncoef) en[g] = CO[tu.coef + lane];
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int g = 0; g < GMAX; g++)
+        if (lane < ncf[g]) blk[g * NN + static_cast<int>(en[g] >> 16)] = static_cast<int16_t>(en[g] & 0xFFFF);
+    wave_sync();
+    const int g = lane >> LOG2N, q = lane & (N - 1);
+    const bool act = g < G;
+    uint64_t ml = gm;
+    for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+    const int k = __ffsll(static_cast<long long>(ml)) - 1;
+    const uint32_t w0 = __shfl(rec.x, k, 64), w1 = __shfl(rec.y, k, 64), w2 = __shfl(rec.z, k, 64);
+    uint32_t wq[4] = {w0, w1, w2, 0};
+    h2j_tu mine;
+    memcpy(&mine, wq, sizeof(mine));
+    const int qp = mine.qp, qm = qp % 6;
+    if (act) {  // dequantise row q, row butterfly
+        const uint8_t* w = f.slist ? sl + f.sl + (LOG2N == 2 ? 0 : 48) : nullptr;
+        int d[N];
+#pragma unroll
+        for (int x = 0; x < N; x++) {
+            const int i = q * N + x;
+            const int lvl = blk[g * NN + i];
+            d[x] = LOG2N == 2 ? h264_scale4(lvl, (w ? w[i] : 16) * h264_norm4(qm, q, x), qp)
+                              : h264_scale8(lvl, (w ? w[i] : 16) * h264_norm8(qm, q, x), qp);
+        }
+        int o[N];
+        if constexpr (LOG2N == 2) {
+            const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+            o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
+        } else {
+            h264_idct8_1d(d, o);
+        }
+#pragma unroll
+        for (int x = 0; x < N; x++) tmp[g * NN + q * N + x] = o[x];
+    }
+    wave_sync();
+    if (act) {  // column q
+        int d[N], o[N];
+#pragma unroll
+        for (int y = 0; y < N; y++) d[y] = tmp[g * NN + y * N + q];
+        if constexpr (LOG2N == 2) {
+            const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+            o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
+        } else {
+            h264_idct8_1d(d, o);
+        }
+#pragma unroll
+        for (int y = 0; y < N; y++) blk[g * NN + y * N + q] = (o[y] + 32) >> 6;
+    }
+    wave_sync();
+    if (act) {  // row q of the residual: one packed store
+        int16_t* R = res + (mine.y + q) * st0 + mine.x;
+        uint32_t packed[N / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; i++)
+            packed[i] = (static_cast<uint32_t>(blk[g * NN + q * N + 2 * i]) & 0xFFFF) |
+                        (static_cast<uint32_t>(blk[g * NN + q * N + 2 * i + 1]) << 16);
+        if constexpr (N == 4) *reinterpret_cast<uint2*>(R) = make_uint2(packed[0], packed[1]);
+        else *reinterpret_cast<uint4*>(R) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    }
     wave_sync();
 }
 
@@ -682,7 +780,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     // ---- records with per-record work, one after another: PCM samples, H.264 residuals, HEVC
     // transform-skip / bypass residuals (regular HEVC transforms run batched below).  H.264:
     // the next such record's coefficients prefetched one record ahead.
-    uint64_t work = __ballot(mine && ((own.flags & H2J_TU_PCM) ||
+    // H.264 luma 4x4 / 8x8 (no DC transform) run batched below, like the regular HEVC transforms
+    const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+                        own.log2n <= 3;
+    uint64_t work = __ballot(mine && !grp264 && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
     uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
     while (work) {
@@ -718,6 +819,24 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         int16_t* R = res + offc;
         if (hevc) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
         else h264_residual(f, tu, CO, co0, sl, R, stc, s);
+    }
+    if (!hevc) {  // H.264 luma 4x4 / 8x8 residuals, 16 / 8 same-size TBs per pass
+#pragma unroll
+        for (int l2 = 2; l2 <= 3; l2++) {
+            uint64_t m = __ballot(grp264 && own.log2n == l2);
+            const int G = 64 >> l2;
+            while (m) {
+                uint64_t gm = 0;
+                int cnt = 0;
+                while (m && cnt < G) {
+                    gm |= m & (0 - m);
+                    m &= m - 1;
+                    cnt++;
+                }
+                if (l2 == 2) h264_residual_group<2>(f, rec, gm, cnt, CO, sl, res, st0, s);
+                else h264_residual_group<3>(f, rec, gm, cnt, CO, sl, res, st0, s);
+            }
+        }
     }
     if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
         const bool batch = lane < nrec && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS));
