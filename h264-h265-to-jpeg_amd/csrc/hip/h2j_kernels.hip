@@ -617,6 +617,88 @@ DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     wave_sync();
 }
 
+// H.264 chroma 8x8 residuals (4:2:0: 2x2 DC Hadamard + four 4x4 blocks), four TBs per pass:
+// lane = (TB g, block b, row / column k).  Same arithmetic as the chroma branch of
+// h264_residual (8.5.11: DC ((f * LevelScale4x4(0,0)) << (qP / 6)) >> 5; 8.5.12 AC scaling).
+DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
+                            const uint8_t* sl, int16_t* res, int st1, int off1, int off2, K0Lds& s) {
+    const int lane = threadIdx.x;
+    int* blk = s.blk;  // [G][8][8] levels, then the final residual
+    int* tmp = s.tmp;  // [G][8][8] after the row pass
+    for (int i = lane; i < G * 64; i += 64) blk[i] = 0;
+    uint32_t en[4];
+    int ncf[4];
+    {
+        uint64_t mm = gm;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            en[g] = 0;
+            ncf[g] = 0;
+            if (g < G) {
+                const int kg = __ffsll(static_cast<long long>(mm)) - 1;
+                mm &= mm - 1;
+                const h2j_tu tu = tu_from_lanes(rec, kg);
+                ncf[g] = tu.ncoef;
+                if (lane < tu.ncoef) en[g] = CO[tu.coef + lane];
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int g = 0; g < 4; g++)
+        if (lane < ncf[g]) blk[g * 64 + static_cast<int>(en[g] >> 16)] = static_cast<int16_t>(en[g] & 0xFFFF);
+    wave_sync();
+    const int g = lane >> 4, b = (lane >> 2) & 3, k = lane & 3;
+    const bool act = g < G;
+    uint64_t ml = gm;
+    for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+    const int kr = __ffsll(static_cast<long long>(ml)) - 1;
+    const uint32_t w0 = __shfl(rec.x, kr, 64), w1 = __shfl(rec.y, kr, 64), w2 = __shfl(rec.z, kr, 64);
+    uint32_t wq[4] = {w0, w1, w2, 0};
+    h2j_tu mine;
+    memcpy(&mine, wq, sizeof(mine));
+    const int qp = mine.qp, qm = qp % 6;
+    const uint8_t* w4 = f.slist ? sl + f.sl + mine.c * 16 : nullptr;
+    int* B = blk + g * 64;
+    const int bx = (b & 1) * 4, by = (b >> 1) * 4;
+    if (act && (lane & 15) < 4) {  // 2x2 DC Hadamard: output (r, q) = lane & 3
+        const int r = (lane >> 1) & 1, q = lane & 1;
+        const int a = B[0], bb = B[4], c = B[32], d = B[36];
+        const int acc = a + (q ? -bb : bb) + (r ? -c : c) + ((r ^ q) ? -d : d);
+        const int ls0 = (w4 ? w4[0] : 16) * kNorm4[qm][0];
+        s.dc[g * 4 + (lane & 3)] = ((acc * ls0) << (qp / 6)) >> 5;
+    }
+    wave_sync();
+    if (act) {  // row k of block b: AC scaling (DC from the Hadamard), row butterfly
+        int d[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const int i = (by + k) * 8 + bx + x;
+            d[x] = (k == 0 && x == 0) ? s.dc[g * 4 + b]
+                                      : h264_scale4(B[i], (w4 ? w4[k * 4 + x] : 16) * h264_norm4(qm, k, x), qp);
+        }
+        const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+        int* o = tmp + g * 64 + (by + k) * 8 + bx;
+        o[0] = e0 + e3; o[1] = e1 + e2; o[2] = e1 - e2; o[3] = e0 - e3;
+    }
+    wave_sync();
+    if (act) {  // column k of block b
+        const int* t = tmp + g * 64 + by * 8 + bx + k;
+        const int d0 = t[0], d1 = t[8], d2 = t[16], d3 = t[24];
+        const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+        int* o = B + by * 8 + bx + k;
+        o[0] = (e0 + e3 + 32) >> 6; o[8] = (e1 + e2 + 32) >> 6; o[16] = (e1 - e2 + 32) >> 6; o[24] = (e0 - e3 + 32) >> 6;
+    }
+    wave_sync();
+    if (act) {  // row k of block b of the residual: 4 samples, one 8-byte store
+        const int* v = B + (by + k) * 8 + bx;
+        int16_t* R = res + (mine.c == 1 ? off1 : off2) + (mine.y + by + k) * st1 + mine.x + bx;
+        *reinterpret_cast<uint2*>(R) = make_uint2((static_cast<uint32_t>(v[0]) & 0xFFFF) | (static_cast<uint32_t>(v[1]) << 16),
+                                                  (static_cast<uint32_t>(v[2]) & 0xFFFF) | (static_cast<uint32_t>(v[3]) << 16));
+    }
+    wave_sync();
+}
+
 // position of a 4x4 block inside its CTB in z-scan order (6.5.2)
 DEVI int zorder4(int ax, int ay) {
     int z = 0;
@@ -783,7 +865,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     // H.264 luma 4x4 / 8x8 (no DC transform) run batched below, like the regular HEVC transforms
     const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
                         own.log2n <= 3;
-    uint64_t work = __ballot(mine && !grp264 && ((own.flags & H2J_TU_PCM) ||
+    // ... and the chroma 8x8 TBs, four per pass
+    const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
+                         own.log2n == 3;
+    uint64_t work = __ballot(mine && !grp264 && !grp264c && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
     uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
     while (work) {
@@ -836,6 +921,17 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                 if (l2 == 2) h264_residual_group<2>(f, rec, gm, cnt, CO, sl, res, st0, s);
                 else h264_residual_group<3>(f, rec, gm, cnt, CO, sl, res, st0, s);
             }
+        }
+        uint64_t m = __ballot(grp264c);
+        while (m) {
+            uint64_t gm = 0;
+            int cnt = 0;
+            while (m && cnt < 4) {
+                gm |= m & (0 - m);
+                m &= m - 1;
+                cnt++;
+            }
+            h264_chroma_group(f, rec, gm, cnt, CO, sl, res, st1, off1, off2, s);
         }
     }
     if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
