@@ -699,6 +699,83 @@ DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, 
     wave_sync();
 }
 
+// H.264 Intra16x16 luma residuals (4x4 DC Hadamard + sixteen 4x4 blocks), four TBs per pass:
+// lane = (TB g, 4x4 block), the block's scaling and both butterfly passes in registers (no LDS
+// round trip between the passes).  Same arithmetic as the i16 branch of h264_residual (8.5.10,
+// 8.5.12).
+DEVI void h264_i16_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
+                         const uint8_t* sl, int16_t* res, int st0, K0Lds& s) {
+    const int lane = threadIdx.x;
+    int* blk = s.blk;  // [G][16][16] levels
+    for (int i = lane; i < G * 256; i += 64) blk[i] = 0;
+    wave_sync();
+    {
+        uint64_t mm = gm;
+        for (int g = 0; g < G; g++) {
+            const int kg = __ffsll(static_cast<long long>(mm)) - 1;
+            mm &= mm - 1;
+            const h2j_tu tu = tu_from_lanes(rec, kg);
+            uint32_t en[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) en[j] = lane + 64 * j < tu.ncoef ? CO[tu.coef + lane + 64 * j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (lane + 64 * j < tu.ncoef) blk[g * 256 + static_cast<int>(en[j] >> 16)] = static_cast<int16_t>(en[j] & 0xFFFF);
+        }
+    }
+    wave_sync();
+    const int g = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+    if (g < G) {
+        uint64_t ml = gm;
+        for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+        const int kr = __ffsll(static_cast<long long>(ml)) - 1;
+        const uint32_t w0 = __shfl(rec.x, kr, 64), w1 = __shfl(rec.y, kr, 64), w2 = __shfl(rec.z, kr, 64);
+        uint32_t wq[4] = {w0, w1, w2, 0};
+        h2j_tu mine;
+        memcpy(&mine, wq, sizeof(mine));
+        const int qp = mine.qp, qm = qp % 6;
+        const uint8_t* w4 = f.slist ? sl + f.sl : nullptr;
+        const int* B = blk + g * 256;
+        // DC Hadamard output (by, bx) = this block's DC
+        int acc = 0;
+    #pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int hr = (by == 0 || (by == 1 && i < 2) || (by == 2 && (i == 0 || i == 3)) || (by == 3 && !(i & 1))) ? 1 : -1;
+    #pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int hc = (bx == 0 || (bx == 1 && j < 2) || (bx == 2 && (j == 0 || j == 3)) || (bx == 3 && !(j & 1))) ? 1 : -1;
+                acc += hr * hc * B[(i * 4) * 16 + j * 4];
+            }
+        }
+        const int ls0 = (w4 ? w4[0] : 16) * kNorm4[qm][0];
+        const int dcv = qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+        int v[4][4];
+    #pragma unroll
+        for (int r = 0; r < 4; r++)
+    #pragma unroll
+            for (int x = 0; x < 4; x++)
+                v[r][x] = (r == 0 && x == 0) ? dcv
+                                             : h264_scale4(B[(by * 4 + r) * 16 + bx * 4 + x],
+                                                           (w4 ? w4[r * 4 + x] : 16) * h264_norm4(qm, r, x), qp);
+    #pragma unroll
+        for (int r = 0; r < 4; r++) {  // rows
+            const int e0 = v[r][0] + v[r][2], e1 = v[r][0] - v[r][2], e2 = (v[r][1] >> 1) - v[r][3], e3 = v[r][1] + (v[r][3] >> 1);
+            v[r][0] = e0 + e3; v[r][1] = e1 + e2; v[r][2] = e1 - e2; v[r][3] = e0 - e3;
+        }
+    #pragma unroll
+        for (int x = 0; x < 4; x++) {  // columns
+            const int e0 = v[0][x] + v[2][x], e1 = v[0][x] - v[2][x], e2 = (v[1][x] >> 1) - v[3][x], e3 = v[1][x] + (v[3][x] >> 1);
+            v[0][x] = (e0 + e3 + 32) >> 6; v[1][x] = (e1 + e2 + 32) >> 6; v[2][x] = (e1 - e2 + 32) >> 6; v[3][x] = (e0 - e3 + 32) >> 6;
+        }
+        int16_t* R = res + (mine.y + by * 4) * st0 + mine.x + bx * 4;
+    #pragma unroll
+        for (int r = 0; r < 4; r++)
+            *reinterpret_cast<uint2*>(R + r * st0) = make_uint2((static_cast<uint32_t>(v[r][0]) & 0xFFFF) | (static_cast<uint32_t>(v[r][1]) << 16),
+                                                                (static_cast<uint32_t>(v[r][2]) & 0xFFFF) | (static_cast<uint32_t>(v[r][3]) << 16));
+    }  // g < G
+    wave_sync();
+}
+
 // position of a 4x4 block inside its CTB in z-scan order (6.5.2)
 DEVI int zorder4(int ax, int ay) {
     int z = 0;
@@ -868,7 +945,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     // ... and the chroma 8x8 TBs, four per pass
     const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
                          own.log2n == 3;
-    uint64_t work = __ballot(mine && !grp264 && !grp264c && ((own.flags & H2J_TU_PCM) ||
+    // ... and the Intra16x16 luma TBs, four per pass
+    const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+                         own.log2n == 4;
+    uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
     uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
     while (work) {
@@ -932,6 +1012,17 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                 cnt++;
             }
             h264_chroma_group(f, rec, gm, cnt, CO, sl, res, st1, off1, off2, s);
+        }
+        m = __ballot(grp264i);
+        while (m) {
+            uint64_t gm = 0;
+            int cnt = 0;
+            while (m && cnt < 4) {
+                gm |= m & (0 - m);
+                m &= m - 1;
+                cnt++;
+            }
+            h264_i16_group(f, rec, gm, cnt, CO, sl, res, st0, s);
         }
     }
     if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
