@@ -228,6 +228,8 @@ def main():
                     help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]/[4]")
     ap.add_argument("--streams", default=None, help="override the workload's stream glob")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-call", action="store_true",
+                    help="skip the configs[0] single-call latencies (profiling runs: no extra 1-picture launches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -348,9 +350,10 @@ def main():
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
         # configs[0]-style single calls: the reference fixture and one stream of this workload
-        with open(os.path.join(ROOT, "tests", "golden", "img01.h265"), "rb") as fx:
-            fixture = fx.read()
-        res["single_call_ms"] = single_call_latency([("img01.h265", fixture), ("workload_stream0", streams[0])])
+        if not args.no_single_call:
+            with open(os.path.join(ROOT, "tests", "golden", "img01.h265"), "rb") as fx:
+                fixture = fx.read()
+            res["single_call_ms"] = single_call_latency([("img01.h265", fixture), ("workload_stream0", streams[0])])
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(streams, args.threads)
         print(json.dumps(res), flush=True)
