@@ -192,7 +192,13 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // availability mask, the CTB -> TU range, the HEVC deblocking maps, PCM
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
-constexpr int kK0Tus = 16;      // H.264 TUs per K0 wave (records held one per lane)
+#ifndef H2J_K0TUS  // (experiment builds: -DH2J_K0TUS=62)
+#define H2J_K0TUS 62
+#endif
+#ifndef H2J_K0G  // experiment builds: bit 0 luma 4x4/8x8, bit 1 chroma, bit 2 I16x16 groups on
+#define H2J_K0G 7
+#endif
+constexpr int kK0Tus = H2J_K0TUS;  // H.264 TUs per K0 wave (records held one per lane)
 constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
 // HEVC K1: launches of > 128 pictures run one 16-wave workgroup per picture split unevenly: the Cb/Cr chain processes each Cb/Cr TB
 // pair in one pass (about 2/3 of a luma row's time), so 9 luma + 7 chroma waves finish a 17-row
@@ -725,11 +731,13 @@ DEVI void h264_i16_group(const K0F& f, const uint4& rec, uint64_t gm, int G, con
     }
     wave_sync();
     const int g = lane >> 4, b = lane & 15, bx = b & 3, by = b >> 2;
+    // this lane's record, fetched with every lane active (ds_bpermute reads nothing from an
+    // inactive source lane, and the record may sit in any of the wave's lanes)
+    uint64_t ml = gm;
+    for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+    const int kr = __ffsll(static_cast<long long>(ml)) - 1;
+    const uint32_t w0 = __shfl(rec.x, kr, 64), w1 = __shfl(rec.y, kr, 64), w2 = __shfl(rec.z, kr, 64);
     if (g < G) {
-        uint64_t ml = gm;
-        for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
-        const int kr = __ffsll(static_cast<long long>(ml)) - 1;
-        const uint32_t w0 = __shfl(rec.x, kr, 64), w1 = __shfl(rec.y, kr, 64), w2 = __shfl(rec.z, kr, 64);
         uint32_t wq[4] = {w0, w1, w2, 0};
         h2j_tu mine;
         memcpy(&mine, wq, sizeof(mine));
@@ -940,13 +948,13 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     // transform-skip / bypass residuals (regular HEVC transforms run batched below).  H.264:
     // the next such record's coefficients prefetched one record ahead.
     // H.264 luma 4x4 / 8x8 (no DC transform) run batched below, like the regular HEVC transforms
-    const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+    const bool grp264 = (H2J_K0G & 1) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
                         own.log2n <= 3;
     // ... and the chroma 8x8 TBs, four per pass
-    const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
+    const bool grp264c = (H2J_K0G & 2) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
                          own.log2n == 3;
     // ... and the Intra16x16 luma TBs, four per pass
-    const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+    const bool grp264i = (H2J_K0G & 4) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
                          own.log2n == 4;
     uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
