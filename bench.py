@@ -41,6 +41,10 @@ WORKLOADS = {
     "hevc2160": dict(streams="tests/golden/bench4k/hevc2160_10b_*.h265", w=3840, h=2160, bps=2,
                      desc="configs[3]: 4K H.265 Main10 I-frames, 10-bit decode -> 8-bit JPEG per GPU",
                      data="4 hevcgen 2160p HEVC Main10 I-frame streams (tests/golden/bench4k)"),
+    "hevc1080_heavy": dict(streams="tests/golden/bench_heavy/hevc1080h_*.h265", w=1920, h=1080, bps=1,
+                           desc="configs[1] on heavier streams (~100-250 KB per picture, SURVEY.md §8(d) aim): "
+                                "batch of 1024 x 1080p H.265 Main 8-bit I-frames -> JPEG per GPU",
+                           data="16 hevcgen 1080p HEVC Main I-frame streams, QP 18-24, noise sigma 0-2 (tests/golden/bench_heavy)"),
     "mixed": dict(streams=None, w=None, h=None, bps=None,
                   desc="configs[4]: mixed 720p/1080p/4K (40/40/20 by count) x H.264/H.265 (50/50) stills, "
                        "LPT-sharded over the GPUs (frames = per-GPU share of the global list)",
@@ -76,7 +80,7 @@ def mixed_list(total):
         cls = "720" if g % 10 < 4 else ("1080" if g % 10 < 8 else "2160")
         codec = 265 if (g // 10) % 2 == 0 else 264
         streams, w, h, bps = sets[(cls, codec)]
-        items.append((streams[(g // 20) % len(streams)], alg_bytes(w, h, bps), w * h))
+        items.append((streams[(g // 20) % len(streams)], alg_bytes(w, h, bps), w * h, bps))
     return items
 
 
@@ -127,23 +131,31 @@ def shard_lpt(costs, world):
     return [sorted(p) for p in parts]
 
 
-def host_cpu_share(local_rank, local_world, requested=0, cap=16):
-    """Host entropy threads for this rank: its slice of the CPUs the job may use
-    (sched_getaffinity, not os.cpu_count, which reports the whole machine), at
-    most `cap`.  With several ranks per node each rank is pinned to a disjoint
-    slice so the ranks' parse pools do not fight over the same cores."""
-    try:
-        cpus = sorted(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        cpus = list(range(os.cpu_count() or 1))
-    per = max(1, len(cpus) // max(1, local_world))
-    if local_world > 1 and len(cpus) >= local_world:
-        mine = cpus[local_rank * per:(local_rank + 1) * per]
-        try:
-            os.sched_setaffinity(0, mine)
-        except (AttributeError, OSError):
-            pass
-    return requested if requested > 0 else max(1, min(cap, per))
+def rank_batch(workload, frames, world, rank):
+    """This rank's share of the job: (indices into the global list, global list).
+
+    Uniform workloads: every rank transcodes its own `frames`-picture batch (weak scaling).
+    configs[4] (mixed): the global list of frames * world stills (65,536 at --frames 8192 on
+    8 GPUs) is LPT-sharded by estimated cost (bitstream bytes for the host CABAC/CAVLC +
+    pixels for the GPU), so the shards are disjoint, complete and balanced."""
+    if workload != "mixed":
+        return list(range(frames)), None
+    items = mixed_list(frames * world)
+    return shard_lpt([len(b) + 0.02 * px for b, _, px, _ in items], world)[rank], items
+
+
+# The reference's own CPU path (FFmpeg git-2021-01-28-6fd0116 through IDecoder), measured in the
+# survey container (8 vCPU Xeon, BASELINE.md) -- a different machine from the GPU box, where the
+# reference's prebuilt FFmpeg libraries may not run; reported beside the oracle port, labelled.
+REFERENCE_CONTAINER = {
+    "where": "survey container, 8 vCPU Intel Xeon (BASELINE.md) -- not this box",
+    "h264_1080p_img01_ms_per_img_1core": 51.1,
+    "h264_1080p_img01_no_probe_ms_1core": 31.4,
+    "h264_1080p_img01_img_per_s_8proc": 66.8,
+    "hevc_1440p_img01_ms_per_img_1core": 127.3,
+    "hevc_1440p_img01_no_probe_ms_1core": 69.3,
+    "hevc_1440p_img01_img_per_s_8proc": 55.5,
+}
 
 
 def cpu_baseline(streams, threads, budget_s=12.0):
@@ -182,6 +194,7 @@ def cpu_baseline(streams, threads, budget_s=12.0):
     n = state["done"]
     return {"value": n / dt, "unit": "frames/s", "cores": max(1, threads), "kind": "port",
             "single_call_ms": round(sorted(lat)[1], 2),
+            "reference_container": REFERENCE_CONTAINER,
             "sample": f"{n} transcodes of the {len(streams)} distinct benchmark streams (round-robin, "
                       f"~{budget_s:.0f} s), oracle decode+JPEG, {max(1, threads)} threads"}
 
@@ -223,7 +236,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=1024, help="frames per GPU per step")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host entropy/Huffman threads per GPU (default: this rank's share of the CPUs, at most 16)")
+                    help="host entropy/Huffman threads per GPU (default: the engine's NUMA-local share, "
+                         "include/h2j.h h2j_engine_create)")
     ap.add_argument("--workload", default="hevc1080", choices=sorted(WORKLOADS),
                     help="hevc1080 = the BASELINE metric's config; the others are configs[2]/[3]/[4]")
     ap.add_argument("--streams", default=None, help="override the workload's stream glob")
@@ -248,20 +262,22 @@ def main():
     import h2j
     wl = WORKLOADS[args.workload]
     n = args.frames
+    mine, items = rank_batch(args.workload, n, world, rank)
     if args.workload == "mixed":
-        items = mixed_list(n * world)
-        # cost model for the LPT shard: bitstream bytes (host CABAC/CAVLC) + pixels (GPU)
-        mine = shard_lpt([len(b) + 0.02 * px for b, _, px in items], world)[rank]
         batch = [items[i][0] for i in mine]
         frame_bytes = [items[i][1] for i in mine]
+        frame_bps = [items[i][3] for i in mine]
         streams = sorted({id(b): b for b in batch}.values(), key=len)
         n = len(batch)
     else:
         streams = load_streams(args.streams or wl["streams"])
         batch = [streams[i % len(streams)] for i in range(n)]
         frame_bytes = [alg_bytes_per_frame(wl)] * n
-    args.threads = host_cpu_share(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))), args.threads)
+        frame_bps = [wl["bps"]] * n
+    # host pool: the engine places it (NUMA node of this rank's GPU, its slice of that node's
+    # CPUs among the node's GPUs, bounded by the cgroup quota; pinned) unless --threads is given
     eng = h2j.Engine(local, args.threads)
+    host = eng.host_info()
 
     # pre-built ctypes arguments: nothing but the C call inside the timed region
     bufs = [(ctypes.c_uint8 * len(s)).from_buffer_copy(s) for s in batch]
@@ -290,6 +306,7 @@ def main():
         step()
     barrier()
     stage_sum = {}
+    chunks_all = []
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -297,6 +314,7 @@ def main():
         st = eng.stats()
         for k, v in st.items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
+        chunks_all += eng.chunk_times()
     t1 = time.perf_counter()
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     barrier()
@@ -316,6 +334,22 @@ def main():
         achieved = alg_bytes_launch / (k1_ms / 1e3) / 1e9
         kern_ms = (per["prep_ms"] + per["recon_ms"] + per["deblock_ms"] + per["sao_ms"] + per["jpeg_ms"]
                    + per["entropy_ms"])
+        # K1's own algorithmic traffic: the int16 residual it reads (2S) + the picture it writes (b*S)
+        k1_own_launch = sum(fb // (4 + bps) * (2 + bps) for fb, bps in zip(frame_bytes, frame_bps)) / chunks
+        frac_k1_own = k1_own_launch / (k1_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+        # BASELINE.md GPU metric: frames * B / t_kernels (K0..K5)
+        frac_pipeline = sum(frame_bytes) / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+        # per launch size: the full (256-picture) chunks and the tail chunks separately
+        variants = {}
+        fb_mean = sum(frame_bytes) / n
+        for frames_c, k1c, _ in chunks_all:
+            v = variants.setdefault(str(frames_c), {"launches": 0, "k1_ms": 0.0})
+            v["launches"] += 1
+            v["k1_ms"] += k1c
+        for key, v in variants.items():
+            v["avg_k1_ms"] = round(v.pop("k1_ms") / v["launches"], 4)
+            v["achieved"] = round(int(key) * fb_mean / (v["avg_k1_ms"] / 1e3) / 1e9, 1)
+            v["frac"] = round(v["achieved"] / HBM_PEAK_GBPS, 4)
         gpu_ms = kern_ms + per["h2d_ms"] + per["d2h_ms"]
         k1_name = {"avc1080": "h2j_k1_recon_h264", "mixed": "h2j_k1_recon_hevc+h2j_k1_recon_h264"}.get(
             args.workload, "h2j_k1_recon_hevc")
@@ -334,12 +368,19 @@ def main():
             "dtype": "u8",
             "data": f"synthetic: {wl['data']} tiled to the batch",
             "config": {"workload": wl["desc"], "workload_key": args.workload,
-                       "frames_per_gpu": n, "global_batch": n * world, "host_threads_per_gpu": args.threads,
+                       "frames_per_gpu": n, "global_batch": n * world, "host_threads_per_gpu": host["threads"],
+                       "host_numa_node": host["numa_node"], "host_pinned_cpus": host["pinned_cpus"],
                        "parallelism": f"independent replicas x{world}"},
             "roofline": {"bound": "hbm", "kernel": k1_name, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes_launch, "frames_per_launch": frames_per_launch,
-                         "avg_launch_ms": k1_ms},
+                         "avg_launch_ms": k1_ms,
+                         "frac_def": "whole-pipeline algorithmic bytes B=(4+b)S of the launch's pictures / K1 time",
+                         "frac_k1_own": frac_k1_own,
+                         "frac_k1_own_def": "K1's own bytes (2S residual in + b*S picture out) / K1 time",
+                         "frac_pipeline": frac_pipeline,
+                         "frac_pipeline_def": "BASELINE.md: frames*B / t_kernels(K0..K5)",
+                         "per_launch_size": variants},
             # value is end to end: host CABAC/CAVLC (north_star keeps entropy decoding on host
             # threads) + PCIe + K0-K5 + container.  With the job records already in HBM the
             # GPU kernels alone sustain hbm_resident_fps; gpu_pipeline_fps adds the PCIe copies.
@@ -347,6 +388,9 @@ def main():
             "hbm_resident_fps": n / (kern_ms / 1e3),
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
             "host_cpu_busy_cores": round(host_cores, 2),
+            "bitstream_kb_per_frame": round(sum(len(b) for b in batch) / n / 1024, 1),
+            "parse_us_per_kb_wall": round(per["parse_ms"] * 1e3 / (sum(len(b) for b in batch) / 1024), 3),
+            "parse_core_us_per_kb": round(per["parse_ms"] * 1e3 * host["threads"] / (sum(len(b) for b in batch) / 1024), 2),
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
         # configs[0]-style single calls: the reference fixture and one stream of this workload
@@ -355,7 +399,7 @@ def main():
                 fixture = fx.read()
             res["single_call_ms"] = single_call_latency([("img01.h265", fixture), ("workload_stream0", streams[0])])
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(streams, args.threads)
+            res["cpu_baseline"] = cpu_baseline(streams, host["threads"])
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()

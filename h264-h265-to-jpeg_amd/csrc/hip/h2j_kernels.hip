@@ -1,27 +1,29 @@
-// MI355X (gfx950, CDNA4, wave64) pixel pipeline for the H.264/H.265 still ->
-// JPEG hot path.  Hand-written HIP; integer work only (no MFMA: small fixed
-// transforms and filters, HBM/latency bound).
+// MI355X (gfx950, CDNA4, wave64) pixel pipeline for the H.264/H.265 still -> JPEG hot path.
+// Hand-written HIP; integer work only (no MFMA: 4-32-point fixed transforms and filters,
+// latency / HBM bound).  Stages, one launch each per chunk of pictures:
 //
-//   K1 h2j_k1_recon    — per picture, one wave walks the transform blocks in
-//                        decoding order: reference-sample gather with z-scan
-//                        availability + substitution (ballot/scan), [1 2 1]
-//                        / strong smoothing, planar/DC/angular prediction,
-//                        dequantisation, column/row inverse transform in LDS
-//                        with zero-bounding-box pruning, clip+store.
-//                        (H.265 8.4.4.2, 8.6.2-8.6.4; H.264 8.3, 8.5)
-//   K2 h2j_k2_deblock  — one thread per 4-line edge segment, vertical pass
-//                        then horizontal pass (H.265 8.7.2, H.264 8.7)
-//   K3 h2j_k3_sao      — one workgroup per (CTB, component), LDS tile + border,
-//                        band/edge offsets
-//                        (H.265 8.7.3)
-//   K4 h2j_k4_*        — JPEG forward path of FFmpeg's mjpeg encoder as
-//                        restated in SURVEY.md Appendix A: MB variance ->
-//                        rate control -> AP-922 FDCT -> 16-bit quantiser ->
-//                        zigzag, plus Huffman symbol histograms.
+//   K0 h2j_k0_prep<codec>   one lane per transform-block record: availability masks, CTB /
+//                           MB record ranges, deblocking maps, PCM samples; dequantisation +
+//                           inverse DCT/DST batched by TB size (lane = TB column, then row)
+//                           into the int16 residual plane (H.265 8.6.2-8.6.4, H.264 8.5)
+//   K1 h2j_k1_recon_*       intra prediction + residual add along the dependency chains:
+//                           HEVC one workgroup per picture (luma and chroma chains in
+//                           separate waves, CTB rows as a wavefront, 32x32 quadrant windows in
+//                           LDS prefetched by LDS-DMA); H.264 one workgroup per picture or
+//                           16-MB-row band, MB-row wavefront in LDS windows
+//                           (H.265 8.4.4.2, H.264 8.3)
+//   K2 h2j_k2_deblock*      HEVC: one thread per 4-line edge segment, V then H pass;
+//                           H.264: MB-row wavefront in LDS windows, banded like K1
+//                           (H.265 8.7.2, H.264 8.7)
+//   K3 h2j_k3_sao           one workgroup per (CTB, component), LDS tile + border (H.265 8.7.3)
+//   K4 h2j_k4_*             FFmpeg mjpeg forward path as restated in SURVEY.md Appendix A:
+//                           pad, MB variance -> rate control -> AP-922 FDCT -> 16-bit
+//                           quantiser -> zigzag, then per-table symbol histograms
+//   (K5, optimal Huffman tables + bitstream emission, lives in h2j_entropy.hip)
 //
 // Reference call sites replaced: /root/reference/src/Decoder.cpp:324,342
-// (avcodec_send_packet / avcodec_receive_frame) and
-// /root/reference/src/Encoder.cpp:250 (avcodec_send_frame, mjpeg).
+// (avcodec_send_packet / avcodec_receive_frame) and /root/reference/src/Encoder.cpp:250
+// (avcodec_send_frame, mjpeg).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -192,13 +194,9 @@ DEVI int h264_pred_nxn(int mode, int x, int y, int n, const int* T, const int* L
 // availability mask, the CTB -> TU range, the HEVC deblocking maps, PCM
 // samples, and the residual (dequantisation + inverse transform) into an
 // int16 plane.  K1 then only walks the serial prediction chain.
-#ifndef H2J_K0TUS  // (experiment builds: -DH2J_K0TUS=62)
-#define H2J_K0TUS 62
-#endif
-#ifndef H2J_K0G  // experiment builds: bit 0 luma 4x4/8x8, bit 1 chroma, bit 2 I16x16 groups on
-#define H2J_K0G 7
-#endif
-constexpr int kK0Tus = H2J_K0TUS;  // H.264 TUs per K0 wave (records held one per lane)
+constexpr int kK0Tus = 62;  // H.264 TUs per K0 wave (records held one per lane)
+// lanes kTus and kTus + 1 hold the neighbour records of a wave's range (h2j_k0_prep)
+static_assert(kK0Tus >= 1 && kK0Tus <= 62, "K0 records per wave: 62 at most");
 constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
 // HEVC K1: launches of > 128 pictures run one 16-wave workgroup per picture split unevenly: the Cb/Cr chain processes each Cb/Cr TB
 // pair in one pass (about 2/3 of a luma row's time), so 9 luma + 7 chroma waves finish a 17-row
@@ -948,13 +946,13 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
     // transform-skip / bypass residuals (regular HEVC transforms run batched below).  H.264:
     // the next such record's coefficients prefetched one record ahead.
     // H.264 luma 4x4 / 8x8 (no DC transform) run batched below, like the regular HEVC transforms
-    const bool grp264 = (H2J_K0G & 1) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+    const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
                         own.log2n <= 3;
     // ... and the chroma 8x8 TBs, four per pass
-    const bool grp264c = (H2J_K0G & 2) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
+    const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
                          own.log2n == 3;
     // ... and the Intra16x16 luma TBs, four per pass
-    const bool grp264i = (H2J_K0G & 4) && !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
+    const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
                          own.log2n == 4;
     uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
@@ -1650,9 +1648,6 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         }
         wave_sync();
     }
-#if defined(H2J_EXP) && H2J_EXP == 2  // timing experiment: reference samples only
-    return;
-#endif
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
     const int16_t* R = filt ? s.ref : s.sub;
     if (mode == 0) {
@@ -1990,12 +1985,8 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                                 static_cast<int16_t>(P[(tu.y + i / n) * u.st(c) + tu.x + (i % n)]);
                         wave_sync();
                     } else {
-#if defined(H2J_EXP) && H2J_EXP == 1  // timing experiment: no TB work at all
-                        (void)ox;
-#else
                         hevc_predict_tb(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top,
                                         w.cs[ci].left, w.k, lane);
-#endif
                     }
                     PROF_ADD(5, 1);
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
@@ -2066,9 +2057,6 @@ __global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame*
     int16_t* line = reinterpret_cast<int16_t*>(k1lds + k1_fixed_lds(W_));
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
-#if defined(H2J_EXP) && (H2J_EXP == 3 || H2J_EXP == 4)  // timing experiment: one chain only (3: chroma, 4: luma)
-    if (static_cast<int>(blockIdx.y) == (H2J_EXP == 3 ? 0 : 1)) return;
-#endif
     if (threadIdx.x < 2 * W_) prog[threadIdx.x] = 0;
     __syncthreads();
     hevc_rows<Pel>(f, tus + ufl(f.tu), arena, static_cast<int>(blockIdx.y), W, prog, line,
@@ -3109,6 +3097,9 @@ int h2j_gpu_device_count(void) {
     return n;
 }
 int h2j_gpu_set_device(int device) { return check(hipSetDevice(device), "hipSetDevice"); }
+int h2j_gpu_pci_bus_id(int device, char* buf, int len) {
+    return check(hipDeviceGetPCIBusId(buf, len, device), "hipDeviceGetPCIBusId");
+}
 void* h2j_gpu_malloc(size_t bytes) {
     void* p = nullptr;
     if (check(hipMalloc(&p, bytes), "hipMalloc")) return nullptr;

@@ -8,6 +8,7 @@
 // src/Encoder.cpp:29), decoder-delay streams are handled (the first picture
 // is decoded directly), 10-bit input is converted with
 // v8 = min(255, (v + 2) >> 2) instead of producing a corrupted JPEG.
+#include <algorithm>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "IDecoder.h"
@@ -40,12 +42,14 @@ void LOG(const char* format, ...) {
 
 namespace {
 
-// One engine per process (GPU 0); IDecoder instances are cheap handles.
-// Concurrent H265ToJpeg calls are batched: callers queue their bitstreams and
-// whichever caller finds the engine idle runs everything queued as one
-// h2j_engine_transcode batch (host entropy decoding fans out over the engine's
-// thread pool, the GPU sees one launch per stage), then hands every caller its
-// JPEG.  A lone caller simply runs a batch of one.
+// One engine per visible GPU (H2J_ENGINES overrides the count; engine i runs on device
+// i % device count); IDecoder instances are cheap handles.  Concurrent H265ToJpeg calls are
+// batched: callers queue their bitstreams, and whichever caller finds engines idle takes
+// everything queued, splits it over the idle engines (longest-processing-time first by
+// bitstream bytes, the host entropy cost) and runs the parts as h2j_engine_transcode batches
+// side by side (host entropy decoding fans out over each engine's thread pool, each GPU sees
+// one launch per stage), then hands every caller its JPEG.  A lone caller runs a batch of one;
+// a JVM calling through JNI from many threads keeps every GPU of the node busy.
 struct Request {
     const uint8_t* data = nullptr;
     size_t size = 0;
@@ -55,15 +59,60 @@ struct Request {
     bool done = false;
 };
 
+struct EngineSlot {
+    h2j_engine* e = nullptr;
+    bool busy = false;
+};
+
 std::mutex g_mu;
 std::condition_variable g_cv;
 std::deque<Request*> g_queue;
-bool g_busy = false;
-h2j_engine* g_engine = nullptr;
+std::vector<EngineSlot> g_engines;
+bool g_engines_init = false;
+
+// create the engines (caller holds g_mu); none when no HIP device is visible
+void init_engines_locked() {
+    if (g_engines_init) return;
+    g_engines_init = true;
+    const int ndev = h2j_device_count();
+    if (ndev <= 0) return;
+    int n = ndev;
+    if (const char* env = getenv("H2J_ENGINES")) {
+        const int v = atoi(env);
+        if (v > 0 && v <= 64) n = v;
+    }
+    for (int i = 0; i < n; i++) {
+        // split the host threads between the engines (each creates a pool of that size)
+        h2j_engine* e = h2j_engine_create(i % ndev, -n);
+        if (e) {
+            EngineSlot slot;
+            slot.e = e;
+            g_engines.push_back(slot);
+        }
+    }
+}
+
+// LPT partition of `work` into k parts by bitstream bytes (each part keeps queue order)
+std::vector<std::vector<Request*>> split_lpt(const std::vector<Request*>& work, int k) {
+    std::vector<int> idx(work.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = static_cast<int>(i);
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return work[a]->size > work[b]->size; });
+    std::vector<size_t> load(static_cast<size_t>(k), 0);
+    std::vector<int> part(work.size());
+    for (int i : idx) {
+        const int m = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+        part[i] = m;
+        load[m] += work[i]->size + 1;
+    }
+    std::vector<std::vector<Request*>> out(static_cast<size_t>(k));
+    for (size_t i = 0; i < work.size(); i++) out[part[i]].push_back(work[i]);
+    return out;
+}
 
 // run one batch (caller holds no lock); fills jpeg / status / error of each request
 void run_batch(h2j_engine* e, std::vector<Request*>& batch) {
     const int n = static_cast<int>(batch.size());
+    if (n == 0) return;
     std::vector<const uint8_t*> ptrs(n);
     std::vector<size_t> sizes(n), off(n), len(n);
     std::vector<int> status(n);
@@ -88,16 +137,28 @@ void run_batch(h2j_engine* e, std::vector<Request*>& batch) {
         Request* q = batch[i];
         q->status = status[i];
         if (r != 0 && status[i] == 0) q->status = r;
-        if (q->status == 0) q->jpeg.assign(out.begin() + static_cast<long>(off[i]),
-                                           out.begin() + static_cast<long>(off[i] + len[i]));
-        else q->error = h2j_engine_error(e);
+        if (q->status == 0) {
+            q->jpeg.assign(out.begin() + static_cast<long>(off[i]), out.begin() + static_cast<long>(off[i] + len[i]));
+        } else {
+            const char* m = status[i] != 0 ? h2j_engine_frame_error(e, i) : "";
+            q->error = (m && *m) ? m : h2j_engine_error(e);
+        }
     }
 }
 
-// transcode pictures through the shared, batching engine (all of `reqs` join the same queue,
-// so a caller's own batch runs as one engine batch together with whatever else is queued)
+// transcode pictures through the shared, batching engines (all of `reqs` join the same queue,
+// so a caller's own batch runs together with whatever else is queued)
 void transcode_shared_many(const std::vector<Request*>& reqs) {
     std::unique_lock<std::mutex> lk(g_mu);
+    init_engines_locked();
+    if (g_engines.empty()) {
+        for (Request* q : reqs) {
+            q->status = -1;
+            q->error = "no HIP device available: the MI355X pipeline cannot run";
+            q->done = true;
+        }
+        return;
+    }
     for (Request* r : reqs) g_queue.push_back(r);
     auto all_done = [&] {
         for (Request* r : reqs)
@@ -105,27 +166,27 @@ void transcode_shared_many(const std::vector<Request*>& reqs) {
         return true;
     };
     while (!all_done()) {
-        if (g_busy) {
+        std::vector<int> idle;
+        for (size_t i = 0; i < g_engines.size(); i++)
+            if (!g_engines[i].busy) idle.push_back(static_cast<int>(i));
+        if (idle.empty() || g_queue.empty()) {
             g_cv.wait(lk);
             continue;
         }
-        g_busy = true;
-        if (!g_engine) g_engine = h2j_engine_create(0, 0);
-        h2j_engine* e = g_engine;
-        std::vector<Request*> batch(g_queue.begin(), g_queue.end());
+        std::vector<Request*> work(g_queue.begin(), g_queue.end());
         g_queue.clear();
+        const int k = static_cast<int>(std::min(idle.size(), work.size()));
+        std::vector<std::vector<Request*>> parts = split_lpt(work, k);
+        for (int j = 0; j < k; j++) g_engines[idle[j]].busy = true;
         lk.unlock();
-        if (e) {
-            run_batch(e, batch);
-        } else {
-            for (Request* q : batch) {
-                q->status = -1;
-                q->error = "no HIP device available: the MI355X pipeline cannot run";
-            }
-        }
+        std::vector<std::thread> helpers;
+        for (int j = 1; j < k; j++)
+            helpers.emplace_back([&, j] { run_batch(g_engines[idle[j]].e, parts[j]); });
+        run_batch(g_engines[idle[0]].e, parts[0]);
+        for (auto& t : helpers) t.join();
         lk.lock();
-        for (Request* q : batch) q->done = true;
-        g_busy = false;
+        for (Request* q : work) q->done = true;
+        for (int j = 0; j < k; j++) g_engines[idle[j]].busy = false;
         g_cv.notify_all();
     }
 }

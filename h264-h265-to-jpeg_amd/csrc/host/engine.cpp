@@ -29,6 +29,10 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
+#include "affinity.h"
 #include "bitstream.h"
 #include "h2j.h"
 #include "h2j_gpu.h"
@@ -46,9 +50,19 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 class ThreadPool {
 public:
-    explicit ThreadPool(int n) : stop_(false), gen_(0), pending_(0) {
+    // n workers; cpus: if non-empty, every worker runs on that CPU set (NUMA-local slice)
+    explicit ThreadPool(int n, const std::vector<int>& cpus = std::vector<int>()) : stop_(false), gen_(0), pending_(0) {
         for (int i = 0; i < n; i++) workers_.emplace_back([this] { loop(); });
+        if (!cpus.empty()) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            for (int c : cpus)
+                if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+            for (auto& t : workers_)
+                if (pthread_setaffinity_np(t.native_handle(), sizeof(set), &set) == 0) pinned_ = true;
+        }
     }
+    bool pinned() const { return pinned_; }
     ~ThreadPool() {
         {
             std::lock_guard<std::mutex> g(m_);
@@ -109,6 +123,7 @@ private:
     std::mutex m_;
     std::condition_variable cv_, done_;
     std::function<void()> task_;
+    bool pinned_ = false;
     bool stop_;
     unsigned long gen_;
     int pending_;
@@ -203,8 +218,15 @@ constexpr size_t kSegBytesPerBlock = 272;
 struct Engine {
     int device = 0;
     ThreadPool* pool = nullptr;
+    HostPlan plan;  // host threads / NUMA placement of the pool
     std::string err;
     std::vector<FrameJob> jobs;
+    std::vector<int> last_status;  // per-picture status of the last transcode (h2j_engine_frame_error)
+    struct ChunkTime {
+        int frames = 0;
+        double k1_ms = 0, kernels_ms = 0;  // K1 launch; K0..K5 (HIP events on the chunk's stream)
+    };
+    std::vector<ChunkTime> chunk_log;  // chunks of the last transcode (h2j_engine_chunk_times)
     Slot slot[2];
     double stats[ST_N] = {0};
 
@@ -217,6 +239,12 @@ struct Engine {
     int fail(const std::string& m) {
         err = m;
         return -1;
+    }
+    // an enqueue that fails after its first async operation: wait for what was queued on the
+    // slot's stream, so the staging / device buffers are idle before anyone reuses or frees them
+    int drain_fail(Slot& s, const std::string& m) {
+        h2j_gpu_stream_sync(s.stream);
+        return fail(m);
     }
 
     // Lay out, pack and enqueue the GPU work of jobs[live] on slot s.
@@ -433,24 +461,24 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     r |= h2j_gpu_memcpy_h2d(din, hin, in_bytes, st);
     r |= h2j_gpu_memset(s.d_arena.p, 0, s.zero_bytes, st);
     r |= h2j_gpu_event_record(s.ev[1], st);
-    if (r) return fail(std::string("upload failed: ") + h2j_gpu_last_error());
-    if (h2j_gpu_prep(&b, st)) return fail(h2j_gpu_last_error());
+    if (r) return drain_fail(s, std::string("upload failed: ") + h2j_gpu_last_error());
+    if (h2j_gpu_prep(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[8], st);
-    if (h2j_gpu_predict(&b, st)) return fail(h2j_gpu_last_error());
+    if (h2j_gpu_predict(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[2], st);
-    if (stages >= 2 && h2j_gpu_deblock(&b, st)) return fail(h2j_gpu_last_error());
+    if (stages >= 2 && h2j_gpu_deblock(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[3], st);
-    if (stages >= 3 && h2j_gpu_sao(&b, st)) return fail(h2j_gpu_last_error());
+    if (stages >= 3 && h2j_gpu_sao(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[4], st);
-    if (stages >= 4 && h2j_gpu_jpeg(&b, st)) return fail(h2j_gpu_last_error());
+    if (stages >= 4 && h2j_gpu_jpeg(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[5], st);
-    if (entropy && h2j_gpu_entropy(&b, st)) return fail(h2j_gpu_last_error());
+    if (entropy && h2j_gpu_entropy(&b, st)) return drain_fail(s, h2j_gpu_last_error());
     h2j_gpu_event_record(s.ev[6], st);
     if (entropy) {
         r |= h2j_gpu_memcpy_d2h(s.h_js.p, s.d_scratch.p, 8, st);  // seg_total
         r |= h2j_gpu_memcpy_d2h(s.h_js.p + 256, static_cast<uint8_t*>(s.d_arena.p) + s.jstat_base,
                                 static_cast<size_t>(nf) * s.jstat_stride, st);
-        if (r) return fail(std::string("download failed: ") + h2j_gpu_last_error());
+        if (r) return drain_fail(s, std::string("download failed: ") + h2j_gpu_last_error());
     }
     h2j_gpu_event_record(s.ev[9], st);
     s.pending = true;
@@ -488,6 +516,11 @@ int Engine::sync(Slot& s) {
     // copies only (the payload copy is enqueued once the host has read the sizes)
     stats[ST_D2H] += h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]) +
                      (s.entropy ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[7]) : 0.0f);
+    ChunkTime ct;
+    ct.frames = static_cast<int>(s.live.size());
+    ct.k1_ms = h2j_gpu_event_elapsed_ms(s.ev[8], s.ev[2]);
+    ct.kernels_ms = h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[6]);
+    chunk_log.push_back(ct);
     return 0;
 }
 
@@ -544,13 +577,17 @@ h2j_engine* h2j_engine_create(int device, int host_threads) {
         }
         for (auto& ev : s.ev) ev = h2j_gpu_event_create();
     }
-    int t = host_threads;
-    if (t <= 0) {
-        t = static_cast<int>(std::thread::hardware_concurrency());
-        if (t > 16) t = 16;
-        if (t < 1) t = 1;
+    // host pool: NUMA-local to the device, sized by the CPU mask / cgroup quota (affinity.h)
+    std::vector<int> nodes;
+    const int ndev = h2j_gpu_device_count();
+    for (int i = 0; i < ndev; i++) {
+        char bus[64] = {0};
+        nodes.push_back(h2j_gpu_pci_bus_id(i, bus, sizeof(bus)) == 0 ? h2j::pci_numa_node(bus) : -1);
     }
-    e.pool = new h2j::ThreadPool(t - 1);
+    const int node = device >= 0 && device < ndev ? nodes[device] : -1;
+    e.plan = h2j::plan_host(device, nodes, h2j::process_cpus(), h2j::node_cpus(node), h2j::cgroup_cpu_quota(),
+                            host_threads > 0 ? host_threads : 0, host_threads < 0 ? -host_threads : 1);
+    e.pool = new h2j::ThreadPool(e.plan.threads - 1, e.plan.cpus);
     return w;
 }
 
@@ -565,6 +602,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
     const double t0 = h2j::now_ms();
     for (auto& v : e.stats) v = 0;
+    e.chunk_log.clear();
     if (static_cast<int>(e.jobs.size()) < n) e.jobs.resize(n);
     for (int i = 0; i < n; i++) {
         out_len[i] = 0;
@@ -684,6 +722,7 @@ int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const
     }
     if (producer.joinable()) producer.join();
     e.stats[h2j::ST_PARSE] = t_parsed - t0;
+    e.last_status.assign(status, status + n);
     if (fail) {
         for (auto& s : e.slot)
             if (s.pending) e.sync(s);
@@ -761,6 +800,40 @@ int h2j_engine_jpeg_coeffs(h2j_engine* w, const uint8_t* data, size_t size, int1
     info[2] = st.qscale;
     info[3] = nmcu;
     return 0;
+}
+
+int h2j_engine_host_info(h2j_engine* w, int* out, int n) {
+    if (!w) return -1;
+    const Engine& e = w->e;
+    const int v[4] = {e.pool->size() + 1, e.plan.numa_node, e.pool->pinned() ? static_cast<int>(e.plan.cpus.size()) : 0,
+                      e.plan.cpus.empty() ? -1 : e.plan.cpus[0]};
+    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
+    return 0;
+}
+
+const char* h2j_engine_frame_error(h2j_engine* w, int i) {
+    if (!w || i < 0 || i >= static_cast<int>(w->e.last_status.size())) return "";
+    switch (w->e.last_status[i]) {
+    case 0: return "";
+    case -50: return "output buffer too small";
+    case -51: return "JPEG payload pool overflow";
+    case -52: return "device-side failure (K1 band hand-off timed out)";
+    default: return i < static_cast<int>(w->e.jobs.size()) ? w->e.jobs[i].message.c_str() : "";
+    }
+}
+
+int h2j_device_count(void) { return h2j_gpu_device_count(); }
+
+int h2j_engine_chunk_times(h2j_engine* w, double* out, int max_chunks) {
+    if (!w) return -1;
+    const auto& log = w->e.chunk_log;
+    const int n = static_cast<int>(log.size());
+    for (int i = 0; i < n && i < max_chunks; i++) {
+        out[3 * i] = log[i].frames;
+        out[3 * i + 1] = log[i].k1_ms;
+        out[3 * i + 2] = log[i].kernels_ms;
+    }
+    return n;
 }
 
 int h2j_engine_stats(h2j_engine* w, double* out, int n) {

@@ -119,7 +119,7 @@ struct Sps {
 struct Pps {
     bool valid = false;
     int sps_id = 0, cabac = 0, bottom_field_pic_order = 0, init_qp = 26, cqp = 0, cqp2 = 0;
-    int deblock_ctrl = 0, redundant_pic_cnt = 0, transform_8x8 = 0;
+    int deblock_ctrl = 0, redundant_pic_cnt = 0, transform_8x8 = 0, scaling_present = 0;
     uint8_t sl4[6][16];
     uint8_t sl8[6][64];
 };
@@ -186,32 +186,47 @@ int parse_sps(BitReader& b, Sps* tab) {
             parse_matrices(b, s.sl4, s.sl8, s.chroma_format_idc != 3 ? 2 : 6, fb4, fb8, true);
         }
     }
-    s.log2_max_frame_num = static_cast<int>(b.ue()) + 4;
-    s.poc_type = static_cast<int>(b.ue());
+    // ranges of 7.4.2.1.1 (FFmpeg h264_ps.c rejects the SPS outside them)
+    const uint32_t lfn = b.ue();
+    if (lfn > 12) return -1;
+    s.log2_max_frame_num = static_cast<int>(lfn) + 4;
+    const uint32_t poc_type = b.ue();
+    if (poc_type > 2) return -1;
+    s.poc_type = static_cast<int>(poc_type);
     if (s.poc_type == 0) {
-        s.log2_max_poc_lsb = static_cast<int>(b.ue()) + 4;
+        const uint32_t lpl = b.ue();
+        if (lpl > 12) return -1;
+        s.log2_max_poc_lsb = static_cast<int>(lpl) + 4;
     } else if (s.poc_type == 1) {
         s.delta_pic_order_always_zero = static_cast<int>(b.u(1));
         b.se();
         b.se();
-        const int n = static_cast<int>(b.ue());
+        const uint32_t n = b.ue();
         if (n > 255) return -1;
-        for (int i = 0; i < n; i++) b.se();
+        for (uint32_t i = 0; i < n; i++) b.se();
     }
     b.ue();
     b.u(1);
-    s.mb_w = static_cast<int>(b.ue()) + 1;
-    s.mb_h = static_cast<int>(b.ue()) + 1;
+    const uint32_t mbw1 = b.ue(), mbh1 = b.ue();
+    if (mbw1 >= 512 || mbh1 >= 512) return -5;
+    s.mb_w = static_cast<int>(mbw1) + 1;
+    s.mb_h = static_cast<int>(mbh1) + 1;
     if (!b.u(1)) return -3;  // interlaced
     b.u(1);
     if (b.u(1)) {
-        s.crop_l = static_cast<int>(b.ue()) * 2;
-        s.crop_r = static_cast<int>(b.ue()) * 2;
-        s.crop_t = static_cast<int>(b.ue()) * 2;
-        s.crop_b = static_cast<int>(b.ue()) * 2;
+        // frame cropping in 2-sample units (4:2:0, frame_mbs_only); like FFmpeg, offsets that
+        // leave no picture are ignored (whole coded picture), not an error
+        const uint32_t cl = b.ue(), cr = b.ue(), ct = b.ue(), cb = b.ue();
+        const uint64_t w = static_cast<uint64_t>(s.mb_w) * 16, h = static_cast<uint64_t>(s.mb_h) * 16;
+        if ((static_cast<uint64_t>(cl) + cr) * 2 < w && (static_cast<uint64_t>(ct) + cb) * 2 < h) {
+            s.crop_l = static_cast<int>(cl) * 2;
+            s.crop_r = static_cast<int>(cr) * 2;
+            s.crop_t = static_cast<int>(ct) * 2;
+            s.crop_b = static_cast<int>(cb) * 2;
+        }
     }
+    if (b.overrun()) return -1;
     if (s.chroma_format_idc != 1 || s.bit_depth > 10 || s.bit_depth_c != s.bit_depth) return -4;
-    if (s.mb_w > 512 || s.mb_h > 512) return -5;
     s.valid = true;
     return 0;
 }
@@ -233,6 +248,7 @@ int parse_pps(BitReader& b, Pps* tab, const Sps* sps) {
     p.init_qp = 26 + b.se();
     b.se();
     p.cqp = b.se();
+    if (p.cqp < -12 || p.cqp > 12) return -1;
     p.deblock_ctrl = static_cast<int>(b.u(1));
     b.u(1);
     p.redundant_pic_cnt = static_cast<int>(b.u(1));
@@ -242,13 +258,15 @@ int parse_pps(BitReader& b, Pps* tab, const Sps* sps) {
     std::memcpy(p.sl8, s.sl8, sizeof(p.sl8));
     if (b.more_rbsp_data()) {
         p.transform_8x8 = static_cast<int>(b.u(1));
-        if (b.u(1)) {
+        p.scaling_present = static_cast<int>(b.u(1));
+        if (p.scaling_present) {
             uint8_t fb4[6][16], fb8[6][64];
             std::memcpy(fb4, s.sl4, sizeof(fb4));
             std::memcpy(fb8, s.sl8, sizeof(fb8));
             parse_matrices(b, p.sl4, p.sl8, p.transform_8x8 ? 2 : 0, fb4, fb8, !s.scaling_present);
         }
         p.cqp2 = b.se();
+        if (p.cqp2 < -12 || p.cqp2 > 12) return -1;
     }
     p.valid = true;
     return 0;
@@ -1069,7 +1087,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             if (have) break;
             if (parse_pps(b, pps_, sps_) < 0) { job_->message = "unsupported or invalid PPS"; return -3; }
         } else if (type == 1 || type == 5) {
-            const int first_mb = static_cast<int>(b.ue());
+            const uint32_t first_mb_u = b.ue();
             const int slice_type = static_cast<int>(b.ue());
             const uint32_t pps_id = b.ue();
             if (pps_id > 255 || !pps_[pps_id].valid || !sps_[pps_[pps_id].sps_id].valid) {
@@ -1078,8 +1096,13 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             }
             const Pps& p = pps_[pps_id];
             const Sps& s = sps_[p.sps_id];
+            const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h) ? static_cast<int>(first_mb_u) : -1;
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            if (first_mb < 0) {  // FFmpeg h264_slice.c: "first_mb_in_slice overflow"
+                job_->message = "first_mb_in_slice outside the picture";
+                return -6;
+            }
             if (slice_type % 5 != 2) { job_->message = "first picture is not intra (P/B slices unsupported)"; return -5; }
             if (type == 5) b.ue();
             if (s.poc_type == 0) {
@@ -1108,10 +1131,14 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             const int qpd = b.se();
             h2j_slice srec{};
             if (p.deblock_ctrl) {
-                srec.deblock_disabled = static_cast<uint8_t>(b.ue());
+                const uint32_t idc = b.ue();
+                if (idc > 2) { job_->message = "disable_deblocking_filter_idc out of range"; return -6; }
+                srec.deblock_disabled = static_cast<uint8_t>(idc);
                 if (srec.deblock_disabled != 1) {
-                    srec.tc_offset = static_cast<int8_t>(b.se() * 2);
-                    srec.beta_offset = static_cast<int8_t>(b.se() * 2);
+                    const int a = b.se(), bb = b.se();
+                    if (a < -6 || a > 6 || bb < -6 || bb > 6) { job_->message = "deblocking offsets out of range"; return -6; }
+                    srec.tc_offset = static_cast<int8_t>(a * 2);
+                    srec.beta_offset = static_cast<int8_t>(bb * 2);
                 }
             }
             srec.cqp_offset[0] = static_cast<int8_t>(p.cqp);
@@ -1143,7 +1170,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 f.mw = f.width / 4;
                 f.mh = f.height / 4;
                 f.lf_across_tiles = 1;
-                if (s.scaling_present || p.transform_8x8) {
+                if (s.scaling_present || p.scaling_present || p.transform_8x8) {
                     // weight scale tables (raster), used by K1 for every H.264 frame with this flag
                     job_->sl.assign(H2J_SL264_BYTES, 16);
                     for (int c = 0; c < 3; c++)
@@ -1156,7 +1183,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 first_idr = type == 5;
             }
             p_ = &p;
-            if (job_->hdr.scaling_list == 0 && (p.transform_8x8 || s.scaling_present)) {
+            if (job_->hdr.scaling_list == 0 && (p.transform_8x8 || p.scaling_present || s.scaling_present)) {
                 job_->message = "scaling matrices changed inside the picture";
                 return -6;
             }

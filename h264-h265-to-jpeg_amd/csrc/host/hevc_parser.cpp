@@ -182,27 +182,42 @@ int parse_sps(BitReader& b, Sps* tab) {
     s = Sps();
     s.chroma_format_idc = static_cast<int>(b.ue());
     if (s.chroma_format_idc == 3) b.u(1);
-    s.width = static_cast<int>(b.ue());
-    s.height = static_cast<int>(b.ue());
+    const uint32_t w = b.ue(), h = b.ue();
+    if (w == 0 || h == 0 || w > 8192 || h > 8192) return -4;
+    s.width = static_cast<int>(w);
+    s.height = static_cast<int>(h);
     if (b.u(1)) {
-        int sw = (s.chroma_format_idc == 1 || s.chroma_format_idc == 2) ? 2 : 1;
-        int shh = s.chroma_format_idc == 1 ? 2 : 1;
-        s.conf_l = static_cast<int>(b.ue()) * sw;
-        s.conf_r = static_cast<int>(b.ue()) * sw;
-        s.conf_t = static_cast<int>(b.ue()) * shh;
-        s.conf_b = static_cast<int>(b.ue()) * shh;
+        // conformance window; like FFmpeg (hevc_ps.c "Invalid cropping offsets ... Displaying the
+        // whole video surface"), offsets that leave no picture are ignored, not an error
+        const uint64_t sw = (s.chroma_format_idc == 1 || s.chroma_format_idc == 2) ? 2 : 1;
+        const uint64_t shh = s.chroma_format_idc == 1 ? 2 : 1;
+        const uint64_t l = b.ue() * sw, r = b.ue() * sw, t = b.ue() * shh, bo = b.ue() * shh;
+        if (l + r < w && t + bo < h) {
+            s.conf_l = static_cast<int>(l);
+            s.conf_r = static_cast<int>(r);
+            s.conf_t = static_cast<int>(t);
+            s.conf_b = static_cast<int>(bo);
+        }
     }
-    s.bit_depth = static_cast<int>(b.ue()) + 8;
-    s.bit_depth_c = static_cast<int>(b.ue()) + 8;
-    s.log2_max_poc_lsb = static_cast<int>(b.ue()) + 4;
+    // the ue() fields below are range-checked (as FFmpeg's ff_hevc_parse_sps does) before any
+    // becomes an int: the syntax allows values up to 2^32 - 2
+    const uint32_t bd = b.ue(), bdc = b.ue(), lpl = b.ue();
+    if (bd > 4 || bdc > 4 || lpl > 12) return -3;
+    s.bit_depth = static_cast<int>(bd) + 8;
+    s.bit_depth_c = static_cast<int>(bdc) + 8;
+    s.log2_max_poc_lsb = static_cast<int>(lpl) + 4;
     int sub = static_cast<int>(b.u(1));
     for (int i = sub ? 0 : msl; i <= msl; i++) { b.ue(); b.ue(); b.ue(); }
-    s.log2_min_cb = static_cast<int>(b.ue()) + 3;
-    s.log2_ctb = s.log2_min_cb + static_cast<int>(b.ue());
-    s.log2_min_tb = static_cast<int>(b.ue()) + 2;
-    s.log2_max_tb = s.log2_min_tb + static_cast<int>(b.ue());
+    const uint32_t mcb = b.ue(), dcb = b.ue(), mtb = b.ue(), dtb = b.ue();
+    if (mcb > 3 || dcb > 3 || mtb > 3 || dtb > 3) return -3;
+    s.log2_min_cb = static_cast<int>(mcb) + 3;
+    s.log2_ctb = s.log2_min_cb + static_cast<int>(dcb);
+    s.log2_min_tb = static_cast<int>(mtb) + 2;
+    s.log2_max_tb = s.log2_min_tb + static_cast<int>(dtb);
     b.ue();
-    s.max_th_depth_intra = static_cast<int>(b.ue());
+    const uint32_t mthd = b.ue();
+    if (mthd > 4) return -3;
+    s.max_th_depth_intra = static_cast<int>(mthd);
     s.scaling_list_enabled = static_cast<int>(b.u(1));
     sl_default(s.sl, s.sl_dc);
     if (s.scaling_list_enabled && b.u(1)) parse_scaling_list(b, s.sl, s.sl_dc);
@@ -212,8 +227,10 @@ int parse_sps(BitReader& b, Sps* tab) {
     if (s.pcm) {
         s.pcm_bd = static_cast<int>(b.u(4)) + 1;
         s.pcm_bd_c = static_cast<int>(b.u(4)) + 1;
-        s.log2_min_pcm = static_cast<int>(b.ue()) + 3;
-        s.log2_max_pcm = s.log2_min_pcm + static_cast<int>(b.ue());
+        const uint32_t mp = b.ue(), dp = b.ue();
+        if (mp > 2 || dp > 2) return -3;
+        s.log2_min_pcm = static_cast<int>(mp) + 3;
+        s.log2_max_pcm = s.log2_min_pcm + static_cast<int>(dp);
         s.pcm_lf_disabled = static_cast<int>(b.u(1));
     }
     s.num_st_rps = static_cast<int>(b.ue());
@@ -222,7 +239,9 @@ int parse_sps(BitReader& b, Sps* tab) {
         if (!parse_st_rps(b, s, i)) return -1;
     s.long_term_present = static_cast<int>(b.u(1));
     if (s.long_term_present) {
-        s.num_lt_sps = static_cast<int>(b.ue());
+        const uint32_t nlt = b.ue();
+        if (nlt > 32) return -1;
+        s.num_lt_sps = static_cast<int>(nlt);
         for (int i = 0; i < s.num_lt_sps; i++) { b.u(s.log2_max_poc_lsb); b.u(1); }
     }
     s.temporal_mvp = static_cast<int>(b.u(1));
@@ -230,7 +249,15 @@ int parse_sps(BitReader& b, Sps* tab) {
     if (s.chroma_format_idc != 1) return -2;
     if (s.log2_ctb > 6 || s.log2_ctb < 4 || s.log2_max_tb > 5 || s.bit_depth > 12 || s.bit_depth_c != s.bit_depth)
         return -3;
-    if (s.width <= 0 || s.height <= 0 || s.width > 8192 || s.height > 8192) return -4;
+    // FFmpeg hevc_ps.c: "Invalid value for log2_min_tb_size", "Invalid coded frame dimensions",
+    // "max transform block size out of range", "max_transform_hierarchy_depth_intra out of range",
+    // "PCM bit depth ... is greater than normal bit depth"
+    if (s.log2_min_tb >= s.log2_min_cb || s.log2_min_cb > s.log2_ctb || s.log2_max_tb > s.log2_ctb) return -3;
+    if (s.max_th_depth_intra > s.log2_ctb - s.log2_min_tb) return -3;
+    if ((s.width & ((1 << s.log2_min_cb) - 1)) || (s.height & ((1 << s.log2_min_cb) - 1))) return -4;
+    if (s.pcm && (s.pcm_bd > s.bit_depth || s.pcm_bd_c > s.bit_depth_c || s.log2_max_pcm > std::min(s.log2_ctb, 5)))
+        return -3;
+    if (b.overrun()) return -1;
     s.valid = true;
     return 0;
 }
@@ -240,7 +267,9 @@ int parse_pps(BitReader& b, Pps* tab) {
     if (id > 63) return -1;
     Pps& p = tab[id];
     p = Pps();
-    p.sps_id = static_cast<int>(b.ue());
+    const uint32_t sps_id = b.ue();
+    if (sps_id > 15) return -1;
+    p.sps_id = static_cast<int>(sps_id);
     p.dependent_slices = static_cast<int>(b.u(1));
     p.output_flag_present = static_cast<int>(b.u(1));
     p.num_extra_bits = static_cast<int>(b.u(3));
@@ -249,12 +278,18 @@ int parse_pps(BitReader& b, Pps* tab) {
     b.ue();
     b.ue();
     p.init_qp = 26 + b.se();
+    if (p.init_qp < -24 || p.init_qp > 51) return -1;
     b.u(1);  // constrained_intra_pred (no effect in all-intra pictures)
     p.transform_skip = static_cast<int>(b.u(1));
     p.cu_qp_delta = static_cast<int>(b.u(1));
-    if (p.cu_qp_delta) p.diff_cu_qp_delta_depth = static_cast<int>(b.ue());
+    if (p.cu_qp_delta) {
+        const uint32_t dd = b.ue();
+        if (dd > 3) return -1;
+        p.diff_cu_qp_delta_depth = static_cast<int>(dd);
+    }
     p.cb_qp_offset = b.se();
     p.cr_qp_offset = b.se();
+    if (p.cb_qp_offset < -12 || p.cb_qp_offset > 12 || p.cr_qp_offset < -12 || p.cr_qp_offset > 12) return -1;
     p.slice_chroma_qp_present = static_cast<int>(b.u(1));
     b.u(1);
     b.u(1);
@@ -262,13 +297,22 @@ int parse_pps(BitReader& b, Pps* tab) {
     p.tiles = static_cast<int>(b.u(1));
     p.wpp = static_cast<int>(b.u(1));
     if (p.tiles) {
-        p.ntc = static_cast<int>(b.ue()) + 1;
-        p.ntr = static_cast<int>(b.ue()) + 1;
-        if (p.ntc > 64 || p.ntr > 64) return -1;
+        const uint32_t ntc = b.ue(), ntr = b.ue();
+        if (ntc > 63 || ntr > 63) return -1;
+        p.ntc = static_cast<int>(ntc) + 1;
+        p.ntr = static_cast<int>(ntr) + 1;
         p.uniform = static_cast<int>(b.u(1));
-        if (!p.uniform) {
-            for (int i = 0; i < p.ntc - 1; i++) p.col_w[i] = static_cast<int>(b.ue()) + 1;
-            for (int i = 0; i < p.ntr - 1; i++) p.row_h[i] = static_cast<int>(b.ue()) + 1;
+        if (!p.uniform) {  // sizes in CTBs; their sums are checked against the picture in setup_tiles
+            for (int i = 0; i < p.ntc - 1; i++) {
+                const uint32_t v = b.ue();
+                if (v >= 512) return -1;
+                p.col_w[i] = static_cast<int>(v) + 1;
+            }
+            for (int i = 0; i < p.ntr - 1; i++) {
+                const uint32_t v = b.ue();
+                if (v >= 512) return -1;
+                p.row_h[i] = static_cast<int>(v) + 1;
+            }
         }
         p.lf_across_tiles = static_cast<int>(b.u(1));
     }
@@ -277,8 +321,10 @@ int parse_pps(BitReader& b, Pps* tab) {
         p.deblock_override = static_cast<int>(b.u(1));
         p.deblock_disabled = static_cast<int>(b.u(1));
         if (!p.deblock_disabled) {
-            p.beta_offset = b.se() * 2;
-            p.tc_offset = b.se() * 2;
+            const int bo = b.se(), to = b.se();
+            if (bo < -6 || bo > 6 || to < -6 || to > 6) return -1;
+            p.beta_offset = bo * 2;
+            p.tc_offset = to * 2;
         }
     }
     p.sl_present = static_cast<int>(b.u(1));
@@ -289,6 +335,7 @@ int parse_pps(BitReader& b, Pps* tab) {
     b.u(1);
     b.ue();
     p.slice_header_ext = static_cast<int>(b.u(1));
+    if (b.overrun()) return -1;
     p.valid = true;
     return 0;
 }
@@ -441,8 +488,8 @@ private:
     int err_ = 0;
 
     int parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, const SliceHdr* prev);
-    void setup_picture();
-    void setup_tiles();
+    bool setup_picture();
+    bool setup_tiles();
     int decode_slice_data(int shi, const uint8_t* p, const uint8_t* end);
     struct WppRows;
     int decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t* end, WppRows& w);
@@ -493,8 +540,9 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
     sh = SliceHdr();
     sh.first_in_pic = static_cast<int>(b.u(1));
     if (nal_type >= 16 && nal_type <= 23) b.u(1);
-    sh.pps_id = static_cast<int>(b.ue());
-    if (sh.pps_id > 63 || !pps_[sh.pps_id].valid) return -1;
+    const uint32_t pps_id = b.ue();
+    if (pps_id > 63 || !pps_[pps_id].valid) return -1;
+    sh.pps_id = static_cast<int>(pps_id);
     const Pps& p = pps_[sh.pps_id];
     if (p.sps_id > 15 || !sps_[p.sps_id].valid) return -1;
     const Sps& s = sps_[p.sps_id];
@@ -527,10 +575,11 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
                 b.u(ceil_log2(s.num_st_rps));
             }
             if (s.long_term_present) {
-                int nsps = 0;
-                if (s.num_lt_sps > 0) nsps = static_cast<int>(b.ue());
-                int npics = static_cast<int>(b.ue());
-                for (int i = 0; i < nsps + npics; i++) {
+                uint32_t nsps = 0;
+                if (s.num_lt_sps > 0) nsps = b.ue();
+                const uint32_t npics = b.ue();
+                if (nsps > static_cast<uint32_t>(s.num_lt_sps) || npics > 32) return -1;
+                for (uint32_t i = 0; i < nsps + npics; i++) {
                     if (i < nsps) {
                         if (s.num_lt_sps > 1) b.u(ceil_log2(s.num_lt_sps));
                     } else {
@@ -551,6 +600,10 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
         if (p.slice_chroma_qp_present) {
             sh.cb_qp_offset = b.se();
             sh.cr_qp_offset = b.se();
+            if (sh.cb_qp_offset < -12 || sh.cb_qp_offset > 12 || sh.cr_qp_offset < -12 || sh.cr_qp_offset > 12 ||
+                p.cb_qp_offset + sh.cb_qp_offset < -12 || p.cb_qp_offset + sh.cb_qp_offset > 12 ||
+                p.cr_qp_offset + sh.cr_qp_offset < -12 || p.cr_qp_offset + sh.cr_qp_offset > 12)
+                return -1;
         }
         int override_ = 0;
         if (p.deblock_override) override_ = static_cast<int>(b.u(1));
@@ -560,8 +613,10 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
         if (override_) {
             sh.deblock_disabled = static_cast<int>(b.u(1));
             if (!sh.deblock_disabled) {
-                sh.beta_offset = b.se() * 2;
-                sh.tc_offset = b.se() * 2;
+                const int bo = b.se(), to = b.se();
+                if (bo < -6 || bo > 6 || to < -6 || to > 6) return -1;
+                sh.beta_offset = bo * 2;
+                sh.tc_offset = to * 2;
             }
         }
         sh.lf_across_slices = p.lf_across_slices;
@@ -571,23 +626,26 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
         if (sh.slice_qp < -6 * (s.bit_depth - 8) || sh.slice_qp > 51) return -1;
     }
     if (p.tiles || p.wpp) {
-        int ne = static_cast<int>(b.ue());
+        const uint32_t ne = b.ue();
+        const int cs = 1 << s.log2_ctb;
+        if (ne >= static_cast<uint32_t>(((s.width + cs - 1) / cs) * ((s.height + cs - 1) / cs))) return -1;
         if (ne > 0) {
-            int len = static_cast<int>(b.ue()) + 1;
+            const uint32_t len = b.ue() + 1;
             if (len > 32) return -1;
-            for (int i = 0; i < ne; i++) sh.entry.push_back(b.u(len) + 1u);
+            for (uint32_t i = 0; i < ne; i++) sh.entry.push_back(b.u(static_cast<int>(len)) + 1u);
         }
     }
     if (p.slice_header_ext) {
-        int len = static_cast<int>(b.ue());
-        for (int i = 0; i < len; i++) b.u(8);
+        const uint32_t len = b.ue();
+        if (len > 256) return -1;
+        for (uint32_t i = 0; i < len; i++) b.u(8);
     }
     b.u(1);
     b.align();
     return b.overrun() ? -1 : 0;
 }
 
-void HevcParser::setup_picture() {
+bool HevcParser::setup_picture() {
     W = s_->width;
     H = s_->height;
     log2ctb = s_->log2_ctb;
@@ -607,7 +665,7 @@ void HevcParser::setup_picture() {
     rs2ts_.assign(nctb, 0);
     ts2rs_.assign(nctb, 0);
     tile_id_.assign(nctb, 0);
-    setup_tiles();
+    if (!setup_tiles()) return false;
     job_->ctbs.assign(nctb, h2j_ctb());
     for (int rs = 0; rs < nctb; rs++) {
         job_->ctbs[rs].ts = static_cast<uint32_t>(rs2ts_[rs]);
@@ -664,10 +722,12 @@ void HevcParser::setup_picture() {
         t[0] = dc[3][0];
         f.scaling_list = 1;
     }
+    return true;
 }
 
-void HevcParser::setup_tiles() {
+bool HevcParser::setup_tiles() {
     const Pps& p = *p_;
+    if (p.ntc > ctbW || p.ntr > ctbH) return false;  // 7.4.3.3: at most one tile per CTB column / row
     std::vector<int> colw(p.ntc), rowh(p.ntr), cbd(p.ntc + 1), rbd(p.ntr + 1);
     int s = 0;
     for (int i = 0; i < p.ntc; i++) {
@@ -681,6 +741,10 @@ void HevcParser::setup_tiles() {
         else rowh[j] = j < p.ntr - 1 ? p.row_h[j] : ctbH - s;
         s += rowh[j];
     }
+    for (int i = 0; i < p.ntc; i++)
+        if (colw[i] <= 0) return false;  // explicit column widths past the picture
+    for (int j = 0; j < p.ntr; j++)
+        if (rowh[j] <= 0) return false;
     cbd[0] = 0;
     for (int i = 0; i < p.ntc; i++) cbd[i + 1] = cbd[i] + colw[i];
     rbd[0] = 0;
@@ -705,6 +769,7 @@ void HevcParser::setup_tiles() {
             for (int y = rbd[j]; y < rbd[j + 1]; y++)
                 for (int x = cbd[i]; x < cbd[i + 1]; x++) tile_id_[rs2ts_[y * ctbW + x]] = tid;
     col_bd_ = cbd;
+    return true;
 }
 
 void HevcParser::qg_start(int xq, int yq) {
@@ -1504,7 +1569,7 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
             if (!have_pic) {
                 p_ = &pps_[sh.pps_id];
                 s_ = &sps_[p_->sps_id];
-                setup_picture();
+                if (!setup_picture()) { job_->message = "invalid tile grid"; return -6; }
                 have_pic = true;
             }
             p_ = &pps_[sh.pps_id];

@@ -51,6 +51,13 @@ def load_library() -> ctypes.CDLL:
                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
     lib.h2j_engine_stats.restype = ctypes.c_int
     lib.h2j_engine_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    lib.h2j_engine_frame_error.restype = ctypes.c_char_p
+    lib.h2j_engine_frame_error.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.h2j_engine_host_info.restype = ctypes.c_int
+    lib.h2j_engine_host_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.h2j_device_count.restype = ctypes.c_int
+    lib.h2j_engine_chunk_times.restype = ctypes.c_int
+    lib.h2j_engine_chunk_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     lib.h2j_version.restype = ctypes.c_char_p
     lib.h2j_gpu_device_count.restype = ctypes.c_int
     _lib = lib
@@ -92,6 +99,16 @@ class Engine:
 
     def error(self) -> str:
         return self._lib.h2j_engine_error(self._h).decode(errors="replace")
+
+    def frame_error(self, i: int) -> str:
+        """Message of picture i of the last transcode ('' if it succeeded)."""
+        return self._lib.h2j_engine_frame_error(self._h, int(i)).decode(errors="replace")
+
+    def host_info(self) -> dict:
+        """Host entropy pool placement (include/h2j.h h2j_engine_host_info)."""
+        arr = (ctypes.c_int * 4)()
+        self._lib.h2j_engine_host_info(self._h, arr, 4)
+        return {"threads": arr[0], "numa_node": arr[1], "pinned_cpus": arr[2], "first_cpu": arr[3]}
 
     def transcode(self, streams: Sequence[bytes]) -> List[Optional[bytes]]:
         """Annex-B H.264/H.265 stills -> JPEG bytes (None for items that failed)."""
@@ -149,6 +166,13 @@ class Engine:
             raise RuntimeError(f"h2j_engine_jpeg_coeffs failed ({rc}): {self.error()}")
         nmcu = info[3]
         return info[2], out[:nmcu * 384].reshape(nmcu, 6, 64).copy()
+
+    def chunk_times(self) -> list:
+        """[(pictures, K1 ms, K0..K5 ms)] per chunk of the last transcode."""
+        cap = 4096
+        arr = (ctypes.c_double * (3 * cap))()
+        n = self._lib.h2j_engine_chunk_times(self._h, arr, cap)
+        return [(int(arr[3 * i]), arr[3 * i + 1], arr[3 * i + 2]) for i in range(min(n, cap))]
 
     def stats(self) -> dict:
         arr = (ctypes.c_double * len(STAT_KEYS))()

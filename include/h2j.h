@@ -24,11 +24,22 @@ extern "C" {
 
 typedef struct h2j_engine h2j_engine;
 
-/* device: HIP device ordinal; host_threads: entropy/Huffman worker threads
- * (<= 0: hardware concurrency, capped at 16). */
+/* Visible HIP devices (0: the MI355X pipeline cannot run). */
+int h2j_device_count(void);
+
+/* device: HIP device ordinal; host_threads: entropy/Huffman threads (the caller's thread
+ * included).  > 0: exactly that many.  0: automatic -- the process's CPUs on the device's NUMA
+ * node, split between the visible devices of that node, bounded by the cgroup CPU quota and 64;
+ * the pool's workers are pinned to that NUMA-local slice (H2J_PIN=0: not pinned).  -k: as 0,
+ * for one of k engines in this process (they share the cgroup quota). */
 h2j_engine *h2j_engine_create(int device, int host_threads);
 void h2j_engine_destroy(h2j_engine *e);
 const char *h2j_engine_error(h2j_engine *e);
+/* Message of picture i of the last h2j_engine_transcode ("" if it succeeded). */
+const char *h2j_engine_frame_error(h2j_engine *e, int i);
+/* Host placement: out[0] threads (incl. the caller), [1] the device's NUMA node (-1 unknown),
+ * [2] CPUs the workers are pinned to (0: not pinned), [3] first of those CPUs. */
+int h2j_engine_host_info(h2j_engine *e, int *out, int n);
 
 /* Transcode n independent Annex-B stills (H.264 or H.265, first picture of
  * each) to baseline JPEG.  JPEG i is written at out + out_off[i], length
@@ -53,6 +64,10 @@ int h2j_engine_jpeg_coeffs(h2j_engine *e, const uint8_t *data, size_t size, int1
  * [5] jpeg (GPU)  [6] d2h  [7] huffman (host, wall)  [8] total (wall)
  * [9] frames  [10] algorithmic bytes of the GPU pixel path. */
 int h2j_engine_stats(h2j_engine *e, double *out, int n);
+/* Per chunk (one GPU launch of each stage) of the last h2j_engine_transcode, in order:
+ * out[3i] pictures, out[3i+1] K1 ms, out[3i+2] K0..K5 ms (HIP events on the chunk's stream).
+ * Returns the number of chunks (entries beyond max_chunks are not written). */
+int h2j_engine_chunk_times(h2j_engine *e, double *out, int max_chunks);
 
 /* In-memory and batch entry points beside IDecoder (the reference has only the
  * file-path call, /root/reference/export_inc/IDecoder.h:29).

@@ -32,6 +32,8 @@ extern "C" {
 /* device / memory / stream plumbing */
 int h2j_gpu_device_count(void);
 int h2j_gpu_set_device(int device);
+/* PCI bus id "dddd:bb:dd.f" of a device (locates its NUMA node in sysfs for host-thread pinning) */
+int h2j_gpu_pci_bus_id(int device, char *buf, int len);
 void *h2j_gpu_malloc(size_t bytes);
 int h2j_gpu_free(void *p);
 void *h2j_gpu_host_alloc(size_t bytes); /* pinned */

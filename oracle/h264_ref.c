@@ -241,11 +241,16 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
     if (!s->frame_mbs_only) return -3; /* interlaced: out of scope */
     ob_u(b, 1);                         /* direct_8x8_inference */
     if (ob_u(b, 1)) {
+        /* FFmpeg h264_ps.c ignores cropping that leaves no picture ("crop values invalid",
+         * "Ignoring cropping information") unless err_recognition has AV_EF_EXPLODE */
         int cx = s->chroma_format_idc == 0 ? 1 : 2, cy = s->chroma_format_idc == 1 ? 2 : 1;
-        s->crop_l = (int)ob_ue(b) * cx;
-        s->crop_r = (int)ob_ue(b) * cx;
-        s->crop_t = (int)ob_ue(b) * cy;
-        s->crop_b = (int)ob_ue(b) * cy;
+        uint64_t cl = ob_ue(b), cr = ob_ue(b), ct = ob_ue(b), cb = ob_ue(b);
+        if ((cl + cr) * cx < (uint64_t)s->mb_w * 16 && (ct + cb) * cy < (uint64_t)s->mb_h * 16) {
+            s->crop_l = (int)cl * cx;
+            s->crop_r = (int)cr * cx;
+            s->crop_t = (int)ct * cy;
+            s->crop_b = (int)cb * cy;
+        }
     }
     if (s->chroma_format_idc != 1) return -4;
     s->valid = 1;
@@ -1507,6 +1512,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             if (!s->valid) { ret = -4; goto done; }
             int frame_num = (int)ob_u(&b, s->log2_max_frame_num);
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            if (first_mb < 0 || first_mb >= s->mb_w * s->mb_h) { ret = -6; goto done; } /* FFmpeg: "first_mb_in_slice overflow" */
             if (slice_type % 5 != 2) { ret = -5; goto done; } /* P/B: the first picture must be intra */
             if (type == 5) ob_ue(&b);                          /* idr_pic_id */
             if (s->poc_type == 0) {

@@ -247,15 +247,22 @@ static int parse_sps(OraBits *b, Sps *tab) {
     memset(s, 0, sizeof(*s));
     s->chroma_format_idc = (int)ob_ue(b);
     if (s->chroma_format_idc == 3) ob_u(b, 1);
-    s->width = (int)ob_ue(b);
-    s->height = (int)ob_ue(b);
+    uint32_t w = ob_ue(b), h = ob_ue(b);
+    if (w == 0 || h == 0 || w > 16888 || h > 16888) return -1;
+    s->width = (int)w;
+    s->height = (int)h;
     if (ob_u(b, 1)) {
-        int sw = (s->chroma_format_idc == 1 || s->chroma_format_idc == 2) ? 2 : 1;
-        int shh = s->chroma_format_idc == 1 ? 2 : 1;
-        s->conf_l = (int)ob_ue(b) * sw;
-        s->conf_r = (int)ob_ue(b) * sw;
-        s->conf_t = (int)ob_ue(b) * shh;
-        s->conf_b = (int)ob_ue(b) * shh;
+        /* FFmpeg hevc_ps.c: offsets that leave no picture are ignored ("Invalid cropping
+         * offsets", "Displaying the whole video surface") unless AV_EF_EXPLODE */
+        uint64_t sw = (s->chroma_format_idc == 1 || s->chroma_format_idc == 2) ? 2 : 1;
+        uint64_t shh = s->chroma_format_idc == 1 ? 2 : 1;
+        uint64_t l = ob_ue(b) * sw, r = ob_ue(b) * sw, t = ob_ue(b) * shh, bo = ob_ue(b) * shh;
+        if (l + r < w && t + bo < h) {
+            s->conf_l = (int)l;
+            s->conf_r = (int)r;
+            s->conf_t = (int)t;
+            s->conf_b = (int)bo;
+        }
     }
     s->bit_depth = (int)ob_ue(b) + 8;
     s->bit_depth_c = (int)ob_ue(b) + 8;
@@ -298,6 +305,8 @@ static int parse_sps(OraBits *b, Sps *tab) {
     /* VUI and extensions are not needed for Main/Main10 decoding */
     if (s->chroma_format_idc != 1) return -2;
     if (s->log2_ctb > 6 || s->log2_ctb < 4 || s->log2_max_tb > 5) return -3;
+    /* FFmpeg hevc_ps.c: "Invalid coded frame dimensions" */
+    if ((s->width & ((1 << s->log2_min_cb) - 1)) || (s->height & ((1 << s->log2_min_cb) - 1))) return -1;
     s->valid = 1;
     return 0;
 }

@@ -59,15 +59,43 @@ def test_shard_lpt_balanced_and_complete(world):
     assert max(loads) - min(loads) <= max(costs)
 
 
-def test_host_cpu_share_slices_affinity():
-    # run in a child: the helper pins the calling process when local_world > 1
-    import subprocess, sys, os
-    code = ("import sys, os; sys.path.insert(0, %r); import bench; "
-            "n = len(os.sched_getaffinity(0)); a = bench.host_cpu_share(0, 1); "
-            "b = bench.host_cpu_share(1, 2); m = len(os.sched_getaffinity(0)); "
-            "print(n, a, b, m)") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.check_output([sys.executable, "-c", code], text=True).split()
-    n, a, b, m = map(int, out)
-    assert a == min(16, n)
-    if n >= 2:
-        assert b == min(16, n // 2) and m == n // 2
+def _mixed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # configs[4]: 65,536 stills over `world` GPUs, per-GPU --frames = 65536 / world
+        mine, items = bench.rank_batch("mixed", 65536 // world, world, rank)
+        shards = [None] * world
+        dist.all_gather_object(shards, mine)
+        cost = sum(len(items[i][0]) + 0.02 * items[i][2] for i in mine)
+        el, fr = bench.reduce_over_ranks(dist, 10.0 + rank, len(mine))
+        q.put((rank, shards, len(items), cost, el, fr))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_mixed_configs4_flow_gloo(world):
+    """bench.py's configs[4] flow over the full 65,536-item list: every rank builds the same
+    global list, the LPT shards are disjoint and complete, the frame SUM and time MAX are right."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = res[0][1]
+    assert all(r[1] == shards for r in res)  # every rank computed the same partition
+    flat = [i for sh in shards for i in sh]
+    assert len(flat) == 65536 and sorted(flat) == list(range(65536))
+    for rank, sh, total, cost, el, fr in res:
+        assert total == 65536
+        assert sh[rank] == shards[rank]
+        assert el == 10.0 + world - 1  # max over ranks
+        assert fr == 65536  # sum over ranks
+    costs = [r[3] for r in res]
+    assert max(costs) - min(costs) <= 0.01 * max(costs)  # LPT: balanced shards

@@ -53,6 +53,12 @@ H264_CASES = [
     ("cavlc_high8x8_pcm", 128, 96, 8, 18, ["--cavlc", "1", "--pcm", "1"]),
     ("cavlc_q0_big_levels", 64, 64, 8, 0, ["--cavlc", "1"]),
     ("cavlc_10bit_slices", 128, 64, 10, 10, ["--cavlc", "1", "--slices", "2", "--cqp", "-3"]),
+    # scaling matrices (fall-back rules A / B), non-IDR I first picture, decoder delay (reordered P pictures)
+    ("sm_sps", 96, 64, 8, 24, ["--sm", "1"]),
+    ("sm_sps_pps", 128, 96, 8, 30, ["--sm", "2"]),
+    ("sm_pps_cavlc", 96, 64, 8, 20, ["--sm", "3", "--cavlc", "1"]),
+    ("nonidr_first", 96, 64, 8, 26, ["--nonidr", "1", "--slices", "2"]),
+    ("delay2", 96, 64, 8, 26, ["--delay", "2"]),
 ]
 
 
@@ -65,6 +71,15 @@ HEVC_CASES = [
     ("default", 96, 64, 8, 27, []),
     ("pcm_bypass_slices", 128, 96, 8, 22, ["--pcm", "1", "--bypass", "1", "--slices", "1"]),
     ("ctb16_10bit", 96, 64, 10, 12, ["--ctb", "16"]),
+    # scaling lists (7.3.4): SPS defaults, explicit SPS, explicit SPS + PPS, PPS over defaults
+    ("sl_sps_default", 96, 64, 8, 27, ["--sl", "1"]),
+    ("sl_sps_explicit", 128, 96, 8, 22, ["--sl", "2", "--depth", "2"]),
+    ("sl_sps_pps_tskip_10bit", 128, 64, 10, 17, ["--sl", "3", "--ctb", "32"]),
+    ("sl_pps_over_default_bypass", 96, 96, 8, 30, ["--sl", "4", "--bypass", "1", "--pcm", "1"]),
+    # CRA / BLA first picture, decoder delay (sps_max_num_reorder_pics, trailing all-skip P pictures)
+    ("cra_first_slices", 128, 96, 8, 27, ["--nut", "21", "--slices", "1"]),
+    ("bla_first_delay", 96, 64, 8, 27, ["--nut", "16", "--delay", "2"]),
+    ("delay1", 136, 72, 8, 30, ["--delay", "1"]),
 ]
 
 

@@ -1,0 +1,56 @@
+"""GPU: SURVEY.md §8 f3 wire-format edge cases and malformed parameter sets.
+
+f3 vectors (tests/golden/f3, tools/make_streams.py f3): decoder-delay streams (VUI
+max_num_reorder_frames / sps_max_num_reorder_pics > 0, then reordered all-skip P pictures)
+and leading non-IDR I / CRA / BLA pictures.  The reference returns false without output for
+the decoder-delay ones (/root/reference/src/Decoder.cpp:342-360: one packet sent, no flush,
+avcodec_receive_frame gives EAGAIN); this build transcodes picture 0 (INTEGRATION.md,
+"Documented differences") -- its planes and JPEG must equal the oracle's.
+
+Malformed vectors (tests/golden/malformed): cropping windows that leave no picture are ignored
+as FFmpeg ignores them (a JPEG of the whole coded picture, equal to the oracle's); the others
+fail cleanly with a per-picture message."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from annexb_variants import variants
+from conftest import golden, read
+
+pytestmark = pytest.mark.gpu
+
+F3 = json.load(open(golden("f3/manifest.json")))
+BAD = json.load(open(golden("malformed/manifest.json")))
+
+
+@pytest.mark.parametrize("e", F3, ids=[e["file"] for e in F3])
+def test_f3_picture0_planes_and_jpeg(engine, e):
+    s = read(golden("f3/" + e["file"]))
+    for stage, skip in ((1, True), (0, False)):
+        gy, gu, gv, bd = engine.decode(s, stage=stage)
+        oy, ou, ov, obd = O.decode(s, e["codec"], skip_loop_filter=skip)
+        assert bd == obd
+        for g, o, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
+            assert np.array_equal(g, o), f"stage {stage} {name}"
+    ref = O.transcode(s)
+    vs = variants(s, e["codec"])
+    outs = engine.transcode([s] + list(vs.values()))
+    assert outs[0] == ref
+    for (vname, _), o in zip(vs.items(), outs[1:]):
+        assert o == ref, vname
+
+
+def test_malformed_parameter_sets(engine):
+    streams = [read(golden("malformed/" + e["file"])) for e in BAD]
+    outs = engine.transcode(streams)
+    for i, (e, s, o) in enumerate(zip(BAD, streams, outs)):
+        if e["expect"] == "ok":
+            assert o is not None, (e["file"], engine.frame_error(i))
+            assert o == O.transcode(s), e["file"]
+            assert engine.frame_error(i) == ""
+        else:
+            assert o is None, e["file"]
+            assert engine.frame_error(i), e["file"]  # a per-picture message, not the engine-wide one

@@ -233,3 +233,75 @@ def test_jni_bytes_and_batch_with_stub_env(tmp_path):
     import oracle_py as O
     want = O.transcode(read(golden("img01.h264")))
     assert o1.read_bytes() == want and o2.read_bytes() == want and not o3.exists()
+
+
+MULTI_ENGINE_DRIVER = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include "h2j.h"
+/* argv: outdir in1 in2 ... -> h2j_h265_to_jpeg_batch over all inputs into outdir/o<i>.jpg */
+int main(int argc, char** argv) {
+    int n = argc - 2;
+    const char** in = (const char**)calloc(n, sizeof(char*));
+    const char** out = (const char**)calloc(n, sizeof(char*));
+    int* ok = (int*)calloc(n, sizeof(int));
+    for (int i = 0; i < n; i++) {
+        char* p = (char*)malloc(4096);
+        snprintf(p, 4096, "%s/o%d.jpg", argv[1], i);
+        in[i] = argv[2 + i];
+        out[i] = p;
+    }
+    int good = h2j_h265_to_jpeg_batch(in, out, n, ok);
+    printf("good=%d\n", good);
+    return 0;
+}
+'''
+
+
+@pytest.mark.parametrize("engines", ["2", "3"])
+def test_facade_splits_batches_over_engines(tmp_path, engines):
+    """The IDecoder / batch facade runs one engine per GPU (H2J_ENGINES overrides the count, so
+    a one-GPU box exercises the split): a batch is LPT-split over the idle engines and every
+    JPEG stays byte-exact; a malformed input fails alone, its LOG line carries its own message."""
+    import glob
+    import oracle_py as O
+    src = tmp_path / "me.c"
+    src.write_text(MULTI_ENGINE_DRIVER)
+    exe = tmp_path / "me"
+    subprocess.check_call(["gcc", "-O1", str(src), "-I", os.path.join(ROOT, "include"), "-L", PKG, "-lH265ToJpeg",
+                           f"-Wl,-rpath,{PKG}", "-o", str(exe)])
+    ins = sorted(glob.glob(golden("hevc/*.h265")))[:10] + sorted(glob.glob(golden("h264/*.h264")))[:10]
+    bad = golden("malformed/m_avc_firstmb_oob.h264")
+    ins.insert(7, bad)
+    env = dict(os.environ, H2J_ENGINES=engines)
+    r = subprocess.run([str(exe), str(tmp_path)] + ins, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert f"good={len(ins) - 1}" in r.stdout
+    assert "first_mb_in_slice outside the picture" in r.stdout
+    for i, p in enumerate(ins):
+        if p == bad:
+            assert not (tmp_path / f"o{i}.jpg").exists()
+        else:
+            assert (tmp_path / f"o{i}.jpg").read_bytes() == O.transcode(read(p)), p
+
+
+def test_concurrent_idecoder_calls_over_two_engines(tmp_path):
+    src = tmp_path / "conc.cpp"
+    src.write_text(CONCURRENT)
+    exe = tmp_path / "conc"
+    subprocess.check_call(["g++", "-std=c++11", "-O1", "-pthread", str(src), "-I", os.path.join(ROOT, "include"),
+                           "-L", PKG, "-lH265ToJpeg", f"-Wl,-rpath,{PKG}", "-o", str(exe)])
+    env = dict(os.environ, H2J_ENGINES="2")
+    r = subprocess.run([str(exe), golden("img01.h265"), golden("img01.h264"), str(tmp_path)], capture_output=True,
+                       text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    import oracle_py as O
+    want = [O.transcode(read(golden("img01.h265"))), O.transcode(read(golden("img01.h264")))]
+    for i in range(12):
+        assert (tmp_path / f"o{i}.jpg").read_bytes() == want[i % 2], i
+
+
+def test_engine_host_placement_reported(engine):
+    info = engine.host_info()
+    assert info["threads"] >= 1
+    assert info["pinned_cpus"] == 0 or info["pinned_cpus"] >= 1

@@ -17,6 +17,9 @@
  * usage: h264gen in.yuv W H bitdepth qp seed out.h264 [options]
  *   --t8x8 0|1 --pcm 0|1 --qpdelta 0|1 --slices N(MB rows, 0 = one)
  *   --alpha A --beta B (div2 offsets) --dbidc 0|1|2 --cqp N --cqp2 N --cavlc 0|1 --recon out.yuv
+ *   --sm 0..3 (scaling matrices, see write_matrices)
+ *   --nonidr 1 (first picture: non-IDR I, nal_unit_type 1)
+ *   --delay K (VUI max_num_reorder_frames = K, then K + 1 all-skip P pictures)
  */
 #include <math.h>
 #include <stdint.h>
@@ -172,7 +175,8 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb;
+    long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
     Mb *mb;
@@ -366,12 +370,18 @@ static int norm8(int m, int i, int j) {
 }
 static int sc4(int l, int ls, int qp) { return qp >= 24 ? (l * ls) << (qp / 6 - 4) : (l * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6); }
 static int sc8(int l, int ls, int qp) { return qp >= 36 ? (l * ls) << (qp / 6 - 6) : (l * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6); }
+/* conformance (8.5.12.1 / 8.5.13.1): scaled coefficients and transform intermediates fit
+ * -2^(7+bitDepth) .. 2^(7+bitDepth)-1 (FFmpeg stores them in int16 at 8-bit) */
+static int g_lim = 1 << 15, g_viol;
+static void range_check(int v) { if (v < -g_lim || v >= g_lim) g_viol = 1; }
 static void idct4(int *b) {
     int t[16];
+    for (int i = 0; i < 16; i++) range_check(b[i]);
     for (int i = 0; i < 4; i++) {
         int *r = b + i * 4, e0 = r[0] + r[2], e1 = r[0] - r[2], e2 = (r[1] >> 1) - r[3], e3 = r[1] + (r[3] >> 1);
         t[i * 4] = e0 + e3; t[i * 4 + 1] = e1 + e2; t[i * 4 + 2] = e1 - e2; t[i * 4 + 3] = e0 - e3;
     }
+    for (int i = 0; i < 16; i++) range_check(t[i]);
     for (int j = 0; j < 4; j++) {
         int f0 = t[j], f1 = t[4 + j], f2 = t[8 + j], f3 = t[12 + j];
         int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
@@ -388,24 +398,26 @@ static void idct8_1d(const int *d, int *o) {
 }
 static void idct8(int *b) {
     int t[64], col[8], o[8];
+    for (int i = 0; i < 64; i++) range_check(b[i]);
     for (int i = 0; i < 8; i++) idct8_1d(b + i * 8, t + i * 8);
+    for (int i = 0; i < 64; i++) range_check(t[i]);
     for (int j = 0; j < 8; j++) {
         for (int i = 0; i < 8; i++) col[i] = t[i * 8 + j];
         idct8_1d(col, o);
         for (int i = 0; i < 8; i++) b[i * 8 + j] = (o[i] + 32) >> 6;
     }
 }
-/* residual of a 4x4 / 8x8 block from raster levels */
-static void res4(const int *lv, int qp, int *r) {
-    for (int i = 0; i < 16; i++) r[i] = sc4(lv[i], 16 * norm4(qp % 6, i >> 2, i & 3), qp);
+/* residual of a 4x4 / 8x8 block from raster levels; w = raster weightScale (8.5.9) */
+static void res4(const int *lv, int qp, int *r, const int *w) {
+    for (int i = 0; i < 16; i++) r[i] = sc4(lv[i], w[i] * norm4(qp % 6, i >> 2, i & 3), qp);
     idct4(r);
 }
-static void res8(const int *lv, int qp, int *r) {
-    for (int i = 0; i < 64; i++) r[i] = sc8(lv[i], 16 * norm8(qp % 6, i >> 3, i & 7), qp);
+static void res8(const int *lv, int qp, int *r, const int *w) {
+    for (int i = 0; i < 64; i++) r[i] = sc8(lv[i], w[i] * norm8(qp % 6, i >> 3, i & 7), qp);
     idct8(r);
 }
 /* MB-wide residual for I16x16 (n = 16, luma) or chroma (n = 8): DC levels at (4i,4j) */
-static void res_dc(const int *lv, int n, int qp, int *r) {
+static void res_dc(const int *lv, int n, int qp, int *r, const int *w) {
     int nb = n / 4, dc[16];
     for (int r0 = 0; r0 < nb; r0++)
         for (int q = 0; q < nb; q++) {
@@ -416,14 +428,15 @@ static void res_dc(const int *lv, int n, int qp, int *r) {
                     int hc = nb == 4 ? ((q == 0 || (q == 1 && j < 2) || (q == 2 && (j == 0 || j == 3)) || (q == 3 && !(j & 1))) ? 1 : -1) : ((q == 0 || j == 0) ? 1 : -1);
                     acc += hr * hc * lv[(i * 4) * n + j * 4];
                 }
-            int ls0 = 16 * k_norm4[qp % 6][0];
+            int ls0 = w[0] * k_norm4[qp % 6][0];
             dc[r0 * nb + q] = nb == 4 ? (qp >= 36 ? (acc * ls0) << (qp / 6 - 6) : (acc * ls0 + (1 << (5 - qp / 6))) >> (6 - qp / 6))
                                       : ((acc * ls0) << (qp / 6)) >> 5;
+            range_check(dc[r0 * nb + q]);
         }
     for (int by = 0; by < nb; by++)
         for (int bx = 0; bx < nb; bx++) {
             int b[16];
-            for (int i = 0; i < 16; i++) b[i] = sc4(lv[(by * 4 + (i >> 2)) * n + bx * 4 + (i & 3)], 16 * norm4(qp % 6, i >> 2, i & 3), qp);
+            for (int i = 0; i < 16; i++) b[i] = sc4(lv[(by * 4 + (i >> 2)) * n + bx * 4 + (i & 3)], w[i] * norm4(qp % 6, i >> 2, i & 3), qp);
             b[0] = dc[by * nb + bx];
             idct4(b);
             for (int i = 0; i < 16; i++) r[(by * 4 + (i >> 2)) * n + bx * 4 + (i & 3)] = b[i];
@@ -432,9 +445,13 @@ static void res_dc(const int *lv, int n, int qp, int *r) {
 
 /* ------------------------------------------------------------ least-squares quantiser against the decoder basis */
 typedef struct { float *basis; int n, npos; } Basis; /* basis[pos][sample] for unit level */
-static Basis g_b4[64], g_b8[64], g_b16[64], g_bc[64];
+static Basis g_b4[64], g_b8[64], g_b16[64], g_bc[2][64];
 
-static void build_basis(Basis *B, int kind, int qp) {
+/* weightScale matrices in raster order (8.5.6 inverse zig-zag of the active scaling lists):
+ * [0..2] Intra Y / Cb / Cr 4x4, g_w8 Intra Y 8x8; flat 16 without scaling matrices */
+static int g_w4[3][16], g_w8[64];
+
+static void build_basis(Basis *B, int kind, int qp, const int *w) {
     int n = kind == 0 ? 4 : (kind == 1 ? 8 : (kind == 2 ? 16 : 8));
     if (B->basis) return;
     B->n = n;
@@ -445,9 +462,9 @@ static void build_basis(Basis *B, int kind, int qp) {
         int lv[256] = {0}, r[256];
         if ((kind == 2 || kind == 3) && 0) {}
         lv[p] = L;
-        if (kind == 0) res4(lv, qp, r);
-        else if (kind == 1) res8(lv, qp, r);
-        else res_dc(lv, n, qp, r);
+        if (kind == 0) res4(lv, qp, r, w);
+        else if (kind == 1) res8(lv, qp, r, w);
+        else res_dc(lv, n, qp, r, w);
         for (int i = 0; i < n * n; i++) B->basis[p * n * n + i] = (float)r[i] / L;
     }
 }
@@ -463,6 +480,18 @@ static void quantize(const Basis *B, const int *x, int *lv, int maxlev) {
         l = (int)(fabs(v) + 1.0 / 3.0);
         if (l > maxlev) l = maxlev;
         lv[p] = v < 0 ? -l : l;
+    }
+}
+/* shrink the levels of a block until its reconstruction stays in the conformant range */
+static void fit(int kind, int *lv, int qp, const int *w) {
+    int n = kind == 0 ? 4 : (kind == 1 ? 8 : (kind == 2 ? 16 : 8)), r[256];
+    for (;;) {
+        g_viol = 0;
+        if (kind == 0) res4(lv, qp, r, w);
+        else if (kind == 1) res8(lv, qp, r, w);
+        else res_dc(lv, n, qp, r, w);
+        if (!g_viol) return;
+        for (int i = 0; i < n * n; i++) lv[i] = lv[i] * 3 / 4;
     }
 }
 
@@ -673,8 +702,9 @@ static void encode_mb(G *g) {
         pred16(g, mode16, pred);
         for (int i = 0; i < 256; i++) src[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
         Basis *Bs = &g_b16[qpl];
-        build_basis(Bs, 2, qpl);
+        build_basis(Bs, 2, qpl, g_w4[0]);
         quantize(Bs, src, lv16, maxlev);
+        fit(2, lv16, qpl, g_w4[0]);
     }
     /* chroma mode + levels need the chroma QP of the final QP */
     int at = B != NULL, al = A != NULL, ad = nb(g, -1, -1) != NULL;
@@ -688,9 +718,10 @@ static void encode_mb(G *g) {
         predc(g, 1 + c, cpm, predc_[c]);
         int x[64];
         for (int i = 0; i < 64; i++) x[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
-        Basis *Bs = &g_bc[qpc[c]];
-        build_basis(Bs, 3, qpc[c]);
+        Basis *Bs = &g_bc[c][qpc[c]];
+        build_basis(Bs, 3, qpc[c], g_w4[1 + c]);
         quantize(Bs, x, lvc[c], maxlev);
+        fit(3, lvc[c], qpc[c], g_w4[1 + c]);
         if (rndn(5) == 0) for (int i = 0; i < 64; i++) if ((i & 3) || (i >> 3) & 3) lvc[c][i] = 0; /* DC-only chroma */
     }
     int chroma_dc = 0, chroma_ac = 0;
@@ -774,10 +805,11 @@ static void encode_mb(G *g) {
             int x[64], rr[64];
             for (int k = 0; k < n * n; k++) x[k] = g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k];
             Basis *Bs = t8 ? &g_b8[qpl] : &g_b4[qpl];
-            build_basis(Bs, t8 ? 1 : 0, qpl);
+            build_basis(Bs, t8 ? 1 : 0, qpl, t8 ? g_w8 : g_w4[0]);
             int *lv = t8 ? lv8[i] : lv4[blk];
             quantize(Bs, x, lv, maxlev);
-            if (t8) res8(lv, qpl, rr); else res4(lv, qpl, rr);
+            fit(t8 ? 1 : 0, lv, qpl, t8 ? g_w8 : g_w4[0]);
+            if (t8) res8(lv, qpl, rr, g_w8); else res4(lv, qpl, rr, g_w4[0]);
             put(g, 0, gx + bx, gy + by, n, p, rr);
         }
     }
@@ -902,17 +934,79 @@ static void encode_mb(G *g) {
     }
     /* reconstruction of I16x16 luma and chroma */
     if (is16) {
-        res_dc(lv16, 16, qpl, r);
+        res_dc(lv16, 16, qpl, r, g_w4[0]);
         pred16(g, mode16, pred);
         put(g, 0, gx, gy, 16, pred, r);
     }
     for (int c = 0; c < 2; c++) {
         int rr[64];
-        res_dc(lvc[c], 8, qpc[c], rr);
+        res_dc(lvc[c], 8, qpc[c], rr, g_w4[1 + c]);
         put(g, 1 + c, gx / 2, gy / 2, 8, predc_[c], rr);
     }
     if (!is16) for (int i = 0; i < 16; i++) if (t8) {} /* ipm already set */
     if (is16) for (int i = 0; i < 16; i++) m->ipm[i] = 2;
+}
+
+/* ------------------------------------------------------------ scaling matrices (7.3.2.1.1.1) */
+/* --sm: 0 none; 1 SPS matrices (fall-back rule A); 2 SPS matrices + PPS matrices (fall-back
+ * rule B); 3 PPS matrices only (fall-back rule A in the PPS).  Each list is, at random: not
+ * present (fall-back), useDefaultScalingMatrixFlag (first delta gives 0), or DPCM-coded values,
+ * sometimes ended early by a 0 (the rest repeats the last value). */
+static const uint8_t k_def4[2][16] = {{6, 13, 13, 20, 20, 20, 28, 28, 28, 28, 32, 32, 32, 37, 37, 42},
+                                      {10, 14, 14, 20, 20, 20, 24, 24, 24, 24, 27, 27, 27, 30, 30, 34}};
+static const uint8_t k_def8[2][64] = {
+    {6,  10, 10, 13, 11, 13, 16, 16, 16, 16, 18, 18, 18, 18, 18, 23, 23, 23, 23, 23, 23, 25,
+     25, 25, 25, 25, 25, 25, 27, 27, 27, 27, 27, 27, 27, 27, 29, 29, 29, 29, 29, 29, 29, 31,
+     31, 31, 31, 31, 31, 33, 33, 33, 33, 33, 36, 36, 36, 36, 38, 38, 38, 40, 40, 42},
+    {9,  13, 13, 15, 13, 15, 17, 17, 17, 17, 19, 19, 19, 19, 19, 21, 21, 21, 21, 21, 21, 22,
+     22, 22, 22, 22, 22, 22, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 27,
+     27, 27, 27, 27, 27, 28, 28, 28, 28, 28, 30, 30, 30, 30, 32, 32, 32, 33, 33, 35}};
+typedef struct { uint8_t l4[6][16], l8[2][64]; } Mat; /* scan (zig-zag) order */
+static Mat g_sps_m, g_pps_m;
+static int g_sps_m_on;
+
+static void write_list(BW *b, uint8_t *list, int n, const uint8_t *def) {
+    int r = rndn(8);
+    if (r == 0) { bw_se(b, -8); memcpy(list, def, (size_t)n); return; } /* useDefaultScalingMatrixFlag */
+    const int wild = r == 1, base = 6 + rndn(24), slope = rndn(4), stop = rndn(3) == 0 ? 1 + rndn(n - 1) : n;
+    int last = 8;
+    for (int j = 0; j < n; j++) {
+        if (j == stop) { /* nextScale 0: the rest repeats lastScale */
+            int d = -last;
+            if (d < -128) d += 256;
+            bw_se(b, d);
+            for (; j < n; j++) list[j] = (uint8_t)last;
+            return;
+        }
+        int v = wild ? 1 + rndn(255) : clip3(1, 255, base + slope * j * (n == 16 ? 2 : 1) / 2 + rndn(5) - 2);
+        int d = v - last;
+        if (d > 127) d -= 256;
+        if (d < -128) d += 256;
+        bw_se(b, d);
+        list[j] = (uint8_t)v;
+        last = v;
+    }
+}
+/* scaling lists 0..5 (4x4) and 6..6+n8-1 (8x8); fb = fall-back rule B source (NULL: rule A) */
+static void write_matrices(BW *b, Mat *M, const Mat *fb, int n8) {
+    for (int i = 0; i < 6; i++) {
+        int pres = rndn(3) != 0;
+        bw_put(b, (uint32_t)pres, 1);
+        if (pres) write_list(b, M->l4[i], 16, k_def4[i >= 3]);
+        else if (i == 0 || i == 3) memcpy(M->l4[i], fb ? fb->l4[i] : k_def4[i >= 3], 16);
+        else memcpy(M->l4[i], M->l4[i - 1], 16);
+    }
+    for (int i = 0; i < n8; i++) {
+        int pres = rndn(3) != 0;
+        bw_put(b, (uint32_t)pres, 1);
+        if (pres) write_list(b, M->l8[i], 64, k_def8[i]);
+        else memcpy(M->l8[i], fb ? fb->l8[i] : k_def8[i], 64);
+    }
+}
+static void set_weights(const Mat *M) {
+    for (int c = 0; c < 3; c++)
+        for (int k = 0; k < 16; k++) g_w4[c][k_zz4[k]] = M ? M->l4[c][k] : 16;
+    for (int k = 0; k < 64; k++) g_w8[k_zz8[k]] = M ? M->l8[0][k] : 16;
 }
 
 /* ------------------------------------------------------------ parameter sets */
@@ -926,8 +1020,11 @@ static void write_sps(FILE *f, G *g, int profile) {
         bw_ue(&b, 1);
         bw_ue(&b, (uint32_t)(g->bd - 8)); bw_ue(&b, (uint32_t)(g->bd - 8));
         bw_put(&b, 0, 1); /* transform bypass */
-        bw_put(&b, 0, 1); /* seq scaling matrix */
+        g_sps_m_on = g->sm == 1 || g->sm == 2;
+        bw_put(&b, (uint32_t)g_sps_m_on, 1); /* seq_scaling_matrix_present_flag */
+        if (g_sps_m_on) write_matrices(&b, &g_sps_m, NULL, 2);
     }
+    set_weights(g_sps_m_on ? &g_sps_m : NULL);
     bw_ue(&b, 0);     /* log2_max_frame_num - 4 */
     bw_ue(&b, 0);     /* poc type 0 */
     bw_ue(&b, 0);     /* log2_max_poc_lsb - 4 */
@@ -938,17 +1035,30 @@ static void write_sps(FILE *f, G *g, int profile) {
     bw_put(&b, 1, 1); /* frame_mbs_only */
     bw_put(&b, 1, 1); /* direct_8x8_inference */
     int crop = g->outW != g->W || g->outH != g->H;
-    bw_put(&b, (uint32_t)crop, 1);
-    if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / 2); }
-    bw_put(&b, 0, 1); /* vui */
+    if (g->rawcrop[0] >= 0) { /* --crop l,r,t,b: raw frame_crop offsets (malformed-SPS vectors) */
+        bw_put(&b, 1, 1);
+        for (int i = 0; i < 4; i++) bw_ue(&b, (uint32_t)g->rawcrop[i]);
+    } else {
+        bw_put(&b, (uint32_t)crop, 1);
+        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / 2); }
+    }
+    bw_put(&b, g->delay > 0, 1); /* vui_parameters_present_flag */
+    if (g->delay) { /* E.1.1: only bitstream_restriction, carrying the reorder depth */
+        bw_put(&b, 0, 8);       /* aspect, overscan, video signal, chroma loc, timing, nal/vcl hrd, pic_struct */
+        bw_put(&b, 1, 1);       /* bitstream_restriction_flag */
+        bw_put(&b, 1, 1);       /* motion_vectors_over_pic_boundaries_flag */
+        bw_ue(&b, 0); bw_ue(&b, 0); bw_ue(&b, 15); bw_ue(&b, 15);
+        bw_ue(&b, (uint32_t)g->delay);     /* max_num_reorder_frames */
+        bw_ue(&b, (uint32_t)g->delay + 1); /* max_dec_frame_buffering */
+    }
     bw_trailing(&b);
     write_nal(f, 3, 7, b.buf, b.n);
     free(b.buf);
 }
-static void write_pps(FILE *f, G *g, int high) {
+static void write_pps(FILE *f, G *g, int high, int id) {
     BW b; bw_init(&b);
-    bw_ue(&b, 0); bw_ue(&b, 0);
-    bw_put(&b, (uint32_t)!g->cavlc, 1); /* entropy_coding_mode_flag */
+    bw_ue(&b, (uint32_t)id); bw_ue(&b, 0);
+    bw_put(&b, (uint32_t)(!g->cavlc && id == 0), 1); /* entropy_coding_mode_flag (PPS 1: CAVLC skip pictures) */
     bw_put(&b, 0, 1);
     bw_ue(&b, 0);     /* slice groups */
     bw_ue(&b, 0); bw_ue(&b, 0);
@@ -961,7 +1071,14 @@ static void write_pps(FILE *f, G *g, int high) {
     bw_put(&b, 0, 1); /* redundant pic cnt */
     if (high) {
         bw_put(&b, (uint32_t)g->t8x8, 1);
-        bw_put(&b, 0, 1);
+        int pm = g->sm >= 2;
+        bw_put(&b, (uint32_t)pm, 1); /* pic_scaling_matrix_present_flag */
+        if (pm) {
+            g_pps_m = g_sps_m; /* 8x8 lists stay the SPS ones without transform_8x8_mode */
+            if (!g_sps_m_on) for (int i = 0; i < 2; i++) memset(g_pps_m.l8[i], 16, 64);
+            write_matrices(&b, &g_pps_m, g_sps_m_on ? &g_sps_m : NULL, g->t8x8 ? 2 : 0);
+            set_weights(&g_pps_m);
+        }
         bw_se(&b, g->cqp2);
     }
     bw_trailing(&b);
@@ -987,7 +1104,16 @@ int main(int argc, char **argv) {
     g->cqp = opt_int(argc, argv, "--cqp", 0);
     g->cqp2 = opt_int(argc, argv, "--cqp2", g->cqp);
     g->cavlc = opt_int(argc, argv, "--cavlc", 0);
-    int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp ? 100 : 77));
+    g->sm = opt_int(argc, argv, "--sm", 0);
+    g->nonidr = opt_int(argc, argv, "--nonidr", 0);
+    g->delay = opt_int(argc, argv, "--delay", 0);
+    g->firstmb = opt_int(argc, argv, "--firstmb", -1);
+    g->rawcrop[0] = -1;
+    if (opt_str(argc, argv, "--crop"))
+        sscanf(opt_str(argc, argv, "--crop"), "%lld,%lld,%lld,%lld", &g->rawcrop[0], &g->rawcrop[1], &g->rawcrop[2], &g->rawcrop[3]);
+    if (g->delay > 6) { fprintf(stderr, "--delay <= 6 (4-bit POC lsb)\n"); return 2; }
+    int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm ? 100 : 77));
+    g_lim = 1 << (7 + g->bd);
     g->W = (g->outW + 15) & ~15; g->H = (g->outH + 15) & ~15;
     g->mbw = g->W / 16; g->mbh = g->H / 16;
     FILE *fi = fopen(argv[1], "rb");
@@ -1008,18 +1134,20 @@ int main(int argc, char **argv) {
     for (int i = 0; i < g->mbw * g->mbh; i++) g->mb[i].slice = -1;
     FILE *fo = fopen(argv[7], "wb");
     write_sps(fo, g, profile);
-    write_pps(fo, g, profile >= 100);
+    write_pps(fo, g, profile >= 100, 0);
+    if (g->delay) write_pps(fo, g, 0, 1);
     int rows = g->slice_rows > 0 ? g->slice_rows : g->mbh;
     int nslice = 0;
     for (int r0 = 0; r0 < g->mbh; r0 += rows, nslice++) {
         BW b; bw_init(&b);
-        bw_ue(&b, (uint32_t)(r0 * g->mbw)); /* first_mb */
+        bw_ue(&b, (uint32_t)(r0 == 0 && g->firstmb >= 0 ? g->firstmb : r0 * g->mbw)); /* first_mb (--firstmb: malformed) */
         bw_ue(&b, 7);                         /* I (all slices I) */
         bw_ue(&b, 0);                         /* pps */
         bw_put(&b, 0, 4);                     /* frame_num */
-        bw_ue(&b, 0);                         /* idr_pic_id */
+        if (!g->nonidr) bw_ue(&b, 0);         /* idr_pic_id */
         bw_put(&b, 0, 4);                     /* poc lsb */
-        bw_put(&b, 0, 1); bw_put(&b, 0, 1);   /* dec_ref_pic_marking (IDR) */
+        if (!g->nonidr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } /* dec_ref_pic_marking (IDR) */
+        else bw_put(&b, 0, 1);                /* adaptive_ref_pic_marking_mode_flag */
         int sqp = clip3(-6 * (g->bd - 8), 51, g->qp + (nslice ? rndn(5) - 2 : 0));
         bw_se(&b, sqp - 26);
         int idc = g->dbidc;
@@ -1046,7 +1174,26 @@ int main(int argc, char **argv) {
         if (!g->cavlc) ce_finish(&g->ce);
         bw_put(&b, 1, 1);
         bw_align_zero(&b);
-        write_nal(fo, 3, 5, b.buf, b.n);
+        write_nal(fo, 3, g->nonidr ? 1 : 5, b.buf, b.n);
+        free(b.buf);
+    }
+    /* decoder delay: delay + 1 all-skip P pictures (CAVLC, PPS 1), output order != decoding order:
+     * frame_num 1, 2, ..., POC 2(delay+1), 2, 4, ... */
+    for (int k = 1; g->delay && k <= g->delay + 1; k++) {
+        BW b; bw_init(&b);
+        bw_ue(&b, 0);                                   /* first_mb_in_slice */
+        bw_ue(&b, 5);                                   /* P (all slices) */
+        bw_ue(&b, 1);                                   /* pps 1 */
+        bw_put(&b, (uint32_t)k, 4);                     /* frame_num */
+        bw_put(&b, (uint32_t)(k == 1 ? 2 * (g->delay + 1) : 2 * (k - 1)), 4); /* poc lsb */
+        bw_put(&b, 0, 1);                               /* num_ref_idx_active_override_flag */
+        bw_put(&b, 0, 1);                               /* ref_pic_list_modification_flag_l0 */
+        bw_put(&b, 0, 1);                               /* adaptive_ref_pic_marking_mode_flag */
+        bw_se(&b, 0);                                   /* slice_qp_delta */
+        bw_ue(&b, 0); bw_se(&b, 0); bw_se(&b, 0);       /* deblocking */
+        bw_ue(&b, (uint32_t)(g->mbw * g->mbh));         /* mb_skip_run: the whole picture */
+        bw_trailing(&b);
+        write_nal(fo, 2, 1, b.buf, b.n);
         free(b.buf);
     }
     fclose(fo);

@@ -20,6 +20,7 @@
  *            --bypass 0|1 --slices N(ctb rows per slice, 0=one)
  *            --depth D (max_transform_hierarchy_depth_intra) --ctb 16|32|64
  *            --beta B --tc T --recon out.yuv --cbqp N --crqp N
+ *            --sl 0..4 (scaling lists, see write_scaling_list_data)
  */
 #include <math.h>
 #include <stdint.h>
@@ -207,6 +208,11 @@ typedef struct {
     int tile_cols, tile_rows, lf_tiles; /* uniform tile grid (1 x 1 = no tiles) */
     int strong;
     int log2maxtb;
+    int sl; /* scaling-list mode (--sl) */
+    int nut;   /* NAL unit type of the (intra) first picture: 19 IDR_W_RADL, 21 CRA, 16 BLA_W_LP */
+    int delay; /* sps_max_num_reorder_pics; the stream then carries delay + 1 all-skip P pictures */
+    long long rawconf[4]; /* --conf: raw conformance window offsets (-1: derived from the size) */
+    int wdelta;           /* --wdelta: subtracted from the signalled picture width */
 } Opt;
 
 typedef struct {
@@ -638,6 +644,97 @@ static void sdh_fix(G *g, int *coef, int log2n, int c, int pred_mode) {
     }
 }
 
+/* ------------------------------------------------------------ scaling lists (7.3.4, 7.4.5) */
+/* --sl: 0 off; 1 scaling_list_enabled with the default lists (no data in SPS or PPS);
+ * 2 explicit SPS lists; 3 explicit SPS lists overridden by explicit PPS lists; 4 default SPS
+ * lists overridden by explicit PPS lists.  Explicit lists mix the three ways of coding each
+ * (sizeId, matrixId): pred_mode 0 with delta 0 (default list), pred_mode 0 with a
+ * scaling_list_pred_matrix_id_delta copy of an earlier matrix (DC included), and DPCM-coded
+ * values (with scaling_list_dc_coef_minus8 for 16x16 / 32x32). */
+typedef struct { uint8_t sl[4][6][64]; uint8_t dc[4][6]; } SList; /* sl in up-right diagonal order */
+static const uint8_t k_sl_def_intra[64] = {
+    16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 16, 17, 16, 17, 18, 17, 18, 18, 17, 18, 21,
+    19, 20, 21, 20, 19, 21, 24, 22, 22, 24, 24, 22, 22, 24, 25, 25, 27, 30, 27, 25, 25, 29,
+    31, 35, 35, 31, 29, 36, 41, 44, 41, 36, 47, 54, 54, 47, 65, 70, 65, 88, 88, 115};
+static const uint8_t k_sl_def_inter[64] = {
+    16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17, 18, 18, 18, 18, 18, 18, 20,
+    20, 20, 20, 20, 20, 20, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 28,
+    28, 28, 28, 28, 28, 33, 33, 33, 33, 33, 41, 41, 41, 41, 54, 54, 54, 71, 71, 91};
+static int g_sl_on;                 /* scaling_list_enabled_flag */
+static uint16_t g_sf[4][3][1024];   /* ScalingFactor m[x][y] (raster y*n+x) per sizeId, cIdx (intra) */
+
+static void sl_default(SList *L) {
+    for (int m = 0; m < 6; m++) {
+        memset(L->sl[0][m], 16, 16);
+        L->dc[0][m] = 16;
+        for (int s = 1; s < 4; s++) {
+            memcpy(L->sl[s][m], m < 3 ? k_sl_def_intra : k_sl_def_inter, 64);
+            L->dc[s][m] = 16;
+        }
+    }
+}
+
+/* scaling_list_data(): random lists, written and applied to L */
+static void write_scaling_list_data(BW *b, SList *L) {
+    sl_default(L);
+    for (int sizeId = 0; sizeId < 4; sizeId++) {
+        const int step = sizeId == 3 ? 3 : 1, n = sizeId ? 64 : 16;
+        for (int m = 0; m < 6; m += step) {
+            int how = rndn(5); /* 0 default, 1 copy, else explicit */
+            if (how == 1 && m < step) how = 2;
+            if (how <= 1) {
+                bw_put(b, 0, 1);
+                if (how == 0) { bw_ue(b, 0); continue; } /* default (already in L) */
+                int delta = 1 + rndn(m / step);
+                bw_ue(b, (uint32_t)delta);
+                int ref = m - delta * step;
+                memcpy(L->sl[sizeId][m], L->sl[sizeId][ref], (size_t)n);
+                L->dc[sizeId][m] = L->dc[sizeId][ref];
+                continue;
+            }
+            bw_put(b, 1, 1);
+            int next = 8;
+            if (sizeId > 1) {
+                int dcv = 1 + rndn(rndn(6) == 0 ? 255 : 40);
+                bw_se(b, dcv - 8);
+                next = dcv;
+                L->dc[sizeId][m] = (uint8_t)dcv;
+            }
+            /* smooth, frequency-increasing lists with jitter; now and then a wild one */
+            const int wild = rndn(6) == 0, base = 6 + rndn(20), slope = rndn(6);
+            for (int i = 0; i < n; i++) {
+                int x = scan_diag[sizeId ? 3 : 2][i][0], y = scan_diag[sizeId ? 3 : 2][i][1];
+                int v = wild ? 1 + rndn(255) : clip3(1, 255, base + slope * (x + y) * (sizeId ? 1 : 2) + rndn(5) - 2);
+                int d = v - next;
+                if (d > 127) d -= 256;
+                if (d < -128) d += 256;
+                bw_se(b, d);
+                next = v;
+                L->sl[sizeId][m][i] = (uint8_t)v;
+            }
+        }
+    }
+}
+
+/* ScalingFactor (7.4.5) of the active lists, intra matrices (matrixId = cIdx) */
+static void sl_expand(const SList *L) {
+    for (int sizeId = 0; sizeId < 4; sizeId++) {
+        const int n = 4 << sizeId;
+        for (int c = 0; c < 3; c++) {
+            if (sizeId == 3 && c) break; /* no 32x32 chroma TBs in 4:2:0 */
+            for (int i = 0; i < (sizeId ? 64 : 16); i++) {
+                int x = scan_diag[sizeId ? 3 : 2][i][0], y = scan_diag[sizeId ? 3 : 2][i][1];
+                int r = sizeId <= 1 ? 1 : (sizeId == 2 ? 2 : 4);
+                for (int yy = 0; yy < r; yy++)
+                    for (int xx = 0; xx < r; xx++) g_sf[sizeId][c][(y * r + yy) * n + x * r + xx] = L->sl[sizeId][c][i];
+            }
+            if (sizeId >= 2) g_sf[sizeId][c][0] = L->dc[sizeId][c];
+        }
+    }
+}
+/* m[x][y] of a TB (8.6.4.2); 16 when scaling lists are off */
+static int sf(int c, int log2n, int i) { return g_sl_on ? g_sf[log2n - 2][c][i] : 16; }
+
 /* ------------------------------------------------------------ quant / recon of one TB */
 static const int k_qscale[6] = {26214, 23302, 20560, 18396, 16384, 14564};
 static const int k_ls[6] = {40, 45, 51, 57, 64, 72};
@@ -668,7 +765,7 @@ static int code_block(G *g, int c, int x0, int y0, int log2n, int pred_mode, int
         long add = (171L << (qbits - 9));
         for (int i = 0; i < n * n; i++) {
             long a = labs((long)tc[i]);
-            int l = (int)((a * k_qscale[qp % 6] + add) >> qbits);
+            int l = (int)((a * k_qscale[qp % 6] * 16 / sf(c, log2n, i) + add) >> qbits);
             if (l > 32767) l = 32767;
             coef[i] = tc[i] < 0 ? -l : l;
             nz |= l != 0;
@@ -690,7 +787,7 @@ static void recon_block(G *g, int c, int x0, int y0, int log2n, int qp, const in
             int d[1024];
             int bdShift = bd + log2n - 5;
             for (int i = 0; i < n * n; i++) {
-                long v = (long)coef[i] * 16 * k_ls[qp % 6];
+                long v = (long)coef[i] * sf(c, log2n, i) * k_ls[qp % 6];
                 v = (v << (qp / 6)) + (1L << (bdShift - 1));
                 v >>= bdShift;
                 d[i] = (int)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
@@ -1106,13 +1203,13 @@ static void ptl(BW *b, int bd) {
     bw_put(b, 123, 8); /* level 4.1 */
 }
 
-static void write_vps(FILE *f, int bd) {
+static void write_vps(FILE *f, int bd, int delay) {
     BW b; bw_init(&b);
     bw_put(&b, 0, 4); bw_put(&b, 1, 1); bw_put(&b, 1, 1); bw_put(&b, 0, 6); bw_put(&b, 0, 3); bw_put(&b, 1, 1);
     bw_put(&b, 0xffff, 16);
     ptl(&b, bd);
     bw_put(&b, 0, 1); /* sub layer ordering info present */
-    bw_ue(&b, 0); bw_ue(&b, 0); bw_ue(&b, 0);
+    bw_ue(&b, (uint32_t)(delay ? delay + 1 : 0)); bw_ue(&b, (uint32_t)delay); bw_ue(&b, 0); /* dpb size, reorder, latency */
     bw_put(&b, 0, 6); bw_ue(&b, 0); bw_put(&b, 0, 1); bw_put(&b, 0, 1);
     bw_trailing(&b);
     write_nal(f, 32, b.buf, b.n);
@@ -1125,21 +1222,34 @@ static void write_sps(FILE *f, const Opt *o) {
     ptl(&b, o->bd);
     bw_ue(&b, 0);          /* sps id */
     bw_ue(&b, 1);          /* 4:2:0 */
-    bw_ue(&b, (uint32_t)o->CW);
+    bw_ue(&b, (uint32_t)(o->CW - o->wdelta)); /* --wdelta: malformed (not a MinCbSize multiple) */
     bw_ue(&b, (uint32_t)o->CH);
     int crop = o->CW != o->outW || o->CH != o->outH;
-    bw_put(&b, (uint32_t)crop, 1);
-    if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(o->CW - o->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(o->CH - o->outH) / 2); }
+    if (o->rawconf[0] >= 0) { /* --conf l,r,t,b: raw conformance_window offsets (malformed-SPS vectors) */
+        bw_put(&b, 1, 1);
+        for (int i = 0; i < 4; i++) bw_ue(&b, (uint32_t)o->rawconf[i]);
+    } else {
+        bw_put(&b, (uint32_t)crop, 1);
+        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(o->CW - o->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(o->CH - o->outH) / 2); }
+    }
     bw_ue(&b, (uint32_t)(o->bd - 8)); bw_ue(&b, (uint32_t)(o->bd - 8));
     bw_ue(&b, 4);          /* log2_max_poc_lsb - 4 */
-    bw_put(&b, 0, 1); bw_ue(&b, 0); bw_ue(&b, 0); bw_ue(&b, 0);
+    bw_put(&b, 0, 1);      /* sub layer ordering info present */
+    bw_ue(&b, (uint32_t)(o->delay ? o->delay + 1 : 0)); bw_ue(&b, (uint32_t)o->delay); bw_ue(&b, 0);
     bw_ue(&b, 0);          /* log2 min cb - 3 */
     bw_ue(&b, (uint32_t)(o->log2ctb - 3));
     bw_ue(&b, 0);          /* log2 min tb - 2 */
     bw_ue(&b, (uint32_t)(o->log2maxtb - 2)); /* max tb */
     bw_ue(&b, 0);          /* depth inter */
     bw_ue(&b, (uint32_t)o->depth);
-    bw_put(&b, 0, 1);      /* scaling list */
+    bw_put(&b, o->sl != 0, 1); /* scaling_list_enabled_flag */
+    if (o->sl) {
+        static SList L;
+        bw_put(&b, o->sl == 2 || o->sl == 3, 1); /* sps_scaling_list_data_present_flag */
+        if (o->sl == 2 || o->sl == 3) write_scaling_list_data(&b, &L);
+        else sl_default(&L);
+        sl_expand(&L);
+    }
     bw_put(&b, 0, 1);      /* amp */
     bw_put(&b, (uint32_t)o->sao, 1);
     bw_put(&b, (uint32_t)o->pcm, 1);
@@ -1186,10 +1296,81 @@ static void write_pps(FILE *f, const Opt *o) {
     int dfc = o->beta != 0 || o->tc != 0;
     bw_put(&b, (uint32_t)dfc, 1);
     if (dfc) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); bw_se(&b, o->beta); bw_se(&b, o->tc); }
-    bw_put(&b, 0, 1);  /* pps scaling list */
+    bw_put(&b, o->sl >= 3, 1); /* pps_scaling_list_data_present_flag */
+    if (o->sl >= 3) {
+        static SList L;
+        write_scaling_list_data(&b, &L);
+        sl_expand(&L); /* the PPS lists replace the SPS lists */
+    }
     bw_put(&b, 0, 1); bw_ue(&b, 0); bw_put(&b, 0, 1); bw_put(&b, 0, 1);
     bw_trailing(&b);
     write_nal(f, 34, b.buf, b.n);
+    free(b.buf);
+}
+
+/* ------------------------------------------------------------ all-skip P picture (--delay) */
+/* One P slice (TRAIL_R) whose CUs are all cu_skip_flag = 1 with MaxNumMergeCand = 1, so the
+ * slice data is split_cu_flag / cu_skip_flag / end_of_slice_segment_flag bins only (initType 1
+ * contexts, Tables 9-11 / 9-13).  Its short-term RPS references the first picture. */
+static void skip_quadtree(G *g, uint8_t *ctx, int x0, int y0, int log2cb, int depth) {
+    const int n = 1 << log2cb;
+    int split;
+    if (x0 + n <= g->o.CW && y0 + n <= g->o.CH && log2cb > 3) {
+        int inc = (x0 > 0 && g->ctd[(y0 >> 2) * g->mw + ((x0 - 1) >> 2)] > depth) +
+                  (y0 > 0 && g->ctd[((y0 - 1) >> 2) * g->mw + (x0 >> 2)] > depth);
+        split = 0;
+        ce_bin(&g->ce, &ctx[inc], split);
+    } else {
+        split = log2cb > 3;
+    }
+    if (split) {
+        int h = n >> 1;
+        skip_quadtree(g, ctx, x0, y0, log2cb - 1, depth + 1);
+        if (x0 + h < g->o.CW) skip_quadtree(g, ctx, x0 + h, y0, log2cb - 1, depth + 1);
+        if (y0 + h < g->o.CH) skip_quadtree(g, ctx, x0, y0 + h, log2cb - 1, depth + 1);
+        if (x0 + h < g->o.CW && y0 + h < g->o.CH) skip_quadtree(g, ctx, x0 + h, y0 + h, log2cb - 1, depth + 1);
+        return;
+    }
+    set_map(g, g->ctd, x0, y0, n, (uint8_t)depth);
+    ce_bin(&g->ce, &ctx[3 + (x0 > 0) + (y0 > 0)], 1); /* cu_skip_flag: both neighbours skipped */
+}
+
+static void write_skip_picture(G *g, FILE *fo, int poc) {
+    static const uint8_t init[6] = {107, 139, 126, 197, 185, 201}; /* split_cu_flag, cu_skip_flag (initType 1) */
+    uint8_t ctx[6];
+    const int qp = g->o.qp;
+    for (int i = 0; i < 6; i++) {
+        int m = (init[i] >> 4) * 5 - 45, nn = ((init[i] & 15) << 3) - 16;
+        int pre = clip3(1, 126, ((m * clip3(0, 51, qp)) >> 4) + nn), mps = pre <= 63 ? 0 : 1;
+        ctx[i] = (uint8_t)(((mps ? pre - 64 : 63 - pre) << 1) | mps);
+    }
+    BW b; bw_init(&b);
+    bw_put(&b, 1, 1);  /* first_slice_segment_in_pic_flag */
+    bw_ue(&b, 0);      /* pps id */
+    bw_ue(&b, 1);      /* P */
+    bw_put(&b, (uint32_t)poc, 8);
+    bw_put(&b, 0, 1);  /* short_term_ref_pic_set_sps_flag */
+    bw_ue(&b, 1); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(poc - 1)); bw_put(&b, 1, 1); /* {POC 0}, used */
+    if (g->o.sao) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); }
+    bw_put(&b, 0, 1);  /* num_ref_idx_active_override_flag */
+    bw_ue(&b, 4);      /* five_minus_max_num_merge_cand */
+    bw_se(&b, qp - 26);
+    bw_put(&b, 1, 1);  /* slice_loop_filter_across_slices_enabled_flag */
+    if (g->o.wpp || g->o.tile_cols > 1 || g->o.tile_rows > 1) { fprintf(stderr, "--delay needs one substream\n"); exit(2); }
+    bw_put(&b, 1, 1);  /* byte_alignment */
+    bw_align_zero(&b);
+    memset(g->ctd, 0, (size_t)g->mw * g->mh);
+    ce_start(&g->ce, &b);
+    const int nctb = g->ctbW * g->ctbH;
+    for (int rs = 0; rs < nctb; rs++) {
+        if (g->o.bypass) { fprintf(stderr, "--delay without --bypass\n"); exit(2); }
+        skip_quadtree(g, ctx, (rs % g->ctbW) << g->o.log2ctb, (rs / g->ctbW) << g->o.log2ctb, g->o.log2ctb, 0);
+        ce_term(&g->ce, rs == nctb - 1);
+    }
+    ce_finish(&g->ce);
+    bw_put(&b, 1, 1);
+    bw_align_zero(&b);
+    write_nal(fo, 1, b.buf, b.n); /* TRAIL_R */
     free(b.buf);
 }
 
@@ -1234,6 +1415,14 @@ int main(int argc, char **argv) {
     o->tile_cols = opt_int(argc, argv, "--tilecols", 1);
     o->tile_rows = opt_int(argc, argv, "--tilerows", 1);
     o->lf_tiles = opt_int(argc, argv, "--lftiles", 1);
+    o->sl = opt_int(argc, argv, "--sl", 0);
+    o->nut = opt_int(argc, argv, "--nut", 19);
+    o->delay = opt_int(argc, argv, "--delay", 0);
+    o->wdelta = opt_int(argc, argv, "--wdelta", 0);
+    o->rawconf[0] = -1;
+    if (opt_str(argc, argv, "--conf"))
+        sscanf(opt_str(argc, argv, "--conf"), "%lld,%lld,%lld,%lld", &o->rawconf[0], &o->rawconf[1], &o->rawconf[2], &o->rawconf[3]);
+    g_sl_on = o->sl != 0;
     o->strong = 1;
     int ctb = opt_int(argc, argv, "--ctb", 64);
     o->log2ctb = ctb == 16 ? 4 : (ctb == 32 ? 5 : 6);
@@ -1306,7 +1495,7 @@ int main(int argc, char **argv) {
     Sao *sao = (Sao *)calloc((size_t)nctb, sizeof(Sao));
 
     FILE *fo = fopen(argv[7], "wb");
-    write_vps(fo, o->bd);
+    write_vps(fo, o->bd, o->delay);
     write_sps(fo, o);
     write_pps(fo, o);
     int rows_per_slice = o->slice_rows > 0 ? o->slice_rows : g->ctbH;
@@ -1324,6 +1513,11 @@ int main(int argc, char **argv) {
             bw_put(&b, (uint32_t)(r0 * g->ctbW), bits);
         }
         bw_ue(&b, 2); /* I */
+        if (o->nut != 19 && o->nut != 20) { /* CRA / BLA: POC lsb + an empty short-term RPS */
+            bw_put(&b, 0, 8);               /* slice_pic_order_cnt_lsb */
+            bw_put(&b, 0, 1);               /* short_term_ref_pic_set_sps_flag */
+            bw_ue(&b, 0); bw_ue(&b, 0);     /* num_negative_pics, num_positive_pics */
+        }
         if (o->sao) { bw_put(&b, 1, 1); bw_put(&b, 1, 1); }
         int sqp_delta = 0;
         if (o->qpdelta && nslice > 0) sqp_delta = rndn(5) - 2;
@@ -1410,9 +1604,11 @@ int main(int argc, char **argv) {
             free(sub[k].buf);
         }
         free(sub);
-        write_nal(fo, 19, b.buf, b.n); /* IDR_W_RADL */
+        write_nal(fo, o->nut, b.buf, b.n); /* IDR_W_RADL unless --nut */
         free(b.buf);
     }
+    /* decoder delay: delay + 1 trailing P pictures, output order != decoding order */
+    for (int k = 1; o->delay && k <= o->delay + 1; k++) write_skip_picture(g, fo, k == 1 ? 2 * (o->delay + 1) : 2 * (k - 1));
     fclose(fo);
     const char *rp = opt_str(argc, argv, "--recon");
     if (rp) {

@@ -13,6 +13,9 @@ reconstruction bit-for-bit.
   python tools/make_streams.py parity264 -> tests/golden/h264/*.h264 + manifest.json (tools/h264gen)
   python tools/make_streams.py bench264  -> tests/golden/bench264/avc1080_XX.h264 (16 streams, High 8x8)
   python tools/make_streams.py mixed     -> tests/golden/mixed/ (720p H.265/H.264, 4K H.264) for configs[4]
+  python tools/make_streams.py f3        -> tests/golden/f3/ (decoder delay, non-IDR / CRA / BLA first pictures)
+  python tools/make_streams.py malformed -> tests/golden/malformed/ (out-of-range SPS / slice header values)
+  python tools/make_streams.py heavy     -> tests/golden/bench_heavy/hevc1080h_XX.h265 (16 streams, ~100-250 KB)
 """
 import json
 import os
@@ -108,6 +111,25 @@ def bench(n=16):
     print("total", total)
 
 
+def heavy(n=16):
+    """configs[1] on heavier content: ~100-250 KB per 1080p picture (SURVEY.md §8(d) aim);
+    the host CABAC cost scales with it (the end-to-end bound)."""
+    out_dir = os.path.join(ROOT, "tests/golden/bench_heavy")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    qps = [18, 20, 22, 24]
+    sigmas = [0, 1, 2, 1]
+    total = 0
+    for i in range(n):
+        qp, sigma = qps[i % 4], sigmas[(i // 4) % 4]
+        content = make_content(planes, 1920, 1080, 400 + i, sigma, 8)
+        path = os.path.join(out_dir, f"hevc1080h_{i:02d}.h265")
+        nb = encode(content, 1920, 1080, 8, qp, 400 + i, path)
+        total += nb
+        print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+    print("total", total, "mean", total // n)
+
+
 PARITY = [
     # name, W, H, bd, qp, seed, sigma, options
     ("p01_416x240_q22", 416, 240, 8, 22, 11, 2, []),
@@ -131,6 +153,12 @@ PARITY = [
     ("p18_416x240_tiles3x2_ctb32", 416, 240, 8, 28, 29, 2, ["--ctb", "32", "--tilecols", "3", "--tilerows", "2"]),
     ("p19_480x272_tiles2x2_wpp_nolf", 480, 272, 8, 30, 30, 2, ["--ctb", "32", "--tilecols", "2", "--tilerows", "2", "--wpp", "1", "--lftiles", "0"]),
     ("p20_80x96_tiles5x3_wpp_narrow", 80, 96, 8, 26, 31, 2, ["--ctb", "16", "--tilecols", "5", "--tilerows", "3", "--wpp", "1"]),
+    # scaling lists (7.3.4 / 7.4.5): SPS defaults (Table 7-6), explicit SPS lists (DC, pred_matrix_id_delta
+    # copies, defaults), explicit PPS lists over explicit / default SPS lists
+    ("p21_416x240_sl_sps_default", 416, 240, 8, 25, 32, 2, ["--sl", "1"]),
+    ("p22_416x240_sl_sps_explicit", 416, 240, 8, 22, 33, 3, ["--sl", "2", "--depth", "2"]),
+    ("p23_480x272_sl_sps_pps_ctb32", 480, 272, 8, 30, 34, 2, ["--sl", "3", "--ctb", "32", "--bypass", "1"]),
+    ("p24_352x288_10bit_sl_pps_over_default", 352, 288, 10, 20, 35, 2, ["--sl", "4", "--pcm", "1"]),
 ]
 
 
@@ -172,6 +200,12 @@ PARITY264 = [
     ("a17_256x144_cavlc_q0_noise", 256, 144, 8, 0, 47, 20, ["--cavlc", "1", "--t8x8", "1"]),
     ("a18_480x272_cavlc_slices_offsets", 480, 272, 8, 33, 48, 2,
      ["--cavlc", "1", "--slices", "2", "--cqp", "2", "--alpha", "1", "--beta", "-1"]),
+    # scaling matrices (7.3.2.1.1.1): SPS lists (fall-back rule A), SPS + PPS lists (rule B),
+    # PPS lists only (rule A in the PPS); useDefaultScalingMatrixFlag and early-ended lists
+    ("a19_416x240_sm_sps_8x8", 416, 240, 8, 24, 49, 2, ["--sm", "1"]),
+    ("a20_416x240_sm_sps_pps_8x8", 416, 240, 8, 30, 50, 3, ["--sm", "2", "--cqp", "2", "--cqp2", "-1"]),
+    ("a21_352x288_sm_pps_cavlc", 352, 288, 8, 20, 51, 2, ["--sm", "3", "--cavlc", "1"]),
+    ("a22_320x176_sm_sps_pps_10bit_4x4", 320, 176, 10, 16, 52, 3, ["--sm", "2", "--t8x8", "0"]),
 ]
 
 
@@ -229,6 +263,76 @@ def mixed():
         print(f"avc2160_{i:02d}: {nb} B", flush=True)
 
 
+F3 = [
+    # decoder-delay streams (the reference returns false without output for
+    # these, /root/reference/src/Decoder.cpp:342-360: avcodec_receive_frame gives EAGAIN after
+    # one packet; we transcode picture 0) and leading non-IDR / CRA / BLA pictures.
+    # name, codec, W, H, qp, seed, options
+    ("f3_avc_delay2", 264, 352, 288, 26, 60, ["--delay", "2"]),
+    ("f3_avc_nonidr_first", 264, 416, 240, 28, 61, ["--nonidr", "1", "--slices", "5"]),
+    ("f3_avc_nonidr_delay1_cavlc", 264, 320, 176, 24, 62, ["--nonidr", "1", "--delay", "1", "--cavlc", "1"]),
+    ("f3_hevc_delay2", 265, 352, 288, 27, 63, ["--delay", "2"]),
+    ("f3_hevc_cra_first", 265, 416, 240, 27, 64, ["--nut", "21", "--slices", "2"]),
+    ("f3_hevc_bla_first_delay1", 265, 320, 184, 30, 65, ["--nut", "16", "--delay", "1", "--ctb", "32"]),
+    ("f3_hevc_cra_wpp", 265, 480, 272, 25, 66, ["--nut", "21", "--wpp", "1"]),
+]
+
+
+def f3():
+    out_dir = os.path.join(ROOT, "tests/golden/f3")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    manifest = []
+    for name, codec, W, H, qp, seed, opts in F3:
+        content = make_content(planes, W, H, seed, 2, 8)
+        ext = ".h265" if codec == 265 else ".h264"
+        path = os.path.join(out_dir, name + ext)
+        nb = encode(content, W, H, 8, qp, seed, path, opts, codec=codec)
+        delay = "--delay" in opts
+        manifest.append({"file": name + ext, "codec": codec, "w": W, "h": H, "options": opts,
+                         "reference_returns": False if delay else None,
+                         "note": "decoder delay: reference silently returns false (EAGAIN, no flush)" if delay
+                         else "leading intra picture without IDR: reference result unpinned (FFmpeg recovery logic)"})
+        print(f"{path}: {nb} B", flush=True)
+    json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
+MALFORMED = [
+    # parameter-set values outside their ranges.  FFmpeg (the reference path) ignores
+    # cropping / conformance windows that leave no picture (h264_ps.c "crop values invalid",
+    # hevc_ps.c "Invalid cropping offsets") and rejects the others; "ok" = a JPEG of the whole
+    # coded picture, "fail" = no JPEG.
+    # name, codec, W, H, options, expect
+    ("m_avc_crop_overflow", 264, 400, 232, ["--crop", "0,300,0,0"], "ok"),
+    ("m_avc_crop_huge", 264, 400, 232, ["--crop", "2147483647,0,5,4"], "ok"),
+    ("m_avc_firstmb_oob", 264, 128, 96, ["--firstmb", "100000"], "fail"),
+    ("m_hevc_conf_overflow", 265, 396, 228, ["--conf", "0,250,0,0"], "ok"),
+    ("m_hevc_conf_huge", 265, 396, 228, ["--conf", "4294967294,0,0,4294967294"], "ok"),
+    ("m_hevc_width_not_mincb", 265, 128, 96, ["--wdelta", "4"], "fail"),
+]
+
+
+def malformed():
+    out_dir = os.path.join(ROOT, "tests/golden/malformed")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    manifest = []
+    for k, (name, codec, W, H, opts, expect) in enumerate(MALFORMED):
+        content = make_content(planes, W, H, 70 + k, 2, 8)
+        ext = ".h265" if codec == 265 else ".h264"
+        path = os.path.join(out_dir, name + ext)
+        yuv = path + ".yuv"
+        with open(yuv, "wb") as f:
+            for p in content:
+                f.write(p.astype(np.uint8).tobytes())
+        subprocess.check_call([GEN if codec == 265 else GEN264, yuv, str(W), str(H), "8", "27", str(70 + k), path]
+                              + opts)
+        os.remove(yuv)
+        manifest.append({"file": name + ext, "codec": codec, "options": opts, "expect": expect})
+        print(f"{path}: {os.path.getsize(path)} B, expect {expect}", flush=True)
+    json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
 def fourk(n=4):
     out_dir = os.path.join(ROOT, "tests/golden/bench4k")
     os.makedirs(out_dir, exist_ok=True)
@@ -245,4 +349,4 @@ if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
-     "mixed": mixed}[what]()
+     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed}[what]()
