@@ -1815,16 +1815,15 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
     }
 }
 
+// One CTB row `row` of one component group (grp 0: luma; grp 1: Cb and Cr) of a picture, by one
+// wave: CTBs left to right, each in z-order quadrants (skipping quadrants outside the picture).
+// `above` / `mine`: the progress words of the row above / this row ((row + 1) << 16 | quadrants
+// done, quadrant granularity); `line`: the group's bottom-line buffer (row r writes the line
+// row r + 1 reads).
 template <typename Pel>
-DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
-                    int16_t* line, int wv, const int W_) {
+DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const uint32_t* rng, int grp, QWave& w,
+                   const uint32_t* above, uint32_t* mine, int16_t* line, const int row) {
     const int lane = threadIdx.x & 63;
-    QWave& w = W[wv];
-    const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
-    const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
-    const int kSlots = 2 * W_;  // (W_: waves of this group, a runtime value: one code copy per sample type)
-    const FU u = make_fu(f, arena);
-    if (wv >= u.ctb_h) return;
     const int shc = grp ? 1 : 0;                 // component subsampling of this group
     const int CS = 1 << u.log2ctb;               // luma CTB size
     const int Sc = CS >> shc;                    // CTB size in this group's components
@@ -1835,21 +1834,19 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     const int Wc = u.width >> shc, Hc = u.height >> shc;
     const int ncomp = grp ? 2 : 1;
     PROF_DECL;
-    // the wave's quadrant sequence: rows wv, wv + W_, ..., CTBs left to right, z-order
-    // quadrants, skipping quadrants outside the picture
-    auto q_inside = [&](int row, int cx, int q) __attribute__((always_inline)) {
+    auto q_inside = [&](int cx, int q) __attribute__((always_inline)) {
         return cx * Sc + (q & 1) * Qc < Wc && row * Sc + (q >> 1) * Qc < Hc;
     };
-    auto q_next = [&](int& row, int& cx, int& q) __attribute__((always_inline)) {  // advance to the next quadrant inside the picture
+    auto q_next = [&](int& cx, int& q) __attribute__((always_inline)) {  // next quadrant of the row inside the picture
         do {
-            if (++q == nqs * nqs) {
+            if (++q == nq) {
                 q = 0;
-                if (++cx == u.ctb_w) { cx = 0; row += W_; }
+                ++cx;
             }
-        } while (row < u.ctb_h && !q_inside(row, cx, q));
+        } while (cx < u.ctb_w && !q_inside(cx, q));
     };
     int cur = 0;  // quadrant window in use (the other one is being filled for the next quadrant)
-    hevc_qres_dma(u, grp, 0, wv * Sc, Qc, w.body[0], lane);
+    hevc_qres_dma(u, grp, 0, row * Sc, Qc, w.body[0], lane);
     lds_dma_wait();
     // this group's record range of a CTB: luma [first, first chroma), chroma [first chroma, end)
     auto grange = [&](int cbi, uint32_t& ra, uint32_t& rb) __attribute__((always_inline)) {
@@ -1859,12 +1856,10 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
         rb = grp ? r.z : mid;
     };
     uint32_t na, nb;
-    grange(wv * u.ctb_w, na, nb);
+    grange(row * u.ctb_w, na, nb);
     uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
     uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
-    for (int row = wv; row < u.ctb_h; row += W_) {
-        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
-        uint32_t* mine = prog + row % kSlots;
+    {
         uint32_t seen = 0;
         const bool below = row + 1 < u.ctb_h;
         for (int cx = 0; cx < u.ctb_w; cx++) {
@@ -1875,18 +1870,13 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
             uint32_t t = a, tb = a;
             uint4 rec = nrec;
             uint2 msk = nmsk;
-            {
-                int nrow = row, ncx = cx + 1;
-                if (ncx == u.ctb_w) { ncx = 0; nrow += W_; }
-                if (nrow < u.ctb_h) {
-                    const int ncb = nrow * u.ctb_w + ncx;
-                    grange(ncb, na, nb);
-                    nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
-                    nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
-                }
+            if (cx + 1 < u.ctb_w) {
+                grange(row * u.ctb_w + cx + 1, na, nb);
+                nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
+                nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
             }
-            for (int q = 0; q < nqs * nqs; q++) {
-                if (!q_inside(row, cx, q)) continue;
+            for (int q = 0; q < nq; q++) {
+                if (!q_inside(cx, q)) continue;
                 const int qx = q & 1, qy = q >> 1;
                 const int X0 = CX0 + qx * Qc, Y0 = CY0 + qy * Qc;
                 // top quadrants need the row above (progress counts its quadrants, nq per CTB):
@@ -1907,7 +1897,7 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                 // the column on the left; sources picked by uniform element offsets from the
                 // start of the group's LDS, one unconditional load each
                 {
-                    int16_t* base = reinterpret_cast<int16_t*>(W);
+                    int16_t* base = reinterpret_cast<int16_t*>(&w);
                     for (int ci = 0; ci < ncomp; ci++) {
                         QComp& C = w.cs[ci];
                         const int o_line = static_cast<int>(line + ci * (Wc + 64) - base);
@@ -1940,13 +1930,13 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
                         }
                     }
                 }
-                {  // prefetch the next quadrant's residual into the other window (its last reader,
-                   // the previous quadrant's store, has finished reading it)
-                    int nr = row, nc = cx, nq = q;
-                    q_next(nr, nc, nq);
+                {  // prefetch the row's next quadrant's residual into the other window (its last
+                   // reader, the previous quadrant's store, has finished reading it)
+                    int nc = cx, nqi = q;
+                    q_next(nc, nqi);
                     lds_reads_done();
-                    if (nr < u.ctb_h)
-                        hevc_qres_dma(u, grp, nc * Sc + (nq & 1) * Qc, nr * Sc + (nq >> 1) * Qc, Qc, w.body[cur ^ 1], lane);
+                    if (nc < u.ctb_w)
+                        hevc_qres_dma(u, grp, nc * Sc + (nqi & 1) * Qc, row * Sc + (nqi >> 1) * Qc, Qc, w.body[cur ^ 1], lane);
                 }
                 wave_sync();
                 PROF_LAP(1);
@@ -2045,6 +2035,20 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     PROF_FLUSH();
 }
 
+// Static row assignment (the <= 128-picture "wide" launches and the mixed-batch kernel): wave wv
+// of a W_-wave group walks rows wv, wv + W_, ...; progress words in 2 * W_ row-tagged slots.
+template <typename Pel>
+DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp, QWave* W, uint32_t* prog,
+                    int16_t* line, int wv, const int W_) {
+    const FU u = make_fu(f, arena);
+    const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
+    const int kSlots = 2 * W_;
+    for (int row = wv; row < u.ctb_h; row += W_)
+        hevc_row<Pel>(u, T, masks, rng, grp, W[wv], prog + (row + kSlots - 1) % kSlots, prog + row % kSlots, line, row);
+}
+
+
 // Separate kernels per codec so each gets its own register budget; a mixed
 // batch launches both and each skips the other codec's pictures.
 // grid (pictures, 2): blockIdx.y = 0 luma chain, 1 chroma chains.
@@ -2109,6 +2113,58 @@ __global__ void __launch_bounds__(64 * (kYWaves + kCWaves)) h2j_k1_recon_hevc_pi
     const h2j_frame& f = frames[blockIdx.x];
     if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
     hevc_picture_groups<Pel>(f, tus + ufl(f.tu), arena, k1lds, ybytes);
+}
+
+// K1 HEVC, picture pool: one 16-wave workgroup reconstructs P pictures.  Its waves take CTB-row
+// jobs from one LDS queue ordered row by row and, inside a row index, picture by picture, luma
+// before chroma (row 0: P0 luma, P0 chroma, P1 luma, ...): a wave that finishes a row takes the
+// next row of either component group and either picture.  Rows of one (picture, group) chain
+// through progress words as in hevc_rows; a job only ever waits on an earlier job, which some
+// wave is running or has finished, so the queue cannot deadlock.  Against one picture per
+// workgroup with a fixed 9 luma / 7 chroma split (h2j_k1_recon_hevc_pic) no wave idles through a
+// second row round, and one picture's wavefront start-up overlaps the other's tail.
+// LDS: QWave[16] | progress words [P][2][maxrows] | queue word (+3 pad) | lines [P][lstride]
+// (luma bottom line at 0, Cb / Cr lines at lchroma).
+constexpr int kPoolWaves = 16;
+__host__ __device__ constexpr size_t k1_pool_lds(int P, int maxrows, int lstride) {
+    return sizeof(QWave) * kPoolWaves + (static_cast<size_t>(P) * 2 * maxrows + 4) * 4 +
+           static_cast<size_t>(P) * lstride * 2;
+}
+template <typename Pel>
+__global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const h2j_frame* frames, const h2j_tu* tus,
+                                                                        uint8_t* arena, int nframes, int P, int maxrows,
+                                                                        int lstride, int lchroma) {
+    extern __shared__ __align__(16) uint8_t k1lds[];
+    QWave* W = reinterpret_cast<QWave*>(k1lds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(k1lds + sizeof(QWave) * kPoolWaves);
+    const int nprog = P * 2 * maxrows;
+    uint32_t* queue = prog + nprog;
+    int16_t* lines = reinterpret_cast<int16_t*>(queue + 4);
+    for (int i = static_cast<int>(threadIdx.x); i < nprog + 4; i += 64 * kPoolWaves) prog[i] = 0;
+    __syncthreads();
+    const int lane = static_cast<int>(threadIdx.x & 63), wv = static_cast<int>(threadIdx.x >> 6);
+    const uint32_t njobs = static_cast<uint32_t>(nprog);
+    for (;;) {
+        uint32_t j = 0;
+        if (lane == 0) j = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        j = ufl(static_cast<uint32_t>(__shfl(static_cast<int>(j), 0, 64)));
+        if (j >= njobs) break;
+        const int row = static_cast<int>(j) / (2 * P), rem = static_cast<int>(j) - row * 2 * P;
+        const int p = rem >> 1, grp = rem & 1;
+        const int fi = static_cast<int>(blockIdx.x) * P + p;
+        if (fi >= nframes) continue;
+        const h2j_frame& f = frames[fi];
+        if (ufl(f.codec) != H2J_CODEC_HEVC || (ufl(f.bit_depth) > 8) != (sizeof(Pel) == 2)) continue;
+        const FU u = make_fu(f, arena);
+        if (row >= u.ctb_h) continue;
+        const h2j_tu* T = tus + ufl(f.tu);
+        const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
+        const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
+        uint32_t* pr = prog + (p * 2 + grp) * maxrows;
+        int16_t* line = lines + p * lstride + (grp ? lchroma : 0);
+        if (grp == 0) hevc_row<Pel>(u, T, masks, rng, 0, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
+        else hevc_row<Pel>(u, T, masks, rng, 1, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
+    }
 }
 
 // K1 for batches mixing HEVC 8-bit, HEVC high bit depth and H.264 pictures (configs[4]): one
@@ -3215,10 +3271,16 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint8_t>),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint16_t>),
                              reinterpret_cast<const void*>(h2j_k1_recon_h264),
-                             reinterpret_cast<const void*>(h2j_k1_recon_any)};
+                             reinterpret_cast<const void*>(h2j_k1_recon_any),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pool<uint8_t>),
+                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pool<uint16_t>)};
         for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
+    static const int pool_p = [] {  // H2J_K1_POOL: max pictures per pool workgroup (0: h2j_k1_recon_hevc_pic)
+        const char* e = std::getenv("H2J_K1_POOL");
+        return e ? std::max(0, std::min(8, std::atoi(e))) : 4;
+    }();
     static const bool merge = [] {  // H2J_K1_MERGE=0: separate launches per kind (A/B timing)
         const char* e = std::getenv("H2J_K1_MERGE");
         return !(e && e[0] == '0');
@@ -3242,6 +3304,23 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
             const dim3 grid(b->nframes, 2), block(64 * kK1WavesWide);
             if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
             if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
+        } else if (pool_p > 0) {
+            // pictures per pool workgroup: ~256 workgroups (one per CU) per launch, as many
+            // pictures each as fit (LDS: one set of line buffers + progress words per picture)
+            const int maxrows = (b->max_h + 15) / 16;
+            const int lstride = 2 * b->max_w + 192, lchroma = b->max_w + 64;
+            int P = std::max(1, std::min(pool_p, (b->nframes + 255) / 256));
+            while (P > 1 && k1_pool_lds(P, maxrows, lstride) > 160 * 1024) P--;
+            const size_t lds = k1_pool_lds(P, maxrows, lstride);
+            if (lds > 160 * 1024) {
+                snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pool: %zu B of LDS per workgroup (max 160 KB)", lds);
+                return -1;
+            }
+            const dim3 grid((b->nframes + P - 1) / P), block(64 * kPoolWaves);
+            if (p8) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint8_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
+                                       b->nframes, P, maxrows, lstride, lchroma);
+            if (p16) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint16_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
+                                        b->nframes, P, maxrows, lstride, lchroma);
         } else {
             if (pbytes > 160 * 1024) {
                 snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pic: %zu B of LDS per workgroup (max 160 KB)", pbytes);

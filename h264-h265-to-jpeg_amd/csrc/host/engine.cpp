@@ -18,7 +18,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -185,6 +187,7 @@ struct Slot {
     HostBuf h_in, h_js, h_seg;
     std::vector<h2j_frame> frames;
     std::vector<int> live;  // job index of each frame of the chunk
+    std::vector<FrameJob>* jobs = nullptr;  // the job set `live` indexes
     h2j_gpu_batch batch{};
     size_t zero_bytes = 0, jcoef_base = 0, jcoef_bytes = 0, jstat_base = 0, jstat_stride = 0;
     int stages = 0;
@@ -215,25 +218,90 @@ constexpr int kK1BandRows = 68;
 // upper bound of one block's entropy-coded size (code lengths <= 16, values <= 16 bits)
 constexpr size_t kSegBytesPerBlock = 272;
 
+// A submitted batch (h2j_engine_submit; h2j_engine_transcode is submit + wait).
+struct Batch {
+    int64_t ticket = 0;
+    int n = 0;
+    const uint8_t* const* data = nullptr;  // caller-owned until the batch is waited for
+    const size_t* sizes = nullptr;
+    uint8_t* out = nullptr;
+    size_t out_cap = 0;
+    size_t* out_off = nullptr;
+    size_t* out_len = nullptr;
+    int* status = nullptr;
+    std::vector<int> bounds;                   // parse chunks: index ranges
+    std::vector<int> chunk_of;
+    std::unique_ptr<std::atomic<int>[]> left;  // pictures of each parse chunk still being parsed
+    int jobset = -1;                           // Engine::jobsets slot the batch parses into
+    bool parsed = false, done = false;
+    int rc = 0;
+    double t0 = 0, t_parsed = 0;
+};
+
 struct Engine {
     int device = 0;
     ThreadPool* pool = nullptr;
     HostPlan plan;  // host threads / NUMA placement of the pool
     std::string err;
-    std::vector<FrameJob> jobs;
-    std::vector<int> last_status;  // per-picture status of the last transcode (h2j_engine_frame_error)
+    std::vector<FrameJob> jobs;  // single-picture entry points (decode / jpeg_coeffs)
+    // Asynchronous batches: a parser thread runs the pool over batch after batch, a driver thread
+    // runs each batch's GPU chunks and JPEG assembly, so one batch's GPU tail overlaps the next
+    // batch's entropy decoding.  At most two batches hold a job set at a time.
+    std::mutex amu;
+    std::condition_variable acv;
+    std::deque<Batch*> parse_q, gpu_q;
+    std::vector<std::unique_ptr<Batch>> batches;  // submitted and not yet waited for
+    std::vector<FrameJob> jobsets[2];
+    bool jobset_busy[2] = {false, false};
+    int64_t next_ticket = 1;
+    int active = 0;  // submitted batches not done
+    bool stop = false;
+    std::thread parser, driver;
+    std::mutex pool_mu;  // held by whoever runs a parallel_for on the pool
+    double last_stats[ST_N] = {0};
+    std::vector<int> working_status;
+    std::vector<int> last_status;          // per-picture status of the last finished batch
+    std::vector<std::string> last_msg;     // ... and the parse messages of its failed pictures
     struct ChunkTime {
         int frames = 0;
         double k1_ms = 0, kernels_ms = 0;  // K1 launch; K0..K5 (HIP events on the chunk's stream)
     };
-    std::vector<ChunkTime> chunk_log;  // chunks of the last transcode (h2j_engine_chunk_times)
+    std::vector<ChunkTime> chunk_log;       // chunks of the batch being driven
+    std::vector<ChunkTime> last_chunk_log;  // chunks of the last finished batch (h2j_engine_chunk_times)
     Slot slot[2];
-    double stats[ST_N] = {0};
+    double stats[ST_N] = {0};  // working stats of the batch being driven
 
     ~Engine() {
+        {
+            std::unique_lock<std::mutex> lk(amu);
+            acv.wait(lk, [&] { return active == 0; });
+            stop = true;
+        }
+        acv.notify_all();
+        if (parser.joinable()) parser.join();
+        if (driver.joinable()) driver.join();
         slot[0].release();
         slot[1].release();
         delete pool;
+    }
+
+    // run f(i), i < n, on the pool if no one else is using it (the parser), else on this thread
+    void par(int n, const std::function<void(int)>& f) {
+        if (pool_mu.try_lock()) {
+            pool->parallel_for(n, f);
+            pool_mu.unlock();
+        } else {
+            for (int i = 0; i < n; i++) f(i);
+        }
+    }
+    void start_threads();
+    void parse_loop();
+    void drive_loop();
+    int run_batch(Batch& b);
+    // wait until no batch is in flight (the single-picture entry points use slot 0 directly)
+    void quiesce() {
+        std::unique_lock<std::mutex> lk(amu);
+        acv.wait(lk, [&] { return active == 0; });
     }
 
     int fail(const std::string& m) {
@@ -250,7 +318,7 @@ struct Engine {
     // Lay out, pack and enqueue the GPU work of jobs[live] on slot s.
     // stages: 1 recon, 2 +deblock, 3 +sao, 4 +jpeg forward path; entropy: +K5.
     // pool_free: the thread pool may be used for packing (not busy parsing).
-    int enqueue(Slot& s, int stages, bool entropy, bool pool_free = true);
+    int enqueue(Slot& s, int stages, bool entropy, bool pool_free = true);  // s.jobs must be set
     // Wait for slot s and copy its payloads down (entropy chunks).
     int sync(Slot& s);
 };
@@ -264,6 +332,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     s.frames.resize(nf);
     size_t ntu = 0, ncoef = 0, nctb = 0, nslice = 0, nsl = 0, nblk = 0;
     int max_w = 0, max_h = 0, max_mcu = 0, max_ntu = 0, max_ctbs = 0;
+    const std::vector<FrameJob>& jobs = *s.jobs;
     for (int k = 0; k < nf; k++) {
         const FrameJob& j = jobs[s.live[k]];
         max_ntu = std::max(max_ntu, static_cast<int>(j.tus.size()));
@@ -420,7 +489,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         if (!j.sl.empty()) std::memcpy(hin + o_sl + bl[k], j.sl.data(), j.sl.size());
     };
     const double tp = now_ms();
-    if (pool_free) pool->parallel_for(nf, pack);
+    if (pool_free) par(nf, pack);
     else for (int k = 0; k < nf; k++) pack(k);
     stats[ST_PACK] += now_ms() - tp;
     uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
@@ -550,6 +619,216 @@ std::vector<int> chunk_plan(int n) {
     return starts;
 }
 
+// Throughput plan (asynchronous batches): one parse chunk of up to 1024 pictures (K1 runs up to
+// four pictures per workgroup on launches that large); the GPU tail of a batch is hidden behind
+// the next batch's entropy decoding instead of being cut into shrinking chunks.
+std::vector<int> chunk_plan_throughput(int n) {
+    int chunk = 1024;
+    const char* e = std::getenv("H2J_CHUNK_ASYNC");
+    if (e && std::atoi(e) > 0) chunk = std::atoi(e);
+    std::vector<int> starts;
+    for (int i = 0; i < n; i += chunk) starts.push_back(i);
+    starts.push_back(n);
+    return starts;
+}
+
+// GPU sub-chunks of a parsed range are bounded by an HBM estimate per slot (pictures, residual,
+// JPEG coefficients, payload pool: ~16 B per luma sample at 8 bits) and by 1024 pictures.
+constexpr double kSlotHbmBudget = 64e9;
+constexpr int kMaxGpuChunk = 1024;
+static double hbm_estimate(const FrameJob& j) {
+    const double px = static_cast<double>(j.hdr.width) * j.hdr.height;
+    return px * (j.hdr.bit_depth > 8 ? 20.0 : 16.0) + (1 << 20);
+}
+
+void Engine::start_threads() {
+    std::lock_guard<std::mutex> g(amu);
+    if (parser.joinable()) return;
+    parser = std::thread([this] { parse_loop(); });
+    driver = std::thread([this] { drive_loop(); });
+}
+
+void Engine::parse_loop() {
+    for (;;) {
+        Batch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(amu);
+            acv.wait(lk, [&] { return stop || !parse_q.empty(); });
+            if (parse_q.empty()) return;
+            b = parse_q.front();
+            parse_q.pop_front();
+            acv.wait(lk, [&] { return !jobset_busy[0] || !jobset_busy[1]; });
+            b->jobset = jobset_busy[0] ? 1 : 0;
+            jobset_busy[b->jobset] = true;
+        }
+        std::vector<FrameJob>& jobs = jobsets[b->jobset];
+        if (static_cast<int>(jobs.size()) < b->n) jobs.resize(static_cast<size_t>(b->n));
+        // batches smaller than the thread pool (a lone IDecoder call): pictures with several
+        // independent slices / WPP rows / tiles parse them on several threads
+        const int slice_threads = std::max(1, (pool->size() + 1) / std::max(1, b->n));
+        {
+            std::lock_guard<std::mutex> g(pool_mu);
+            pool->parallel_for(b->n, [&](int i) {
+                jobs[i].threads = slice_threads;
+                parse_any(b->data[i], b->sizes[i], jobs[i]);
+                if (b->left[b->chunk_of[i]].fetch_sub(1) == 1) {
+                    std::lock_guard<std::mutex> g2(amu);
+                    acv.notify_all();
+                }
+            });
+        }
+        std::lock_guard<std::mutex> g(amu);
+        b->t_parsed = now_ms();
+        b->parsed = true;
+        acv.notify_all();
+    }
+}
+
+void Engine::drive_loop() {
+    h2j_gpu_set_device(device);  // HIP's current device is per thread
+    for (;;) {
+        Batch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(amu);
+            acv.wait(lk, [&] { return stop || !gpu_q.empty(); });
+            if (gpu_q.empty()) return;
+            b = gpu_q.front();
+            gpu_q.pop_front();
+        }
+        const int rc = run_batch(*b);
+        std::unique_lock<std::mutex> lk(amu);
+        acv.wait(lk, [&] { return b->parsed; });  // a failed batch may still be parsing
+        std::vector<FrameJob>* jobs = b->jobset >= 0 ? &jobsets[b->jobset] : nullptr;
+        stats[ST_PARSE] = b->t_parsed > 0 ? b->t_parsed - b->t0 : 0;
+        stats[ST_TOTAL] = now_ms() - b->t0;
+        std::memcpy(last_stats, stats, sizeof(stats));
+        last_chunk_log = chunk_log;
+        last_status.assign(b->status, b->status + b->n);
+        last_msg.assign(static_cast<size_t>(b->n), std::string());
+        if (jobs)
+            for (int i = 0; i < b->n; i++)
+                if (b->status[i] != 0 && (*jobs)[i].error != 0) last_msg[i] = (*jobs)[i].message;
+        if (b->jobset >= 0) jobset_busy[b->jobset] = false;
+        b->rc = rc;
+        b->done = true;
+        active--;
+        acv.notify_all();
+    }
+}
+
+// The GPU side of one batch (driver thread): as parse chunks complete, their pictures go to the
+// two slots in GPU sub-chunks (HBM budget); slot c+1 is enqueued before slot c is assembled, so
+// the GPU runs one sub-chunk while the host writes the JPEGs of the previous one.
+int Engine::run_batch(Batch& b) {
+    for (auto& v : stats) v = 0;
+    chunk_log.clear();
+    const int nchunks = static_cast<int>(b.bounds.size()) - 1;
+    if (b.n == 0 || nchunks <= 0) return 0;
+    size_t pos = 0;
+    int rc = 0;
+    int* status = b.status;
+    auto assemble = [&](Slot& s) -> int {
+        if (sync(s)) return -2;
+        const double ta = now_ms();
+        const int nf = static_cast<int>(s.live.size());
+        const uint8_t* js = s.h_js.p + 256;
+        std::vector<size_t> sz(nf);
+        auto size_of = [&](int k) {
+            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            sz[k] = st->seg_off == ~0ull ? 0 : jpeg_container_size(*st, s.h_seg.p + st->seg_off, kLavcIdent);
+        };
+        par(nf, size_of);
+        std::vector<size_t> at(nf);
+        for (int k = 0; k < nf; k++) {
+            const int i = s.live[k];
+            const h2j_jstat* stk = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            if (stk->dev_error) {  // a device-side failure (e.g. a K1 band hand-off timed out)
+                status[i] = -52;
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
+            if (!sz[k]) {
+                status[i] = -51;  // payload pool overflow
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
+            if (pos + sz[k] > b.out_cap) {
+                status[i] = -50;
+                rc = -3;
+                at[k] = ~static_cast<size_t>(0);
+                continue;
+            }
+            at[k] = pos;
+            b.out_off[i] = pos;
+            b.out_len[i] = sz[k];
+            pos += sz[k];
+        }
+        auto write = [&](int k) {
+            if (at[k] == ~static_cast<size_t>(0)) return;
+            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
+            const h2j_frame& f = s.frames[k];
+            jpeg_write_container(*st, s.h_seg.p + st->seg_off, f.out_w, f.out_h, kLavcIdent, b.out + at[k]);
+        };
+        par(nf, write);
+        stats[ST_ASSEMBLE] += now_ms() - ta;
+        stats[ST_FRAMES] += nf;
+        return 0;
+    };
+    int fail = 0, sc = 0;
+    for (int c = 0; c < nchunks && !fail; c++) {
+        {
+            std::unique_lock<std::mutex> lk(amu);
+            acv.wait(lk, [&] { return b.left[c].load() == 0; });
+        }
+        std::vector<FrameJob>& jobs = jobsets[b.jobset];
+        int i = b.bounds[c];
+        const int end = b.bounds[c + 1];
+        // equal shares of the range's HBM estimate, as few as the budget allows (uneven splits
+        // leave small, latency-bound launches behind)
+        double total = 0;
+        for (int k = i; k < end; k++) total += hbm_estimate(jobs[k]);
+        const int parts = std::max(static_cast<int>(std::ceil(total / kSlotHbmBudget)),
+                                   (end - i + kMaxGpuChunk - 1) / kMaxGpuChunk);
+        const double share = total / std::max(1, parts);
+        while (i < end && !fail) {
+            int j = i;
+            double est = 0;
+            while (j < end && j - i < kMaxGpuChunk) {
+                const double cst = hbm_estimate(jobs[j]);
+                if (j > i && (est + cst > kSlotHbmBudget || est + cst / 2 > share)) break;
+                est += cst;
+                j++;
+            }
+            Slot& s = slot[sc & 1];
+            if (s.pending && assemble(s)) { fail = 1; break; }
+            s.live.clear();
+            s.jobs = &jobs;
+            for (int k = i; k < j; k++) {
+                status[k] = jobs[k].error;
+                if (jobs[k].error == 0) s.live.push_back(k);
+            }
+            if (enqueue(s, 4, true, true)) { fail = 1; break; }
+            Slot& prev = slot[(sc + 1) & 1];
+            if (sc > 0 && prev.pending && assemble(prev)) { fail = 1; break; }
+            sc++;
+            i = j;
+        }
+    }
+    for (int k = 0; k < 2 && !fail; k++) {
+        Slot& s = slot[(sc + k) & 1];
+        if (s.pending && assemble(s)) fail = 1;
+    }
+    if (fail) {
+        for (auto& s : slot)
+            if (s.pending) sync(s);
+        return -2;
+    }
+    if (rc) err = "output buffer too small or payload pool overflow";
+    return rc;
+}
+
 }  // namespace h2j
 
 using h2j::Engine;
@@ -595,152 +874,81 @@ void h2j_engine_destroy(h2j_engine* e) { delete e; }
 
 const char* h2j_engine_error(h2j_engine* e) { return e ? e->e.err.c_str() : "no engine"; }
 
-int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const size_t* sizes, uint8_t* out,
-                         size_t out_cap, size_t* out_off, size_t* out_len, int* status) {
-    if (!w) return -1;
+// submit one batch; latency: the synchronous plan (small tail chunks), else the throughput plan
+static int64_t submit_batch(h2j_engine* w, int n, const uint8_t* const* data, const size_t* sizes, uint8_t* out,
+                            size_t out_cap, size_t* out_off, size_t* out_len, int* status, bool latency) {
     Engine& e = w->e;
-    if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
-    const double t0 = h2j::now_ms();
-    for (auto& v : e.stats) v = 0;
-    e.chunk_log.clear();
-    if (static_cast<int>(e.jobs.size()) < n) e.jobs.resize(n);
+    std::unique_ptr<h2j::Batch> b(new h2j::Batch());
+    b->n = n;
+    b->data = data;
+    b->sizes = sizes;
+    b->out = out;
+    b->out_cap = out_cap;
+    b->out_off = out_off;
+    b->out_len = out_len;
+    b->status = status;
     for (int i = 0; i < n; i++) {
         out_len[i] = 0;
         out_off[i] = 0;
         status[i] = 0;
     }
-    const std::vector<int> bounds = h2j::chunk_plan(n);
-    const int nchunks = static_cast<int>(bounds.size()) - 1;
-    std::vector<int> chunk_of(n);
+    b->bounds = latency ? h2j::chunk_plan(n) : h2j::chunk_plan_throughput(n);
+    const int nchunks = static_cast<int>(b->bounds.size()) - 1;
+    b->chunk_of.assign(static_cast<size_t>(n), 0);
     for (int c = 0; c < nchunks; c++)
-        for (int i = bounds[c]; i < bounds[c + 1]; i++) chunk_of[i] = c;
-    size_t pos = 0;
-    int rc = 0;
-    // Parsing runs ahead on the pool (frames claimed in order), so chunk c+1
-    // parses while the GPU runs chunk c and the host assembles chunk c-1.
-    const bool overlap = nchunks > 1;
-    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[nchunks]);
-    for (int c = 0; c < nchunks; c++) left[c] = bounds[c + 1] - bounds[c];
-    std::mutex mu;
-    std::condition_variable cv;
-    double t_parsed = t0;
-    // once every picture is parsed the pool is idle: the pipeline's tail (packing, assembly)
-    // then fans out over it instead of running on this thread alone
-    std::atomic<bool> parsed(false);
-    auto pool_idle = [&]() { return !overlap || parsed.load(std::memory_order_acquire); };
-    // batches smaller than the thread pool (a lone IDecoder call): pictures with several
-    // independent slices parse them on several threads
-    const int slice_threads = std::max(1, (e.pool->size() + 1) / std::max(1, n));
-    auto parse_all = [&]() {
-        e.pool->parallel_for(n, [&](int i) {
-            e.jobs[i].threads = slice_threads;
-            h2j::parse_any(data[i], sizes[i], e.jobs[i]);
-            if (left[chunk_of[i]].fetch_sub(1) == 1) {
-                std::lock_guard<std::mutex> g(mu);
-                cv.notify_all();
-            }
-        });
-        t_parsed = h2j::now_ms();
-        parsed.store(true, std::memory_order_release);
-    };
-    std::thread producer;
-    if (overlap) producer = std::thread(parse_all);
-    else parse_all();
-    // assemble the JPEGs of a finished slot into out (in frame order)
-    auto assemble = [&](Slot& s) -> int {
-        if (e.sync(s)) return -2;
-        const double ta = h2j::now_ms();
-        const int nf = static_cast<int>(s.live.size());
-        const uint8_t* js = s.h_js.p + 256;
-        std::vector<size_t> sz(nf);
-        auto size_of = [&](int k) {
-            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
-            sz[k] = st->seg_off == ~0ull ? 0 : h2j::jpeg_container_size(*st, s.h_seg.p + st->seg_off, h2j::kLavcIdent);
-        };
-        if (!pool_idle()) for (int k = 0; k < nf; k++) size_of(k);
-        else e.pool->parallel_for(nf, size_of);
-        std::vector<size_t> at(nf);
-        for (int k = 0; k < nf; k++) {
-            const int i = s.live[k];
-            const h2j_jstat* stk = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
-            if (stk->dev_error) {  // a device-side failure (e.g. a K1 band hand-off timed out)
-                status[i] = -52;
-                rc = -3;
-                at[k] = ~static_cast<size_t>(0);
-                continue;
-            }
-            if (!sz[k]) {
-                status[i] = -51;  // payload pool overflow
-                rc = -3;
-                at[k] = ~static_cast<size_t>(0);
-                continue;
-            }
-            if (pos + sz[k] > out_cap) {
-                status[i] = -50;
-                rc = -3;
-                at[k] = ~static_cast<size_t>(0);
-                continue;
-            }
-            at[k] = pos;
-            out_off[i] = pos;
-            out_len[i] = sz[k];
-            pos += sz[k];
-        }
-        auto write = [&](int k) {
-            if (at[k] == ~static_cast<size_t>(0)) return;
-            const h2j_jstat* st = reinterpret_cast<const h2j_jstat*>(js + k * s.jstat_stride);
-            const h2j_frame& f = s.frames[k];
-            h2j::jpeg_write_container(*st, s.h_seg.p + st->seg_off, f.out_w, f.out_h, h2j::kLavcIdent, out + at[k]);
-        };
-        if (!pool_idle()) for (int k = 0; k < nf; k++) write(k);
-        else e.pool->parallel_for(nf, write);
-        e.stats[h2j::ST_ASSEMBLE] += h2j::now_ms() - ta;
-        e.stats[h2j::ST_FRAMES] += nf;
-        return 0;
-    };
-    int fail = 0;
-    for (int c = 0; c < nchunks && !fail; c++) {
-        const int i0 = bounds[c], i1 = bounds[c + 1];
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return left[c].load() == 0; });
-        }
-        Slot& s = e.slot[c & 1];
-        if (s.pending && assemble(s)) { fail = 1; break; }
-        s.live.clear();
-        for (int i = i0; i < i1; i++) {
-            status[i] = e.jobs[i].error;
-            if (e.jobs[i].error == 0) s.live.push_back(i);
-        }
-        if (e.enqueue(s, 4, true, pool_idle())) { fail = 1; break; }
-        Slot& prev = e.slot[(c + 1) & 1];
-        if (c > 0 && prev.pending && assemble(prev)) { fail = 1; break; }
-    }
-    for (int c = 0; c < 2 && !fail; c++) {
-        Slot& s = e.slot[(nchunks + c) & 1];
-        if (s.pending && assemble(s)) fail = 1;
-    }
-    if (producer.joinable()) producer.join();
-    e.stats[h2j::ST_PARSE] = t_parsed - t0;
-    e.last_status.assign(status, status + n);
-    if (fail) {
-        for (auto& s : e.slot)
-            if (s.pending) e.sync(s);
-        return -2;
-    }
-    e.stats[h2j::ST_TOTAL] = h2j::now_ms() - t0;
-    if (rc) e.err = "output buffer too small or payload pool overflow";
+        for (int i = b->bounds[c]; i < b->bounds[c + 1]; i++) b->chunk_of[i] = c;
+    b->left.reset(new std::atomic<int>[std::max(1, nchunks)]);
+    for (int c = 0; c < nchunks; c++) b->left[c] = b->bounds[c + 1] - b->bounds[c];
+    e.start_threads();
+    std::lock_guard<std::mutex> g(e.amu);
+    b->ticket = e.next_ticket++;
+    b->t0 = h2j::now_ms();
+    const int64_t t = b->ticket;
+    e.active++;
+    e.parse_q.push_back(b.get());
+    e.gpu_q.push_back(b.get());
+    e.batches.push_back(std::move(b));
+    e.acv.notify_all();
+    return t;
+}
+
+int64_t h2j_engine_submit(h2j_engine* w, int n, const uint8_t* const* data, const size_t* sizes, uint8_t* out,
+                          size_t out_cap, size_t* out_off, size_t* out_len, int* status) {
+    if (!w || n < 0) return -1;
+    return submit_batch(w, n, data, sizes, out, out_cap, out_off, out_len, status, false);
+}
+
+int h2j_engine_wait(h2j_engine* w, int64_t ticket) {
+    if (!w) return -1;
+    Engine& e = w->e;
+    std::unique_lock<std::mutex> lk(e.amu);
+    auto it = std::find_if(e.batches.begin(), e.batches.end(),
+                           [&](const std::unique_ptr<h2j::Batch>& b) { return b->ticket == ticket; });
+    if (it == e.batches.end()) return -1;
+    h2j::Batch* b = it->get();
+    e.acv.wait(lk, [&] { return b->done; });
+    const int rc = b->rc;
+    e.batches.erase(it);
     return rc;
+}
+
+int h2j_engine_transcode(h2j_engine* w, int n, const uint8_t* const* data, const size_t* sizes, uint8_t* out,
+                         size_t out_cap, size_t* out_off, size_t* out_len, int* status) {
+    if (!w) return -1;
+    const int64_t t = submit_batch(w, n, data, sizes, out, out_cap, out_off, out_len, status, true);
+    return h2j_engine_wait(w, t);
 }
 
 static int single_job(h2j_engine* w, const uint8_t* data, size_t size) {
     Engine& e = w->e;
+    e.quiesce();
     if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
     if (e.jobs.empty()) e.jobs.resize(1);
     e.jobs[0].threads = e.pool->size() + 1;  // independent slices on several threads
     int r = h2j::parse_any(data, size, e.jobs[0]);
     if (r) return e.fail("parse failed: " + e.jobs[0].message);
     e.slot[0].live.assign(1, 0);
+    e.slot[0].jobs = &e.jobs;
     return 0;
 }
 
@@ -818,7 +1026,7 @@ const char* h2j_engine_frame_error(h2j_engine* w, int i) {
     case -50: return "output buffer too small";
     case -51: return "JPEG payload pool overflow";
     case -52: return "device-side failure (K1 band hand-off timed out)";
-    default: return i < static_cast<int>(w->e.jobs.size()) ? w->e.jobs[i].message.c_str() : "";
+    default: return i < static_cast<int>(w->e.last_msg.size()) ? w->e.last_msg[i].c_str() : "";
     }
 }
 
@@ -826,7 +1034,8 @@ int h2j_device_count(void) { return h2j_gpu_device_count(); }
 
 int h2j_engine_chunk_times(h2j_engine* w, double* out, int max_chunks) {
     if (!w) return -1;
-    const auto& log = w->e.chunk_log;
+    std::lock_guard<std::mutex> g(w->e.amu);
+    const auto& log = w->e.last_chunk_log;
     const int n = static_cast<int>(log.size());
     for (int i = 0; i < n && i < max_chunks; i++) {
         out[3 * i] = log[i].frames;
@@ -838,7 +1047,8 @@ int h2j_engine_chunk_times(h2j_engine* w, double* out, int max_chunks) {
 
 int h2j_engine_stats(h2j_engine* w, double* out, int n) {
     if (!w) return -1;
-    for (int i = 0; i < n && i < h2j::ST_N; i++) out[i] = w->e.stats[i];
+    std::lock_guard<std::mutex> g(w->e.amu);
+    for (int i = 0; i < n && i < h2j::ST_N; i++) out[i] = w->e.last_stats[i];
     return 0;
 }
 

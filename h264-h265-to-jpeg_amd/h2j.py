@@ -49,6 +49,11 @@ def load_library() -> ctypes.CDLL:
     lib.h2j_engine_jpeg_coeffs.restype = ctypes.c_int
     lib.h2j_engine_jpeg_coeffs.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int16),
                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
+    lib.h2j_engine_submit.restype = ctypes.c_int64
+    lib.h2j_engine_submit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(u8p), szp, u8p,
+                                      ctypes.c_size_t, szp, szp, ctypes.POINTER(ctypes.c_int)]
+    lib.h2j_engine_wait.restype = ctypes.c_int
+    lib.h2j_engine_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     lib.h2j_engine_stats.restype = ctypes.c_int
     lib.h2j_engine_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     lib.h2j_engine_frame_error.restype = ctypes.c_char_p
@@ -132,6 +137,39 @@ class Engine:
     def transcode_raw(self, ptrs, sizes, n, out, cap, offs, lens, status) -> int:
         """Zero-copy variant for benchmarks (pre-built ctypes arrays)."""
         return self._lib.h2j_engine_transcode(self._h, n, ptrs, sizes, out, cap, offs, lens, status)
+
+    def submit_raw(self, ptrs, sizes, n, out, cap, offs, lens, status) -> int:
+        """Asynchronous batch (h2j_engine_submit): returns a ticket; the ctypes arrays must stay
+        alive until wait(ticket)."""
+        t = self._lib.h2j_engine_submit(self._h, n, ptrs, sizes, out, cap, offs, lens, status)
+        if t <= 0:
+            raise RuntimeError(f"h2j_engine_submit failed ({t})")
+        return t
+
+    def wait(self, ticket: int) -> int:
+        return self._lib.h2j_engine_wait(self._h, int(ticket))
+
+    def transcode_async(self, batches: Sequence[Sequence[bytes]]) -> List[List[Optional[bytes]]]:
+        """Several batches through the asynchronous path, all submitted before the first wait."""
+        held, tickets = [], []
+        for streams in batches:
+            n = len(streams)
+            bufs = [_u8(s) for s in streams]
+            ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+            sizes = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+            cap = sum(len(s) for s in streams) * 4 + n * (8 << 20)
+            out = (ctypes.c_uint8 * cap)()
+            offs, lens, status = (ctypes.c_size_t * n)(), (ctypes.c_size_t * n)(), (ctypes.c_int * n)()
+            held.append((bufs, ptrs, sizes, out, offs, lens, status, n))
+            tickets.append(self.submit_raw(ptrs, sizes, n, out, cap, offs, lens, status))
+        res = []
+        for t, (bufs, ptrs, sizes, out, offs, lens, status, n) in zip(tickets, held):
+            rc = self.wait(t)
+            if rc < 0 and rc != -3:
+                raise RuntimeError(f"h2j_engine_wait failed ({rc}): {self.error()}")
+            mv = memoryview(out)
+            res.append([bytes(mv[offs[i]:offs[i] + lens[i]]) if status[i] == 0 else None for i in range(n)])
+        return res
 
     def decode(self, stream: bytes, stage: int = 0):
         """Decoded picture planes (uint16 numpy Y, U, V) of the first picture.

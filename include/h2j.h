@@ -49,6 +49,19 @@ int h2j_engine_host_info(h2j_engine *e, int *out, int n);
 int h2j_engine_transcode(h2j_engine *e, int n, const uint8_t *const *data, const size_t *sizes,
                          uint8_t *out, size_t out_cap, size_t *out_off, size_t *out_len, int *status);
 
+/* Asynchronous batches.  h2j_engine_submit queues a batch (same arguments and per-item
+ * semantics as h2j_engine_transcode) and returns a ticket (> 0) at once; the engine parses
+ * batches in submission order on its thread pool and runs their GPU work and JPEG assembly on a
+ * driver thread, so one batch's GPU tail overlaps the next batch's entropy decoding.  A
+ * submitted batch is cut into chunks of up to 1024 pictures (K1 then reconstructs up to four
+ * pictures per workgroup).  Every pointer passed to submit must stay valid until
+ * h2j_engine_wait returns for that ticket; h2j_engine_wait returns what h2j_engine_transcode
+ * would have.  h2j_engine_transcode is submit + wait with smaller, latency-oriented chunks.
+ * Stats, chunk times and frame errors describe the last batch that finished. */
+int64_t h2j_engine_submit(h2j_engine *e, int n, const uint8_t *const *data, const size_t *sizes,
+                          uint8_t *out, size_t out_cap, size_t *out_off, size_t *out_len, int *status);
+int h2j_engine_wait(h2j_engine *e, int64_t ticket);
+
 /* Test / inspection entry points (one picture).
  * stage: 0 final decoded picture, 1 pre-loop-filter, 2 deblocked (pre-SAO).
  * planes_out: uint16 Y (w*h) then U, V ((w/2)*(h/2)) of the cropped picture.

@@ -104,3 +104,22 @@ def test_4k_main10_stream(engine):
     for g, o, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
         assert np.array_equal(g, o), name
     assert engine.transcode([s])[0] == O.transcode(s)
+
+
+def test_async_batches_and_pooled_k1(engine):
+    """h2j_engine_submit / h2j_engine_wait with three batches in flight.  Batches over 256 pictures
+    run K1's picture pool (h2j_k1_recon_hevc_pool) with several pictures per workgroup: 520
+    pictures -> 3 per workgroup, 300 -> 2; 8-bit and 10-bit parity vectors (two pool launches),
+    scaling lists, PCM, tiles, WPP.  A mixed-codec batch takes the merged K1 launch."""
+    streams = [read(p) for p in PARITY]
+    h264 = [read(p) for p in sorted(glob.glob(os.path.join(golden("h264"), "*.h264")))]
+    big = (streams * 30)[:520]
+    mixed = [x for pair in zip(streams * 8, h264 * 8) for x in pair][:300]
+    batches = [big, streams[:7], big[:300], mixed]
+    outs = engine.transcode_async(batches)
+    ref = {s: O.transcode(s) for s in set(streams) | set(h264)}
+    for b_in, b_out in zip(batches, outs):
+        assert len(b_in) == len(b_out)
+        for k, (s, o) in enumerate(zip(b_in, b_out)):
+            assert o == ref[s], k
+    assert engine.transcode([streams[0]])[0] == ref[streams[0]]  # the synchronous path still works
