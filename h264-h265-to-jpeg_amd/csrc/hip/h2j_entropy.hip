@@ -2,22 +2,24 @@
 // Huffman tables and baseline-JPEG bit emission, all on the GPU, so only the
 // entropy-coded payload (~1/30 of the coefficient bytes) crosses PCIe.
 //
-//   K4d h2j_k4d_histogram  — per 256-block tile: coefficients staged through
-//                            LDS (coalesced 16 B loads, padded rows), per-lane
-//                            non-zero mask walk, LDS histogram, one global
-//                            atomic per (tile, symbol)
+//   (K4c h2j_k4c_fdct_sym, h2j_kernels.hip, writes each block's quantised DC and
+//   its AC symbols -- run/size + magnitude bits -- and counts the AC histograms)
+//   K4e h2j_k4e_dc_hist    — per 256-block tile: DC differences from the tiles'
+//                            DC arrays, LDS histogram, one global atomic per
+//                            (tile, category)
 //   K5a h2j_k5a_tables     — one workgroup per (frame, table): AV_QSORT +
 //                            package-merge (max length 16) restated without
 //                            item lists (per-level probability arrays + leaf
 //                            prefix counts), then the length sort and canonical
 //                            code assignment of mjpegenc_huffman.c
-//   K5b h2j_k5b_tile_bits  — bits per 256-block tile
+//   K5b h2j_k5b_tile_bits  — bits per 256-block tile, from the symbol stream
 //   K5c h2j_k5c_scan       — per-frame tile offsets, payload sizes, then the
 //                            batch-level segment offsets (one workgroup)
 //   K5z h2j_k5z_zero       — clears the used part of the segment pool
 //   K5d h2j_k5d_emit       — per lane one block: workgroup scan of block bit
-//                            counts, MSB-first words, atomicOr only on the two
-//                            words a block can share with its neighbours
+//                            counts, MSB-first words from the symbol stream,
+//                            atomicOr only on the two words a block can share
+//                            with its neighbours
 //
 // Byte stuffing (0xFF -> 0xFF 0x00) is left to the host, which copies the
 // payload into the JPEG container anyway.  Reference semantics: FFmpeg
@@ -29,13 +31,13 @@
 #include <cstdio>
 
 #include "h2j_gpu.h"
+#include "jpeg_tile.h"
 
 #define DEVI __device__ __forceinline__
 
 namespace {
 
 constexpr int kTile = 256;      // blocks per workgroup
-constexpr int kRow = 33;        // LDS words per staged block (32 + 1 pad: conflict-free lane-per-block reads)
 
 DEVI int nbits16(int v) {
     const unsigned a = static_cast<unsigned>(v < 0 ? -v : v);
@@ -44,82 +46,36 @@ DEVI int nbits16(int v) {
 
 DEVI int nblocks(const h2j_frame& f) { return ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6; }
 
-// Stage blocks [b0, b0+nb) of a frame's zigzag coefficients into LDS rows.
-DEVI void stage_tile(const int16_t* co, int b0, int nb, uint32_t* lds) {
-    const uint4* src = reinterpret_cast<const uint4*>(co + static_cast<size_t>(b0) * 64);
-    for (int i = threadIdx.x; i < nb * 8; i += blockDim.x) {
-        const uint4 v = src[i];
-        uint32_t* d = lds + (i >> 3) * kRow + (i & 7) * 4;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
-    }
+// quantised DC of block bi (the tiles' DC arrays) and its DPCM predictor (MCU order Y0 Y1 Y2 Y3
+// Cb Cr, FFmpeg's last_dc = 128 at the scan start)
+DEVI int dc_of(const uint8_t* base, int bi) {
+    return reinterpret_cast<const int16_t*>(base + static_cast<size_t>(bi >> 8) * kJTileBytes + kJDcOff)[bi & 255];
 }
-
-DEVI int coef_at(const uint32_t* row, int i) {
-    const uint32_t w = row[i >> 1];
-    return static_cast<int16_t>((i & 1) ? (w >> 16) : (w & 0xffff));
-}
-
-// Non-zero mask of AC coefficients 1..63 of a staged block.
-DEVI uint64_t ac_mask(const uint32_t* row) {
-    uint64_t m = 0;
-#pragma unroll
-    for (int w = 0; w < 32; w++) {
-        const uint32_t x = row[w];
-        m |= static_cast<uint64_t>((x & 0xffff) != 0) << (2 * w);
-        m |= static_cast<uint64_t>((x >> 16) != 0) << (2 * w + 1);
-    }
-    return m & ~1ull;
-}
-
-// DC predictor of block bi (MCU order Y0 Y1 Y2 Y3 Cb Cr, FFmpeg last_dc = 128 start)
-DEVI int prev_dc(const int16_t* co, const uint32_t* lds, int b0, int bi) {
+DEVI int prev_dc(const uint8_t* base, int bi) {
     const int mcu = bi / 6, b = bi - mcu * 6;
     int pb;
     if (b < 4) pb = b > 0 ? bi - 1 : (mcu > 0 ? bi - 3 : -1);
     else pb = mcu > 0 ? bi - 6 : -1;
-    if (pb < 0) return 128;
-    if (pb >= b0) return coef_at(lds + (pb - b0) * kRow, 0);
-    return co[static_cast<size_t>(pb) * 64];
+    return pb < 0 ? 128 : dc_of(base, pb);
 }
 
-// ---------------------------------------------------------------- K4d
-__global__ void __launch_bounds__(kTile) h2j_k4d_histogram(const h2j_frame* frames, uint8_t* arena) {
-    __shared__ uint32_t lds[kTile * kRow];
-    __shared__ unsigned hist[4][256];
+// ---------------------------------------------------------------- K4e
+__global__ void __launch_bounds__(kTile) h2j_k4e_dc_hist(const h2j_frame* frames, uint8_t* arena) {
+    __shared__ unsigned hist[2][16];
     const h2j_frame& f = frames[blockIdx.y];
     const int nblk = nblocks(f);
     const int b0 = blockIdx.x * kTile;
     if (b0 >= nblk) return;
-    const int nb = min(kTile, nblk - b0);
-    for (int i = threadIdx.x; i < 1024; i += kTile) (&hist[0][0])[i] = 0;
-    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
-    stage_tile(co, b0, nb, lds);
+    if (threadIdx.x < 32) (&hist[0][0])[threadIdx.x] = 0;
     __syncthreads();
-    if (static_cast<int>(threadIdx.x) < nb) {
-        const int bi = b0 + threadIdx.x;
-        const uint32_t* row = lds + threadIdx.x * kRow;
-        const int tab = (bi % 6) < 4 ? 0 : 1;
-        atomicAdd(&hist[tab][nbits16(coef_at(row, 0) - prev_dc(co, lds, b0, bi))], 1u);
-        uint64_t m = ac_mask(row);
-        int prev = 0;
-        while (m) {
-            const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
-            m &= m - 1;
-            int run = i - prev - 1;
-            prev = i;
-            if (run >= 16) atomicAdd(&hist[2 + tab][0xF0], static_cast<unsigned>(run >> 4));
-            atomicAdd(&hist[2 + tab][((run & 15) << 4) | nbits16(coef_at(row, i))], 1u);
-        }
-        if (prev < 63) atomicAdd(&hist[2 + tab][0], 1u);
-    }
+    const uint8_t* base = arena + f.jcoef;
+    const int bi = b0 + threadIdx.x;
+    if (bi < nblk) atomicAdd(&hist[(bi % 6) < 4 ? 0 : 1][nbits16(dc_of(base, bi) - prev_dc(base, bi))], 1u);
     __syncthreads();
     h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
-    for (int i = threadIdx.x; i < 1024; i += kTile) {
-        const unsigned v = (&hist[0][0])[i];
-        if (v) atomicAdd(&js->hist[i >> 8][i & 255], v);
+    if (threadIdx.x < 32) {
+        const unsigned v = (&hist[0][0])[threadIdx.x];
+        if (v) atomicAdd(&js->hist[threadIdx.x >> 4][threadIdx.x & 15], v);
     }
 }
 
@@ -309,20 +265,15 @@ DEVI void load_codes(const h2j_jstat* js, CodeLds& c, bool with_codes) {
     }
 }
 
-DEVI uint32_t block_bits(const CodeLds& c, const uint32_t* row, int dc_diff, int tab) {
+// bits of block t of a tile: DC code + magnitude, then the AC symbols' codes + magnitudes
+DEVI uint32_t block_bits(const CodeLds& c, const uint32_t* sym, int cnt, int t, int dc_diff, int tab) {
     const int nd = nbits16(dc_diff);
     uint32_t bits = c.len[tab][nd] + nd;
-    uint64_t m = ac_mask(row);
-    int prev = 0;
-    while (m) {
-        const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
-        m &= m - 1;
-        const int run = i - prev - 1;
-        prev = i;
-        const int n = nbits16(coef_at(row, i));
-        bits += (run >> 4) * c.len[2 + tab][0xF0] + c.len[2 + tab][((run & 15) << 4) | n] + n;
+    const uint8_t* al = c.len[2 + tab];
+    for (int k = 0; k < cnt; k++) {
+        const uint32_t w = sym[k * kTile + t];
+        bits += al[w & 0xFF] + ((w >> 8) & 15);
     }
-    if (prev < 63) bits += c.len[2 + tab][0];
     return bits;
 }
 
@@ -350,7 +301,6 @@ DEVI uint32_t wg_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
 // ---------------------------------------------------------------- K5b
 __global__ void __launch_bounds__(kTile) h2j_k5b_tile_bits(const h2j_frame* frames, uint8_t* arena,
                                                            uint32_t* tile_bits, int max_tiles) {
-    __shared__ uint32_t lds[kTile * kRow];
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
     const h2j_frame& f = frames[blockIdx.y];
@@ -359,15 +309,16 @@ __global__ void __launch_bounds__(kTile) h2j_k5b_tile_bits(const h2j_frame* fram
     if (b0 >= nblk) return;
     const int nb = min(kTile, nblk - b0);
     const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
-    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+    const uint8_t* base = arena + f.jcoef;
+    const uint8_t* tile = base + static_cast<size_t>(blockIdx.x) * kJTileBytes;
     load_codes(js, cl, false);
-    stage_tile(co, b0, nb, lds);
     __syncthreads();
     uint32_t bits = 0;
-    if (static_cast<int>(threadIdx.x) < nb) {
-        const int bi = b0 + threadIdx.x;
-        const uint32_t* row = lds + threadIdx.x * kRow;
-        bits = block_bits(cl, row, coef_at(row, 0) - prev_dc(co, lds, b0, bi), (bi % 6) < 4 ? 0 : 1);
+    const int t = threadIdx.x;
+    if (t < nb) {
+        const int bi = b0 + t;
+        bits = block_bits(cl, reinterpret_cast<const uint32_t*>(tile), tile[kJCntOff + t], t,
+                          dc_of(base, bi) - prev_dc(base, bi), (bi % 6) < 4 ? 0 : 1);
     }
     uint32_t total;
     wg_excl_scan(bits, sh, total);
@@ -457,7 +408,6 @@ struct BitSink {
 
 __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, uint8_t* arena,
                                                       const uint32_t* tile_bits, int max_tiles, uint8_t* seg) {
-    __shared__ uint32_t lds[kTile * kRow];
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
     const h2j_frame& f = frames[blockIdx.y];
@@ -467,19 +417,21 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
     if (js->seg_off == ~0ull) return;  // pool overflow: host reports the frame as failed
     const int nb = min(kTile, nblk - b0);
-    const int16_t* co = reinterpret_cast<const int16_t*>(arena + f.jcoef);
+    const uint8_t* base = arena + f.jcoef;
+    const uint8_t* tile = base + static_cast<size_t>(blockIdx.x) * kJTileBytes;
+    const uint32_t* sym = reinterpret_cast<const uint32_t*>(tile);
     load_codes(js, cl, true);
-    stage_tile(co, b0, nb, lds);
     __syncthreads();
-    const bool mine = static_cast<int>(threadIdx.x) < nb;
-    const int bi = b0 + threadIdx.x;
-    const uint32_t* row = lds + threadIdx.x * kRow;
+    const int t = threadIdx.x;
+    const bool mine = t < nb;
+    const int bi = b0 + t;
     const int tab = (bi % 6) < 4 ? 0 : 1;
-    int diff = 0;
+    int diff = 0, cnt = 0;
     uint32_t bits = 0;
     if (mine) {
-        diff = coef_at(row, 0) - prev_dc(co, lds, b0, bi);
-        bits = block_bits(cl, row, diff, tab);
+        diff = dc_of(base, bi) - prev_dc(base, bi);
+        cnt = tile[kJCntOff + t];
+        bits = block_bits(cl, sym, cnt, t, diff, tab);
     }
     uint32_t total;
     const uint32_t ex = wg_excl_scan(bits, sh, total);
@@ -496,21 +448,12 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     if (nd) s.put(static_cast<uint32_t>(diff < 0 ? diff - 1 : diff) & ((1u << nd) - 1u), nd);
     const uint8_t* al = cl.len[2 + tab];
     const uint16_t* ac = cl.code[2 + tab];
-    uint64_t m = ac_mask(row);
-    int prev = 0;
-    while (m) {
-        const int i = __ffsll(static_cast<unsigned long long>(m)) - 1;
-        m &= m - 1;
-        int run = i - prev - 1;
-        prev = i;
-        for (; run >= 16; run -= 16) s.put(ac[0xF0], al[0xF0]);
-        const int v = coef_at(row, i);
-        const int n = nbits16(v);
-        const int sym = (run << 4) | n;
-        s.put(ac[sym], al[sym]);
-        s.put(static_cast<uint32_t>(v < 0 ? v - 1 : v) & ((1u << n) - 1u), n);
+    for (int k = 0; k < cnt; k++) {
+        const uint32_t w = sym[k * kTile + t];
+        const int sv = static_cast<int>(w & 0xFF), n = static_cast<int>((w >> 8) & 15);
+        s.put(ac[sv], al[sv]);
+        if (n) s.put(w >> 12, n);
     }
-    if (prev < 63) s.put(ac[0], al[0]);
     if (bi == nblk - 1) {
         const int pad = (8 - static_cast<int>((bit0 + bits) & 7)) & 7;  // FFmpeg: pad with 1-bits
         if (pad) s.put((1u << pad) - 1u, pad);
@@ -533,8 +476,8 @@ int h2j_gpu_histogram(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int tiles = (b->max_mcu * 6 + kTile - 1) / kTile;
-    hipLaunchKernelGGL(h2j_k4d_histogram, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena);
-    return check(hipGetLastError(), "h2j_k4d_histogram");
+    hipLaunchKernelGGL(h2j_k4e_dc_hist, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena);
+    return check(hipGetLastError(), "h2j_k4e_dc_hist");
 }
 
 int h2j_gpu_entropy(const h2j_gpu_batch* b, void* stream) {

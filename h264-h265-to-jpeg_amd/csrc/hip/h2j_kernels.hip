@@ -32,6 +32,7 @@
 #include <cstring>
 
 #include "h2j_gpu.h"
+#include "jpeg_tile.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -1364,15 +1365,23 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     const h2j_tu tu = s.tus[t];
                     h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? bdc : bdy, s, lane);
                 }
-                // ---- store the macroblock
+                // ---- store the macroblock: one aligned 4-sample (luma) / 2-sample (chroma) store
+                // per lane, 16 contiguous bytes per row, instead of byte stores
                 {
                     const int r = lane >> 2, c4 = (lane & 3) * 4;
                     Pel* d = PY + (gy + r) * sty + gx + c4;
-                    for (int k = 0; k < 4; k++) d[k] = static_cast<Pel>(s.wy[r + 1][c4 + k + 1]);
+                    const uint32_t y0 = s.wy[r + 1][c4 + 1], y1 = s.wy[r + 1][c4 + 2];
+                    const uint32_t y2 = s.wy[r + 1][c4 + 3], y3 = s.wy[r + 1][c4 + 4];
                     const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
                     Pel* e = PC[c] + (cy + rr) * stc + cx + c2;
-                    e[0] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 1]);
-                    e[1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
+                    const uint32_t u0 = s.wc[c][rr + 1][c2 + 1], u1 = s.wc[c][rr + 1][c2 + 2];
+                    if (sizeof(Pel) == 1) {
+                        *reinterpret_cast<uint32_t*>(d) = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
+                        *reinterpret_cast<uint16_t*>(e) = static_cast<uint16_t>(u0 | (u1 << 8));
+                    } else {
+                        *reinterpret_cast<uint2*>(d) = make_uint2(y0 | (y1 << 16), y2 | (y3 << 16));
+                        *reinterpret_cast<uint32_t*>(e) = u0 | (u1 << 16);
+                    }
                 }
             }
             // bottom row for the MB row below; right column becomes the next MB's left column
@@ -2441,6 +2450,8 @@ constexpr int kAvcDbWaves = 16;
 struct DbWin {
     uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
     uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
+    uint16_t py[16][12];    // previous MB, columns 0..11 (final, not yet stored)
+    uint16_t pc[2][8][8];   // previous MB, chroma columns 0..6 (+ pad)
 };
 
 template <typename Pel>
@@ -2514,12 +2525,6 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
         const bool from_band = nbands > 1 && band > 0 && row == rbeg;
         const bool to_band = nbands > 1 && band < nbands - 1 && row == rend - 1;
         const uint64_t o_xin = o_xl + 12ull * (band - 1) * width, o_xout = o_xl + 12ull * band * width;
-        // stores of a boundary row go through to the coherence point (the band below writes the
-        // same bottom rows once its top edges are filtered, possibly from another XCD)
-        auto put = [&](Pel* p, Pel v) __attribute__((always_inline)) {
-            if (to_band) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else *p = v;
-        };
         for (int mx = 0; mx < mbw; mx++) {
             if (from_band) {
                 const uint32_t need = static_cast<uint32_t>(mbw + min(mx + 2, mbw));
@@ -2681,32 +2686,62 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
             lmf = mf;
             lqp = mqp;
             lsaddr = static_cast<int>(ufl(static_cast<uint32_t>(SC->slice_addr_rs)));
-            // write back: left columns (MB x-1), rows above (MB row y-1), the MB itself
+            // write back, every sample once and only when final, 4 (luma) / 4 (chroma) samples per
+            // lane store.  A sample of MB (x, y) is last changed by this MB's own edges, by MB
+            // (x + 1, y)'s left edge (columns 13..15, chroma 7) or by MB (x, y + 1)'s top edge
+            // (rows 13..15, chroma 7).  So at MB (x, y): rows 12..15 of MB (x, y - 1) (top edge
+            // just filtered; its right columns were finished by the row above) and rows 0..11 of
+            // MB (x - 1, y) (left edge just filtered; 0..15 on the picture's last row, where no row
+            // follows) are final; the last MB of a row also stores its own rows.  Rows 12..15 of a
+            // band's last row are stored by the band below (they reach it through the boundary
+            // buffer), so the two workgroups never write the same line.
             {
-                const int r = lane >> 2, c4 = (lane & 3) * 4;
-                Pel* d = PY + (row * 16 + r) * sty + mx * 16 + c4;
-#pragma unroll
-                for (int k = 0; k < 4; k++) put(d + k, static_cast<Pel>(w.y[r + 4][c4 + k + 4]));
-                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
-                Pel* e = PC[c] + (row * 8 + rr) * stc + mx * 8 + c2;
-                put(e, static_cast<Pel>(w.c[c][rr + 2][c2 + 2]));
-                put(e + 1, static_cast<Pel>(w.c[c][rr + 2][c2 + 3]));
-                if (active && mx > 0) {
-                    if (lane < 48) {  // luma columns -3..-1, rows 0..15
-                        const int lr = lane / 3, lc = lane - lr * 3 + 1;
-                        put(PY + (row * 16 + lr) * sty + mx * 16 + lc - 4, static_cast<Pel>(w.y[lr + 4][lc]));
-                    } else {  // chroma column -1, rows 0..7, both comps
-                        const int cc = (lane - 48) >> 3, cr = lane & 7;
-                        put(PC[cc] + (row * 8 + cr) * stc + mx * 8 - 1, static_cast<Pel>(w.c[cc][cr + 2][1]));
-                    }
+                const bool last_row = row == mbh - 1;
+                const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
+                auto st4 = [&](Pel* d, uint32_t a, uint32_t b, uint32_t c2_, uint32_t d2) __attribute__((always_inline)) {
+                    if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = a | (b << 8) | (c2_ << 16) | (d2 << 24);
+                    else *reinterpret_cast<uint2*>(d) = make_uint2(a | (b << 16), c2_ | (d2 << 16));
+                };
+                if (row > 0 && lane < 16) {  // luma rows 12..15 of the MB above
+                    const int tr = lane >> 2, c4 = (lane & 3) * 4;
+                    st4(PY + (row * 16 - 4 + tr) * sty + mx * 16 + c4, w.y[tr][c4 + 4], w.y[tr][c4 + 5], w.y[tr][c4 + 6],
+                        w.y[tr][c4 + 7]);
+                } else if (row > 0 && lane >= 16 && lane < 24) {  // chroma rows 6..7 of the MB above
+                    const int k = lane - 16, cc = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
+                    st4(PC[cc] + (row * 8 - 2 + cr) * stc + mx * 8 + c4, w.c[cc][cr][c4 + 2], w.c[cc][cr][c4 + 3],
+                        w.c[cc][cr][c4 + 4], w.c[cc][cr][c4 + 5]);
                 }
-                if (active && row > 0) {
-                    if (lane < 48) {  // luma rows -3..-1, columns 0..15
-                        const int tr = lane >> 4, tc = lane & 15;
-                        PY[(row * 16 - 3 + tr) * sty + mx * 16 + tc] = static_cast<Pel>(w.y[tr + 1][tc + 4]);
-                    } else {  // chroma row -1, columns 0..7, both comps
-                        const int cc = (lane - 48) >> 3, ck = lane & 7;
-                        PC[cc][(row * 8 - 1) * stc + mx * 8 + ck] = static_cast<Pel>(w.c[cc][1][ck + 2]);
+                if (mx > 0 && lane < nr * 4) {  // luma of the previous MB: columns 0..11 saved, 12..15 in the window
+                    const int r = lane >> 2, c4 = (lane & 3) * 4;
+                    uint32_t v0, v1, v2, v3;
+                    if (c4 < 12) { v0 = w.py[r][c4]; v1 = w.py[r][c4 + 1]; v2 = w.py[r][c4 + 2]; v3 = w.py[r][c4 + 3]; }
+                    else { v0 = w.y[r + 4][0]; v1 = w.y[r + 4][1]; v2 = w.y[r + 4][2]; v3 = w.y[r + 4][3]; }
+                    st4(PY + (row * 16 + r) * sty + (mx - 1) * 16 + c4, v0, v1, v2, v3);
+                }
+                if (mx > 0 && lane < 4 * ncr) {  // chroma of the previous MB: column 7 in the window
+                    const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
+                    const uint32_t v3 = c4 ? w.c[cc][cr + 2][1] : w.pc[cc][cr][3];
+                    st4(PC[cc] + (row * 8 + cr) * stc + (mx - 1) * 8 + c4, w.pc[cc][cr][c4], w.pc[cc][cr][c4 + 1],
+                        w.pc[cc][cr][c4 + 2], v3);
+                }
+                // this MB's columns 0..11 / chroma 0..6 wait for the next MB (in-order LDS: the reads
+                // above have returned their values before these writes land)
+                for (int i = lane; i < 192; i += 64) w.py[i / 12][i % 12] = w.y[i / 12 + 4][i % 12 + 4];
+                if (lane < 64) {
+                    const int cc = lane >> 5, k = lane & 31, cr = k >> 2, c2 = (k & 3) * 2;
+                    w.pc[cc][cr][c2] = w.c[cc][cr + 2][c2 + 2];
+                    w.pc[cc][cr][c2 + 1] = w.c[cc][cr + 2][c2 + 3];
+                }
+                if (mx == mbw - 1) {  // the row's last MB: nothing to its right, store its rows now
+                    if (lane < nr * 4) {
+                        const int r = lane >> 2, c4 = (lane & 3) * 4;
+                        st4(PY + (row * 16 + r) * sty + mx * 16 + c4, w.y[r + 4][c4 + 4], w.y[r + 4][c4 + 5],
+                            w.y[r + 4][c4 + 6], w.y[r + 4][c4 + 7]);
+                    }
+                    if (lane < 4 * ncr) {
+                        const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
+                        st4(PC[cc] + (row * 8 + cr) * stc + mx * 8 + c4, w.c[cc][cr + 2][c4 + 2], w.c[cc][cr + 2][c4 + 3],
+                            w.c[cc][cr + 2][c4 + 4], w.c[cc][cr + 2][c4 + 5]);
                     }
                 }
             }
@@ -3118,6 +3153,116 @@ DEVI void jpeg_block(const h2j_frame& f, uint8_t* arena, int bi) {
     }
 }
 
+// ---- K4c, symbol form (the production path).  One workgroup = one 256-block tile of a
+// frame; a lane computes its block's FDCT + quantiser as jpeg_block, then, instead of the dense
+// int16 plane, writes the block's JPEG symbols: its quantised DC (int16) and the AC symbols in
+// emission order -- ZRL / run-size symbols with their magnitude bits, EOB -- one uint32 each
+// (bits 0-7 symbol, 8-11 magnitude bit count, 12-27 magnitude bits), stored symbol-major
+// ([k][lane]: the readers in h2j_entropy.hip load symbol k of 64 blocks with one coalesced load).
+// The AC symbol histograms (the optimal Huffman tables' input) are counted here in LDS, so the
+// coefficients are never re-read: K5b / K5d consume the ~4 B per symbol instead of 128 B per
+// block.  Tile layout (kJTileBytes, jpeg_tile.h conventions shared with h2j_entropy.hip):
+// [kJSymMax][256] uint32 | count[256] uint8 | dc[256] int16.
+template <typename Pel>
+DEVI void jpeg_block_coefs(const h2j_frame& f, const uint8_t* arena, int bi, int16_t (&out)[64]) {
+    const int mbw = (f.out_w + 15) >> 4;
+    const int mcu = bi / 6, b = bi % 6;
+    const int mx = mcu % mbw, my = mcu / mbw;
+    int c, x0, y0;
+    if (b < 4) { c = 0; x0 = mx * 16 + (b & 1) * 8; y0 = my * 16 + (b >> 1) * 8; }
+    else { c = b - 3; x0 = mx * 8; y0 = my * 8; }
+    int16_t blk[64];
+    const int shc = c ? 1 : 0;
+    const int pw = f.out_w >> shc, ph = f.out_h >> shc;
+    const int cx = f.crop_x >> shc, cy = f.crop_y >> shc;
+    if (sizeof(Pel) == 1 && x0 + 8 <= pw && y0 + 8 <= ph && ((cx + x0) & 7) == 0 && (f.pic_stride[c] & 7) == 0) {
+        // the block lies inside the picture: eight 8-byte row loads
+        const uint8_t* p = arena + f.pic2 + f.pic_off[c] + static_cast<size_t>(cy + y0) * f.pic_stride[c] + cx + x0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint2 v = *reinterpret_cast<const uint2*>(p + static_cast<size_t>(j) * f.pic_stride[c]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                blk[j * 8 + i] = static_cast<int16_t>((v.x >> (8 * i)) & 0xFF);
+                blk[j * 8 + 4 + i] = static_cast<int16_t>((v.y >> (8 * i)) & 0xFF);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) blk[j * 8 + i] = static_cast<int16_t>(jpeg_sample<Pel>(f, arena, c, x0 + i, y0 + j));
+    }
+    fdct_ap922(blk);
+    const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
+    out[0] = static_cast<int16_t>(((blk[0] >> 2) + 8) / 16);
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+        const int i = kZigzag[k];
+        const int X = blk[i];
+        const unsigned a = static_cast<unsigned>(X < 0 ? -X : X);
+        unsigned tt = a + js->b16[i];
+        tt = tt > 65535u ? 65535u : tt;
+        int L = static_cast<int>((tt * js->q16[i]) >> 16);
+        L = L > 1023 ? 1023 : L;
+        out[k] = static_cast<int16_t>(X < 0 ? -L : L);
+    }
+}
+
+DEVI int jnbits(int v) {
+    const unsigned a = static_cast<unsigned>(v < 0 ? -v : v);
+    return a ? 32 - __clz(a) : 0;
+}
+
+__global__ void __launch_bounds__(256) h2j_k4c_fdct_sym(const h2j_frame* frames, uint8_t* arena) {
+    __shared__ unsigned hist[2][256];
+    const h2j_frame& f = frames[blockIdx.y];
+    const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
+    const int b0 = blockIdx.x * 256;
+    if (b0 >= nblk) return;
+    for (int i = threadIdx.x; i < 512; i += 256) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const int t = threadIdx.x, bi = b0 + t;
+    uint8_t* tile = arena + f.jcoef + static_cast<size_t>(blockIdx.x) * kJTileBytes;
+    uint32_t* sym = reinterpret_cast<uint32_t*>(tile);
+    if (bi < nblk) {
+        int16_t out[64];
+        if (f.bit_depth == 8) jpeg_block_coefs<uint8_t>(f, arena, bi, out);
+        else jpeg_block_coefs<uint16_t>(f, arena, bi, out);
+        const int tab = (bi % 6) < 4 ? 0 : 1;
+        int n = 0, prev = 0;
+#pragma unroll
+        for (int k = 1; k < 64; k++) {
+            const int v = out[k];
+            if (v) {
+                int run = k - prev - 1;
+                prev = k;
+                for (; run >= 16; run -= 16) {
+                    sym[n++ * 256 + t] = 0xF0u;
+                    atomicAdd(&hist[tab][0xF0], 1u);
+                }
+                const int nb = jnbits(v);
+                const int s2 = (run << 4) | nb;
+                const uint32_t mag = static_cast<uint32_t>(v < 0 ? v - 1 : v) & ((1u << nb) - 1u);
+                sym[n++ * 256 + t] = static_cast<uint32_t>(s2) | (static_cast<uint32_t>(nb) << 8) | (mag << 12);
+                atomicAdd(&hist[tab][s2], 1u);
+            }
+        }
+        if (prev < 63) {
+            sym[n++ * 256 + t] = 0u;  // EOB
+            atomicAdd(&hist[tab][0], 1u);
+        }
+        tile[kJCntOff + t] = static_cast<uint8_t>(n);
+        reinterpret_cast<int16_t*>(tile + kJDcOff)[t] = out[0];
+    }
+    __syncthreads();
+    h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const unsigned v = (&hist[0][0])[i];
+        if (v) atomicAdd(&js->hist[2 + (i >> 8)][i & 255], v);
+    }
+}
+
 __global__ void __launch_bounds__(256) h2j_k4c_fdct_quant(const h2j_frame* frames, uint8_t* arena) {
     const h2j_frame& f = frames[blockIdx.y];
     const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
@@ -3397,10 +3542,14 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     r = check(hipGetLastError(), "h2j_k4b_ratecontrol");
     if (r) return r;
     const int nblk = mbs * 6;
-    hipLaunchKernelGGL(h2j_k4c_fdct_quant, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
-    r = check(hipGetLastError(), "h2j_k4c_fdct_quant");
+    if (b->jpeg_dense) {  // inspection path (h2j_engine_jpeg_coeffs): the dense int16 plane
+        hipLaunchKernelGGL(h2j_k4c_fdct_quant, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+        return check(hipGetLastError(), "h2j_k4c_fdct_quant");
+    }
+    hipLaunchKernelGGL(h2j_k4c_fdct_sym, dim3((nblk + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    r = check(hipGetLastError(), "h2j_k4c_fdct_sym");
     if (r) return r;
-    return h2j_gpu_histogram(b, stream);
+    return h2j_gpu_histogram(b, stream);  // DC histograms
 }
 
 }  // extern "C"

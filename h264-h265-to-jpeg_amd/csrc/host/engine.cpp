@@ -395,10 +395,11 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
             off = align_up(off + (ysz + 2 * csz) * pel, 256);
         }
     s.jcoef_base = off;
-    for (int k = 0; k < nf; k++) {
+    for (int k = 0; k < nf; k++) {  // dense int16 plane (inspection) or the JPEG symbol tiles
         h2j_frame& f = s.frames[k];
         f.jcoef = off;
-        off = align_up(off + static_cast<size_t>(((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4)) * 6 * 64 * 2, 256);
+        const size_t blocks = static_cast<size_t>(((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4)) * 6;
+        off = align_up(off + std::max(blocks * 64 * 2, (blocks + 255) / 256 * static_cast<size_t>(H2J_JTILE_BYTES)), 256);
     }
     s.jcoef_bytes = off - s.jcoef_base;
     for (int k = 0; k < nf; k++) {
@@ -520,6 +521,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     for (int k = 0; k < nf; k++)
         if (s.frames[k].codec == H2J_CODEC_HEVC) b.hevc_pels |= (s.frames[k].bit_depth > 8 || s.frames[k].bit_depth_c > 8) ? 2 : 1;
     b.arena = static_cast<uint8_t*>(s.d_arena.p);
+    b.jpeg_dense = entropy ? 0 : 1;
     b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
     b.seg_cap = entropy ? seg_cap : 0;
     b.seg_total = entropy ? static_cast<uint64_t*>(s.d_scratch.p) : nullptr;
@@ -633,12 +635,12 @@ std::vector<int> chunk_plan_throughput(int n) {
 }
 
 // GPU sub-chunks of a parsed range are bounded by an HBM estimate per slot (pictures, residual,
-// JPEG coefficients, payload pool: ~16 B per luma sample at 8 bits) and by 1024 pictures.
+// JPEG symbol tiles, payload pool: ~20 B per luma sample at 8 bits) and by 1024 pictures.
 constexpr double kSlotHbmBudget = 64e9;
 constexpr int kMaxGpuChunk = 1024;
 static double hbm_estimate(const FrameJob& j) {
     const double px = static_cast<double>(j.hdr.width) * j.hdr.height;
-    return px * (j.hdr.bit_depth > 8 ? 20.0 : 16.0) + (1 << 20);
+    return px * (j.hdr.bit_depth > 8 ? 24.0 : 20.0) + (1 << 20);
 }
 
 void Engine::start_threads() {

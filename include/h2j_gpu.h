@@ -50,6 +50,11 @@ int h2j_gpu_event_record(void *ev, void *stream);
 float h2j_gpu_event_elapsed_ms(void *start, void *stop);
 const char *h2j_gpu_last_error(void);
 
+/* JPEG symbol stream (production path): per frame, one tile of H2J_JTILE_BYTES per 256 blocks
+ * at h2j_frame.jcoef (the dense int16 plane occupies the same region on the inspection path). */
+#define H2J_JSYM_MAX 68
+#define H2J_JTILE_BYTES (H2J_JSYM_MAX * 256 * 4 + 256 + 512)
+
 /* One batch of pictures resident in HBM.  All pointers are device pointers. */
 typedef struct {
     int32_t nframes;
@@ -76,6 +81,7 @@ typedef struct {
     uint64_t seg_cap;           /* pool bytes */
     uint32_t *tile_bits;        /* scratch: nframes x ceil(max_mcu*6/256) */
     uint64_t *seg_total;        /* device scalar: pool bytes used (16-byte units x16) */
+    int32_t jpeg_dense;         /* 1: K4 writes the dense int16 coefficient plane (inspection), no K5 */
 } h2j_gpu_batch;
 
 /* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
