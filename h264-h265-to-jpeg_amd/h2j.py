@@ -123,12 +123,17 @@ class Engine:
         bufs = [_u8(s) for s in streams]
         ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
         sizes = (ctypes.c_size_t * n)(*[len(s) for s in streams])
-        cap = sum(len(s) for s in streams) * 4 + n * (8 << 20)
-        out = (ctypes.c_uint8 * cap)()
+        # JPEG bytes: usually well under 1 MiB per still; on -50 (output buffer too small) retry larger
+        cap = sum(max(1 << 20, 4 * len(s)) for s in streams)
         offs = (ctypes.c_size_t * n)()
         lens = (ctypes.c_size_t * n)()
         status = (ctypes.c_int * n)()
-        rc = self._lib.h2j_engine_transcode(self._h, n, ptrs, sizes, out, cap, offs, lens, status)
+        for _ in range(4):
+            out = (ctypes.c_uint8 * cap)()
+            rc = self._lib.h2j_engine_transcode(self._h, n, ptrs, sizes, out, cap, offs, lens, status)
+            if not any(status[i] == -50 for i in range(n)):
+                break
+            cap *= 4
         if rc < 0 and rc != -3:
             raise RuntimeError(f"h2j_engine_transcode failed ({rc}): {self.error()}")
         mv = memoryview(out)
@@ -157,7 +162,7 @@ class Engine:
             bufs = [_u8(s) for s in streams]
             ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
             sizes = (ctypes.c_size_t * n)(*[len(s) for s in streams])
-            cap = sum(len(s) for s in streams) * 4 + n * (8 << 20)
+            cap = sum(max(2 << 20, 4 * len(s)) for s in streams)
             out = (ctypes.c_uint8 * cap)()
             offs, lens, status = (ctypes.c_size_t * n)(), (ctypes.c_size_t * n)(), (ctypes.c_int * n)()
             held.append((bufs, ptrs, sizes, out, offs, lens, status, n))

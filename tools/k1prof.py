@@ -16,7 +16,8 @@ for path in files:
     data = open(path, "rb").read()
     eng.transcode([data] * 8)
     hip.h2j_gpu_prof(buf, 16, 1)
-    outs = eng.transcode([data] * n)
+    # over 256 pictures: the asynchronous path (one 1024-picture chunk, the K1 picture pool)
+    outs = eng.transcode_async([[data] * n])[0] if n > 256 else eng.transcode([data] * n)
     assert all(o is not None for o in outs)
     st = eng.stats()
     if hip.h2j_gpu_prof(buf, 16, 1) != 0:
