@@ -1494,6 +1494,9 @@ __host__ __device__ constexpr size_t k1_fixed_lds(int waves) { return sizeof(QWa
 // intraPredAngle / invAngle (H.265 Tables 8-4, 8-5) from the mode with scalar
 // arithmetic on packed constants (no memory round trip per TB):
 // d = m - 26 (vertical) or 10 - m (horizontal), angle = sign(d) * mag[|d|].
+// 24-bit signed multiply (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate): every use
+// multiplies a sample (<= 16 bits) or a window / angle index by a small factor
+DEVI int m24(int a, int b) { return __mul24(a, b); }
 DEVI int hevc_angle(int m) {
     const int d = m >= 18 ? m - 26 : 10 - m;
     const int k = d < 0 ? -d : d;
@@ -1565,7 +1568,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             const int j = le ? 64 * ch + 63 - static_cast<int>(__clzll(le)) : fb[ch];
             const int xn = j > 2 * n ? ox + (j - 2 * n - 1) : ox - 1;
             const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
-            const int idx = yn < 0 ? topo + xn + 1 : (xn < 0 ? lefto + yn : yn * S + xn);
+            const int idx = yn < 0 ? topo + xn + 1 : (xn < 0 ? lefto + yn : m24(yn, S) + xn);
             const int raw = body[idx];  // unconditional: idx stays inside the wave's window
             const int v = any ? raw : (1 << (bd - 1));
             if (ch == 0) v0 = v;
@@ -1599,7 +1602,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         if (mode == 0) {
             const int tr = __builtin_amdgcn_readlane(r, 3 * n + 1), bl = __builtin_amdgcn_readlane(r, n - 1);
             const int left = __shfl(r, 2 * n - 1 - y, 64), above = __shfl(r, 2 * n + 1 + x, 64);
-            pv = ((n - 1 - x) * left + (x + 1) * tr + (n - 1 - y) * above + (y + 1) * bl + n) >> (log2n + 1);
+            pv = (m24(n - 1 - x, left) + m24(x + 1, tr) + m24(n - 1 - y, above) + m24(y + 1, bl) + n) >> (log2n + 1);
         } else if (mode == 1) {
             const int above = __shfl(r, 2 * n + 1 + x, 64), left = __shfl(r, 2 * n - 1 - y, 64);
             pv = dc;
@@ -1614,21 +1617,21 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             const int sgn = vert ? 1 : -1;
             const bool bnd = edge && (mode == 26 || mode == 10);
             const int a = vert ? y : x, b = vert ? x : y;
-            const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+            const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
             const int k1 = b + idx + 1, k2 = k1 + 1;
-            const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
-            const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
-            const int r1 = __shfl(r, 2 * n + sgn * o1, 64), r2 = __shfl(r, 2 * n + sgn * o2, 64);
-            pv = ((32 - fr) * r1 + fr * r2 + 16) >> 5;
+            const int o1 = k1 >= 0 ? k1 : -((m24(k1, inv) + 128) >> 8);
+            const int o2 = k2 >= 0 ? k2 : -((m24(k2, inv) + 128) >> 8);
+            const int r1 = __shfl(r, 2 * n + (vert ? o1 : -o1), 64), r2 = __shfl(r, 2 * n + (vert ? o2 : -o2), 64);
+            pv = (m24(32 - fr, r1) + m24(fr, r2) + 16) >> 5;
             if (bnd) {
-                const int side = __shfl(r, 2 * n - sgn * (a + 1), 64);
+                const int side = __shfl(r, 2 * n + (vert ? -(a + 1) : a + 1), 64);
                 const int e = clip3(0, maxv, __builtin_amdgcn_readlane(r, 2 * n + sgn) +
                                                  ((side - __builtin_amdgcn_readlane(r, 2 * n)) >> 1));
                 pv = b == 0 ? e : pv;
             }
         }
         if (i < nn) {
-            int16_t* d = body + (oy + y) * S + ox + x;
+            int16_t* d = body + m24(oy + y, S) + ox + x;
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
         wave_sync();
@@ -1645,8 +1648,8 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             for (int k = lane; k < L; k += 64) {
                 int v;
                 if (k == 0 || k == 4 * n || k == 2 * n) v = s.sub[k];
-                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = ((63 - y) * corner + (y + 1) * bl + 32) >> 6; }
-                else { const int x = k - 2 * n - 1; v = ((63 - x) * corner + (x + 1) * tr + 32) >> 6; }
+                else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = (m24(63 - y, corner) + m24(y + 1, bl) + 32) >> 6; }
+                else { const int x = k - 2 * n - 1; v = (m24(63 - x, corner) + m24(x + 1, tr) + 32) >> 6; }
                 s.ref[k] = v;
             }
         } else {
@@ -1663,9 +1666,9 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         const int tr = R[3 * n + 1], bl = R[n - 1];
         for (int i = lane; i < nn; i += 64) {
             const int x = i & (n - 1), y = i >> log2n;
-            const int pv = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * tr + (n - 1 - y) * R[2 * n + 1 + x] +
-                            (y + 1) * bl + n) >> (log2n + 1);
-            int16_t* d = body + (oy + y) * S + ox + x;
+            const int pv = (m24(n - 1 - x, R[2 * n - 1 - y]) + m24(x + 1, tr) + m24(n - 1 - y, R[2 * n + 1 + x]) +
+                            m24(y + 1, bl) + n) >> (log2n + 1);
+            int16_t* d = body + m24(oy + y, S) + ox + x;
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
     } else if (mode == 1) {
@@ -1677,7 +1680,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                 else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
                 else pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
             }
-            int16_t* d = body + (oy + y) * S + ox + x;
+            int16_t* d = body + m24(oy + y, S) + ox + x;
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
     } else {
@@ -1690,18 +1693,18 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         for (int i = lane; i < nn; i += 64) {
             const int x = i & (n - 1), y = i >> log2n;
             const int a = vert ? y : x, b = vert ? x : y;  // a: distance from the main reference, b: position along it
-            const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+            const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
             const int k1 = b + idx + 1, k2 = k1 + 1;
             // negative k projects onto the side reference through invAngle; both forms are
             // computed and selected (no divergent branch)
-            const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
-            const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
-            int pv = ((32 - fr) * R[2 * n + sgn * o1] + fr * R[2 * n + sgn * o2] + 16) >> 5;
+            const int o1 = k1 >= 0 ? k1 : -((m24(k1, inv) + 128) >> 8);
+            const int o2 = k2 >= 0 ? k2 : -((m24(k2, inv) + 128) >> 8);
+            int pv = (m24(32 - fr, R[2 * n + (vert ? o1 : -o1)]) + m24(fr, R[2 * n + (vert ? o2 : -o2)]) + 16) >> 5;
             if (bnd) {
-                const int e = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n - sgn * (a + 1)] - R[2 * n]) >> 1));
+                const int e = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n + (vert ? -(a + 1) : a + 1)] - R[2 * n]) >> 1));
                 pv = b == 0 ? e : pv;
             }
-            int16_t* d = body + (oy + y) * S + ox + x;
+            int16_t* d = body + m24(oy + y, S) + ox + x;
             *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
         }
     }
@@ -1731,7 +1734,7 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
     const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
     const int top_cb = static_cast<int>(tcb - bcb), left_cb = static_cast<int>(lcb - bcb);
     const int top_cr = static_cast<int>(tcr - bcr), left_cr = static_cast<int>(lcr - bcr);
-    const int in = yn * S + xn;
+    const int in = m24(yn, S) + xn;
     const int icb = yn < 0 ? top_cb + xn + 1 : (xn < 0 ? left_cb + yn : in);
     const int icr = yn < 0 ? top_cr + xn + 1 : (xn < 0 ? left_cr + yn : in);
     const int half = 1 << (u.bdc - 1);
@@ -1750,27 +1753,26 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
         const int trr = __builtin_amdgcn_readlane(rr, 3 * n + 1), blr = __builtin_amdgcn_readlane(rr, n - 1);
         const int il = 2 * n - 1 - y, ia = 2 * n + 1 + x;
         const int lb = __shfl(rb, il, 64), ab = __shfl(rb, ia, 64), lr = __shfl(rr, il, 64), ar = __shfl(rr, ia, 64);
-        pb = ((n - 1 - x) * lb + (x + 1) * trb + (n - 1 - y) * ab + (y + 1) * blb + n) >> (log2n + 1);
-        pr = ((n - 1 - x) * lr + (x + 1) * trr + (n - 1 - y) * ar + (y + 1) * blr + n) >> (log2n + 1);
+        pb = (m24(n - 1 - x, lb) + m24(x + 1, trb) + m24(n - 1 - y, ab) + m24(y + 1, blb) + n) >> (log2n + 1);
+        pr = (m24(n - 1 - x, lr) + m24(x + 1, trr) + m24(n - 1 - y, ar) + m24(y + 1, blr) + n) >> (log2n + 1);
     } else if (mode == 1) {
         pb = dcb;
         pr = dcr;
     } else {
         const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
         const bool vert = mode >= 18;
-        const int sgn = vert ? 1 : -1;
         const int a = vert ? y : x, b = vert ? x : y;
-        const int pos = (a + 1) * angle, idx = pos >> 5, fr = pos & 31;
+        const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
         const int k1 = b + idx + 1, k2 = k1 + 1;
-        const int o1 = k1 >= 0 ? k1 : -((k1 * inv + 128) >> 8);
-        const int o2 = k2 >= 0 ? k2 : -((k2 * inv + 128) >> 8);
-        const int i1 = 2 * n + sgn * o1, i2 = 2 * n + sgn * o2;
-        pb = ((32 - fr) * __shfl(rb, i1, 64) + fr * __shfl(rb, i2, 64) + 16) >> 5;
-        pr = ((32 - fr) * __shfl(rr, i1, 64) + fr * __shfl(rr, i2, 64) + 16) >> 5;
+        const int o1 = k1 >= 0 ? k1 : -((m24(k1, inv) + 128) >> 8);
+        const int o2 = k2 >= 0 ? k2 : -((m24(k2, inv) + 128) >> 8);
+        const int i1 = 2 * n + (vert ? o1 : -o1), i2 = 2 * n + (vert ? o2 : -o2);
+        pb = (m24(32 - fr, __shfl(rb, i1, 64)) + m24(fr, __shfl(rb, i2, 64)) + 16) >> 5;
+        pr = (m24(32 - fr, __shfl(rr, i1, 64)) + m24(fr, __shfl(rr, i2, 64)) + 16) >> 5;
     }
     if (i < nn) {
-        int16_t* db = bcb + (oy + y) * S + ox + x;
-        int16_t* dr = bcr + (oy + y) * S + ox + x;
+        int16_t* db = bcb + m24(oy + y, S) + ox + x;
+        int16_t* dr = bcr + m24(oy + y, S) + ox + x;
         *db = static_cast<int16_t>(clip3(0, maxv, pb + (cbf_cb ? *db : 0)));
         *dr = static_cast<int16_t>(clip3(0, maxv, pr + (cbf_cr ? *dr : 0)));
     }
@@ -1804,10 +1806,10 @@ DEVI uint32_t lds_addr(const void* p) {
 DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* body, int lane) {
     if (grp == 0) {
         const int16_t* R = u.rplane(0);
-        const int cpr = Qc >> 3;
+        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;  // log2 of 16-B chunks per row
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-            const int idx = lane + 64 * j, yy = idx / cpr, xx = (idx - yy * cpr) * 8;
+            const int idx = lane + 64 * j, yy = idx >> lc, xx = (idx & ((1 << lc) - 1)) * 8;
             const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
             if (ok) lds_dma16(R + (Y0 + yy) * u.sty + X0 + xx, lds_addr(body + 512 * j));
             else *reinterpret_cast<uint4*>(body + idx * 8) = make_uint4(0, 0, 0, 0);
@@ -1815,7 +1817,8 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
     } else {
 #pragma unroll
         for (int k = 0; k < 4; k++) {  // (plane, half): 64 lanes x 2 samples
-            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e / Qc, xx = e - yy * Qc;
+            const int lq = __builtin_ctz(static_cast<unsigned>(Qc));
+            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e >> lq, xx = e & (Qc - 1);
             const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
             int16_t* dst = body + c * 256 + (k & 1) * 128;
             if (ok) lds_dma4(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx, lds_addr(dst));
@@ -1888,6 +1891,14 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                 if (!q_inside(cx, q)) continue;
                 const int qx = q & 1, qy = q >> 1;
                 const int X0 = CX0 + qx * Qc, Y0 = CY0 + qy * Qc;
+                {  // prefetch the row's next quadrant's residual into the other window (its last
+                   // reader, the previous quadrant's store, has finished reading it)
+                    int nc = cx, nqi = q;
+                    q_next(nc, nqi);
+                    lds_reads_done();
+                    if (nc < u.ctb_w)
+                        hevc_qres_dma(u, grp, nc * Sc + (nqi & 1) * Qc, row * Sc + (nqi >> 1) * Qc, Qc, w.body[cur ^ 1], lane);
+                }
                 // top quadrants need the row above (progress counts its quadrants, nq per CTB):
                 // the left one up to this CTB, the right one also the next CTB's bottom-left
                 // quadrant (whose top line is the right one's above-right reference)
@@ -1903,49 +1914,44 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                 }
                 PROF_LAP(0);
                 // neighbour arrays of the quadrant: one pass, lane = x of the line above and y of
-                // the column on the left; sources picked by uniform element offsets from the
-                // start of the group's LDS, one unconditional load each
+                // the column on the left, lane 0 also the top-left corner; sources picked by
+                // uniform element offsets from the start of the group's LDS, one unconditional
+                // load each, all loads of both components issued before the first write
                 {
                     int16_t* base = reinterpret_cast<int16_t*>(&w);
-                    for (int ci = 0; ci < ncomp; ci++) {
+                    int16_t tv[2], lv[2], cv[2];
+                    bool ta[2], la[2], cz[2];
+#pragma unroll
+                    for (int ci = 0; ci < 2; ci++) {
+                        if (ci >= ncomp) break;
                         QComp& C = w.cs[ci];
                         const int o_line = static_cast<int>(line + ci * (Wc + 64) - base);
                         const int o_qbot = static_cast<int>(C.qbot - base);
                         const int o_prev = static_cast<int>(C.prevR[pprev] - base);
                         const int o_qr = static_cast<int>(C.qright - base);
+                        const int o_cor = static_cast<int>(&C.corner - base);
                         const int x = lane, y = lane;
-                        bool ta;
-                        int to;
-                        if (qy == 0) { ta = row > 0 && X0 + x < Wc; to = o_line + X0 + x; }
-                        else { ta = qx * Qc + x < 2 * Qc; to = o_qbot + qx * Qc + x; }
-                        bool la;
-                        int lo;
-                        if (qx == 0) { la = cx > 0 && qy * Qc + y < Sc; lo = o_prev + qy * Qc + y; }
-                        else { la = y < Qc; lo = o_qr + y; }
-                        const int16_t tv = base[ta ? to : o_qbot];
-                        const int16_t lv = base[la ? lo : o_qbot];
-                        if (lane < 2 * Qc) {
-                            C.top[lane + 1] = ta ? tv : int16_t(0);
-                            C.left[lane] = la ? lv : int16_t(0);
-                        }
-                        if (lane == 0) {  // top-left corner
-                            int16_t cv = 0;
-                            if (qy == 0) {
-                                if (row > 0 && X0 > 0) cv = qx == 0 ? C.corner : line[ci * (Wc + 64) + X0 - 1];
-                            } else {
-                                cv = qx == 0 ? (cx > 0 ? C.prevR[pprev][Qc - 1] : int16_t(0)) : C.qbot[Qc - 1];
-                            }
-                            C.top[0] = cv;
-                        }
+                        int to, lo, co;
+                        if (qy == 0) { ta[ci] = row > 0 && X0 + x < Wc; to = o_line + X0 + x; }
+                        else { ta[ci] = qx * Qc + x < 2 * Qc; to = o_qbot + qx * Qc + x; }
+                        if (qx == 0) { la[ci] = cx > 0 && qy * Qc + y < Sc; lo = o_prev + qy * Qc + y; }
+                        else { la[ci] = y < Qc; lo = o_qr + y; }
+                        if (qy == 0) { cz[ci] = !(row > 0 && X0 > 0); co = qx == 0 ? o_cor : o_line + X0 - 1; }
+                        else { cz[ci] = qx == 0 && cx == 0; co = qx == 0 ? o_prev + Qc - 1 : o_qbot + Qc - 1; }
+                        tv[ci] = base[ta[ci] ? to : o_qbot];
+                        lv[ci] = base[la[ci] ? lo : o_qbot];
+                        cv[ci] = base[cz[ci] ? o_qbot : co];
                     }
-                }
-                {  // prefetch the row's next quadrant's residual into the other window (its last
-                   // reader, the previous quadrant's store, has finished reading it)
-                    int nc = cx, nqi = q;
-                    q_next(nc, nqi);
-                    lds_reads_done();
-                    if (nc < u.ctb_w)
-                        hevc_qres_dma(u, grp, nc * Sc + (nqi & 1) * Qc, row * Sc + (nqi >> 1) * Qc, Qc, w.body[cur ^ 1], lane);
+#pragma unroll
+                    for (int ci = 0; ci < 2; ci++) {
+                        if (ci >= ncomp) break;
+                        QComp& C = w.cs[ci];
+                        if (lane < 2 * Qc) {
+                            C.top[lane + 1] = ta[ci] ? tv[ci] : int16_t(0);
+                            C.left[lane] = la[ci] ? lv[ci] : int16_t(0);
+                        }
+                        if (lane == 0) C.top[0] = cz[ci] ? int16_t(0) : cv[ci];
+                    }
                 }
                 wave_sync();
                 PROF_LAP(1);
@@ -1995,16 +2001,19 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                 // landed by now (issued a whole quadrant ago), retire it before the stores
                 lds_dma_wait();
                 const int wq = min(Qc, Wc - X0), hq = min(Qc, Hc - Y0);
+                const int lq = __builtin_ctz(static_cast<unsigned>(Qc)) - 2;  // log2 of 4-sample steps per row
                 for (int ci = 0; ci < ncomp; ci++) {
                     const int c = grp ? ci + 1 : 0;
                     QComp& C = w.cs[ci];
                     const int16_t* body = w.body[cur] + ci * 256;
                     Pel* P = u.plane<Pel>(c);
                     const int st = u.st(c);
-                    const int qn = wq >> 2;  // 4 samples per lane step (component widths are multiples of 4)
-                    for (int i = lane; i < hq * qn; i += 64) {
-                        const int y = i / qn, x = (i - y * qn) * 4;
-                        const uint2 v = *reinterpret_cast<const uint2*>(body + y * Qc + x);
+                    // 4 samples per lane step (component widths are multiples of 4); rows of the
+                    // window beyond the picture's right edge masked
+                    for (int i = lane; i < (hq << lq); i += 64) {
+                        const int y = i >> lq, x = (i & ((1 << lq) - 1)) * 4;
+                        if (x >= wq) continue;
+                        const uint2 v = *reinterpret_cast<const uint2*>(body + (y << (lq + 2)) + x);
                         Pel* d = P + (Y0 + y) * st + X0 + x;
                         if (sizeof(Pel) == 1) {
                             *reinterpret_cast<uint32_t*>(d) =
@@ -2013,16 +2022,20 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                             *reinterpret_cast<uint2*>(d) = v;
                         }
                     }
-                    if (qy == nqs - 1 && below)  // bottom line for the CTB row below
-                        for (int i = lane; i < wq; i += 64) line[ci * (Wc + 64) + X0 + i] = body[(Qc - 1) * Qc + i];
-                    if (qy == 0 && nqs == 2)
-                        for (int i = lane; i < Qc; i += 64) C.qbot[qx * Qc + i] = body[(Qc - 1) * Qc + i];
-                    if (qx == 0 && nqs == 2)
-                        for (int i = lane; i < Qc; i += 64) C.qright[i] = body[i * Qc + Qc - 1];
-                    if (qx == nqs - 1) {
-                        for (int i = lane; i < Qc; i += 64) C.prevR[pin][qy * Qc + i] = body[i * Qc + Qc - 1];
-                        if (qy == 0 && lane == 0) C.corner = C.top[Qc];
+                    // carries: the bottom row (line for the CTB row below, qbot for the bottom
+                    // quadrants) and the right column (qright for the right quadrant, prevR for
+                    // the next CTB), each read once
+                    const int k = lane & (Qc - 1);
+                    const int16_t bv = body[(Qc - 1) * Qc + k];
+                    const int16_t rv = body[k * Qc + Qc - 1];
+                    const int16_t tq = C.top[Qc];
+                    if (lane < Qc) {
+                        if (qy == nqs - 1 && below && lane < wq) line[ci * (Wc + 64) + X0 + lane] = bv;
+                        if (qy == 0 && nqs == 2) C.qbot[qx * Qc + lane] = bv;
+                        if (qx == 0 && nqs == 2) C.qright[lane] = rv;
+                        if (qx == nqs - 1) C.prevR[pin][qy * Qc + lane] = rv;
                     }
+                    if (qx == nqs - 1 && qy == 0 && lane == 0) C.corner = tq;
                 }
                 wave_sync();
                 cur ^= 1;

@@ -1,7 +1,7 @@
 """K1 cycle accounting: run N frames of a stream through the -DH2J_PROF build
 and print where the K1 waves spend their cycles (s_memtime, shader clock).
   make -C h264-h265-to-jpeg_amd prof && python tools/k1prof.py tests/golden/bench/hevc1080_00.h265 256"""
-import ctypes, os, sys
+import ctypes, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
 os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", os.environ.get("H2J_PROF_VARIANT", "prof"))
@@ -14,14 +14,18 @@ hip = ctypes.CDLL(os.path.join(os.environ["H2J_LIB_DIR"], "libh2j_hip.so"))
 buf = (ctypes.c_ulonglong * 16)()
 for path in files:
     data = open(path, "rb").read()
+    t0 = time.time()
     eng.transcode([data] * 8)
+    print(f"warm-up done {time.time() - t0:.1f}s", flush=True)
     hip.h2j_gpu_prof(buf, 16, 1)
     # over 256 pictures: the asynchronous path (one 1024-picture chunk, the K1 picture pool)
     outs = eng.transcode_async([[data] * n])[0] if n > 256 else eng.transcode([data] * n)
     assert all(o is not None for o in outs)
+    print(f"batch done {time.time() - t0:.1f}s", flush=True)
     st = eng.stats()
     if hip.h2j_gpu_prof(buf, 16, 1) != 0:
-        raise SystemExit("not a -DH2J_PROF build")
+        print(f"not a -DH2J_PROF build (K1 {st['recon_ms']:.2f} ms)")
+        continue
     v = list(buf)
     waves = None
     tot = sum(v[0:4]) + sum(v[8:16])
