@@ -15,7 +15,7 @@
 //   K2 h2j_k2_deblock*      HEVC: one thread per 4-line edge segment, V then H pass;
 //                           H.264: MB-row wavefront in LDS windows, banded like K1
 //                           (H.265 8.7.2, H.264 8.7)
-//   K3 h2j_k3_sao           one workgroup per (CTB, component), LDS tile + border (H.265 8.7.3)
+//   K3 h2j_k3_sao           one workgroup per CTB (Y, Cb, Cr), all loads issued up front, LDS tiles + border (H.265 8.7.3)
 //   K4 h2j_k4_*             FFmpeg mjpeg forward path as restated in SURVEY.md Appendix A:
 //                           pad, MB variance -> rate control -> AP-922 FDCT -> 16-bit
 //                           quantiser -> zigzag, then per-table symbol histograms
@@ -249,6 +249,20 @@ __device__ unsigned long long g_prof[16];
 DEVI uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 DEVI uint64_t ufl64(uint64_t v) {
     return (static_cast<uint64_t>(ufl(static_cast<uint32_t>(v >> 32))) << 32) | ufl(static_cast<uint32_t>(v));
+}
+
+// a record at a wave-uniform address, read as dwords into scalar registers (byte fields would
+// otherwise be re-read with per-lane byte loads at every use)
+template <typename T>
+DEVI T uload(const T* p) {
+    static_assert(sizeof(T) % 4 == 0 && alignof(T) >= 4, "dword-aligned records only");
+    uint32_t w[sizeof(T) / 4];
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int k = 0; k < static_cast<int>(sizeof(T) / 4); k++) w[k] = ufl(q[k]);
+    T t;
+    memcpy(&t, w, sizeof(T));
+    return t;
 }
 
 DEVI h2j_tu tu_from_lanes(const uint4& r, int l) {
@@ -2848,109 +2862,144 @@ __global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_
 }
 
 // ---------------------------------------------------------------- K3: SAO
-// K3 SAO (H.265 8.7.3): one 256-thread workgroup per (CTB, component).  The
-// CTB's deblocked samples plus a one-sample border are staged in LDS (int16,
-// -1 = outside the picture), the CTB's SAO parameters and the usability of
-// its 8 neighbour CTBs across slice / tile boundaries are resolved once per
-// workgroup, then every thread filters 4 horizontally adjacent samples and
-// writes them with one store.  Pictures without SAO alias pic2 = pic and are
-// skipped (the host lays them out that way).
-constexpr int kSaoTile = 66 * 66;
+// K3 SAO (H.265 8.7.3): one 256-thread workgroup per CTB, all three components.  Every load of
+// the CTB is issued before the first LDS write (the deblocked samples of Y, Cb and Cr plus a
+// one-sample border, 4 samples per load; the border columns; the per-4x4 "loop filters off"
+// flags), so a workgroup waits for HBM once instead of once per loop iteration.  Samples are
+// staged as int16 (-1 = outside the picture) in LDS tiles whose interior starts at column 4
+// (8-byte aligned rows).  The CTB's SAO parameters and the usability of its 8 neighbour CTBs
+// across slice / tile boundaries are resolved once; each thread then filters 4 horizontally
+// adjacent samples per step and writes them with one store.  Pictures without SAO alias
+// pic2 = pic and are skipped (the host lays them out that way).
+constexpr int kSaoTsY = 72, kSaoTsC = 40;  // LDS tile row strides (int16): 4 + 64 + 4, 4 + 32 + 4
+struct SaoLds {
+    int16_t y[66 * kSaoTsY];
+    int16_t c[2][34 * kSaoTsC];
+    uint8_t keep[256];  // per 4x4 luma block of the CTB: pcm / transquant bypass with loop filters off
+    uint32_t nbm;       // usable neighbour CTBs (sao_stage_store)
+};
 
 template <typename Pel>
-DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, int ctb, int c,
-                  int16_t* tile, int* nbok) {
-    const int tid = threadIdx.x;
-    const int shc = c ? 1 : 0;
-    const int S = (1 << f.log2ctb) >> shc;
-    const int cxi = ctb % f.ctb_w, cyi = ctb / f.ctb_w;
-    const int x0 = cxi * S, y0 = cyi * S;
-    const int pw = f.width >> shc, ph = f.height >> shc;
-    const int w = min(S, pw - x0), h = min(S, ph - y0);
-    const Pel* src = plane<Pel>(f, arena, f.pic, c);
-    Pel* dst = plane<Pel>(f, arena, f.pic2, c);
-    const int st = f.pic_stride[c];
-    const h2j_ctb& cc = C[ctb];
-    const h2j_slice& sc = SL[cc.slice];
-    const int type = cc.type[c];
-    const bool on = type != 0 && (c == 0 ? sc.sao_luma : sc.sao_chroma);
-    if (!on) {  // plain copy, 4 samples per thread step
-        const int q = w >> 2;
-        for (int i = tid; i < h * q; i += 256) {
-            const int y = i / q, x = (i - y * q) * 4;
-            const Pel* s = src + (y0 + y) * st + x0 + x;
-            Pel* d = dst + (y0 + y) * st + x0 + x;
-            if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
-            else *reinterpret_cast<uint2*>(d) = *reinterpret_cast<const uint2*>(s);
-        }
-        return;
+DEVI uint2 sao_load4(const Pel* p) {  // 4 samples -> 4 int16 halves of a uint2
+    if (sizeof(Pel) == 1) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+        return make_uint2((v & 0xFFu) | ((v & 0xFF00u) << 8), ((v >> 16) & 0xFFu) | ((v >> 8) & 0xFF0000u));
     }
+    return *reinterpret_cast<const uint2*>(p);
+}
+
+// geometry of component c of a CTB
+struct SaoGeo {
+    int S, x0, y0, w, h, pw, ph, lq, ts;  // lq: log2 of 4-sample chunks per CTB row; ts: tile stride
+};
+DEVI SaoGeo sao_geo(const h2j_frame& f, int ctb, int c) {
+    const int sh = c ? 1 : 0;
+    const int l2 = f.log2ctb, CS = 1 << l2;
+    const int cxi = ctb % f.ctb_w, cyi = ctb / f.ctb_w;
+    SaoGeo g;
+    g.S = CS >> sh;
+    g.x0 = (cxi * CS) >> sh;
+    g.y0 = (cyi * CS) >> sh;
+    g.pw = f.width >> sh;
+    g.ph = f.height >> sh;
+    g.w = min(g.S, g.pw - g.x0);
+    g.h = min(g.S, g.ph - g.y0);
+    g.lq = l2 - 2 - sh;
+    g.ts = c ? kSaoTsC : kSaoTsY;
+    return g;
+}
+
+// stage loads of component c: interior chunks (rows -1 .. h of the CTB) and the two border
+// columns, held in registers until every load of the CTB is in flight
+template <typename Pel, int NI>
+DEVI void sao_stage_load(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c, uint2 (&iv)[NI], int16_t& bv) {
+    const int tid = threadIdx.x;
+    const Pel* P = plane<Pel>(f, arena, f.pic, c);
+    const int st = f.pic_stride[c];
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+        const int i = tid + 256 * k, r = i >> g.lq, ch = i & ((1 << g.lq) - 1);
+        const int y = g.y0 + r - 1, x = g.x0 + 4 * ch;
+        iv[k] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (r < g.h + 2 && 4 * ch < g.w && y >= 0 && y < g.ph) iv[k] = sao_load4(P + y * st + x);
+    }
+    const int r = tid >> 1, x = (tid & 1) ? g.x0 + g.w : g.x0 - 1, y = g.y0 + r - 1;
+    bv = -1;
+    if (r < g.h + 2 && x >= 0 && x < g.pw && y >= 0 && y < g.ph) bv = static_cast<int16_t>(P[y * st + x]);
+}
+template <int NI>
+DEVI void sao_stage_store(const SaoGeo& g, int16_t* T, const uint2 (&iv)[NI], int16_t bv) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+        const int i = tid + 256 * k, r = i >> g.lq, ch = i & ((1 << g.lq) - 1);
+        if (r < g.h + 2) *reinterpret_cast<uint2*>(T + r * g.ts + 4 + 4 * ch) = iv[k];
+    }
+    const int r = tid >> 1;
+    if (r < g.h + 2) T[r * g.ts + ((tid & 1) ? 4 + g.w : 3)] = bv;
+}
+// The staged rows -1 and h and the border columns belong to the 8 neighbour CTBs; samples of a
+// neighbour that may not be used across a slice / tile boundary (bit (dy + 1) * 3 + dx + 1 of
+// nbm clear) are overwritten with -1, like samples outside the picture (8.7.3.2: the edge
+// offset then leaves the sample unmodified).  Only CTBs at such boundaries take this pass.
+DEVI void sao_stage_mask(const SaoGeo& g, int16_t* T, uint32_t nbm) {
+    const int tid = threadIdx.x;
+    auto usable = [&](int r, int dx) __attribute__((always_inline)) {
+        const int dy = r == 0 ? -1 : (r == g.h + 1 ? 1 : 0);
+        return ((nbm >> ((dy + 1) * 3 + dx + 1)) & 1u) != 0;
+    };
+    if (tid < 2 * g.w) {  // rows -1 and h
+        const int r = tid < g.w ? 0 : g.h + 1, x = tid < g.w ? tid : tid - g.w;
+        if (!usable(r, 0)) T[r * g.ts + 4 + x] = -1;
+    }
+    const int r = tid >> 1, dx = (tid & 1) ? 1 : -1;
+    if (r < g.h + 2 && !usable(r, dx)) T[r * g.ts + ((tid & 1) ? 4 + g.w : 3)] = -1;
+}
+
+// filter component c (uniform: its SAO parameters sit in scalar registers)
+template <typename Pel>
+DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c, const h2j_ctb& cc, bool on,
+                     const int16_t* T, const SaoLds& L) {
+    const int tid = threadIdx.x;
+    Pel* D = plane<Pel>(f, arena, f.pic2, c);
+    const int st = f.pic_stride[c];
+    const int type = on ? cc.type[c] : 0;
     const int bd = c ? f.bit_depth_c : f.bit_depth;
     const int maxv = (1 << bd) - 1;
-    const int cls = cc.eo_class[c];
-    if (type == 2) {
-        // stage the tile + border; -1 marks samples outside the picture
-        const int tw = w + 2, th = h + 2;
-        for (int i = tid; i < tw * th; i += 256) {
-            const int ty = i / tw, tx = i - ty * tw;
-            const int x = x0 + tx - 1, y = y0 + ty - 1;
-            tile[ty * 66 + tx] = (x >= 0 && y >= 0 && x < pw && y < ph) ? static_cast<int16_t>(src[y * st + x]) : -1;
-        }
-        if (tid < 9) {  // neighbour CTB (dx, dy) usable across slice / tile boundaries (8.7.3.2)
-            const int dx = tid % 3 - 1, dy = tid / 3 - 1;
-            const int nx = cxi + dx, ny = cyi + dy;
-            int ok = 1;
-            if (nx >= 0 && ny >= 0 && nx < f.ctb_w && ny < f.ctb_h && (dx || dy)) {
-                const h2j_ctb& nc = C[ny * f.ctb_w + nx];
-                const h2j_slice& sn = SL[nc.slice];
-                if (sn.slice_addr_rs != sc.slice_addr_rs) {
-                    if (nc.ts < cc.ts && !sc.lf_across_slices) ok = 0;
-                    if (cc.ts < nc.ts && !sn.lf_across_slices) ok = 0;
-                }
-                if (!f.lf_across_tiles && nc.tile != cc.tile) ok = 0;
-            }
-            nbok[tid] = ok;
-        }
-        __syncthreads();
-    }
+    const int cls = cc.eo_class[c], band = cc.band_pos[c];
+    const int o0 = cc.off[c][0], o1 = cc.off[c][1], o2 = cc.off[c][2], o3 = cc.off[c][3];
     const int hx = cls == 0 ? -1 : (cls == 1 ? 0 : (cls == 2 ? -1 : 1));
     const int vy = cls == 0 ? 0 : -1;
-    const uint8_t* fmap = arena + f.maps;
-    const int q = w >> 2;
-    for (int i = tid; i < h * q; i += 256) {
-        const int y = i / q, x = (i - y * q) * 4;
-        const Pel* s = src + (y0 + y) * st + x0 + x;
-        int v[4];
-        if (type == 2) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = tile[(y + 1) * 66 + x + k + 1];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = s[k];
-        }
+    const int sh = c ? 1 : 0, l2b = f.log2ctb - 2;
+    const int ts = g.ts;
+    for (int i = tid; i < (g.h << g.lq); i += 256) {
+        const int y = i >> g.lq, x = (i & ((1 << g.lq) - 1)) * 4;
+        if (x >= g.w) continue;
+        const uint2 vv = *reinterpret_cast<const uint2*>(T + (y + 1) * ts + 4 + x);
+        const int v[4] = {static_cast<int>(vv.x & 0xFFFF), static_cast<int>(vv.x >> 16), static_cast<int>(vv.y & 0xFFFF),
+                          static_cast<int>(vv.y >> 16)};
         // samples of pcm (loop filter off) / transquant-bypass blocks stay untouched
-        const bool keep = (fmap[(((y0 + y) << shc) >> 2) * f.mw + (((x0 + x) << shc) >> 2)] & 4) != 0;
+        const bool keep = type == 0 || L.keep[(((y << sh) >> 2) << l2b) + ((x << sh) >> 2)] != 0;
         int o[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            int off = 0;
+            int sel = -1;  // offset index 0..3, -1 none
             if (type == 1) {
-                const int b = ((v[k] >> (bd - 5)) - cc.band_pos[c]) & 31;
-                if (b < 4) off = cc.off[c][b];
-            } else {
+                const int b = ((v[k] >> (bd - 5)) - band) & 31;
+                sel = b < 4 ? b : -1;
+            } else if (type == 2) {
                 const int xa = x + k + hx, ya = y + vy, xb = x + k - hx, yb = y - vy;
-                const int a = tile[(ya + 1) * 66 + xa + 1], bb = tile[(yb + 1) * 66 + xb + 1];
-                const int na = ((ya < 0 ? 0 : (ya >= S ? 2 : 1)) * 3) + (xa < 0 ? 0 : (xa >= S ? 2 : 1));
-                const int nb = ((yb < 0 ? 0 : (yb >= S ? 2 : 1)) * 3) + (xb < 0 ? 0 : (xb >= S ? 2 : 1));
-                if (a >= 0 && bb >= 0 && nbok[na] && nbok[nb]) {
-                    int e = 2 + ((v[k] > a) - (v[k] < a)) + ((v[k] > bb) - (v[k] < bb));
-                    e = e == 0 ? 1 : (e == 1 ? 2 : (e == 2 ? 0 : e));
-                    if (e) off = cc.off[c][e - 1];
+                const int a = T[(ya + 1) * ts + 4 + xa], bb = T[(yb + 1) * ts + 4 + xb];
+                if (a >= 0 && bb >= 0) {
+                    const int e = 2 + ((v[k] > a) - (v[k] < a)) + ((v[k] > bb) - (v[k] < bb));
+                    // edgeIdx 0, 1, 2, 3, 4 -> category 1, 2, 0, 3, 4 -> offset index 0, 1, -, 2, 3
+                    sel = e == 0 ? 0 : (e == 1 ? 1 : (e == 2 ? -1 : e - 1));
                 }
             }
+            const int off = sel == 0 ? o0 : (sel == 1 ? o1 : (sel == 2 ? o2 : (sel == 3 ? o3 : 0)));
             o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
         }
-        Pel* d = dst + (y0 + y) * st + x0 + x;
+        Pel* d = D + (g.y0 + y) * st + g.x0 + x;
         if (sizeof(Pel) == 1) {
             *reinterpret_cast<uint32_t*>(d) = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 8) |
                                               (static_cast<uint32_t>(o[2]) << 16) | (static_cast<uint32_t>(o[3]) << 24);
@@ -2961,19 +3010,96 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
     }
 }
 
-// grid (ctbs * 3, pictures): blockIdx.x = ctb * 3 + component
-__global__ void __launch_bounds__(256) h2j_k3_sao(const h2j_frame* frames, const h2j_ctb* ctbs,
-                                                 const h2j_slice* slices, uint8_t* arena) {
-    __shared__ int16_t tile[kSaoTile];
-    __shared__ int nbok[9];
+// staged loads of one CTB (registers), written to LDS once the previous CTB is filtered
+struct SaoRegs {
+    uint2 iy[5], ib[2], ir[2];  // (66 x 16) and 2 x (34 x 8) 4-sample chunks over 256 threads
+    int16_t by, bb, br;
+    uint8_t kf;
+};
+template <typename Pel>
+DEVI void sao_load(const h2j_frame& f, uint8_t* arena, int ctb, SaoRegs& R) {
+    const int tid = threadIdx.x;
+    const SaoGeo gy = sao_geo(f, ctb, 0), gb = sao_geo(f, ctb, 1), gr = sao_geo(f, ctb, 2);
+    sao_stage_load<Pel>(f, arena, gy, 0, R.iy, R.by);
+    sao_stage_load<Pel>(f, arena, gb, 1, R.ib, R.bb);
+    sao_stage_load<Pel>(f, arena, gr, 2, R.ir, R.br);
+    R.kf = 0;
+    const int lb = f.log2ctb - 2, bY = tid >> lb, bX = tid & ((1 << lb) - 1);
+    const int gyy = (gy.y0 >> 2) + bY, gxx = (gy.x0 >> 2) + bX;
+    if (bY < (1 << lb) && gxx < f.mw && gyy < f.mh) R.kf = arena[f.maps + static_cast<size_t>(gyy) * f.mw + gxx] & 4;
+}
+
+// usability of neighbour CTB (dx, dy) = (k % 3 - 1, k / 3 - 1) of CTB (cx, row) for SAO across
+// slice / tile boundaries (8.7.3.2); outside the picture counts as usable (those samples are
+// staged as -1 anyway)
+DEVI bool sao_nb_ok(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, int cx, int row, int k) {
+    const int dx = k % 3 - 1, dy = k / 3 - 1;
+    const int nx = cx + dx, ny = row + dy;
+    if (nx < 0 || ny < 0 || nx >= f.ctb_w || ny >= f.ctb_h || (dx == 0 && dy == 0)) return true;
+    const h2j_ctb& cc = C[row * f.ctb_w + cx];
+    const h2j_ctb& nc = C[ny * f.ctb_w + nx];
+    const h2j_slice& sc = SL[cc.slice];
+    const h2j_slice& sn = SL[nc.slice];
+    bool ok = true;
+    if (sn.slice_addr_rs != sc.slice_addr_rs) {
+        if (nc.ts < cc.ts && !sc.lf_across_slices) ok = false;
+        if (cc.ts < nc.ts && !sn.lf_across_slices) ok = false;
+    }
+    if (!f.lf_across_tiles && nc.tile != cc.tile) ok = false;
+    return ok;
+}
+
+// one CTB (Y, Cb, Cr) per workgroup
+template <typename Pel>
+DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, int ctb, SaoLds& L) {
+    const int tid = threadIdx.x;
+    const int cx = ctb % f.ctb_w, row = ctb / f.ctb_w;
+    const h2j_ctb cc = uload(C + ctb);
+    const h2j_slice sc = uload(SL + cc.slice);
+    const bool onY = cc.type[0] != 0 && sc.sao_luma, onC = sc.sao_chroma;
+    const bool onCb = onC && cc.type[1] != 0, onCr = onC && cc.type[2] != 0;
+    const bool eo = (onY && cc.type[0] == 2) || (onCb && cc.type[1] == 2) || (onCr && cc.type[2] == 2);
+    const SaoGeo gy = sao_geo(f, ctb, 0), gb = sao_geo(f, ctb, 1), gr = sao_geo(f, ctb, 2);
+    // 1. every load of the CTB in flight at once
+    SaoRegs R;
+    sao_load<Pel>(f, arena, ctb, R);
+    const bool nok = !eo || tid >= 9 || sao_nb_ok(f, C, SL, cx, row, tid);
+    // 2. LDS
+    if (tid < 64) {
+        const uint64_t m = __ballot(tid < 9 && nok);
+        if (tid == 0) L.nbm = static_cast<uint32_t>(m & 0x1FFu);
+    }
+    sao_stage_store(gy, L.y, R.iy, R.by);
+    sao_stage_store(gb, L.c[0], R.ib, R.bb);
+    sao_stage_store(gr, L.c[1], R.ir, R.br);
+    L.keep[tid] = R.kf;
+    __syncthreads();
+    const uint32_t nbm = L.nbm;
+    if (nbm != 0x1FFu) {
+        sao_stage_mask(gy, L.y, nbm);
+        sao_stage_mask(gb, L.c[0], nbm);
+        sao_stage_mask(gr, L.c[1], nbm);
+        __syncthreads();
+    }
+    // 3. filter and store, one component at a time
+    sao_filter<Pel>(f, arena, gy, 0, cc, onY, L.y, L);
+    sao_filter<Pel>(f, arena, gb, 1, cc, onCb, L.c[0], L);
+    sao_filter<Pel>(f, arena, gr, 2, cc, onCr, L.c[1], L);
+}
+
+// grid (CTBs of the largest picture at the smallest CTB size, pictures)
+__global__ void __launch_bounds__(256) h2j_k3_sao(const h2j_frame* __restrict__ frames,
+                                                 const h2j_ctb* __restrict__ ctbs,
+                                                 const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena) {
+    __shared__ SaoLds L;
     const h2j_frame& f = frames[blockIdx.y];
     if (f.codec != H2J_CODEC_HEVC || f.pic2 == f.pic) return;
-    const int ctb = blockIdx.x / 3, c = blockIdx.x - ctb * 3;
+    const int ctb = blockIdx.x;
     if (ctb >= f.ctb_w * f.ctb_h) return;
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) sao_ctb<uint8_t>(f, C, S, arena, ctb, c, tile, nbok);
-    else sao_ctb<uint16_t>(f, C, S, arena, ctb, c, tile, nbok);
+    if (f.bit_depth == 8) sao_ctb<uint8_t>(f, C, S, arena, ctb, L);
+    else sao_ctb<uint16_t>(f, C, S, arena, ctb, L);
 }
 
 // ---------------------------------------------------------------- K4: JPEG
@@ -3539,7 +3665,7 @@ int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0 || !b->has_hevc) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     // CTB grid of the largest picture at the smallest CTB size present is bounded by max_ctbs
-    dim3 grid(static_cast<unsigned>(b->max_ctbs) * 3, b->nframes);
+    dim3 grid(static_cast<unsigned>(b->max_ctbs), b->nframes);
     hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena);
     return check(hipGetLastError(), "h2j_k3_sao");
 }
