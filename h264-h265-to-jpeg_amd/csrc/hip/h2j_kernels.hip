@@ -2257,6 +2257,33 @@ __constant__ uint8_t kTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 
 __constant__ int kChromaQp265[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
 DEVI int chroma_qp_tab(int qpi) { return qpi < 30 ? qpi : (qpi > 43 ? qpi - 6 : kChromaQp265[qpi - 30]); }
 
+// 4 samples at p (4-sample aligned) <-> ints; one dword (8-bit) / two (16-bit) per access
+template <typename Pel>
+DEVI void ld4(const Pel* p, int (&v)[4]) {
+    if (sizeof(Pel) == 1) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+        v[0] = w & 0xFF; v[1] = (w >> 8) & 0xFF; v[2] = (w >> 16) & 0xFF; v[3] = w >> 24;
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2*>(p);
+        v[0] = w.x & 0xFFFF; v[1] = w.x >> 16; v[2] = w.y & 0xFFFF; v[3] = w.y >> 16;
+    }
+}
+template <typename Pel>
+DEVI void st4(Pel* p, const int (&v)[4]) {
+    if (sizeof(Pel) == 1) {
+        *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(v[0]) | (static_cast<uint32_t>(v[1]) << 8) |
+                                          (static_cast<uint32_t>(v[2]) << 16) | (static_cast<uint32_t>(v[3]) << 24);
+    } else {
+        *reinterpret_cast<uint2*>(p) = make_uint2(static_cast<uint32_t>(v[0]) | (static_cast<uint32_t>(v[1]) << 16),
+                                                  static_cast<uint32_t>(v[2]) | (static_cast<uint32_t>(v[3]) << 16));
+    }
+}
+
+// One 4-line luma edge segment (8.7.2.5.3 decisions, 8.7.2.5.7 filters).  Edges lie on the 8x8
+// grid, so the 8-sample window across an edge (4 on each side) is 4-sample aligned and the
+// windows of different edges of one pass never overlap: each line is read and written back as
+// whole 4-sample words (vertical edges: 2 words per line; horizontal edges: one word per row
+// of 4 lines).  P[k][i] / Q[k][i]: line k, distance i from the edge.
 template <typename Pel>
 DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fmap, const int8_t* qmap,
                          const h2j_slice& sl, bool vert, int xe, int ye) {
@@ -2267,18 +2294,26 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
     const int beta = kBeta[clip3(0, 51, qpl + sl.beta_offset)] * (1 << (bd - 8));
     const int tc = kTc[clip3(0, 53, qpl + 2 + sl.tc_offset)] * (1 << (bd - 8));
     const int maxv = (1 << bd) - 1;
-    // sample addressing: line k, distance i (0..3) from the edge
-    const int sa = vert ? st : 1;   // along the edge
-    const int sx = vert ? 1 : st;   // across the edge
-    Pel* q = pl + ye * st + xe;
     int P[4][4], Q[4][4];
+    if (vert) {
 #pragma unroll
-    for (int k = 0; k < 4; k++)
+        for (int k = 0; k < 4; k++) {
+            int a[4], c[4];
+            ld4(pl + (ye + k) * st + xe - 4, a);
+            ld4(pl + (ye + k) * st + xe, c);
+#pragma unroll
+            for (int i = 0; i < 4; i++) { P[k][i] = a[3 - i]; Q[k][i] = c[i]; }
+        }
+    } else {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            P[k][i] = q[k * sa - (i + 1) * sx];
-            Q[k][i] = q[k * sa + i * sx];
+            int a[4], c[4];
+            ld4(pl + (ye - 1 - i) * st + xe, a);
+            ld4(pl + (ye + i) * st + xe, c);
+#pragma unroll
+            for (int k = 0; k < 4; k++) { P[k][i] = a[k]; Q[k][i] = c[k]; }
         }
+    }
     const int dp0 = abs(P[0][2] - 2 * P[0][1] + P[0][0]), dp3 = abs(P[3][2] - 2 * P[3][1] + P[3][0]);
     const int dq0 = abs(Q[0][2] - 2 * Q[0][1] + Q[0][0]), dq3 = abs(Q[3][2] - 2 * Q[3][1] + Q[3][0]);
     const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
@@ -2291,41 +2326,56 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
     const bool dEq = dq < ((beta + (beta >> 1)) >> 3);
     const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
     const bool nfq = fmap[(ye >> 2) * f.mw + (xe >> 2)] & 4;
+    int NP[4][4], NQ[4][4];  // filtered lines (unfiltered samples keep their value)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int p0 = P[k][0], p1 = P[k][1], p2 = P[k][2], p3 = P[k][3];
         const int q0 = Q[k][0], q1 = Q[k][1], q2 = Q[k][2], q3 = Q[k][3];
-        Pel* e = q + k * sa;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { NP[k][i] = P[k][i]; NQ[k][i] = Q[k][i]; }
         if (s0 && s3) {
             if (!nfp) {
-                e[-1 * sx] = static_cast<Pel>(clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3));
-                e[-2 * sx] = static_cast<Pel>(clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2));
-                e[-3 * sx] = static_cast<Pel>(clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3));
+                NP[k][0] = clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+                NP[k][1] = clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
+                NP[k][2] = clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
             }
             if (!nfq) {
-                e[0] = static_cast<Pel>(clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3));
-                e[sx] = static_cast<Pel>(clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2));
-                e[2 * sx] = static_cast<Pel>(clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3));
+                NQ[k][0] = clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+                NQ[k][1] = clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
+                NQ[k][2] = clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
             }
         } else {
             int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
             if (abs(delta) < tc * 10) {
                 delta = clip3(-tc, tc, delta);
-                if (!nfp) e[-sx] = static_cast<Pel>(clip3(0, maxv, p0 + delta));
-                if (!nfq) e[0] = static_cast<Pel>(clip3(0, maxv, q0 - delta));
-                if (dEp && !nfp) {
-                    const int d2 = clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1);
-                    e[-2 * sx] = static_cast<Pel>(clip3(0, maxv, p1 + d2));
-                }
-                if (dEq && !nfq) {
-                    const int d2 = clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1);
-                    e[sx] = static_cast<Pel>(clip3(0, maxv, q1 + d2));
-                }
+                if (!nfp) NP[k][0] = clip3(0, maxv, p0 + delta);
+                if (!nfq) NQ[k][0] = clip3(0, maxv, q0 - delta);
+                if (dEp && !nfp) NP[k][1] = clip3(0, maxv, p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
+                if (dEq && !nfq) NQ[k][1] = clip3(0, maxv, q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
             }
+        }
+    }
+    if (vert) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int a[4] = {NP[k][3], NP[k][2], NP[k][1], NP[k][0]};
+            if (!nfp) st4(pl + (ye + k) * st + xe - 4, a);
+            if (!nfq) st4(pl + (ye + k) * st + xe, NQ[k]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {  // rows at distance 3 are never modified
+            const int a[4] = {NP[0][i], NP[1][i], NP[2][i], NP[3][i]};
+            const int c[4] = {NQ[0][i], NQ[1][i], NQ[2][i], NQ[3][i]};
+            if (!nfp) st4(pl + (ye - 1 - i) * st + xe, a);
+            if (!nfq) st4(pl + (ye + i) * st + xe, c);
         }
     }
 }
 
+// One 4-line chroma edge segment (8.7.2.5.5) on the 8x8 chroma grid, whole 4-sample words as
+// for luma (vertical edges: the words at xc - 4 and xc of each line; horizontal: rows yc - 2 ..
+// yc + 1 at xc).
 template <typename Pel>
 DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, const uint8_t* fmap,
                            const int8_t* qmap, const h2j_slice& sl, int cqpoff, bool vert, int xc, int yc) {
@@ -2338,15 +2388,34 @@ DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, 
     const int maxv = (1 << bd) - 1;
     const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
     const bool nfq = fmap[(yl >> 2) * f.mw + (xl >> 2)] & 4;
-    const int sa = vert ? st : 1, sx = vert ? 1 : st;
-    Pel* q = pl + yc * st + xc;
-    for (int k = 0; k < 4; k++) {
-        if (vert ? (yc + k >= ph) : (xc + k >= pw)) break;
-        Pel* e = q + k * sa;
-        const int p0 = e[-sx], p1 = e[-2 * sx], q0 = e[0], q1 = e[sx];
-        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
-        if (!nfp) e[-sx] = static_cast<Pel>(clip3(0, maxv, p0 + delta));
-        if (!nfq) e[0] = static_cast<Pel>(clip3(0, maxv, q0 - delta));
+    if (vert) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (yc + k >= ph) break;
+            Pel* row = pl + (yc + k) * st + xc;
+            int a[4], c[4];
+            ld4(row - 4, a);
+            ld4(row, c);
+            const int p0 = a[3], p1 = a[2], q0 = c[0], q1 = c[1];
+            const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
+            a[3] = clip3(0, maxv, p0 + delta);
+            c[0] = clip3(0, maxv, q0 - delta);
+            if (!nfp) st4(row - 4, a);
+            if (!nfq) st4(row, c);
+        }
+    } else {
+        int r[4][4];  // rows yc - 2 .. yc + 1, columns xc .. xc + 3 (chroma widths are multiples of 4)
+#pragma unroll
+        for (int j = 0; j < 4; j++) ld4(pl + (yc - 2 + j) * st + xc, r[j]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p1 = r[0][k], p0 = r[1][k], q0 = r[2][k], q1 = r[3][k];
+            const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
+            r[1][k] = clip3(0, maxv, p0 + delta);
+            r[2][k] = clip3(0, maxv, q0 - delta);
+        }
+        if (!nfp) st4(pl + (yc - 1) * st + xc, r[1]);
+        if (!nfq) st4(pl + yc * st + xc, r[2]);
     }
 }
 
@@ -2373,8 +2442,10 @@ DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slic
     }
 }
 
-__global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* frames, const h2j_ctb* ctbs,
-                                                     const h2j_slice* slices, uint8_t* arena, int vert) {
+__global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* __restrict__ frames,
+                                                     const h2j_ctb* __restrict__ ctbs,
+                                                     const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena,
+                                                     int vert) {
     const h2j_frame& f = frames[blockIdx.y];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= f.mw * f.mh) return;

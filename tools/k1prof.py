@@ -18,8 +18,8 @@ for path in files:
     eng.transcode([data] * 8)
     print(f"warm-up done {time.time() - t0:.1f}s", flush=True)
     hip.h2j_gpu_prof(buf, 16, 1)
-    # over 256 pictures: the asynchronous path (one 1024-picture chunk, the K1 picture pool)
-    outs = eng.transcode_async([[data] * n])[0] if n > 256 else eng.transcode([data] * n)
+    # K1PROF_ASYNC=1: through the asynchronous path (one chunk of up to 1024 pictures)
+    outs = eng.transcode_async([[data] * n])[0] if os.environ.get("K1PROF_ASYNC") else eng.transcode([data] * n)
     assert all(o is not None for o in outs)
     print(f"batch done {time.time() - t0:.1f}s", flush=True)
     st = eng.stats()
