@@ -1220,6 +1220,60 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
     wave_sync();
 }
 
+// The Cb and Cr blocks of one macroblock (8x8 each at 4:2:0; same mode and availability) in
+// one pass: Cb's references in top / left, Cr's in ftop / fleft (the 8x8 luma filter buffers,
+// unused by chroma), both predicted + reconstructed per lane (8.3.4).
+DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t mask, int bd, H4WaveLds& s,
+                                   int lane) {
+    const int maxv = (1 << bd) - 1;
+    const bool cbf_b = (tb.flags & H2J_TU_CBF) != 0, cbf_r = (tr.flags & H2J_TU_CBF) != 0;
+    const int fl = static_cast<int>(mask & 15);  // bits: 0 top, 1 left, 2 corner
+    // lanes 0..8: top (corner first), lanes 16..24: left (corner first), both components
+    if (lane <= 8) {
+        const int i = lane;
+        const bool ok = i == 0 ? (fl & 4) != 0 : (fl & 1) != 0;
+        s.top[i] = ok ? s.wc[0][0][i] : 0;
+        s.ftop[i] = ok ? s.wc[1][0][i] : 0;
+    } else if (lane >= 16 && lane <= 24) {
+        const int i = lane - 16;
+        const bool ok = i == 0 ? (fl & 4) != 0 : (fl & 2) != 0;
+        s.left[i] = ok ? s.wc[0][i][0] : 0;
+        s.fleft[i] = ok ? s.wc[1][i][0] : 0;
+    }
+    wave_sync();
+    const int mode = tb.mode;
+    const int x = lane & 7, y = lane >> 3;
+    const bool at = fl & 1, al = fl & 2;
+    auto pred = [&](const int* TT, const int* LL) __attribute__((always_inline)) -> int {
+        if (mode == 1) return LL[y];
+        if (mode == 2) return TT[x];
+        if (mode == 3) {
+            int H = 0, V = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                H += (k + 1) * (TT[4 + k] - TT[2 - k]);
+                V += (k + 1) * (LL[4 + k] - LL[2 - k]);
+            }
+            const int a = 16 * (LL[7] + TT[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+            return clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+        }
+        const int bx = x >> 2, by = y >> 2;
+        int st4 = 0, sl4 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) { st4 += TT[bx * 4 + k]; sl4 += LL[by * 4 + k]; }
+        if (bx == by) return (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1)));
+        if (bx) return at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1));
+        return al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
+    };
+#pragma unroll 1
+    for (int c = 0; c < 2; c++) {  // one code path for both components (register pressure)
+        const int pv = pred(c ? s.ftop + 1 : s.top + 1, c ? s.fleft + 1 : s.left + 1);
+        const int r = (c ? cbf_r : cbf_b) ? s.rc[c][y][x] : 0;
+        s.wc[c][y + 1][x + 1] = static_cast<uint16_t>(clip3(0, maxv, pv + r));
+    }
+    wave_sync();
+}
+
 // H.264 macroblock rows.  Per MB: the records (held one per lane, prefetched
 // while the previous MB runs: in raster order the next MB's records start
 // where this MB's end), the K0 residual (registers, one MB ahead), the line
@@ -1377,6 +1431,11 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             } else {
                 for (uint32_t t = 0; t < ntu; t++) {
                     const h2j_tu tu = s.tus[t];
+                    if (tu.c == 1 && tu.log2n == 3 && t + 1 < ntu && s.tus[t + 1].c == 2 && s.tus[t + 1].log2n == 3) {  // Cb + Cr in one pass
+                        h264_predict_chroma_pair(tu, s.tus[t + 1], s.masks[t], bdc, s, lane);
+                        t++;
+                        continue;
+                    }
                     h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? bdc : bdy, s, lane);
                 }
                 // ---- store the macroblock: one aligned 4-sample (luma) / 2-sample (chroma) store
