@@ -3719,11 +3719,11 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
             if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
             if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
         } else if (pool_p > 0) {
-            // pictures per pool workgroup: ~256 workgroups (one per CU) per launch, as many
-            // pictures each as fit (LDS: one set of line buffers + progress words per picture)
+            // pictures per pool workgroup: at least 256 workgroups (one per CU) per launch, as
+            // many pictures each as fit (LDS: one set of line buffers + progress words per picture)
             const int maxrows = (b->max_h + 15) / 16;
             const int lstride = 2 * b->max_w + 192, lchroma = b->max_w + 64;
-            int P = std::max(1, std::min(pool_p, (b->nframes + 255) / 256));
+            int P = std::max(1, std::min(pool_p, b->nframes / 256));  // never fewer than 256 workgroups
             while (P > 1 && k1_pool_lds(P, maxrows, lstride) > 160 * 1024) P--;
             const size_t lds = k1_pool_lds(P, maxrows, lstride);
             if (lds > 160 * 1024) {
