@@ -212,10 +212,17 @@ struct K0Lds {
     int dc[16];
 };
 
-DEVI int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+
+// Wave-wide integer sum with DPP row shifts + row broadcasts (no LDS trip);
+// call with all 64 lanes active.
+DEVI int wave_sum_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return __builtin_amdgcn_readlane(x, 63);
 }
 
 // lanes of one wave exchanging data through LDS
@@ -1163,13 +1170,13 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
         TT = s.ftop + 1;
         LL = s.fleft + 1;
     }
-    // DC value
+    // DC value (luma DC mode 2 only; DPP sum, every lane active: mode is uniform)
     int dcv = 0;
-    if (!chroma) {
+    if (!chroma && mode == 2) {
         const bool at = fl & 1, al = fl & 2;
         int part = 0;
         for (int i = lane; i < n; i += 64) part += (at ? TT[i] : 0) + (al ? LL[i] : 0);
-        const int sum = wave_sum(part);
+        const int sum = wave_sum_dpp(part);
         if (at && al) dcv = (sum + n) >> (log2n + 1);
         else if (at || al) dcv = (sum + (n >> 1)) >> log2n;
         else dcv = 1 << (bd - 1);
@@ -1584,17 +1591,6 @@ DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / 
     return -v;
 }
 
-// Wave-wide integer sum with DPP row shifts + row broadcasts (no LDS trip);
-// call with all 64 lanes active.
-DEVI int wave_sum_dpp(int x) {
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
-    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return __builtin_amdgcn_readlane(x, 63);
-}
 
 // One HEVC TB predicted + reconstructed inside the wave's CTB window
 // (H.265 8.4.4.2.2 substitution, 8.4.4.2.3 filtering, 8.4.4.2.4-6 planar / DC /
