@@ -1091,17 +1091,43 @@ struct K1WaveLds {  // HEVC reference arrays (4n + 1 <= 129 samples)
     int16_t ref[132];
 };
 
+// Asynchronous global -> LDS copies (LDS-DMA): lane i's bytes land at lds + i * size, with no
+// VGPR destination.  M0 carries the wave-uniform LDS byte address (set and restored inside the
+// statement, the compiler reserves M0).  Issued as asm, so the compiler does not track them:
+// every use of the data waits vmcnt(0) explicitly (lds_dma_wait).
+DEVI void lds_dma16(const void* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+DEVI void lds_dma4(const void* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+DEVI void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+DEVI void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+DEVI uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
+}
+
 // H.264: one macroblock plus its top line and left column, per wave.
 // Window coordinates: (x - mb_x + 1, y - mb_y + 1); row 0 is the line
 // above (luma incl. the 8 top-right samples), column 0 the left column.
 constexpr int kH4MaxTus = 24;
-struct H4WaveLds {
+struct alignas(16) H4In {  // one MB's inputs, filled by LDS-DMA while the previous MB runs
+    h2j_tu tus[kH4MaxTus];                       // records (16 B each: one dwordx4 per lane)
+    uint32_t mlo[kH4MaxTus], mhi[kH4MaxTus];     // availability masks, low / high dwords
+    int16_t ry[16][16];                          // K0 residual: luma, then (contiguous) chroma
+    int16_t rc[2][8][8];
+    DEVI uint64_t mask(int t) const { return static_cast<uint64_t>(mlo[t]) | (static_cast<uint64_t>(mhi[t]) << 32); }
+};
+static_assert(offsetof(H4In, rc) == offsetof(H4In, ry) + 512 && offsetof(H4In, ry) % 16 == 0,
+              "one 48-lane dwordx4 DMA fills ry then rc");
+struct alignas(16) H4WaveLds {
+    H4In in[2];     // ping-pong: the MB being reconstructed / the next one
     uint16_t wy[17][25];
     uint16_t wc[2][9][9];
-    int16_t ry[16][16];   // residual (K0)
-    int16_t rc[2][8][8];
-    h2j_tu tus[kH4MaxTus];
-    uint64_t masks[kH4MaxTus];
     int top[40];    // top[0] = corner, top[1 + i] = p[i, -1]
     int left[20];   // left[0] = corner, left[1 + i] = p[-1, i]
     int ftop[40], fleft[20];
@@ -1110,7 +1136,8 @@ struct H4WaveLds {
 
 // One H.264 prediction block (I4x4 / I8x8 / I16x16 / chroma) inside the
 // wave's macroblock window; all sample traffic is LDS.
-DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int bd, H4WaveLds& s, int lane) {
+DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int bd, H4WaveLds& s, const H4In& in,
+                           int lane) {
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
     const int ox = c ? tu.x - mbx * 8 : tu.x - mbx * 16;   // block origin inside the macroblock
     const int oy = c ? tu.y - mby * 8 : tu.y - mby * 16;
@@ -1181,9 +1208,10 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
         else if (at || al) dcv = (sum + (n >> 1)) >> log2n;
         else dcv = 1 << (bd - 1);
     }
+#pragma unroll 1
     for (int i = lane; i < nn; i += 64) {
         const int x = i & (n - 1), y = i >> log2n;
-        const int r = cbf ? (chroma ? s.rc[c - 1][oy + y][ox + x] : s.ry[oy + y][ox + x]) : 0;
+        const int r = cbf ? (chroma ? in.rc[c - 1][oy + y][ox + x] : in.ry[oy + y][ox + x]) : 0;
         int pv;
         if (nxn) {
             pv = h264_pred_nxn(mode, x, y, n, TT, LL, dcv);
@@ -1231,7 +1259,7 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
 // one pass: Cb's references in top / left, Cr's in ftop / fleft (the 8x8 luma filter buffers,
 // unused by chroma), both predicted + reconstructed per lane (8.3.4).
 DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t mask, int bd, H4WaveLds& s,
-                                   int lane) {
+                                   const H4In& in, int lane) {
     const int maxv = (1 << bd) - 1;
     const bool cbf_b = (tb.flags & H2J_TU_CBF) != 0, cbf_r = (tr.flags & H2J_TU_CBF) != 0;
     const int fl = static_cast<int>(mask & 15);  // bits: 0 top, 1 left, 2 corner
@@ -1275,25 +1303,17 @@ DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t 
 #pragma unroll 1
     for (int c = 0; c < 2; c++) {  // one code path for both components (register pressure)
         const int pv = pred(c ? s.ftop + 1 : s.top + 1, c ? s.fleft + 1 : s.left + 1);
-        const int r = (c ? cbf_r : cbf_b) ? s.rc[c][y][x] : 0;
+        const int r = (c ? cbf_r : cbf_b) ? in.rc[c][y][x] : 0;
         s.wc[c][y + 1][x + 1] = static_cast<uint16_t>(clip3(0, maxv, pv + r));
     }
     wave_sync();
 }
 
-// H.264 macroblock rows.  Per MB: the records (held one per lane, prefetched
-// while the previous MB runs: in raster order the next MB's records start
-// where this MB's end), the K0 residual (registers, one MB ahead), the line
-// above from a per-picture LDS line buffer (each row leaves its unfiltered
-// bottom samples there; the top-left corner is carried), the prediction
-// chain in the LDS window, one store of the MB.
-struct H4Pre {      // one MB's prefetched inputs
-    uint4 rec;      // lane t < 24: record t
-    uint2 msk;
-    uint2 ry;       // luma residual: 4 per lane
-    uint32_t rc;    // chroma residual: 2 per lane
-};
-
+// H.264 macroblock rows.  Per MB: the records, availability masks and K0 residual, fetched by
+// LDS-DMA into the wave's other H4In buffer while the previous MB runs (in raster order the next
+// MB's records start where this MB's end; no registers are held across the MB), the line above
+// from a per-picture LDS line buffer (each row leaves its unfiltered bottom samples there; the
+// top-left corner is carried), the prediction chain in the LDS window, one store of the MB.
 template <typename Pel>
 DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog,
                     uint16_t* line, int band, int nbands) {
@@ -1319,18 +1339,28 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     // the boundary rows, both accessed with agent-scope atomics (coherent across CUs / XCDs)
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
     if (rbeg + w >= rend) return;
-    auto fetch = [&](int mx, int my, uint32_t a, H4Pre& p) __attribute__((always_inline)) {
-        const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
-        p.rec = reinterpret_cast<const uint4*>(T)[ri];
-        p.msk = reinterpret_cast<const uint2*>(masks)[ri];
-        const int r = lane >> 2, c4 = (lane & 3) * 4;
-        p.ry = *reinterpret_cast<const uint2*>(RY + (my * 16 + r) * sty + mx * 16 + c4);
-        const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
-        p.rc = *reinterpret_cast<const uint32_t*>(RC[c] + (my * 8 + rr) * stc + mx * 8 + c2);
+    const uint32_t* masks32 = reinterpret_cast<const uint32_t*>(masks);
+    // records (lanes 0..23, dwordx4), mask halves (dword each) and residual (lanes 0..31: luma
+    // half rows of 8, lanes 32..47: chroma rows; 16 B each, ry and rc contiguous) of MB (mx, my)
+    auto in_recs = [&](uint32_t a, H4In& d) __attribute__((always_inline)) {
+        if (lane < kH4MaxTus) {
+            const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
+            lds_dma16(T + ri, lds_addr(d.tus));
+            lds_dma4(masks32 + 2 * ri, lds_addr(d.mlo));
+            lds_dma4(masks32 + 2 * ri + 1, lds_addr(d.mhi));
+        }
     };
-    H4Pre pre;
+    auto in_fetch = [&](int mx, int my, uint32_t a, H4In& d) __attribute__((always_inline)) {
+        in_recs(a, d);
+        if (lane < 32) lds_dma16(RY + (my * 16 + (lane >> 1)) * sty + mx * 16 + (lane & 1) * 8, lds_addr(d.ry));
+        else if (lane < 48) {
+            const int k = lane - 32;
+            lds_dma16(RC[k >> 3] + (my * 8 + (k & 7)) * stc + mx * 8, lds_addr(d.ry));
+        }
+    };
+    int cur = 0;
     uint32_t pre_a = rng[4 * ((rbeg + w) * mbw)];  // first record the prefetch assumed
-    fetch(0, rbeg + w, pre_a, pre);
+    in_fetch(0, rbeg + w, pre_a, s.in[0]);
     uint16_t cy_corner = 0, cc_corner[2] = {0, 0};  // carried top-left samples (luma, Cb, Cr)
     for (int row = rbeg + w; row < rend; row += kAvcWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
@@ -1369,21 +1399,13 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
             }
-            // ---- window: prefetched records / residual, line above from LDS, left column carried
+            // ---- window: the DMA'd inputs, line above from LDS, left column carried
+            H4In& in = s.in[cur];
+            lds_dma_wait();
             if (pre_a != a) {  // an MB without records before this one: reload the records
-                const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
-                pre.rec = reinterpret_cast<const uint4*>(T)[ri];
-                pre.msk = reinterpret_cast<const uint2*>(masks)[ri];
-            }
-            if (lane < static_cast<int>(ntu)) {
-                memcpy(&s.tus[lane], &pre.rec, sizeof(h2j_tu));
-                s.masks[lane] = static_cast<uint64_t>(pre.msk.x) | (static_cast<uint64_t>(pre.msk.y) << 32);
-            }
-            {
-                const int r = lane >> 2, c4 = (lane & 3) * 4;
-                *reinterpret_cast<uint2*>(&s.ry[r][c4]) = pre.ry;
-                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
-                *reinterpret_cast<uint32_t*>(&s.rc[c][rr][c2]) = pre.rc;
+                lds_reads_done();
+                in_recs(a, in);
+                lds_dma_wait();
             }
             if (from_band) {  // boundary row of the band above (uint16 pairs in dwords, agent-scope loads)
                 int x = -1, e = 0;
@@ -1418,7 +1440,8 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     na = ny < mbh ? rng[4 * (ny * mbw)] : 0;
                 }
                 if (ny < mbh) {
-                    fetch(nx, ny, na, pre);
+                    lds_reads_done();  // the other buffer's last reader, the previous MB, has finished
+                    in_fetch(nx, ny, na, s.in[cur ^ 1]);
                     pre_a = na;
                 }
             }
@@ -1427,7 +1450,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             cy_corner = s.wy[0][16];
             cc_corner[0] = s.wc[0][0][8];
             cc_corner[1] = s.wc[1][0][8];
-            const bool pcm = ntu > 0 && (s.tus[0].flags & H2J_TU_PCM);
+            const bool pcm = ntu > 0 && (in.tus[0].flags & H2J_TU_PCM);
             if (pcm) {  // samples written by K0: pull them into the window
                 for (int i = lane; i < 256; i += 64) s.wy[(i >> 4) + 1][(i & 15) + 1] = PY[(gy + (i >> 4)) * sty + gx + (i & 15)];
                 for (int i = lane; i < 128; i += 64) {
@@ -1437,13 +1460,13 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 wave_sync();
             } else {
                 for (uint32_t t = 0; t < ntu; t++) {
-                    const h2j_tu tu = s.tus[t];
-                    if (tu.c == 1 && tu.log2n == 3 && t + 1 < ntu && s.tus[t + 1].c == 2 && s.tus[t + 1].log2n == 3) {  // Cb + Cr in one pass
-                        h264_predict_chroma_pair(tu, s.tus[t + 1], s.masks[t], bdc, s, lane);
+                    const h2j_tu tu = in.tus[t];
+                    if (tu.c == 1 && tu.log2n == 3 && t + 1 < ntu && in.tus[t + 1].c == 2 && in.tus[t + 1].log2n == 3) {  // Cb + Cr in one pass
+                        h264_predict_chroma_pair(tu, in.tus[t + 1], in.mask(t), bdc, s, in, lane);
                         t++;
                         continue;
                     }
-                    h264_predict_tu(tu, s.masks[t], mx, row, tu.c ? bdc : bdy, s, lane);
+                    h264_predict_tu(tu, in.mask(t), mx, row, tu.c ? bdc : bdy, s, in, lane);
                 }
                 // ---- store the macroblock: one aligned 4-sample (luma) / 2-sample (chroma) store
                 // per lane, 16 contiguous bytes per row, instead of byte stores
@@ -1497,6 +1520,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             if (lane == 0)
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            cur ^= 1;
         }
     }
 }
@@ -1846,26 +1870,6 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
         *dr = static_cast<int16_t>(clip3(0, maxv, pr + (cbf_cr ? *dr : 0)));
     }
     wave_sync();
-}
-
-// Asynchronous global -> LDS copies (LDS-DMA): lane i's bytes land at lds + i * size, with no
-// VGPR destination.  M0 carries the wave-uniform LDS byte address (set and restored inside the
-// statement, the compiler reserves M0).  Issued as asm, so the compiler does not track them:
-// every use of the data waits vmcnt(0) explicitly (lds_dma_wait).
-DEVI void lds_dma16(const void* g, uint32_t lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-DEVI void lds_dma4(const void* g, uint32_t lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-DEVI void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-DEVI void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-DEVI uint32_t lds_addr(const void* p) {
-    return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
 }
 
 // K0 residual of one quadrant -> a quadrant window in LDS by LDS-DMA (no registers held while
@@ -2294,8 +2298,8 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
         uint16_t* line = reinterpret_cast<uint16_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4);
         const int band = static_cast<int>(me & 0xFF);
         const int nbands = ufl(f.k1bands);
-        if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
-        __syncthreads();
+            if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
+            __syncthreads();
         H4WaveLds& s = wl[threadIdx.x >> 6];
         if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
         else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
@@ -3684,7 +3688,12 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
                              reinterpret_cast<const void*>(h2j_k1_recon_any),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc_pool<uint8_t>),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc_pool<uint16_t>)};
-        for (const void* fn : fns) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        for (const void* fn : fns) {  // dynamic LDS up to 160 KB minus the kernel's static LDS
+            hipFuncAttributes fa{};
+            const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(160 * 1024 - st));
+        }
+        (void)hipGetLastError();  // attribute calls must not leave an error for the launch checks
         attr = true;
     }
     static const int pool_p = [] {  // H2J_K1_POOL: max pictures per pool workgroup (0: h2j_k1_recon_hevc_pic)
