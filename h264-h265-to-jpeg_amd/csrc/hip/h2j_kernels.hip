@@ -1126,6 +1126,7 @@ static_assert(offsetof(H4In, rc) == offsetof(H4In, ry) + 512 && offsetof(H4In, r
               "one 48-lane dwordx4 DMA fills ry then rc");
 struct alignas(16) H4WaveLds {
     H4In in[2];     // ping-pong: the MB being reconstructed / the next one
+    alignas(16) uint8_t stage[3 * 16 * 64];  // 4 reconstructed MBs (Pel): luma [16][64], chroma [2][8][32]
     uint16_t wy[17][25];
     uint16_t wc[2][9][9];
     int top[40];    // top[0] = corner, top[1 + i] = p[i, -1]
@@ -1468,22 +1469,42 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     }
                     h264_predict_tu(tu, in.mask(t), mx, row, tu.c ? bdc : bdy, s, in, lane);
                 }
-                // ---- store the macroblock: one aligned 4-sample (luma) / 2-sample (chroma) store
-                // per lane, 16 contiguous bytes per row, instead of byte stores
-                {
-                    const int r = lane >> 2, c4 = (lane & 3) * 4;
-                    Pel* d = PY + (gy + r) * sty + gx + c4;
-                    const uint32_t y0 = s.wy[r + 1][c4 + 1], y1 = s.wy[r + 1][c4 + 2];
-                    const uint32_t y2 = s.wy[r + 1][c4 + 3], y3 = s.wy[r + 1][c4 + 4];
-                    const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
-                    Pel* e = PC[c] + (cy + rr) * stc + cx + c2;
-                    const uint32_t u0 = s.wc[c][rr + 1][c2 + 1], u1 = s.wc[c][rr + 1][c2 + 2];
-                    if (sizeof(Pel) == 1) {
-                        *reinterpret_cast<uint32_t*>(d) = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
-                        *reinterpret_cast<uint16_t*>(e) = static_cast<uint16_t>(u0 | (u1 << 8));
-                    } else {
-                        *reinterpret_cast<uint2*>(d) = make_uint2(y0 | (y1 << 16), y2 | (y3 << 16));
-                        *reinterpret_cast<uint32_t*>(e) = u0 | (u1 << 16);
+            }
+            // ---- stage the macroblock in the wave's 4-MB-wide staging rows; every 4th MB (and the
+            // row's last) the group goes out as 64-sample luma / 32-sample chroma rows, whole
+            // 64-byte segments at 8 bits instead of 16-byte pieces per MB (a PCM MB's samples,
+            // already in the picture, are rewritten unchanged)
+            {
+                Pel* SY = reinterpret_cast<Pel*>(s.stage);
+                Pel* SC = SY + 16 * 64;  // [2][8][32]
+                const int r = lane >> 2, c4 = (lane & 3) * 4, sx = (mx & 3) * 16;
+#pragma unroll
+                for (int k = 0; k < 4; k++) SY[r * 64 + sx + c4 + k] = static_cast<Pel>(s.wy[r + 1][c4 + 1 + k]);
+                const int c = lane >> 5, kk = lane & 31, rr = kk >> 2, c2 = (kk & 3) * 2, scx = (mx & 3) * 8;
+                SC[(c * 8 + rr) * 32 + scx + c2] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 1]);
+                SC[(c * 8 + rr) * 32 + scx + c2 + 1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
+            }
+            if ((mx & 3) == 3 || mx == mbw - 1) {
+                wave_sync();
+                const Pel* SY = reinterpret_cast<const Pel*>(s.stage);
+                const Pel* SC = SY + 16 * 64;
+                const int g0 = mx & ~3, nmb = mx - g0 + 1;
+                {  // luma: lane = (row, 16-sample segment)
+                    const int r = lane >> 2, sg = lane & 3;
+                    if (sg < nmb) {
+                        const uint4* src = reinterpret_cast<const uint4*>(SY + r * 64 + sg * 16);
+                        uint4* dst = reinterpret_cast<uint4*>(PY + (gy + r) * sty + g0 * 16 + sg * 16);
+                        dst[0] = src[0];
+                        if (sizeof(Pel) == 2) dst[1] = src[1];
+                    }
+                }
+                {  // chroma: lane = (component, row, 8-sample segment)
+                    const int c = lane >> 5, cr = (lane >> 2) & 7, sg = lane & 3;
+                    if (sg < nmb) {
+                        const Pel* src = SC + (c * 8 + cr) * 32 + sg * 8;
+                        Pel* dst = PC[c] + (cy + cr) * stc + g0 * 8 + sg * 8;
+                        if (sizeof(Pel) == 1) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
+                        else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
                     }
                 }
             }

@@ -1,5 +1,5 @@
-# PMC instruction mix / wait of one kernel (regex $1) on workload $2 (1024 pictures, one step);
-# two passes: SQ counters, then cache / LDS-bank counters.
+# PMC counters of one kernel (regex $1) on workload $2 (1024 pictures, one step), two passes:
+# SQ instruction mix / waits (default) or MODE=hbm: FETCH_SIZE then WRITE_SIZE (KiB).
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -7,6 +7,8 @@ K=${1:-h2j_k3_sao}
 WL=${2:-hevc1080}
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 P2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH"
+if [ "${MODE:-sq}" = hbm ]; then P1="FETCH_SIZE"; P2="WRITE_SIZE"; fi  # KiB, separate passes (MI355X guide)
+rm -rf gpurun_out/pmck_1 gpurun_out/pmck_2
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
