@@ -2625,12 +2625,28 @@ DEVI void h264_filt_reg(int (&v)[LEN], bool on, int bs, int alpha, int beta, int
 // anyone else before) are prefetched into registers one MB ahead.  After the
 // 8 luma + 4 chroma edge passes the window is written back once.
 constexpr int kAvcDbWaves = 16;
-struct DbWin {
+struct alignas(16) DbWin {
     uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
     uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
     uint16_t py[16][12];    // previous MB, columns 0..11 (final, not yet stored)
     uint16_t pc[2][8][8];   // previous MB, chroma columns 0..6 (+ pad)
+    // final samples staged 4 MBs wide (Pel) and written as whole rows: rows 12..15 of the MBs
+    // above (luma [4][64], chroma [2][2][32]) and rows of this row's MBs (luma [16][64], chroma
+    // [2][8][32])
+    alignas(16) uint8_t sa[2 * (4 * 64 + 2 * 2 * 32)];
+    alignas(16) uint8_t sb[2 * (16 * 64 + 2 * 8 * 32)];
 };
+// n (4, 8 or 16) Pel between 16-byte-aligned LDS staging and the picture
+template <typename Pel, int N>
+DEVI void db264_copy(Pel* dst, const Pel* src) {
+    constexpr int B = N * static_cast<int>(sizeof(Pel));
+    if constexpr (B == 4) *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+    else if constexpr (B == 8) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
+    else {
+#pragma unroll
+        for (int k = 0; k < B / 16; k++) reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
+    }
+}
 
 template <typename Pel>
 struct DbPrefetch {  // one MB: luma 4 samples + chroma 2 samples per lane
@@ -2876,31 +2892,57 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
             {
                 const bool last_row = row == mbh - 1;
                 const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
-                auto st4 = [&](Pel* d, uint32_t a, uint32_t b, uint32_t c2_, uint32_t d2) __attribute__((always_inline)) {
-                    if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = a | (b << 8) | (c2_ << 16) | (d2 << 24);
-                    else *reinterpret_cast<uint2*>(d) = make_uint2(a | (b << 16), c2_ | (d2 << 16));
+                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][64] | chroma [2][2][32]
+                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][64] | chroma [2][8][32]
+                auto put4 = [&](Pel* d, uint32_t a, uint32_t b, uint32_t c2_, uint32_t d2) __attribute__((always_inline)) {
+                    d[0] = static_cast<Pel>(a); d[1] = static_cast<Pel>(b); d[2] = static_cast<Pel>(c2_); d[3] = static_cast<Pel>(d2);
                 };
-                if (row > 0 && lane < 16) {  // luma rows 12..15 of the MB above
+                // rows 12..15 of the MB above, staged at its 4-MB group column
+                if (row > 0 && lane < 16) {
                     const int tr = lane >> 2, c4 = (lane & 3) * 4;
-                    st4(PY + (row * 16 - 4 + tr) * sty + mx * 16 + c4, w.y[tr][c4 + 4], w.y[tr][c4 + 5], w.y[tr][c4 + 6],
-                        w.y[tr][c4 + 7]);
-                } else if (row > 0 && lane >= 16 && lane < 24) {  // chroma rows 6..7 of the MB above
+                    put4(SA + tr * 64 + (mx & 3) * 16 + c4, w.y[tr][c4 + 4], w.y[tr][c4 + 5], w.y[tr][c4 + 6], w.y[tr][c4 + 7]);
+                } else if (row > 0 && lane >= 16 && lane < 24) {  // chroma rows 6..7
                     const int k = lane - 16, cc = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
-                    st4(PC[cc] + (row * 8 - 2 + cr) * stc + mx * 8 + c4, w.c[cc][cr][c4 + 2], w.c[cc][cr][c4 + 3],
-                        w.c[cc][cr][c4 + 4], w.c[cc][cr][c4 + 5]);
+                    put4(SA + 256 + (cc * 2 + cr) * 32 + (mx & 3) * 8 + c4, w.c[cc][cr][c4 + 2], w.c[cc][cr][c4 + 3],
+                         w.c[cc][cr][c4 + 4], w.c[cc][cr][c4 + 5]);
                 }
-                if (mx > 0 && lane < nr * 4) {  // luma of the previous MB: columns 0..11 saved, 12..15 in the window
-                    const int r = lane >> 2, c4 = (lane & 3) * 4;
-                    uint32_t v0, v1, v2, v3;
-                    if (c4 < 12) { v0 = w.py[r][c4]; v1 = w.py[r][c4 + 1]; v2 = w.py[r][c4 + 2]; v3 = w.py[r][c4 + 3]; }
-                    else { v0 = w.y[r + 4][0]; v1 = w.y[r + 4][1]; v2 = w.y[r + 4][2]; v3 = w.y[r + 4][3]; }
-                    st4(PY + (row * 16 + r) * sty + (mx - 1) * 16 + c4, v0, v1, v2, v3);
+                if (row > 0 && ((mx & 3) == 3 || mx == mbw - 1)) {  // the group's rows 12..15 out
+                    wave_sync();
+                    const int g0 = mx & ~3, nmb = mx - g0 + 1;
+                    const int tr = lane >> 4, sg = lane & 15;  // luma: 4 rows x 16 segments of 4
+                    if (sg < 4 * nmb) db264_copy<Pel, 4>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * 4, SA + tr * 64 + sg * 4);
+                    if (lane < 32) {  // chroma: 2 comps x 2 rows x 8 segments of 4
+                        const int cc = lane >> 4, cr = (lane >> 3) & 1, cs = lane & 7;
+                        if (cs < 2 * nmb)
+                            db264_copy<Pel, 4>(PC[cc] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * 4, SA + 256 + (cc * 2 + cr) * 32 + cs * 4);
+                    }
                 }
-                if (mx > 0 && lane < 4 * ncr) {  // chroma of the previous MB: column 7 in the window
-                    const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
-                    const uint32_t v3 = c4 ? w.c[cc][cr + 2][1] : w.pc[cc][cr][3];
-                    st4(PC[cc] + (row * 8 + cr) * stc + (mx - 1) * 8 + c4, w.pc[cc][cr][c4], w.pc[cc][cr][c4 + 1],
-                        w.pc[cc][cr][c4 + 2], v3);
+                // this row's final rows: the previous MB (columns 0..11 saved, 12..15 in the window)
+                // and, on the row's last MB, the MB itself; staged at their group columns
+                auto flush_b = [&](int g0, int nmb) __attribute__((always_inline)) {
+                    wave_sync();
+                    const int r = lane >> 2, sg = lane & 3;  // luma: 16 rows x 4 segments of 16
+                    if (r < nr && sg < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sg * 16, SB + r * 64 + sg * 16);
+                    const int cc = lane >> 5, cr = (lane >> 2) & 7;  // chroma: 2 comps x 8 rows x 4 segments of 8
+                    if (cr < ncr && sg < nmb)
+                        db264_copy<Pel, 8>(PC[cc] + (row * 8 + cr) * stc + g0 * 8 + sg * 8, SB + 1024 + (cc * 8 + cr) * 32 + sg * 8);
+                };
+                if (mx > 0) {
+                    const int sx = ((mx - 1) & 3) * 16;
+                    if (lane < nr * 4) {
+                        const int r = lane >> 2, c4 = (lane & 3) * 4;
+                        uint32_t v0, v1, v2, v3;
+                        if (c4 < 12) { v0 = w.py[r][c4]; v1 = w.py[r][c4 + 1]; v2 = w.py[r][c4 + 2]; v3 = w.py[r][c4 + 3]; }
+                        else { v0 = w.y[r + 4][0]; v1 = w.y[r + 4][1]; v2 = w.y[r + 4][2]; v3 = w.y[r + 4][3]; }
+                        put4(SB + r * 64 + sx + c4, v0, v1, v2, v3);
+                    }
+                    if (lane < 4 * ncr) {  // chroma: column 7 in the window
+                        const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
+                        const uint32_t v3 = c4 ? w.c[cc][cr + 2][1] : w.pc[cc][cr][3];
+                        put4(SB + 1024 + (cc * 8 + cr) * 32 + (sx >> 1) + c4, w.pc[cc][cr][c4], w.pc[cc][cr][c4 + 1],
+                             w.pc[cc][cr][c4 + 2], v3);
+                    }
+                    if (((mx - 1) & 3) == 3) flush_b(mx - 4, 4);
                 }
                 // this MB's columns 0..11 / chroma 0..6 wait for the next MB (in-order LDS: the reads
                 // above have returned their values before these writes land)
@@ -2910,17 +2952,18 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                     w.pc[cc][cr][c2] = w.c[cc][cr + 2][c2 + 2];
                     w.pc[cc][cr][c2 + 1] = w.c[cc][cr + 2][c2 + 3];
                 }
-                if (mx == mbw - 1) {  // the row's last MB: nothing to its right, store its rows now
+                if (mx == mbw - 1) {  // the row's last MB: nothing to its right, its rows are final now
+                    const int sx = (mx & 3) * 16;
                     if (lane < nr * 4) {
                         const int r = lane >> 2, c4 = (lane & 3) * 4;
-                        st4(PY + (row * 16 + r) * sty + mx * 16 + c4, w.y[r + 4][c4 + 4], w.y[r + 4][c4 + 5],
-                            w.y[r + 4][c4 + 6], w.y[r + 4][c4 + 7]);
+                        put4(SB + r * 64 + sx + c4, w.y[r + 4][c4 + 4], w.y[r + 4][c4 + 5], w.y[r + 4][c4 + 6], w.y[r + 4][c4 + 7]);
                     }
                     if (lane < 4 * ncr) {
                         const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
-                        st4(PC[cc] + (row * 8 + cr) * stc + mx * 8 + c4, w.c[cc][cr + 2][c4 + 2], w.c[cc][cr + 2][c4 + 3],
-                            w.c[cc][cr + 2][c4 + 4], w.c[cc][cr + 2][c4 + 5]);
+                        put4(SB + 1024 + (cc * 8 + cr) * 32 + (sx >> 1) + c4, w.c[cc][cr + 2][c4 + 2], w.c[cc][cr + 2][c4 + 3],
+                             w.c[cc][cr + 2][c4 + 4], w.c[cc][cr + 2][c4 + 5]);
                     }
+                    flush_b(mx & ~3, (mx & 3) + 1);
                 }
             }
             // line buffer for the row below: the MB's bottom rows (columns final so far) and
