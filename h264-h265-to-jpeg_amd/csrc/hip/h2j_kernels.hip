@@ -208,7 +208,7 @@ constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) pe
 
 struct K0Lds {
     int blk[32 * 32];
-    int tmp[32 * 32];
+    int tmp[32 * 34];  // HEVC groups: int16 rows padded to N + 2 (bank-conflict-free transposition)
     int dc[16];
 };
 
@@ -348,9 +348,10 @@ template <int LOG2N>
 DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
                               const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0Lds& s) {
     constexpr int N = 1 << LOG2N, NN = N * N, MSH = 5 - LOG2N;
+    constexpr int P = N + 2, NP = N * P;  // tmp row stride (int16): odd dword stride across lanes
     const int lane = threadIdx.x;
     int16_t* blk = reinterpret_cast<int16_t*>(s.blk);  // [G][N][N] dequantised coefficients
-    int16_t* tmp = reinterpret_cast<int16_t*>(s.tmp);  // [G][N][N] after the column pass (row-major)
+    int16_t* tmp = reinterpret_cast<int16_t*>(s.tmp);  // [G][N][P] after the column pass (row-major, padded)
     for (int i = lane * 8; i < G * NN; i += 512) *reinterpret_cast<uint4*>(blk + i) = make_uint4(0, 0, 0, 0);
     wave_sync();
     int mx = 0, my = 0;
@@ -409,7 +410,7 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
             for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
         }
 #pragma unroll
-        for (int i = 0; i < N; i++) tmp[g * NN + i * N + q] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
+        for (int i = 0; i < N; i++) tmp[g * NP + i * P + q] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
     }
     wave_sync();
     if (act) {  // rows: r[y][x] = (sum_j M[j][x] * tmp[y][j] + rnd) >> (20 - bitDepth)
@@ -417,7 +418,7 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
 #pragma unroll
         for (int i = 0; i < N; i++) acc[i] = 0;
         for (int j = 0; j <= mxx; j++) {
-            const int v = tmp[g * NN + q * N + j];
+            const int v = tmp[g * NP + q * P + j];
 #pragma unroll
             for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
         }
