@@ -93,6 +93,14 @@ std::vector<int> node_cpus(int node) {
     return parse_cpulist(line);
 }
 
+int local_procs() {
+    for (const char* name : {"H2J_LOCAL_PROCS", "LOCAL_WORLD_SIZE"}) {
+        const char* v = std::getenv(name);
+        if (v && std::atoi(v) > 0) return std::atoi(v);
+    }
+    return 1;
+}
+
 HostPlan plan_host(int device, const std::vector<int>& device_nodes, const std::vector<int>& cpus,
                    const std::vector<int>& node_cpu_list, double quota, int requested, int engines) {
     HostPlan plan;
@@ -131,7 +139,8 @@ HostPlan plan_host(int device, const std::vector<int>& device_nodes, const std::
     int t = requested;
     if (t <= 0) {
         t = static_cast<int>(slice.size());
-        if (quota > 0) t = std::min(t, std::max(1, static_cast<int>(std::ceil(quota / engines))));
+        // the cgroup quota is shared by every engine of every process of the node's job
+        if (quota > 0) t = std::min(t, std::max(1, static_cast<int>(std::ceil(quota / (engines * local_procs())))));
         t = std::min(t, 64);
     }
     plan.threads = std::max(1, t);

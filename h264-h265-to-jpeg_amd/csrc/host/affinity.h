@@ -23,8 +23,13 @@ double cgroup_cpu_quota();                             // cores (cgroup v2 cpu.m
 int pci_numa_node(const std::string& bus_id);          // sysfs numa_node of a PCI device, -1 unknown
 std::vector<int> node_cpus(int node);                  // sysfs cpulist of a NUMA node
 
+// processes of this job on the node that share the cgroup CPU quota: $H2J_LOCAL_PROCS, else
+// torchrun's $LOCAL_WORLD_SIZE, else 1
+int local_procs();
+
 // device_nodes[i]: NUMA node of visible device i.  requested > 0 fixes the thread count;
-// engines: engines of this process (their share of the cgroup quota).  H2J_PIN=0 disables pinning.
+// engines: engines of this process; the cgroup quota is divided by engines x local_procs().
+// H2J_PIN=0 disables pinning.
 HostPlan plan_host(int device, const std::vector<int>& device_nodes, const std::vector<int>& cpus,
                    const std::vector<int>& node_cpu_list, double quota, int requested, int engines);
 

@@ -35,8 +35,8 @@ def _sysfs(tmp_path, nodes, cpu_max=None, pci=None):
     return str(tmp_path)
 
 
-def _plan(probe, root, device, nodes, cpus, quota=0, requested=0, engines=1, pin="1"):
-    env = dict(os.environ, H2J_SYSFS_ROOT=root, H2J_PIN=pin)
+def _plan(probe, root, device, nodes, cpus, quota=0, requested=0, engines=1, pin="1", procs=1):
+    env = dict(os.environ, H2J_SYSFS_ROOT=root, H2J_PIN=pin, H2J_LOCAL_PROCS=str(procs))
     out = subprocess.check_output([probe, "plan", str(device), ",".join(map(str, nodes)), cpus, str(quota),
                                    str(requested), str(engines)], env=env, text=True).split()
     kv = dict(x.split("=", 1) for x in out)
@@ -69,6 +69,21 @@ def test_quota_bounds_threads_and_is_shared_by_engines(probe, tmp_path):
     assert t == 64  # no quota: capped at 64
     t, _, _ = _plan(probe, root, 0, [0], "0-127", requested=5)
     assert t == 5
+
+
+def test_quota_is_shared_by_the_ranks_of_a_node(probe, tmp_path):
+    # torchrun: 8 rank processes in one cgroup with a 128-CPU quota, 8 GPUs on 2 NUMA nodes
+    root = _sysfs(tmp_path, {0: "0-127", 1: "128-255"})
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    for dev in range(8):
+        t, n, cl = _plan(probe, root, dev, nodes, "0-255", quota=128, procs=8)
+        assert t == 16 and n == nodes[dev] and len(cl) == 32
+    # LOCAL_WORLD_SIZE (torchrun) is the fallback for H2J_LOCAL_PROCS
+    env = dict(os.environ, H2J_SYSFS_ROOT=root, H2J_PIN="1", LOCAL_WORLD_SIZE="4")
+    env.pop("H2J_LOCAL_PROCS", None)
+    out = subprocess.check_output([probe, "plan", "0", ",".join(map(str, nodes)), "0-255", "128", "0", "1"],
+                                  env=env, text=True)
+    assert out.startswith("threads=32 ")
 
 
 def test_mask_outside_node_and_unknown_topology(probe, tmp_path):
