@@ -400,28 +400,49 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
         if (LOG2N != 2) return cv;
         return dst ? kDst4i[j][i] : cv;
     };
+    // One pass of the N-point inverse transform over inputs 0..jmax: acc[i] = sum_j M[j][i] * in(j).
+    // DCT rows are even / odd symmetric (M[j][N-1-i] = (-1)^j M[j][i]), so for N >= 8 the even and
+    // odd input rows each feed N/2 partial sums: E[i] +/- O[i] (half the multiply-adds, same sums).
+    auto pass = [&](int jmax, auto in, int (&acc)[N]) __attribute__((always_inline)) {
+        if constexpr (N >= 8) {
+            int E[N / 2], O[N / 2];
+#pragma unroll
+            for (int i = 0; i < N / 2; i++) E[i] = O[i] = 0;
+            for (int j = 0; j <= jmax; j += 2) {
+                const int v = in(j);
+#pragma unroll
+                for (int i = 0; i < N / 2; i++) E[i] += coef(j, i) * v;
+            }
+            for (int j = 1; j <= jmax; j += 2) {
+                const int v = in(j);
+#pragma unroll
+                for (int i = 0; i < N / 2; i++) O[i] += coef(j, i) * v;
+            }
+#pragma unroll
+            for (int i = 0; i < N / 2; i++) {
+                acc[i] = E[i] + O[i];
+                acc[N - 1 - i] = E[i] - O[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; i++) acc[i] = 0;
+            for (int j = 0; j <= jmax; j++) {
+                const int v = in(j);
+#pragma unroll
+                for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
+            }
+        }
+    };
     if (act) {  // columns: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
         int acc[N];
-#pragma unroll
-        for (int i = 0; i < N; i++) acc[i] = 0;
-        for (int j = 0; j <= myy; j++) {
-            const int v = blk[g * NN + j * N + q];
-#pragma unroll
-            for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
-        }
+        pass(myy, [&](int j) { return static_cast<int>(blk[g * NN + j * N + q]); }, acc);
 #pragma unroll
         for (int i = 0; i < N; i++) tmp[g * NP + i * P + q] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
     }
     wave_sync();
     if (act) {  // rows: r[y][x] = (sum_j M[j][x] * tmp[y][j] + rnd) >> (20 - bitDepth)
         int acc[N];
-#pragma unroll
-        for (int i = 0; i < N; i++) acc[i] = 0;
-        for (int j = 0; j <= mxx; j++) {
-            const int v = tmp[g * NP + q * P + j];
-#pragma unroll
-            for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
-        }
+        pass(mxx, [&](int j) { return static_cast<int>(tmp[g * NP + q * P + j]); }, acc);
         const int bdS = 20 - (mine.c ? f.bdc : f.bd);
         const int c = mine.c;
         int16_t* R = res + (c == 0 ? 0 : (c == 1 ? off1 : off2)) + (mine.y + q) * (c ? st1 : st0) + mine.x;
