@@ -3335,34 +3335,56 @@ DEVI int jpeg_sample(const h2j_frame& f, const uint8_t* arena, int c, int x, int
     return v;
 }
 
-template <typename Pel>
-DEVI long long mb_var(const h2j_frame& f, const uint8_t* arena, int mx, int my) {
-    unsigned s = 0, n = 0;
-    for (int j = 0; j < 16; j++)
-        for (int i = 0; i < 16; i++) {
-            const unsigned p = static_cast<unsigned>(jpeg_sample<Pel>(f, arena, 0, mx * 16 + i, my * 16 + j));
-            s += p;
-            n += p * p;
-        }
-    return static_cast<long long>((n - ((s * s) >> 8) + 500 + 128) >> 8);
-}
 
-__global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* frames, uint8_t* arena) {
+// 16 lanes per macroblock, one 16-sample row each (4 dword loads at 8 bits inside the picture,
+// jpeg_sample's clamped path at the edges / above 8 bits); the row sums meet by DPP row shifts.
+DEVI unsigned row16_sum(unsigned x) {  // inclusive prefix over each 16-lane row: lane 15 = total
+    x += static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false));
+    x += static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false));
+    x += static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false));
+    x += static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
+    return x;
+}
+__global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restrict__ frames, uint8_t* __restrict__ arena) {
     const h2j_frame& f = frames[blockIdx.y];
     const int mbw = (f.out_w + 15) >> 4, mbh = (f.out_h + 15) >> 4;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    long long v = 0;
-    if (idx < mbw * mbh) {
-        v = f.bit_depth == 8 ? mb_var<uint8_t>(f, arena, idx % mbw, idx / mbw)
-                             : mb_var<uint16_t>(f, arena, idx % mbw, idx / mbw);
-    }
+    const int mb = blockIdx.x * 16 + static_cast<int>(threadIdx.x >> 4), r = threadIdx.x & 15;
+    unsigned s = 0, n = 0;
+    const bool live = mb < mbw * mbh;
+    if (live) {
+        const int mx = mb % mbw, my = mb / mbw;
+        if (f.bit_depth == 8 && mx * 16 + 15 < f.out_w && (f.crop_x & 3) == 0) {
+            const int y = min(my * 16 + r, f.out_h - 1);
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(arena + f.pic2 + f.pic_off[0] +
+                                                                  static_cast<size_t>(y + f.crop_y) * f.pic_stride[0] +
+                                                                  mx * 16 + f.crop_x);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __shared__ long long part[4];
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+            for (int k = 0; k < 4; k++) {
+                const uint32_t w = p[k];
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const unsigned v = (w >> (8 * b)) & 0xFF;
+                    s += v;
+                    n += v * v;
+                }
+            }
+        } else {
+            for (int i = 0; i < 16; i++) {
+                const unsigned v = static_cast<unsigned>(f.bit_depth == 8 ? jpeg_sample<uint8_t>(f, arena, 0, mx * 16 + i, my * 16 + r)
+                                                                          : jpeg_sample<uint16_t>(f, arena, 0, mx * 16 + i, my * 16 + r));
+                s += v;
+                n += v * v;
+            }
+        }
+    }
+    s = row16_sum(s);
+    n = row16_sum(n);
+    __shared__ long long part[16];
+    if (r == 15) part[threadIdx.x >> 4] = live ? static_cast<long long>((n - ((s * s) >> 8) + 500 + 128) >> 8) : 0;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const long long t = part[0] + part[1] + part[2] + part[3];
+        long long t = 0;
+        for (int k = 0; k < 16; k++) t += part[k];
         if (t) {
             h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
             atomicAdd(reinterpret_cast<unsigned long long*>(&js->var_sum), static_cast<unsigned long long>(t));
@@ -3895,7 +3917,7 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int mbs = b->max_mcu;
-    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 255) / 256, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena);
     int r = check(hipGetLastError(), "h2j_k4a_variance");
     if (r) return r;
     hipLaunchKernelGGL(h2j_k4b_ratecontrol, dim3(b->nframes), dim3(64), 0, s, b->frames, b->arena);
