@@ -270,9 +270,13 @@ DEVI uint32_t block_bits(const CodeLds& c, const uint32_t* sym, int cnt, int t, 
     const int nd = nbits16(dc_diff);
     uint32_t bits = c.len[tab][nd] + nd;
     const uint8_t* al = c.len[2 + tab];
-    for (int k = 0; k < cnt; k++) {
-        const uint32_t w = sym[k * kTile + t];
-        bits += al[w & 0xFF] + ((w >> 8) & 15);
+    for (int k = 0; k < cnt; k += 8) {  // 8 symbol loads in flight per lane
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = k + j < cnt ? sym[(k + j) * kTile + t] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (k + j < cnt) bits += al[w[j] & 0xFF] + ((w[j] >> 8) & 15);
     }
     return bits;
 }
@@ -448,11 +452,17 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     if (nd) s.put(static_cast<uint32_t>(diff < 0 ? diff - 1 : diff) & ((1u << nd) - 1u), nd);
     const uint8_t* al = cl.len[2 + tab];
     const uint16_t* ac = cl.code[2 + tab];
-    for (int k = 0; k < cnt; k++) {
-        const uint32_t w = sym[k * kTile + t];
-        const int sv = static_cast<int>(w & 0xFF), n = static_cast<int>((w >> 8) & 15);
-        s.put(ac[sv], al[sv]);
-        if (n) s.put(w >> 12, n);
+    for (int k = 0; k < cnt; k += 8) {  // 8 symbol loads in flight per lane
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = k + j < cnt ? sym[(k + j) * kTile + t] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (k + j >= cnt) break;
+            const int sv = static_cast<int>(w[j] & 0xFF), n = static_cast<int>((w[j] >> 8) & 15);
+            s.put(ac[sv], al[sv]);
+            if (n) s.put(w[j] >> 12, n);
+        }
     }
     if (bi == nblk - 1) {
         const int pad = (8 - static_cast<int>((bit0 + bits) & 7)) & 7;  // FFmpeg: pad with 1-bits
