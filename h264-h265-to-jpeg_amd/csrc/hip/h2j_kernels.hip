@@ -3353,8 +3353,9 @@ __global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restr
     const bool live = mb < mbw * mbh;
     if (live) {
         const int mx = mb % mbw, my = mb / mbw;
-        if (f.bit_depth == 8 && mx * 16 + 15 < f.out_w && (f.crop_x & 3) == 0) {
-            const int y = min(my * 16 + r, f.out_h - 1);
+        const bool inside = mx * 16 + 15 < f.out_w && (f.crop_x & 3) == 0;
+        const int y = min(my * 16 + r, f.out_h - 1);
+        if (inside && f.bit_depth == 8) {
             const uint32_t* p = reinterpret_cast<const uint32_t*>(arena + f.pic2 + f.pic_off[0] +
                                                                   static_cast<size_t>(y + f.crop_y) * f.pic_stride[0] +
                                                                   mx * 16 + f.crop_x);
@@ -3364,6 +3365,22 @@ __global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restr
 #pragma unroll
                 for (int b = 0; b < 4; b++) {
                     const unsigned v = (w >> (8 * b)) & 0xFF;
+                    s += v;
+                    n += v * v;
+                }
+            }
+        } else if (inside && f.bit_depth > 8) {  // 16-bit samples, converted as jpeg_sample does
+            const uint2* p = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(arena + f.pic2) + f.pic_off[0] +
+                                                            static_cast<size_t>(y + f.crop_y) * f.pic_stride[0] +
+                                                            mx * 16 + f.crop_x);
+            const int bd = f.bit_depth;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint2 w = p[k];
+                const uint32_t h[4] = {w.x & 0xFFFF, w.x >> 16, w.y & 0xFFFF, w.y >> 16};
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const unsigned v = min((h[b] + (1u << (bd - 9))) >> (bd - 8), 255u);
                     s += v;
                     n += v * v;
                 }
@@ -3562,6 +3579,25 @@ DEVI void jpeg_block_coefs(const h2j_frame& f, const uint8_t* arena, int bi, int
             for (int i = 0; i < 4; i++) {
                 blk[j * 8 + i] = static_cast<int16_t>((v.x >> (8 * i)) & 0xFF);
                 blk[j * 8 + 4 + i] = static_cast<int16_t>((v.y >> (8 * i)) & 0xFF);
+            }
+        }
+    } else if (sizeof(Pel) == 2 && x0 + 8 <= pw && y0 + 8 <= ph && ((cx + x0) & 7) == 0 && (f.pic_stride[c] & 7) == 0) {
+        // 16-bit samples inside the picture: eight 16-byte row loads, converted as jpeg_sample does
+        const uint16_t* p = reinterpret_cast<const uint16_t*>(arena + f.pic2) + f.pic_off[c] +
+                            static_cast<size_t>(cy + y0) * f.pic_stride[c] + cx + x0;
+        const int bd = c ? f.bit_depth_c : f.bit_depth;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(p + static_cast<size_t>(j) * f.pic_stride[c]);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                int u = static_cast<int>((w[i >> 1] >> (16 * (i & 1))) & 0xFFFF);
+                if (bd > 8) {
+                    u = (u + (1 << (bd - 9))) >> (bd - 8);
+                    u = u > 255 ? 255 : u;
+                }
+                blk[j * 8 + i] = static_cast<int16_t>(u);
             }
         }
     } else {
