@@ -1665,9 +1665,12 @@ DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / 
 // 2n+1 .. 4n = p(k-2n-1, -1).  Each lane first resolves which sample its
 // (possibly substituted) reference comes from using only the availability
 // ballots, then reads it with one LDS load.
+// LN >= 0: a copy specialised for TBs of size 1 << LN (compile-time sizes fold the index
+// arithmetic of the common small TBs); LN < 0: any size.
+template <int LN>
 DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
                           const int16_t* top, const int16_t* left, K1WaveLds& s, int lane) {
-    const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
+    const int c = tu.c, log2n = LN >= 0 ? LN : tu.log2n, n = 1 << log2n, nn = n * n;
     const int bd = c ? u.bdc : u.bd;
     const int maxv = (1 << bd) - 1;
     const bool cbf = (tu.flags & H2J_TU_CBF) != 0;
@@ -1851,10 +1854,11 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
 // components share geometry, availability and the intra mode (chroma is never filtered, no
 // boundary smoothing), so the substitution indices, the reference gathers and the prediction
 // indices are computed once and applied to two register sets (lane k: Cb and Cr reference k).
+template <int LN>  // TB size 1 << LN (2 or 3), compile-time
 DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, uint64_t mask, int ox, int oy,
                                    int S, int16_t* bcb, int16_t* bcr, const int16_t* tcb, const int16_t* lcb,
                                    const int16_t* tcr, const int16_t* lcr, int lane) {
-    const int log2n = tb.log2n, n = 1 << log2n, nn = n * n;
+    constexpr int log2n = LN, n = 1 << log2n, nn = n * n;
     const int maxv = (1 << u.bdc) - 1;
     const bool cbf_cb = (tb.flags & H2J_TU_CBF) != 0;
     const int L = 4 * n + 1, nu = n;  // unit = 2 chroma samples
@@ -2089,9 +2093,14 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                         // Cb TB followed by the Cr TB at the same place: one pass for both
                         const h2j_tu tr = tu_from_lanes(rec, l + 1);
                         if (tr.c == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2n == tu.log2n && !(tr.flags & H2J_TU_PCM)) {
-                            hevc_predict_chroma_pair(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
-                                                     body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
-                                                     w.cs[1].left, lane);
+                            if (tu.log2n == 2)
+                                hevc_predict_chroma_pair<2>(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
+                                                            body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
+                                                            w.cs[1].left, lane);
+                            else
+                                hevc_predict_chroma_pair<3>(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
+                                                            body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
+                                                            w.cs[1].left, lane);
                             PROF_ADD(5, 2);
                             PROF_LAPK(tu.log2n - 2 + 4);
                             t += 2;
@@ -2106,8 +2115,12 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                                 static_cast<int16_t>(P[(tu.y + i / n) * u.st(c) + tu.x + (i % n)]);
                         wave_sync();
                     } else {
-                        hevc_predict_tb(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top,
-                                        w.cs[ci].left, w.k, lane);
+                        if (tu.log2n == 2)
+                            hevc_predict_tb<2>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                        else if (tu.log2n == 3)
+                            hevc_predict_tb<3>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                        else
+                            hevc_predict_tb<-1>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
                     }
                     PROF_ADD(5, 1);
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
