@@ -1665,8 +1665,8 @@ DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / 
 // 2n+1 .. 4n = p(k-2n-1, -1).  Each lane first resolves which sample its
 // (possibly substituted) reference comes from using only the availability
 // ballots, then reads it with one LDS load.
-// LN >= 0: a copy specialised for TBs of size 1 << LN (compile-time sizes fold the index
-// arithmetic of the common small TBs); LN < 0: any size.
+// One copy per TB size 1 << LN (compile-time sizes fold the index arithmetic; LN < 0: any
+// size, from tu.log2n).
 template <int LN>
 DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
                           const int16_t* top, const int16_t* left, K1WaveLds& s, int lane) {
@@ -2119,8 +2119,10 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                             hevc_predict_tb<2>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
                         else if (tu.log2n == 3)
                             hevc_predict_tb<3>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
-                        else
-                            hevc_predict_tb<-1>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                        else if (tu.log2n == 4)
+                            hevc_predict_tb<4>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                        else  // 32x32 (TB sizes are 4..32)
+                            hevc_predict_tb<5>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
                     }
                     PROF_ADD(5, 1);
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
