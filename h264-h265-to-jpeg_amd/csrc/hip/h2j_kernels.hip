@@ -27,6 +27,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2283,13 +2286,13 @@ __host__ __device__ constexpr size_t k1_pool_lds(int P, int maxrows, int lstride
     return sizeof(QWave) * kPoolWaves + (static_cast<size_t>(P) * 2 * maxrows + 4) * 4 +
            static_cast<size_t>(P) * lstride * 2;
 }
+// The pool's job loop over pictures fi0 .. fi0 + P - 1 (those below `nframes`) in `lds` (see
+// k1_pool_lds); every thread of the 16-wave workgroup calls it.
 template <typename Pel>
-__global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const h2j_frame* frames, const h2j_tu* tus,
-                                                                        uint8_t* arena, int nframes, int P, int maxrows,
-                                                                        int lstride, int lchroma) {
-    extern __shared__ __align__(16) uint8_t k1lds[];
-    QWave* W = reinterpret_cast<QWave*>(k1lds);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(k1lds + sizeof(QWave) * kPoolWaves);
+DEVI void hevc_pool_jobs(const h2j_frame* frames, const h2j_tu* tus, uint8_t* arena, int fi0, int nframes, int P,
+                         int maxrows, int lstride, int lchroma, uint8_t* lds) {
+    QWave* W = reinterpret_cast<QWave*>(lds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(lds + sizeof(QWave) * kPoolWaves);
     const int nprog = P * 2 * maxrows;
     uint32_t* queue = prog + nprog;
     int16_t* lines = reinterpret_cast<int16_t*>(queue + 4);
@@ -2304,7 +2307,7 @@ __global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const 
         if (j >= njobs) break;
         const int row = static_cast<int>(j) / (2 * P), rem = static_cast<int>(j) - row * 2 * P;
         const int p = rem >> 1, grp = rem & 1;
-        const int fi = static_cast<int>(blockIdx.x) * P + p;
+        const int fi = fi0 + p;
         if (fi >= nframes) continue;
         const h2j_frame& f = frames[fi];
         if (ufl(f.codec) != H2J_CODEC_HEVC || (ufl(f.bit_depth) > 8) != (sizeof(Pel) == 2)) continue;
@@ -2318,6 +2321,13 @@ __global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const 
         if (grp == 0) hevc_row<Pel>(u, T, masks, rng, 0, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
         else hevc_row<Pel>(u, T, masks, rng, 1, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
     }
+}
+template <typename Pel>
+__global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const h2j_frame* frames, const h2j_tu* tus,
+                                                                        uint8_t* arena, int nframes, int P, int maxrows,
+                                                                        int lstride, int lchroma) {
+    extern __shared__ __align__(16) uint8_t k1lds[];
+    hevc_pool_jobs<Pel>(frames, tus, arena, static_cast<int>(blockIdx.x) * P, nframes, P, maxrows, lstride, lchroma, k1lds);
 }
 
 // K1 for batches mixing HEVC 8-bit, HEVC high bit depth and H.264 pictures (configs[4]): one
@@ -2347,9 +2357,13 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
         const int wv = static_cast<int>(threadIdx.x >> 6);
         if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_rows<uint8_t>(f, T, arena, grp, W, prog, line, wv, kK1WavesWide);
         else hevc_rows<uint16_t>(f, T, arena, grp, W, prog, line, wv, kK1WavesWide);
-    } else if (me & 0x80000000u) {
-        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8) hevc_picture_groups<uint8_t>(f, T, arena, anylds, ybytes);
-        else hevc_picture_groups<uint16_t>(f, T, arena, anylds, ybytes);
+    } else if (me & 0x80000000u) {  // one HEVC picture: the pool's job loop over its rows (P = 1)
+        const int fi = static_cast<int>((me >> 8) & 0x3FFFFFu);
+        const int w = static_cast<int>(ufl(f.width)), rows = static_cast<int>(ufl(f.ctb_h));
+        if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8)
+            hevc_pool_jobs<uint8_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds);
+        else
+            hevc_pool_jobs<uint16_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds);
     } else {
         H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(anylds);
         uint32_t* prog = reinterpret_cast<uint32_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves);
@@ -3827,6 +3841,29 @@ int h2j_gpu_prof(unsigned long long* out, int n, int reset) {
 #endif
 }
 
+// companion stream + fork / join events of a chunk stream (created on first use, kept)
+struct AuxStream {
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static AuxStream* aux_stream(hipStream_t s) {
+    static std::mutex mu;
+    static std::vector<std::pair<hipStream_t, AuxStream*>> all;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : all)
+        if (e.first == s) return e.second;
+    AuxStream* a = new AuxStream();
+    if (hipStreamCreateWithFlags(&a->s2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&a->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a->join, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        delete a;
+        return nullptr;
+    }
+    all.emplace_back(s, a);
+    return a;
+}
+
 int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -3867,13 +3904,30 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     const size_t ybytes = (k1_fixed_lds(kYWaves) + line_bytes + 15) & ~size_t(15);   // luma group of a picture workgroup
     const size_t pbytes = ybytes + k1_fixed_lds(kCWaves) + line_bytes;                 // the whole picture workgroup
     const size_t wbytes = k1_fixed_lds(kK1WavesWide) + line_bytes;
-    const size_t lds_any = std::max(std::max(pbytes, lds264), wbytes);
+    // merged launch: an HEVC picture workgroup runs the pool's job loop with P = 1 (hevc_pool_jobs)
+    const size_t pool1 = k1_pool_lds(1, (b->max_h + 15) / 16, 2 * b->max_w + 192);
+    const size_t lds_any = std::max(std::max(pool1, lds264), wbytes);
     // one launch for every kind of picture (unless the widest picture's line buffers would not
     // fit one workgroup's LDS: then the per-kind launches below)
     if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
         hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
                            b->arena, b->k1all, static_cast<uint32_t>(ybytes));
         return check(hipGetLastError(), "h2j_k1_recon_any");
+    }
+    // per-kind launches: H.264 on a companion stream forked from (and joined back into) the
+    // chunk's stream, so its workgroups fill the CUs the HEVC launches leave idle
+    AuxStream* ax = (b->has_hevc && b->has_h264 && b->k1wgs > 0) ? aux_stream(s) : nullptr;
+    if (ax) {
+        (void)hipEventRecord(ax->fork, s);
+        (void)hipStreamWaitEvent(ax->s2, ax->fork, 0);
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, ax->s2, b->frames, b->tus,
+                           b->arena, b->k1map);
+        const int r = check(hipGetLastError(), "h2j_k1_recon_h264");
+        (void)hipEventRecord(ax->join, ax->s2);
+        if (r) {
+            (void)hipStreamWaitEvent(s, ax->join, 0);
+            return r;
+        }
     }
     if (b->has_hevc) {
         const bool p8 = pels == 0 || (pels & 1), p16 = pels == 0 || (pels & 2);
@@ -3911,9 +3965,10 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
                                         static_cast<uint32_t>(ybytes));
         }
         int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
+        if (ax) (void)hipStreamWaitEvent(s, ax->join, 0);
         if (r) return r;
     }
-    if (b->has_h264) {
+    if (b->has_h264 && !ax) {
         // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
         if (b->k1wgs > 0)
             hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, s, b->frames, b->tus,
