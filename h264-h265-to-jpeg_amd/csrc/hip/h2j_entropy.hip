@@ -83,7 +83,9 @@ __global__ void __launch_bounds__(kTile) h2j_k4e_dc_hist(const h2j_frame* frames
 struct HuffLds {
     int pv[260], pp[260];     // leaves (symbol, count), sorted by AV_QSORT
     int P[2][520];            // item probabilities of the previous / current list
-    uint16_t cum[16][520];    // cum[t][m] = leaves among the first m items of list t
+    uint64_t leaf[16][9];     // bit m of level t: item m of list t is a leaf (cumulative counts
+                              // by popcount; 1 KB instead of a 16 KB count table: more
+                              // workgroups per CU for this latency-bound serial kernel)
     int nlist[17];
     int nb[260];              // code length per symbol
     int hc[256], hl[256];     // (symbol, length) pairs
@@ -187,23 +189,30 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
     for (int lvl = 0; lvl <= 16; lvl++) {
         int* Pc = s.P[cur];
         const int* Pp = s.P[cur ^ 1];
-        int j = 0, n = 0, leaves = 0;
-        if (lvl < 16) {
-            i = 0;
-            s.cum[lvl][0] = 0;
-        }
+        int j = 0, n = 0;
+        uint64_t word = 0;  // leaf bits of the current 64 items
+        if (lvl < 16) i = 0;
         while (i < size || j + 1 < np) {
+            bool leaf;
             if (i < size && (j + 1 >= np || s.pp[i] < Pp[j] + Pp[j + 1])) {
                 Pc[n] = s.pp[i];
                 i++;
-                leaves++;
+                leaf = true;
             } else {
                 Pc[n] = Pp[j] + Pp[j + 1];
                 j += 2;
+                leaf = false;
+            }
+            if (lvl < 16) {
+                word |= static_cast<uint64_t>(leaf) << (n & 63);
+                if ((n & 63) == 63) {
+                    s.leaf[lvl][n >> 6] = word;
+                    word = 0;
+                }
             }
             n++;
-            if (lvl < 16) s.cum[lvl][n] = static_cast<uint16_t>(leaves);
         }
+        if (lvl < 16 && (n & 63)) s.leaf[lvl][n >> 6] = word;
         s.nlist[lvl] = n;
         np = n;
         cur ^= 1;
@@ -213,7 +222,9 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
         const int mn = size - 1 < s.nlist[16] ? size - 1 : s.nlist[16];
         int m = 2 * mn;
         for (int lvl = 15; lvl >= 0 && m > 0; lvl--) {
-            const int lv = s.cum[lvl][m];
+            int lv = 0;  // leaves among the first m items of list lvl
+            for (int wd = 0; wd < (m >> 6); wd++) lv += __popcll(s.leaf[lvl][wd]);
+            if (m & 63) lv += __popcll(s.leaf[lvl][m >> 6] & ((1ull << (m & 63)) - 1ull));
             for (int k = 0; k < lv; k++) s.nb[s.pv[k]]++;
             m = 2 * (m - lv);
         }
