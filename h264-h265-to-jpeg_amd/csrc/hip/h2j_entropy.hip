@@ -394,17 +394,22 @@ __global__ void __launch_bounds__(256) h2j_k5z_zero(uint8_t* seg, const uint64_t
 }
 
 // ---------------------------------------------------------------- K5d
+// MSB-first bit writer of one block into 32-bit big-endian words; the block's first word and
+// its last partial word may be shared with the neighbouring blocks (OR), the others are its own.
+// kLds: words of the workgroup's LDS image of its tile (index word - w0), else global words.
+template <bool kLds>
 struct BitSink {
     uint32_t* out;
-    uint32_t word;
+    uint32_t word, w0;
     uint64_t acc;
     int nacc;
     bool first;
 
     DEVI void store(uint32_t w, bool atomic) {
         const uint32_t be = __builtin_bswap32(w);
-        if (atomic) atomicOr(out + word, be);
-        else out[word] = be;
+        uint32_t* p = out + (kLds ? word - w0 : word);
+        if (atomic) atomicOr(p, be);
+        else *p = be;
         word++;
     }
     DEVI void put(uint32_t v, int n) {
@@ -421,10 +426,45 @@ struct BitSink {
     }
 };
 
+// A tile's payload is assembled in LDS when it fits (the usual case: a few hundred bytes per
+// 256 blocks): the blocks' shared boundary words meet in LDS atomics, and the tile goes out as
+// whole-word stores, only its first and last word by global atomics (shared with the
+// neighbouring tiles).  Larger tiles write straight to global memory as before.
+constexpr int kEmitWords = 8192;  // 32 KB
+
+template <bool kLds>
+DEVI void emit_block(uint32_t* out, uint32_t w0, uint32_t bit0, uint32_t bits, const CodeLds& cl, const uint32_t* sym,
+                     int cnt, int t, int diff, int tab, bool last_block) {
+    BitSink<kLds> s;
+    s.out = out;
+    s.w0 = w0;
+    s.word = bit0 >> 5;
+    s.acc = 0;
+    s.nacc = bit0 & 31;
+    s.first = true;
+    const int nd = nbits16(diff);
+    s.put(cl.code[tab][nd], cl.len[tab][nd]);
+    if (nd) s.put(static_cast<uint32_t>(diff < 0 ? diff - 1 : diff) & ((1u << nd) - 1u), nd);
+    const uint8_t* al = cl.len[2 + tab];
+    const uint16_t* ac = cl.code[2 + tab];
+    for (int k = 0; k < cnt; k++) {
+        const uint32_t w = sym[k * kTile + t];
+        const int sv = static_cast<int>(w & 0xFF), n = static_cast<int>((w >> 8) & 15);
+        s.put(ac[sv], al[sv]);
+        if (n) s.put(w >> 12, n);
+    }
+    if (last_block) {
+        const int pad = (8 - static_cast<int>((bit0 + bits) & 7)) & 7;  // FFmpeg: pad with 1-bits
+        if (pad) s.put((1u << pad) - 1u, pad);
+    }
+    s.finish();
+}
+
 __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, uint8_t* arena,
                                                       const uint32_t* tile_bits, int max_tiles, uint8_t* seg) {
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
+    __shared__ uint32_t img[kEmitWords];
     const h2j_frame& f = frames[blockIdx.y];
     const int nblk = nblocks(f);
     const int b0 = blockIdx.x * kTile;
@@ -450,36 +490,27 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     }
     uint32_t total;
     const uint32_t ex = wg_excl_scan(bits, sh, total);
-    if (!mine) return;
-    const uint32_t bit0 = tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x] + ex;
-    BitSink s;
-    s.out = reinterpret_cast<uint32_t*>(seg + js->seg_off);
-    s.word = bit0 >> 5;
-    s.acc = 0;
-    s.nacc = bit0 & 31;
-    s.first = true;
-    const int nd = nbits16(diff);
-    s.put(cl.code[tab][nd], cl.len[tab][nd]);
-    if (nd) s.put(static_cast<uint32_t>(diff < 0 ? diff - 1 : diff) & ((1u << nd) - 1u), nd);
-    const uint8_t* al = cl.len[2 + tab];
-    const uint16_t* ac = cl.code[2 + tab];
-    for (int k = 0; k < cnt; k += 8) {  // 8 symbol loads in flight per lane
-        uint32_t w[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) w[j] = k + j < cnt ? sym[(k + j) * kTile + t] : 0u;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (k + j >= cnt) break;
-            const int sv = static_cast<int>(w[j] & 0xFF), n = static_cast<int>((w[j] >> 8) & 15);
-            s.put(ac[sv], al[sv]);
-            if (n) s.put(w[j] >> 12, n);
+    const uint32_t tile0 = tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x];
+    const uint32_t bit0 = tile0 + ex;
+    uint32_t* out = reinterpret_cast<uint32_t*>(seg + js->seg_off);
+    const uint32_t w_lo = tile0 >> 5, w_hi = (tile0 + total + 31) >> 5;
+    const int nw = static_cast<int>(w_hi - w_lo);
+    if (nw > kEmitWords) {  // rare: straight to global memory
+        if (mine) emit_block<false>(out, 0, bit0, bits, cl, sym, cnt, t, diff, tab, bi == nblk - 1);
+        return;
+    }
+    for (int i = t; i < nw; i += kTile) img[i] = 0;
+    __syncthreads();
+    if (mine) emit_block<true>(img, w_lo, bit0, bits, cl, sym, cnt, t, diff, tab, bi == nblk - 1);
+    __syncthreads();
+    for (int i = t; i < nw; i += kTile) {
+        const uint32_t v = img[i];
+        if (i == 0 || i == nw - 1) {
+            if (v) atomicOr(out + w_lo + i, v);
+        } else {
+            out[w_lo + i] = v;
         }
     }
-    if (bi == nblk - 1) {
-        const int pad = (8 - static_cast<int>((bit0 + bits) & 7)) & 7;  // FFmpeg: pad with 1-bits
-        if (pad) s.put((1u << pad) - 1u, pad);
-    }
-    s.finish();
 }
 
 }  // namespace
