@@ -3217,6 +3217,13 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
     const int vy = cls == 0 ? 0 : -1;
     const int sh = c ? 1 : 0, l2b = f.log2ctb - 2;
     const int ts = g.ts;
+    // offsets as 6-bit signed fields (|SaoOffsetVal| <= 31 without range extensions; else the
+    // select form): etab by edgeIdx + 2 = 0..4 (categories 1, 2, none, 3, 4), btab by band 0..3
+    const auto f6 = [](int v) { return static_cast<uint32_t>(v) & 63u; };
+    const bool packed = max(max(abs(o0), abs(o1)), max(abs(o2), abs(o3))) <= 31;
+    const int etab = static_cast<int>(f6(o0) | (f6(o1) << 6) | (f6(o2) << 18) | (f6(o3) << 24));
+    const int btab = static_cast<int>(f6(o0) | (f6(o1) << 6) | (f6(o2) << 12) | (f6(o3) << 18));
+    const int da = vy * ts + hx;  // element offset of neighbour a (b is at -da)
     for (int i = tid; i < (g.h << g.lq); i += 256) {
         const int y = i >> g.lq, x = (i & ((1 << g.lq) - 1)) * 4;
         if (x >= g.w) continue;
@@ -3226,6 +3233,23 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
         // samples of pcm (loop filter off) / transquant-bypass blocks stay untouched
         const bool keep = type == 0 || L.keep[(((y << sh) >> 2) << l2b) + ((x << sh) >> 2)] != 0;
         int o[4];
+        if (type == 2 && packed) {  // edge offset, table form
+            const int16_t* C0 = T + (y + 1) * ts + 4 + x;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int a = C0[k + da], bb = C0[k - da];
+                const int sa = max(-1, min(1, v[k] - a)), sb = max(-1, min(1, v[k] - bb));
+                const int off = __builtin_amdgcn_sbfe(etab, 6 * (2 + sa + sb), 6);
+                o[k] = (keep || (a | bb) < 0) ? v[k] : clip3(0, maxv, v[k] + off);
+            }
+        } else if (type == 1 && packed) {  // band offset, table form
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int bi = ((v[k] >> (bd - 5)) - band) & 31;
+                const int off = bi < 4 ? __builtin_amdgcn_sbfe(btab, 6 * bi, 6) : 0;
+                o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             int sel = -1;  // offset index 0..3, -1 none
@@ -3243,6 +3267,7 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
             }
             const int off = sel == 0 ? o0 : (sel == 1 ? o1 : (sel == 2 ? o2 : (sel == 3 ? o3 : 0)));
             o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
+        }
         }
         Pel* d = D + (g.y0 + y) * st + g.x0 + x;
         if (sizeof(Pel) == 1) {
