@@ -408,13 +408,26 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     // odd input rows each feed N/2 partial sums: E[i] +/- O[i] (half the multiply-adds, same sums).
     auto pass = [&](int jmax, auto in, int (&acc)[N]) __attribute__((always_inline)) {
         if constexpr (N >= 8) {
-            int E[N / 2], O[N / 2];
+            // even rows once more: rows 0 mod 4 (EE) and 2 mod 4 (EO) of the N/2-point half
+            int E[N / 2], O[N / 2], EE[N / 4], EO[N / 4];
 #pragma unroll
-            for (int i = 0; i < N / 2; i++) E[i] = O[i] = 0;
-            for (int j = 0; j <= jmax; j += 2) {
+            for (int i = 0; i < N / 2; i++) O[i] = 0;
+#pragma unroll
+            for (int i = 0; i < N / 4; i++) EE[i] = EO[i] = 0;
+            for (int j = 0; j <= jmax; j += 4) {
                 const int v = in(j);
 #pragma unroll
-                for (int i = 0; i < N / 2; i++) E[i] += coef(j, i) * v;
+                for (int i = 0; i < N / 4; i++) EE[i] += coef(j, i) * v;
+            }
+            for (int j = 2; j <= jmax; j += 4) {
+                const int v = in(j);
+#pragma unroll
+                for (int i = 0; i < N / 4; i++) EO[i] += coef(j, i) * v;
+            }
+#pragma unroll
+            for (int i = 0; i < N / 4; i++) {
+                E[i] = EE[i] + EO[i];
+                E[N / 2 - 1 - i] = EE[i] - EO[i];
             }
             for (int j = 1; j <= jmax; j += 2) {
                 const int v = in(j);
