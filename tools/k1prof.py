@@ -5,6 +5,9 @@ import ctypes, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
 os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", os.environ.get("H2J_PROF_VARIANT", "prof"))
+# the cycle counters are read from the per-picture K1 kernels (h2j_k1_recon_hevc_pic / _hevc<16>);
+# the -DH2J_PROF build of the picture-pool kernel does not finish, so the pool is switched off
+os.environ.setdefault("H2J_K1_POOL", "0")
 sys.path.insert(0, PKG)
 import h2j
 files = [a for a in sys.argv[1:] if not a.isdigit()]
