@@ -31,6 +31,7 @@
 #include <cstdio>
 
 #include "h2j_gpu.h"
+#include "grid.h"
 #include "jpeg_tile.h"
 
 #define DEVI __device__ __forceinline__
@@ -316,16 +317,17 @@ DEVI uint32_t wg_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
 // ---------------------------------------------------------------- K5b
 __global__ void __launch_bounds__(kTile) h2j_k5b_tile_bits(const h2j_frame* frames, uint8_t* arena,
                                                            uint32_t* tile_bits, int max_tiles) {
+    const GridPos gp = xcd_grid_pos();
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
-    const h2j_frame& f = frames[blockIdx.y];
+    const h2j_frame& f = frames[gp.y];
     const int nblk = nblocks(f);
-    const int b0 = blockIdx.x * kTile;
+    const int b0 = gp.x * kTile;
     if (b0 >= nblk) return;
     const int nb = min(kTile, nblk - b0);
     const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
     const uint8_t* base = arena + f.jcoef;
-    const uint8_t* tile = base + static_cast<size_t>(blockIdx.x) * kJTileBytes;
+    const uint8_t* tile = base + static_cast<size_t>(gp.x) * kJTileBytes;
     load_codes(js, cl, false);
     __syncthreads();
     uint32_t bits = 0;
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(kTile) h2j_k5b_tile_bits(const h2j_frame* fram
     }
     uint32_t total;
     wg_excl_scan(bits, sh, total);
-    if (threadIdx.x == 0) tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x] = total;
+    if (threadIdx.x == 0) tile_bits[static_cast<size_t>(gp.y) * max_tiles + gp.x] = total;
 }
 
 // ---------------------------------------------------------------- K5c
@@ -462,18 +464,19 @@ DEVI void emit_block(uint32_t* out, uint32_t w0, uint32_t bit0, uint32_t bits, c
 
 __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, uint8_t* arena,
                                                       const uint32_t* tile_bits, int max_tiles, uint8_t* seg) {
+    const GridPos gp = xcd_grid_pos();
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
     __shared__ uint32_t img[kEmitWords];
-    const h2j_frame& f = frames[blockIdx.y];
+    const h2j_frame& f = frames[gp.y];
     const int nblk = nblocks(f);
-    const int b0 = blockIdx.x * kTile;
+    const int b0 = gp.x * kTile;
     if (b0 >= nblk) return;
     const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
     if (js->seg_off == ~0ull) return;  // pool overflow: host reports the frame as failed
     const int nb = min(kTile, nblk - b0);
     const uint8_t* base = arena + f.jcoef;
-    const uint8_t* tile = base + static_cast<size_t>(blockIdx.x) * kJTileBytes;
+    const uint8_t* tile = base + static_cast<size_t>(gp.x) * kJTileBytes;
     const uint32_t* sym = reinterpret_cast<const uint32_t*>(tile);
     load_codes(js, cl, true);
     __syncthreads();
@@ -490,7 +493,7 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     }
     uint32_t total;
     const uint32_t ex = wg_excl_scan(bits, sh, total);
-    const uint32_t tile0 = tile_bits[static_cast<size_t>(blockIdx.y) * max_tiles + blockIdx.x];
+    const uint32_t tile0 = tile_bits[static_cast<size_t>(gp.y) * max_tiles + gp.x];
     const uint32_t bit0 = tile0 + ex;
     uint32_t* out = reinterpret_cast<uint32_t*>(seg + js->seg_off);
     const uint32_t w_lo = tile0 >> 5, w_hi = (tile0 + total + 31) >> 5;

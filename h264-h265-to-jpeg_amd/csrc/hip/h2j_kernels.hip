@@ -35,6 +35,7 @@
 #include <cstring>
 
 #include "h2j_gpu.h"
+#include "grid.h"
 #include "jpeg_tile.h"
 
 #define DEVI __device__ __forceinline__
@@ -856,12 +857,13 @@ template <bool HEVC>
 __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
                                                  uint8_t* arena) {
+    const GridPos gp = xcd_grid_pos();
     constexpr int kTus = HEVC ? kK0TusHevc : kK0Tus;
     __shared__ K0Lds s;
-    const h2j_frame& fr = frames[blockIdx.y];
+    const h2j_frame& fr = frames[gp.y];
     if ((ufl(fr.codec) == H2J_CODEC_HEVC) != HEVC) return;
     const uint32_t ntu = ufl(fr.ntu);
-    const uint32_t t0 = blockIdx.x * kTus;
+    const uint32_t t0 = gp.x * kTus;
     if (t0 >= ntu) return;
     const int lane = threadIdx.x;
     constexpr bool hevc = HEVC;
@@ -3374,10 +3376,11 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
 __global__ void __launch_bounds__(256) h2j_k3_sao(const h2j_frame* __restrict__ frames,
                                                  const h2j_ctb* __restrict__ ctbs,
                                                  const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena) {
+    const GridPos gp = xcd_grid_pos();
     __shared__ SaoLds L;
-    const h2j_frame& f = frames[blockIdx.y];
+    const h2j_frame& f = frames[gp.y];
     if (f.codec != H2J_CODEC_HEVC || f.pic2 == f.pic) return;
-    const int ctb = blockIdx.x;
+    const int ctb = gp.x;
     if (ctb >= f.ctb_w * f.ctb_h) return;
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
@@ -3695,15 +3698,16 @@ DEVI int jnbits(int v) {
 }
 
 __global__ void __launch_bounds__(256) h2j_k4c_fdct_sym(const h2j_frame* frames, uint8_t* arena) {
+    const GridPos gp = xcd_grid_pos();
     __shared__ unsigned hist[2][256];
-    const h2j_frame& f = frames[blockIdx.y];
+    const h2j_frame& f = frames[gp.y];
     const int nblk = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4) * 6;
-    const int b0 = blockIdx.x * 256;
+    const int b0 = gp.x * 256;
     if (b0 >= nblk) return;
     for (int i = threadIdx.x; i < 512; i += 256) (&hist[0][0])[i] = 0;
     __syncthreads();
     const int t = threadIdx.x, bi = b0 + t;
-    uint8_t* tile = arena + f.jcoef + static_cast<size_t>(blockIdx.x) * kJTileBytes;
+    uint8_t* tile = arena + f.jcoef + static_cast<size_t>(gp.x) * kJTileBytes;
     uint32_t* sym = reinterpret_cast<uint32_t*>(tile);
     if (bi < nblk) {
         int16_t out[64];
