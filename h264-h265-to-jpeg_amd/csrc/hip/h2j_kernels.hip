@@ -85,7 +85,7 @@ DEVI bool avail(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices
 // HEVC 32x32 inverse transform matrix entries from the 33 distinct cosines
 __constant__ int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
 // the 32x32 HEVC DCT matrix (8.6.4.2, transMatrix), built at compile time from the 33 cosines
-// above; an N-point transform uses rows j * 32 / N.  int32 entries: rows load into scalar registers.
+// above; an N-point transform uses rows j * 32 / N (packed into kDctPk below).
 struct DctMat {
     int v[32][32];
 };
@@ -101,8 +101,58 @@ constexpr DctMat make_dct32() {
         }
     return t;
 }
-__constant__ DctMat kDct32 = make_dct32();
-__constant__ int kDst4i[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+
+// Paired-input layout of the batched HEVC inverse transforms (hevc_residual_group): the inputs
+// j of one N-point pass sit as int16 pairs in dwords, ordered the way the even/odd decomposition
+// consumes them -- slots [0, N/8): rows 0 mod 8 with 4 mod 8 (EE), [N/8, N/4): 2 mod 8 with 6
+// mod 8 (EO), [N/4, N/2): 1 mod 4 with 3 mod 4 (O); N = 4: (0, 1), (2, 3) -- so one
+// v_dot2c_i32_i16 (2 multiply-adds) consumes a dword against a packed pair of matrix entries.
+template <int N>
+__host__ __device__ constexpr int k0_pslot(int j) {
+    return N == 4 ? (j >> 1)
+           : (j & 1) ? N / 4 + (j >> 2)
+           : (j & 3) == 0 ? (j >> 3)
+                          : N / 8 + (j >> 3);
+}
+template <int N>
+__host__ __device__ constexpr int k0_phalf(int j) {
+    return N == 4 ? (j & 1) : (j & 1) ? ((j >> 1) & 1) : ((j >> 2) & 1);
+}
+// packed matrix entries (c(j0, i) in the low half, c(j1, i) in the high half) of slot s, output
+// i, for N = 4 << L (c = the rows of transMatrix an N-point transform uses); DST 4x4 apart
+struct DctPk {
+    int v[4][16][16];
+    int dst[2][4];
+};
+constexpr DctPk make_dct_pk() {
+    DctPk t{};
+    const DctMat m = make_dct32();
+    for (int L = 0; L < 4; L++) {
+        const int N = 4 << L, sh = 3 - L;
+        for (int s = 0; s < N / 2; s++) {
+            int j0 = 0, j1 = 0;
+            if (N == 4) { j0 = 2 * s; j1 = j0 + 1; }
+            else if (s < N / 8) { j0 = 8 * s; j1 = j0 + 4; }
+            else if (s < N / 4) { j0 = 8 * (s - N / 8) + 2; j1 = j0 + 4; }
+            else { j0 = 4 * (s - N / 4) + 1; j1 = j0 + 2; }
+            for (int i = 0; i < 16 && i < N; i++)
+                t.v[L][s][i] = static_cast<int>((static_cast<unsigned>(m.v[j0 << sh][i]) & 0xFFFFu) |
+                                                (static_cast<unsigned>(m.v[j1 << sh][i]) << 16));
+        }
+    }
+    constexpr int d[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+    for (int s = 0; s < 2; s++)
+        for (int i = 0; i < 4; i++)
+            t.dst[s][i] = static_cast<int>((static_cast<unsigned>(d[2 * s][i]) & 0xFFFFu) |
+                                           (static_cast<unsigned>(d[2 * s + 1][i]) << 16));
+    return t;
+}
+__constant__ DctPk kDctPk = make_dct_pk();
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// acc + lo(a) * lo(b) + hi(a) * hi(b), int16 halves, int32 accumulation (v_dot2c_i32_i16)
+__device__ __forceinline__ int dot2(int a, int b, int acc) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), acc, false);
+}
 
 // ---------------------------------------------------------------- K1: H.264
 // H.264 8.3 (intra prediction), 8.5 (scaling + transforms).  Records: luma
@@ -351,11 +401,11 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
 template <int LOG2N>
 DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
                               const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0Lds& s) {
-    constexpr int N = 1 << LOG2N, NN = N * N, MSH = 5 - LOG2N;
+    constexpr int N = 1 << LOG2N, NN = N * N;
     constexpr int P = N + 2, NP = N * P;  // tmp row stride (int16): odd dword stride across lanes
     const int lane = threadIdx.x;
-    int16_t* blk = reinterpret_cast<int16_t*>(s.blk);  // [G][N][N] dequantised coefficients
-    int16_t* tmp = reinterpret_cast<int16_t*>(s.tmp);  // [G][N][P] after the column pass (row-major, padded)
+    int16_t* blk = reinterpret_cast<int16_t*>(s.blk);  // [G][N/2 slots][N columns][2] dequantised coefficients
+    int16_t* tmp = reinterpret_cast<int16_t*>(s.tmp);  // [G][N rows][P] after the column pass, columns paired
     for (int i = lane * 8; i < G * NN; i += 512) *reinterpret_cast<uint4*>(blk + i) = make_uint4(0, 0, 0, 0);
     wave_sync();
     int mx = 0, my = 0;
@@ -376,7 +426,9 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
             const int m = slt ? slt[pos] : 16;
             long long v = static_cast<long long>(lvl) * m * ls;
             v = (v + (1ll << (bdShift - 1))) >> bdShift;
-            blk[g * NN + pos] = static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+            const int jr = pos >> LOG2N, xc = pos & (N - 1);
+            blk[g * NN + 2 * (k0_pslot<N>(jr) * N + xc) + k0_phalf<N>(jr)] =
+                static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
             mx = max(mx, pos & (N - 1));
             my = max(my, pos >> LOG2N);
         }
@@ -399,41 +451,39 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     h2j_tu mine;
     memcpy(&mine, wq, sizeof(mine));
     const bool dst = LOG2N == 2 && (mine.flags & H2J_TU_DST) != 0;
-    auto coef = [&](int j, int i) __attribute__((always_inline)) {
-        const int cv = kDct32.v[j << MSH][i];
-        if (LOG2N != 2) return cv;
-        return dst ? kDst4i[j][i] : cv;
-    };
-    // One pass of the N-point inverse transform over inputs 0..jmax: acc[i] = sum_j M[j][i] * in(j).
-    // DCT rows are even / odd symmetric (M[j][N-1-i] = (-1)^j M[j][i]), so for N >= 8 the even and
-    // odd input rows each feed N/2 partial sums: E[i] +/- O[i] (half the multiply-adds, same sums).
-    auto pass = [&](int jmax, auto in, int (&acc)[N]) __attribute__((always_inline)) {
+    // One pass of the N-point inverse transform over inputs 0..jmax: acc[i] = sum_j M[j][i] * in(j),
+    // the inputs read as paired dwords (k0_pslot) and consumed two per v_dot2c_i32_i16.  DCT rows
+    // are even / odd symmetric (M[j][N-1-i] = (-1)^j M[j][i]), so for N >= 8 the even and odd
+    // input rows each feed N/2 partial sums: E[i] +/- O[i], and the even half splits once more
+    // into rows 0 mod 4 (EE) and 2 mod 4 (EO).  Slots past jmax hold zeros, so a slot whose first
+    // input is <= jmax is taken whole.
+    constexpr int L = LOG2N - 2;
+    auto pass = [&](int jmax, auto inpair, int (&acc)[N]) __attribute__((always_inline)) {
         if constexpr (N >= 8) {
-            // even rows once more: rows 0 mod 4 (EE) and 2 mod 4 (EO) of the N/2-point half
             int E[N / 2], O[N / 2], EE[N / 4], EO[N / 4];
 #pragma unroll
             for (int i = 0; i < N / 2; i++) O[i] = 0;
 #pragma unroll
             for (int i = 0; i < N / 4; i++) EE[i] = EO[i] = 0;
-            for (int j = 0; j <= jmax; j += 4) {
-                const int v = in(j);
+            for (int ps = 0; ps < N / 8 && 8 * ps <= jmax; ps++) {
+                const int v = inpair(ps);
 #pragma unroll
-                for (int i = 0; i < N / 4; i++) EE[i] += coef(j, i) * v;
+                for (int i = 0; i < N / 4; i++) EE[i] = dot2(kDctPk.v[L][ps][i], v, EE[i]);
             }
-            for (int j = 2; j <= jmax; j += 4) {
-                const int v = in(j);
+            for (int ps = 0; ps < N / 8 && 8 * ps + 2 <= jmax; ps++) {
+                const int v = inpair(N / 8 + ps);
 #pragma unroll
-                for (int i = 0; i < N / 4; i++) EO[i] += coef(j, i) * v;
+                for (int i = 0; i < N / 4; i++) EO[i] = dot2(kDctPk.v[L][N / 8 + ps][i], v, EO[i]);
             }
 #pragma unroll
             for (int i = 0; i < N / 4; i++) {
                 E[i] = EE[i] + EO[i];
                 E[N / 2 - 1 - i] = EE[i] - EO[i];
             }
-            for (int j = 1; j <= jmax; j += 2) {
-                const int v = in(j);
+            for (int ps = 0; ps < N / 4 && 4 * ps + 1 <= jmax; ps++) {
+                const int v = inpair(N / 4 + ps);
 #pragma unroll
-                for (int i = 0; i < N / 2; i++) O[i] += coef(j, i) * v;
+                for (int i = 0; i < N / 2; i++) O[i] = dot2(kDctPk.v[L][N / 4 + ps][i], v, O[i]);
             }
 #pragma unroll
             for (int i = 0; i < N / 2; i++) {
@@ -443,23 +493,26 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
         } else {
 #pragma unroll
             for (int i = 0; i < N; i++) acc[i] = 0;
-            for (int j = 0; j <= jmax; j++) {
-                const int v = in(j);
+            for (int ps = 0; ps < 2 && 2 * ps <= jmax; ps++) {
+                const int v = inpair(ps);
 #pragma unroll
-                for (int i = 0; i < N; i++) acc[i] += coef(j, i) * v;
+                for (int i = 0; i < N; i++) acc[i] = dot2(dst ? kDctPk.dst[ps][i] : kDctPk.v[0][ps][i], v, acc[i]);
             }
         }
     };
+    const int* blk32 = reinterpret_cast<const int*>(blk);
+    const int* tmp32 = reinterpret_cast<const int*>(tmp);
+    const int qcol = 2 * k0_pslot<N>(q) + k0_phalf<N>(q);  // this lane's column in the paired tmp rows
     if (act) {  // columns: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
         int acc[N];
-        pass(myy, [&](int j) { return static_cast<int>(blk[g * NN + j * N + q]); }, acc);
+        pass(myy, [&](int ps) { return blk32[g * (NN / 2) + ps * N + q]; }, acc);
 #pragma unroll
-        for (int i = 0; i < N; i++) tmp[g * NP + i * P + q] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
+        for (int i = 0; i < N; i++) tmp[g * NP + i * P + qcol] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
     }
     wave_sync();
     if (act) {  // rows: r[y][x] = (sum_j M[j][x] * tmp[y][j] + rnd) >> (20 - bitDepth)
         int acc[N];
-        pass(mxx, [&](int j) { return static_cast<int>(tmp[g * NP + q * P + j]); }, acc);
+        pass(mxx, [&](int ps) { return tmp32[(g * NP + q * P) / 2 + ps]; }, acc);
         const int bdS = 20 - (mine.c ? f.bdc : f.bd);
         const int c = mine.c;
         int16_t* R = res + (c == 0 ? 0 : (c == 1 ? off1 : off2)) + (mine.y + q) * (c ? st1 : st0) + mine.x;
@@ -900,7 +953,7 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
         if (lane == kTus + 1) ri = static_cast<int>(t1);
         if (lane <= kTus + 1 && ri >= 0 && ri < static_cast<int>(ntu)) rec = reinterpret_cast<const uint4*>(T)[ri];
     }
-    // (the HEVC matrices are constants: kDct32 / kDst4i; transform-skip and bypass TBs use none)
+    // (the HEVC matrices are constants: kDctPk; transform-skip and bypass TBs use none)
     wave_sync();
     auto ctb_of_tu = [&](const h2j_tu& tu) __attribute__((always_inline)) {
         const int sh = tu.c ? 1 : 0;
