@@ -7,10 +7,11 @@
 //                           inverse DCT/DST batched by TB size (lane = TB column, then row)
 //                           into the int16 residual plane (H.265 8.6.2-8.6.4, H.264 8.5)
 //   K1 h2j_k1_recon_*       intra prediction + residual add along the dependency chains:
-//                           HEVC one workgroup per picture (luma and chroma chains in
-//                           separate waves, CTB rows as a wavefront, 32x32 quadrant windows in
-//                           LDS prefetched by LDS-DMA); H.264 one workgroup per picture or
-//                           16-MB-row band, MB-row wavefront in LDS windows
+//                           HEVC picture pool (a 16-wave workgroup reconstructs up to 4
+//                           pictures; waves take CTB-row jobs -- a picture's luma or Cb/Cr
+//                           chain -- from an LDS queue, rows run as a wavefront, 32x32
+//                           quadrant windows in LDS prefetched by LDS-DMA); H.264 one workgroup
+//                           per picture or 16-MB-row band, MB-row wavefront in LDS windows
 //                           (H.265 8.4.4.2, H.264 8.3)
 //   K2 h2j_k2_deblock*      HEVC: one thread per 4-line edge segment, V then H pass;
 //                           H.264: MB-row wavefront in LDS windows, banded like K1
