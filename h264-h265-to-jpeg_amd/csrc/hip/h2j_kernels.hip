@@ -2680,35 +2680,22 @@ __constant__ int kTc0_264[52][3] = {
 
 __constant__ int kChromaQp264[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
 
-// H.264 edge filter (8.7.2.3-8.7.2.4) on a line held in registers: the edge lies between
+// H.264 edge filter (8.7.2.3-8.7.2.4) on a line held in registers, for a lane that holds either a
+// luma line or a chroma line (`chroma`), so luma and chroma lanes run one instruction stream: chroma (8.7.2.3-8.7.2.4 with chromaEdgeFlag = 1) is the
+// luma filter with ap / aq < beta forced false -- tc = tc0 + 1, p1 / q1 untouched for bS < 4, the
+// 3-tap p0 / q0 form for bS 4 -- and only p1..q1 of it matter.  v: 20 samples, the edge between
 // v[E - 1] and v[E]; `on` false leaves the line as is.  Selects only (lanes diverge on data).
-template <int E, bool CHROMA, int LEN>
-DEVI void h264_filt_reg(int (&v)[LEN], bool on, int bs, int alpha, int beta, int tc0, int maxv) {
-    static_assert(E >= (CHROMA ? 2 : 4) && E + (CHROMA ? 2 : 4) <= LEN, "edge taps inside the line");
-    const int p0 = v[E - 1], p1 = v[E - 2], q0 = v[E], q1 = v[E + 1];
+template <int E>
+DEVI void h264_filt_line(int (&v)[20], bool on, int bs, int alpha, int beta, int tc0, int maxv, bool chroma) {
+    const int p0 = v[E - 1], p1 = v[E - 2], p2 = v[E - 3], q0 = v[E], q1 = v[E + 1], q2 = v[E + 2];
     const bool f = on && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta;
-    if constexpr (CHROMA) {
-        int np0, nq0;
-        if (bs < 4) {
-            const int tc = tc0 + 1;
-            const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
-            np0 = clip3(0, maxv, p0 + dl);
-            nq0 = clip3(0, maxv, q0 - dl);
-        } else {
-            np0 = (2 * p1 + p0 + q1 + 2) >> 2;
-            nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
-        }
-        v[E - 1] = f ? np0 : p0;
-        v[E] = f ? nq0 : q0;
-    } else {
-    const int p2 = v[E - 3], q2 = v[E + 2];
-    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+    const bool apb = !chroma && abs(p2 - p0) < beta, aqb = !chroma && abs(q2 - q0) < beta;
     if (bs < 4) {
-        const int tc = tc0 + (ap < beta) + (aq < beta);
+        const int tc = chroma ? tc0 + 1 : tc0 + apb + aqb;
         const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
         const int avg = (p0 + q0 + 1) >> 1;
-        const int np1 = ap < beta ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 * 2)) >> 1) : p1;
-        const int nq1 = aq < beta ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 * 2)) >> 1) : q1;
+        const int np1 = apb ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 * 2)) >> 1) : p1;
+        const int nq1 = aqb ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 * 2)) >> 1) : q1;
         v[E - 1] = f ? clip3(0, maxv, p0 + dl) : p0;
         v[E] = f ? clip3(0, maxv, q0 - dl) : q0;
         v[E - 2] = f ? np1 : p1;
@@ -2716,7 +2703,7 @@ DEVI void h264_filt_reg(int (&v)[LEN], bool on, int bs, int alpha, int beta, int
     } else {
         const int p3 = v[E - 4], q3 = v[E + 3];
         const bool sm = abs(p0 - q0) < ((alpha >> 2) + 2);
-        const bool sp = ap < beta && sm, sq = aq < beta && sm;
+        const bool sp = apb && sm, sq = aqb && sm;
         const int np0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
         const int np1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
         const int np2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
@@ -2729,7 +2716,6 @@ DEVI void h264_filt_reg(int (&v)[LEN], bool on, int bs, int alpha, int beta, int
         v[E] = f ? nq0 : q0;
         v[E + 1] = f ? nq1 : q1;
         v[E + 2] = f ? nq2 : q2;
-    }
     }
 }
 
@@ -2944,54 +2930,53 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                     tb = TB.beta[ib] << sh;
                     tt = TB.tc0[ia] << sh;
                 }
-                // Each lane filters a whole line through all edges of a direction in registers
-                // (lanes 0-15: luma rows / columns, 32-47: chroma rows / columns), one LDS
-                // round trip per direction instead of one per edge.  Edge e of a direction: the MB
-                // edge (e = 0, bS 4, if filtered at all) or internal (bS 3; luma e = 1, 3 not in
-                // 8x8-transform MBs; chroma only e = 0, 2).
+                // Each lane filters a whole line through all edges of a direction in registers, one
+                // LDS round trip per direction: lanes 0-15 luma rows / columns, 16-23 Cb, 24-31 Cr
+                // lines, all in one instruction stream (h264_filt_line).  A chroma line sits at
+                // v[2..11] so its MB edge and its internal edge fall on the luma positions 4 and 8;
+                // the luma-only edges 12 and 16 are off for it.  Edge e of a direction: the MB edge
+                // (e = 0, bS 4, if filtered at all) or internal (bS 3; luma e = 1, 3 not in
+                // 8x8-transform MBs).
                 const bool t8 = (mf & 2) != 0;
-                const bool luma_lane = lane < 16, chroma_lane = lane >= 32 && lane < 48;
-                const int cc = (lane - 32) >> 3, ck = lane & 7;  // chroma lanes: component, line
-                const int maxy = (1 << bd) - 1, maxc = (1 << bdc) - 1;
+                const bool luma_lane = lane < 16, chroma = lane >= 16;
+                const int cc = (lane >> 3) & 1, ck = lane & 7;  // chroma lanes: component, line
+                const int maxv = chroma ? (1 << bdc) - 1 : (1 << bd) - 1;
                 for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
                     const bool vert = dir == 0;
                     // left neighbour = the previous MB of this row (carried), top neighbour loaded
                     const int nmf = vert ? (mx > 0 ? lmf : 0) : tmf;
                     bool mb_edge = (nmf & 4) != 0;
                     if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
-                    const int la0 = __builtin_amdgcn_readlane(ta, dir), lb0 = __builtin_amdgcn_readlane(tb, dir);
-                    const int la1 = __builtin_amdgcn_readlane(ta, 2), lb1 = __builtin_amdgcn_readlane(tb, 2);
-                    const int lt1 = __builtin_amdgcn_readlane(tt, 2);
-                    if (luma_lane) {
+                    // threshold sets: 3 * component + (dir for the MB edge, 2 for internal edges)
+                    const int am = __builtin_amdgcn_readlane(ta, dir), bm = __builtin_amdgcn_readlane(tb, dir);
+                    const int ai = __builtin_amdgcn_readlane(ta, 2), bi = __builtin_amdgcn_readlane(tb, 2);
+                    const int ti = __builtin_amdgcn_readlane(tt, 2);
+                    const int amb = __builtin_amdgcn_readlane(ta, 3 + dir), amr = __builtin_amdgcn_readlane(ta, 6 + dir);
+                    const int bmb = __builtin_amdgcn_readlane(tb, 3 + dir), bmr = __builtin_amdgcn_readlane(tb, 6 + dir);
+                    const int aib = __builtin_amdgcn_readlane(ta, 5), air = __builtin_amdgcn_readlane(ta, 8);
+                    const int bib = __builtin_amdgcn_readlane(tb, 5), bir = __builtin_amdgcn_readlane(tb, 8);
+                    const int tib = __builtin_amdgcn_readlane(tt, 5), tir = __builtin_amdgcn_readlane(tt, 8);
+                    const int aM = luma_lane ? am : (cc ? amr : amb), bM = luma_lane ? bm : (cc ? bmr : bmb);
+                    const int aI = luma_lane ? ai : (cc ? air : aib), bI = luma_lane ? bi : (cc ? bir : bib);
+                    const int tI = luma_lane ? ti : (cc ? tir : tib);
+                    if (lane < 32) {
+                        // element i of the line at base + i * stp (chroma: base two steps before
+                        // the window line, so its samples land at v[2..11]; the other v are
+                        // loaded from inside the wave's own window and never used)
+                        const int stp = vert ? 1 : (luma_lane ? 20 : 10);
+                        const uint16_t* base = luma_lane ? (vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4])
+                                                         : (vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2]) - 2 * stp;
                         int v[20];
-                        const int stp = vert ? 1 : 20;
-                        const uint16_t* src = vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4];
 #pragma unroll
-                        for (int i = 0; i < 20; i++) v[i] = src[i * stp];
-                        h264_filt_reg<4, false>(v, mb_edge, 4, la0, lb0, 0, maxy);
-                        h264_filt_reg<8, false>(v, !t8, 3, la1, lb1, lt1, maxy);
-                        h264_filt_reg<12, false>(v, true, 3, la1, lb1, lt1, maxy);
-                        h264_filt_reg<16, false>(v, !t8, 3, la1, lb1, lt1, maxy);
-                        uint16_t* dst = vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4];
+                        for (int i = 0; i < 20; i++) v[i] = base[i * stp];
+                        h264_filt_line<4>(v, mb_edge, 4, aM, bM, 0, maxv, chroma);
+                        h264_filt_line<8>(v, chroma || !t8, 3, aI, bI, tI, maxv, chroma);
+                        h264_filt_line<12>(v, luma_lane, 3, aI, bI, tI, maxv, chroma);
+                        h264_filt_line<16>(v, luma_lane && !t8, 3, aI, bI, tI, maxv, chroma);
+                        uint16_t* dst = const_cast<uint16_t*>(base);
 #pragma unroll
-                        for (int i = 1; i < 19; i++) dst[i * stp] = static_cast<uint16_t>(v[i]);
-                    } else if (chroma_lane) {
-                        // Cb sets 3..5, Cr sets 6..8: fetch both, select per lane
-                        const int a0 = __builtin_amdgcn_readlane(ta, 3 + dir), a3 = __builtin_amdgcn_readlane(ta, 6 + dir);
-                        const int b0 = __builtin_amdgcn_readlane(tb, 3 + dir), b3 = __builtin_amdgcn_readlane(tb, 6 + dir);
-                        const int a1 = __builtin_amdgcn_readlane(ta, 5), a4 = __builtin_amdgcn_readlane(ta, 8);
-                        const int b1 = __builtin_amdgcn_readlane(tb, 5), b4 = __builtin_amdgcn_readlane(tb, 8);
-                        const int t1 = __builtin_amdgcn_readlane(tt, 5), t4 = __builtin_amdgcn_readlane(tt, 8);
-                        int v[10];
-                        const int stp = vert ? 1 : 10;
-                        const uint16_t* src = vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2];
-#pragma unroll
-                        for (int i = 0; i < 10; i++) v[i] = src[i * stp];
-                        h264_filt_reg<2, true>(v, mb_edge, 4, cc ? a3 : a0, cc ? b3 : b0, 0, maxc);
-                        h264_filt_reg<6, true>(v, true, 3, cc ? a4 : a1, cc ? b4 : b1, cc ? t4 : t1, maxc);
-                        uint16_t* dst = vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2];
-#pragma unroll
-                        for (int i = 1; i < 7; i++) dst[i * stp] = static_cast<uint16_t>(v[i]);
+                        for (int i = 1; i < 19; i++)
+                            if (luma_lane || (i >= 3 && i <= 8)) dst[i * stp] = static_cast<uint16_t>(v[i]);
                     }
                     wave_sync();
                     PROF_LAPK(dir * 4);
