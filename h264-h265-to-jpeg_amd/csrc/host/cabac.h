@@ -18,8 +18,6 @@ extern const uint8_t kCabacRenorm[32];
 // next context state ((pStateIdx << 1) | valMps) after an MPS / LPS bin
 extern const uint16_t kCabacNextMps[128];
 extern const uint16_t kCabacNextLps[128];
-// the same, merged for branch-free decoding: [(state << 1) | bin_was_lps]
-extern const uint16_t kCabacNext[256];
 // rangeTabLps by (state, range >> 6): [(pStateIdx << 1) | valMps][8], columns 4..7 used
 extern const uint8_t kCabacLpsByState[128][8];
 
@@ -52,26 +50,11 @@ public:
         for (int i = 0; i < 4; i++) value_ = (value_ << 8) | (cur_ < end_ ? *cur_++ : 0u);
         bits_ = 32 - 9;
     }
+    // The MPS/LPS outcome as a mask, never a branch: context-coded bins are one dependency chain
+    // (range -> LPS range -> compare -> renormalisation), and a mispredicted branch per bin costs
+    // more than the selects (measured on the GPU box's host CPU, tools/gpu_parse_ab.sh: the
+    // branch form for skewed contexts was 2.5-6 % slower end to end).
     inline int decision(uint16_t& ctx) {
-        H2J_COUNT(g_bins_ctx, 1);
-        const unsigned st = ctx;
-        const uint32_t lps = kCabacLpsByState[st][range_ >> 6];
-        const uint32_t rmps = range_ - lps;
-        const uint64_t scaled = static_cast<uint64_t>(rmps) << bits_;
-        const bool is_lps = value_ >= scaled;
-        value_ -= is_lps ? scaled : 0;
-        const uint32_t r = is_lps ? lps : rmps;
-        ctx = is_lps ? kCabacNextLps[st] : kCabacNextMps[st];
-        const int sh = __builtin_clz(r) - 23;
-        range_ = r << sh;
-        bits_ -= sh;
-        if (bits_ < 0) refill();
-        return static_cast<int>(st & 1) ^ static_cast<int>(is_lps);
-    }
-    // The same with the MPS/LPS outcome as a mask, never a branch.  For contexts near 50 %
-    // (significance flags) a branch mispredicts on every other bin; for skewed contexts the
-    // predicted branch is faster (the next bin starts speculatively), so decision() keeps it.
-    inline int decision_bf(uint16_t& ctx) {
         H2J_COUNT(g_bins_ctx, 1);
         const unsigned st = ctx;
         const uint32_t lps = kCabacLpsByState[st][range_ >> 6];
@@ -81,7 +64,10 @@ public:
         const uint64_t m = 0 - static_cast<uint64_t>(is_lps);
         value_ -= scaled & m;
         const uint32_t r = rmps ^ ((rmps ^ lps) & static_cast<uint32_t>(m));
-        ctx = kCabacNext[(st << 1) | is_lps];
+        // next state from two loads that depend only on the state (issued early), then a select:
+        // a load indexed by the outcome would sit on the chain of a context used twice in a row
+        const uint16_t nm = kCabacNextMps[st], nl = kCabacNextLps[st];
+        ctx = is_lps ? nl : nm;
         const int sh = __builtin_clz(r) - 23;
         range_ = r << sh;
         bits_ -= sh;
@@ -109,6 +95,19 @@ public:
         value_ -= (static_cast<uint64_t>(q) * range_) << sh;
         bits_ = sh;
         return q;
+    }
+    // The next k (1..24) bypass bins without consuming them (MSB first) ...
+    inline uint32_t bypass_peek(int k) {
+        if (bits_ < k) refill();
+        return static_cast<uint32_t>((value_ >> (bits_ - k)) / range_);
+    }
+    // ... and consuming the first n of them, whose value (the top n bits of the peek) is top:
+    // the quotient's leading bits are the quotient of the truncated dividend
+    inline void bypass_skip(int n, uint32_t top) {
+        H2J_COUNT(g_bins_byp, n);
+        const int sh = bits_ - n;
+        value_ -= (static_cast<uint64_t>(top) * range_) << sh;
+        bits_ = sh;
     }
     inline uint32_t bypass_bits(int n) {
         if (n <= 2) {

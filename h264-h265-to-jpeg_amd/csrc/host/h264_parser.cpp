@@ -484,25 +484,25 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     bool last_found = false;
     if (cat == 5) {
         for (int i = 0; i < max_num - 1; i++)
-            if (cc.decision_bf(ctx[402 + kSig8x8[i]])) {
+            if (cc.decision(ctx[402 + kSig8x8[i]])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
-                if (cc.decision_bf(ctx[417 + kLast8x8[i]])) { last_found = true; break; }
+                if (cc.decision(ctx[417 + kLast8x8[i]])) { last_found = true; break; }
             }
     } else if (cat == 3) {
         for (int i = 0; i < max_num - 1; i++) {
             const int inc = i < 2 ? i : 2;
-            if (cc.decision_bf(ctx[105 + kSigOff[3] + inc])) {
+            if (cc.decision(ctx[105 + kSigOff[3] + inc])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
-                if (cc.decision_bf(ctx[166 + kSigOff[3] + inc])) { last_found = true; break; }
+                if (cc.decision(ctx[166 + kSigOff[3] + inc])) { last_found = true; break; }
             }
         }
     } else {
         uint16_t* const sctx = ctx + 105 + kSigOff[cat];
         uint16_t* const lctx = ctx + 166 + kSigOff[cat];
         for (int i = 0; i < max_num - 1; i++)
-            if (cc.decision_bf(sctx[i])) {
+            if (cc.decision(sctx[i])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
-                if (cc.decision_bf(lctx[i])) { last_found = true; break; }
+                if (cc.decision(lctx[i])) { last_found = true; break; }
             }
     }
     if (!last_found) pos[nsig++] = static_cast<uint8_t>(max_num - 1);

@@ -950,7 +950,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             const uint8_t* sig = sigtab[prevCsbf][(xs | ys) ? 1 : 0];
             // bins feed the mask arithmetically (no data-dependent branch per bin)
             unsigned got = 0;
-            for (int nn = nstart; nn > 0; nn--) got |= static_cast<unsigned>(cc.decision_bf(ctx[sig[nn]])) << nn;
+            for (int nn = nstart; nn > 0; nn--) got |= static_cast<unsigned>(cc.decision(ctx[sig[nn]])) << nn;
             sigmask |= got;
             infer_dc = infer_dc && got == 0;
             if (nstart >= 0) {
@@ -1003,14 +1003,31 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             int baseL = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0);
             int lvl = baseL;
             if (baseL == ((numSig < 8) ? ((nn == lastG1) ? 3 : 2) : 1)) {
-                int prefix = 0;
-                while (prefix < 32 && cc.bypass()) prefix++;
-                int rem;
-                if (prefix < 3) rem = (prefix << rice) + static_cast<int>(cc.bypass_bits(rice));
-                else {
-                    int pm3 = prefix - 3;
-                    if (pm3 + rice > 30) { err_ = -21; cc_ = cc; return; }
-                    rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc.bypass_bits(pm3 + rice));
+                // coeff_abs_level_remaining: unary prefix + suffix, usually both inside one
+                // 20-bin peek (one division instead of a bin loop with a mispredicted exit)
+                constexpr int kPeek = 20;
+                const uint32_t q = cc.bypass_peek(kPeek);
+                const uint32_t inv = ~q << (32 - kPeek);
+                int prefix = inv ? __builtin_clz(inv) : kPeek;
+                int rem = -1;
+                if (prefix < kPeek) {
+                    const int slen = prefix < 3 ? rice : prefix - 3 + rice, total = prefix + 1 + slen;
+                    if (total <= kPeek) {
+                        const uint32_t top = q >> (kPeek - total);
+                        cc.bypass_skip(total, top);
+                        const int suf = static_cast<int>(top & ((1u << slen) - 1u));
+                        rem = prefix < 3 ? (prefix << rice) + suf : (((1 << (prefix - 3)) + 2) << rice) + suf;
+                    }
+                }
+                if (rem < 0) {
+                    prefix = 0;
+                    while (prefix < 32 && cc.bypass()) prefix++;
+                    if (prefix < 3) rem = (prefix << rice) + static_cast<int>(cc.bypass_bits(rice));
+                    else {
+                        int pm3 = prefix - 3;
+                        if (pm3 + rice > 30) { err_ = -21; cc_ = cc; return; }
+                        rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc.bypass_bits(pm3 + rice));
+                    }
                 }
                 lvl = baseL + rem;
                 if (lvl > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
