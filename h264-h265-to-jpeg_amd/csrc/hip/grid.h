@@ -7,16 +7,27 @@
 // all XCDs and HBM channels at once, which is what a read-once stream wants; HEVC deblocking
 // was neutral.
 #pragma once
+#ifdef __HIP__
 #include <hip/hip_runtime.h>
+#define H2J_GRID_FN __host__ __device__ __forceinline__
+#else
+#define H2J_GRID_FN inline  // plain C++ (tests/test_grid_remap.py checks the mapping on the host)
+#endif
 
 // XCD-aware order (guide §5.5 T1).  The dispatcher deals consecutive workgroups of a launch
 // round-robin to the 8 XCDs, each with a private L2, so tiles that share halo rows / columns
 // or 128-B lines (a CTB and its neighbours, consecutive 8x8-block tiles) would each be fetched
 // once per XCD.  The linear workgroup id is remapped so that the workgroups one XCD receives
 // (orig % 8 labels them) cover one contiguous range of (picture, tile) ids.  Bijective for any
-// grid size (q = n / 8, r = n % 8); it changes only where a tile runs, never a result -- no
+// grid size n (q = n / 8, r = n % 8); it changes only where a tile runs, never a result -- no
 // kernel using it depends on dispatch order.  -DH2J_NO_XCD_REMAP restores the plain order
 // (A/B builds).
+H2J_GRID_FN unsigned xcd_remap(unsigned orig, unsigned n) {
+    const unsigned xcd = orig & 7u, q = n >> 3, r = n & 7u;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+#ifdef __HIP__
 struct GridPos {
     int x, y;
 };
@@ -24,10 +35,9 @@ __device__ __forceinline__ GridPos xcd_grid_pos() {
 #ifdef H2J_NO_XCD_REMAP
     return GridPos{static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y)};
 #else
-    const unsigned gx = gridDim.x, n = gx * gridDim.y;
-    const unsigned orig = blockIdx.y * gx + blockIdx.x;
-    const unsigned xcd = orig & 7u, q = n >> 3, r = n & 7u;
-    const unsigned id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    const unsigned gx = gridDim.x;
+    const unsigned id = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gridDim.y);
     return GridPos{static_cast<int>(id % gx), static_cast<int>(id / gx)};
 #endif
 }
+#endif
