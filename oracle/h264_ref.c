@@ -732,7 +732,7 @@ static void pred8x8(H4Dec *d, int b8, int mode, int *pred) {
     if (ad) C = px(d, 0, gx - 1, gy - 1);
     (void)T; (void)L; (void)p;
     /* 8.3.2.2.1 reference sample filtering */
-    int Tf[16], Lf[8], Cf = C;
+    int Tf[16] = {0}, Lf[8] = {0}, Cf = C;  /* read only when available (8.3.2.2) */
     if (at) {
         Tf[0] = ad ? (C + 2 * Tr[0] + Tr[1] + 2) >> 2 : (3 * Tr[0] + Tr[1] + 2) >> 2;
         for (int x = 1; x < 15; x++) Tf[x] = (Tr[x - 1] + 2 * Tr[x] + Tr[x + 1] + 2) >> 2;
