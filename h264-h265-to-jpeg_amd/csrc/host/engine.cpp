@@ -668,9 +668,17 @@ void Engine::parse_loop() {
         // batches smaller than the thread pool (a lone IDecoder call): pictures with several
         // independent slices / WPP rows / tiles parse them on several threads
         const int slice_threads = std::max(1, (pool->size() + 1) / std::max(1, b->n));
+        // inside each chunk the largest bitstreams start first (the threads then finish a chunk
+        // together instead of idling behind one large picture); chunks keep their order
+        std::vector<int> order(static_cast<size_t>(b->n));
+        for (int i = 0; i < b->n; i++) order[i] = i;
+        for (size_t c = 0; c + 1 < b->bounds.size(); c++)
+            std::stable_sort(order.begin() + b->bounds[c], order.begin() + b->bounds[c + 1],
+                             [&](int x, int y) { return b->sizes[x] > b->sizes[y]; });
         {
             std::lock_guard<std::mutex> g(pool_mu);
-            pool->parallel_for(b->n, [&](int i) {
+            pool->parallel_for(b->n, [&](int k) {
+                const int i = order[static_cast<size_t>(k)];
                 jobs[i].threads = slice_threads;
                 parse_any(b->data[i], b->sizes[i], jobs[i]);
                 if (b->left[b->chunk_of[i]].fetch_sub(1) == 1) {
