@@ -28,6 +28,7 @@
 // csrc/host/jpeg_writer.cpp.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdio>
 
 #include "h2j_gpu.h"
@@ -163,7 +164,11 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
     const int t = blockIdx.x;
     // the counts through LDS (one wide pass by every lane; a serial loop of global loads
     // would wait for each of them)
-    for (int i = threadIdx.x; i < 256; i += 64) s.hist[i] = js->hist[t][i];
+    for (int i = threadIdx.x; i < 256; i += 64) {
+        s.hist[i] = js->hist[t][i];
+        js->len[t][i] = 0;  // by every lane; lane 0 writes the used entries below (same wave:
+        js->code[t][i] = 0; // its later stores to these addresses land after these)
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;  // serial by construction (AV_QSORT tie order)
     int nval = 0;
@@ -185,7 +190,10 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
             x = s.pp[a]; s.pp[a] = s.pp[b]; s.pp[b] = x;
         },
         s.stk);
-    // package-merge, 16 levels + the final pairing round (i not reset)
+    // package-merge, 16 levels + the final pairing round (i not reset).  The next two leaf
+    // weights and the next two pair sums ride in registers (INT_MAX once a list is used up), so
+    // a step's leaf-or-pair decision compares registers and the loads it needs were issued a
+    // step earlier: one lane walking LDS waited a round trip per step before.
     int np = 0, cur = 0, i = 0;
     for (int lvl = 0; lvl <= 16; lvl++) {
         int* Pc = s.P[cur];
@@ -193,16 +201,23 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
         int j = 0, n = 0;
         uint64_t word = 0;  // leaf bits of the current 64 items
         if (lvl < 16) i = 0;
+        const int npv = np;
+        auto ldleaf = [&](int k) { return k < size ? s.pp[k] : INT_MAX; };
+        auto ldpair = [&](int k) { return k + 1 < npv ? Pp[k] + Pp[k + 1] : INT_MAX; };
+        int l0 = ldleaf(i), l1 = ldleaf(i + 1), q0 = ldpair(j), q1 = ldpair(j + 2);
         while (i < size || j + 1 < np) {
-            bool leaf;
-            if (i < size && (j + 1 >= np || s.pp[i] < Pp[j] + Pp[j + 1])) {
-                Pc[n] = s.pp[i];
+            // = i < size && (j + 1 >= np || pp[i] < Pp[j] + Pp[j + 1]): weights stay far below INT_MAX
+            const bool leaf = l0 < q0;
+            if (leaf) {
+                Pc[n] = l0;
                 i++;
-                leaf = true;
+                l0 = l1;
+                l1 = ldleaf(i + 1);
             } else {
-                Pc[n] = Pp[j] + Pp[j + 1];
+                Pc[n] = q0;
                 j += 2;
-                leaf = false;
+                q0 = q1;
+                q1 = ldpair(j + 2);
             }
             if (lvl < 16) {
                 word |= static_cast<uint64_t>(leaf) << (n & 63);
@@ -244,19 +259,21 @@ __global__ void __launch_bounds__(64) h2j_k5a_tables(const h2j_frame* frames, ui
             x = s.hl[a]; s.hl[a] = s.hl[b]; s.hl[b] = x;
         },
         s.stk);
-    for (int k = 0; k < 20; k++) js->bits[t][k] = 0;
-    for (int k = 0; k < 256; k++) {
-        js->len[t][k] = 0;
-        js->code[t][k] = 0;
-    }
+    // codes per length counted in registers / LDS, not by read-modify-writes of global memory
+    int bits[17];
+#pragma unroll
+    for (int l = 0; l <= 16; l++) bits[l] = 0;
     for (int k = 0; k < nval; k++) {
+        const int l = s.hl[k];
+#pragma unroll
+        for (int q = 1; q <= 16; q++) bits[q] += l == q ? 1 : 0;
         js->val[t][k] = static_cast<uint8_t>(s.hc[k]);
-        js->bits[t][s.hl[k]]++;
     }
+    for (int k = 0; k < 20; k++) js->bits[t][k] = k <= 16 ? static_cast<uint8_t>(bits[k]) : 0;
     js->nval[t] = static_cast<uint32_t>(nval);
     int c = 0, k = 0;
     for (int l = 1; l <= 16; l++) {
-        for (int q = 0; q < js->bits[t][l]; q++, k++) {
+        for (int q = 0; q < bits[l]; q++, k++) {
             js->code[t][s.hc[k]] = static_cast<uint16_t>(c++);
             js->len[t][s.hc[k]] = static_cast<uint8_t>(l);
         }
