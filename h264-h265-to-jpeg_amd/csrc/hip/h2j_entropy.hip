@@ -83,17 +83,24 @@ __global__ void __launch_bounds__(kTile) h2j_k4e_dc_hist(const h2j_frame* frames
 
 // ---------------------------------------------------------------- K5a
 struct HuffLds {
-    int pv[260], pp[260];     // leaves (symbol, count), sorted by AV_QSORT
-    int P[2][520];            // item probabilities of the previous / current list
     uint64_t leaf[16][9];     // bit m of level t: item m of list t is a leaf (cumulative counts
-                              // by popcount; 1 KB instead of a 16 KB count table: more
-                              // workgroups per CU for this latency-bound serial kernel)
+                              // by popcount; 1 KB instead of a 16 KB count table)
+    int pv[260], pp[260];     // leaves (symbol, count), sorted by AV_QSORT
+    union {                   // three phases that never overlap in time:
+        unsigned hist[256];   // the table's symbol counts, staged by all lanes (until the leaves
+                              // are collected)
+        int P[2][520];        // item probabilities of the previous / current package-merge list
+        struct {
+            int hc[256], hl[256];  // (symbol, length) pairs, once the code lengths are known
+        };
+    };
     int nlist[17];
     int nb[260];              // code length per symbol
-    int hc[256], hl[256];     // (symbol, length) pairs
     int stk[64][2];
-    unsigned hist[256];       // the table's symbol counts, staged by all lanes
 };
+// ~9 KB: the 16 tables a CU gets (4 per picture over 1024 pictures on 256 CUs) all fit its
+// 160 KB of LDS at once, so this latency-bound serial kernel runs them in one round
+static_assert(sizeof(HuffLds) <= 10 * 1024, "K5a LDS per table");
 
 // libavutil/qsort.h AV_QSORT on index range [0, num) (unstable: tie order
 // must be FFmpeg's own, so this is a literal restatement, run by one lane).
