@@ -456,7 +456,10 @@ struct BitSink {
 // 256 blocks): the blocks' shared boundary words meet in LDS atomics, and the tile goes out as
 // whole-word stores, only its first and last word by global atomics (shared with the
 // neighbouring tiles).  Larger tiles write straight to global memory as before.
-constexpr int kEmitWords = 8192;  // 32 KB
+// 8 KB: with the 3 KB code tables a 256-thread workgroup holds 11 KB, so 8 of them (the wave
+// limit) share a CU; a 32 KB image allowed 4, and the kernel waited on its symbol loads with half
+// the waves (hevc1080 per 1024 pictures 1.52 -> see DESIGN.md)
+constexpr int kEmitWords = 2048;
 
 template <bool kLds>
 DEVI void emit_block(uint32_t* out, uint32_t w0, uint32_t bit0, uint32_t bits, const CodeLds& cl, const uint32_t* sym,
