@@ -458,7 +458,7 @@ struct BitSink {
 // neighbouring tiles).  Larger tiles write straight to global memory as before.
 // 8 KB: with the 3 KB code tables a 256-thread workgroup holds 11 KB, so 8 of them (the wave
 // limit) share a CU; a 32 KB image allowed 4, and the kernel waited on its symbol loads with half
-// the waves (hevc1080 per 1024 pictures 1.52 -> see DESIGN.md)
+// the waves (per 1024 pictures: hevc1080 1.53 -> 0.94 ms, 4K Main10 2.0 -> 0.9 ms)
 constexpr int kEmitWords = 2048;
 
 template <bool kLds>
