@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -261,10 +262,20 @@ constexpr int kYWaves = 9, kCWaves = 7;
 constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
-struct K0Lds {
+struct K0Lds {  // H.264
     int blk[32 * 32];
-    int tmp[32 * 34];  // HEVC groups: int16 rows padded to N + 2 (bank-conflict-free transposition)
+    int tmp[32 * 34];
     int dc[16];
+};
+// HEVC: the column pass's output (int16 rows padded to N + 2, bank-conflict-free
+// transposition) overlays the dequantised coefficients it was computed from (every lane holds
+// its column's sums in registers across a wave barrier): 4.3 KB instead of 8.5 KB per wave, so
+// the VGPR limit (6 waves per SIMD at 79 VGPRs), not LDS (4.5), bounds the occupancy
+struct K0LdsHevc {
+    union {
+        int blk[32 * 32];
+        int tmp[32 * 34];
+    };
 };
 
 
@@ -351,7 +362,7 @@ struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
     uint32_t sl;
 };
 DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
-                        int16_t* R, int rst, K0Lds& s) {
+                        int16_t* R, int rst, K0LdsHevc& s) {
     const int lane = threadIdx.x;
     const int c = tu.c, log2n = tu.log2n, n = 1 << log2n, nn = n * n;
     const int bd = c ? f.bdc : f.bd;
@@ -401,7 +412,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
 // Transform-skip and bypass TBs are not batched (hevc_residual).
 template <int LOG2N>
 DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
-                              const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0Lds& s) {
+                              const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0LdsHevc& s) {
     constexpr int N = 1 << LOG2N, NN = N * N;
     constexpr int P = N + 2, NP = N * P;  // tmp row stride (int16): odd dword stride across lanes
     const int lane = threadIdx.x;
@@ -504,11 +515,14 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     const int* blk32 = reinterpret_cast<const int*>(blk);
     const int* tmp32 = reinterpret_cast<const int*>(tmp);
     const int qcol = 2 * k0_pslot<N>(q) + k0_phalf<N>(q);  // this lane's column in the paired tmp rows
-    if (act) {  // columns: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
+    {  // columns: tmp[y][x] = clip16((sum_j M[j][y] * d[j][x] + 64) >> 7)
         int acc[N];
-        pass(myy, [&](int ps) { return blk32[g * (NN / 2) + ps * N + q]; }, acc);
+        if (act) pass(myy, [&](int ps) { return blk32[g * (NN / 2) + ps * N + q]; }, acc);
+        wave_sync();  // tmp overlays blk (K0LdsHevc): every column has been read
+        if (act) {
 #pragma unroll
-        for (int i = 0; i < N; i++) tmp[g * NP + i * P + qcol] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
+            for (int i = 0; i < N; i++) tmp[g * NP + i * P + qcol] = static_cast<int16_t>(clip3(-32768, 32767, (acc[i] + 64) >> 7));
+        }
     }
     wave_sync();
     if (act) {  // rows: r[y][x] = (sum_j M[j][x] * tmp[y][j] + rnd) >> (20 - bitDepth)
@@ -913,7 +927,7 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                                                  uint8_t* arena) {
     const GridPos gp = xcd_grid_pos();
     constexpr int kTus = HEVC ? kK0TusHevc : kK0Tus;
-    __shared__ K0Lds s;
+    __shared__ typename std::conditional<HEVC, K0LdsHevc, K0Lds>::type s;
     const h2j_frame& fr = frames[gp.y];
     if ((ufl(fr.codec) == H2J_CODEC_HEVC) != HEVC) return;
     const uint32_t ntu = ufl(fr.ntu);
@@ -1104,10 +1118,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
             continue;
         }
         int16_t* R = res + offc;
-        if (hevc) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
+        if constexpr (HEVC) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
         else h264_residual(f, tu, CO, co0, sl, R, stc, s);
     }
-    if (!hevc) {  // H.264 luma 4x4 / 8x8 residuals, 16 / 8 same-size TBs per pass
+    if constexpr (!HEVC) {  // H.264 luma 4x4 / 8x8 residuals, 16 / 8 same-size TBs per pass
 #pragma unroll
         for (int l2 = 2; l2 <= 3; l2++) {
             uint64_t m = __ballot(grp264 && own.log2n == l2);
@@ -1147,7 +1161,7 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
             h264_i16_group(f, rec, gm, cnt, CO, sl, res, st0, s);
         }
     }
-    if (hevc) {  // HEVC residuals, 64 / N same-size TBs per pass
+    if constexpr (HEVC) {  // HEVC residuals, 64 / N same-size TBs per pass
         const bool batch = lane < nrec && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_TSKIP | H2J_TU_BYPASS));
 #pragma unroll
         for (int l2 = 2; l2 <= 5; l2++) {
