@@ -262,11 +262,11 @@ constexpr int kYWaves = 9, kCWaves = 7;
 constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
-struct K0Lds {  // H.264
-    int blk[32 * 32];
-    int tmp[32 * 34];
+struct K0Lds {    // H.264
+    int blk[32 * 32];  // up to 4 Intra16x16 MBs' levels ([G][16][16], h264_i16_group)
+    int tmp[512];      // row-pass output: at most 8 8x8 / 16 4x4 blocks ([G][N][N])
     int dc[16];
-};
+};                     // 6.2 KB: 5 waves per SIMD (the 95-VGPR limit) instead of 4.5 (LDS)
 // HEVC: the column pass's output (int16 rows padded to N + 2, bank-conflict-free
 // transposition) overlays the dequantised coefficients it was computed from (every lane holds
 // its column's sums in registers across a wave barrier): 4.3 KB instead of 8.5 KB per wave, so
