@@ -2635,9 +2635,8 @@ DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, 
 
 template <typename Pel>
 DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, uint8_t* arena,
-                         bool vert, int idx) {
-    const int x4 = idx % f.mw, y4 = idx / f.mw;
-    if (y4 >= f.mh) return;
+                         bool vert, int x4, int y4) {
+    const int idx = y4 * f.mw + x4;
     const uint8_t* fmap = arena + f.maps;
     const int8_t* qmap = reinterpret_cast<const int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
     const uint8_t fl = fmap[idx];
@@ -2661,13 +2660,28 @@ __global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* __restric
                                                      const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena,
                                                      int vert) {
     const h2j_frame& f = frames[blockIdx.y];
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= f.mw * f.mh) return;
     if (f.codec != H2J_CODEC_HEVC) return;
+    // threads only on the 8x8 edge grid of the pass: even 4x4 columns (vertical edges) or even
+    // 4x4 rows (horizontal edges) -- one thread per 4x4 block left half the lanes of every
+    // vertical-pass wave idle and half the horizontal-pass waves empty
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    int x4, y4;
+    if (vert) {
+        const int mw2 = (f.mw + 1) >> 1;
+        if (idx >= mw2 * f.mh) return;
+        y4 = idx / mw2;
+        x4 = (idx - y4 * mw2) * 2;
+    } else {
+        const int mh2 = (f.mh + 1) >> 1;
+        if (idx >= f.mw * mh2) return;
+        const int r = idx / f.mw;
+        x4 = idx - r * f.mw;
+        y4 = r * 2;
+    }
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) deblock_thread<uint8_t>(f, C, S, arena, vert != 0, idx);
-    else deblock_thread<uint16_t>(f, C, S, arena, vert != 0, idx);
+    if (f.bit_depth == 8) deblock_thread<uint8_t>(f, C, S, arena, vert != 0, x4, y4);
+    else deblock_thread<uint16_t>(f, C, S, arena, vert != 0, x4, y4);
 }
 
 
@@ -4085,12 +4099,12 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (b->has_hevc) {
-        const int maps = ((b->max_w + 3) >> 2) * ((b->max_h + 3) >> 2);
-        dim3 grid((maps + 255) / 256, b->nframes);
-        hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
+        const int mw = (b->max_w + 3) >> 2, mh = (b->max_h + 3) >> 2;  // 4x4 grid of the largest picture
+        const dim3 gv((((mw + 1) >> 1) * mh + 255) / 256, b->nframes), gh((mw * ((mh + 1) >> 1) + 255) / 256, b->nframes);
+        hipLaunchKernelGGL(h2j_k2_deblock, gv, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
         int r = check(hipGetLastError(), "h2j_k2_deblock(v)");
         if (r) return r;
-        hipLaunchKernelGGL(h2j_k2_deblock, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
+        hipLaunchKernelGGL(h2j_k2_deblock, gh, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 0);
         r = check(hipGetLastError(), "h2j_k2_deblock(h)");
         if (r) return r;
     }
