@@ -3861,6 +3861,9 @@ void* h2j_gpu_malloc(size_t bytes) {
     return p;
 }
 int h2j_gpu_free(void* p) { return check(hipFree(p), "hipFree"); }
+int h2j_gpu_mem_info(size_t* free_bytes, size_t* total_bytes) {
+    return check(hipMemGetInfo(free_bytes, total_bytes), "hipMemGetInfo");
+}
 void* h2j_gpu_host_alloc(size_t bytes) {
     void* p = nullptr;
     if (check(hipHostMalloc(&p, bytes, hipHostMallocDefault), "hipHostMalloc")) return nullptr;

@@ -20,10 +20,15 @@ extern const uint16_t kCabacNextMps[128];
 extern const uint16_t kCabacNextLps[128];
 // rangeTabLps by (state, range >> 6): [(pStateIdx << 1) | valMps][8], columns 4..7 used
 extern const uint8_t kCabacLpsByState[128][8];
+// A context variable as one 64-bit word: bits 0-31 hold rangeTabLps[pStateIdx][0..3] (one byte per
+// range quarter, (range >> 6) & 3), bits 32-38 the state (pStateIdx << 1) | valMps.  The LPS range
+// of a bin is then a shift of a register by the range, not a table load after it.
+typedef uint64_t CabacState;
+// word of each state, and the word after an MPS / LPS bin
+extern const uint64_t (&kCabacWord)[128];
+extern const uint64_t (&kCabacNextMpsW)[128];
+extern const uint64_t (&kCabacNextLpsW)[128];
 
-struct CabacCtx {
-    uint8_t state;  // (pStateIdx << 1) | valMps
-};
 
 inline uint8_t cabac_init_state(int m, int n, int qp) {
     if (qp < 0) qp = 0;
@@ -35,6 +40,7 @@ inline uint8_t cabac_init_state(int m, int n, int qp) {
     int st = mps ? pre - 64 : 63 - pre;
     return static_cast<uint8_t>((st << 1) | mps);
 }
+inline CabacState cabac_init_word(int m, int n, int qp) { return kCabacWord[cabac_init_state(m, n, qp)]; }
 
 // Branch-free on the MPS/LPS decision: the offset lives at the top of a
 // 64-bit window (value = offset << bits | look-ahead), renormalisation is a
@@ -50,27 +56,45 @@ public:
         for (int i = 0; i < 4; i++) value_ = (value_ << 8) | (cur_ < end_ ? *cur_++ : 0u);
         bits_ = 32 - 9;
     }
-    // The MPS/LPS outcome as a mask, never a branch: context-coded bins are one dependency chain
-    // (range -> LPS range -> compare -> renormalisation), and a mispredicted branch per bin costs
-    // more than the selects (measured on the GPU box's host CPU, tools/gpu_parse_ab.sh: the
-    // branch form for skewed contexts was 2.5-6 % slower end to end).
-    inline int decision(uint16_t& ctx) {
+    // The MPS/LPS outcome as conditional moves, never a branch: context-coded bins are one dependency
+    // chain, and a mispredicted branch per bin costs more than the selects (measured on the GPU
+    // box's host CPU, tools/gpu_parse_ab.sh: the branch form for skewed contexts was 2.5-6 % slower
+    // end to end).  Both outcomes' renormalised ranges are ready when the compare resolves (rLPS
+    // shifted by its leading zeros; rMPS = range - rLPS >= 128 shifted by 0 or 1), so the chain
+    // per bin is range -> byte shift of the context word -> subtract -> scale -> compare -> cmov.
+    inline int decision(CabacState& ctx) {
         H2J_COUNT(g_bins_ctx, 1);
-        const unsigned st = ctx;
-        const uint32_t lps = kCabacLpsByState[st][range_ >> 6];
+        const uint64_t w = ctx;
+        const unsigned st = static_cast<unsigned>(w >> 32);
+        const uint32_t lps = static_cast<uint32_t>(w >> ((range_ >> 3) & 24)) & 0xffu;
         const uint32_t rmps = range_ - lps;
         const uint64_t scaled = static_cast<uint64_t>(rmps) << bits_;
-        const uint32_t is_lps = value_ >= scaled ? 1u : 0u;
-        const uint64_t m = 0 - static_cast<uint64_t>(is_lps);
-        value_ -= scaled & m;
-        const uint32_t r = rmps ^ ((rmps ^ lps) & static_cast<uint32_t>(m));
-        // next state from two loads that depend only on the state (issued early), then a select:
-        // a load indexed by the outcome would sit on the chain of a context used twice in a row
-        const uint16_t nm = kCabacNextMps[st], nl = kCabacNextLps[st];
-        ctx = is_lps ? nl : nm;
-        const int sh = __builtin_clz(r) - 23;
-        range_ = r << sh;
-        bits_ -= sh;
+        const uint32_t msh = (rmps >> 8) ^ 1u;
+        uint32_t r = rmps << msh, sh = msh;
+        const uint32_t lsh = static_cast<uint32_t>(__builtin_clz(lps)) - 23u;
+        const uint32_t lr = lps << lsh;
+        // next state words from two loads that depend only on the state (issued early), then a
+        // select: a load indexed by the outcome would sit on the chain of a context used twice
+        uint64_t nx = kCabacNextMpsW[st];
+        const uint64_t nl = kCabacNextLpsW[st];
+        uint64_t v = value_;
+        const uint64_t vl = value_ - scaled;
+        uint32_t is_lps = 0;
+        // one compare, then conditional moves (the compiler turns a C select of these into a
+        // branch, mispredicted on every LPS bin)
+        __asm__("cmpq %[sc], %[v]\n\t"
+                "cmovaeq %[vl], %[v]\n\t"
+                "cmovael %[lr], %[r]\n\t"
+                "cmovael %[ls], %[sh]\n\t"
+                "cmovaeq %[nl], %[nx]\n\t"
+                "setae %b[il]"
+                : [v] "+r"(v), [r] "+r"(r), [sh] "+r"(sh), [nx] "+r"(nx), [il] "+q"(is_lps)
+                : [sc] "r"(scaled), [vl] "r"(vl), [lr] "r"(lr), [ls] "r"(lsh), [nl] "r"(nl)
+                : "cc");
+        value_ = v;
+        range_ = r;
+        bits_ -= static_cast<int>(sh);
+        ctx = nx;
         if (bits_ < 0) refill();
         return static_cast<int>((st & 1) ^ is_lps);
     }

@@ -218,6 +218,11 @@ constexpr int kK1BandRows = 68;
 // upper bound of one block's entropy-coded size (code lengths <= 16, values <= 16 bits)
 constexpr size_t kSegBytesPerBlock = 272;
 
+struct ChunkTime {
+    int frames = 0;
+    double k1_ms = 0, kernels_ms = 0;  // K1 launch; K0..K5 (HIP events on the chunk's stream)
+};
+
 // A submitted batch (h2j_engine_submit; h2j_engine_transcode is submit + wait).
 struct Batch {
     int64_t ticket = 0;
@@ -236,6 +241,12 @@ struct Batch {
     bool parsed = false, done = false;
     int rc = 0;
     double t0 = 0, t_parsed = 0;
+    // results handed to the caller by h2j_engine_wait (per ticket: a later batch that finishes
+    // before this one is waited for does not overwrite them)
+    double stats[ST_N] = {0};
+    std::vector<ChunkTime> chunk_log;
+    std::vector<std::string> msg;  // parse messages of the failed pictures
+    std::string err;
 };
 
 struct Engine {
@@ -258,18 +269,18 @@ struct Engine {
     bool stop = false;
     std::thread parser, driver;
     std::mutex pool_mu;  // held by whoever runs a parallel_for on the pool
+    // results of the last batch a caller waited for (h2j_engine_wait copies them under amu; they
+    // stay valid until the next wait returns)
     double last_stats[ST_N] = {0};
-    std::vector<int> working_status;
-    std::vector<int> last_status;          // per-picture status of the last finished batch
+    std::vector<int> last_status;          // per-picture status
     std::vector<std::string> last_msg;     // ... and the parse messages of its failed pictures
-    struct ChunkTime {
-        int frames = 0;
-        double k1_ms = 0, kernels_ms = 0;  // K1 launch; K0..K5 (HIP events on the chunk's stream)
-    };
-    std::vector<ChunkTime> chunk_log;       // chunks of the batch being driven
-    std::vector<ChunkTime> last_chunk_log;  // chunks of the last finished batch (h2j_engine_chunk_times)
+    std::vector<ChunkTime> last_chunk_log;  // its chunks (h2j_engine_chunk_times)
+    std::vector<ChunkTime> chunk_log;       // chunks of the batch being driven (driver thread)
+    std::string derr;                       // error of the batch being driven (driver thread)
     Slot slot[2];
     double stats[ST_N] = {0};  // working stats of the batch being driven
+    double slot_hbm_budget = 64e9;  // per slot; shared with the other engines on the device
+    bool strict_reference = false;  // H2J_STRICT_REFERENCE=1: fail where the reference returns false
 
     ~Engine() {
         {
@@ -304,8 +315,10 @@ struct Engine {
         acv.wait(lk, [&] { return active == 0; });
     }
 
+    // the driver thread reports into the batch it drives (a caller may be reading `err`)
     int fail(const std::string& m) {
-        err = m;
+        if (driver.joinable() && std::this_thread::get_id() == driver.get_id()) derr = m;
+        else err = m;
         return -1;
     }
     // an enqueue that fails after its first async operation: wait for what was queued on the
@@ -636,7 +649,7 @@ std::vector<int> chunk_plan_throughput(int n) {
 
 // GPU sub-chunks of a parsed range are bounded by an HBM estimate per slot (pictures, residual,
 // JPEG symbol tiles, payload pool: ~20 B per luma sample at 8 bits) and by 1024 pictures.
-constexpr double kSlotHbmBudget = 64e9;
+constexpr double kSlotHbmBudget = 64e9;  // at most, per slot (two slots per engine)
 constexpr int kMaxGpuChunk = 1024;
 static double hbm_estimate(const FrameJob& j) {
     const double px = static_cast<double>(j.hdr.width) * j.hdr.height;
@@ -705,19 +718,20 @@ void Engine::drive_loop() {
             b = gpu_q.front();
             gpu_q.pop_front();
         }
+        derr.clear();
         const int rc = run_batch(*b);
         std::unique_lock<std::mutex> lk(amu);
         acv.wait(lk, [&] { return b->parsed; });  // a failed batch may still be parsing
         std::vector<FrameJob>* jobs = b->jobset >= 0 ? &jobsets[b->jobset] : nullptr;
         stats[ST_PARSE] = b->t_parsed > 0 ? b->t_parsed - b->t0 : 0;
         stats[ST_TOTAL] = now_ms() - b->t0;
-        std::memcpy(last_stats, stats, sizeof(stats));
-        last_chunk_log = chunk_log;
-        last_status.assign(b->status, b->status + b->n);
-        last_msg.assign(static_cast<size_t>(b->n), std::string());
+        std::memcpy(b->stats, stats, sizeof(stats));
+        b->chunk_log = chunk_log;
+        b->err = derr;
+        b->msg.assign(static_cast<size_t>(b->n), std::string());
         if (jobs)
             for (int i = 0; i < b->n; i++)
-                if (b->status[i] != 0 && (*jobs)[i].error != 0) last_msg[i] = (*jobs)[i].message;
+                if (b->status[i] != 0 && (*jobs)[i].error != 0) b->msg[i] = (*jobs)[i].message;
         if (b->jobset >= 0) jobset_busy[b->jobset] = false;
         b->rc = rc;
         b->done = true;
@@ -799,7 +813,8 @@ int Engine::run_batch(Batch& b) {
         // leave small, latency-bound launches behind)
         double total = 0;
         for (int k = i; k < end; k++) total += hbm_estimate(jobs[k]);
-        const int parts = std::max(static_cast<int>(std::ceil(total / kSlotHbmBudget)),
+        const double budget = slot_hbm_budget;
+        const int parts = std::max(static_cast<int>(std::ceil(total / budget)),
                                    (end - i + kMaxGpuChunk - 1) / kMaxGpuChunk);
         const double share = total / std::max(1, parts);
         while (i < end && !fail) {
@@ -807,7 +822,7 @@ int Engine::run_batch(Batch& b) {
             double est = 0;
             while (j < end && j - i < kMaxGpuChunk) {
                 const double cst = hbm_estimate(jobs[j]);
-                if (j > i && (est + cst > kSlotHbmBudget || est + cst / 2 > share)) break;
+                if (j > i && (est + cst > budget || est + cst / 2 > share)) break;
                 est += cst;
                 j++;
             }
@@ -816,6 +831,13 @@ int Engine::run_batch(Batch& b) {
             s.live.clear();
             s.jobs = &jobs;
             for (int k = i; k < j; k++) {
+                if (strict_reference && jobs[k].error == 0 && jobs[k].reorder_delay) {
+                    // the reference sends one packet and never flushes: avcodec_receive_frame gives
+                    // EAGAIN for a stream with output reordering and H265ToJpeg returns false
+                    // (/root/reference/src/Decoder.cpp:324, 342-360)
+                    jobs[k].error = -7;
+                    jobs[k].message = "decoder delay: no picture before a flush (H2J_STRICT_REFERENCE)";
+                }
                 status[k] = jobs[k].error;
                 if (jobs[k].error == 0) s.live.push_back(k);
             }
@@ -835,7 +857,7 @@ int Engine::run_batch(Batch& b) {
             if (s.pending) sync(s);
         return -2;
     }
-    if (rc) err = "output buffer too small or payload pool overflow";
+    if (rc) derr = "output buffer too small or payload pool overflow";
     return rc;
 }
 
@@ -877,6 +899,17 @@ h2j_engine* h2j_engine_create(int device, int host_threads) {
     e.plan = h2j::plan_host(device, nodes, h2j::process_cpus(), h2j::node_cpus(node), h2j::cgroup_cpu_quota(),
                             host_threads > 0 ? host_threads : 0, host_threads < 0 ? -host_threads : 1);
     e.pool = new h2j::ThreadPool(e.plan.threads - 1, e.plan.cpus);
+    // HBM per slot: 64 GB at most, and the device's memory split between the two slots of every
+    // engine of this process on the device (host_threads = -k: k engines dealt over the devices)
+    const int k = host_threads < 0 ? -host_threads : 1;
+    const int per_dev = std::max(1, k / std::max(1, ndev) + (device < k % std::max(1, ndev) ? 1 : 0));
+    size_t free_b = 0, total_b = 0;
+    double budget = h2j::kSlotHbmBudget;
+    if (h2j_gpu_mem_info(&free_b, &total_b) == 0 && total_b > 0)
+        budget = std::min(budget, 0.8 * static_cast<double>(total_b) / (2.0 * per_dev));
+    e.slot_hbm_budget = budget;
+    const char* strict = std::getenv("H2J_STRICT_REFERENCE");
+    e.strict_reference = strict && strict[0] == '1';
     return w;
 }
 
@@ -938,6 +971,11 @@ int h2j_engine_wait(h2j_engine* w, int64_t ticket) {
     h2j::Batch* b = it->get();
     e.acv.wait(lk, [&] { return b->done; });
     const int rc = b->rc;
+    std::memcpy(e.last_stats, b->stats, sizeof(b->stats));
+    e.last_chunk_log.swap(b->chunk_log);
+    e.last_status.assign(b->status, b->status + b->n);
+    e.last_msg.swap(b->msg);
+    if (rc) e.err = b->err;
     e.batches.erase(it);
     return rc;
 }
@@ -1030,7 +1068,9 @@ int h2j_engine_host_info(h2j_engine* w, int* out, int n) {
 }
 
 const char* h2j_engine_frame_error(h2j_engine* w, int i) {
-    if (!w || i < 0 || i >= static_cast<int>(w->e.last_status.size())) return "";
+    if (!w) return "";
+    std::lock_guard<std::mutex> g(w->e.amu);
+    if (i < 0 || i >= static_cast<int>(w->e.last_status.size())) return "";
     switch (w->e.last_status[i]) {
     case 0: return "";
     case -50: return "output buffer too small";

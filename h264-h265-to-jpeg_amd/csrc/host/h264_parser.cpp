@@ -111,10 +111,58 @@ struct Sps {
     int log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4, delta_pic_order_always_zero = 0;
     int mb_w = 0, mb_h = 0;
     int crop_l = 0, crop_r = 0, crop_t = 0, crop_b = 0;
+    int num_reorder_frames = 0;  // VUI bitstream_restriction (0 when absent)
     bool scaling_present = false;
     uint8_t sl4[6][16];
     uint8_t sl8[6][64];
 };
+
+// E.1.2 hrd_parameters (skipped)
+bool skip_hrd(BitReader& b) {
+    const uint32_t cnt = b.ue();
+    if (cnt > 31) return false;
+    b.u(8);  // bit_rate_scale, cpb_size_scale
+    for (uint32_t i = 0; i <= cnt; i++) {
+        b.ue();
+        b.ue();
+        b.u(1);
+    }
+    b.u(20);  // initial_cpb_removal_delay_length .. time_offset_length (4 x 5 bits)
+    return true;
+}
+
+// E.1.1 vui_parameters, read as far as max_num_reorder_frames: FFmpeg (h264_slice.c) takes the
+// output delay from it when bitstream_restriction_flag is set.  Returns the reorder depth, 0 when
+// the VUI carries none or is truncated (FFmpeg then keeps no delay either).
+int parse_vui_reorder(BitReader& b) {
+    if (b.u(1) && b.u(8) == 255) b.u(32);  // aspect_ratio_idc, Extended_SAR
+    if (b.u(1)) b.u(1);                    // overscan
+    if (b.u(1)) {                          // video_signal_type
+        b.u(4);
+        if (b.u(1)) b.u(24);
+    }
+    if (b.u(1)) {  // chroma_loc_info
+        b.ue();
+        b.ue();
+    }
+    if (b.u(1)) b.u(32), b.u(32), b.u(1);  // timing_info
+    const bool nal = b.u(1) != 0;
+    if (nal && !skip_hrd(b)) return 0;
+    const bool vcl = b.u(1) != 0;
+    if (vcl && !skip_hrd(b)) return 0;
+    if (nal || vcl) b.u(1);  // low_delay_hrd_flag
+    b.u(1);                  // pic_struct_present_flag
+    if (!b.u(1)) return 0;   // bitstream_restriction_flag
+    b.u(1);
+    b.ue();
+    b.ue();
+    b.ue();
+    b.ue();
+    const uint32_t reorder = b.ue();
+    b.ue();  // max_dec_frame_buffering
+    if (b.overrun()) return 0;
+    return reorder > 16 ? 16 : static_cast<int>(reorder);
+}
 
 struct Pps {
     bool valid = false;
@@ -214,18 +262,23 @@ int parse_sps(BitReader& b, Sps* tab) {
     if (!b.u(1)) return -3;  // interlaced
     b.u(1);
     if (b.u(1)) {
-        // frame cropping in 2-sample units (4:2:0, frame_mbs_only); like FFmpeg, offsets that
-        // leave no picture are ignored (whole coded picture), not an error
+        // frame cropping in 2-sample units (4:2:0, frame_mbs_only).  FFmpeg 4.3 h264_ps.c
+        // (libavcodec 58.x, the reference's decoder) rejects the SPS ("crop values invalid",
+        // goto fail) when an offset exceeds INT_MAX / 4 / step or the window leaves no
+        // picture, so no frame is decoded; only its HEVC SPS parser ignores such a window.
         const uint32_t cl = b.ue(), cr = b.ue(), ct = b.ue(), cb = b.ue();
         const uint64_t w = static_cast<uint64_t>(s.mb_w) * 16, h = static_cast<uint64_t>(s.mb_h) * 16;
-        if ((static_cast<uint64_t>(cl) + cr) * 2 < w && (static_cast<uint64_t>(ct) + cb) * 2 < h) {
-            s.crop_l = static_cast<int>(cl) * 2;
-            s.crop_r = static_cast<int>(cr) * 2;
-            s.crop_t = static_cast<int>(ct) * 2;
-            s.crop_b = static_cast<int>(cb) * 2;
-        }
+        const uint32_t lim = 0x7fffffffu / 4 / 2;
+        if (cl > lim || cr > lim || ct > lim || cb > lim || (static_cast<uint64_t>(cl) + cr) * 2 >= w ||
+            (static_cast<uint64_t>(ct) + cb) * 2 >= h)
+            return -6;
+        s.crop_l = static_cast<int>(cl) * 2;
+        s.crop_r = static_cast<int>(cr) * 2;
+        s.crop_t = static_cast<int>(ct) * 2;
+        s.crop_b = static_cast<int>(cb) * 2;
     }
     if (b.overrun()) return -1;
+    if (b.u(1)) s.num_reorder_frames = parse_vui_reorder(b);
     if (s.chroma_format_idc != 1 || s.bit_depth > 10 || s.bit_depth_c != s.bit_depth) return -4;
     s.valid = true;
     return 0;
@@ -422,7 +475,7 @@ private:
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
-    uint16_t ctx_[460];  // 16-bit: stores must not alias the engine state
+    CabacState ctx_[460];
     int err_ = 0;
 
     VlcBits vb_;  // CAVLC slice data
@@ -475,7 +528,7 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     static const int kSigOff[6] = {0, 15, 29, 44, 47, 0};
     static const int kAbsOff[6] = {0, 10, 20, 30, 39, 0};
     Cabac cc = cc_;  // engine state in registers for the block
-    uint16_t* const ctx = ctx_;
+    CabacState* const ctx = ctx_;
     if (cat != 5 && !cc.decision(ctx[85 + kCbfOff[cat] + cbf_inc])) {
         cc_ = cc;
         return 0;
@@ -497,8 +550,8 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
             }
         }
     } else {
-        uint16_t* const sctx = ctx + 105 + kSigOff[cat];
-        uint16_t* const lctx = ctx + 166 + kSigOff[cat];
+        CabacState* const sctx = ctx + 105 + kSigOff[cat];
+        CabacState* const lctx = ctx + 166 + kSigOff[cat];
         for (int i = 0; i < max_num - 1; i++)
             if (cc.decision(sctx[i])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
@@ -507,7 +560,7 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     }
     if (!last_found) pos[nsig++] = static_cast<uint8_t>(max_num - 1);
     int eq1 = 0, gt1 = 0;
-    uint16_t* const absc = ctx + (cat == 5 ? 426 : 227 + kAbsOff[cat]);
+    CabacState* const absc = ctx + (cat == 5 ? 426 : 227 + kAbsOff[cat]);
     const int gt_cap = 4 - (cat == 3 ? 1 : 0);
     for (int k = nsig - 1; k >= 0; k--) {
         const int inc = gt1 ? 0 : std::min(4, 1 + eq1);
@@ -516,7 +569,7 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
             v = 1;
             eq1++;
         } else {
-            uint16_t& c2 = absc[5 + std::min(gt_cap, gt1)];
+            CabacState& c2 = absc[5 + std::min(gt_cap, gt1)];
             int p = 1;
             while (p < 14 && cc.decision(c2)) p++;
             v = p + 1;
@@ -1099,7 +1152,11 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h) ? static_cast<int>(first_mb_u) : -1;
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
-            if (first_mb < 0) {  // FFmpeg h264_slice.c: "first_mb_in_slice overflow"
+            // FFmpeg h264_slice.c: "first_mb_in_slice overflow" drops the slice; once a slice of
+            // picture 0 is collected the picture is still output, so stop there as at a
+            // picture boundary, and fail only when nothing of picture 0 was accepted
+            if (have && first_mb < 0) break;
+            if (first_mb < 0) {
                 job_->message = "first_mb_in_slice outside the picture";
                 return -6;
             }
@@ -1146,6 +1203,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             srec.slice_addr_rs = first_mb;
             if (!have) {
                 s_ = &s;
+                job_->reorder_delay = s.num_reorder_frames > 0;
                 mbw_ = s.mb_w;
                 mbh_ = s.mb_h;
                 qpbd_ = 6 * (s.bit_depth - 8);
@@ -1275,7 +1333,7 @@ int H264Parser::decode_slice(const SliceWork& w) {
     if (w.cabac) {
         end_ = w.data.data() + w.nbytes;
         cc_.init(w.data.data(), end_);
-        for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_state(kInitI[i][0], kInitI[i][1], qp_);
+        for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_word(kInitI[i][0], kInitI[i][1], qp_);
         for (;;) {
             if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
             mbx_ = addr % mbw_;

@@ -51,6 +51,7 @@ struct Sps {
     int chroma_format_idc = 0, width = 0, height = 0;
     int conf_l = 0, conf_r = 0, conf_t = 0, conf_b = 0;
     int bit_depth = 8, bit_depth_c = 8, log2_max_poc_lsb = 4;
+    int num_reorder_pics = 0;  // sps_max_num_reorder_pics[sps_max_sub_layers_minus1]
     int log2_min_cb = 3, log2_ctb = 4, log2_min_tb = 2, log2_max_tb = 5, max_th_depth_intra = 0;
     int scaling_list_enabled = 0;
     uint8_t sl[4][6][64];
@@ -207,7 +208,12 @@ int parse_sps(BitReader& b, Sps* tab) {
     s.bit_depth_c = static_cast<int>(bdc) + 8;
     s.log2_max_poc_lsb = static_cast<int>(lpl) + 4;
     int sub = static_cast<int>(b.u(1));
-    for (int i = sub ? 0 : msl; i <= msl; i++) { b.ue(); b.ue(); b.ue(); }
+    for (int i = sub ? 0 : msl; i <= msl; i++) {
+        b.ue();
+        const uint32_t reorder = b.ue();
+        b.ue();
+        if (i == msl) s.num_reorder_pics = reorder > 16 ? 16 : static_cast<int>(reorder);
+    }
     const uint32_t mcb = b.ue(), dcb = b.ue(), mtb = b.ue(), dtb = b.ue();
     if (mcb > 3 || dcb > 3 || mtb > 3 || dtb > 3) return -3;
     s.log2_min_cb = static_cast<int>(mcb) + 3;
@@ -479,7 +485,7 @@ private:
     int cur_idx_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
-    uint16_t ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];  // 16-bit: stores must not alias the engine state
+    CabacState ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];
     bool have_ds_ = false;
     int qp_y_ = 0, qg_pred_ = 0, qpd_val_ = 0, last_cu_qp_ = 0;
     bool is_qpd_coded_ = false, first_qg_ = true;
@@ -501,7 +507,7 @@ private:
     void init_contexts(int qp) {
         for (int i = 0; i < NUM_CTX; i++) {
             int iv = kInitI[i];
-            ctx_[i] = cabac_init_state((iv >> 4) * 5 - 45, ((iv & 15) << 3) - 16, qp);
+            ctx_[i] = cabac_init_word((iv >> 4) * 5 - 45, ((iv & 15) << 3) - 16, qp);
         }
     }
     bool same_region(int xc, int yc, int xn, int yn) const {
@@ -880,7 +886,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     // hot path: engine state in a local (registers), contexts by pointer,
     // coefficients into a local buffer appended once per TU
     Cabac cc = cc_;
-    uint16_t* const ctx = ctx_;
+    CabacState* const ctx = ctx_;
     const int n = 1 << log2n;
     if (p_->transform_skip && !cu_bypass_ && log2n <= 2 && cc.decision(ctx[C_TSKIP + (c ? 1 : 0)]))
         tu.flags |= H2J_TU_TSKIP;
@@ -925,7 +931,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     uint32_t out[32 * 32];
     int nout = 0;
     const uint8_t(*const sigtab)[2][16] = g_sigctx[c ? 1 : 0][lsb][scanIdx];
-    uint16_t* const gt1ctx = ctx + C_GT1 + (c ? 16 : 0);
+    CabacState* const gt1ctx = ctx + C_GT1 + (c ? 16 : 0);
     for (int i = lastSub; i >= 0; i--) {
         const int xs = sc[lsb][i][0], ys = sc[lsb][i][1];
         bool infer_dc = false;
@@ -969,7 +975,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         unsigned g1mask = 0;
         int numG1 = 0, lastG1 = -1;
         const int lastSig = 31 - __builtin_clz(sigmask), firstSig = __builtin_ctz(sigmask);
-        uint16_t* const g1c = gt1ctx + ctxSet * 4;
+        CabacState* const g1c = gt1ctx + ctxSet * 4;
         for (unsigned m = sigmask; m && numG1 < 8; numG1++) {
             const int nn = 31 - __builtin_clz(m);
             m &= ~(1u << nn);
@@ -1395,7 +1401,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
 // split-flag, availability and SAO-merge neighbours lie at most one CTB up and to the right).
 struct HevcParser::WppRows {
     std::unique_ptr<std::atomic<int>[]> done;      // per row: CTBs finished
-    std::vector<std::array<uint16_t, NUM_CTX>> ctx;  // per row: contexts after its 2nd CTB
+    std::vector<std::array<CabacState, NUM_CTX>> ctx;  // per row: contexts after its 2nd CTB
     std::atomic<bool> failed{false};
 };
 
@@ -1587,6 +1593,7 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
                 p_ = &pps_[sh.pps_id];
                 s_ = &sps_[p_->sps_id];
                 if (!setup_picture()) { job_->message = "invalid tile grid"; return -6; }
+                job_->reorder_delay = s_->num_reorder_pics > 0;
                 have_pic = true;
             }
             p_ = &pps_[sh.pps_id];

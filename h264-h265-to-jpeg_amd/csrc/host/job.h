@@ -18,6 +18,10 @@ struct FrameJob {
     int error = 0;            // 0 ok, <0 parse error
     std::string message;
     int threads = 1;          // threads the parser may use inside this picture (independent slices)
+    // the SPS signals output reordering (H.264 VUI max_num_reorder_frames > 0, H.265
+    // sps_max_num_reorder_pics[HighestTid] > 0): FFmpeg holds the picture back until more
+    // pictures or a flush arrive (only H2J_STRICT_REFERENCE acts on it)
+    bool reorder_delay = false;
 
     void clear() {
         hdr = h2j_frame{};
@@ -28,6 +32,7 @@ struct FrameJob {
         sl.clear();
         error = 0;
         message.clear();
+        reorder_delay = false;
     }
 };
 

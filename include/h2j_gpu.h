@@ -36,6 +36,7 @@ int h2j_gpu_set_device(int device);
 int h2j_gpu_pci_bus_id(int device, char *buf, int len);
 void *h2j_gpu_malloc(size_t bytes);
 int h2j_gpu_free(void *p);
+int h2j_gpu_mem_info(size_t *free_bytes, size_t *total_bytes); /* current device */
 void *h2j_gpu_host_alloc(size_t bytes); /* pinned */
 int h2j_gpu_host_free(void *p);
 void *h2j_gpu_stream_create(void);

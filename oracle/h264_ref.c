@@ -13,7 +13,8 @@
  * test/img/img01.h264, Main profile CABAC) and by img01.h264.jpeg.
  * The 8x8 transform / 8x8 CABAC contexts (High profile) are exercised only by
  * generated vectors: parity for those is pinned to this restatement.
- * CAVLC (7.3.5.3.2 / 9.2) with the VLC tables of tools/gen_cavlc_tables.py.
+ * CAVLC (7.3.5.3.2 / 9.2) with its own hand-typed VLC tables (cavlc_spec.h), checked
+ * against the product's generated ones by tests/test_cavlc_tables.py.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -22,7 +23,7 @@
 
 #include "bits.h"
 #include "cabac_tables.h"
-#include "cavlc_tables.h"
+#include "cavlc_spec.h"
 #include "oracle.h"
 
 /* ------------------------------------------------------------ CABAC init (I slices) */
@@ -241,16 +242,19 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
     if (!s->frame_mbs_only) return -3; /* interlaced: out of scope */
     ob_u(b, 1);                         /* direct_8x8_inference */
     if (ob_u(b, 1)) {
-        /* FFmpeg h264_ps.c ignores cropping that leaves no picture ("crop values invalid",
-         * "Ignoring cropping information") unless err_recognition has AV_EF_EXPLODE */
+        /* FFmpeg 4.3 h264_ps.c rejects the SPS ("crop values invalid", goto fail) when an
+         * offset exceeds INT_MAX / 4 / step or the window leaves no picture (only hevc_ps.c
+         * ignores such a window and shows the whole surface) */
         int cx = s->chroma_format_idc == 0 ? 1 : 2, cy = s->chroma_format_idc == 1 ? 2 : 1;
         uint64_t cl = ob_ue(b), cr = ob_ue(b), ct = ob_ue(b), cb = ob_ue(b);
-        if ((cl + cr) * cx < (uint64_t)s->mb_w * 16 && (ct + cb) * cy < (uint64_t)s->mb_h * 16) {
-            s->crop_l = (int)cl * cx;
-            s->crop_r = (int)cr * cx;
-            s->crop_t = (int)ct * cy;
-            s->crop_b = (int)cb * cy;
-        }
+        uint64_t lx = 0x7fffffffu / 4 / (unsigned)cx, ly = 0x7fffffffu / 4 / (unsigned)cy;
+        if (cl > lx || cr > lx || ct > ly || cb > ly || (cl + cr) * cx >= (uint64_t)s->mb_w * 16 ||
+            (ct + cb) * cy >= (uint64_t)s->mb_h * 16)
+            return -6;
+        s->crop_l = (int)cl * cx;
+        s->crop_r = (int)cr * cx;
+        s->crop_t = (int)ct * cy;
+        s->crop_b = (int)cb * cy;
     }
     if (s->chroma_format_idc != 1) return -4;
     s->valid = 1;
@@ -1148,14 +1152,13 @@ static int decode_mb(H4Dec *d, int slice_idx) {
 }
 
 /* ------------------------------------------------------------ CAVLC (7.3.5.3.2, 9.2) */
-static int vlc_read(OraBits *b, const uint8_t *lens, const void *codes, int wide, int n) {
+/* the index of the first entry (of n) whose code the next bits match; bit by bit, as 9.2 reads */
+static int vlc_read(OraBits *b, const uint8_t *lens, const uint8_t *codes, int n) {
     uint32_t code = 0;
     for (int len = 1; len <= 16; len++) {
         code = (code << 1) | (uint32_t)ob_bit(b);
-        for (int i = 0; i < n; i++) {
-            uint32_t c = wide ? ((const uint16_t *)codes)[i] : ((const uint8_t *)codes)[i];
-            if (lens[i] == len && c == code) return i;
-        }
+        for (int i = 0; i < n; i++)
+            if (lens[i] == len && codes[i] == code) return i;
     }
     return -1;
 }
@@ -1169,18 +1172,12 @@ static int cavlc_coeff_token(OraBits *b, int nC, int *t1) {
         if ((v >> 2) + 1 < *t1) return -1;
         return (v >> 2) + 1;
     }
-    int col = nC < 0 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
-    uint32_t code = 0;
-    for (int len = 1; len <= 16; len++) {
-        code = (code << 1) | (uint32_t)ob_bit(b);
-        for (int t = 0; t < 4; t++)
-            for (int tc = 0; tc <= 16; tc++)
-                if (kCoeffTokenLen[col][t][tc] == len && kCoeffTokenCode[col][t][tc] == code) {
-                    *t1 = t;
-                    return tc;
-                }
-    }
-    return -1;
+    /* Table 9-5, indexed TotalCoeff * 4 + TrailingOnes */
+    int i = nC < 0 ? vlc_read(b, k_ct_dc_len, k_ct_dc_bits, 4 * 5)
+                   : vlc_read(b, k_ct_len[nC < 2 ? 0 : (nC < 4 ? 1 : 2)], k_ct_bits[nC < 2 ? 0 : (nC < 4 ? 1 : 2)], 4 * 17);
+    if (i < 0) return -1;
+    *t1 = i & 3;
+    return i >> 2;
 }
 
 /* residual_block_cavlc: coeffLevel[0..maxNum-1] in scan order; returns TotalCoeff (-1 error) */
@@ -1213,14 +1210,14 @@ static int cavlc_block(H4Dec *d, int nC, int maxNum, int *out) {
     }
     int zerosLeft = 0;
     if (tc < maxNum) {
-        if (maxNum == 4) zerosLeft = vlc_read(b, kTotalZerosDcLen[tc - 1], kTotalZerosDcCode[tc - 1], 0, 5 - tc);
-        else zerosLeft = vlc_read(b, kTotalZerosLen[tc - 1], kTotalZerosCode[tc - 1], 0, 17 - tc);
+        if (maxNum == 4) zerosLeft = vlc_read(b, k_tz_dc_len[tc - 1], k_tz_dc_bits[tc - 1], 5 - tc);
+        else zerosLeft = vlc_read(b, k_tz_len[tc - 1], k_tz_bits[tc - 1], 17 - tc);
         if (zerosLeft < 0 || zerosLeft > maxNum - tc) return -1;
     }
     for (int i = 0; i < tc - 1; i++) {
         if (zerosLeft > 0) {
             int zl = zerosLeft < 7 ? zerosLeft : 7;
-            int r = vlc_read(b, kRunBeforeLen[zl - 1], kRunBeforeCode[zl - 1], 1, zl < 7 ? zl + 1 : 15);
+            int r = vlc_read(b, k_run_len[zl - 1], k_run_bits[zl - 1], zl < 7 ? zl + 1 : 15);
             if (r < 0 || r > zerosLeft) return -1;
             run[i] = r;
             zerosLeft -= r;
@@ -1314,7 +1311,7 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     } else {
         uint32_t cn = ob_ue(b);
         if (cn > 47) return -1;
-        m->cbp = kCbpIntra[cn];
+        m->cbp = k_cbp_intra[cn];
     }
     if ((m->cbp & 15) || (m->cbp >> 4) || is16) {
         int qpd = ob_se(b);
@@ -1512,7 +1509,13 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             if (!s->valid) { ret = -4; goto done; }
             int frame_num = (int)ob_u(&b, s->log2_max_frame_num);
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
-            if (first_mb < 0 || first_mb >= s->mb_w * s->mb_h) { ret = -6; goto done; } /* FFmpeg: "first_mb_in_slice overflow" */
+            /* FFmpeg: "first_mb_in_slice overflow" drops the slice; picture 0 is output from the
+             * slices already collected, and fails only when none was */
+            if (first_mb < 0 || first_mb >= s->mb_w * s->mb_h) {
+                if (have) break;
+                ret = -6;
+                goto done;
+            }
             if (slice_type % 5 != 2) { ret = -5; goto done; } /* P/B: the first picture must be intra */
             if (type == 5) ob_ue(&b);                          /* idr_pic_id */
             if (s->poc_type == 0) {

@@ -7,9 +7,13 @@ the decoder-delay ones (/root/reference/src/Decoder.cpp:342-360: one packet sent
 avcodec_receive_frame gives EAGAIN); this build transcodes picture 0 (INTEGRATION.md,
 "Documented differences") -- its planes and JPEG must equal the oracle's.
 
-Malformed vectors (tests/golden/malformed): cropping windows that leave no picture are ignored
-as FFmpeg ignores them (a JPEG of the whole coded picture, equal to the oracle's); the others
-fail cleanly with a per-picture message."""
+With H2J_STRICT_REFERENCE=1 the engine returns no JPEG for the decoder-delay streams, as the
+reference does, and keeps transcoding every other vector.
+
+Malformed vectors (tests/golden/malformed): HEVC conformance windows that leave no picture are
+ignored as FFmpeg's hevc_ps.c ignores them (a JPEG of the whole coded picture, equal to the
+oracle's); H.264 cropping that leaves no picture fails as h264_ps.c rejects the SPS; the other
+vectors fail cleanly with a per-picture message."""
 import json
 import os
 
@@ -54,3 +58,24 @@ def test_malformed_parameter_sets(engine):
         else:
             assert o is None, e["file"]
             assert engine.frame_error(i), e["file"]  # a per-picture message, not the engine-wide one
+
+
+def test_strict_reference_mode_on_decoder_delay_streams(engine):
+    """H2J_STRICT_REFERENCE=1: false (no JPEG, a per-picture message) exactly where the reference
+    returns false (/root/reference/src/Decoder.cpp:342-360); the default engine transcodes them."""
+    import h2j
+    streams = [read(golden("f3/" + e["file"])) for e in F3]
+    default = engine.transcode(streams)
+    os.environ["H2J_STRICT_REFERENCE"] = "1"
+    try:
+        strict_engine = h2j.Engine()
+    finally:
+        del os.environ["H2J_STRICT_REFERENCE"]
+    strict = strict_engine.transcode(streams)
+    for i, (e, d, st) in enumerate(zip(F3, default, strict)):
+        assert d is not None and d[:2] == b"\xff\xd8", e["file"]
+        if e["reference_returns"] is False:
+            assert st is None, e["file"]
+            assert "decoder delay" in strict_engine.frame_error(i), e["file"]
+        else:
+            assert st == d, e["file"]

@@ -89,6 +89,21 @@ def test_bench_streams_sample(engine):
         assert o == O.transcode(s), p
 
 
+def test_bench_nosdh_1080p(engine):
+    """configs[1]-sized pictures with sign-data hiding off (tools/make_streams.py nosdh): the path
+    the reference fixture img01.h265 pins, at 1080p; planes and JPEG equal the oracle's."""
+    paths = sorted(glob.glob(os.path.join(golden("bench_nosdh"), "*.h265")))
+    assert len(paths) == 2
+    streams = [read(p) for p in paths]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, paths):
+        assert o == O.transcode(s), p
+        gy, gu, gv, bd = engine.decode(s, stage=0)
+        oy, ou, ov, obd = O.decode(s, 265)
+        for g, q, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
+            assert np.array_equal(g, q), (p, name)
+
+
 def test_invalid_inputs_fail_cleanly(engine):
     outs = engine.transcode([b"", b"\x00\x00\x01\x40garbage", read(golden("img01.h265"))[:1000]])
     assert outs[0] is None and outs[1] is None

@@ -1,6 +1,7 @@
 """Generate the H.264 CAVLC VLC tables (ITU-T H.264 Tables 9-5, 9-7, 9-8,
-9-9(a), 9-10 and the intra column of Table 9-4) as C headers for the oracle,
-the host parser and tools/h264gen, after checking every table is prefix-free
+9-9(a), 9-10 and the intra column of Table 9-4) as C headers for the host
+parser and tools/h264gen (the oracle has an independent hand-typed copy,
+oracle/cavlc_spec.h), after checking every table is prefix-free
 (and printing its Kraft sum).  Spec data, written once here.
 
   python tools/gen_cavlc_tables.py
@@ -193,7 +194,9 @@ def main():
     out.append("static const uint8_t kCbpIntra[48] = {" + ", ".join(map(str, CBP_INTRA)) + "};")
     out += ["", "#endif", ""]
     text = "\n".join(out)
-    for path in ("oracle/cavlc_tables.h", "h264-h265-to-jpeg_amd/csrc/host/cavlc_tables.h", "tools/h264gen/cavlc_tables.h"):
+    # the oracle keeps its own hand-typed copy (oracle/cavlc_spec.h), checked against these by
+    # tests/test_cavlc_tables.py
+    for path in ("h264-h265-to-jpeg_amd/csrc/host/cavlc_tables.h", "tools/h264gen/cavlc_tables.h"):
         open(os.path.join(ROOT, path), "w").write(text)
         print("wrote", path)
 

@@ -130,6 +130,19 @@ def heavy(n=16):
     print("total", total, "mean", total // n)
 
 
+def nosdh(n=2):
+    """configs[1]-sized pictures with sign-data hiding off: the path img01.h265 (the reference
+    fixture) pins, exercised at 1080p as well (bench streams use --sdh 1, hevcgen's default)."""
+    out_dir = os.path.join(ROOT, "tests/golden/bench_nosdh")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    for i, (qp, sigma) in enumerate([(22, 2), (32, 0)][:n]):
+        content = make_content(planes, 1920, 1080, 500 + i, sigma, 8)
+        path = os.path.join(out_dir, f"hevc1080_nosdh_{i:02d}.h265")
+        nb = encode(content, 1920, 1080, 8, qp, 500 + i, path, ["--sdh", "0"])
+        print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+
+
 PARITY = [
     # name, W, H, bd, qp, seed, sigma, options
     ("p01_416x240_q22", 416, 240, 8, 22, 11, 2, []),
@@ -298,13 +311,14 @@ def f3():
 
 
 MALFORMED = [
-    # parameter-set values outside their ranges.  FFmpeg (the reference path) ignores
-    # cropping / conformance windows that leave no picture (h264_ps.c "crop values invalid",
-    # hevc_ps.c "Invalid cropping offsets") and rejects the others; "ok" = a JPEG of the whole
-    # coded picture, "fail" = no JPEG.
+    # parameter-set values outside their ranges.  FFmpeg 4.3 (the reference path)
+    # rejects an H.264 SPS whose cropping leaves no picture (h264_ps.c "crop values invalid",
+    # goto fail) but ignores such an HEVC conformance window (hevc_ps.c "Invalid cropping
+    # offsets ... Displaying the whole video surface"); "ok" = a JPEG of the whole coded
+    # picture, "fail" = no JPEG.
     # name, codec, W, H, options, expect
-    ("m_avc_crop_overflow", 264, 400, 232, ["--crop", "0,300,0,0"], "ok"),
-    ("m_avc_crop_huge", 264, 400, 232, ["--crop", "2147483647,0,5,4"], "ok"),
+    ("m_avc_crop_overflow", 264, 400, 232, ["--crop", "0,300,0,0"], "fail"),
+    ("m_avc_crop_huge", 264, 400, 232, ["--crop", "2147483647,0,5,4"], "fail"),
     ("m_avc_firstmb_oob", 264, 128, 96, ["--firstmb", "100000"], "fail"),
     ("m_hevc_conf_overflow", 265, 396, 228, ["--conf", "0,250,0,0"], "ok"),
     ("m_hevc_conf_huge", 265, 396, 228, ["--conf", "4294967294,0,0,4294967294"], "ok"),
@@ -349,4 +363,4 @@ if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
-     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed}[what]()
+     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh}[what]()
