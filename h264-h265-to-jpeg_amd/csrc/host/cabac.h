@@ -25,9 +25,9 @@ extern const uint8_t kCabacLpsByState[128][8];
 // of a bin is then a shift of a register by the range, not a table load after it.
 typedef uint64_t CabacState;
 // word of each state, and the word after an MPS / LPS bin
-extern const uint64_t (&kCabacWord)[128];
-extern const uint64_t (&kCabacNextMpsW)[128];
-extern const uint64_t (&kCabacNextLpsW)[128];
+extern const uint64_t kCabacWord[128];
+extern const uint64_t kCabacNextMpsW[128];
+extern const uint64_t kCabacNextLpsW[128];
 
 
 inline uint8_t cabac_init_state(int m, int n, int qp) {
@@ -62,7 +62,7 @@ public:
     // end to end).  Both outcomes' renormalised ranges are ready when the compare resolves (rLPS
     // shifted by its leading zeros; rMPS = range - rLPS >= 128 shifted by 0 or 1), so the chain
     // per bin is range -> byte shift of the context word -> subtract -> scale -> compare -> cmov.
-    inline int decision(CabacState& ctx) {
+    __attribute__((always_inline)) inline int decision(CabacState& ctx) {
         H2J_COUNT(g_bins_ctx, 1);
         const uint64_t w = ctx;
         const unsigned st = static_cast<unsigned>(w >> 32);
