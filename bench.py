@@ -229,6 +229,45 @@ def single_call_latency(streams, calls=9):
     return res
 
 
+def timed_batches(eng, batch, steps, warmup):
+    """Frames/s of `steps` pipelined 1024-picture steps (after `warmup`) of `batch` on `eng`, the
+    same submit/wait pattern as the main measurement; returns (fps, per-step stats)."""
+    n = len(batch)
+    bufs = [(ctypes.c_uint8 * len(s)).from_buffer_copy(s) for s in batch]
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    sizes = (ctypes.c_size_t * n)(*[len(s) for s in batch])
+    cap = n * (2 << 20)
+    outsets = [((ctypes.c_uint8 * cap)(), (ctypes.c_size_t * n)(), (ctypes.c_size_t * n)(), (ctypes.c_int * n)())
+               for _ in range(2)]
+    acc = {}
+
+    def run(k_steps, record):
+        inflight = []
+        for k in range(k_steps + 1):
+            if k < k_steps:
+                out, offs, lens, status = outsets[k % 2]
+                inflight.append((eng.submit_raw(ptrs, sizes, n, out, cap, offs, lens, status), status))
+            if k > 0:
+                t, status = inflight.pop(0)
+                if eng.wait(t) != 0 or any(status[i] != 0 for i in range(n)):
+                    raise RuntimeError(f"transcode failed: {eng.error()}")
+                if record:
+                    for key, v in eng.stats().items():
+                        acc[key] = acc.get(key, 0.0) + v
+
+    run(warmup, False)
+    t0 = time.perf_counter()
+    run(steps, True)
+    dt = time.perf_counter() - t0
+    return n * steps / dt, {k: v / steps for k, v in acc.items()}
+
+
+def parse_core_us_per_kb(per, threads, batch):
+    """Host entropy cost: the pool's wall time on a batch (first to last picture parsed) x its
+    threads, per KB of bitstream."""
+    return round(per["parse_run_ms"] * 1e3 * threads / (sum(len(b) for b in batch) / 1024), 2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,6 +285,8 @@ def main():
                     help="one synchronous h2j_engine_transcode per step (no cross-step overlap)")
     ap.add_argument("--no-single-call", action="store_true",
                     help="skip the configs[0] single-call latencies (profiling runs: no extra 1-picture launches)")
+    ap.add_argument("--no-aim", action="store_true",
+                    help="skip value_aim (configs[1] on the 100-250 KB/picture set) and the host-thread sweep")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,6 +444,8 @@ def main():
                          "frac_k1_own_def": "K1's own bytes (2S residual in + b*S picture out) / K1 time",
                          "frac_pipeline": frac_pipeline,
                          "frac_pipeline_def": "BASELINE.md: frames*B / t_kernels(K0..K5)",
+                         "traffic_ratio_k1_own": (traffic / k1_own_launch) if traffic else None,
+                         "traffic_ratio_k1_own_def": "PMC HBM bytes per K1 launch / K1's own bytes (2S + b*S)",
                          "per_launch_size": variants},
             # value is end to end: host CABAC/CAVLC (north_star keeps entropy decoding on host
             # threads) + PCIe + K0-K5 + container.  With the job records already in HBM the
@@ -414,8 +457,10 @@ def main():
             "gpu_pipeline_fps": n / (gpu_ms / 1e3),
             "host_cpu_busy_cores": round(host_cores, 2),
             "bitstream_kb_per_frame": round(sum(len(b) for b in batch) / n / 1024, 1),
-            "parse_us_per_kb_wall": round(per["parse_ms"] * 1e3 / (sum(len(b) for b in batch) / 1024), 3),
-            "parse_core_us_per_kb": round(per["parse_ms"] * 1e3 * host["threads"] / (sum(len(b) for b in batch) / 1024), 2),
+            "parse_us_per_kb_wall": round(per["parse_run_ms"] * 1e3 / (sum(len(b) for b in batch) / 1024), 3),
+            "parse_core_us_per_kb": parse_core_us_per_kb(per, host["threads"], batch),
+            "parse_core_def": "pool wall time from the batch's first to its last parsed picture x host threads / KB "
+                              "(r02 used submission -> last parsed, which counted the wait behind the previous batch)",
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
         }
         # configs[0]-style single calls: the reference fixture and one stream of this workload
@@ -423,6 +468,27 @@ def main():
             with open(os.path.join(ROOT, "tests", "golden", "img01.h265"), "rb") as fx:
                 fixture = fx.read()
             res["single_call_ms"] = single_call_latency([("img01.h265", fixture), ("workload_stream0", streams[0])])
+        # N = 1 only: configs[1] on the SURVEY.md §8(d)-aim set (100-250 KB per picture), and the
+        # end-to-end rate against the host entropy threads on this one GPU (DESIGN.md §7 predicts
+        # the 1 -> 8 GPU curve from it)
+        if world == 1 and args.workload == "hevc1080" and not args.no_aim:
+            heavy = load_streams(WORKLOADS["hevc1080_heavy"]["streams"])
+            hbatch = [heavy[i % len(heavy)] for i in range(n)]
+            fps, hper = timed_batches(eng, hbatch, 4, 1)
+            res["value_aim"] = fps
+            res["value_aim_def"] = ("configs[1] on tests/golden/bench_heavy (16 hevcgen 1080p streams, "
+                                    f"{sum(len(b) for b in hbatch) / n / 1024:.1f} KB/picture), same engine and timing")
+            res["value_aim_parse_core_us_per_kb"] = parse_core_us_per_kb(hper, host["threads"], hbatch)
+            sweep = {}
+            for t in (2, 4, 8, 16):
+                if t > host["threads"]:
+                    continue
+                e2 = eng if t == host["threads"] else h2j.Engine(local, t)
+                fps_t, _ = timed_batches(e2, batch, 2 if t >= 8 else 1, 1)
+                sweep[str(t)] = round(fps_t, 1)
+                if e2 is not eng:
+                    e2.close()
+            res["host_thread_sweep_fps"] = sweep
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(streams, host["threads"])
         print(json.dumps(res), flush=True)

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cstdio>
 
 #include "h2j_gpu.h"
@@ -489,8 +490,11 @@ DEVI void emit_block(uint32_t* out, uint32_t w0, uint32_t bit0, uint32_t bits, c
     s.finish();
 }
 
+// emit_words: tiles whose payload spans more words take the global-memory path (kEmitWords;
+// H2J_EMIT_GLOBAL=1 passes 0, every tile on the global path: coverage of that path in tests)
 __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, uint8_t* arena,
-                                                      const uint32_t* tile_bits, int max_tiles, uint8_t* seg) {
+                                                      const uint32_t* tile_bits, int max_tiles, uint8_t* seg,
+                                                      int emit_words) {
     const GridPos gp = xcd_grid_pos();
     __shared__ CodeLds cl;
     __shared__ uint32_t sh[kTile / 64];
@@ -525,7 +529,7 @@ __global__ void __launch_bounds__(kTile) h2j_k5d_emit(const h2j_frame* frames, u
     uint32_t* out = reinterpret_cast<uint32_t*>(seg + js->seg_off);
     const uint32_t w_lo = tile0 >> 5, w_hi = (tile0 + total + 31) >> 5;
     const int nw = static_cast<int>(w_hi - w_lo);
-    if (nw > kEmitWords) {  // rare: straight to global memory
+    if (nw > emit_words) {  // rare: straight to global memory
         if (mine) emit_block<false>(out, 0, bit0, bits, cl, sym, cnt, t, diff, tab, bi == nblk - 1);
         return;
     }
@@ -584,8 +588,10 @@ int h2j_gpu_entropy(const h2j_gpu_batch* b, void* stream) {
     if ((r = check(hipGetLastError(), "h2j_k5c_scan_frames"))) return r;
     hipLaunchKernelGGL(h2j_k5z_zero, dim3(1024), dim3(256), 0, s, b->seg, b->seg_total);
     if ((r = check(hipGetLastError(), "h2j_k5z_zero"))) return r;
+    const char* eg = std::getenv("H2J_EMIT_GLOBAL");  // read per launch: tests switch it inside one process
+    const int emit_words = (eg && eg[0] == '1') ? 0 : kEmitWords;
     hipLaunchKernelGGL(h2j_k5d_emit, dim3(tiles, b->nframes), dim3(kTile), 0, s, b->frames, b->arena, b->tile_bits,
-                       tiles, b->seg);
+                       tiles, b->seg, emit_words);
     return check(hipGetLastError(), "h2j_k5d_emit");
 }
 

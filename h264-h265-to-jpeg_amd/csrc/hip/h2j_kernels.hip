@@ -298,18 +298,53 @@ DEVI void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Device-side failure flags of a picture (h2j_jstat.dev_error): a wait that never completes flags
+// its picture and gives up instead of hanging the GPU.
+enum : uint32_t {
+    kDevErrK1Band = 1u,       // H.264 K1: band hand-off (global flag) timed out
+    kDevErrDbBand = 2u,       // H.264 deblocking: band hand-off timed out
+    kDevErrK1Row = 4u,        // HEVC K1: row progress word (LDS) timed out
+    kDevErrK1Row264 = 8u,     // H.264 K1: row progress word timed out
+    kDevErrDbRow264 = 16u,    // H.264 deblocking: row progress word timed out
+};
+DEVI uint32_t* dev_error_word(uint8_t* arena, const h2j_frame& f) {
+    return reinterpret_cast<uint32_t*>(arena + (static_cast<uint64_t>(f.jstat) + offsetof(h2j_jstat, dev_error)));
+}
+// Wait (s_sleep polling, workgroup scope, acquire) until the LDS progress word reaches `need`.
+// Legitimate waits end within one picture's reconstruction (milliseconds); after 2^24 polls
+// (~0.4 s) the picture is flagged with `bit` and the wait returns ~0u, so every later wait of the
+// row passes and the workgroup drains.
+DEVI uint32_t wait_progress(const uint32_t* word, uint32_t need, uint32_t* err, uint32_t bit) {
+    uint32_t seen, it = 0;
+    while ((seen = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > (1u << 24)) {
+            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            seen = ~0u;
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return seen;
+}
+
 // Optional K1 cycle accounting (build with -DH2J_PROF: `make prof`), read via h2j_gpu_prof().
 #ifdef H2J_PROF
 __device__ unsigned long long g_prof[16];
 #define PROF_T() __builtin_amdgcn_s_memtime()
-#define PROF_ADD(i, v) (pacc[i] += (v))
-#define PROF_DECL unsigned long long pacc[16] = {0}; unsigned long long pt0 = PROF_T(), pt1, prt0 = __builtin_amdgcn_s_memrealtime(), pmt0 = pt0
-#define PROF_LAP(i) (pt1 = PROF_T(), PROF_ADD(i, pt1 - pt0), pt0 = pt1)
-#define PROF_LAPK(k) do { pt1 = PROF_T(); const unsigned long long d_ = pt1 - pt0; pt0 = pt1; \
-    switch (k) { case 0: pacc[8] += d_; break; case 1: pacc[9] += d_; break; case 2: pacc[10] += d_; break; \
-    case 3: pacc[11] += d_; break; case 4: pacc[12] += d_; break; case 5: pacc[13] += d_; break; \
-    case 6: pacc[14] += d_; break; default: pacc[15] += d_; break; } } while (0)
-#define PROF_FLUSH() do { pacc[4] = __builtin_amdgcn_s_memrealtime() - prt0; pacc[7] = PROF_T() - pmt0; if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd(&g_prof[q_], pacc[q_]); } while (0)
+// Accumulators per wave in LDS, added to by lane 0 (r02 kept 16 64-bit accumulators in registers:
+// that build of the pool kernel, already at its register limit with SGPR spills, never finished)
+#define PROF_DECL                                                                                  \
+    __shared__ unsigned long long prof_acc_[16][16];                                               \
+    unsigned long long* const pacc_ = prof_acc_[threadIdx.x >> 6];                                 \
+    if ((threadIdx.x & 63) < 16) pacc_[threadIdx.x & 63] = 0;                                      \
+    unsigned long long pt0 = PROF_T(), pt1;                                                        \
+    const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime(), pmt0 = pt0
+#define PROF_ADD(i, v) do { if ((threadIdx.x & 63) == 0) pacc_[i] += (v); } while (0)
+#define PROF_LAP(i) do { pt1 = PROF_T(); PROF_ADD(i, pt1 - pt0); pt0 = pt1; } while (0)
+#define PROF_LAPK(k) do { pt1 = PROF_T(); PROF_ADD(8 + ((k) < 7 ? (k) : 7), pt1 - pt0); pt0 = pt1; } while (0)
+#define PROF_FLUSH() do { PROF_ADD(4, __builtin_amdgcn_s_memrealtime() - prt0); PROF_ADD(7, PROF_T() - pmt0); \
+    if ((threadIdx.x & 63) < 16) atomicAdd(&g_prof[threadIdx.x & 63], pacc_[threadIdx.x & 63]); } while (0)
 #else
 #define PROF_DECL
 #define PROF_ADD(i, v)
@@ -1214,6 +1249,8 @@ DEVI void lds_dma4(const void* g, uint32_t lds) {
                  : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 }
 DEVI void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16 zero bytes per lane: the source of LDS-DMA lanes that fall outside a plane
+__device__ uint4 g_zero_src[64];
 DEVI void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 DEVI uint32_t lds_addr(const void* p) {
     return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
@@ -1493,8 +1530,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
                         __builtin_amdgcn_s_sleep(2);
                         if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
-                            uint32_t* err = reinterpret_cast<uint32_t*>(arena + ufl64(f.jstat) + offsetof(h2j_jstat, dev_error));
-                            if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (lane == 0) __hip_atomic_fetch_or(dev_error_word(arena, f), kDevErrK1Band, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             seen = static_cast<uint32_t>(mbw);
                             break;
                         }
@@ -1502,11 +1538,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 }
             } else if (row > rbeg || (row > 0 && nbands <= 1)) {
                 const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
-                if (seen < need) {
-                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                        __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
+                if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrK1Row264);
             }
             // ---- window: the DMA'd inputs, line above from LDS, left column carried
             H4In& in = s.in[cur];
@@ -1682,6 +1714,7 @@ struct FU {
     uint8_t* pic;     // plane 0 base (bytes); planes 1/2 at off1/off2 elements
     int16_t* res;     // residual plane 0; planes 1/2 at the same element offsets
     int off1, off2;
+    uint32_t* derr;   // the picture's h2j_jstat.dev_error
     DEVI int st(int c) const { return c ? stc : sty; }
     DEVI int off(int c) const { return c == 0 ? 0 : (c == 1 ? off1 : off2); }
     template <typename Pel>
@@ -1704,6 +1737,7 @@ DEVI FU make_fu(const h2j_frame& f, uint8_t* arena) {
     u.off2 = ufl(f.pic_off[2]);
     u.pic = arena + ufl64(f.pic);
     u.res = reinterpret_cast<int16_t*>(arena + ufl64(f.res));
+    u.derr = dev_error_word(arena, f);
     return u;
 }
 
@@ -2010,9 +2044,14 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
 // budget).  Luma: 2 x 16 B per lane, row-major Qc x Qc; chroma: 4 B per lane, Cb at element 0
 // and Cr at 256, Qc x Qc each.  Lanes outside the picture write zeros instead.
 DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* body, int lane) {
+    // lanes outside the picture copy 16 / 4 zero bytes from g_zero_src instead of branching
+    // around the copy (the branch kept an address live across an exec-mask change: a scratch
+    // spill store + reload per quadrant at this kernel's register budget)
+    const char* zero = reinterpret_cast<const char*>(g_zero_src);
+#ifdef H2J_DMA_BRANCH  // r02 form (A/B builds only): lanes outside the plane branch around the copy
     if (grp == 0) {
         const int16_t* R = u.rplane(0);
-        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;  // log2 of 16-B chunks per row
+        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int idx = lane + 64 * j, yy = idx >> lc, xx = (idx & ((1 << lc) - 1)) * 8;
@@ -2022,13 +2061,37 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {  // (plane, half): 64 lanes x 2 samples
+        for (int k = 0; k < 4; k++) {
             const int lq = __builtin_ctz(static_cast<unsigned>(Qc));
             const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e >> lq, xx = e & (Qc - 1);
             const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
             int16_t* dst = body + c * 256 + (k & 1) * 128;
             if (ok) lds_dma4(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx, lds_addr(dst));
             else *reinterpret_cast<uint32_t*>(dst + lane * 2) = 0u;
+        }
+    }
+    return;
+#endif
+    if (grp == 0) {
+        const int16_t* R = u.rplane(0);
+        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;  // log2 of 16-B chunks per row
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int idx = lane + 64 * j, yy = idx >> lc, xx = (idx & ((1 << lc) - 1)) * 8;
+            const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
+            const void* src = ok ? static_cast<const void*>(R + (Y0 + yy) * u.sty + X0 + xx) : static_cast<const void*>(zero);
+            lds_dma16(src, lds_addr(body + 512 * j));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // (plane, half): 64 lanes x 2 samples
+            const int lq = __builtin_ctz(static_cast<unsigned>(Qc));
+            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e >> lq, xx = e & (Qc - 1);
+            const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
+            int16_t* dst = body + c * 256 + (k & 1) * 128;
+            const void* src = ok ? static_cast<const void*>(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx)
+                                 : static_cast<const void*>(zero);
+            lds_dma4(src, lds_addr(dst));
         }
     }
 }
@@ -2040,7 +2103,7 @@ DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* b
 // row r + 1 reads).
 template <typename Pel>
 DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const uint32_t* rng, int grp, QWave& w,
-                   const uint32_t* above, uint32_t* mine, int16_t* line, const int row) {
+                   const uint32_t* above, uint32_t* mine, int16_t* line, const int row, Pel* stg) {
     const int lane = threadIdx.x & 63;
     const int shc = grp ? 1 : 0;                 // component subsampling of this group
     const int CS = 1 << u.log2ctb;               // luma CTB size
@@ -2112,11 +2175,7 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                     int cnt = nq * (cx + 1);
                     if (qx == nqs - 1 && cx + 1 < u.ctb_w) cnt += nqs == 2 ? 3 : 1;
                     const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(cnt);
-                    if (seen < need) {
-                        while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                            __builtin_amdgcn_s_sleep(1);
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    }
+                    if (seen < need) seen = wait_progress(above, need, u.derr, kDevErrK1Row);
                 }
                 PROF_LAP(0);
                 // neighbour arrays of the quadrant: one pass, lane = x of the line above and y of
@@ -2219,24 +2278,57 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                 lds_dma_wait();
                 const int wq = min(Qc, Wc - X0), hq = min(Qc, Hc - Y0);
                 const int lq = __builtin_ctz(static_cast<unsigned>(Qc)) - 2;  // log2 of 4-sample steps per row
+                // quadrant pairs (TL | TR, BL | BR) leave as whole CTB-wide rows (64 B of 8-bit luma
+                // instead of two 32-B halves, 32 B of chroma instead of 16): a left quadrant whose
+                // right neighbour lies inside the picture is parked in `stg` (the wave's staging
+                // tile, samples packed as Pel) and stored with it
+                const bool pair = stg != nullptr && nqs == 2;
+                const bool park = pair && qx == 0 && X0 + Qc < Wc;
+                const bool joined = pair && qx == 1;
                 for (int ci = 0; ci < ncomp; ci++) {
                     const int c = grp ? ci + 1 : 0;
                     QComp& C = w.cs[ci];
                     const int16_t* body = w.body[cur] + ci * 256;
                     Pel* P = u.plane<Pel>(c);
                     const int st = u.st(c);
-                    // 4 samples per lane step (component widths are multiples of 4); rows of the
-                    // window beyond the picture's right edge masked
-                    for (int i = lane; i < (hq << lq); i += 64) {
-                        const int y = i >> lq, x = (i & ((1 << lq) - 1)) * 4;
-                        if (x >= wq) continue;
-                        const uint2 v = *reinterpret_cast<const uint2*>(body + (y << (lq + 2)) + x);
-                        Pel* d = P + (Y0 + y) * st + X0 + x;
-                        if (sizeof(Pel) == 1) {
-                            *reinterpret_cast<uint32_t*>(d) =
-                                (v.x & 0xFF) | ((v.x >> 8) & 0xFF00) | ((v.y & 0xFF) << 16) | ((v.y >> 16) << 24);
-                        } else {
-                            *reinterpret_cast<uint2*>(d) = v;
+                    auto pack4 = [&](const int16_t* src) __attribute__((always_inline)) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(src);
+                        return sizeof(Pel) == 1 ? make_uint2((v.x & 0xFF) | ((v.x >> 8) & 0xFF00) | ((v.y & 0xFF) << 16) | ((v.y >> 16) << 24), 0u)
+                                                : v;
+                    };
+                    auto put4 = [&](Pel* d, uint2 v) __attribute__((always_inline)) {
+                        if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = v.x;
+                        else *reinterpret_cast<uint2*>(d) = v;
+                    };
+                    if (park) {  // Qc x hq samples into the staging tile (rows of Qc, Cb at 0, Cr at 256)
+                        Pel* sg = stg + ci * 256;
+                        for (int i = lane; i < (hq << lq); i += 64) {
+                            const int y = i >> lq, x = (i & ((1 << lq) - 1)) * 4;
+                            put4(sg + (y << (lq + 2)) + x, pack4(body + (y << (lq + 2)) + x));
+                        }
+                    } else if (joined) {  // rows of 2Qc: the parked left quadrant, then this one
+                        const Pel* sg = stg + ci * 256;
+                        const int l2 = lq + 1;  // log2 of 4-sample steps per joined row
+                        for (int i = lane; i < (hq << l2); i += 64) {
+                            const int y = i >> l2, x = (i & ((1 << l2) - 1)) * 4;
+                            if (x >= Qc + wq) continue;
+                            uint2 v;
+                            if (x < Qc) {
+                                const Pel* q = sg + (y << (lq + 2)) + x;
+                                v = sizeof(Pel) == 1 ? make_uint2(*reinterpret_cast<const uint32_t*>(q), 0u)
+                                                     : *reinterpret_cast<const uint2*>(q);
+                            } else {
+                                v = pack4(body + (y << (lq + 2)) + x - Qc);
+                            }
+                            put4(P + (Y0 + y) * st + X0 - Qc + x, v);
+                        }
+                    } else {
+                        // 4 samples per lane step (component widths are multiples of 4); rows of
+                        // the window beyond the picture's right edge masked
+                        for (int i = lane; i < (hq << lq); i += 64) {
+                            const int y = i >> lq, x = (i & ((1 << lq) - 1)) * 4;
+                            if (x >= wq) continue;
+                            put4(P + (Y0 + y) * st + X0 + x, pack4(body + (y << (lq + 2)) + x));
                         }
                     }
                     // carries: the bottom row (line for the CTB row below, qbot for the bottom
@@ -2284,7 +2376,8 @@ DEVI void hevc_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, int grp
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
     const int kSlots = 2 * W_;
     for (int row = wv; row < u.ctb_h; row += W_)
-        hevc_row<Pel>(u, T, masks, rng, grp, W[wv], prog + (row + kSlots - 1) % kSlots, prog + row % kSlots, line, row);
+        hevc_row<Pel>(u, T, masks, rng, grp, W[wv], prog + (row + kSlots - 1) % kSlots, prog + row % kSlots, line, row,
+                      static_cast<Pel*>(nullptr));
 }
 
 
@@ -2369,11 +2462,16 @@ __host__ __device__ constexpr size_t k1_pool_lds(int P, int maxrows, int lstride
     return sizeof(QWave) * kPoolWaves + (static_cast<size_t>(P) * 2 * maxrows + 4) * 4 +
            static_cast<size_t>(P) * lstride * 2;
 }
+// + per wave a staging tile of 32 x 32 samples (quadrant pairs stored as whole CTB-wide rows)
+__host__ __device__ constexpr size_t k1_pool_stage_lds(int pel_bytes) {
+    return static_cast<size_t>(kPoolWaves) * 32 * 32 * pel_bytes;
+}
 // The pool's job loop over pictures fi0 .. fi0 + P - 1 (those below `nframes`) in `lds` (see
 // k1_pool_lds); every thread of the 16-wave workgroup calls it.
+// `staged`: the LDS also holds the staging tiles (k1_pool_stage_lds, after k1_pool_lds rounded to 16 B).
 template <typename Pel>
 DEVI void hevc_pool_jobs(const h2j_frame* frames, const h2j_tu* tus, uint8_t* arena, int fi0, int nframes, int P,
-                         int maxrows, int lstride, int lchroma, uint8_t* lds) {
+                         int maxrows, int lstride, int lchroma, uint8_t* lds, bool staged) {
     QWave* W = reinterpret_cast<QWave*>(lds);
     uint32_t* prog = reinterpret_cast<uint32_t*>(lds + sizeof(QWave) * kPoolWaves);
     const int nprog = P * 2 * maxrows;
@@ -2383,6 +2481,8 @@ DEVI void hevc_pool_jobs(const h2j_frame* frames, const h2j_tu* tus, uint8_t* ar
     __syncthreads();
     const int lane = static_cast<int>(threadIdx.x & 63), wv = static_cast<int>(threadIdx.x >> 6);
     const uint32_t njobs = static_cast<uint32_t>(nprog);
+    Pel* stg = staged ? reinterpret_cast<Pel*>(lds + ((k1_pool_lds(P, maxrows, lstride) + 15) & ~size_t(15))) + wv * 1024
+                      : static_cast<Pel*>(nullptr);
     for (;;) {
         uint32_t j = 0;
         if (lane == 0) j = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2401,16 +2501,17 @@ DEVI void hevc_pool_jobs(const h2j_frame* frames, const h2j_tu* tus, uint8_t* ar
         const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
         uint32_t* pr = prog + (p * 2 + grp) * maxrows;
         int16_t* line = lines + p * lstride + (grp ? lchroma : 0);
-        if (grp == 0) hevc_row<Pel>(u, T, masks, rng, 0, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
-        else hevc_row<Pel>(u, T, masks, rng, 1, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row);
+        if (grp == 0) hevc_row<Pel>(u, T, masks, rng, 0, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row, stg);
+        else hevc_row<Pel>(u, T, masks, rng, 1, W[wv], pr + (row ? row - 1 : 0), pr + row, line, row, stg);
     }
 }
 template <typename Pel>
 __global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const h2j_frame* frames, const h2j_tu* tus,
                                                                         uint8_t* arena, int nframes, int P, int maxrows,
-                                                                        int lstride, int lchroma) {
+                                                                        int lstride, int lchroma, int staged) {
     extern __shared__ __align__(16) uint8_t k1lds[];
-    hevc_pool_jobs<Pel>(frames, tus, arena, static_cast<int>(blockIdx.x) * P, nframes, P, maxrows, lstride, lchroma, k1lds);
+    hevc_pool_jobs<Pel>(frames, tus, arena, static_cast<int>(blockIdx.x) * P, nframes, P, maxrows, lstride, lchroma, k1lds,
+                        staged != 0);
 }
 
 // K1 for batches mixing HEVC 8-bit, HEVC high bit depth and H.264 pictures (configs[4]): one
@@ -2444,9 +2545,9 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
         const int fi = static_cast<int>((me >> 8) & 0x3FFFFFu);
         const int w = static_cast<int>(ufl(f.width)), rows = static_cast<int>(ufl(f.ctb_h));
         if (ufl(f.bit_depth) == 8 && ufl(f.bit_depth_c) == 8)
-            hevc_pool_jobs<uint8_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds);
+            hevc_pool_jobs<uint8_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds, false);
         else
-            hevc_pool_jobs<uint16_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds);
+            hevc_pool_jobs<uint16_t>(frames, tus, arena, fi, fi + 1, 1, rows, 2 * w + 192, w + 64, anylds, false);
     } else {
         H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(anylds);
         uint32_t* prog = reinterpret_cast<uint32_t*>(anylds + sizeof(H4WaveLds) * kAvcWaves);
@@ -2862,8 +2963,7 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                     while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
                         __builtin_amdgcn_s_sleep(2);
                         if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
-                            uint32_t* err = reinterpret_cast<uint32_t*>(arena + ufl64(f.jstat) + offsetof(h2j_jstat, dev_error));
-                            if (lane == 0) __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (lane == 0) __hip_atomic_fetch_or(dev_error_word(arena, f), kDevErrDbBand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             seen = 2u * mbw;
                             break;
                         }
@@ -2871,11 +2971,7 @@ DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* 
                 }
             } else if (row > rbeg || (row > 0 && nbands <= 1)) {
                 const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
-                if (seen < need) {
-                    while ((seen = __hip_atomic_load(above, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                        __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
+                if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrDbRow264);
             }
             PROF_LAP(0);
             // window: MB body (prefetched), rows above (line buffer); the left columns are carried
@@ -4056,18 +4152,30 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
             // many pictures each as fit (LDS: one set of line buffers + progress words per picture)
             const int maxrows = (b->max_h + 15) / 16;
             const int lstride = 2 * b->max_w + 192, lchroma = b->max_w + 64;
-            int P = std::max(1, std::min(pool_p, b->nframes / 256));  // never fewer than 256 workgroups
-            while (P > 1 && k1_pool_lds(P, maxrows, lstride) > 160 * 1024) P--;
-            const size_t lds = k1_pool_lds(P, maxrows, lstride);
-            if (lds > 160 * 1024) {
-                snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pool: %zu B of LDS per workgroup (max 160 KB)", lds);
-                return -1;
+            // LDS: the pool's layout + the staging tiles (k1_pool_stage_lds) of the launch's sample size;
+            // H2J_K1_STAGE=0: quadrants stored one by one (A/B timing)
+            static const bool staged = [] {
+                const char* e = std::getenv("H2J_K1_STAGE");
+                return !(e && e[0] == '0');
+            }();
+            auto pool_lds = [&](int P, int pel) {
+                return ((k1_pool_lds(P, maxrows, lstride) + 15) & ~size_t(15)) + (staged ? k1_pool_stage_lds(pel) : 0);
+            };
+            for (int pel = 1; pel <= 2; pel++) {
+                if (!(pel == 1 ? p8 : p16)) continue;
+                int P = std::max(1, std::min(pool_p, b->nframes / 256));  // never fewer than 256 workgroups
+                while (P > 1 && pool_lds(P, pel) > 160 * 1024) P--;
+                const size_t lds = pool_lds(P, pel);
+                if (lds > 160 * 1024) {
+                    snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pool: %zu B of LDS per workgroup (max 160 KB)", lds);
+                    return -1;
+                }
+                const dim3 grid((b->nframes + P - 1) / P), block(64 * kPoolWaves);
+                if (pel == 1) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint8_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
+                                                 b->nframes, P, maxrows, lstride, lchroma, staged ? 1 : 0);
+                else hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint16_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
+                                        b->nframes, P, maxrows, lstride, lchroma, staged ? 1 : 0);
             }
-            const dim3 grid((b->nframes + P - 1) / P), block(64 * kPoolWaves);
-            if (p8) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint8_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
-                                       b->nframes, P, maxrows, lstride, lchroma);
-            if (p16) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint16_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
-                                        b->nframes, P, maxrows, lstride, lchroma);
         } else {
             if (pbytes > 160 * 1024) {
                 snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pic: %zu B of LDS per workgroup (max 160 KB)", pbytes);

@@ -209,8 +209,10 @@ struct Slot {
 };
 
 // stats slots (h2j_engine_stats): times in ms summed over chunks; ST_RECON is K1 only, ST_PREP is K0
+// ST_PARSE: submission -> last picture parsed (includes waiting behind the previous batch's parse);
+// ST_PARSE_RUN: first -> last picture parsed (the pool's time on this batch)
 enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
-       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_N };  // ST_PACK: host time packing records into staging
+       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_PARSE_RUN, ST_N };  // ST_PACK: host time packing records into staging
 
 // H.264 pictures with more MB rows than this are reconstructed by several K1 workgroups
 constexpr int kK1BandRows = 68;
@@ -240,7 +242,7 @@ struct Batch {
     int jobset = -1;                           // Engine::jobsets slot the batch parses into
     bool parsed = false, done = false;
     int rc = 0;
-    double t0 = 0, t_parsed = 0;
+    double t0 = 0, t_parse0 = 0, t_parsed = 0;
     // results handed to the caller by h2j_engine_wait (per ticket: a later batch that finishes
     // before this one is waited for does not overwrite them)
     double stats[ST_N] = {0};
@@ -676,6 +678,7 @@ void Engine::parse_loop() {
             b->jobset = jobset_busy[0] ? 1 : 0;
             jobset_busy[b->jobset] = true;
         }
+        b->t_parse0 = now_ms();
         std::vector<FrameJob>& jobs = jobsets[b->jobset];
         if (static_cast<int>(jobs.size()) < b->n) jobs.resize(static_cast<size_t>(b->n));
         // batches smaller than the thread pool (a lone IDecoder call): pictures with several
@@ -724,6 +727,7 @@ void Engine::drive_loop() {
         acv.wait(lk, [&] { return b->parsed; });  // a failed batch may still be parsing
         std::vector<FrameJob>* jobs = b->jobset >= 0 ? &jobsets[b->jobset] : nullptr;
         stats[ST_PARSE] = b->t_parsed > 0 ? b->t_parsed - b->t0 : 0;
+        stats[ST_PARSE_RUN] = b->t_parsed > 0 ? b->t_parsed - b->t_parse0 : 0;
         stats[ST_TOTAL] = now_ms() - b->t0;
         std::memcpy(b->stats, stats, sizeof(stats));
         b->chunk_log = chunk_log;
@@ -1075,7 +1079,7 @@ const char* h2j_engine_frame_error(h2j_engine* w, int i) {
     case 0: return "";
     case -50: return "output buffer too small";
     case -51: return "JPEG payload pool overflow";
-    case -52: return "device-side failure (K1 band hand-off timed out)";
+    case -52: return "device-side failure (a K1 / deblocking progress wait timed out)";
     default: return i < static_cast<int>(w->e.last_msg.size()) ? w->e.last_msg[i].c_str() : "";
     }
 }

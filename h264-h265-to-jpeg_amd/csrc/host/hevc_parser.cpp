@@ -954,9 +954,27 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             if (xs + 1 < sbw) prevCsbf |= csbf[xs + 1][ys];
             if (ys + 1 < sbw) prevCsbf |= csbf[xs][ys + 1] << 1;
             const uint8_t* sig = sigtab[prevCsbf][(xs | ys) ? 1 : 0];
-            // bins feed the mask arithmetically (no data-dependent branch per bin)
+            // bins feed the mask arithmetically (no data-dependent branch per bin).  Consecutive
+            // positions often share a context: the word of the previous bin's context stays in a
+            // register and is taken by a select when the next bin uses it again, and only the
+            // previous context's word is stored each bin -- a store and reload of the word the
+            // next bin needs would put store-to-load forwarding on the decision chain
             unsigned got = 0;
-            for (int nn = nstart; nn > 0; nn--) got |= static_cast<unsigned>(cc.decision(ctx[sig[nn]])) << nn;
+            if (nstart > 0) {
+                int pidx = sig[nstart];
+                CabacState pw = ctx[pidx];
+                got = static_cast<unsigned>(cc.decision(pw)) << nstart;
+                for (int nn = nstart - 1; nn > 0; nn--) {
+                    const int idx = sig[nn];
+                    const CabacState lw = ctx[idx];
+                    ctx[pidx] = pw;
+                    CabacState w = idx == pidx ? pw : lw;
+                    got |= static_cast<unsigned>(cc.decision(w)) << nn;
+                    pw = w;
+                    pidx = idx;
+                }
+                ctx[pidx] = pw;
+            }
             sigmask |= got;
             infer_dc = infer_dc && got == 0;
             if (nstart >= 0) {

@@ -72,10 +72,12 @@ int h2j_engine_decode(h2j_engine *e, const uint8_t *data, size_t size, int stage
  * info[0..3] = w, h, qscale, nmcu. */
 int h2j_engine_jpeg_coeffs(h2j_engine *e, const uint8_t *data, size_t size, int16_t *out, size_t cap_elems,
                            int *info);
-/* Timing of the last h2j_engine_transcode call, milliseconds:
- * [0] parse (host, wall)  [1] h2d  [2] recon  [3] deblock  [4] sao
+/* Timing of the batch the last h2j_engine_transcode / h2j_engine_wait returned, milliseconds:
+ * [0] parse (host, wall, from submission)  [1] h2d  [2] recon  [3] deblock  [4] sao
  * [5] jpeg (GPU)  [6] d2h  [7] huffman (host, wall)  [8] total (wall)
- * [9] frames  [10] algorithmic bytes of the GPU pixel path. */
+ * [9] frames  [10] algorithmic bytes of the GPU pixel path  [11] GPU entropy
+ * [12] K0 prep  [13] chunks  [14] record packing (host)  [15] parse (host, wall, first to last
+ * picture of the batch: without the wait behind the previous batch). */
 int h2j_engine_stats(h2j_engine *e, double *out, int n);
 /* Per chunk (one GPU launch of each stage) of the last h2j_engine_transcode, in order:
  * out[3i] pictures, out[3i+1] K1 ms, out[3i+2] K0..K5 ms (HIP events on the chunk's stream).

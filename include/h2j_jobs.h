@@ -130,7 +130,9 @@ typedef struct {
     uint32_t nbits;         /* payload bits before the 1-padding */
     uint32_t nbytes;        /* padded payload bytes (no 0xFF stuffing) */
     uint64_t seg_off;       /* byte offset of the payload in the segment pool */
-    uint32_t dev_error;     /* device-side failure flags (bit 0: K1 band hand-off timed out) */
+    uint32_t dev_error;     /* device-side failure flags: a progress wait timed out (bit 0 H.264 K1 band hand-off,
+                               1 H.264 deblocking band hand-off, 2 HEVC K1 row, 3 H.264 K1 row, 4 H.264
+                               deblocking row); the picture fails with status -52 */
     uint32_t pad_e;
 } h2j_jstat;
 

@@ -104,6 +104,21 @@ def test_bench_nosdh_1080p(engine):
             assert np.array_equal(g, q), (p, name)
 
 
+def test_high_entropy_tiles_both_emit_paths(engine):
+    """tiles over kEmitWords words take K5d's global-memory path beside LDS-path tiles
+    (tests/test_entropy_vectors.py proves the vectors straddle the limit); H2J_EMIT_GLOBAL=1 puts
+    every tile on the global path.  Every JPEG byte-exact against the oracle on both."""
+    paths = sorted(glob.glob(os.path.join(golden("entropy"), "*.h265")))
+    streams = [read(p) for p in paths] + [read(p) for p in PARITY[:6]] + [read(golden("img01.h265"))]
+    refs = [O.transcode(s) for s in streams]
+    assert engine.transcode(streams) == refs
+    os.environ["H2J_EMIT_GLOBAL"] = "1"
+    try:
+        assert engine.transcode(streams) == refs
+    finally:
+        del os.environ["H2J_EMIT_GLOBAL"]
+
+
 def test_invalid_inputs_fail_cleanly(engine):
     outs = engine.transcode([b"", b"\x00\x00\x01\x40garbage", read(golden("img01.h265"))[:1000]])
     assert outs[0] is None and outs[1] is None

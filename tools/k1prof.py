@@ -5,9 +5,7 @@ import ctypes, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "h264-h265-to-jpeg_amd")
 os.environ["H2J_LIB_DIR"] = os.path.join(PKG, "build", os.environ.get("H2J_PROF_VARIANT", "prof"))
-# the cycle counters are read from the per-picture K1 kernels (h2j_k1_recon_hevc_pic / _hevc<16>);
-# the -DH2J_PROF build of the picture-pool kernel does not finish, so the pool is switched off
-os.environ.setdefault("H2J_K1_POOL", "0")
+# the cycle counters cover every HEVC K1 kernel, the picture pool (default, H2J_K1_POOL=4) included
 sys.path.insert(0, PKG)
 import h2j
 files = [a for a in sys.argv[1:] if not a.isdigit()]
@@ -23,7 +21,10 @@ for path in files:
     hip.h2j_gpu_prof(buf, 16, 1)
     # K1PROF_ASYNC=1: through the asynchronous path (one chunk of up to 1024 pictures)
     outs = eng.transcode_async([[data] * n])[0] if os.environ.get("K1PROF_ASYNC") else eng.transcode([data] * n)
-    assert all(o is not None for o in outs)
+    bad = [i for i, o in enumerate(outs) if o is None]
+    if bad:
+        print(f"{len(bad)} pictures failed, e.g. {eng.frame_error(bad[0])!r}", flush=True)
+        sys.exit(1)
     print(f"batch done {time.time() - t0:.1f}s", flush=True)
     st = eng.stats()
     if hip.h2j_gpu_prof(buf, 16, 1) != 0:

@@ -17,6 +17,7 @@ reconstruction bit-for-bit.
   python tools/make_streams.py malformed -> tests/golden/malformed/ (out-of-range SPS / slice header values)
   python tools/make_streams.py heavy     -> tests/golden/bench_heavy/hevc1080h_XX.h265 (16 streams, ~100-250 KB)
 """
+import glob
 import json
 import os
 import subprocess
@@ -141,6 +142,29 @@ def nosdh(n=2):
         path = os.path.join(out_dir, f"hevc1080_nosdh_{i:02d}.h265")
         nb = encode(content, 1920, 1080, 8, qp, 500 + i, path, ["--sdh", "0"])
         print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+
+
+def entropy():
+    """High-entropy pictures for the JPEG payload emitter: 512x256 HEVC, QP 4, uniform
+    noise in 32 rows (the top rows, or rows 96..127) and flat grey elsewhere, so the noisy 256-block
+    tiles carry more than 32 JPEG bytes per block (K5d's global-memory path, kEmitWords) while the
+    flat tiles beside them stay on the LDS path (tests/test_entropy_vectors.py checks both)."""
+    out_dir = os.path.join(ROOT, "tests/golden/entropy")
+    os.makedirs(out_dir, exist_ok=True)
+    for f in glob.glob(os.path.join(out_dir, "*.h265")):
+        os.remove(f)
+    W, H = 512, 256
+    rng = np.random.default_rng(7)
+    for name, r0 in (("noise_top", 0), ("noise_mid", 96)):
+        y = np.full((H, W), 128, np.uint8)
+        u = np.full((H // 2, W // 2), 128, np.uint8)
+        v = u.copy()
+        y[r0:r0 + 32] = rng.integers(0, 256, (32, W))
+        u[r0 // 2:r0 // 2 + 16] = rng.integers(0, 256, (16, W // 2))
+        v[r0 // 2:r0 // 2 + 16] = rng.integers(0, 256, (16, W // 2))
+        path = os.path.join(out_dir, f"{name}_512x256_q4.h265")
+        nb = encode([y.astype(np.int32), u.astype(np.int32), v.astype(np.int32)], W, H, 8, 4, 7, path)
+        print(f"{path}: {nb} B", flush=True)
 
 
 PARITY = [
@@ -363,4 +387,4 @@ if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
-     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh}[what]()
+     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy}[what]()
