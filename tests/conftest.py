@@ -15,6 +15,24 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
+def _first_diff(a, b):
+    return next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
+
+
+def pytest_assertrepr_compare(op, left, right):
+    """Short reports for JPEG / plane byte comparisons: pytest's default diff of two 100 KB byte
+    strings (or lists of them) runs for minutes and turns a mismatch into a test timeout."""
+    if op != "==":
+        return None
+    if isinstance(left, (bytes, bytearray)) and isinstance(right, (bytes, bytearray)):
+        return [f"bytes differ: {len(left)} vs {len(right)} B, first difference at offset {_first_diff(left, right)}"]
+    if isinstance(left, (list, tuple)) and isinstance(right, (list, tuple)) and any(
+            isinstance(v, (bytes, bytearray)) for v in list(left) + list(right)):
+        bad = [i for i, (x, y) in enumerate(zip(left, right)) if x != y]
+        return [f"sequences differ: lengths {len(left)} vs {len(right)}, unequal items {bad[:16]}"]
+    return None
+
+
 def golden(name: str) -> str:
     return os.path.join(GOLDEN, name)
 

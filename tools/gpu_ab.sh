@@ -10,7 +10,7 @@ for wl in ${WLS:-hevc1080}; do
     for v in A B; do
       if [ $v = A ]; then D=$PKG; else D=$PKG/${B_DIR:-build/ab}; fi
       out=gpurun_out/ab_${wl}_${v}_$rep
-      H2J_LIB_DIR=$D timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o stats -- python3 bench.py --workload $wl --steps 2 --warmup 1 --no-cpu-baseline --no-single-call > $out.log 2>&1
+      H2J_LIB_DIR=$D timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o stats -- python3 bench.py --workload $wl --steps 2 --warmup 1 --no-cpu-baseline --no-single-call --no-aim > $out.log 2>&1
       f=$(find $out -name "*kernel_stats.csv" | head -1)
       python3 - "$f" "$wl $v$rep" <<'PY'
 import csv, re, sys

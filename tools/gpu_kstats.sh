@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 WL=${1:-avc1080}
 TAG=${2:-kstats}
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_$WL -o stats -- python3 bench.py --workload $WL --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_${WL}.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_$WL -o stats -- python3 bench.py --workload $WL --steps 1 --warmup 1 --no-cpu-baseline --no-aim > gpurun_out/${TAG}_${WL}.log 2>&1
 f=$(find gpurun_out/${TAG}_$WL -name "*kernel_stats.csv" | head -1)
 python3 -c "
 import csv,sys

@@ -12,7 +12,7 @@ rm -rf gpurun_out/pmck_1 gpurun_out/pmck_2
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmck_$i -o pmc -- python3 bench.py --workload $WL --steps 1 --warmup 0 --no-cpu-baseline --no-single-call > gpurun_out/pmck_$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmck_$i -o pmc -- python3 bench.py --workload $WL --steps 1 --warmup 0 --no-cpu-baseline --no-single-call --no-aim > gpurun_out/pmck_$i.log 2>&1
 done
 python3 - <<'PY'
 import csv, glob, collections
