@@ -536,27 +536,11 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     int nsig = 0;
     bool last_found = false;
     if (cat == 5) {
-        // consecutive positions often share a significance context (kSig8x8): the previous one's
-        // word stays in a register and is taken by a select when it repeats, and only the
-        // previous context is stored each bin (a store and reload of the word the next bin needs
-        // would put store-to-load forwarding on the decision chain)
-        CabacState* const sctx = ctx + 402;
-        int pidx = kSig8x8[0];
-        CabacState pw = sctx[pidx];
-        for (int i = 0; i < max_num - 1; i++) {
-            const int idx = kSig8x8[i];
-            const CabacState lw = sctx[idx];
-            sctx[pidx] = pw;
-            CabacState w = idx == pidx ? pw : lw;
-            const int sig = cc.decision(w);
-            pw = w;
-            pidx = idx;
-            if (sig) {
+        for (int i = 0; i < max_num - 1; i++)
+            if (cc.decision(ctx[402 + kSig8x8[i]])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
                 if (cc.decision(ctx[417 + kLast8x8[i]])) { last_found = true; break; }
             }
-        }
-        sctx[pidx] = pw;
     } else if (cat == 3) {
         for (int i = 0; i < max_num - 1; i++) {
             const int inc = i < 2 ? i : 2;

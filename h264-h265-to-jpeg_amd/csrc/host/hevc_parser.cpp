@@ -900,9 +900,27 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         shift = log2n - 2;
     }
     const int maxp = (log2n << 1) - 1;
-    int lx = 0, ly = 0;
-    while (lx < maxp && cc.decision(ctx[C_LAST_X + off + (lx >> shift)])) lx++;
-    while (ly < maxp && cc.decision(ctx[C_LAST_Y + off + (ly >> shift)])) ly++;
+    // unary prefixes; bins k >> shift share a context (the word forwarded in a register, as in
+    // the significance loop below)
+    auto last_prefix = [&](CabacState* lc) __attribute__((always_inline)) {
+        int k = 0, pk = 0;
+        CabacState pw = lc[0];
+        while (k < maxp) {
+            const int ci = k >> shift;
+            const CabacState lw = lc[ci];
+            lc[pk] = pw;
+            CabacState w = ci == pk ? pw : lw;
+            const int b = cc.decision(w);
+            pw = w;
+            pk = ci;
+            if (!b) break;
+            k++;
+        }
+        lc[pk] = pw;
+        return k;
+    };
+    int lx = last_prefix(ctx + C_LAST_X + off);
+    int ly = last_prefix(ctx + C_LAST_Y + off);
     if (lx > 3) {
         int nb = (lx >> 1) - 1;
         lx = (1 << nb) * (2 + (lx & 1)) + static_cast<int>(cc.bypass_bits(nb));
@@ -994,14 +1012,32 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         int numG1 = 0, lastG1 = -1;
         const int lastSig = 31 - __builtin_clz(sigmask), firstSig = __builtin_ctz(sigmask);
         CabacState* const g1c = gt1ctx + ctxSet * 4;
-        for (unsigned m = sigmask; m && numG1 < 8; numG1++) {
-            const int nn = 31 - __builtin_clz(m);
-            m &= ~(1u << nn);
-            const unsigned d = static_cast<unsigned>(cc.decision(g1c[greater1_ctx]));
-            g1mask |= d << nn;
-            // greater1Ctx: 0 once a bin was 1, else 1 -> 2 -> 3 (saturating), as a mask select
-            const int inc = greater1_ctx + ((greater1_ctx > 0) & (greater1_ctx < 3));
-            greater1_ctx = inc & (static_cast<int>(d) - 1);
+        {
+            // greater1Ctx runs 1, 2, 3, 3, ... until a bin is 1 and is 0 from then on, so the
+            // context of bin k is known before bin k - 1 resolves except for that one switch:
+            // the four words stay in registers (a load indexed by the previous outcome, plus a
+            // store / reload when the context repeats, sat on the decision chain)
+            CabacState w0 = g1c[0], w1 = g1c[1], w2 = g1c[2], w3 = g1c[3];
+            unsigned seen = 0, m = sigmask;
+            auto bin = [&](CabacState& slot) __attribute__((always_inline)) {
+                const int nn = 31 - __builtin_clz(m);
+                m &= ~(1u << nn);
+                CabacState w = seen ? w0 : slot;
+                const unsigned d = static_cast<unsigned>(cc.decision(w));
+                if (seen) w0 = w;
+                else slot = w;
+                seen |= d;
+                g1mask |= d << nn;
+                numG1++;
+            };
+            if (m) bin(w1);
+            if (m) bin(w2);
+            while (m && numG1 < 8) bin(w3);
+            g1c[0] = w0;
+            g1c[1] = w1;
+            g1c[2] = w2;
+            g1c[3] = w3;
+            greater1_ctx = seen ? 0 : 1;  // only "== 0" matters (ctxSet of the next sub-block)
         }
         if (g1mask) lastG1 = 31 - __builtin_clz(g1mask);
         const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
