@@ -396,6 +396,19 @@ struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
     int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo;
     uint32_t sl;
 };
+// Sample (x, y) of component c in the tiled HEVC residual planes (h2j_res_q, include/h2j_gpu.h);
+// rows of a tile are 1 << h2j_res_q(log2ctb, c) elements apart.
+DEVI int16_t* hevc_res_at(int16_t* res, int width, int height, int log2ctb, int c, int x, int y) {
+    const int q = h2j_res_q(log2ctb, c), qm = (1 << q) - 1;
+    const int wc = c ? width >> 1 : width;
+    long long base = 0;
+    if (c) {
+        base = h2j_res_plane(width, height, h2j_res_q(log2ctb, 0));
+        if (c == 2) base += h2j_res_plane(width >> 1, height >> 1, q);
+    }
+    const long long tile = static_cast<long long>(y >> q) * h2j_res_tiles(wc, q) + (x >> q);
+    return res + base + (tile << (2 * q)) + ((y & qm) << q) + (x & qm);
+}
 DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
                         int16_t* R, int rst, K0LdsHevc& s) {
     const int lane = threadIdx.x;
@@ -434,7 +447,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
         for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
     }
     wave_sync();
-    for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    for (int i = lane; i < nn; i += 64) R[(i >> log2n) * rst + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
     wave_sync();
 }
 
@@ -447,7 +460,7 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
 // Transform-skip and bypass TBs are not batched (hevc_residual).
 template <int LOG2N>
 DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
-                              const uint8_t* sl, int16_t* res, int st0, int st1, int off1, int off2, K0LdsHevc& s) {
+                              const uint8_t* sl, int16_t* res, K0LdsHevc& s) {
     constexpr int N = 1 << LOG2N, NN = N * N;
     constexpr int P = N + 2, NP = N * P;  // tmp row stride (int16): odd dword stride across lanes
     const int lane = threadIdx.x;
@@ -565,7 +578,7 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
         pass(mxx, [&](int ps) { return tmp32[(g * NP + q * P) / 2 + ps]; }, acc);
         const int bdS = 20 - (mine.c ? f.bdc : f.bd);
         const int c = mine.c;
-        int16_t* R = res + (c == 0 ? 0 : (c == 1 ? off1 : off2)) + (mine.y + q) * (c ? st1 : st0) + mine.x;
+        int16_t* R = hevc_res_at(res, f.width, f.height, f.log2ctb, c, mine.x, mine.y) + (q << h2j_res_q(f.log2ctb, c));
         uint32_t packed[N / 2];
 #pragma unroll
         for (int i = 0; i < N / 2; i++) {
@@ -1152,9 +1165,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
             }
             continue;
         }
-        int16_t* R = res + offc;
-        if constexpr (HEVC) hevc_residual(f, tu, CO, co0, sl, R, stc, s);
-        else h264_residual(f, tu, CO, co0, sl, R, stc, s);
+        if constexpr (HEVC)  // R: the TB's origin in its tile, rows 1 << h2j_res_q apart
+            hevc_residual(f, tu, CO, co0, sl, hevc_res_at(res, f.width, f.height, f.log2ctb, c, x0, y0),
+                          1 << h2j_res_q(f.log2ctb, c), s);
+        else h264_residual(f, tu, CO, co0, sl, res + offc, stc, s);
     }
     if constexpr (!HEVC) {  // H.264 luma 4x4 / 8x8 residuals, 16 / 8 same-size TBs per pass
 #pragma unroll
@@ -1211,10 +1225,10 @@ __global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const
                     cnt++;
                 }
                 switch (l2) {
-                    case 2: hevc_residual_group<2>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
-                    case 3: hevc_residual_group<3>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
-                    case 4: hevc_residual_group<4>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
-                    default: hevc_residual_group<5>(f, rec, gm, cnt, CO, sl, res, st0, st1, off1, off2, s); break;
+                    case 2: hevc_residual_group<2>(f, rec, gm, cnt, CO, sl, res, s); break;
+                    case 3: hevc_residual_group<3>(f, rec, gm, cnt, CO, sl, res, s); break;
+                    case 4: hevc_residual_group<4>(f, rec, gm, cnt, CO, sl, res, s); break;
+                    default: hevc_residual_group<5>(f, rec, gm, cnt, CO, sl, res, s); break;
                 }
             }
         }
@@ -1249,8 +1263,6 @@ DEVI void lds_dma4(const void* g, uint32_t lds) {
                  : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 }
 DEVI void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// 16 zero bytes per lane: the source of LDS-DMA lanes that fall outside a plane
-__device__ uint4 g_zero_src[64];
 DEVI void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 DEVI uint32_t lds_addr(const void* p) {
     return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
@@ -1712,14 +1724,13 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
 struct FU {
     int width, height, log2ctb, ctb_w, ctb_h, bd, bdc, strong, sty, stc;
     uint8_t* pic;     // plane 0 base (bytes); planes 1/2 at off1/off2 elements
-    int16_t* res;     // residual plane 0; planes 1/2 at the same element offsets
+    int16_t* res;     // residual planes, tiled by quadrant (hevc_res_at)
     int off1, off2;
     uint32_t* derr;   // the picture's h2j_jstat.dev_error
     DEVI int st(int c) const { return c ? stc : sty; }
     DEVI int off(int c) const { return c == 0 ? 0 : (c == 1 ? off1 : off2); }
     template <typename Pel>
     DEVI Pel* plane(int c) const { return reinterpret_cast<Pel*>(pic) + off(c); }
-    DEVI const int16_t* rplane(int c) const { return res + off(c); }
 };
 DEVI FU make_fu(const h2j_frame& f, uint8_t* arena) {
     FU u;
@@ -2040,58 +2051,23 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
 }
 
 // K0 residual of one quadrant -> a quadrant window in LDS by LDS-DMA (no registers held while
-// it is in flight; the register prefetch it replaces spilled to scratch at this kernel's VGPR
-// budget).  Luma: 2 x 16 B per lane, row-major Qc x Qc; chroma: 4 B per lane, Cb at element 0
-// and Cr at 256, Qc x Qc each.  Lanes outside the picture write zeros instead.
+// it is in flight).  The residual planes are tiled by quadrant (h2j_res_q): the quadrant is one
+// contiguous tile, copied in 16-B pieces (luma: Qc x Qc row-major; chroma: Cb at element 0 and
+// Cr at 256, Qc x Qc each).  Tiles past the picture's right / bottom edge exist in full (samples
+// there are never used), so no lane needs a bounds test.
 DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* body, int lane) {
-    // lanes outside the picture copy 16 / 4 zero bytes from g_zero_src instead of branching
-    // around the copy (the branch kept an address live across an exec-mask change: a scratch
-    // spill store + reload per quadrant at this kernel's register budget)
-    const char* zero = reinterpret_cast<const char*>(g_zero_src);
-#ifdef H2J_DMA_BRANCH  // r02 form (A/B builds only): lanes outside the plane branch around the copy
+    const int chunks = (Qc * Qc) >> 3;  // 16-B pieces of one plane's tile
     if (grp == 0) {
-        const int16_t* R = u.rplane(0);
-        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;
+        const int16_t* R = hevc_res_at(u.res, u.width, u.height, u.log2ctb, 0, X0, Y0);
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-            const int idx = lane + 64 * j, yy = idx >> lc, xx = (idx & ((1 << lc) - 1)) * 8;
-            const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
-            if (ok) lds_dma16(R + (Y0 + yy) * u.sty + X0 + xx, lds_addr(body + 512 * j));
-            else *reinterpret_cast<uint4*>(body + idx * 8) = make_uint4(0, 0, 0, 0);
+            if (64 * j < chunks && lane + 64 * j < chunks) lds_dma16(R + (lane + 64 * j) * 8, lds_addr(body + 512 * j));
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int lq = __builtin_ctz(static_cast<unsigned>(Qc));
-            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e >> lq, xx = e & (Qc - 1);
-            const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
-            int16_t* dst = body + c * 256 + (k & 1) * 128;
-            if (ok) lds_dma4(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx, lds_addr(dst));
-            else *reinterpret_cast<uint32_t*>(dst + lane * 2) = 0u;
-        }
-    }
-    return;
-#endif
-    if (grp == 0) {
-        const int16_t* R = u.rplane(0);
-        const int lc = __builtin_ctz(static_cast<unsigned>(Qc)) - 3;  // log2 of 16-B chunks per row
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int idx = lane + 64 * j, yy = idx >> lc, xx = (idx & ((1 << lc) - 1)) * 8;
-            const bool ok = yy < Qc && Y0 + yy < u.height && X0 + xx < u.width;
-            const void* src = ok ? static_cast<const void*>(R + (Y0 + yy) * u.sty + X0 + xx) : static_cast<const void*>(zero);
-            lds_dma16(src, lds_addr(body + 512 * j));
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {  // (plane, half): 64 lanes x 2 samples
-            const int lq = __builtin_ctz(static_cast<unsigned>(Qc));
-            const int c = k >> 1, e = (k & 1) * 128 + lane * 2, yy = e >> lq, xx = e & (Qc - 1);
-            const bool ok = yy < Qc && Y0 + yy < (u.height >> 1) && X0 + xx < (u.width >> 1);
-            int16_t* dst = body + c * 256 + (k & 1) * 128;
-            const void* src = ok ? static_cast<const void*>(u.rplane(1 + c) + (Y0 + yy) * u.stc + X0 + xx)
-                                 : static_cast<const void*>(zero);
-            lds_dma4(src, lds_addr(dst));
+        for (int c = 0; c < 2; c++) {
+            const int16_t* R = hevc_res_at(u.res, u.width, u.height, u.log2ctb, 1 + c, X0, Y0);
+            if (lane < chunks) lds_dma16(R + lane * 8, lds_addr(body + 256 * c));
         }
     }
 }

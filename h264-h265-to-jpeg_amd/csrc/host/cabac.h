@@ -26,10 +26,7 @@ extern const uint8_t kCabacLpsByState[128][8];
 typedef uint64_t CabacState;
 // word of each state, and the word after an MPS / LPS bin
 extern const uint64_t kCabacWord[128];
-// ceil(2^44 / r) for r = 256..511 (index r - 256): the bypass quotient floor(v / range) of a
-// dividend v < 2^33 as a multiply and a shift (exact: v * (ceil - 2^44 / r) < 2^42 keeps the
-// rounding below one unit)
-extern const uint64_t kCabacInvRange[256];
+
 extern const uint64_t kCabacNextMpsW[128];
 extern const uint64_t kCabacNextLpsW[128];
 
@@ -119,7 +116,7 @@ public:
         if (bits_ < k) refill();
         const int sh = bits_ - k;
         const uint64_t v = value_ >> sh;
-        const uint32_t q = quotient(v);
+        const uint32_t q = static_cast<uint32_t>(v / range_);
         value_ -= (static_cast<uint64_t>(q) * range_) << sh;
         bits_ = sh;
         return q;
@@ -127,7 +124,7 @@ public:
     // The next k (1..24) bypass bins without consuming them (MSB first) ...
     inline uint32_t bypass_peek(int k) {
         if (bits_ < k) refill();
-        return quotient(value_ >> (bits_ - k));
+        return static_cast<uint32_t>((value_ >> (bits_ - k)) / range_);
     }
     // ... and consuming the first n of them, whose value (the top n bits of the peek) is top:
     // the quotient's leading bits are the quotient of the truncated dividend
@@ -164,10 +161,6 @@ public:
     const uint8_t* aligned_pos() const { return cur_ - (bits_ >> 3); }
 
 private:
-    // floor(v / range_) for v < range_ << 24 (the bypass dividends)
-    inline uint32_t quotient(uint64_t v) const {
-        return static_cast<uint32_t>((static_cast<unsigned __int128>(v) * kCabacInvRange[range_ - 256]) >> 44);
-    }
     void refill() {
         uint32_t w;
         if (end_ - cur_ >= 4) {

@@ -420,8 +420,13 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     for (int k = 0; k < nf; k++) {
         h2j_frame& f = s.frames[k];
         const size_t ysz = static_cast<size_t>(f.width) * f.height;
+        // HEVC residual planes are tiled by K1 quadrant (include/h2j_gpu.h h2j_res_elems: whole
+        // tiles, a little more than the picture); H.264 keeps the picture's raster layout
+        const size_t res_elems = f.codec == H2J_CODEC_HEVC
+                                     ? static_cast<size_t>(h2j_res_elems(f.width, f.height, f.log2ctb))
+                                     : ysz + ysz / 2;
         f.res = off;
-        off = align_up(off + (ysz + ysz / 2) * 2, 256);
+        off = align_up(off + res_elems * 2, 256);
         f.aux = off;
         off = align_up(off + static_cast<size_t>(f.ntu) * 8, 256);
         if (f.k1bands > 1) {  // per band boundary: K1 1 luma + 2 chroma rows, K2 4 luma + 2x2 chroma rows (uint16)

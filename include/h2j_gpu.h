@@ -51,6 +51,21 @@ int h2j_gpu_event_record(void *ev, void *stream);
 float h2j_gpu_event_elapsed_ms(void *start, void *stop);
 const char *h2j_gpu_last_error(void);
 
+#ifdef __cplusplus
+/* HEVC residual planes (K0 writes, K1 reads) in quadrant tiles: each component in tiles of
+ * 2^q x 2^q int16 samples (q = the K1 quadrant size: min(log2ctb, 5) for luma, one less for
+ * chroma), tiles in raster order, planes Y, Cb, Cr back to back.  A K1 quadrant is then one
+ * contiguous tile (2 KB luma, 512 B per chroma plane) and every TB lies inside one tile.
+ * (constexpr: host and device code share it) */
+constexpr int h2j_res_q(int log2ctb, int c) { return (log2ctb < 5 ? log2ctb : 5) - (c ? 1 : 0); }
+constexpr long long h2j_res_tiles(int n, int q) { return (n + (1 << q) - 1) >> q; }
+constexpr long long h2j_res_plane(int w, int h, int q) { return (h2j_res_tiles(w, q) * h2j_res_tiles(h, q)) << (2 * q); }
+/* int16 elements of the three tiled planes of a w x h 4:2:0 picture */
+constexpr long long h2j_res_elems(int w, int h, int log2ctb) {
+    return h2j_res_plane(w, h, h2j_res_q(log2ctb, 0)) + 2 * h2j_res_plane(w / 2, h / 2, h2j_res_q(log2ctb, 1));
+}
+#endif
+
 /* JPEG symbol stream (production path): per frame, one tile of H2J_JTILE_BYTES per 256 blocks
  * at h2j_frame.jcoef (the dense int16 plane occupies the same region on the inspection path). */
 #define H2J_JSYM_MAX 68

@@ -101,7 +101,8 @@ typedef struct {
     uint64_t maps;                  /* per-4x4 deblocking maps: flags (u8) then qp (i8) */
     uint64_t jcoef;                 /* JPEG coefficients int16 [mcu][6][64] */
     uint64_t jstat;                 /* JPEG per-frame stats (h2j_jstat) */
-    uint64_t res;                   /* int16 residual planes (K0 -> K1), pic geometry */
+    uint64_t res;                   /* int16 residual planes (K0 -> K1): HEVC tiled by K1 quadrant
+                                       (h2j_res_q in h2j_gpu.h), H.264 the picture's raster layout */
     uint64_t aux;                   /* K0 -> K1: uint64 reference-availability mask per TU */
     uint64_t ctbrng;                /* K0 -> K1: uint32 [first, end) TU range per CTB (zeroed) */
     int32_t pic_stride[3];          /* elements */
