@@ -15,6 +15,9 @@ INC = os.path.join(ROOT, "include")
 def _declared(header):
     src = open(os.path.join(INC, header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    # inline constexpr helpers (C++ only, header-defined) are not exports
+    src = re.sub(r"^constexpr[^\n]*\{[^\n]*\}[^\n]*$", "", src, flags=re.M)
+    src = re.sub(r"^constexpr[^\n]*\{\n.*?^\}", "", src, flags=re.S | re.M)
     return sorted(set(re.findall(r"\b(h2j_[a-z0-9_]+)\s*\(", src)))
 
 

@@ -35,6 +35,14 @@ for path in files:
     tot = sum(v[0:4]) + sum(v[8:16])
     ntu, nctb = v[5], v[6]
     print(f"{os.path.basename(path)}: {n} frames, K1 {st['recon_ms']:.2f} ms, TUs {ntu}, CTBs {nctb}")
+    if path.endswith((".h264", ".264")):
+        # H.264: the counters are the K2 deblock wave's (h264_db_rows), per macroblock
+        names = ["wait", "window", "params", "store"]
+        for i, nm in enumerate(names):
+            print(f"  {nm:8s} {v[i] / max(1, nctb):10.0f} cyc/MB  {100 * v[i] / tot:5.1f}%")
+        for k, nm in ((0, "V edges"), (4, "H edges")):
+            print(f"  {nm:8s} {v[8 + k] / max(1, nctb):10.0f} cyc/MB  {100 * v[8 + k] / tot:5.1f}%")
+        continue
     names = ["wait", "setup", "-", "store"]
     for i, nm in enumerate(names):
         if i != 2:
