@@ -4199,8 +4199,12 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
     const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + sizeof(DbTables) + 12 * static_cast<size_t>(b->max_w);
     static bool attr = false;
     if (!attr) {  // line buffers of pictures wider than ~3.6K need more than the 64 KB default
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(h2j_k2_deblock264),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        // (160 KB minus the kernel's static LDS: the -DH2J_PROF build adds its counters there)
+        const void* fn = reinterpret_cast<const void*>(h2j_k2_deblock264);
+        hipFuncAttributes fa{};
+        const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(160 * 1024 - st));
+        (void)hipGetLastError();
         attr = true;
     }
     if (b->k1wgs <= 0) return 0;
