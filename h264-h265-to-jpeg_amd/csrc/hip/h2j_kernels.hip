@@ -3260,6 +3260,427 @@ __global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_
     else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line, band, nbands, TB);
 }
 
+// ---- H.264 K2, two macroblock rows per wave (fill the wave).  A workgroup of
+// kDbPairWaves waves deblocks a picture (or a 16-row band of a tall one); wave w takes the row
+// pairs (2p, 2p + 1), p = w, w + kDbPairWaves, ...: lanes 0-31 (half 0) walk row 2p, lanes 32-63
+// (half 1) walk row 2p + 1 kDbLag MBs behind.  h264_db_rows left lanes 32-63 idle through the
+// line filter (32 lines per MB: 16 luma, 8 + 8 chroma); here they filter the second row's MB in
+// the same instructions, and the data movement around the filter moves each MB with 32 lanes
+// instead of 64 (the same instructions per MB).  Dependencies are those of h264_db_rows: MB
+// (x, y) needs row y - 1 finished through MB x + 1 -- inside a wave by the lag (half 0 has
+// finished x + kDbLag MBs when half 1 starts MB x), across waves by the progress word of row
+// 2p - 1.  The halves share the picture's line buffer: at one step they touch disjoint MB
+// columns of it (half 0 columns s - 1 and s, half 1 columns s - 3 and s - 2).  Pictures wider
+// than the LDS line buffer allows (line_w) keep it in global memory, in the picture's residual
+// region (K1's input, dead once K1 has run).
+constexpr int kDbPairWaves = 8;
+constexpr int kDbLag = 2;
+constexpr int kDbPairSlots = 4 * kDbPairWaves;  // progress words: 2 rows in flight per wave, twice over
+static_assert(sizeof(h2j_slice) == 12 && offsetof(h2j_slice, slice_addr_rs) == 8 &&
+                  offsetof(h2j_slice, deblock_disabled) == 5 && offsetof(h2j_slice, cqp_offset) == 6,
+              "slice dwords assumed by h264_db_pairs");
+template <typename Pel>
+struct DbPrefetch2 {  // one MB per half: 8 luma + 4 chroma samples per lane, as loaded
+    typename std::conditional<sizeof(Pel) == 1, uint2, uint4>::type y;
+    typename std::conditional<sizeof(Pel) == 1, uint32_t, uint2>::type c;
+};
+template <typename Pel>
+DEVI void db264_fetch2(const Pel* PY, const Pel* const* PC, int sty, int stc, int mx, int my, DbPrefetch2<Pel>& r, int hl) {
+    using TY = decltype(r.y);
+    using TC = decltype(r.c);
+    r.y = *reinterpret_cast<const TY*>(PY + (my * 16 + (hl >> 1)) * sty + mx * 16 + (hl & 1) * 8);
+    const int k = hl & 15;
+    r.c = *reinterpret_cast<const TC*>(PC[hl >> 4] + (my * 8 + (k >> 1)) * stc + mx * 8 + (k & 1) * 4);
+}
+// 4 uint16 window samples (two dwords) as 4 Pel of the picture / staging
+DEVI uint32_t db_pk8(uint2 v) { return __builtin_amdgcn_perm(v.y, v.x, 0x06040200u); }
+template <typename Pel>
+DEVI void db_st4(Pel* d, uint2 v) {
+    if constexpr (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = db_pk8(v);
+    else *reinterpret_cast<uint2*>(d) = v;
+}
+template <typename Pel>
+DEVI void db_st8(Pel* d, uint2 a, uint2 b) {
+    if constexpr (sizeof(Pel) == 1) *reinterpret_cast<uint2*>(d) = make_uint2(db_pk8(a), db_pk8(b));
+    else *reinterpret_cast<uint4*>(d) = make_uint4(a.x, a.y, b.x, b.y);
+}
+DEVI uint2 db_ld4a8(const uint16_t* p) { return *reinterpret_cast<const uint2*>(p); }  // 8-byte aligned
+DEVI uint2 db_ld4a4(const uint16_t* p) {                                              // 4-byte aligned
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    return make_uint2(q[0], q[1]);
+}
+DEVI uint32_t db_u16pair(const uint16_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+DEVI void db_put_u16pair(uint16_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+
+template <typename Pel, bool GLine>
+DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
+                        uint32_t* prog, uint16_t* line, int band, int nbands, const DbTables& TB) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, hl = lane & 31;
+    DbWin& w = W[2 * wv + h];
+    const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
+    const int bd = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
+    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
+    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
+    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
+    uint16_t* LY = line;              // [4][width]: rows 12..15 of the MB row above
+    uint16_t* LC = line + 4 * width;  // [2 comps][2 rows][width / 2]: chroma rows 6..7
+    const int cw = width >> 1;
+    const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
+    const int npairs = (rend - rbeg + 1) >> 1;
+    const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
+    if (wv >= npairs) return;
+    PROF_DECL;
+    // filter lanes of a half: 0-15 luma lines, 16-23 Cb, 24-31 Cr
+    const bool luma_lane = hl < 16, chroma = !luma_lane;
+    const int cc = (hl >> 3) & 1, ck = hl & 7;
+    const int maxv = chroma ? (1 << bdc) - 1 : (1 << bd) - 1;
+    const int tsh = chroma ? bdc - 8 : bd - 8, clo = -6 * (bdc - 8);
+    DbPrefetch2<Pel> pf;
+    uint32_t ninfo = 0;
+    {
+        const int r = rbeg + 2 * wv + h;
+        if (r < rend) {
+            db264_fetch2<Pel>(PY, PC, sty, stc, 0, r, pf, hl);
+            ninfo = db264_info_raw(mbs, mbw, 0, r, hl);
+        }
+    }
+    int lmf = 0, lqp = 0, lsaddr = -1;  // left neighbour (previous MB of the half's row)
+    for (int p = wv; p < npairs; p += kDbPairWaves) {
+        const int r0 = rbeg + 2 * p;
+        const bool two = r0 + 1 < rend;
+        const int row = r0 + h;
+        const bool hv = h == 0 || two;
+        const int nsteps = two ? mbw + kDbLag : mbw;
+        const bool from_band = nbands > 1 && band > 0 && p == 0;  // half 0's row is the band's first
+        const bool fb = from_band && h == 0;
+        const bool to_band = nbands > 1 && band < nbands - 1 && row == rend - 1;
+        const uint64_t o_xin = o_xl + 12ull * (band - 1) * width, o_xout = o_xl + 12ull * band * width;
+        uint32_t* above = prog + (r0 + kDbPairSlots - 1) % kDbPairSlots;  // row r0 - 1
+        uint32_t* mine = prog + (r0 + 1) % kDbPairSlots;                  // row r0 + 1 (half 1)
+        uint32_t seen = 0;
+        for (int s = 0; s < nsteps; s++) {
+            const int mx = s - kDbLag * h;
+            const bool live = hv && mx >= 0 && mx < mbw;
+            // half 0's MB s needs row r0 - 1 through MB s + 1 (half 1's row is covered by the lag)
+            if (s < mbw) {
+                if (from_band) {
+                    const uint32_t need = static_cast<uint32_t>(mbw + min(s + 2, mbw));
+                    if (seen < need) {
+                        uint32_t it = 0;
+                        uint32_t* fl = reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * ((r0 - 1) * mbw);
+                        while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+                            __builtin_amdgcn_s_sleep(2);
+                            if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
+                                if (lane == 0) __hip_atomic_fetch_or(dev_error_word(arena, f), kDevErrDbBand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                seen = 2u * mbw;
+                                break;
+                            }
+                        }
+                    }
+                } else if (r0 > rbeg || (r0 > 0 && nbands <= 1)) {
+                    const uint32_t need = (static_cast<uint32_t>(r0) << 16) | static_cast<uint32_t>(min(s + 2, mbw));
+                    if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrDbRow264);
+                }
+            }
+            PROF_LAP(0);
+            if (live) {
+                // window: the MB body (prefetched), the rows above (line buffer), left columns carried
+                {
+                    uint16_t* d = &w.y[(hl >> 1) + 4][(hl & 1) * 8 + 4];  // 8-byte aligned
+                    if constexpr (sizeof(Pel) == 1) {
+                        *reinterpret_cast<uint2*>(d) = make_uint2(__builtin_amdgcn_perm(0u, pf.y.x, 0x0c010c00u), __builtin_amdgcn_perm(0u, pf.y.x, 0x0c030c02u));
+                        *reinterpret_cast<uint2*>(d + 4) = make_uint2(__builtin_amdgcn_perm(0u, pf.y.y, 0x0c010c00u), __builtin_amdgcn_perm(0u, pf.y.y, 0x0c030c02u));
+                    } else {
+                        *reinterpret_cast<uint2*>(d) = make_uint2(pf.y.x, pf.y.y);
+                        *reinterpret_cast<uint2*>(d + 4) = make_uint2(pf.y.z, pf.y.w);
+                    }
+                    const int k = hl & 15;
+                    uint16_t* e = &w.c[hl >> 4][(k >> 1) + 2][(k & 1) * 4 + 2];  // 4-byte aligned
+                    if constexpr (sizeof(Pel) == 1) {
+                        db_put_u16pair(e, __builtin_amdgcn_perm(0u, pf.c, 0x0c010c00u));
+                        db_put_u16pair(e + 2, __builtin_amdgcn_perm(0u, pf.c, 0x0c030c02u));
+                    } else {
+                        db_put_u16pair(e, pf.c.x);
+                        db_put_u16pair(e + 2, pf.c.y);
+                    }
+                }
+                if (fb) {
+                    const uint16_t* X = reinterpret_cast<const uint16_t*>(arena + o_xin);
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int e = hl * 2 + j, tr = e >> 4, tc = e & 15;
+                        w.y[tr][tc + 4] = __hip_atomic_load(X + tr * width + mx * 16 + tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;
+                    w.c[c2][cr][k2 + 2] = __hip_atomic_load(X + 4 * width + (c2 * 2 + cr) * cw + mx * 8 + k2,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (row > 0) {
+                    const int tr = hl >> 3, tc = (hl & 7) * 2;  // 4 rows x 16 luma columns, 2 per lane
+                    db_put_u16pair(&w.y[tr][tc + 4], db_u16pair(LY + tr * width + mx * 16 + tc));
+                    const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // 2 comps x 2 rows x 8 columns
+                    w.c[c2][cr][k2 + 2] = LC[(c2 * 2 + cr) * cw + mx * 8 + k2];
+                }
+                // prefetch the half's next MB (its next row: two pairs on)
+                int nx = mx + 1, ny = row;
+                if (nx == mbw) { nx = 0; ny += 2 * kDbPairWaves; }
+                if (ny < mbh) db264_fetch2<Pel>(PY, PC, sty, stc, nx, ny, pf, hl);
+            }
+            wave_sync();
+            PROF_LAP(1);
+            const uint32_t cur = ninfo;
+            if (live) {  // parameters of the half's next MB
+                int nx = mx + 1, ny = row;
+                if (nx == mbw) { nx = 0; ny += 2 * kDbPairWaves; }
+                if (ny < mbh) ninfo = db264_info_raw(mbs, mbw, nx, ny, hl);
+            }
+            auto pick = [&](int k) __attribute__((always_inline)) {
+                const uint32_t a = __builtin_amdgcn_readlane(cur, k), b = __builtin_amdgcn_readlane(cur, 32 + k);
+                return h ? b : a;
+            };
+            const uint32_t i0 = pick(0), i1 = pick(1), i2 = pick(2), i3 = pick(3);
+            const int mf = static_cast<int>((i1 >> 8) & 0xFF), mqp = static_cast<int8_t>(i1 & 0xFF);
+            const int csl = static_cast<int>((i0 >> 8) & 0xFF), tsl = static_cast<int>((i2 >> 8) & 0xFF);
+            const int tmf = row > 0 ? static_cast<int>((i3 >> 8) & 0xFF) : 0, tqp = static_cast<int8_t>(i3 & 0xFF);
+            // the slice's dwords {beta, tc, sao, sao}, {lf, dd, cqp0, cqp1}, {first MB}
+            uint32_t s0, s1, s2, ts2 = ~0u;
+            const uint32_t* TBS = reinterpret_cast<const uint32_t*>(TB.sl);
+            const uint32_t* GS = reinterpret_cast<const uint32_t*>(slices);
+            if (csl < kDbSlices) { s0 = TBS[3 * csl]; s1 = TBS[3 * csl + 1]; s2 = TBS[3 * csl + 2]; }
+            else { s0 = GS[3 * csl]; s1 = GS[3 * csl + 1]; s2 = GS[3 * csl + 2]; }
+            if (row > 0) ts2 = tsl < kDbSlices ? TBS[3 * tsl + 2] : GS[3 * tsl + 2];
+            const int dd = static_cast<int>((s1 >> 8) & 0xFF);
+            const int beo = static_cast<int8_t>(s0 & 0xFF), tco = static_cast<int8_t>((s0 >> 8) & 0xFF);
+            const int cq0 = static_cast<int8_t>((s1 >> 16) & 0xFF), cq1 = static_cast<int8_t>(s1 >> 24);
+            const int saddr = static_cast<int>(s2), tsaddr = static_cast<int>(ts2);
+            PROF_LAP(2);
+            if (live && (mf & 4) && dd != 1) {
+                // thresholds of the lane's component, per lane (no cross-lane traffic): the left and
+                // top MB edges and the internal edges (8.7.2.2; chroma QPs through Table 8-15)
+                const int qm = (mf & 1) ? 0 : mqp, ql = (lmf & 1) ? 0 : lqp, qt = (tmf & 1) ? 0 : tqp;
+                const int off = cc ? cq1 : cq0;
+                auto cqp = [&](int q) __attribute__((always_inline)) {
+                    const int a = clip3(clo, 51, q + off);
+                    const int m = a < 30 ? a : TB.cqp[max(a - 30, 0)];
+                    return chroma ? m : q;
+                };
+                const int qmc = cqp(qm), qlc = cqp(ql), qtc = cqp(qt);
+                const int qaL = (qlc + qmc + 1) >> 1, qaT = (qtc + qmc + 1) >> 1;
+                const int iaL = clip3(0, 51, qaL + tco), ibL = clip3(0, 51, qaL + beo);
+                const int iaT = clip3(0, 51, qaT + tco), ibT = clip3(0, 51, qaT + beo);
+                const int iaI = clip3(0, 51, qmc + tco), ibI = clip3(0, 51, qmc + beo);
+                const int aL = TB.alpha[iaL] << tsh, bL = TB.beta[ibL] << tsh;
+                const int aT = TB.alpha[iaT] << tsh, bT = TB.beta[ibT] << tsh;
+                const int aI = TB.alpha[iaI] << tsh, bI = TB.beta[ibI] << tsh, tI = TB.tc0[iaI] << tsh;
+                const bool t8 = (mf & 2) != 0;
+                for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
+                    const bool vert = dir == 0;
+                    const int nmf = vert ? (mx > 0 ? lmf : 0) : tmf;
+                    bool mb_edge = (nmf & 4) != 0;
+                    if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
+                    const int aM = vert ? aL : aT, bM = vert ? bL : bT;
+                    // the line of this lane, as in h264_db_rows (chroma at v[2..11])
+                    const int stp = vert ? 1 : (luma_lane ? 20 : 10);
+                    const uint16_t* base = luma_lane ? (vert ? &w.y[hl + 4][0] : &w.y[0][hl + 4])
+                                                     : (vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2]) - 2 * stp;
+                    int v[20];
+#pragma unroll
+                    for (int i = 0; i < 20; i++) v[i] = base[i * stp];
+                    h264_filt_line<4>(v, mb_edge, 4, aM, bM, 0, maxv, chroma);
+                    h264_filt_line<8>(v, chroma || !t8, 3, aI, bI, tI, maxv, chroma);
+                    h264_filt_line<12>(v, luma_lane, 3, aI, bI, tI, maxv, chroma);
+                    h264_filt_line<16>(v, luma_lane && !t8, 3, aI, bI, tI, maxv, chroma);
+                    uint16_t* dst = const_cast<uint16_t*>(base);
+#pragma unroll
+                    for (int i = 1; i < 19; i++)
+                        if (luma_lane || (i >= 3 && i <= 8)) dst[i * stp] = static_cast<uint16_t>(v[i]);
+                    wave_sync();
+                    PROF_LAPK(dir * 4);
+                }
+            }
+            if (live) {
+                lmf = mf;
+                lqp = mqp;
+                lsaddr = saddr;
+                // write back (the rules of h264_db_rows): rows 12..15 of MB (x, y - 1), rows of
+                // MB (x - 1, y), and on the row's last MB its own rows; staged 4 MBs wide
+                const bool last_row = row == mbh - 1, last = mx == mbw - 1;
+                const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
+                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][64] | chroma [2][2][32]
+                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][64] | chroma [2][8][32]
+                if (row > 0) {
+                    if (hl < 16) {
+                        const int tr = hl >> 2, c4 = (hl & 3) * 4;
+                        db_st4<Pel>(SA + tr * 64 + (mx & 3) * 16 + c4, db_ld4a8(&w.y[tr][c4 + 4]));
+                    } else if (hl < 24) {  // chroma rows 6..7
+                        const int k = hl - 16, c2 = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
+                        db_st4<Pel>(SA + 256 + (c2 * 2 + cr) * 32 + (mx & 3) * 8 + c4, db_ld4a4(&w.c[c2][cr][c4 + 2]));
+                    }
+                    if ((mx & 3) == 3 || last) {  // the group's rows 12..15 out
+                        wave_sync();
+                        const int g0 = mx & ~3, nmb = mx - g0 + 1;
+                        const int tr = hl >> 3, sg = hl & 7;  // luma: 4 rows x 8 segments of 8
+                        if (sg < 2 * nmb) db264_copy<Pel, 8>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * 8, SA + tr * 64 + sg * 8);
+                        const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;  // chroma: 2 x 2 rows x 8 segments of 4
+                        if (cs < 2 * nmb)
+                            db264_copy<Pel, 4>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * 4, SA + 256 + (c2 * 2 + cr) * 32 + cs * 4);
+                    }
+                }
+                auto flush_b = [&](int g0, int nmb) __attribute__((always_inline)) {
+                    wave_sync();
+                    const int r = hl >> 1, sp = (hl & 1) * 2;  // luma: 16 rows x 2 x 2 segments of 16
+                    if (r < nr) {
+                        if (sp < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sp * 16, SB + r * 64 + sp * 16);
+                        if (sp + 1 < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sp * 16 + 16, SB + r * 64 + sp * 16 + 16);
+                    }
+                    const int c2 = hl >> 4, cr = (hl >> 1) & 7;  // chroma: 2 comps x 8 rows x 2 x 2 segments of 8
+                    if (cr < ncr) {
+                        Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8 + sp * 8;
+                        const Pel* q = SB + 1024 + (c2 * 8 + cr) * 32 + sp * 8;
+                        if (sp < nmb) db264_copy<Pel, 8>(d, q);
+                        if (sp + 1 < nmb) db264_copy<Pel, 8>(d + 8, q + 8);
+                    }
+                };
+                if (mx > 0) {  // the previous MB: columns 0..11 saved in py, 12..15 in the window
+                    const int sx = ((mx - 1) & 3) * 16;
+                    {
+                        const int r = hl >> 1, c8 = (hl & 1) * 8;
+                        if (r < nr) {
+                            const uint2 a = db_ld4a8(&w.py[r][c8]);
+                            const uint2 b = c8 ? db_ld4a8(&w.y[r + 4][0]) : db_ld4a8(&w.py[r][4]);
+                            db_st8<Pel>(SB + r * 64 + sx + c8, a, b);
+                        }
+                    }
+                    {
+                        const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
+                        if (cr < ncr) {  // chroma column 7 sits in the window
+                            uint2 a = db_ld4a8(&w.pc[c2][cr][c4]);
+                            if (c4) a.y = (a.y & 0xFFFFu) | (static_cast<uint32_t>(w.c[c2][cr + 2][1]) << 16);
+                            db_st4<Pel>(SB + 1024 + (c2 * 8 + cr) * 32 + (sx >> 1) + c4, a);
+                        }
+                    }
+                    if (((mx - 1) & 3) == 3) flush_b(mx - 4, 4);
+                }
+                // this MB's columns 0..11 / chroma 0..7 wait for the next MB (in-order LDS)
+                {
+                    const int r = hl >> 1, c6 = (hl & 1) * 6;
+#pragma unroll
+                    for (int k = 0; k < 6; k += 2) db_put_u16pair(&w.py[r][c6 + k], db_u16pair(&w.y[r + 4][c6 + k + 4]));
+                    const int c2 = hl >> 4, cr = (hl >> 1) & 7, c4 = (hl & 1) * 4;
+                    *reinterpret_cast<uint2*>(&w.pc[c2][cr][c4]) = db_ld4a4(&w.c[c2][cr + 2][c4 + 2]);
+                }
+                if (last) {  // the row's last MB: its rows are final now
+                    const int sx = (mx & 3) * 16;
+                    {
+                        const int r = hl >> 1, c8 = (hl & 1) * 8;
+                        if (r < nr) db_st8<Pel>(SB + r * 64 + sx + c8, db_ld4a8(&w.y[r + 4][c8 + 4]), db_ld4a8(&w.y[r + 4][c8 + 8]));
+                    }
+                    {
+                        const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
+                        if (cr < ncr) db_st4<Pel>(SB + 1024 + (c2 * 8 + cr) * 32 + (sx >> 1) + c4, db_ld4a4(&w.c[c2][cr + 2][c4 + 2]));
+                    }
+                    flush_b(mx & ~3, (mx & 3) + 1);
+                }
+                // line buffer for the row below: the MB's bottom rows (columns final so far) and the
+                // previous MB's last columns, which this MB's left edge has just finished
+                if (to_band) {  // into the boundary buffer of the band below
+                    uint16_t* X = reinterpret_cast<uint16_t*>(arena + o_xout);
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int e = hl + 32 * j, tr = e >> 4, tc = e & 15;
+                        if (tc < 12 || last)
+                            __hip_atomic_store(X + tr * width + mx * 16 + tc, w.y[tr + 16][tc + 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (mx > 0 && hl < 16) {
+                        const int tr = hl >> 2, tc = hl & 3;
+                        __hip_atomic_store(X + tr * width + mx * 16 - 4 + tc, w.y[tr + 16][tc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    {
+                        const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;
+                        uint16_t* XC = X + 4 * width + (c2 * 2 + cr) * cw + mx * 8;
+                        if (k2 < 6 || last)
+                            __hip_atomic_store(XC + k2, w.c[c2][cr + 8][k2 + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (mx > 0 && k2 < 2)
+                            __hip_atomic_store(XC - 2 + k2, w.c[c2][cr + 8][k2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): picture and boundary stores have completed
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (hl == 0)
+                        __hip_atomic_store(reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * (row * mbw),
+                                           static_cast<uint32_t>(mbw + mx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (row + 1 < mbh) {
+                    {
+                        const int tr = hl >> 3, tc = (hl & 7) * 2;  // rows 12..15 of this MB, 2 per lane
+                        if (tc < 12 || last) db_put_u16pair(LY + tr * width + mx * 16 + tc, db_u16pair(&w.y[tr + 16][tc + 4]));
+                    }
+                    if (mx > 0 && hl < 8) {
+                        const int tr = hl >> 1, tc = (hl & 1) * 2;
+                        db_put_u16pair(LY + tr * width + mx * 16 - 4 + tc, db_u16pair(&w.y[tr + 16][tc]));
+                    }
+                    const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // chroma rows 6..7
+                    if (k2 < 6 || last) LC[(c2 * 2 + cr) * cw + mx * 8 + k2] = w.c[c2][cr + 8][k2 + 2];
+                    if (mx > 0 && k2 < 2) LC[(c2 * 2 + cr) * cw + mx * 8 - 2 + k2] = w.c[c2][cr + 8][k2];
+                }
+                wave_sync();
+                {  // carry the last columns into the next MB's left strip
+                    const int r = hl >> 1, k2 = (hl & 1) * 2;
+                    db_put_u16pair(&w.y[r + 4][k2], db_u16pair(&w.y[r + 4][k2 + 16]));
+                    const int c2 = hl >> 4, r2 = (hl >> 1) & 7, k = hl & 1;
+                    w.c[c2][r2 + 2][k] = w.c[c2][r2 + 2][k + 8];
+                }
+                if constexpr (GLine) __builtin_amdgcn_s_waitcnt(0x0F70);  // global line buffer stores done
+                wave_sync();
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0 && two && s >= kDbLag)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(r0) + 2) << 16) | static_cast<uint32_t>(s - kDbLag + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            PROF_LAP(3);
+            PROF_ADD(6, 1 + (two && s >= kDbLag && s - kDbLag < mbw ? 1 : 0) - (s < mbw ? 0 : 1));
+        }
+    }
+    PROF_FLUSH();
+}
+
+// line_w: the widest picture whose line buffer the launch's LDS holds (wider: global memory)
+__global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                                      const h2j_slice* slices, uint8_t* arena,
+                                                                      const uint32_t* map, int line_w) {
+    // LDS: windows (two per wave) | progress | tables | line buffer (h2j_gpu_deblock)
+    extern __shared__ __align__(16) uint8_t dblds[];
+    DbWin* W = reinterpret_cast<DbWin*>(dblds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * 2 * kDbPairWaves);
+    DbTables& TB = *reinterpret_cast<DbTables*>(dblds + sizeof(DbWin) * 2 * kDbPairWaves + kDbPairSlots * 4);
+    uint16_t* line = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(&TB) + sizeof(DbTables));
+    const uint32_t me = map[blockIdx.x];  // same (picture, band) map as K1
+    const h2j_frame& f = frames[me >> 8];
+    const int band = static_cast<int>(me & 0xFF);
+    if (f.codec != H2J_CODEC_H264) return;
+    const int nbands = ufl(f.k1bands);
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    const int t = threadIdx.x;
+    if (t < kDbPairSlots) prog[t] = 0;
+    if (t < 52) {
+        TB.alpha[t] = kAlpha264[t];
+        TB.beta[t] = kBeta264[t];
+        TB.tc0[t] = kTc0_264[t][2];
+    }
+    if (t < 22) TB.cqp[t] = kChromaQp264[t];
+    const int nsl = min(static_cast<int>(ufl(f.nslice)), kDbSlices);
+    if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
+        reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
+    __syncthreads();
+    if (ufl(f.width) <= line_w) {
+        if (f.bit_depth == 8) h264_db_pairs<uint8_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
+        else h264_db_pairs<uint16_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
+    } else {  // one line buffer per band in the picture's residual region (12 bytes per column)
+        uint16_t* gl = reinterpret_cast<uint16_t*>(arena + ufl64(f.res)) + static_cast<size_t>(band) * 6 * ufl(f.width);
+        if (f.bit_depth == 8) h264_db_pairs<uint8_t, true>(f, C, S, arena, W, prog, gl, band, nbands, TB);
+        else h264_db_pairs<uint16_t, true>(f, C, S, arena, W, prog, gl, band, nbands, TB);
+    }
+}
+
 // ---------------------------------------------------------------- K3: SAO
 // K3 SAO (H.265 8.7.3): one 256-thread workgroup per CTB, all three components.  Every load of
 // the CTB is issued before the first LDS write (the deblocked samples of Y, Cb and Cr plus a
@@ -3276,7 +3697,16 @@ struct SaoLds {
     int16_t c[2][34 * kSaoTsC];
     uint8_t keep[256];  // per 4x4 luma block of the CTB: pcm / transquant bypass with loop filters off
     uint32_t nbm;       // usable neighbour CTBs (sao_stage_store)
+    unsigned long long var[16];  // K4a's per-MB sums of the CTB's final luma: (sum << 32) | sum of squares
 };
+
+// K4a's macroblock variances (the JPEG rate control input) are summed by K3 from the SAO output
+// it holds in registers, when the output's 16x16 MB grid is aligned with the CTB grid; K4a then
+// skips the picture (one full read of the final picture less).
+DEVI bool sao_sums_variance(const h2j_frame& f, int fold) {
+    return fold && f.codec == H2J_CODEC_HEVC && f.pic2 != f.pic && (f.crop_x & 15) == 0 && (f.crop_y & 15) == 0 &&
+           (f.out_w & 15) == 0;
+}
 
 template <typename Pel>
 DEVI uint2 sao_load4(const Pel* p) {  // 4 samples -> 4 int16 halves of a uint2
@@ -3358,7 +3788,7 @@ DEVI void sao_stage_mask(const SaoGeo& g, int16_t* T, uint32_t nbm) {
 // filter component c (uniform: its SAO parameters sit in scalar registers)
 template <typename Pel>
 DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c, const h2j_ctb& cc, bool on,
-                     const int16_t* T, const SaoLds& L) {
+                     const int16_t* T, const SaoLds& L, unsigned long long* vacc = nullptr) {
     const int tid = threadIdx.x;
     Pel* D = plane<Pel>(f, arena, f.pic2, c);
     const int st = f.pic_stride[c];
@@ -3423,6 +3853,24 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
             o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
         }
         }
+        if (vacc) {  // luma of a sao_sums_variance picture: K4a's sums, per MB of the CTB
+            // output rows below the picture repeat its last row (jpeg_sample), so that row counts
+            // for them too; rows / columns outside the output count 0
+            const int oy = g.y0 + y - f.crop_y, ox = g.x0 + x - f.crop_x, last = f.out_h - 1;
+            const unsigned wgt = (oy < 0 || ox >= f.out_w) ? 0u : (oy < last ? 1u : (oy == last ? 16u - (last & 15) : 0u));
+            if (wgt) {
+                unsigned s4 = 0, n4 = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const unsigned u = bd > 8 ? min(static_cast<unsigned>(o[k] + (1 << (bd - 9))) >> (bd - 8), 255u)
+                                              : static_cast<unsigned>(o[k]);
+                    s4 += u;
+                    n4 += u * u;
+                }
+                atomicAdd(&vacc[((y >> 4) << (f.log2ctb - 4)) + (x >> 4)],
+                          (static_cast<unsigned long long>(s4 * wgt) << 32) | (n4 * wgt));
+            }
+        }
         Pel* d = D + (g.y0 + y) * st + g.x0 + x;
         if (sizeof(Pel) == 1) {
             *reinterpret_cast<uint32_t*>(d) = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 8) |
@@ -3475,7 +3923,7 @@ DEVI bool sao_nb_ok(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, i
 
 // one CTB (Y, Cb, Cr) per workgroup
 template <typename Pel>
-DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, int ctb, SaoLds& L) {
+DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, int ctb, SaoLds& L, int fold) {
     const int tid = threadIdx.x;
     const int cx = ctb % f.ctb_w, row = ctb / f.ctb_w;
     const h2j_ctb cc = uload(C + ctb);
@@ -3497,6 +3945,8 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
     sao_stage_store(gb, L.c[0], R.ib, R.bb);
     sao_stage_store(gr, L.c[1], R.ir, R.br);
     L.keep[tid] = R.kf;
+    const bool var = sao_sums_variance(f, fold);
+    if (tid < 16) L.var[tid] = 0;
     __syncthreads();
     const uint32_t nbm = L.nbm;
     if (nbm != 0x1FFu) {
@@ -3506,9 +3956,30 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
         __syncthreads();
     }
     // 3. filter and store, one component at a time
-    sao_filter<Pel>(f, arena, gy, 0, cc, onY, L.y, L);
+    sao_filter<Pel>(f, arena, gy, 0, cc, onY, L.y, L, var ? L.var : nullptr);
     sao_filter<Pel>(f, arena, gb, 1, cc, onCb, L.c[0], L);
     sao_filter<Pel>(f, arena, gr, 2, cc, onCr, L.c[1], L);
+    if (var) {  // the CTB's MBs inside the output: K4a's formula, one atomic per CTB
+        __syncthreads();
+        if (tid < 64) {
+            const int l2m = f.log2ctb - 4;
+            unsigned long long t = 0;
+            if (tid < (1 << (2 * l2m))) {
+                const int oy0 = gy.y0 - f.crop_y + ((tid >> l2m) << 4), ox0 = gy.x0 - f.crop_x + ((tid & ((1 << l2m) - 1)) << 4);
+                if (oy0 >= 0 && oy0 < f.out_h && ox0 < f.out_w) {
+                    const unsigned long long a = L.var[tid];
+                    const unsigned sm = static_cast<unsigned>(a >> 32), n = static_cast<unsigned>(a);
+                    t = (n - ((sm * sm) >> 8) + 500 + 128) >> 8;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+            if (tid == 0 && t) {
+                h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&js->var_sum), t);
+            }
+        }
+    }
 }
 
 // grid (CTBs of the largest picture at the smallest CTB size, pictures)
@@ -3517,7 +3988,8 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
 // 4.18 -> 3.53 ms)
 __global__ void __launch_bounds__(256, 8) h2j_k3_sao(const h2j_frame* __restrict__ frames,
                                                  const h2j_ctb* __restrict__ ctbs,
-                                                 const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena) {
+                                                 const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena,
+                                                 int fold) {
     const GridPos gp = xcd_grid_pos();
     __shared__ SaoLds L;
     const h2j_frame& f = frames[gp.y];
@@ -3526,8 +3998,8 @@ __global__ void __launch_bounds__(256, 8) h2j_k3_sao(const h2j_frame* __restrict
     if (ctb >= f.ctb_w * f.ctb_h) return;
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
-    if (f.bit_depth == 8) sao_ctb<uint8_t>(f, C, S, arena, ctb, L);
-    else sao_ctb<uint16_t>(f, C, S, arena, ctb, L);
+    if (f.bit_depth == 8) sao_ctb<uint8_t>(f, C, S, arena, ctb, L, fold);
+    else sao_ctb<uint16_t>(f, C, S, arena, ctb, L, fold);
 }
 
 // ---------------------------------------------------------------- K4: JPEG
@@ -3557,8 +4029,9 @@ DEVI unsigned row16_sum(unsigned x) {  // inclusive prefix over each 16-lane row
     x += static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
     return x;
 }
-__global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restrict__ frames, uint8_t* __restrict__ arena) {
+__global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restrict__ frames, uint8_t* __restrict__ arena, int fold) {
     const h2j_frame& f = frames[blockIdx.y];
+    if (sao_sums_variance(f, fold)) return;  // K3 has summed this picture's MB variances
     const int mbw = (f.out_w + 15) >> 4, mbh = (f.out_h + 15) >> 4;
     const int mb = blockIdx.x * 16 + static_cast<int>(threadIdx.x >> 4), r = threadIdx.x & 15;
     unsigned s = 0, n = 0;
@@ -4196,21 +4669,44 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         if (r) return r;
     }
     if (!b->has_h264) return 0;
-    const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + sizeof(DbTables) + 12 * static_cast<size_t>(b->max_w);
-    static bool attr = false;
-    if (!attr) {  // line buffers of pictures wider than ~3.6K need more than the 64 KB default
-        // (160 KB minus the kernel's static LDS: the -DH2J_PROF build adds its counters there)
-        const void* fn = reinterpret_cast<const void*>(h2j_k2_deblock264);
-        hipFuncAttributes fa{};
-        const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(160 * 1024 - st));
+    // H2J_DB264=rows: one MB row per wave (h2j_k2_deblock264, A/B timing); default two
+    static const bool rows = [] {
+        const char* e = std::getenv("H2J_DB264");
+        return e && std::strcmp(e, "rows") == 0;
+    }();
+    static size_t cap[2] = {0, 0};  // dynamic LDS limit per kernel: 160 KB minus its static LDS
+    if (!cap[0]) {  // (line buffers of pictures wider than ~3.6K need more than the 64 KB default)
+        const void* fns[2] = {reinterpret_cast<const void*>(h2j_k2_deblock264), reinterpret_cast<const void*>(h2j_k2_deblock264p)};
+        for (int i = 0; i < 2; i++) {
+            hipFuncAttributes fa{};
+            const size_t st = hipFuncGetAttributes(&fa, fns[i]) == hipSuccess ? fa.sharedSizeBytes : 0;
+            cap[i] = 160 * 1024 - st;
+            (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(cap[i]));
+        }
         (void)hipGetLastError();
-        attr = true;
     }
     if (b->k1wgs <= 0) return 0;
-    hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->k1wgs), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
-                       b->slices, b->arena, b->k1map);
-    return check(hipGetLastError(), "h2j_k2_deblock264");
+    if (rows) {
+        const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + sizeof(DbTables) + 12 * static_cast<size_t>(b->max_w);
+        hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->k1wgs), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
+                           b->slices, b->arena, b->k1map);
+        return check(hipGetLastError(), "h2j_k2_deblock264");
+    }
+    const size_t fixed = sizeof(DbWin) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
+    const int line_w = std::min(b->max_w, static_cast<int>((cap[1] - fixed) / 12) & ~15);
+    hipLaunchKernelGGL(h2j_k2_deblock264p, dim3(b->k1wgs), dim3(64 * kDbPairWaves), fixed + 12 * static_cast<size_t>(line_w), s,
+                       b->frames, b->ctbs, b->slices, b->arena, b->k1map, line_w);
+    return check(hipGetLastError(), "h2j_k2_deblock264p");
+}
+
+// H2J_SAO_VAR=0: K4a sums every picture's MB variances (A/B timing); default K3 sums them for
+// the pictures sao_sums_variance admits
+static int sao_var_fold() {
+    static const int v = [] {
+        const char* e = std::getenv("H2J_SAO_VAR");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v;
 }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
@@ -4218,7 +4714,7 @@ int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     // CTB grid of the largest picture at the smallest CTB size present is bounded by max_ctbs
     dim3 grid(static_cast<unsigned>(b->max_ctbs), b->nframes);
-    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena);
+    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, sao_var_fold());
     return check(hipGetLastError(), "h2j_k3_sao");
 }
 
@@ -4226,7 +4722,7 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int mbs = b->max_mcu;
-    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena);
+    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena, sao_var_fold());
     int r = check(hipGetLastError(), "h2j_k4a_variance");
     if (r) return r;
     hipLaunchKernelGGL(h2j_k4b_ratecontrol, dim3(b->nframes), dim3(64), 0, s, b->frames, b->arena);

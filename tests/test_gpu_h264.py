@@ -37,13 +37,15 @@ import glob
 import os
 
 H264_DIR = golden("h264")
-PARITY264 = sorted(glob.glob(os.path.join(H264_DIR, "*.h264")))
+# h264wide: wider than the deblocking kernel's LDS line buffer (global line buffer path)
+PARITY264 = sorted(glob.glob(os.path.join(H264_DIR, "*.h264"))) + sorted(glob.glob(os.path.join(golden("h264wide"), "*.h264")))
 
 
 @pytest.mark.parametrize("path", PARITY264, ids=[os.path.basename(p) for p in PARITY264])
 def test_h264_parity_vectors(engine, path):
     """h264gen vectors: Main/High/High10, I8x8, PCM, slices, QP deltas,
-    chroma QP offsets, deblocking offsets and disable_deblocking_filter_idc."""
+    chroma QP offsets, deblocking offsets and disable_deblocking_filter_idc; 6144- and
+    8192-wide pictures."""
     s = read(path)
     for stage, skip in ((1, True), (0, False)):
         gy, gu, gv, bd = engine.decode(s, stage=stage)

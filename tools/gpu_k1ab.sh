@@ -18,7 +18,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 def short(n):
     n = n.split('(')[0]
     return re.sub(r'^.*::', '', n).replace('h2j_', '')
-print(sys.argv[2], ' '.join('%s=%.3f' % (short(r['Name']), float(r['AverageNs']) / 1e6) for r in rows[:8]))
+print(sys.argv[2], ' '.join('%s=%.3f' % (short(r['Name']), float(r['AverageNs']) / 1e6) for r in rows[:12]))
 PY
     done
   done

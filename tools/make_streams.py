@@ -11,6 +11,7 @@ reconstruction bit-for-bit.
   python tools/make_streams.py parity  -> tests/golden/hevc/*.h265 + manifest.json
   python tools/make_streams.py 4k      -> tests/golden/bench4k/hevc2160_10b_XX.h265
   python tools/make_streams.py parity264 -> tests/golden/h264/*.h264 + manifest.json (tools/h264gen)
+  python tools/make_streams.py wide264   -> tests/golden/h264wide/*.h264 (line buffer in global memory)
   python tools/make_streams.py bench264  -> tests/golden/bench264/avc1080_XX.h264 (16 streams, High 8x8)
   python tools/make_streams.py mixed     -> tests/golden/mixed/ (720p H.265/H.264, 4K H.264) for configs[4]
   python tools/make_streams.py f3        -> tests/golden/f3/ (decoder delay, non-IDR / CRA / BLA first pictures)
@@ -371,6 +372,29 @@ def malformed():
     json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
 
 
+WIDE264 = [
+    # pictures wider than the H.264 deblocking kernel's LDS line buffer holds (~5.9K): the
+    # line buffer then lives in global memory (h2j_k2_deblock264p, GLine)
+    ("w01_8192x48_wide", 8192, 48, 8, 28, 53, 3, ["--slices", "2"]),
+    ("w02_6144x32_wide_10bit", 6144, 32, 10, 24, 54, 2, ["--t8x8", "0"]),
+]
+
+
+def wide264():
+    out_dir = os.path.join(ROOT, "tests/golden/h264wide")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    manifest = []
+    for name, W, H, bd, qp, seed, sigma, opts in WIDE264:
+        up = -(-W // planes[0].shape[1])
+        content = make_content(planes, W, H, seed, sigma, bd, upsample=up)
+        path = os.path.join(out_dir, name + ".h264")
+        nb = encode(content, W, H, bd, qp, seed, path, opts, codec=264)
+        manifest.append({"file": name + ".h264", "w": W, "h": H, "bit_depth": bd, "qp": qp, "options": opts})
+        print(f"{path}: {nb} B", flush=True)
+    json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
 def fourk(n=4):
     out_dir = os.path.join(ROOT, "tests/golden/bench4k")
     os.makedirs(out_dir, exist_ok=True)
@@ -387,4 +411,5 @@ if __name__ == "__main__":
     build_gen()
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
-     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy}[what]()
+     "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy,
+     "wide264": wide264}[what]()
