@@ -16,8 +16,8 @@ for wl in ${WLS:-hevc1080}; do
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 def short(n):
-    n = n.split('(')[0]
-    return re.sub(r'^.*::', '', n).replace('h2j_', '')
+    n = re.sub(r'^void ', '', n.replace('(anonymous namespace)::', ''))
+    return re.sub(r'^.*::', '', n.split('(')[0]).replace('h2j_', '')
 print(sys.argv[2], ' '.join('%s=%.3f' % (short(r['Name']), float(r['AverageNs']) / 1e6) for r in rows[:12]))
 PY
     done
