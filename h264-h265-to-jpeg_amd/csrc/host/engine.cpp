@@ -442,14 +442,31 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const size_t o_ctbs = align_up(o_coefs + ncoef * sizeof(h2j_coef), 256);
     const size_t o_slices = align_up(o_ctbs + nctb * sizeof(h2j_ctb), 256);
     const size_t o_sl = align_up(o_slices + nslice * sizeof(h2j_slice), 256);
-    // H.264 K1 workgroup map: banded pictures first (their long chains start early), bands in order
+    static const bool balance = [] {  // H2J_K1_BALANCE=0: H.264 K1 workgroups in frame order (A/B timing)
+        const char* e = std::getenv("H2J_K1_BALANCE");
+        return !(e && e[0] == '0');
+    }();
+    // H.264 K1 workgroup map: banded pictures first (their long chains start early), bands in order,
+    // then the others by transform-block count, most first (the dispatcher hands workgroups out in
+    // map order: the heaviest pictures start in the first round, not in the launch's tail)
     std::vector<uint32_t> k1map;
-    for (int pass = 0; pass < 2; pass++)
+    for (int k = 0; k < nf; k++) {
+        const h2j_frame& f = s.frames[k];
+        if (f.codec != H2J_CODEC_H264 || f.k1bands <= 1) continue;
+        for (int bnd = 0; bnd < f.k1bands; bnd++) k1map.push_back((static_cast<uint32_t>(k) << 8) | bnd);
+    }
+    {
+        std::vector<std::pair<uint32_t, uint32_t>> un;
         for (int k = 0; k < nf; k++) {
             const h2j_frame& f = s.frames[k];
-            if (f.codec != H2J_CODEC_H264 || (f.k1bands > 1) != (pass == 0)) continue;
-            for (int bnd = 0; bnd < f.k1bands; bnd++) k1map.push_back((static_cast<uint32_t>(k) << 8) | bnd);
+            if (f.codec == H2J_CODEC_H264 && f.k1bands <= 1) un.emplace_back(f.ntu, static_cast<uint32_t>(k));
         }
+        if (balance)
+            std::stable_sort(un.begin(), un.end(), [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
+                return a.first > b.first;
+            });
+        for (const auto& x : un) k1map.push_back(x.second << 8);
+    }
     // mixed-batch K1 map (h2j_k1_recon_any): every HEVC picture and H.264 band, tallest first so
     // the longest chains start first; bands of one picture stay in order
     std::vector<uint32_t> k1all;

@@ -16,6 +16,9 @@
 #include "bitstream.h"
 #include "cabac.h"
 #include "job.h"
+#ifdef H2J_SAMPLE
+#include "sampler.h"
+#endif
 
 #ifdef H2J_CABAC_COUNT
 namespace h2j {
@@ -24,6 +27,9 @@ thread_local unsigned long long g_bins_ctx = 0, g_bins_byp = 0;
 #endif
 
 int main(int argc, char** argv) {
+#ifdef H2J_SAMPLE
+    h2j_sample::start();
+#endif
     if (argc < 2) {
         std::fprintf(stderr, "usage: parse_bench file... [-r reps] [-t threads] [-d (output digest)]\n");
         return 2;
