@@ -1960,16 +1960,23 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         // horizontal: main = left column (refH(k) = R[2n - k], k < 0 projected from the top row)
         const int sgn = vert ? 1 : -1;
         const bool bnd = edge && (mode == 26 || mode == 10);
+        // the main reference extended to negative positions once per TB (8.4.4.2.6: ref[k] for
+        // k < 0 projects onto the side reference through invAngle), M[n + k] for k = -n .. 2n + 1, in
+        // the reference array R is not: the sample loop then reads two entries with no projection
+        int16_t* M = filt ? s.sub : s.ref;
+        for (int k = lane; k < 3 * n + 2; k += 64) {
+            const int kk = k - n;
+            const int o = kk >= 0 ? kk : -((m24(kk, inv) + 128) >> 8);
+            // (entry 2n + 1 is only ever read with weight 0 -- clamped into R)
+            M[k] = R[clip3(0, 4 * n, 2 * n + sgn * o)];
+        }
+        wave_sync();
         for (int i = lane; i < nn; i += 64) {
             const int x = i & (n - 1), y = i >> log2n;
             const int a = vert ? y : x, b = vert ? x : y;  // a: distance from the main reference, b: position along it
             const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
-            const int k1 = b + idx + 1, k2 = k1 + 1;
-            // negative k projects onto the side reference through invAngle; both forms are
-            // computed and selected (no divergent branch)
-            const int o1 = k1 >= 0 ? k1 : -((m24(k1, inv) + 128) >> 8);
-            const int o2 = k2 >= 0 ? k2 : -((m24(k2, inv) + 128) >> 8);
-            int pv = (m24(32 - fr, R[2 * n + (vert ? o1 : -o1)]) + m24(fr, R[2 * n + (vert ? o2 : -o2)]) + 16) >> 5;
+            const int k1 = n + b + idx + 1;
+            int pv = (m24(32 - fr, M[k1]) + m24(fr, M[k1 + 1]) + 16) >> 5;
             if (bnd) {
                 const int e = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n + (vert ? -(a + 1) : a + 1)] - R[2 * n]) >> 1));
                 pv = b == 0 ? e : pv;
