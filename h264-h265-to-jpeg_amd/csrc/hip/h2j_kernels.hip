@@ -1932,26 +1932,42 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     }
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
     const int16_t* R = filt ? s.ref : s.sub;
+    // two horizontally adjacent samples per lane (n >= 16): the residual pair read and the
+    // reconstructed pair written as one window dword each, the index arithmetic done once per pair
+    // (TB origins and window rows are even, so the pair is dword aligned)
+    const int hsh = log2n - 1, nh = nn >> 1;
+    auto put2 = [&](int x, int y, int p0, int p1) __attribute__((always_inline)) {
+        int* d = reinterpret_cast<int*>(body + m24(oy + y, S) + ox + x);
+        int r0 = 0, r1 = 0;
+        if (cbf) {
+            const int rr = *d;
+            r0 = (rr << 16) >> 16;
+            r1 = rr >> 16;
+        }
+        *d = clip3(0, maxv, p0 + r0) | (clip3(0, maxv, p1 + r1) << 16);
+    };
     if (mode == 0) {
         const int tr = R[3 * n + 1], bl = R[n - 1];
-        for (int i = lane; i < nn; i += 64) {
-            const int x = i & (n - 1), y = i >> log2n;
-            const int pv = (m24(n - 1 - x, R[2 * n - 1 - y]) + m24(x + 1, tr) + m24(n - 1 - y, R[2 * n + 1 + x]) +
-                            m24(y + 1, bl) + n) >> (log2n + 1);
-            int16_t* d = body + m24(oy + y, S) + ox + x;
-            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+        for (int i = lane; i < nh; i += 64) {
+            const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
+            const int ly = R[2 * n - 1 - y], t0 = R[2 * n + 1 + x], t1 = R[2 * n + 2 + x];
+            const int base = m24(y + 1, bl) + n, wy = n - 1 - y;
+            const int a0 = m24(n - 1 - x, ly) + m24(x + 1, tr), a1 = a0 - ly + tr;
+            put2(x, y, (a0 + m24(wy, t0) + base) >> (log2n + 1), (a1 + m24(wy, t1) + base) >> (log2n + 1));
         }
     } else if (mode == 1) {
-        for (int i = lane; i < nn; i += 64) {
-            const int x = i & (n - 1), y = i >> log2n;
-            int pv = dc;
+        for (int i = lane; i < nh; i += 64) {
+            const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
+            int p0 = dc, p1 = dc;
             if (edge && (x == 0 || y == 0)) {
-                if (x == 0 && y == 0) pv = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
-                else if (y == 0) pv = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                else pv = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                if (y == 0) {
+                    p0 = x == 0 ? (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2 : (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                    p1 = (R[2 * n + 2 + x] + 3 * dc + 2) >> 2;
+                } else {
+                    p0 = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                }
             }
-            int16_t* d = body + m24(oy + y, S) + ox + x;
-            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+            put2(x, y, p0, p1);
         }
     } else {
         const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
@@ -1962,7 +1978,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         const bool bnd = edge && (mode == 26 || mode == 10);
         // the main reference extended to negative positions once per TB (8.4.4.2.6: ref[k] for
         // k < 0 projects onto the side reference through invAngle), M[n + k] for k = -n .. 2n + 1, in
-        // the reference array R is not: the sample loop then reads two entries with no projection
+        // the reference array R is not: the sample loop then reads entries with no projection
         int16_t* M = filt ? s.sub : s.ref;
         for (int k = lane; k < 3 * n + 2; k += 64) {
             const int kk = k - n;
@@ -1971,18 +1987,31 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             M[k] = R[clip3(0, 4 * n, 2 * n + sgn * o)];
         }
         wave_sync();
-        for (int i = lane; i < nn; i += 64) {
-            const int x = i & (n - 1), y = i >> log2n;
-            const int a = vert ? y : x, b = vert ? x : y;  // a: distance from the main reference, b: position along it
-            const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
-            const int k1 = n + b + idx + 1;
-            int pv = (m24(32 - fr, M[k1]) + m24(fr, M[k1 + 1]) + 16) >> 5;
-            if (bnd) {
-                const int e = clip3(0, maxv, R[2 * n + sgn] + ((R[2 * n + (vert ? -(a + 1) : a + 1)] - R[2 * n]) >> 1));
-                pv = b == 0 ? e : pv;
+        if (vert) {  // the pair shares its row, so its position along the angle: three entries
+            for (int i = lane; i < nh; i += 64) {
+                const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
+                const int pos = m24(y + 1, angle), idx = pos >> 5, fr = pos & 31;
+                const int k1 = n + x + idx + 1;
+                const int m0 = M[k1], m1 = M[k1 + 1], m2 = M[k1 + 2];
+                int p0 = (m24(32 - fr, m0) + m24(fr, m1) + 16) >> 5;
+                const int p1 = (m24(32 - fr, m1) + m24(fr, m2) + 16) >> 5;
+                if (bnd && x == 0) p0 = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - (y + 1)] - R[2 * n]) >> 1));
+                put2(x, y, p0, p1);
             }
-            int16_t* d = body + m24(oy + y, S) + ox + x;
-            *d = static_cast<int16_t>(clip3(0, maxv, pv + (cbf ? *d : 0)));
+        } else {
+            for (int i = lane; i < nh; i += 64) {
+                const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
+                const int pos0 = m24(x + 1, angle), pos1 = pos0 + angle;
+                const int k0 = n + y + (pos0 >> 5) + 1, k1 = n + y + (pos1 >> 5) + 1;
+                const int f0 = pos0 & 31, f1 = pos1 & 31;
+                int p0 = (m24(32 - f0, M[k0]) + m24(f0, M[k0 + 1]) + 16) >> 5;
+                int p1 = (m24(32 - f1, M[k1]) + m24(f1, M[k1 + 1]) + 16) >> 5;
+                if (bnd && y == 0) {
+                    p0 = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + x + 1] - R[2 * n]) >> 1));
+                    p1 = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + x + 2] - R[2 * n]) >> 1));
+                }
+                put2(x, y, p0, p1);
+            }
         }
     }
     wave_sync();
