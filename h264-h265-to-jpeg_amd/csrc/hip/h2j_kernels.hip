@@ -2460,8 +2460,8 @@ __global__ void __launch_bounds__(64 * (kYWaves + kCWaves)) h2j_k1_recon_hevc_pi
 }
 
 // K1 HEVC, picture pool: one 16-wave workgroup reconstructs P pictures.  Its waves take CTB-row
-// jobs from one LDS queue ordered row by row and, inside a row index, picture by picture, luma
-// before chroma (row 0: P0 luma, P0 chroma, P1 luma, ...): a wave that finishes a row takes the
+// jobs from one LDS queue ordered row by row and, inside a row index, the pictures' luma rows
+// before their chroma rows (row 0: P0 luma, P1 luma, ..., P0 chroma, ...): a wave that finishes a row takes the
 // next row of either component group and either picture.  Rows of one (picture, group) chain
 // through progress words as in hevc_rows; a job only ever waits on an earlier job, which some
 // wave is running or has finished, so the queue cannot deadlock.  Against one picture per
@@ -2500,8 +2500,11 @@ DEVI void hevc_pool_jobs(const h2j_frame* frames, const h2j_tu* tus, uint8_t* ar
         if (lane == 0) j = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         j = ufl(static_cast<uint32_t>(__shfl(static_cast<int>(j), 0, 64)));
         if (j >= njobs) break;
+        // a row index's luma rows of the P pictures, then their chroma rows (the longer luma
+        // chains start first; same-box 9.28 -> 9.18 ms per 1024 hevc1080 pictures against
+        // luma / chroma alternating per picture)
         const int row = static_cast<int>(j) / (2 * P), rem = static_cast<int>(j) - row * 2 * P;
-        const int p = rem >> 1, grp = rem & 1;
+        const int grp = rem >= P ? 1 : 0, p = rem - grp * P;
         const int fi = fi0 + p;
         if (fi >= nframes) continue;
         const h2j_frame& f = frames[fi];
