@@ -2086,6 +2086,114 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
     wave_sync();
 }
 
+// The Cb and Cr 16x16 TBs at the same place in one pass (the chroma quadrant of a 64x64 CTB):
+// availability, substitution indices and prediction indices computed once, the sample work done
+// for both components.  Cb references in s.sub, Cr in s.ref (chroma is never filtered, no
+// boundary smoothing), the angular modes' extended main references after them (from index 66).
+DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr, uint64_t mask, int ox, int oy, int S,
+                                     int16_t* bcb, int16_t* bcr, const int16_t* tcb, const int16_t* lcb,
+                                     const int16_t* tcr, const int16_t* lcr, K1WaveLds& s, int lane) {
+    constexpr int log2n = 4, n = 16, L = 4 * n + 1, nu = n, nh = n * n / 2;  // unit = 2 chroma samples
+    const int maxv = (1 << u.bdc) - 1;
+    const bool cbf_cb = (tb.flags & H2J_TU_CBF) != 0;
+    unsigned long long m[2];
+#pragma unroll
+    for (int ch = 0; ch < 2; ch++) {
+        const int k = lane + 64 * ch;
+        const int unit = k < 2 * n ? (k >> 1) : nu + ((k - 2 * n + 1) >> 1);
+        m[ch] = __ballot(k < L && ((mask >> unit) & 1ull));
+    }
+    const bool any = (m[0] | m[1]) != 0;
+    const int first = m[0] ? __ffsll(static_cast<long long>(m[0])) - 1
+                           : (m[1] ? 64 + __ffsll(static_cast<long long>(m[1])) - 1 : 128);
+    const int fb[2] = {first, m[0] ? 63 - __clzll(m[0]) : first};
+    const int top_cb = static_cast<int>(tcb - bcb), left_cb = static_cast<int>(lcb - bcb);
+    const int top_cr = static_cast<int>(tcr - bcr), left_cr = static_cast<int>(lcr - bcr);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int half = 1 << (u.bdc - 1);
+    int dsb = 0, dsr = 0;
+#pragma unroll
+    for (int ch = 0; ch < 2; ch++) {
+        const int k = lane + 64 * ch;
+        const unsigned long long le = m[ch] & upto;
+        const int j = le ? 64 * ch + 63 - static_cast<int>(__clzll(le)) : fb[ch];
+        const int xn = j > 2 * n ? ox + (j - 2 * n - 1) : ox - 1;
+        const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
+        const int in = m24(yn, S) + xn;
+        const int icb = yn < 0 ? top_cb + xn + 1 : (xn < 0 ? left_cb + yn : in);
+        const int icr = yn < 0 ? top_cr + xn + 1 : (xn < 0 ? left_cr + yn : in);
+        const int vb = any ? bcb[icb] : half, vr = any ? bcr[icr] : half;
+        s.sub[k < L ? k : 131] = static_cast<int16_t>(vb);
+        s.ref[k < L ? k : 131] = static_cast<int16_t>(vr);
+        const bool dk = k >= n && k <= 3 * n && k != 2 * n;
+        dsb += dk ? vb : 0;
+        dsr += dk ? vr : 0;
+    }
+    const int mode = tb.mode;
+    wave_sync();
+    const int16_t* Rb = s.sub;
+    const int16_t* Rr = s.ref;
+    auto put2 = [&](int x, int y, int b0, int b1, int r0, int r1) __attribute__((always_inline)) {
+        const int o = m24(oy + y, S) + ox + x;
+        int* db = reinterpret_cast<int*>(bcb + o);
+        int* dr = reinterpret_cast<int*>(bcr + o);
+        int rb0 = 0, rb1 = 0, rr0 = 0, rr1 = 0;
+        if (cbf_cb) { const int v = *db; rb0 = (v << 16) >> 16; rb1 = v >> 16; }
+        if (cbf_cr) { const int v = *dr; rr0 = (v << 16) >> 16; rr1 = v >> 16; }
+        *db = clip3(0, maxv, b0 + rb0) | (clip3(0, maxv, b1 + rb1) << 16);
+        *dr = clip3(0, maxv, r0 + rr0) | (clip3(0, maxv, r1 + rr1) << 16);
+    };
+    if (mode == 0) {
+        const int trb = Rb[3 * n + 1], blb = Rb[n - 1], trr = Rr[3 * n + 1], blr = Rr[n - 1];
+        for (int i = lane; i < nh; i += 64) {
+            const int x = (i & 7) * 2, y = i >> 3, wy = n - 1 - y;
+            const int lb = Rb[2 * n - 1 - y], lr = Rr[2 * n - 1 - y];
+            const int bb = m24(y + 1, blb) + n, br = m24(y + 1, blr) + n;
+            const int a0b = m24(n - 1 - x, lb) + m24(x + 1, trb), a0r = m24(n - 1 - x, lr) + m24(x + 1, trr);
+            put2(x, y, (a0b + m24(wy, Rb[2 * n + 1 + x]) + bb) >> (log2n + 1),
+                 (a0b - lb + trb + m24(wy, Rb[2 * n + 2 + x]) + bb) >> (log2n + 1),
+                 (a0r + m24(wy, Rr[2 * n + 1 + x]) + br) >> (log2n + 1),
+                 (a0r - lr + trr + m24(wy, Rr[2 * n + 2 + x]) + br) >> (log2n + 1));
+        }
+    } else if (mode == 1) {
+        const int dcb = (wave_sum_dpp(dsb) + n) >> (log2n + 1), dcr = (wave_sum_dpp(dsr) + n) >> (log2n + 1);
+        for (int i = lane; i < nh; i += 64) put2((i & 7) * 2, i >> 3, dcb, dcb, dcr, dcr);
+    } else {
+        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+        const bool vert = mode >= 18;
+        const int sgn = vert ? 1 : -1;
+        int16_t* Mb = s.sub + 66;  // M[n + k], k = -n .. 2n + 1 (as hevc_predict_tb)
+        int16_t* Mr = s.ref + 66;
+        if (lane < 3 * n + 2) {
+            const int kk = lane - n;
+            const int o = kk >= 0 ? kk : -((m24(kk, inv) + 128) >> 8);
+            const int ix = clip3(0, 4 * n, 2 * n + sgn * o);
+            Mb[lane] = Rb[ix];
+            Mr[lane] = Rr[ix];
+        }
+        wave_sync();
+        for (int i = lane; i < nh; i += 64) {
+            const int x = (i & 7) * 2, y = i >> 3;
+            if (vert) {
+                const int pos = m24(y + 1, angle), fr = pos & 31, k1 = n + x + (pos >> 5) + 1;
+                const int b0 = Mb[k1], b1 = Mb[k1 + 1], b2 = Mb[k1 + 2];
+                const int r0 = Mr[k1], r1 = Mr[k1 + 1], r2 = Mr[k1 + 2];
+                put2(x, y, (m24(32 - fr, b0) + m24(fr, b1) + 16) >> 5, (m24(32 - fr, b1) + m24(fr, b2) + 16) >> 5,
+                     (m24(32 - fr, r0) + m24(fr, r1) + 16) >> 5, (m24(32 - fr, r1) + m24(fr, r2) + 16) >> 5);
+            } else {
+                const int pos0 = m24(x + 1, angle), pos1 = pos0 + angle;
+                const int f0 = pos0 & 31, f1 = pos1 & 31;
+                const int k0 = n + y + (pos0 >> 5) + 1, k1 = n + y + (pos1 >> 5) + 1;
+                put2(x, y, (m24(32 - f0, Mb[k0]) + m24(f0, Mb[k0 + 1]) + 16) >> 5,
+                     (m24(32 - f1, Mb[k1]) + m24(f1, Mb[k1 + 1]) + 16) >> 5,
+                     (m24(32 - f0, Mr[k0]) + m24(f0, Mr[k0 + 1]) + 16) >> 5,
+                     (m24(32 - f1, Mr[k1]) + m24(f1, Mr[k1 + 1]) + 16) >> 5);
+            }
+        }
+    }
+    wave_sync();
+}
+
 // K0 residual of one quadrant -> a quadrant window in LDS by LDS-DMA (no registers held while
 // it is in flight).  The residual planes are tiled by quadrant (h2j_res_q): the quadrant is one
 // contiguous tile, copied in 16-B pieces (luma: Qc x Qc row-major; chroma: Cb at element 0 and
@@ -2246,11 +2354,15 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                     if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
                     const int ci = c == 2 ? 1 : 0;
                     int16_t* body = w.body[cur] + ci * 256;
-                    if (c == 1 && tu.log2n <= 3 && l + 1 < 64 && t + 1 < b && !(tu.flags & H2J_TU_PCM)) {
+                    if (c == 1 && tu.log2n <= 4 && l + 1 < 64 && t + 1 < b && !(tu.flags & H2J_TU_PCM)) {
                         // Cb TB followed by the Cr TB at the same place: one pass for both
                         const h2j_tu tr = tu_from_lanes(rec, l + 1);
                         if (tr.c == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2n == tu.log2n && !(tr.flags & H2J_TU_PCM)) {
-                            if (tu.log2n == 2)
+                            if (tu.log2n == 4)
+                                hevc_predict_chroma_pair16(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
+                                                           body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
+                                                           w.cs[1].left, w.k, lane);
+                            else if (tu.log2n == 2)
                                 hevc_predict_chroma_pair<2>(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
                                                             body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
                                                             w.cs[1].left, lane);
