@@ -1,0 +1,8 @@
+# r03aa: HEVC K1 8-bit quadrant stores 16 samples per lane step (one 16-byte store;
+# four window dwords packed by v_perm): GPU HEVC parity, then same-box A/B against the previous build (build/base).
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_hevc.py tests/test_gpu_f3.py tests/test_gpu_idecoder.py -x -q --timeout 120 --timeout-method thread -m gpu 2>&1 | tail -4
+WLS="hevc1080 hevc2160" VARIANTS="st16:.: base:build/base:" REPS=3 bash tools/gpu_k1ab.sh
