@@ -2424,34 +2424,40 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                         if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = v.x;
                         else *reinterpret_cast<uint2*>(d) = v;
                     };
-                    // 8-bit quadrants 16 or 32 samples wide and whole inside the picture: 16 samples
-                    // per lane step (four window dwords -> one 16-byte store) instead of 4
-                    const bool wide = sizeof(Pel) == 1 && Qc >= 16 && wq == Qc && ((st | u.off(c)) & 15) == 0;
+                    // quadrants 16 or 32 samples wide and whole inside the picture: one 16-byte
+                    // store per lane step -- 16 samples at 8 bits (four window dwords packed by
+                    // v_perm), 8 at 16 bits -- instead of 4 samples
+                    constexpr int SC = 16 / static_cast<int>(sizeof(Pel));  // samples per 16-byte chunk
+                    const bool wide = Qc >= 16 && wq == Qc && ((st | u.off(c)) & (SC - 1)) == 0;
                     auto pack16 = [&](const int16_t* src) __attribute__((always_inline)) {
                         const uint2* q = reinterpret_cast<const uint2*>(src);
+                        if (sizeof(Pel) == 2) {
+                            const uint2 a = q[0], b = q[1];
+                            return make_uint4(a.x, a.y, b.x, b.y);
+                        }
                         const uint2 a = q[0], b = q[1], c2 = q[2], d = q[3];
                         return make_uint4(__builtin_amdgcn_perm(a.y, a.x, 0x06040200u), __builtin_amdgcn_perm(b.y, b.x, 0x06040200u),
                                           __builtin_amdgcn_perm(c2.y, c2.x, 0x06040200u), __builtin_amdgcn_perm(d.y, d.x, 0x06040200u));
                     };
-                    const int lc = Qc == 32 ? 1 : 0;  // log2 of 16-sample chunks per quadrant row
+                    const int lc = __builtin_ctz(static_cast<unsigned>(Qc / SC));  // log2 of chunks per quadrant row
                     if (wide && park) {
-                        uint8_t* sg = reinterpret_cast<uint8_t*>(stg) + ci * 256;
+                        Pel* sg = stg + ci * 256;
                         for (int i = lane; i < (hq << lc); i += 64) {
-                            const int y = i >> lc, x = (i & ((1 << lc) - 1)) * 16;
+                            const int y = i >> lc, x = (i & ((1 << lc) - 1)) * SC;
                             *reinterpret_cast<uint4*>(sg + y * Qc + x) = pack16(body + y * Qc + x);
                         }
                     } else if (wide && joined) {
-                        const uint8_t* sg = reinterpret_cast<const uint8_t*>(stg) + ci * 256;
-                        uint8_t* D = reinterpret_cast<uint8_t*>(P) + (Y0 * st + X0 - Qc);
+                        const Pel* sg = stg + ci * 256;
+                        Pel* D = P + (Y0 * st + X0 - Qc);
                         for (int i = lane; i < (hq << (lc + 1)); i += 64) {
-                            const int y = i >> (lc + 1), x = (i & ((2 << lc) - 1)) * 16;
+                            const int y = i >> (lc + 1), x = (i & ((2 << lc) - 1)) * SC;
                             const uint4 v = x < Qc ? *reinterpret_cast<const uint4*>(sg + y * Qc + x) : pack16(body + y * Qc + x - Qc);
                             *reinterpret_cast<uint4*>(D + y * st + x) = v;
                         }
                     } else if (wide) {
-                        uint8_t* D = reinterpret_cast<uint8_t*>(P) + (Y0 * st + X0);
+                        Pel* D = P + (Y0 * st + X0);
                         for (int i = lane; i < (hq << lc); i += 64) {
-                            const int y = i >> lc, x = (i & ((1 << lc) - 1)) * 16;
+                            const int y = i >> lc, x = (i & ((1 << lc) - 1)) * SC;
                             *reinterpret_cast<uint4*>(D + y * st + x) = pack16(body + y * Qc + x);
                         }
                     } else if (park) {  // Qc x hq samples into the staging tile (rows of Qc, Cb at 0, Cr at 256)
