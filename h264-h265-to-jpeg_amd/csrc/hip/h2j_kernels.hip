@@ -1932,42 +1932,49 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     }
     // p(-1,y) = R[2n-1-y], p(x,-1) = R[2n+1+x], p(-1,-1) = R[2n]
     const int16_t* R = filt ? s.ref : s.sub;
-    // two horizontally adjacent samples per lane (n >= 16): the residual pair read and the
-    // reconstructed pair written as one window dword each, the index arithmetic done once per pair
-    // (TB origins and window rows are even, so the pair is dword aligned)
-    const int hsh = log2n - 1, nh = nn >> 1;
-    auto put2 = [&](int x, int y, int p0, int p1) __attribute__((always_inline)) {
-        int* d = reinterpret_cast<int*>(body + m24(oy + y, S) + ox + x);
-        int r0 = 0, r1 = 0;
+    // four horizontally adjacent samples per lane (n >= 16): the residual quad read and the
+    // reconstructed quad written as one 8-byte window access each, the index arithmetic done
+    // once per quad (TB origins and window rows are multiples of 4 samples, so the quad is 8-byte
+    // aligned)
+    const int qsh = log2n - 2, nq4 = nn >> 2;
+    auto put4 = [&](int x, int y, int p0, int p1, int p2, int p3) __attribute__((always_inline)) {
+        uint2* d = reinterpret_cast<uint2*>(body + m24(oy + y, S) + ox + x);
+        int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
         if (cbf) {
-            const int rr = *d;
-            r0 = (rr << 16) >> 16;
-            r1 = rr >> 16;
+            const uint2 rr = *d;
+            r0 = static_cast<int>(rr.x << 16) >> 16;
+            r1 = static_cast<int>(rr.x) >> 16;
+            r2 = static_cast<int>(rr.y << 16) >> 16;
+            r3 = static_cast<int>(rr.y) >> 16;
         }
-        *d = clip3(0, maxv, p0 + r0) | (clip3(0, maxv, p1 + r1) << 16);
+        *d = make_uint2(static_cast<uint32_t>(clip3(0, maxv, p0 + r0) | (clip3(0, maxv, p1 + r1) << 16)),
+                        static_cast<uint32_t>(clip3(0, maxv, p2 + r2) | (clip3(0, maxv, p3 + r3) << 16)));
     };
     if (mode == 0) {
         const int tr = R[3 * n + 1], bl = R[n - 1];
-        for (int i = lane; i < nh; i += 64) {
-            const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
-            const int ly = R[2 * n - 1 - y], t0 = R[2 * n + 1 + x], t1 = R[2 * n + 2 + x];
-            const int base = m24(y + 1, bl) + n, wy = n - 1 - y;
-            const int a0 = m24(n - 1 - x, ly) + m24(x + 1, tr), a1 = a0 - ly + tr;
-            put2(x, y, (a0 + m24(wy, t0) + base) >> (log2n + 1), (a1 + m24(wy, t1) + base) >> (log2n + 1));
+        for (int i = lane; i < nq4; i += 64) {
+            const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
+            const int ly = R[2 * n - 1 - y];
+            const int base = m24(y + 1, bl) + n, wy = n - 1 - y, dd = tr - ly;
+            const int a0 = m24(n - 1 - x, ly) + m24(x + 1, tr) + base;
+            put4(x, y, (a0 + m24(wy, R[2 * n + 1 + x])) >> (log2n + 1), (a0 + dd + m24(wy, R[2 * n + 2 + x])) >> (log2n + 1),
+                 (a0 + 2 * dd + m24(wy, R[2 * n + 3 + x])) >> (log2n + 1), (a0 + 3 * dd + m24(wy, R[2 * n + 4 + x])) >> (log2n + 1));
         }
     } else if (mode == 1) {
-        for (int i = lane; i < nh; i += 64) {
-            const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
-            int p0 = dc, p1 = dc;
+        for (int i = lane; i < nq4; i += 64) {
+            const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
+            int p0 = dc, p1 = dc, p2 = dc, p3 = dc;
             if (edge && (x == 0 || y == 0)) {
                 if (y == 0) {
                     p0 = x == 0 ? (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2 : (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
                     p1 = (R[2 * n + 2 + x] + 3 * dc + 2) >> 2;
+                    p2 = (R[2 * n + 3 + x] + 3 * dc + 2) >> 2;
+                    p3 = (R[2 * n + 4 + x] + 3 * dc + 2) >> 2;
                 } else {
                     p0 = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
                 }
             }
-            put2(x, y, p0, p1);
+            put4(x, y, p0, p1, p2, p3);
         }
     } else {
         const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
@@ -1987,30 +1994,28 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             M[k] = R[clip3(0, 4 * n, 2 * n + sgn * o)];
         }
         wave_sync();
-        if (vert) {  // the pair shares its row, so its position along the angle: three entries
-            for (int i = lane; i < nh; i += 64) {
-                const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
-                const int pos = m24(y + 1, angle), idx = pos >> 5, fr = pos & 31;
-                const int k1 = n + x + idx + 1;
-                const int m0 = M[k1], m1 = M[k1 + 1], m2 = M[k1 + 2];
-                int p0 = (m24(32 - fr, m0) + m24(fr, m1) + 16) >> 5;
-                const int p1 = (m24(32 - fr, m1) + m24(fr, m2) + 16) >> 5;
+        auto lerp = [](int fr, int a, int b) __attribute__((always_inline)) { return (m24(32 - fr, a) + m24(fr, b) + 16) >> 5; };
+        if (vert) {  // the quad shares its row, so its position along the angle: five entries
+            for (int i = lane; i < nq4; i += 64) {
+                const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
+                const int pos = m24(y + 1, angle), fr = pos & 31;
+                const int k1 = n + x + (pos >> 5) + 1;
+                const int m0 = M[k1], m1 = M[k1 + 1], m2 = M[k1 + 2], m3 = M[k1 + 3], m4 = M[k1 + 4];
+                int p0 = lerp(fr, m0, m1);
                 if (bnd && x == 0) p0 = clip3(0, maxv, R[2 * n + 1] + ((R[2 * n - (y + 1)] - R[2 * n]) >> 1));
-                put2(x, y, p0, p1);
+                put4(x, y, p0, lerp(fr, m1, m2), lerp(fr, m2, m3), lerp(fr, m3, m4));
             }
         } else {
-            for (int i = lane; i < nh; i += 64) {
-                const int x = (i & ((n >> 1) - 1)) * 2, y = i >> hsh;
-                const int pos0 = m24(x + 1, angle), pos1 = pos0 + angle;
-                const int k0 = n + y + (pos0 >> 5) + 1, k1 = n + y + (pos1 >> 5) + 1;
-                const int f0 = pos0 & 31, f1 = pos1 & 31;
-                int p0 = (m24(32 - f0, M[k0]) + m24(f0, M[k0 + 1]) + 16) >> 5;
-                int p1 = (m24(32 - f1, M[k1]) + m24(f1, M[k1 + 1]) + 16) >> 5;
-                if (bnd && y == 0) {
-                    p0 = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + x + 1] - R[2 * n]) >> 1));
-                    p1 = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + x + 2] - R[2 * n]) >> 1));
+            for (int i = lane; i < nq4; i += 64) {
+                const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
+                int p[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int pos = m24(x + q + 1, angle), k = n + y + (pos >> 5) + 1;
+                    p[q] = lerp(pos & 31, M[k], M[k + 1]);
+                    if (bnd && y == 0) p[q] = clip3(0, maxv, R[2 * n - 1] + ((R[2 * n + x + q + 1] - R[2 * n]) >> 1));
                 }
-                put2(x, y, p0, p1);
+                put4(x, y, p[0], p[1], p[2], p[3]);
             }
         }
     }
