@@ -4127,7 +4127,8 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
     // 1. every load of the CTB in flight at once
     SaoRegs R;
     sao_load<Pel>(f, arena, ctb, R);
-    const bool nok = !eo || tid >= 9 || sao_nb_ok(f, C, SL, cx, row, tid);
+    // one slice from CTB 0 and one tile (frame.topo 0): every neighbour CTB is usable, no record loads
+    const bool nok = !eo || tid >= 9 || !f.topo || sao_nb_ok(f, C, SL, cx, row, tid);
     // 2. LDS
     if (tid < 64) {
         const uint64_t m = __ballot(tid < 9 && nok);
