@@ -2911,17 +2911,21 @@ DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slic
     const uint8_t fl = fmap[idx];
     if (!(fl & (vert ? 1 : 2))) return;
     const int xe = x4 * 4, ye = y4 * 4;
-    const int ctb = (ye >> f.log2ctb) * f.ctb_w + (xe >> f.log2ctb);
-    const h2j_slice& sl = slices[ctbs[ctb].slice];
-    hevc_luma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 0), f.pic_stride[0], fmap, qmap, sl, vert, xe, ye);
-    // chroma edges lie on the 16-luma grid; one chroma segment = 8 luma lines
-    if ((vert ? (xe & 15) == 0 && (ye & 7) == 0 : (ye & 15) == 0 && (xe & 7) == 0)) {
-        const int pw = f.width >> 1, ph = f.height >> 1;
-        hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 1), f.pic_stride[1], pw, ph, fmap, qmap, sl,
-                              f.cb_qp_offset, vert, xe >> 1, ye >> 1);
-        hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 2), f.pic_stride[2], pw, ph, fmap, qmap, sl,
-                              f.cr_qp_offset, vert, xe >> 1, ye >> 1);
-    }
+    auto run = [&](const h2j_slice& sl) __attribute__((always_inline)) {
+        hevc_luma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 0), f.pic_stride[0], fmap, qmap, sl, vert, xe, ye);
+        // chroma edges lie on the 16-luma grid; one chroma segment = 8 luma lines
+        if ((vert ? (xe & 15) == 0 && (ye & 7) == 0 : (ye & 15) == 0 && (xe & 7) == 0)) {
+            const int pw = f.width >> 1, ph = f.height >> 1;
+            hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 1), f.pic_stride[1], pw, ph, fmap, qmap, sl,
+                                  f.cb_qp_offset, vert, xe >> 1, ye >> 1);
+            hevc_chroma_edge<Pel>(f, plane<Pel>(f, arena, f.pic, 2), f.pic_stride[2], pw, ph, fmap, qmap, sl,
+                                  f.cr_qp_offset, vert, xe >> 1, ye >> 1);
+        }
+    };
+    // one slice from CTB 0 and one tile (frame.topo 0): the picture's first slice, a uniform
+    // (scalar) load, instead of two dependent per-thread loads (the CTB record, then its slice)
+    if (f.topo) run(slices[ctbs[(ye >> f.log2ctb) * f.ctb_w + (xe >> f.log2ctb)].slice]);
+    else run(slices[0]);
 }
 
 __global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* __restrict__ frames,
