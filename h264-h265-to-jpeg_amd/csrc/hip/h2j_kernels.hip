@@ -4521,6 +4521,7 @@ __global__ void __launch_bounds__(256) h2j_k4c_fdct_sym(const h2j_frame* frames,
     const int t = threadIdx.x, bi = b0 + t;
     uint8_t* tile = arena + f.jcoef + static_cast<size_t>(gp.x) * kJTileBytes;
     uint32_t* sym = reinterpret_cast<uint32_t*>(tile);
+    bool eob = false;
     if (bi < nblk) {
         int16_t out[64];
         if (f.bit_depth == 8) jpeg_block_coefs<uint8_t>(f, arena, bi, out);
@@ -4544,12 +4545,18 @@ __global__ void __launch_bounds__(256) h2j_k4c_fdct_sym(const h2j_frame* frames,
                 atomicAdd(&hist[tab][s2], 1u);
             }
         }
-        if (prev < 63) {
-            sym[n++ * 256 + t] = 0u;  // EOB
-            atomicAdd(&hist[tab][0], 1u);
-        }
+        eob = prev < 63;
+        if (eob) sym[n++ * 256 + t] = 0u;  // EOB
         tile[kJCntOff + t] = static_cast<uint8_t>(n);
         reinterpret_cast<int16_t*>(tile + kJDcOff)[t] = out[0];
+    }
+    {  // EOB counts per wave and table: one LDS atomic each instead of one per block (same bin)
+        const int tab = ((b0 + t) % 6) < 4 ? 0 : 1;
+        const unsigned long long e0 = __ballot(eob && tab == 0), e1 = __ballot(eob && tab == 1);
+        if ((t & 63) == 0) {
+            if (e0) atomicAdd(&hist[0][0], static_cast<unsigned>(__popcll(e0)));
+            if (e1) atomicAdd(&hist[1][0], static_cast<unsigned>(__popcll(e1)));
+        }
     }
     __syncthreads();
     h2j_jstat* js = reinterpret_cast<h2j_jstat*>(arena + f.jstat);
