@@ -970,7 +970,7 @@ DEVI int zorder4(int ax, int ay) {
 // One kernel per codec (HEVC: batched transforms, more records per wave; each gets its own
 // register budget), each skipping the other codec's pictures.
 template <bool HEVC>
-__global__ void __launch_bounds__(64) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
+__global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, const h2j_tu* tus, const h2j_coef* coefs,
                                                  const h2j_ctb* ctbs, const h2j_slice* slices, const uint8_t* sl,
                                                  uint8_t* arena) {
     const GridPos gp = xcd_grid_pos();
@@ -2928,7 +2928,7 @@ DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slic
     else run(slices[0]);
 }
 
-__global__ void __launch_bounds__(256) h2j_k2_deblock(const h2j_frame* __restrict__ frames,
+__global__ void __launch_bounds__(256, 8) h2j_k2_deblock(const h2j_frame* __restrict__ frames,
                                                      const h2j_ctb* __restrict__ ctbs,
                                                      const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena,
                                                      int vert) {
