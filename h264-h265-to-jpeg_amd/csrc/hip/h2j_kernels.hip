@@ -4242,14 +4242,10 @@ __global__ void __launch_bounds__(256) h2j_k4a_variance(const h2j_frame* __restr
                                                                   static_cast<size_t>(y + f.crop_y) * f.pic_stride[0] +
                                                                   mx * 16 + f.crop_x);
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < 4; k++) {  // 4 samples per v_dot4_u32_u8: the sum and the sum of squares
                 const uint32_t w = p[k];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const unsigned v = (w >> (8 * b)) & 0xFF;
-                    s += v;
-                    n += v * v;
-                }
+                s = __builtin_amdgcn_udot4(w, 0x01010101u, s, false);
+                n = __builtin_amdgcn_udot4(w, w, n, false);
             }
         } else if (inside && f.bit_depth > 8) {  // 16-bit samples, converted as jpeg_sample does
             const uint2* p = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(arena + f.pic2) + f.pic_off[0] +
