@@ -3899,10 +3899,7 @@ struct SaoLds {
 // K4a's macroblock variances (the JPEG rate control input) are summed by K3 from the SAO output
 // it holds in registers, when the output's 16x16 MB grid is aligned with the CTB grid; K4a then
 // skips the picture (one full read of the final picture less).
-DEVI bool sao_sums_variance(const h2j_frame& f, int fold) {
-    return fold && f.codec == H2J_CODEC_HEVC && f.pic2 != f.pic && (f.crop_x & 15) == 0 && (f.crop_y & 15) == 0 &&
-           (f.out_w & 15) == 0;
-}
+DEVI bool sao_sums_variance(const h2j_frame& f, int fold) { return fold && h2j_sao_folds_variance(f); }
 
 template <typename Pel>
 DEVI uint2 sao_load4(const Pel* p) {  // 4 samples -> 4 int16 halves of a uint2
@@ -4908,6 +4905,7 @@ static int sao_var_fold() {
     }();
     return v;
 }
+int h2j_gpu_sao_var_fold(void) { return sao_var_fold(); }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0 || !b->has_hevc) return 0;
@@ -4922,9 +4920,12 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int mbs = b->max_mcu;
-    hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena, sao_var_fold());
-    int r = check(hipGetLastError(), "h2j_k4a_variance");
-    if (r) return r;
+    if (b->k4a_frames > 0) {  // none: K3 has summed every picture's MB variances
+        hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena, sao_var_fold());
+        const int r = check(hipGetLastError(), "h2j_k4a_variance");
+        if (r) return r;
+    }
+    int r = 0;
     hipLaunchKernelGGL(h2j_k4b_ratecontrol, dim3(b->nframes), dim3(64), 0, s, b->frames, b->arena);
     r = check(hipGetLastError(), "h2j_k4b_ratecontrol");
     if (r) return r;

@@ -559,6 +559,12 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         if (s.frames[k].codec == H2J_CODEC_HEVC) b.hevc_pels |= (s.frames[k].bit_depth > 8 || s.frames[k].bit_depth_c > 8) ? 2 : 1;
     b.arena = static_cast<uint8_t*>(s.d_arena.p);
     b.jpeg_dense = entropy ? 0 : 1;
+    {  // pictures whose MB variances K4a sums (K3 sums the others'; no K4a launch when none is left)
+        static const int fold = h2j_gpu_sao_var_fold();
+        int k4a = 0;
+        for (int k = 0; k < nf; k++) k4a += (fold && h2j_sao_folds_variance(s.frames[k])) ? 0 : 1;
+        b.k4a_frames = k4a;
+    }
     b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
     b.seg_cap = entropy ? seg_cap : 0;
     b.seg_total = entropy ? static_cast<uint64_t*>(s.d_scratch.p) : nullptr;
