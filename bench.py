@@ -118,6 +118,39 @@ def reduce_over_ranks(dist, elapsed, frames, local_rank=0):
     return float(t.item()), int(c.item())
 
 
+def sum_over_ranks(dist, value, local_rank=0):
+    """SUM of an integer counter over ranks (the output-check mismatch count)."""
+    if dist is None:
+        return value
+    import torch
+    use_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+    dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    c = torch.tensor([value], dtype=torch.int64, device=dev)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return int(c.item())
+
+
+def verify_outputs(batch, out, offs, lens, manifest):
+    """After the timed region: md5 of every JPEG of one step against tests/golden/bench_manifest.json
+    (md5(stream) -> md5 of the oracle's JPEG, minted by tools/make_bench_manifest.py).  Returns
+    (pictures checked, mismatches, streams missing from the manifest)."""
+    import hashlib
+    mv = memoryview(out)
+    smd5 = {}
+    bad = missing = 0
+    for i, b in enumerate(batch):
+        key = smd5.get(id(b))
+        if key is None:
+            key = smd5[id(b)] = hashlib.md5(b).hexdigest()
+        ent = manifest.get(key)
+        if ent is None:
+            missing += 1
+            continue
+        if hashlib.md5(mv[offs[i]:offs[i] + lens[i]]).hexdigest() != ent["jpeg_md5"]:
+            bad += 1
+    return len(batch), bad, missing
+
+
 def shard_lpt(costs, world):
     """Size-balanced LPT partition of independent stills over `world` GPUs
     (SURVEY.md §8e, config 5): returns one index list per rank."""
@@ -356,6 +389,7 @@ def main():
             for k in range(k_steps):
                 out, offs, lens, status = outsets[0]
                 check(eng.transcode_raw(ptrs, sizes, n, out, cap, offs, lens, status), status)
+                last_out[0] = outsets[0]
                 if record:
                     collect()
             return
@@ -367,6 +401,7 @@ def main():
             if k > 0:  # wait for step k - 1 (step k is parsing by now: its stats are not published yet)
                 t, status = inflight.pop(0)
                 check(eng.wait(t), status)
+                last_out[0] = outsets[(k - 1) % 2]
                 if record:
                     collect()
 
@@ -375,6 +410,7 @@ def main():
             dist.barrier()
 
     run_steps(args.warmup, False)
+    last_out = [None]  # the output set of the last step waited for (checked after the timed region)
     barrier()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
@@ -386,6 +422,13 @@ def main():
     # host CPU time of this process (all threads) over the timed region, in busy cores
     host_cores = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / max(elapsed, 1e-9)
     elapsed, total_frames = reduce_over_ranks(dist, elapsed, n * args.steps, local)
+    # outside the timed region: every JPEG of the last timed step against the oracle's md5s
+    man_path = os.path.join(ROOT, "tests", "golden", "bench_manifest.json")
+    manifest = json.load(open(man_path)) if os.path.exists(man_path) else {}
+    out, offs, lens, _ = last_out[0]
+    checked, bad, missing = verify_outputs(batch, out, offs, lens, manifest)
+    bad_all = sum_over_ranks(dist, bad + missing, local)
+    checked_all = sum_over_ranks(dist, checked, local)
 
     if rank == 0:
         steps = args.steps
@@ -462,6 +505,11 @@ def main():
             "parse_core_def": "pool wall time from the batch's first to its last parsed picture x host threads / KB "
                               "(r02 used submission -> last parsed, which counted the wait behind the previous batch)",
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
+            "outputs_verified": bool(manifest) and bad_all == 0,
+            "outputs_checked": {"pictures": checked_all, "mismatched_or_unknown": bad_all,
+                                "def": "md5 of every JPEG of the last timed step (all ranks) == md5 of the oracle's "
+                                       "JPEG of its stream (tests/golden/bench_manifest.json, "
+                                       "tools/make_bench_manifest.py); checked after the timed region"},
         }
         # configs[0]-style single calls: the reference fixture and one stream of this workload
         if not args.no_single_call:

@@ -255,11 +255,7 @@ constexpr int kK0Tus = 62;  // H.264 TUs per K0 wave (records held one per lane)
 // lanes kTus and kTus + 1 hold the neighbour records of a wave's range (h2j_k0_prep)
 static_assert(kK0Tus >= 1 && kK0Tus <= 62, "K0 records per wave: 62 at most");
 constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
-// HEVC K1: launches of > 128 pictures run one 16-wave workgroup per picture split unevenly: the Cb/Cr chain processes each Cb/Cr TB
-// pair in one pass (about 2/3 of a luma row's time), so 9 luma + 7 chroma waves finish a 17-row
-// 1080p picture in 2 luma rounds instead of 3 (8 + 8)
-constexpr int kYWaves = 9, kCWaves = 7;
-constexpr int kK1WavesWide = 16;  // ... launches of <= 128 pictures (one group per CU)
+constexpr int kK1WavesWide = 16;  // HEVC K1, launches of <= 128 pictures: waves per group (one group per CU)
 constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
 
 struct K0Lds {    // H.264
@@ -2202,8 +2198,12 @@ DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr,
 // K0 residual of one quadrant -> a quadrant window in LDS by LDS-DMA (no registers held while
 // it is in flight).  The residual planes are tiled by quadrant (h2j_res_q): the quadrant is one
 // contiguous tile, copied in 16-B pieces (luma: Qc x Qc row-major; chroma: Cb at element 0 and
-// Cr at 256, Qc x Qc each).  Tiles past the picture's right / bottom edge exist in full (samples
-// there are never used), so no lane needs a bounds test.
+// Cr at 256, Qc x Qc each).  Tiles past the picture's right / bottom edge exist in full, so no
+// lane needs a bounds test; their samples outside the picture are never written by K0 (stale
+// arena bytes) and never read by reconstruction: every TB lies inside the coded picture, because
+// the parser rejects widths / heights that are not a multiple of MinCbSize (hevc_parser.cpp,
+// vector m_hevc_width_not_mincb) and the coding quadtree splits implicitly at the picture edge
+// (7.3.8.4), so every CB -- and with it every TB -- ends inside the picture.
 DEVI void hevc_qres_dma(const FU& u, int grp, int X0, int Y0, int Qc, int16_t* body, int lane) {
     const int chunks = (Qc * Qc) >> 3;  // 16-B pieces of one plane's tile
     if (grp == 0) {
@@ -2585,40 +2585,13 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
     else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
 }
 
-// One HEVC picture in one 16-wave workgroup: waves 0..kYWaves-1 the luma chain, the rest the
-// Cb/Cr chain, each group with its own LDS region (luma first, `ybytes` long).
-template <typename Pel>
-DEVI void hevc_picture_groups(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, uint8_t* lds, uint32_t ybytes) {
-    const int wave = static_cast<int>(threadIdx.x >> 6);
-    const int grp = wave < kYWaves ? 0 : 1;
-    const int nw = grp ? kCWaves : kYWaves;
-    uint8_t* gb = lds + (grp ? ybytes : 0);
-    QWave* W = reinterpret_cast<QWave*>(gb);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(gb + sizeof(QWave) * nw);
-    int16_t* line = reinterpret_cast<int16_t*>(gb + k1_fixed_lds(nw));
-    const int tl = static_cast<int>(threadIdx.x) - (grp ? 64 * kYWaves : 0);
-    if (tl < 2 * nw) prog[tl] = 0;
-    __syncthreads();
-    if (grp == 0) hevc_rows<Pel>(f, T, arena, 0, W, prog, line, wave, kYWaves);  // one specialised copy per group
-    else hevc_rows<Pel>(f, T, arena, 1, W, prog, line, wave - kYWaves, kCWaves);
-}
-// launches of > 128 pictures: one workgroup per picture (see kYWaves)
-template <typename Pel>
-__global__ void __launch_bounds__(64 * (kYWaves + kCWaves)) h2j_k1_recon_hevc_pic(const h2j_frame* frames, const h2j_tu* tus,
-                                                                                uint8_t* arena, uint32_t ybytes) {
-    extern __shared__ __align__(16) uint8_t k1lds[];
-    const h2j_frame& f = frames[blockIdx.x];
-    if (f.codec != H2J_CODEC_HEVC || (f.bit_depth > 8) != (sizeof(Pel) == 2)) return;
-    hevc_picture_groups<Pel>(f, tus + ufl(f.tu), arena, k1lds, ybytes);
-}
-
 // K1 HEVC, picture pool: one 16-wave workgroup reconstructs P pictures.  Its waves take CTB-row
 // jobs from one LDS queue ordered row by row and, inside a row index, the pictures' luma rows
 // before their chroma rows (row 0: P0 luma, P1 luma, ..., P0 chroma, ...): a wave that finishes a row takes the
 // next row of either component group and either picture.  Rows of one (picture, group) chain
 // through progress words as in hevc_rows; a job only ever waits on an earlier job, which some
 // wave is running or has finished, so the queue cannot deadlock.  Against one picture per
-// workgroup with a fixed 9 luma / 7 chroma split (h2j_k1_recon_hevc_pic) no wave idles through a
+// workgroup with a fixed 9 luma / 7 chroma split (r01) no wave idles through a
 // second row round, and one picture's wavefront start-up overlaps the other's tail.
 // LDS: QWave[16] | progress words [P][2][maxrows] | queue word (+3 pad) | lines [P][lstride]
 // (luma bottom line at 0, Cb / Cr lines at lchroma).
@@ -2689,12 +2662,9 @@ __global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const 
 // workgroup; an H.264 workgroup is one band as in h2j_k1_recon_h264.  Tall HEVC pictures (the
 // longest chains of such a batch) instead get one 16-wave workgroup per component group, twice
 // the rows in flight.  `map`: the host's list, longest chains first; bit 31 marks HEVC entries,
-// bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).  `ybytes`: LDS bytes of the luma group of a
-// picture workgroup (hevc_picture_groups).
+// bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_frame* frames, const h2j_tu* tus,
-                                                                 uint8_t* arena, const uint32_t* map,
-                                                                 uint32_t ybytes) {
-    static_assert(kYWaves + kCWaves == kAvcWaves, "an HEVC picture's two groups fill one H.264-sized workgroup");
+                                                                 uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t anylds[];
     const uint32_t me = map[blockIdx.x];
     const h2j_frame& f = frames[(me >> 8) & 0x3FFFFFu];
@@ -3020,18 +2990,12 @@ DEVI void h264_filt_line(int (&v)[20], bool on, int bs, int alpha, int beta, int
     }
 }
 
-// one phase (vertical or horizontal edges) of one MB, one lane = one line
-// H.264 K2 (8.7): one workgroup per picture; wave w deblocks macroblock rows
-// w, w + kAvcDbWaves, ... in raster order.  MB (x, y) starts once row y-1
-// has finished MBs 0..x+1: its top edge reads and modifies row y-1's bottom
-// rows, which MB (x+1, y-1)'s left edge modifies too.  Each wave filters its
-// MB inside an LDS window (the MB, 4 luma / 2 chroma rows above it, 4 / 2
-// columns left of it); the rows above come from a per-picture LDS line
-// buffer that every row leaves behind, the columns on the left are carried
-// from the previous MB, and the MB's own samples (K1 output, not touched by
-// anyone else before) are prefetched into registers one MB ahead.  After the
-// 8 luma + 4 chroma edge passes the window is written back once.
-constexpr int kAvcDbWaves = 16;
+// H.264 K2 (8.7) window of one MB: MB (x, y) starts once row y-1 has finished MBs 0..x+1 (its
+// top edge reads and modifies row y-1's bottom rows, which MB (x+1, y-1)'s left edge modifies
+// too).  The MB is filtered inside an LDS window (the MB, 4 luma / 2 chroma rows above it, 4 / 2
+// columns left of it); the rows above come from a per-picture line buffer that every row leaves
+// behind, the columns on the left are carried from the previous MB.  After the 8 luma + 4 chroma
+// edge passes the window is written back once.
 struct alignas(16) DbWin {
     uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
     uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
@@ -3055,24 +3019,6 @@ DEVI void db264_copy(Pel* dst, const Pel* src) {
     }
 }
 
-template <typename Pel>
-struct DbPrefetch {  // one MB: luma 4 samples + chroma 2 samples per lane
-    Pel y[4];
-    Pel c[2];
-};
-
-template <typename Pel>
-DEVI void db264_fetch(const Pel* PY, const Pel* const* PC, int sty, int stc, int mx, int my, DbPrefetch<Pel>& r,
-                      int lane) {
-    const Pel* s = PY + (my * 16 + (lane >> 2)) * sty + mx * 16 + (lane & 3) * 4;
-#pragma unroll
-    for (int k = 0; k < 4; k++) r.y[k] = s[k];
-    const int c = lane >> 5, k = lane & 31;
-    const Pel* t = PC[c] + (my * 8 + (k >> 2)) * stc + mx * 8 + (k & 3) * 2;
-    r.c[0] = t[0];
-    r.c[1] = t[1];
-}
-
 // Deblocking parameters of one MB and of its top neighbour, loaded one MB ahead with VECTOR
 // loads (lane 0/1: the MB's dwords 2 and 9, lane 2/3: the top MB's): scalar loads would be
 // waited with lgkmcnt(0), which also drains every LDS access in between (the old form cost
@@ -3093,368 +3039,6 @@ struct DbTables {
     int cqp[22];                       // chroma QP map above 29
     h2j_slice sl[kDbSlices];
 };
-
-template <typename Pel>
-DEVI void h264_db_rows(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
-                       uint32_t* prog, uint16_t* line, int band, int nbands, const DbTables& TB) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    DbWin& w = W[wv];
-    const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
-    const int bd = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
-    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
-    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
-    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
-    uint16_t* LY = line;                  // [4][width]: rows 12..15 of the MB row above
-    uint16_t* LC = line + 4 * width;      // [2 comps][2 rows][width / 2]: chroma rows 6..7
-    const int cw = width >> 1;
-    constexpr int kSlots = 2 * kAvcDbWaves;
-    // rows of this workgroup: the K1 banding (h2j_frame.k1bands); across a band boundary the line
-    // buffer lives in frame.xline (3W dwords per boundary) and progress in the row's 4th CTB-range
-    // word, which K1 left at mbw (K2 counts on from there), both with agent-scope atomics
-    const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
-    const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
-    if (rbeg + wv >= rend) return;
-    PROF_DECL;
-    DbPrefetch<Pel> pf;
-    db264_fetch<Pel>(PY, PC, sty, stc, 0, rbeg + wv, pf, lane);
-    uint32_t ninfo = db264_info_raw(mbs, mbw, 0, rbeg + wv, lane);
-    int lmf = 0, lqp = 0, lsaddr = -1;  // left neighbour (previous MB of the row)
-    for (int row = rbeg + wv; row < rend; row += kAvcDbWaves) {
-        uint32_t* above = prog + (row + kSlots - 1) % kSlots;
-        uint32_t* mine = prog + row % kSlots;
-        uint32_t seen = 0;
-        const bool from_band = nbands > 1 && band > 0 && row == rbeg;
-        const bool to_band = nbands > 1 && band < nbands - 1 && row == rend - 1;
-        const uint64_t o_xin = o_xl + 12ull * (band - 1) * width, o_xout = o_xl + 12ull * band * width;
-        for (int mx = 0; mx < mbw; mx++) {
-            if (from_band) {
-                const uint32_t need = static_cast<uint32_t>(mbw + min(mx + 2, mbw));
-                if (seen < need) {
-                    uint32_t it = 0;
-                    uint32_t* fl = reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * ((row - 1) * mbw);
-                    while ((seen = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++it > (1u << 22)) {  // never expected: flag the picture, do not hang the GPU
-                            if (lane == 0) __hip_atomic_fetch_or(dev_error_word(arena, f), kDevErrDbBand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            seen = 2u * mbw;
-                            break;
-                        }
-                    }
-                }
-            } else if (row > rbeg || (row > 0 && nbands <= 1)) {
-                const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
-                if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrDbRow264);
-            }
-            PROF_LAP(0);
-            // window: MB body (prefetched), rows above (line buffer); the left columns are carried
-            {
-                const int r = lane >> 2, c4 = (lane & 3) * 4;
-#pragma unroll
-                for (int k = 0; k < 4; k++) w.y[r + 4][c4 + k + 4] = pf.y[k];
-                const int c = lane >> 5, k = lane & 31, rr = k >> 2, c2 = (k & 3) * 2;
-                w.c[c][rr + 2][c2 + 2] = pf.c[0];
-                w.c[c][rr + 2][c2 + 3] = pf.c[1];
-                if (from_band) {
-                    const uint16_t* X = reinterpret_cast<const uint16_t*>(arena + o_xin);
-                    const int tr = lane >> 4, tc = lane & 15;
-                    w.y[tr][tc + 4] = __hip_atomic_load(X + tr * width + mx * 16 + tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (lane < 32) {
-                        const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
-                        w.c[cc][cr][ck + 2] = __hip_atomic_load(X + 4 * width + (cc * 2 + cr) * cw + mx * 8 + ck,
-                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                } else if (row > 0) {
-                    const int tr = lane >> 4, tc = lane & 15;  // 4 rows x 16 luma columns
-                    w.y[tr][tc + 4] = LY[tr * width + mx * 16 + tc];
-                    if (lane < 32) {  // 2 comps x 2 rows x 8 columns
-                        const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
-                        w.c[cc][cr][ck + 2] = LC[(cc * 2 + cr) * cw + mx * 8 + ck];
-                    }
-                }
-            }
-            {  // prefetch the next MB of this wave
-                int nx = mx + 1, ny = row;
-                if (nx == mbw) { nx = 0; ny += kAvcDbWaves; }
-                if (ny < mbh) db264_fetch<Pel>(PY, PC, sty, stc, nx, ny, pf, lane);
-            }
-            wave_sync();
-            PROF_LAP(1);
-            const uint32_t cur = ninfo;
-            {  // parameters of the wave's next MB
-                int nx = mx + 1, ny = row;
-                if (nx == mbw) { nx = 0; ny += kAvcDbWaves; }
-                if (ny < mbh) ninfo = db264_info_raw(mbs, mbw, nx, ny, lane);
-            }
-            const uint32_t r0 = __builtin_amdgcn_readlane(cur, 0), r1 = __builtin_amdgcn_readlane(cur, 1);
-            const uint32_t r2 = __builtin_amdgcn_readlane(cur, 2), r3 = __builtin_amdgcn_readlane(cur, 3);
-            const int mf = static_cast<int>((r1 >> 8) & 0xFF), mqp = static_cast<int8_t>(r1 & 0xFF);
-            const int csl = static_cast<int>((r0 >> 8) & 0xFF), tsl = static_cast<int>((r2 >> 8) & 0xFF);
-            const int tmf = row > 0 ? static_cast<int>((r3 >> 8) & 0xFF) : 0, tqp = static_cast<int8_t>(r3 & 0xFF);
-            const h2j_slice* SC = csl < kDbSlices ? &TB.sl[csl] : slices + csl;
-            const int dd = ufl(SC->deblock_disabled);
-            PROF_LAP(2);
-            const bool active = (mf & 4) && dd != 1;
-            if (active) {
-                const int qm = (mf & 1) ? 0 : mqp;
-                const int tco = static_cast<int>(ufl(static_cast<uint32_t>(SC->tc_offset)));
-                const int beo = static_cast<int>(ufl(static_cast<uint32_t>(SC->beta_offset)));
-                const int cq0 = static_cast<int>(ufl(static_cast<uint32_t>(SC->cqp_offset[0])));
-                const int cq1 = static_cast<int>(ufl(static_cast<uint32_t>(SC->cqp_offset[1])));
-                const int saddr = static_cast<int>(ufl(static_cast<uint32_t>(SC->slice_addr_rs)));
-                const int tsaddr = row > 0 ? static_cast<int>(ufl(static_cast<uint32_t>(
-                                                 (tsl < kDbSlices ? TB.sl[tsl] : slices[tsl]).slice_addr_rs)))
-                                           : -1;
-                // the MB's nine threshold sets, one per lane, from the LDS tables in one pass:
-                // lane = 3 * component + (0 left MB edge, 1 top MB edge, 2 internal edges)
-                int ta = 0, tb = 0, tt = 0;
-                if (lane < 9) {
-                    const int kind = lane % 3, comp = lane / 3;
-                    const int qleft = (lmf & 1) ? 0 : lqp, qtop = (tmf & 1) ? 0 : tqp;
-                    const int qn = kind == 0 ? qleft : (kind == 1 ? qtop : qm);
-                    int qa;
-                    if (comp == 0) {
-                        qa = (qn + qm + 1) >> 1;
-                    } else {
-                        const int off = comp == 1 ? cq0 : cq1, lo = -6 * (bdc - 8);
-                        const int a = clip3(lo, 51, qn + off), b = clip3(lo, 51, qm + off);
-                        const int qpp = a < 30 ? a : TB.cqp[a - 30], qpq = b < 30 ? b : TB.cqp[b - 30];
-                        qa = (qpp + qpq + 1) >> 1;
-                    }
-                    const int ia = clip3(0, 51, qa + tco), ib = clip3(0, 51, qa + beo);
-                    const int sh = comp ? bdc - 8 : bd - 8;
-                    ta = TB.alpha[ia] << sh;
-                    tb = TB.beta[ib] << sh;
-                    tt = TB.tc0[ia] << sh;
-                }
-                // Each lane filters a whole line through all edges of a direction in registers, one
-                // LDS round trip per direction: lanes 0-15 luma rows / columns, 16-23 Cb, 24-31 Cr
-                // lines, all in one instruction stream (h264_filt_line).  A chroma line sits at
-                // v[2..11] so its MB edge and its internal edge fall on the luma positions 4 and 8;
-                // the luma-only edges 12 and 16 are off for it.  Edge e of a direction: the MB edge
-                // (e = 0, bS 4, if filtered at all) or internal (bS 3; luma e = 1, 3 not in
-                // 8x8-transform MBs).
-                const bool t8 = (mf & 2) != 0;
-                const bool luma_lane = lane < 16, chroma = lane >= 16;
-                const int cc = (lane >> 3) & 1, ck = lane & 7;  // chroma lanes: component, line
-                const int maxv = chroma ? (1 << bdc) - 1 : (1 << bd) - 1;
-                for (int dir = 0; dir < 2; dir++) {  // 0: vertical edges, 1: horizontal edges
-                    const bool vert = dir == 0;
-                    // left neighbour = the previous MB of this row (carried), top neighbour loaded
-                    const int nmf = vert ? (mx > 0 ? lmf : 0) : tmf;
-                    bool mb_edge = (nmf & 4) != 0;
-                    if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
-                    // threshold sets: 3 * component + (dir for the MB edge, 2 for internal edges)
-                    const int am = __builtin_amdgcn_readlane(ta, dir), bm = __builtin_amdgcn_readlane(tb, dir);
-                    const int ai = __builtin_amdgcn_readlane(ta, 2), bi = __builtin_amdgcn_readlane(tb, 2);
-                    const int ti = __builtin_amdgcn_readlane(tt, 2);
-                    const int amb = __builtin_amdgcn_readlane(ta, 3 + dir), amr = __builtin_amdgcn_readlane(ta, 6 + dir);
-                    const int bmb = __builtin_amdgcn_readlane(tb, 3 + dir), bmr = __builtin_amdgcn_readlane(tb, 6 + dir);
-                    const int aib = __builtin_amdgcn_readlane(ta, 5), air = __builtin_amdgcn_readlane(ta, 8);
-                    const int bib = __builtin_amdgcn_readlane(tb, 5), bir = __builtin_amdgcn_readlane(tb, 8);
-                    const int tib = __builtin_amdgcn_readlane(tt, 5), tir = __builtin_amdgcn_readlane(tt, 8);
-                    const int aM = luma_lane ? am : (cc ? amr : amb), bM = luma_lane ? bm : (cc ? bmr : bmb);
-                    const int aI = luma_lane ? ai : (cc ? air : aib), bI = luma_lane ? bi : (cc ? bir : bib);
-                    const int tI = luma_lane ? ti : (cc ? tir : tib);
-                    if (lane < 32) {
-                        // element i of the line at base + i * stp (chroma: base two steps before
-                        // the window line, so its samples land at v[2..11]; the other v are
-                        // loaded from inside the wave's own window and never used)
-                        const int stp = vert ? 1 : (luma_lane ? 20 : 10);
-                        const uint16_t* base = luma_lane ? (vert ? &w.y[lane + 4][0] : &w.y[0][lane + 4])
-                                                         : (vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2]) - 2 * stp;
-                        int v[20];
-#pragma unroll
-                        for (int i = 0; i < 20; i++) v[i] = base[i * stp];
-                        h264_filt_line<4>(v, mb_edge, 4, aM, bM, 0, maxv, chroma);
-                        h264_filt_line<8>(v, chroma || !t8, 3, aI, bI, tI, maxv, chroma);
-                        h264_filt_line<12>(v, luma_lane, 3, aI, bI, tI, maxv, chroma);
-                        h264_filt_line<16>(v, luma_lane && !t8, 3, aI, bI, tI, maxv, chroma);
-                        uint16_t* dst = const_cast<uint16_t*>(base);
-#pragma unroll
-                        for (int i = 1; i < 19; i++)
-                            if (luma_lane || (i >= 3 && i <= 8)) dst[i * stp] = static_cast<uint16_t>(v[i]);
-                    }
-                    wave_sync();
-                    PROF_LAPK(dir * 4);
-                }
-            }
-            lmf = mf;
-            lqp = mqp;
-            lsaddr = static_cast<int>(ufl(static_cast<uint32_t>(SC->slice_addr_rs)));
-            // write back, every sample once and only when final, 4 (luma) / 4 (chroma) samples per
-            // lane store.  A sample of MB (x, y) is last changed by this MB's own edges, by MB
-            // (x + 1, y)'s left edge (columns 13..15, chroma 7) or by MB (x, y + 1)'s top edge
-            // (rows 13..15, chroma 7).  So at MB (x, y): rows 12..15 of MB (x, y - 1) (top edge
-            // just filtered; its right columns were finished by the row above) and rows 0..11 of
-            // MB (x - 1, y) (left edge just filtered; 0..15 on the picture's last row, where no row
-            // follows) are final; the last MB of a row also stores its own rows.  Rows 12..15 of a
-            // band's last row are stored by the band below (they reach it through the boundary
-            // buffer), so the two workgroups never write the same line.
-            {
-                const bool last_row = row == mbh - 1;
-                const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
-                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][64] | chroma [2][2][32]
-                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][64] | chroma [2][8][32]
-                auto put4 = [&](Pel* d, uint32_t a, uint32_t b, uint32_t c2_, uint32_t d2) __attribute__((always_inline)) {
-                    d[0] = static_cast<Pel>(a); d[1] = static_cast<Pel>(b); d[2] = static_cast<Pel>(c2_); d[3] = static_cast<Pel>(d2);
-                };
-                // rows 12..15 of the MB above, staged at its 4-MB group column
-                if (row > 0 && lane < 16) {
-                    const int tr = lane >> 2, c4 = (lane & 3) * 4;
-                    put4(SA + tr * 64 + (mx & 3) * 16 + c4, w.y[tr][c4 + 4], w.y[tr][c4 + 5], w.y[tr][c4 + 6], w.y[tr][c4 + 7]);
-                } else if (row > 0 && lane >= 16 && lane < 24) {  // chroma rows 6..7
-                    const int k = lane - 16, cc = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
-                    put4(SA + 256 + (cc * 2 + cr) * 32 + (mx & 3) * 8 + c4, w.c[cc][cr][c4 + 2], w.c[cc][cr][c4 + 3],
-                         w.c[cc][cr][c4 + 4], w.c[cc][cr][c4 + 5]);
-                }
-                if (row > 0 && ((mx & 3) == 3 || mx == mbw - 1)) {  // the group's rows 12..15 out
-                    wave_sync();
-                    const int g0 = mx & ~3, nmb = mx - g0 + 1;
-                    const int tr = lane >> 4, sg = lane & 15;  // luma: 4 rows x 16 segments of 4
-                    if (sg < 4 * nmb) db264_copy<Pel, 4>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * 4, SA + tr * 64 + sg * 4);
-                    if (lane < 32) {  // chroma: 2 comps x 2 rows x 8 segments of 4
-                        const int cc = lane >> 4, cr = (lane >> 3) & 1, cs = lane & 7;
-                        if (cs < 2 * nmb)
-                            db264_copy<Pel, 4>(PC[cc] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * 4, SA + 256 + (cc * 2 + cr) * 32 + cs * 4);
-                    }
-                }
-                // this row's final rows: the previous MB (columns 0..11 saved, 12..15 in the window)
-                // and, on the row's last MB, the MB itself; staged at their group columns
-                auto flush_b = [&](int g0, int nmb) __attribute__((always_inline)) {
-                    wave_sync();
-                    const int r = lane >> 2, sg = lane & 3;  // luma: 16 rows x 4 segments of 16
-                    if (r < nr && sg < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sg * 16, SB + r * 64 + sg * 16);
-                    const int cc = lane >> 5, cr = (lane >> 2) & 7;  // chroma: 2 comps x 8 rows x 4 segments of 8
-                    if (cr < ncr && sg < nmb)
-                        db264_copy<Pel, 8>(PC[cc] + (row * 8 + cr) * stc + g0 * 8 + sg * 8, SB + 1024 + (cc * 8 + cr) * 32 + sg * 8);
-                };
-                if (mx > 0) {
-                    const int sx = ((mx - 1) & 3) * 16;
-                    if (lane < nr * 4) {
-                        const int r = lane >> 2, c4 = (lane & 3) * 4;
-                        uint32_t v0, v1, v2, v3;
-                        if (c4 < 12) { v0 = w.py[r][c4]; v1 = w.py[r][c4 + 1]; v2 = w.py[r][c4 + 2]; v3 = w.py[r][c4 + 3]; }
-                        else { v0 = w.y[r + 4][0]; v1 = w.y[r + 4][1]; v2 = w.y[r + 4][2]; v3 = w.y[r + 4][3]; }
-                        put4(SB + r * 64 + sx + c4, v0, v1, v2, v3);
-                    }
-                    if (lane < 4 * ncr) {  // chroma: column 7 in the window
-                        const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
-                        const uint32_t v3 = c4 ? w.c[cc][cr + 2][1] : w.pc[cc][cr][3];
-                        put4(SB + 1024 + (cc * 8 + cr) * 32 + (sx >> 1) + c4, w.pc[cc][cr][c4], w.pc[cc][cr][c4 + 1],
-                             w.pc[cc][cr][c4 + 2], v3);
-                    }
-                    if (((mx - 1) & 3) == 3) flush_b(mx - 4, 4);
-                }
-                // this MB's columns 0..11 / chroma 0..6 wait for the next MB (in-order LDS: the reads
-                // above have returned their values before these writes land)
-                for (int i = lane; i < 192; i += 64) w.py[i / 12][i % 12] = w.y[i / 12 + 4][i % 12 + 4];
-                if (lane < 64) {
-                    const int cc = lane >> 5, k = lane & 31, cr = k >> 2, c2 = (k & 3) * 2;
-                    w.pc[cc][cr][c2] = w.c[cc][cr + 2][c2 + 2];
-                    w.pc[cc][cr][c2 + 1] = w.c[cc][cr + 2][c2 + 3];
-                }
-                if (mx == mbw - 1) {  // the row's last MB: nothing to its right, its rows are final now
-                    const int sx = (mx & 3) * 16;
-                    if (lane < nr * 4) {
-                        const int r = lane >> 2, c4 = (lane & 3) * 4;
-                        put4(SB + r * 64 + sx + c4, w.y[r + 4][c4 + 4], w.y[r + 4][c4 + 5], w.y[r + 4][c4 + 6], w.y[r + 4][c4 + 7]);
-                    }
-                    if (lane < 4 * ncr) {
-                        const int cc = lane / (2 * ncr), k = lane - cc * 2 * ncr, cr = k >> 1, c4 = (k & 1) * 4;
-                        put4(SB + 1024 + (cc * 8 + cr) * 32 + (sx >> 1) + c4, w.c[cc][cr + 2][c4 + 2], w.c[cc][cr + 2][c4 + 3],
-                             w.c[cc][cr + 2][c4 + 4], w.c[cc][cr + 2][c4 + 5]);
-                    }
-                    flush_b(mx & ~3, (mx & 3) + 1);
-                }
-            }
-            // line buffer for the row below: the MB's bottom rows (columns final so far) and
-            // the previous MB's last columns, which this MB's left edge has just finished
-            if (to_band) {  // the same, into the boundary buffer of the band below
-                uint16_t* X = reinterpret_cast<uint16_t*>(arena + o_xout);
-                const bool last = mx == mbw - 1;
-                const int tr = lane >> 4, tc = lane & 15;
-                if (tc < 12 || last)
-                    __hip_atomic_store(X + tr * width + mx * 16 + tc, w.y[tr + 16][tc + 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (mx > 0 && tc < 4)
-                    __hip_atomic_store(X + tr * width + mx * 16 - 4 + tc, w.y[tr + 16][tc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lane < 32) {
-                    const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
-                    uint16_t* XC = X + 4 * width + (cc * 2 + cr) * cw + mx * 8;
-                    if (ck < 6 || last)
-                        __hip_atomic_store(XC + ck, w.c[cc][cr + 8][ck + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (mx > 0 && ck < 2)
-                        __hip_atomic_store(XC - 2 + ck, w.c[cc][cr + 8][ck], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): picture and boundary stores have completed
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0)
-                    __hip_atomic_store(reinterpret_cast<uint32_t*>(arena + o_flag) + 4 * (row * mbw),
-                                       static_cast<uint32_t>(mbw + mx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (row + 1 < mbh) {
-                const bool last = mx == mbw - 1;
-                const int tr = lane >> 4, tc = lane & 15;  // rows 12..15 of this MB
-                if (tc < 12 || last) LY[tr * width + mx * 16 + tc] = w.y[tr + 16][tc + 4];
-                if (mx > 0 && tc < 4) LY[tr * width + mx * 16 - 4 + tc] = w.y[tr + 16][tc];
-                if (lane < 32) {  // chroma rows 6..7
-                    const int cc = lane >> 4, cr = (lane >> 3) & 1, ck = lane & 7;
-                    if (ck < 6 || last) LC[(cc * 2 + cr) * cw + mx * 8 + ck] = w.c[cc][cr + 8][ck + 2];
-                    if (mx > 0 && ck < 2) LC[(cc * 2 + cr) * cw + mx * 8 - 2 + ck] = w.c[cc][cr + 8][ck];
-                }
-            }
-            wave_sync();
-            // carry the last columns into the next MB's left strip
-            if (lane < 64) {
-                const int r = lane >> 2, k = lane & 3;
-                w.y[r + 4][k] = w.y[r + 4][k + 16];
-            }
-            if (lane < 32) {
-                const int cc = lane >> 4, r = (lane >> 1) & 7, k = lane & 1;
-                w.c[cc][r + 2][k] = w.c[cc][r + 2][k + 8];
-            }
-            wave_sync();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0)
-                __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            PROF_LAP(3);
-            PROF_ADD(6, 1);
-        }
-    }
-    PROF_FLUSH();
-}
-
-__global__ void __launch_bounds__(64 * kAvcDbWaves) h2j_k2_deblock264(const h2j_frame* frames, const h2j_ctb* ctbs,
-                                                                    const h2j_slice* slices, uint8_t* arena,
-                                                                    const uint32_t* map) {
-    // LDS: windows | progress | tables | line buffer (db264_lds_bytes)
-    extern __shared__ __align__(16) uint8_t dblds[];
-    DbWin* W = reinterpret_cast<DbWin*>(dblds);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * kAvcDbWaves);
-    DbTables& TB = *reinterpret_cast<DbTables*>(dblds + sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4);
-    uint16_t* line = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(&TB) + sizeof(DbTables));
-    const uint32_t me = map[blockIdx.x];  // same (picture, band) map as K1
-    const h2j_frame& f = frames[me >> 8];
-    const int band = static_cast<int>(me & 0xFF);
-    if (f.codec != H2J_CODEC_H264) return;
-    const int nbands = ufl(f.k1bands);
-    const h2j_ctb* C = ctbs + f.ctb;
-    const h2j_slice* S = slices + f.slice;
-    const int t = threadIdx.x;
-    if (t < 2 * kAvcDbWaves) prog[t] = 0;
-    if (t < 52) {
-        TB.alpha[t] = kAlpha264[t];
-        TB.beta[t] = kBeta264[t];
-        TB.tc0[t] = kTc0_264[t][2];
-    }
-    if (t < 22) TB.cqp[t] = kChromaQp264[t];
-    const int nsl = min(static_cast<int>(ufl(f.nslice)), kDbSlices);
-    if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
-        reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
-    __syncthreads();
-    if (f.bit_depth == 8) h264_db_rows<uint8_t>(f, C, S, arena, W, prog, line, band, nbands, TB);
-    else h264_db_rows<uint16_t>(f, C, S, arena, W, prog, line, band, nbands, TB);
-}
 
 // ---- H.264 K2, two macroblock rows per wave (fill the wave).  A workgroup of
 // kDbPairWaves waves deblocks a picture (or a 16-row band of a tall one); wave w takes the row
@@ -4048,9 +3632,9 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
         }
         if (vacc) {  // luma of a sao_sums_variance picture: K4a's sums, per MB of the CTB
             // output rows below the picture repeat its last row (jpeg_sample), so that row counts
-            // for them too; rows / columns outside the output count 0
+            // for them too; rows / columns outside the output (above / left of the crop window too) count 0
             const int oy = g.y0 + y - f.crop_y, ox = g.x0 + x - f.crop_x, last = f.out_h - 1;
-            const unsigned wgt = (oy < 0 || ox >= f.out_w) ? 0u : (oy < last ? 1u : (oy == last ? 16u - (last & 15) : 0u));
+            const unsigned wgt = (oy < 0 || ox < 0 || ox >= f.out_w) ? 0u : (oy < last ? 1u : (oy == last ? 16u - (last & 15) : 0u));
             if (wgt) {
                 unsigned s4 = 0, n4 = 0;
 #pragma unroll
@@ -4160,7 +3744,7 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
             unsigned long long t = 0;
             if (tid < (1 << (2 * l2m))) {
                 const int oy0 = gy.y0 - f.crop_y + ((tid >> l2m) << 4), ox0 = gy.x0 - f.crop_x + ((tid & ((1 << l2m) - 1)) << 4);
-                if (oy0 >= 0 && oy0 < f.out_h && ox0 < f.out_w) {
+                if (oy0 >= 0 && oy0 < f.out_h && ox0 >= 0 && ox0 < f.out_w) {
                     const unsigned long long a = L.var[tid];
                     const unsigned sm = static_cast<unsigned>(a >> 32), n = static_cast<unsigned>(a);
                     t = (n - ((sm * sm) >> 8) + 500 + 128) >> 8;
@@ -4735,8 +4319,6 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     if (!attr) {
         const void* fns[] = {reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint16_t, kK1WavesWide>),
-                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint8_t>),
-                             reinterpret_cast<const void*>(h2j_k1_recon_hevc_pic<uint16_t>),
                              reinterpret_cast<const void*>(h2j_k1_recon_h264),
                              reinterpret_cast<const void*>(h2j_k1_recon_any),
                              reinterpret_cast<const void*>(h2j_k1_recon_hevc_pool<uint8_t>),
@@ -4749,26 +4331,17 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         (void)hipGetLastError();  // attribute calls must not leave an error for the launch checks
         attr = true;
     }
-    static const int pool_p = [] {  // H2J_K1_POOL: max pictures per pool workgroup (0: h2j_k1_recon_hevc_pic)
-        const char* e = std::getenv("H2J_K1_POOL");
-        return e ? std::max(0, std::min(8, std::atoi(e))) : 4;
-    }();
-    static const bool merge = [] {  // H2J_K1_MERGE=0: separate launches per kind (A/B timing)
-        const char* e = std::getenv("H2J_K1_MERGE");
-        return !(e && e[0] == '0');
-    }();
+    constexpr int pool_p = 4;  // max pictures per pool workgroup
     const size_t line_bytes = 2 * (static_cast<size_t>(b->max_w) + 64) * sizeof(int16_t);
-    const size_t ybytes = (k1_fixed_lds(kYWaves) + line_bytes + 15) & ~size_t(15);   // luma group of a picture workgroup
-    const size_t pbytes = ybytes + k1_fixed_lds(kCWaves) + line_bytes;                 // the whole picture workgroup
     const size_t wbytes = k1_fixed_lds(kK1WavesWide) + line_bytes;
     // merged launch: an HEVC picture workgroup runs the pool's job loop with P = 1 (hevc_pool_jobs)
     const size_t pool1 = k1_pool_lds(1, (b->max_h + 15) / 16, 2 * b->max_w + 192);
     const size_t lds_any = std::max(std::max(pool1, lds264), wbytes);
     // one launch for every kind of picture (unless the widest picture's line buffers would not
     // fit one workgroup's LDS: then the per-kind launches below)
-    if (merge && !wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
+    if (!wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
         hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
-                           b->arena, b->k1all, static_cast<uint32_t>(ybytes));
+                           b->arena, b->k1all);
         return check(hipGetLastError(), "h2j_k1_recon_any");
     }
     // per-kind launches: H.264 on a companion stream forked from (and joined back into) the
@@ -4793,19 +4366,14 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
             const dim3 grid(b->nframes, 2), block(64 * kK1WavesWide);
             if (p8) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint8_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
             if (p16) hipLaunchKernelGGL((h2j_k1_recon_hevc<uint16_t, kK1WavesWide>), grid, block, lds, s, b->frames, b->tus, b->arena);
-        } else if (pool_p > 0) {
+        } else {
             // pictures per pool workgroup: at least 256 workgroups (one per CU) per launch, as
             // many pictures each as fit (LDS: one set of line buffers + progress words per picture)
             const int maxrows = (b->max_h + 15) / 16;
             const int lstride = 2 * b->max_w + 192, lchroma = b->max_w + 64;
-            // LDS: the pool's layout + the staging tiles (k1_pool_stage_lds) of the launch's sample size;
-            // H2J_K1_STAGE=0: quadrants stored one by one (A/B timing)
-            static const bool staged = [] {
-                const char* e = std::getenv("H2J_K1_STAGE");
-                return !(e && e[0] == '0');
-            }();
+            // LDS: the pool's layout + the staging tiles (k1_pool_stage_lds) of the launch's sample size
             auto pool_lds = [&](int P, int pel) {
-                return ((k1_pool_lds(P, maxrows, lstride) + 15) & ~size_t(15)) + (staged ? k1_pool_stage_lds(pel) : 0);
+                return ((k1_pool_lds(P, maxrows, lstride) + 15) & ~size_t(15)) + k1_pool_stage_lds(pel);
             };
             for (int pel = 1; pel <= 2; pel++) {
                 if (!(pel == 1 ? p8 : p16)) continue;
@@ -4818,20 +4386,10 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
                 }
                 const dim3 grid((b->nframes + P - 1) / P), block(64 * kPoolWaves);
                 if (pel == 1) hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint8_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
-                                                 b->nframes, P, maxrows, lstride, lchroma, staged ? 1 : 0);
+                                                 b->nframes, P, maxrows, lstride, lchroma, 1);
                 else hipLaunchKernelGGL(h2j_k1_recon_hevc_pool<uint16_t>, grid, block, lds, s, b->frames, b->tus, b->arena,
-                                        b->nframes, P, maxrows, lstride, lchroma, staged ? 1 : 0);
+                                        b->nframes, P, maxrows, lstride, lchroma, 1);
             }
-        } else {
-            if (pbytes > 160 * 1024) {
-                snprintf(g_err, sizeof(g_err), "h2j_k1_recon_hevc_pic: %zu B of LDS per workgroup (max 160 KB)", pbytes);
-                return -1;
-            }
-            const dim3 grid(b->nframes), block(64 * (kYWaves + kCWaves));
-            if (p8) hipLaunchKernelGGL(h2j_k1_recon_hevc_pic<uint8_t>, grid, block, pbytes, s, b->frames, b->tus, b->arena,
-                                       static_cast<uint32_t>(ybytes));
-            if (p16) hipLaunchKernelGGL(h2j_k1_recon_hevc_pic<uint16_t>, grid, block, pbytes, s, b->frames, b->tus, b->arena,
-                                        static_cast<uint32_t>(ybytes));
         }
         int r = check(hipGetLastError(), "h2j_k1_recon_hevc");
         if (ax) (void)hipStreamWaitEvent(s, ax->join, 0);
@@ -4866,53 +4424,29 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         if (r) return r;
     }
     if (!b->has_h264) return 0;
-    // H2J_DB264=rows: one MB row per wave (h2j_k2_deblock264, A/B timing); default two
-    static const bool rows = [] {
-        const char* e = std::getenv("H2J_DB264");
-        return e && std::strcmp(e, "rows") == 0;
-    }();
-    static size_t cap[2] = {0, 0};  // dynamic LDS limit per kernel: 160 KB minus its static LDS
-    if (!cap[0]) {  // (line buffers of pictures wider than ~3.6K need more than the 64 KB default)
-        const void* fns[2] = {reinterpret_cast<const void*>(h2j_k2_deblock264), reinterpret_cast<const void*>(h2j_k2_deblock264p)};
-        for (int i = 0; i < 2; i++) {
-            hipFuncAttributes fa{};
-            const size_t st = hipFuncGetAttributes(&fa, fns[i]) == hipSuccess ? fa.sharedSizeBytes : 0;
-            cap[i] = 160 * 1024 - st;
-            (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(cap[i]));
-        }
+    static size_t cap = 0;  // dynamic LDS limit: 160 KB minus the kernel's static LDS
+    if (!cap) {  // (line buffers of pictures wider than ~3.6K need more than the 64 KB default)
+        const void* fn = reinterpret_cast<const void*>(h2j_k2_deblock264p);
+        hipFuncAttributes fa{};
+        const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
+        cap = 160 * 1024 - st;
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(cap));
         (void)hipGetLastError();
     }
     if (b->k1wgs <= 0) return 0;
-    if (rows) {
-        const size_t lds = sizeof(DbWin) * kAvcDbWaves + 2 * kAvcDbWaves * 4 + sizeof(DbTables) + 12 * static_cast<size_t>(b->max_w);
-        hipLaunchKernelGGL(h2j_k2_deblock264, dim3(b->k1wgs), dim3(64 * kAvcDbWaves), lds, s, b->frames, b->ctbs,
-                           b->slices, b->arena, b->k1map);
-        return check(hipGetLastError(), "h2j_k2_deblock264");
-    }
     const size_t fixed = sizeof(DbWin) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
-    const int line_w = std::min(b->max_w, static_cast<int>((cap[1] - fixed) / 12) & ~15);
+    const int line_w = std::min(b->max_w, static_cast<int>((cap - fixed) / 12) & ~15);
     hipLaunchKernelGGL(h2j_k2_deblock264p, dim3(b->k1wgs), dim3(64 * kDbPairWaves), fixed + 12 * static_cast<size_t>(line_w), s,
                        b->frames, b->ctbs, b->slices, b->arena, b->k1map, line_w);
     return check(hipGetLastError(), "h2j_k2_deblock264p");
 }
-
-// H2J_SAO_VAR=0: K4a sums every picture's MB variances (A/B timing); default K3 sums them for
-// the pictures sao_sums_variance admits
-static int sao_var_fold() {
-    static const int v = [] {
-        const char* e = std::getenv("H2J_SAO_VAR");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v;
-}
-int h2j_gpu_sao_var_fold(void) { return sao_var_fold(); }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0 || !b->has_hevc) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     // CTB grid of the largest picture at the smallest CTB size present is bounded by max_ctbs
     dim3 grid(static_cast<unsigned>(b->max_ctbs), b->nframes);
-    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, sao_var_fold());
+    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
     return check(hipGetLastError(), "h2j_k3_sao");
 }
 
@@ -4921,7 +4455,7 @@ int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int mbs = b->max_mcu;
     if (b->k4a_frames > 0) {  // none: K3 has summed every picture's MB variances
-        hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena, sao_var_fold());
+        hipLaunchKernelGGL(h2j_k4a_variance, dim3((mbs + 15) / 16, b->nframes), dim3(256), 0, s, b->frames, b->arena, 1);
         const int r = check(hipGetLastError(), "h2j_k4a_variance");
         if (r) return r;
     }

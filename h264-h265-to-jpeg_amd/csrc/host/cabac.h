@@ -81,6 +81,7 @@ public:
         uint64_t v = value_;
         const uint64_t vl = value_ - scaled;
         uint32_t is_lps = 0;
+#if defined(__x86_64__)
         // one compare, then conditional moves (the compiler turns a C select of these into a
         // branch, mispredicted on every LPS bin)
         __asm__("cmpq %[sc], %[v]\n\t"
@@ -92,6 +93,14 @@ public:
                 : [v] "+r"(v), [r] "+r"(r), [sh] "+r"(sh), [nx] "+r"(nx), [il] "+q"(is_lps)
                 : [sc] "r"(scaled), [vl] "r"(vl), [lr] "r"(lr), [ls] "r"(lsh), [nl] "r"(nl)
                 : "cc");
+#else
+        // portable form (other targets): the same selects in C
+        is_lps = v >= scaled ? 1u : 0u;
+        v = is_lps ? vl : v;
+        r = is_lps ? lr : r;
+        sh = is_lps ? lsh : sh;
+        nx = is_lps ? nl : nx;
+#endif
         value_ = v;
         range_ = r;
         bits_ -= static_cast<int>(sh);

@@ -442,10 +442,6 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const size_t o_ctbs = align_up(o_coefs + ncoef * sizeof(h2j_coef), 256);
     const size_t o_slices = align_up(o_ctbs + nctb * sizeof(h2j_ctb), 256);
     const size_t o_sl = align_up(o_slices + nslice * sizeof(h2j_slice), 256);
-    static const bool balance = [] {  // H2J_K1_BALANCE=0: H.264 K1 workgroups in frame order (A/B timing)
-        const char* e = std::getenv("H2J_K1_BALANCE");
-        return !(e && e[0] == '0');
-    }();
     // H.264 K1 workgroup map: banded pictures first (their long chains start early), bands in order,
     // then the others by transform-block count, most first (the dispatcher hands workgroups out in
     // map order: the heaviest pictures start in the first round, not in the launch's tail)
@@ -461,8 +457,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
             const h2j_frame& f = s.frames[k];
             if (f.codec == H2J_CODEC_H264 && f.k1bands <= 1) un.emplace_back(f.ntu, static_cast<uint32_t>(k));
         }
-        if (balance)
-            std::stable_sort(un.begin(), un.end(), [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
+        std::stable_sort(un.begin(), un.end(), [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
                 return a.first > b.first;
             });
         for (const auto& x : un) k1map.push_back(x.second << 8);
@@ -560,9 +555,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.arena = static_cast<uint8_t*>(s.d_arena.p);
     b.jpeg_dense = entropy ? 0 : 1;
     {  // pictures whose MB variances K4a sums (K3 sums the others'; no K4a launch when none is left)
-        static const int fold = h2j_gpu_sao_var_fold();
         int k4a = 0;
-        for (int k = 0; k < nf; k++) k4a += (fold && h2j_sao_folds_variance(s.frames[k])) ? 0 : 1;
+        for (int k = 0; k < nf; k++) k4a += h2j_sao_folds_variance(s.frames[k]) ? 0 : 1;
         b.k4a_frames = k4a;
     }
     b.seg = entropy ? static_cast<uint8_t*>(s.d_seg.p) : nullptr;
@@ -1032,15 +1026,9 @@ static int single_job(h2j_engine* w, const uint8_t* data, size_t size) {
     return 0;
 }
 
-int h2j_engine_decode(h2j_engine* w, const uint8_t* data, size_t size, int stage, uint16_t* planes_out,
-                      size_t cap, int* info) {
-    if (!w) return -1;
-    Engine& e = w->e;
-    if (single_job(w, data, size)) return -2;
-    const int stages = stage == 1 ? 1 : (stage == 2 ? 2 : 3);
-    Slot& s = e.slot[0];
-    if (e.enqueue(s, stages, false) || e.sync(s)) return -3;
-    const h2j_frame& f = s.frames[0];
+// copy picture k of slot s (after sync) out as uint16 cropped planes
+static int copy_planes(Engine& e, Slot& s, int k, int stage, uint16_t* planes_out, size_t cap, int* info) {
+    const h2j_frame& f = s.frames[k];
     const int w_ = f.out_w, h_ = f.out_h;
     const size_t need = static_cast<size_t>(w_) * h_ * 3 / 2;
     info[0] = w_;
@@ -1066,6 +1054,43 @@ int h2j_engine_decode(h2j_engine* w, const uint8_t* data, size_t size, int stage
             }
     }
     return 0;
+}
+
+int h2j_engine_decode(h2j_engine* w, const uint8_t* data, size_t size, int stage, uint16_t* planes_out,
+                      size_t cap, int* info) {
+    if (!w) return -1;
+    Engine& e = w->e;
+    if (single_job(w, data, size)) return -2;
+    const int stages = stage == 1 ? 1 : (stage == 2 ? 2 : 3);
+    Slot& s = e.slot[0];
+    if (e.enqueue(s, stages, false) || e.sync(s)) return -3;
+    return copy_planes(e, s, 0, stage, planes_out, cap, info);
+}
+
+int h2j_engine_decode_batch(h2j_engine* w, int n, const uint8_t* const* data, const size_t* sizes, int stage, int pick,
+                            uint16_t* planes_out, size_t cap, int* info) {
+    if (!w || n <= 0 || pick < 0 || pick >= n) return -1;
+    Engine& e = w->e;
+    e.quiesce();
+    if (h2j_gpu_set_device(e.device)) return e.fail(h2j_gpu_last_error());
+    e.jobs.resize(n);
+    std::vector<int> rc(n, 0);
+    e.par(n, [&](int i) {
+        e.jobs[i].threads = 1;
+        rc[i] = h2j::parse_any(data[i], sizes[i], e.jobs[i]);
+    });
+    for (int i = 0; i < n; i++)
+        if (rc[i]) {
+            e.fail("parse failed (picture " + std::to_string(i) + "): " + e.jobs[i].message);
+            return -2;
+        }
+    Slot& s = e.slot[0];
+    s.live.resize(n);
+    for (int i = 0; i < n; i++) s.live[i] = i;
+    s.jobs = &e.jobs;
+    const int stages = stage == 1 ? 1 : (stage == 2 ? 2 : 3);
+    if (e.enqueue(s, stages, false) || e.sync(s)) return -3;
+    return copy_planes(e, s, pick, stage, planes_out, cap, info);
 }
 
 int h2j_engine_jpeg_coeffs(h2j_engine* w, const uint8_t* data, size_t size, int16_t* out, size_t cap, int* info) {
@@ -1108,7 +1133,13 @@ const char* h2j_engine_frame_error(h2j_engine* w, int i) {
     case -50: return "output buffer too small";
     case -51: return "JPEG payload pool overflow";
     case -52: return "device-side failure (a K1 / deblocking progress wait timed out)";
-    default: return i < static_cast<int>(w->e.last_msg.size()) ? w->e.last_msg[i].c_str() : "";
+    default: {
+        // copied under the lock into a per-thread buffer: h2j_engine_wait on another thread may
+        // replace last_msg (and free its strings) as soon as the lock is released
+        static thread_local std::string buf;
+        buf = i < static_cast<int>(w->e.last_msg.size()) ? w->e.last_msg[i] : std::string();
+        return buf.c_str();
+    }
     }
 }
 

@@ -117,7 +117,8 @@ struct Sps {
     uint8_t sl8[6][64];
 };
 
-// E.1.2 hrd_parameters (skipped)
+// E.1.2 hrd_parameters (skipped); false on cpb_cnt_minus1 > 31, which FFmpeg 4.3 h264_ps.c
+// rejects ("cpb_count %d invalid": the VUI and with it the SPS fail)
 bool skip_hrd(BitReader& b) {
     const uint32_t cnt = b.ue();
     if (cnt > 31) return false;
@@ -133,7 +134,9 @@ bool skip_hrd(BitReader& b) {
 
 // E.1.1 vui_parameters, read as far as max_num_reorder_frames: FFmpeg (h264_slice.c) takes the
 // output delay from it when bitstream_restriction_flag is set.  Returns the reorder depth, 0 when
-// the VUI carries none or is truncated (FFmpeg then keeps no delay either).
+// the VUI carries none or is truncated (FFmpeg then keeps no delay either), -1 where FFmpeg 4.3
+// h264_ps.c fails the SPS: an HRD with more than 32 CPBs, or max_num_reorder_frames > 16
+// ("Clipping illegal num_reorder_frames", AVERROR_INVALIDDATA).
 int parse_vui_reorder(BitReader& b) {
     if (b.u(1) && b.u(8) == 255) b.u(32);  // aspect_ratio_idc, Extended_SAR
     if (b.u(1)) b.u(1);                    // overscan
@@ -147,9 +150,9 @@ int parse_vui_reorder(BitReader& b) {
     }
     if (b.u(1)) b.u(32), b.u(32), b.u(1);  // timing_info
     const bool nal = b.u(1) != 0;
-    if (nal && !skip_hrd(b)) return 0;
+    if (nal && !skip_hrd(b)) return -1;
     const bool vcl = b.u(1) != 0;
-    if (vcl && !skip_hrd(b)) return 0;
+    if (vcl && !skip_hrd(b)) return -1;
     if (nal || vcl) b.u(1);  // low_delay_hrd_flag
     b.u(1);                  // pic_struct_present_flag
     if (!b.u(1)) return 0;   // bitstream_restriction_flag
@@ -161,7 +164,7 @@ int parse_vui_reorder(BitReader& b) {
     const uint32_t reorder = b.ue();
     b.ue();  // max_dec_frame_buffering
     if (b.overrun()) return 0;
-    return reorder > 16 ? 16 : static_cast<int>(reorder);
+    return reorder > 16 ? -1 : static_cast<int>(reorder);
 }
 
 struct Pps {
@@ -278,7 +281,10 @@ int parse_sps(BitReader& b, Sps* tab) {
         s.crop_b = static_cast<int>(cb) * 2;
     }
     if (b.overrun()) return -1;
-    if (b.u(1)) s.num_reorder_frames = parse_vui_reorder(b);
+    if (b.u(1)) {
+        s.num_reorder_frames = parse_vui_reorder(b);
+        if (s.num_reorder_frames < 0) return -1;
+    }
     if (s.chroma_format_idc != 1 || s.bit_depth > 10 || s.bit_depth_c != s.bit_depth) return -4;
     s.valid = true;
     return 0;

@@ -46,6 +46,10 @@ def load_library() -> ctypes.CDLL:
     lib.h2j_engine_decode.restype = ctypes.c_int
     lib.h2j_engine_decode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_uint16), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
+    lib.h2j_engine_decode_batch.restype = ctypes.c_int
+    lib.h2j_engine_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(u8p), szp, ctypes.c_int,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_uint16), ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_int)]
     lib.h2j_engine_jpeg_coeffs.restype = ctypes.c_int
     lib.h2j_engine_jpeg_coeffs.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int16),
                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
@@ -190,6 +194,26 @@ class Engine:
                                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), cap, info)
         if rc < 0:
             raise RuntimeError(f"h2j_engine_decode failed ({rc}): {self.error()}")
+        return self._planes(out, info)
+
+    def decode_batch(self, streams: Sequence[bytes], pick: int, stage: int = 0):
+        """Planes of picture `pick` of `streams` reconstructed as one GPU batch (the launch shapes
+        of a production chunk of that many pictures)."""
+        n = len(streams)
+        bufs = [_u8(s) for s in streams]
+        ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+        sizes = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+        cap = 8192 * 8192 * 3 // 2
+        out = np.zeros(cap, dtype=np.uint16)
+        info = (ctypes.c_int * 3)()
+        rc = self._lib.h2j_engine_decode_batch(self._h, n, ptrs, sizes, int(stage), int(pick),
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), cap, info)
+        if rc < 0:
+            raise RuntimeError(f"h2j_engine_decode_batch failed ({rc}): {self.error()}")
+        return self._planes(out, info)
+
+    @staticmethod
+    def _planes(out, info):
         w, h, bd = info[0], info[1], info[2]
         ys = w * h
         cs = (w // 2) * (h // 2)

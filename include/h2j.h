@@ -35,7 +35,8 @@ int h2j_device_count(void);
 h2j_engine *h2j_engine_create(int device, int host_threads);
 void h2j_engine_destroy(h2j_engine *e);
 const char *h2j_engine_error(h2j_engine *e);
-/* Message of picture i of the last h2j_engine_transcode ("" if it succeeded). */
+/* Message of picture i of the last h2j_engine_transcode ("" if it succeeded).  The string stays
+ * valid until the calling thread's next h2j_engine_frame_error call. */
 const char *h2j_engine_frame_error(h2j_engine *e, int i);
 /* Host placement: out[0] threads (incl. the caller), [1] the device's NUMA node (-1 unknown),
  * [2] CPUs the workers are pinned to (0: not pinned), [3] first of those CPUs. */
@@ -68,6 +69,11 @@ int h2j_engine_wait(h2j_engine *e, int64_t ticket);
  * info[0..2] = w, h, bit_depth. */
 int h2j_engine_decode(h2j_engine *e, const uint8_t *data, size_t size, int stage, uint16_t *planes_out,
                       size_t cap_elems, int *info);
+/* The same for picture `pick` of n pictures reconstructed as ONE GPU batch (the launch shapes of
+ * a production chunk of n pictures: K1's picture pool with up to 4 pictures per workgroup at
+ * n >= 1024), so parity tests can read planes from inside a bench-sized batch. */
+int h2j_engine_decode_batch(h2j_engine *e, int n, const uint8_t *const *data, const size_t *sizes, int stage,
+                            int pick, uint16_t *planes_out, size_t cap_elems, int *info);
 /* JPEG coefficients int16 [mcu][6][64] zigzag of the decoded picture;
  * info[0..3] = w, h, qscale, nmcu. */
 int h2j_engine_jpeg_coeffs(h2j_engine *e, const uint8_t *data, size_t size, int16_t *out, size_t cap_elems,

@@ -65,9 +65,8 @@ constexpr long long h2j_res_elems(int w, int h, int log2ctb) {
     return h2j_res_plane(w, h, h2j_res_q(log2ctb, 0)) + 2 * h2j_res_plane(w / 2, h / 2, h2j_res_q(log2ctb, 1));
 }
 /* K3 SAO sums the JPEG rate control's MB variances of a picture (K4a skips it) when the picture
- * has SAO (its own output plane) and its 16x16 output MB grid is aligned with the CTB grid; only
- * while h2j_gpu_sao_var_fold() is 1 (H2J_SAO_VAR=0 turns the fold off).  (constexpr: host and
- * device code share it) */
+ * has SAO (its own output plane) and its 16x16 output MB grid is aligned with the CTB grid.
+ * (constexpr: host and device code share it) */
 constexpr bool h2j_sao_folds_variance(const h2j_frame &f) {
     return f.codec == H2J_CODEC_HEVC && f.pic2 != f.pic && (f.crop_x & 15) == 0 && (f.crop_y & 15) == 0 &&
            (f.out_w & 15) == 0;
@@ -125,8 +124,6 @@ int h2j_gpu_prof(unsigned long long *out, int n, int reset);
 int h2j_gpu_deblock(const h2j_gpu_batch *b, void *stream);
 /* K3: SAO frame.pic -> frame.pic2 (copies when SAO is off) */
 int h2j_gpu_sao(const h2j_gpu_batch *b, void *stream);
-/* 1 while K3 sums the MB variances of h2j_sao_folds_variance pictures (default; H2J_SAO_VAR=0: 0) */
-int h2j_gpu_sao_var_fold(void);
 /* K4: JPEG forward path on frame.pic2 -> frame.jcoef / frame.jstat
  * (variance, rate control, FDCT + quantiser + zigzag, symbol histograms) */
 int h2j_gpu_jpeg(const h2j_gpu_batch *b, void *stream);

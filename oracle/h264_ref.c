@@ -194,6 +194,41 @@ static void parse_matrices(OraBits *b, uint8_t sl4[6][16], uint8_t sl8[6][64], i
     }
 }
 
+/* E.1.1 vui_parameters as far as FFmpeg 4.3 (h264_ps.c decode_vui_parameters /
+ * decode_hrd_parameters, behind /root/reference/src/Decoder.cpp:324) can fail the SPS on them:
+ * an HRD with cpb_cnt_minus1 > 31 ("cpb_count invalid") or max_num_reorder_frames > 16
+ * ("Clipping illegal num_reorder_frames", AVERROR_INVALIDDATA).  A VUI cut short by the end of
+ * the SPS counts as no bitstream restriction (FFmpeg resets it).  1 = the SPS fails. */
+static int vui_fails(OraBits *b) {
+    if (ob_u(b, 1) && ob_u(b, 8) == 255) ob_u(b, 32); /* aspect_ratio_info, Extended_SAR */
+    if (ob_u(b, 1)) ob_u(b, 1);                       /* overscan_info */
+    if (ob_u(b, 1)) {                                 /* video_signal_type */
+        ob_u(b, 4);
+        if (ob_u(b, 1)) ob_u(b, 24);                  /* colour description */
+    }
+    if (ob_u(b, 1)) { ob_ue(b); ob_ue(b); }           /* chroma_loc_info */
+    if (ob_u(b, 1)) { ob_u(b, 32); ob_u(b, 32); ob_u(b, 1); } /* timing_info */
+    int hrd = 0;
+    for (int k = 0; k < 2; k++) {                     /* NAL, then VCL hrd_parameters (E.1.2) */
+        if (!ob_u(b, 1)) continue;
+        hrd = 1;
+        uint32_t cpb_minus1 = ob_ue(b);
+        if (cpb_minus1 > 31) return 1;
+        ob_u(b, 8);
+        for (uint32_t i = 0; i <= cpb_minus1; i++) { ob_ue(b); ob_ue(b); ob_u(b, 1); }
+        ob_u(b, 20);
+    }
+    if (hrd) ob_u(b, 1);                              /* low_delay_hrd_flag */
+    ob_u(b, 1);                                       /* pic_struct_present_flag */
+    if (!ob_u(b, 1)) return 0;                        /* bitstream_restriction_flag */
+    ob_u(b, 1);
+    for (int i = 0; i < 4; i++) ob_ue(b);
+    uint32_t reorder = ob_ue(b);
+    ob_ue(b);                                         /* max_dec_frame_buffering */
+    if (b->pos > b->n * 8) return 0;
+    return reorder > 16;
+}
+
 static int parse_sps(OraBits *b, H4Sps *tab) {
     int profile = (int)ob_u(b, 8);
     ob_u(b, 8);
@@ -256,6 +291,7 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
         s->crop_t = (int)ct * cy;
         s->crop_b = (int)cb * cy;
     }
+    if (ob_u(b, 1) && vui_fails(b)) return -7; /* vui_parameters_present_flag */
     if (s->chroma_format_idc != 1) return -4;
     s->valid = 1;
     return 0;

@@ -25,7 +25,8 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         el, fr = bench.reduce_over_ranks(dist, 1.0 + rank, 100 * (rank + 1))
-        q.put((rank, el, fr))
+        bad = bench.sum_over_ranks(dist, rank + 1)
+        q.put((rank, el, fr, bad))
     finally:
         dist.destroy_process_group()
 
@@ -41,9 +42,10 @@ def test_reduce_over_ranks_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, el, fr in res:
+    for rank, el, fr, bad in res:
         assert el == 2.0  # max over ranks
         assert fr == 300  # sum over ranks
+        assert bad == 3  # output-check counters summed over ranks
 
 
 def test_reduce_over_ranks_single():
@@ -99,3 +101,30 @@ def test_mixed_configs4_flow_gloo(world):
         assert fr == 65536  # sum over ranks
     costs = [r[3] for r in res]
     assert max(costs) - min(costs) <= 0.01 * max(costs)  # LPT: balanced shards
+
+
+def test_verify_outputs_against_manifest():
+    """bench.py's post-timing output check: every committed bench stream is in the manifest, the
+    oracle's own JPEG passes, a flipped byte and an unknown stream are counted."""
+    import glob
+    import hashlib
+    import json
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_py as O
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    man = json.load(open(os.path.join(root, "tests", "golden", "bench_manifest.json")))
+    for wl in bench.WORKLOADS.values():
+        if wl["streams"]:
+            for f in glob.glob(os.path.join(root, wl["streams"])):
+                assert hashlib.md5(open(f, "rb").read()).hexdigest() in man, f
+    for pat, *_ in bench.MIXED_SETS.values():
+        for f in glob.glob(os.path.join(root, pat)):
+            assert hashlib.md5(open(f, "rb").read()).hexdigest() in man, f
+    s = open(os.path.join(root, "tests", "golden", "bench264", "avc1080_00.h264"), "rb").read()
+    j = O.transcode(s)
+    batch = [s, s, b"unknown"]
+    out = bytearray(j + j + j)
+    offs, lens = [0, len(j), 2 * len(j)], [len(j)] * 3
+    assert bench.verify_outputs(batch, out, offs, lens, man) == (3, 0, 1)
+    out[len(j) + 100] ^= 1
+    assert bench.verify_outputs(batch, out, offs, lens, man) == (3, 1, 1)

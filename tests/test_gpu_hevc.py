@@ -138,8 +138,9 @@ def test_4k_main10_stream(engine):
 
 def test_async_batches_and_pooled_k1(engine):
     """h2j_engine_submit / h2j_engine_wait with three batches in flight.  Batches over 256 pictures
-    run K1's picture pool (h2j_k1_recon_hevc_pool) with several pictures per workgroup: 520
-    pictures -> 3 per workgroup, 300 -> 2; 8-bit and 10-bit parity vectors (two pool launches),
+    run K1's picture pool (h2j_k1_recon_hevc_pool) with P = min(4, pictures // 256) pictures per
+    workgroup: 520 pictures -> 2 per workgroup, 300 -> 1 (tests/test_gpu_benchsize.py covers
+    P = 3 and 4 at the bench's sizes); 8-bit and 10-bit parity vectors (two pool launches),
     scaling lists, PCM, tiles, WPP.  A mixed-codec batch takes the merged K1 launch."""
     streams = [read(p) for p in PARITY]
     h264 = [read(p) for p in sorted(glob.glob(os.path.join(golden("h264"), "*.h264")))]

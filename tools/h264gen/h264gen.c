@@ -175,7 +175,7 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -1042,14 +1042,28 @@ static void write_sps(FILE *f, G *g, int profile) {
         bw_put(&b, (uint32_t)crop, 1);
         if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / 2); }
     }
-    bw_put(&b, g->delay > 0, 1); /* vui_parameters_present_flag */
-    if (g->delay) { /* E.1.1: only bitstream_restriction, carrying the reorder depth */
-        bw_put(&b, 0, 8);       /* aspect, overscan, video signal, chroma loc, timing, nal/vcl hrd, pic_struct */
+    /* --vuireorder K: the VUI's reorder depth alone (no extra pictures; malformed-SPS vectors use
+     * K > 16); --vuicpb K: a NAL HRD with cpb_cnt_minus1 = K (K > 31 is malformed) */
+    const int reorder = g->vuireorder >= 0 ? g->vuireorder : g->delay;
+    const int vui = g->delay > 0 || g->vuireorder >= 0 || g->vuicpb >= 0;
+    bw_put(&b, (uint32_t)vui, 1); /* vui_parameters_present_flag */
+    if (vui) { /* E.1.1: bitstream_restriction carrying the reorder depth (+ an optional NAL HRD) */
+        bw_put(&b, 0, 5);       /* aspect, overscan, video signal, chroma loc, timing */
+        bw_put(&b, g->vuicpb >= 0, 1); /* nal_hrd_parameters_present_flag */
+        if (g->vuicpb >= 0) {   /* E.1.2 */
+            bw_ue(&b, (uint32_t)g->vuicpb);
+            bw_put(&b, 0, 8);   /* bit_rate_scale, cpb_size_scale */
+            for (int i = 0; i <= g->vuicpb && i < 40; i++) { bw_ue(&b, 1000); bw_ue(&b, 1000); bw_put(&b, 0, 1); }
+            bw_put(&b, 0x5AD6B, 20); /* four 5-bit lengths */
+        }
+        bw_put(&b, 0, 1);       /* vcl_hrd_parameters_present_flag */
+        if (g->vuicpb >= 0) bw_put(&b, 0, 1); /* low_delay_hrd_flag */
+        bw_put(&b, 0, 1);       /* pic_struct_present_flag */
         bw_put(&b, 1, 1);       /* bitstream_restriction_flag */
         bw_put(&b, 1, 1);       /* motion_vectors_over_pic_boundaries_flag */
         bw_ue(&b, 0); bw_ue(&b, 0); bw_ue(&b, 15); bw_ue(&b, 15);
-        bw_ue(&b, (uint32_t)g->delay);     /* max_num_reorder_frames */
-        bw_ue(&b, (uint32_t)g->delay + 1); /* max_dec_frame_buffering */
+        bw_ue(&b, (uint32_t)reorder);     /* max_num_reorder_frames */
+        bw_ue(&b, (uint32_t)reorder + 1); /* max_dec_frame_buffering */
     }
     bw_trailing(&b);
     write_nal(f, 3, 7, b.buf, b.n);
@@ -1108,6 +1122,8 @@ int main(int argc, char **argv) {
     g->nonidr = opt_int(argc, argv, "--nonidr", 0);
     g->delay = opt_int(argc, argv, "--delay", 0);
     g->firstmb = opt_int(argc, argv, "--firstmb", -1);
+    g->vuireorder = opt_int(argc, argv, "--vuireorder", -1);
+    g->vuicpb = opt_int(argc, argv, "--vuicpb", -1);
     g->rawcrop[0] = -1;
     if (opt_str(argc, argv, "--crop"))
         sscanf(opt_str(argc, argv, "--crop"), "%lld,%lld,%lld,%lld", &g->rawcrop[0], &g->rawcrop[1], &g->rawcrop[2], &g->rawcrop[3]);

@@ -348,6 +348,11 @@ MALFORMED = [
     ("m_hevc_conf_overflow", 265, 396, 228, ["--conf", "0,250,0,0"], "ok"),
     ("m_hevc_conf_huge", 265, 396, 228, ["--conf", "4294967294,0,0,4294967294"], "ok"),
     ("m_hevc_width_not_mincb", 265, 128, 96, ["--wdelta", "4"], "fail"),
+    # FFmpeg 4.3 h264_ps.c fails the SPS on max_num_reorder_frames > 16 and on an HRD
+    # with cpb_cnt_minus1 > 31; the same VUI fields in range decode
+    ("m_avc_vui_reorder17", 264, 160, 96, ["--vuireorder", "17"], "fail"),
+    ("m_avc_vui_cpb33", 264, 160, 96, ["--vuicpb", "32", "--vuireorder", "0"], "fail"),
+    ("m_avc_vui_cpb32_ok", 264, 160, 96, ["--vuicpb", "31", "--vuireorder", "0"], "ok"),
 ]
 
 
@@ -370,6 +375,47 @@ def malformed():
         manifest.append({"file": name + ext, "codec": codec, "options": opts, "expect": expect})
         print(f"{path}: {os.path.getsize(path)} B, expect {expect}", flush=True)
     json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+
+
+def leftcrop():
+    """an HEVC picture whose conformance window starts 64 luma samples from the
+    left and 16 from the top, with an output of 336x224 (16-aligned), so K3 SAO sums the JPEG rate
+    control's MB variances (h2j_sao_folds_variance).  The cropped-away left columns are noise and
+    the kept picture is smooth, so summing them would move qscale.  Written into tests/golden/hevc
+    (the parity suite: planes, JPEG, mixed batches).  The oracle's cropped decode must equal the
+    encoder's reconstruction inside the window."""
+    out_dir = os.path.join(ROOT, "tests/golden/hevc")
+    planes = source_planes()
+    W, H, cl, ct = 400, 240, 64, 16
+    content = make_content(planes, W, H, 36, 0, 8)
+    rng = np.random.default_rng(36)
+    content[0][:, :cl] = rng.integers(0, 256, (H, cl))
+    for c in (1, 2):
+        content[c][:, :cl // 2] = rng.integers(0, 256, (H // 2, cl // 2))
+    name = "p25_400x240_conf_left64_top16"
+    path = os.path.join(out_dir, name + ".h265")
+    yuv, rec = path + ".yuv", path + ".rec"
+    with open(yuv, "wb") as f:
+        for p in content:
+            f.write(p.astype(np.uint8).tobytes())
+    subprocess.check_call([GEN, yuv, str(W), str(H), "8", "26", "36", path, "--recon", rec,
+                           "--conf", f"{cl // 2},0,{ct // 2},0"])
+    y, u, v, _ = O.decode(open(path, "rb").read(), 265, skip_loop_filter=True)
+    r = np.fromfile(rec, dtype=np.uint8).astype(np.int32)
+    ys, cs = W * H, (W // 2) * (H // 2)
+    ry = r[:ys].reshape(H, W)[ct:, cl:]
+    ru = r[ys:ys + cs].reshape(H // 2, W // 2)[ct // 2:, cl // 2:]
+    rv = r[ys + cs:].reshape(H // 2, W // 2)[ct // 2:, cl // 2:]
+    os.remove(yuv)
+    os.remove(rec)
+    if not (np.array_equal(y, ry) and np.array_equal(u, ru) and np.array_equal(v, rv)):
+        raise SystemExit(f"{path}: oracle decode != encoder reconstruction (window)")
+    man_path = os.path.join(out_dir, "manifest.json")
+    manifest = [m for m in json.load(open(man_path)) if m["file"] != name + ".h265"]
+    manifest.append({"file": name + ".h265", "w": W, "h": H, "bit_depth": 8, "qp": 26,
+                     "options": ["--conf", f"{cl // 2},0,{ct // 2},0"], "output": [W - cl, H - ct]})
+    json.dump(manifest, open(man_path, "w"), indent=1)
+    print(f"{path}: {os.path.getsize(path)} B, output {y.shape[1]}x{y.shape[0]}", flush=True)
 
 
 WIDE264 = [
@@ -412,4 +458,4 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
      "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy,
-     "wide264": wide264}[what]()
+     "wide264": wide264, "leftcrop": leftcrop}[what]()
