@@ -377,6 +377,7 @@ def main():
 
     stage_sum = {}
     chunks_all = []
+    last_out = [None]  # the output set of the last step waited for (checked after the timed region)
 
     def collect():
         st = eng.stats()
@@ -410,7 +411,6 @@ def main():
             dist.barrier()
 
     run_steps(args.warmup, False)
-    last_out = [None]  # the output set of the last step waited for (checked after the timed region)
     barrier()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()

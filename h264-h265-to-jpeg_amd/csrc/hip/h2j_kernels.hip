@@ -405,6 +405,14 @@ DEVI int16_t* hevc_res_at(int16_t* res, int width, int height, int log2ctb, int 
     const long long tile = static_cast<long long>(y >> q) * h2j_res_tiles(wc, q) + (x >> q);
     return res + base + (tile << (2 * q)) + ((y & qm) << q) + (x & qm);
 }
+// Sample (x, y) of component c in the H.264 residual, tiled by macroblock: MB m (raster order)
+// holds its 16x16 luma, then 8x8 Cb, 8x8 Cr residual, 384 int16 (768 B) back to back, so K1
+// fetches an MB as one contiguous piece (h264_rows).  Rows of a block are 16 (luma) / 8 (chroma)
+// elements apart.
+DEVI int16_t* h264_res_at(int16_t* res, int mbw, int c, int x, int y) {
+    if (c == 0) return res + ((y >> 4) * mbw + (x >> 4)) * 384 + ((y & 15) << 4) + (x & 15);
+    return res + ((y >> 3) * mbw + (x >> 3)) * 384 + 256 + (c - 1) * 64 + ((y & 7) << 3) + (x & 7);
+}
 DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
                         int16_t* R, int rst, K0LdsHevc& s) {
     const int lane = threadIdx.x;
@@ -697,7 +705,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
             wave_sync();
         }
     }
-    for (int i = lane; i < nn; i += 64) R[(tu.y + (i >> log2n)) * rst + tu.x + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+    for (int i = lane; i < nn; i += 64) R[(i >> log2n) * rst + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
     wave_sync();
 }
 
@@ -707,7 +715,7 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
 // arithmetic as h264_residual (8.5.12, 8.5.13): int intermediates, (x + 32) >> 6 at the end.
 template <int LOG2N>
 DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
-                              const uint8_t* sl, int16_t* res, int st0, K0Lds& s) {
+                              const uint8_t* sl, int16_t* res, int mbw, K0Lds& s) {
     constexpr int N = 1 << LOG2N, NN = N * N, GMAX = 64 / N;
     const int lane = threadIdx.x;
     int* blk = s.blk;  // [G][N][N] levels, then the final residual
@@ -782,7 +790,7 @@ DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     }
     wave_sync();
     if (act) {  // row q of the residual: one packed store
-        int16_t* R = res + (mine.y + q) * st0 + mine.x;
+        int16_t* R = h264_res_at(res, mbw, 0, mine.x, mine.y) + q * 16;
         uint32_t packed[N / 2];
 #pragma unroll
         for (int i = 0; i < N / 2; i++)
@@ -798,7 +806,7 @@ DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
 // lane = (TB g, block b, row / column k).  Same arithmetic as the chroma branch of
 // h264_residual (8.5.11: DC ((f * LevelScale4x4(0,0)) << (qP / 6)) >> 5; 8.5.12 AC scaling).
 DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
-                            const uint8_t* sl, int16_t* res, int st1, int off1, int off2, K0Lds& s) {
+                            const uint8_t* sl, int16_t* res, int mbw, K0Lds& s) {
     const int lane = threadIdx.x;
     int* blk = s.blk;  // [G][8][8] levels, then the final residual
     int* tmp = s.tmp;  // [G][8][8] after the row pass
@@ -869,7 +877,7 @@ DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, 
     wave_sync();
     if (act) {  // row k of block b of the residual: 4 samples, one 8-byte store
         const int* v = B + (by + k) * 8 + bx;
-        int16_t* R = res + (mine.c == 1 ? off1 : off2) + (mine.y + by + k) * st1 + mine.x + bx;
+        int16_t* R = h264_res_at(res, mbw, mine.c, mine.x + bx, mine.y + by + k);
         *reinterpret_cast<uint2*>(R) = make_uint2((static_cast<uint32_t>(v[0]) & 0xFFFF) | (static_cast<uint32_t>(v[1]) << 16),
                                                   (static_cast<uint32_t>(v[2]) & 0xFFFF) | (static_cast<uint32_t>(v[3]) << 16));
     }
@@ -881,7 +889,7 @@ DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, 
 // round trip between the passes).  Same arithmetic as the i16 branch of h264_residual (8.5.10,
 // 8.5.12).
 DEVI void h264_i16_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
-                         const uint8_t* sl, int16_t* res, int st0, K0Lds& s) {
+                         const uint8_t* sl, int16_t* res, int mbw, K0Lds& s) {
     const int lane = threadIdx.x;
     int* blk = s.blk;  // [G][16][16] levels
     for (int i = lane; i < G * 256; i += 64) blk[i] = 0;
@@ -946,10 +954,10 @@ DEVI void h264_i16_group(const K0F& f, const uint4& rec, uint64_t gm, int G, con
             const int e0 = v[0][x] + v[2][x], e1 = v[0][x] - v[2][x], e2 = (v[1][x] >> 1) - v[3][x], e3 = v[1][x] + (v[3][x] >> 1);
             v[0][x] = (e0 + e3 + 32) >> 6; v[1][x] = (e1 + e2 + 32) >> 6; v[2][x] = (e1 - e2 + 32) >> 6; v[3][x] = (e0 - e3 + 32) >> 6;
         }
-        int16_t* R = res + (mine.y + by * 4) * st0 + mine.x + bx * 4;
+        int16_t* R = h264_res_at(res, mbw, 0, mine.x + bx * 4, mine.y + by * 4);
     #pragma unroll
         for (int r = 0; r < 4; r++)
-            *reinterpret_cast<uint2*>(R + r * st0) = make_uint2((static_cast<uint32_t>(v[r][0]) & 0xFFFF) | (static_cast<uint32_t>(v[r][1]) << 16),
+            *reinterpret_cast<uint2*>(R + r * 16) = make_uint2((static_cast<uint32_t>(v[r][0]) & 0xFFFF) | (static_cast<uint32_t>(v[r][1]) << 16),
                                                                 (static_cast<uint32_t>(v[r][2]) & 0xFFFF) | (static_cast<uint32_t>(v[r][3]) << 16));
     }  // g < G
     wave_sync();
@@ -1164,7 +1172,7 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
         if constexpr (HEVC)  // R: the TB's origin in its tile, rows 1 << h2j_res_q apart
             hevc_residual(f, tu, CO, co0, sl, hevc_res_at(res, f.width, f.height, f.log2ctb, c, x0, y0),
                           1 << h2j_res_q(f.log2ctb, c), s);
-        else h264_residual(f, tu, CO, co0, sl, res + offc, stc, s);
+        else h264_residual(f, tu, CO, co0, sl, h264_res_at(res, f.ctb_w, c, x0, y0), c ? 8 : 16, s);
     }
     if constexpr (!HEVC) {  // H.264 luma 4x4 / 8x8 residuals, 16 / 8 same-size TBs per pass
 #pragma unroll
@@ -1179,8 +1187,8 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                     m &= m - 1;
                     cnt++;
                 }
-                if (l2 == 2) h264_residual_group<2>(f, rec, gm, cnt, CO, sl, res, st0, s);
-                else h264_residual_group<3>(f, rec, gm, cnt, CO, sl, res, st0, s);
+                if (l2 == 2) h264_residual_group<2>(f, rec, gm, cnt, CO, sl, res, f.ctb_w, s);
+                else h264_residual_group<3>(f, rec, gm, cnt, CO, sl, res, f.ctb_w, s);
             }
         }
         uint64_t m = __ballot(grp264c);
@@ -1192,7 +1200,7 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                 m &= m - 1;
                 cnt++;
             }
-            h264_chroma_group(f, rec, gm, cnt, CO, sl, res, st1, off1, off2, s);
+            h264_chroma_group(f, rec, gm, cnt, CO, sl, res, f.ctb_w, s);
         }
         m = __ballot(grp264i);
         while (m) {
@@ -1203,7 +1211,7 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                 m &= m - 1;
                 cnt++;
             }
-            h264_i16_group(f, rec, gm, cnt, CO, sl, res, st0, s);
+            h264_i16_group(f, rec, gm, cnt, CO, sl, res, f.ctb_w, s);
         }
     }
     if constexpr (HEVC) {  // HEVC residuals, 64 / N same-size TBs per pass
@@ -1481,8 +1489,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
     Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
     Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
-    const int16_t* RY = reinterpret_cast<const int16_t*>(arena + ufl64(f.res));
-    const int16_t* RC[2] = {RY + ufl(f.pic_off[1]), RY + ufl(f.pic_off[2])};
+    const int16_t* RY = reinterpret_cast<const int16_t*>(arena + ufl64(f.res));  // MB tiles (h264_res_at)
     uint16_t* LY = line;            // [W]: bottom luma row of the MB row above
     uint16_t* LC = line + W;        // [2][Wc]
     const uint32_t ntot = ufl(f.ntu);
@@ -1494,8 +1501,8 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
     if (rbeg + w >= rend) return;
     const uint32_t* masks32 = reinterpret_cast<const uint32_t*>(masks);
-    // records (lanes 0..23, dwordx4), mask halves (dword each) and residual (lanes 0..31: luma
-    // half rows of 8, lanes 32..47: chroma rows; 16 B each, ry and rc contiguous) of MB (mx, my)
+    // records (lanes 0..23, dwordx4), mask halves (dword each) and residual (the MB's 768-B tile,
+    // lanes 0..47 16 B each: ry and rc are contiguous in H4In as in the tile) of MB (mx, my)
     auto in_recs = [&](uint32_t a, H4In& d) __attribute__((always_inline)) {
         if (lane < kH4MaxTus) {
             const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
@@ -1506,11 +1513,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     };
     auto in_fetch = [&](int mx, int my, uint32_t a, H4In& d) __attribute__((always_inline)) {
         in_recs(a, d);
-        if (lane < 32) lds_dma16(RY + (my * 16 + (lane >> 1)) * sty + mx * 16 + (lane & 1) * 8, lds_addr(d.ry));
-        else if (lane < 48) {
-            const int k = lane - 32;
-            lds_dma16(RC[k >> 3] + (my * 8 + (k & 7)) * stc + mx * 8, lds_addr(d.ry));
-        }
+        if (lane < 48) lds_dma16(RY + static_cast<size_t>(my * mbw + mx) * 384 + lane * 8, lds_addr(d.ry));
     };
     int cur = 0;
     uint32_t pre_a = rng[4 * ((rbeg + w) * mbw)];  // first record the prefetch assumed

@@ -109,7 +109,8 @@ struct Sps {
     bool valid = false;
     int profile = 0, chroma_format_idc = 1, bit_depth = 8, bit_depth_c = 8;
     int log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4, delta_pic_order_always_zero = 0;
-    int mb_w = 0, mb_h = 0;
+    int mb_w = 0, mb_h = 0;          // frame size in MBs (FrameHeightInMbs: map units x (2 - frame_mbs_only))
+    int frame_mbs_only = 1, mbaff = 0;
     int crop_l = 0, crop_r = 0, crop_t = 0, crop_b = 0;
     int num_reorder_frames = 0;  // VUI bitstream_restriction (0 when absent)
     bool scaling_present = false;
@@ -260,25 +261,28 @@ int parse_sps(BitReader& b, Sps* tab) {
     b.u(1);
     const uint32_t mbw1 = b.ue(), mbh1 = b.ue();
     if (mbw1 >= 512 || mbh1 >= 512) return -5;
+    s.frame_mbs_only = static_cast<int>(b.u(1));
+    if (!s.frame_mbs_only) s.mbaff = static_cast<int>(b.u(1));  // mb_adaptive_frame_field_flag
     s.mb_w = static_cast<int>(mbw1) + 1;
-    s.mb_h = static_cast<int>(mbh1) + 1;
-    if (!b.u(1)) return -3;  // interlaced
+    s.mb_h = (static_cast<int>(mbh1) + 1) * (2 - s.frame_mbs_only);  // 7.4.2.1.1 FrameHeightInMbs
     b.u(1);
     if (b.u(1)) {
-        // frame cropping in 2-sample units (4:2:0, frame_mbs_only).  FFmpeg 4.3 h264_ps.c
+        // frame cropping in CropUnitX = 2 / CropUnitY = 2 * (2 - frame_mbs_only) sample units
+        // (4:2:0, 7.4.2.1.1).  FFmpeg 4.3 h264_ps.c
         // (libavcodec 58.x, the reference's decoder) rejects the SPS ("crop values invalid",
         // goto fail) when an offset exceeds INT_MAX / 4 / step or the window leaves no
         // picture, so no frame is decoded; only its HEVC SPS parser ignores such a window.
         const uint32_t cl = b.ue(), cr = b.ue(), ct = b.ue(), cb = b.ue();
         const uint64_t w = static_cast<uint64_t>(s.mb_w) * 16, h = static_cast<uint64_t>(s.mb_h) * 16;
-        const uint32_t lim = 0x7fffffffu / 4 / 2;
-        if (cl > lim || cr > lim || ct > lim || cb > lim || (static_cast<uint64_t>(cl) + cr) * 2 >= w ||
-            (static_cast<uint64_t>(ct) + cb) * 2 >= h)
+        const uint32_t uy = 2u * (2u - static_cast<uint32_t>(s.frame_mbs_only));
+        const uint32_t lim = 0x7fffffffu / 4 / 2, limy = 0x7fffffffu / 4 / uy;
+        if (cl > lim || cr > lim || ct > limy || cb > limy || (static_cast<uint64_t>(cl) + cr) * 2 >= w ||
+            (static_cast<uint64_t>(ct) + cb) * uy >= h)
             return -6;
         s.crop_l = static_cast<int>(cl) * 2;
         s.crop_r = static_cast<int>(cr) * 2;
-        s.crop_t = static_cast<int>(ct) * 2;
-        s.crop_b = static_cast<int>(cb) * 2;
+        s.crop_t = static_cast<int>(ct * uy);
+        s.crop_b = static_cast<int>(cb * uy);
     }
     if (b.overrun()) return -1;
     if (b.u(1)) {
@@ -1157,6 +1161,19 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             const Sps& s = sps_[p.sps_id];
             const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h) ? static_cast<int>(first_mb_u) : -1;
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
+            if (!s.frame_mbs_only && b.u(1)) {
+                // field_pic_flag: a field picture (PAFF).  The reference's FFmpeg holds a first
+                // field until its second field arrives ("Wait for second field", h264dec.c), and
+                // the reference sends one packet (one field: the h264 parser splits fields, a
+                // first_mb_in_slice that does not increase starts a packet), so it receives no
+                // frame and returns false (/root/reference/src/Decoder.cpp:324-360).
+                job_->message = "field picture (PAFF): the reference decodes no frame from one field";
+                return -3;
+            }
+            if (s.mbaff) {
+                job_->message = "MBAFF frames are not supported";
+                return -3;
+            }
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
             // FFmpeg h264_slice.c: "first_mb_in_slice overflow" drops the slice; once a slice of
             // picture 0 is collected the picture is still output, so stop there as at a

@@ -125,7 +125,7 @@ static const uint8_t k_blk_y[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3,
 typedef struct {
     int valid, profile, chroma_format_idc, bit_depth, bit_depth_c;
     int log2_max_frame_num, poc_type, log2_max_poc_lsb, delta_pic_order_always_zero;
-    int mb_w, mb_h, frame_mbs_only;
+    int mb_w, mb_h, frame_mbs_only, mbaff;
     int crop_l, crop_r, crop_t, crop_b; /* luma samples */
     int scaling_present;
     uint8_t sl4[6][16], sl8[6][64];
@@ -272,15 +272,16 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
     ob_ue(b); /* max_num_ref_frames */
     ob_u(b, 1);
     s->mb_w = (int)ob_ue(b) + 1;
-    s->mb_h = (int)ob_ue(b) + 1;
+    s->mb_h = (int)ob_ue(b) + 1; /* map units */
     s->frame_mbs_only = (int)ob_u(b, 1);
-    if (!s->frame_mbs_only) return -3; /* interlaced: out of scope */
+    if (!s->frame_mbs_only) s->mbaff = (int)ob_u(b, 1);
+    s->mb_h *= 2 - s->frame_mbs_only; /* 7.4.2.1.1: FrameHeightInMbs */
     ob_u(b, 1);                         /* direct_8x8_inference */
     if (ob_u(b, 1)) {
         /* FFmpeg 4.3 h264_ps.c rejects the SPS ("crop values invalid", goto fail) when an
          * offset exceeds INT_MAX / 4 / step or the window leaves no picture (only hevc_ps.c
          * ignores such a window and shows the whole surface) */
-        int cx = s->chroma_format_idc == 0 ? 1 : 2, cy = s->chroma_format_idc == 1 ? 2 : 1;
+        int cx = s->chroma_format_idc == 0 ? 1 : 2, cy = (s->chroma_format_idc == 1 ? 2 : 1) * (2 - s->frame_mbs_only);
         uint64_t cl = ob_ue(b), cr = ob_ue(b), ct = ob_ue(b), cb = ob_ue(b);
         uint64_t lx = 0x7fffffffu / 4 / (unsigned)cx, ly = 0x7fffffffu / 4 / (unsigned)cy;
         if (cl > lx || cr > lx || ct > ly || cb > ly || (cl + cr) * cx >= (uint64_t)s->mb_w * 16 ||
@@ -1544,6 +1545,10 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             const H4Sps *s = &d->sps[p->sps_id];
             if (!s->valid) { ret = -4; goto done; }
             int frame_num = (int)ob_u(&b, s->log2_max_frame_num);
+            /* field_pic_flag: a field (PAFF) -- FFmpeg outputs no frame for the first field alone
+             * (h264dec.c "Wait for second field"), so the reference returns false */
+            if (!s->frame_mbs_only && ob_u(&b, 1)) { ret = -3; goto done; }
+            if (s->mbaff) { ret = -3; goto done; } /* MBAFF: not restated */
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
             /* FFmpeg: "first_mb_in_slice overflow" drops the slice; picture 0 is output from the
              * slices already collected, and fails only when none was */

@@ -175,7 +175,7 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -1031,8 +1031,12 @@ static void write_sps(FILE *f, G *g, int profile) {
     bw_ue(&b, 1);     /* max_num_ref_frames */
     bw_put(&b, 0, 1);
     bw_ue(&b, (uint32_t)(g->mbw - 1));
-    bw_ue(&b, (uint32_t)(g->mbh - 1));
-    bw_put(&b, 1, 1); /* frame_mbs_only */
+    /* --ilsps 1: an interlace-capable SPS (frame_mbs_only_flag 0, mb_adaptive_frame_field_flag 0)
+     * coding a frame picture: the height is sent in field MB rows (map units) and the vertical
+     * crop in units of 4 rows (7.4.2.1.1) */
+    bw_ue(&b, (uint32_t)(g->ilsps ? g->mbh / 2 - 1 : g->mbh - 1));
+    bw_put(&b, (uint32_t)!g->ilsps, 1); /* frame_mbs_only */
+    if (g->ilsps) bw_put(&b, 0, 1);     /* mb_adaptive_frame_field_flag */
     bw_put(&b, 1, 1); /* direct_8x8_inference */
     int crop = g->outW != g->W || g->outH != g->H;
     if (g->rawcrop[0] >= 0) { /* --crop l,r,t,b: raw frame_crop offsets (malformed-SPS vectors) */
@@ -1040,7 +1044,7 @@ static void write_sps(FILE *f, G *g, int profile) {
         for (int i = 0; i < 4; i++) bw_ue(&b, (uint32_t)g->rawcrop[i]);
     } else {
         bw_put(&b, (uint32_t)crop, 1);
-        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / 2); }
+        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / (g->ilsps ? 4 : 2)); }
     }
     /* --vuireorder K: the VUI's reorder depth alone (no extra pictures; malformed-SPS vectors use
      * K > 16); --vuicpb K: a NAL HRD with cpb_cnt_minus1 = K (K > 31 is malformed) */
@@ -1124,13 +1128,15 @@ int main(int argc, char **argv) {
     g->firstmb = opt_int(argc, argv, "--firstmb", -1);
     g->vuireorder = opt_int(argc, argv, "--vuireorder", -1);
     g->vuicpb = opt_int(argc, argv, "--vuicpb", -1);
+    g->ilsps = opt_int(argc, argv, "--ilsps", 0);
     g->rawcrop[0] = -1;
     if (opt_str(argc, argv, "--crop"))
         sscanf(opt_str(argc, argv, "--crop"), "%lld,%lld,%lld,%lld", &g->rawcrop[0], &g->rawcrop[1], &g->rawcrop[2], &g->rawcrop[3]);
     if (g->delay > 6) { fprintf(stderr, "--delay <= 6 (4-bit POC lsb)\n"); return 2; }
     int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm ? 100 : 77));
     g_lim = 1 << (7 + g->bd);
-    g->W = (g->outW + 15) & ~15; g->H = (g->outH + 15) & ~15;
+    g->W = (g->outW + 15) & ~15; g->H = g->ilsps ? (g->outH + 31) & ~31 : (g->outH + 15) & ~15;
+    if (g->ilsps && (g->H - g->outH) % 4) { fprintf(stderr, "--ilsps: the height must crop in 4-row units\n"); return 2; }
     g->mbw = g->W / 16; g->mbh = g->H / 16;
     FILE *fi = fopen(argv[1], "rb");
     if (!fi) { perror("input"); return 1; }
@@ -1160,6 +1166,7 @@ int main(int argc, char **argv) {
         bw_ue(&b, 7);                         /* I (all slices I) */
         bw_ue(&b, 0);                         /* pps */
         bw_put(&b, 0, 4);                     /* frame_num */
+        if (g->ilsps) bw_put(&b, 0, 1);       /* field_pic_flag: a frame */
         if (!g->nonidr) bw_ue(&b, 0);         /* idr_pic_id */
         bw_put(&b, 0, 4);                     /* poc lsb */
         if (!g->nonidr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } /* dec_ref_pic_marking (IDR) */

@@ -244,6 +244,10 @@ PARITY264 = [
     ("a20_416x240_sm_sps_pps_8x8", 416, 240, 8, 30, 50, 3, ["--sm", "2", "--cqp", "2", "--cqp2", "-1"]),
     ("a21_352x288_sm_pps_cavlc", 352, 288, 8, 20, 51, 2, ["--sm", "3", "--cavlc", "1"]),
     ("a22_320x176_sm_sps_pps_10bit_4x4", 320, 176, 10, 16, 52, 3, ["--sm", "2", "--t8x8", "0"]),
+    # interlace-capable SPS (frame_mbs_only_flag 0) coding a frame picture without MBAFF: height in
+    # field MB rows, vertical crop in 4-row units, field_pic_flag in the slice header
+    ("a23_416x232_ilsps_frame", 416, 232, 8, 27, 55, 2, ["--ilsps", "1", "--slices", "4"]),
+    ("a24_336x180_ilsps_frame_cavlc", 336, 180, 8, 24, 56, 3, ["--ilsps", "1", "--cavlc", "1"]),
 ]
 
 
