@@ -624,9 +624,27 @@ DEVI void h264_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     wave_sync();
     for (int e = lane; e < tu.ncoef; e += 64) {
         const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
-        s.blk[en >> 16] = static_cast<int16_t>(en & 0xFFFF);
+        s.blk[en >> 24] = static_cast<int>(en << 8) >> 8;  // H2J_COEF264: 24-bit level
     }
     wave_sync();
+    if (tu.flags & H2J_TU_BYPASS) {
+        // TransformBypassModeFlag: the residual is the levels (DC levels included, at (4i, 4j));
+        // vertical / horizontal intra predictions accumulate it down the columns / along the
+        // rows of the whole block (8.5.15), one lane per column / row
+        const bool dv = tu.flags & H2J_TU_DPCM_V, dh = tu.flags & H2J_TU_DPCM_H;
+        if ((dv || dh) && lane < n) {
+            int acc = 0;
+            for (int k = 0; k < n; k++) {
+                const int i = dv ? k * n + lane : lane * n + k;
+                acc += s.blk[i];
+                s.blk[i] = acc;
+            }
+        }
+        wave_sync();
+        for (int i = lane; i < nn; i += 64) R[(i >> log2n) * rst + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
+        wave_sync();
+        return;
+    }
     const uint8_t* w4 = f.slist ? sl + f.sl + c * 16 : nullptr;
     if (i16 || chroma) {
         // DC transform (Hadamard 4x4 / 2x2) on the levels at (4i, 4j)
@@ -742,7 +760,7 @@ DEVI void h264_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     wave_sync();
 #pragma unroll
     for (int g = 0; g < GMAX; g++)
-        if (lane < ncf[g]) blk[g * NN + static_cast<int>(en[g] >> 16)] = static_cast<int16_t>(en[g] & 0xFFFF);
+        if (lane < ncf[g]) blk[g * NN + static_cast<int>(en[g] >> 24)] = static_cast<int>(en[g] << 8) >> 8;
     wave_sync();
     const int g = lane >> LOG2N, q = lane & (N - 1);
     const bool act = g < G;
@@ -831,7 +849,7 @@ DEVI void h264_chroma_group(const K0F& f, const uint4& rec, uint64_t gm, int G, 
     wave_sync();
 #pragma unroll
     for (int g = 0; g < 4; g++)
-        if (lane < ncf[g]) blk[g * 64 + static_cast<int>(en[g] >> 16)] = static_cast<int16_t>(en[g] & 0xFFFF);
+        if (lane < ncf[g]) blk[g * 64 + static_cast<int>(en[g] >> 24)] = static_cast<int>(en[g] << 8) >> 8;
     wave_sync();
     const int g = lane >> 4, b = (lane >> 2) & 3, k = lane & 3;
     const bool act = g < G;
@@ -905,7 +923,7 @@ DEVI void h264_i16_group(const K0F& f, const uint4& rec, uint64_t gm, int G, con
             for (int j = 0; j < 4; j++) en[j] = lane + 64 * j < tu.ncoef ? CO[tu.coef + lane + 64 * j] : 0u;
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if (lane + 64 * j < tu.ncoef) blk[g * 256 + static_cast<int>(en[j] >> 16)] = static_cast<int16_t>(en[j] & 0xFFFF);
+                if (lane + 64 * j < tu.ncoef) blk[g * 256 + static_cast<int>(en[j] >> 24)] = static_cast<int>(en[j] << 8) >> 8;
         }
     }
     wave_sync();
@@ -1128,14 +1146,14 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
     // transform-skip / bypass residuals (regular HEVC transforms run batched below).  H.264:
     // the next such record's coefficients prefetched one record ahead.
     // H.264 luma 4x4 / 8x8 (no DC transform) run batched below, like the regular HEVC transforms
-    const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
-                        own.log2n <= 3;
+    const bool grp264 = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_BYPASS)) &&
+                        own.c == 0 && own.log2n <= 3;
     // ... and the chroma 8x8 TBs, four per pass
-    const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c > 0 &&
-                         own.log2n == 3;
+    const bool grp264c = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_BYPASS)) &&
+                         own.c > 0 && own.log2n == 3;
     // ... and the Intra16x16 luma TBs, four per pass
-    const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & H2J_TU_PCM) && own.c == 0 &&
-                         own.log2n == 4;
+    const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_BYPASS)) &&
+                         own.c == 0 && own.log2n == 4;
     uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
     uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
@@ -2959,24 +2977,36 @@ __constant__ int kChromaQp264[22] = {29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36,
 // luma filter with ap / aq < beta forced false -- tc = tc0 + 1, p1 / q1 untouched for bS < 4, the
 // 3-tap p0 / q0 form for bS 4 -- and only p1..q1 of it matter.  v: 20 samples, the edge between
 // v[E - 1] and v[E]; `on` false leaves the line as is.  Selects only (lanes diverge on data).
+// Every sample of v is in [0, 65535] (loaded from uint16, and the filters' outputs stay between
+// their inputs), so |a - b| is one v_sad_u16 (the high halves are zero); the clips below all have
+// lo <= hi, where clip3 is one v_med3_i32 (the compiler emits min + max for runtime bounds).
+DEVI int db_absd(int a, int b) {
+    return static_cast<int>(__builtin_amdgcn_sad_u16(static_cast<uint32_t>(a), static_cast<uint32_t>(b), 0u));
+}
+DEVI int db_clip(int lo, int hi, int v) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+    return r;
+}
 template <int E>
 DEVI void h264_filt_line(int (&v)[20], bool on, int bs, int alpha, int beta, int tc0, int maxv, bool chroma) {
     const int p0 = v[E - 1], p1 = v[E - 2], p2 = v[E - 3], q0 = v[E], q1 = v[E + 1], q2 = v[E + 2];
-    const bool f = on && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta;
-    const bool apb = !chroma && abs(p2 - p0) < beta, aqb = !chroma && abs(q2 - q0) < beta;
+    const int d0 = db_absd(p0, q0);
+    const bool f = on && d0 < alpha && db_absd(p1, p0) < beta && db_absd(q1, q0) < beta;
+    const bool apb = !chroma && db_absd(p2, p0) < beta, aqb = !chroma && db_absd(q2, q0) < beta;
     if (bs < 4) {
         const int tc = chroma ? tc0 + 1 : tc0 + apb + aqb;
-        const int dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+        const int dl = db_clip(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
         const int avg = (p0 + q0 + 1) >> 1;
-        const int np1 = apb ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 * 2)) >> 1) : p1;
-        const int nq1 = aqb ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 * 2)) >> 1) : q1;
-        v[E - 1] = f ? clip3(0, maxv, p0 + dl) : p0;
-        v[E] = f ? clip3(0, maxv, q0 - dl) : q0;
+        const int np1 = apb ? p1 + db_clip(-tc0, tc0, (p2 + avg - (p1 * 2)) >> 1) : p1;
+        const int nq1 = aqb ? q1 + db_clip(-tc0, tc0, (q2 + avg - (q1 * 2)) >> 1) : q1;
+        v[E - 1] = f ? db_clip(0, maxv, p0 + dl) : p0;
+        v[E] = f ? db_clip(0, maxv, q0 - dl) : q0;
         v[E - 2] = f ? np1 : p1;
         v[E + 1] = f ? nq1 : q1;
     } else {
         const int p3 = v[E - 4], q3 = v[E + 3];
-        const bool sm = abs(p0 - q0) < ((alpha >> 2) + 2);
+        const bool sm = d0 < ((alpha >> 2) + 2);
         const bool sp = apb && sm, sq = aqb && sm;
         const int np0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
         const int np1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;

@@ -111,6 +111,7 @@ struct Sps {
     int log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4, delta_pic_order_always_zero = 0;
     int mb_w = 0, mb_h = 0;          // frame size in MBs (FrameHeightInMbs: map units x (2 - frame_mbs_only))
     int frame_mbs_only = 1, mbaff = 0;
+    int transform_bypass = 0;        // qpprime_y_zero_transform_bypass_flag
     int crop_l = 0, crop_r = 0, crop_t = 0, crop_b = 0;
     int num_reorder_frames = 0;  // VUI bitstream_restriction (0 when absent)
     bool scaling_present = false;
@@ -231,7 +232,7 @@ int parse_sps(BitReader& b, Sps* tab) {
         if (s.chroma_format_idc == 3) b.u(1);
         s.bit_depth = static_cast<int>(b.ue()) + 8;
         s.bit_depth_c = static_cast<int>(b.ue()) + 8;
-        if (b.u(1)) return -2;  // lossless transform bypass (High 4:4:4 Predictive only)
+        s.transform_bypass = static_cast<int>(b.u(1));  // qpprime_y_zero_transform_bypass_flag
         s.scaling_present = b.u(1) != 0;
         if (s.scaling_present) {
             uint8_t fb4[6][16], fb8[6][64];
@@ -289,7 +290,12 @@ int parse_sps(BitReader& b, Sps* tab) {
         s.num_reorder_frames = parse_vui_reorder(b);
         if (s.num_reorder_frames < 0) return -1;
     }
-    if (s.chroma_format_idc != 1 || s.bit_depth > 10 || s.bit_depth_c != s.bit_depth) return -4;
+    // FFmpeg 4.3 decodes 4:2:0 at 8, 9, 10, 12 and 14 bits with equal luma / chroma depths
+    // (h264_ps.c "Different chroma and luma bit depth"; h264_slice.c get_pixel_format has no 11- or
+    // 13-bit format, "Unsupported bit depth")
+    if (s.chroma_format_idc != 1 || s.bit_depth_c != s.bit_depth || s.bit_depth > 14 || s.bit_depth == 11 ||
+        s.bit_depth == 13)
+        return -4;
     s.valid = true;
     return 0;
 }
@@ -612,6 +618,18 @@ void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, c
     job_->coefs.insert(job_->coefs.end(), e, e + n);
     t.ncoef = static_cast<uint16_t>(n);
     t.flags = n ? H2J_TU_CBF : 0;
+    // TransformBypassModeFlag (qpprime_y_zero_transform_bypass_flag and QP'Y 0, 8.5.12 / 8.5.15):
+    // the residual is the levels; FFmpeg (h264_mb.c) accumulates it along vertical / horizontal
+    // intra predictions only for profile_idc 244.  Luma NxN and 16x16 modes: 0 vertical,
+    // 1 horizontal; chroma: 1 horizontal, 2 vertical.
+    if (s_->transform_bypass && qp_ + qpbd_ == 0) {
+        t.flags |= H2J_TU_BYPASS;
+        if (s_->profile == 244) {
+            const bool v = c == 0 ? mode == 0 : mode == 2, h = c == 0 ? mode == 1 : mode == 1;
+            if (v) t.flags |= H2J_TU_DPCM_V;
+            if (h) t.flags |= H2J_TU_DPCM_H;
+        }
+    }
     job_->tus.push_back(t);
 }
 
@@ -780,7 +798,7 @@ void H264Parser::decode_mb() {
     int lvl[64];
     uint32_t mbe[256];  // I16x16: the whole macroblock's levels
     int nmb = 0;
-    auto entry = [](int p, int v) { return (static_cast<uint32_t>(p) << 16) | static_cast<uint16_t>(v); };
+    auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
     if (is16) {
         Mb* A = nb(-1, 0);
         Mb* B = nb(0, -1);
@@ -1052,7 +1070,7 @@ void H264Parser::decode_mb_cavlc() {
     int lvl[16];
     uint32_t mbe[256];
     int nmb = 0;
-    auto entry = [](int p, int v) { return (static_cast<uint32_t>(p) << 16) | static_cast<uint16_t>(v); };
+    auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
     if (is16) {
         const int n = cavlc_block(nc_luma(0), 16, pos, lvl);
         if (n < 0) { err_ = -44; return; }

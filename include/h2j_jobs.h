@@ -32,8 +32,17 @@ enum {
     H2J_TU_EDGE_L = 1u << 4,  /* left edge is a deblocking edge (filterEdgeFlag && on 8 grid) */
     H2J_TU_EDGE_T = 1u << 5,  /* top edge is a deblocking edge */
     H2J_TU_NOFILT = 1u << 6,  /* samples excluded from deblock/SAO (pcm+lf disabled, bypass) */
-    H2J_TU_DST = 1u << 7      /* HEVC 4x4 luma intra: DST-VII instead of DCT */
+    H2J_TU_DST = 1u << 7,     /* HEVC 4x4 luma intra: DST-VII instead of DCT */
+    /* H.264 transform-bypass TBs (H2J_TU_BYPASS) with a vertical / horizontal intra prediction:
+     * the residual accumulates down the columns / along the rows (8.5.15); the bits are HEVC's
+     * deblocking-edge flags, which H.264 records do not use */
+    H2J_TU_DPCM_V = 1u << 4,
+    H2J_TU_DPCM_H = 1u << 5
 };
+/* H.264 coefficient entries carry 24-bit levels (10- to 14-bit video: levels up to
+ * +-2^(7 + bitDepth)): (pos << 24) | (level & 0xFFFFFF); HEVC entries and PCM samples keep
+ * (pos << 16) | (uint16_t)value */
+#define H2J_COEF264(pos, level) ((((uint32_t)(pos)) << 24) | (((uint32_t)(level)) & 0xFFFFFFu))
 
 /* One transform block of one colour component, in decoding order.
  * HEVC: every luma/chroma TB of the picture (prediction happens per TB even
@@ -50,7 +59,7 @@ typedef struct {
     uint32_t coef;   /* first entry (frame-relative) */
 } h2j_tu;
 
-/* coefficient entry: (pos << 16) | (uint16_t)level, pos = y * n + x */
+/* coefficient entry: (pos << 16) | (uint16_t)level, pos = y * n + x (H.264 levels: H2J_COEF264) */
 typedef uint32_t h2j_coef;
 
 /* One HEVC CTB or one H.264 macroblock (log2ctb 4). */

@@ -126,6 +126,7 @@ typedef struct {
     int valid, profile, chroma_format_idc, bit_depth, bit_depth_c;
     int log2_max_frame_num, poc_type, log2_max_poc_lsb, delta_pic_order_always_zero;
     int mb_w, mb_h, frame_mbs_only, mbaff;
+    int transform_bypass; /* qpprime_y_zero_transform_bypass_flag */
     int crop_l, crop_r, crop_t, crop_b; /* luma samples */
     int scaling_present;
     uint8_t sl4[6][16], sl8[6][64];
@@ -249,7 +250,7 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
         if (s->chroma_format_idc == 3) ob_u(b, 1);
         s->bit_depth = (int)ob_ue(b) + 8;
         s->bit_depth_c = (int)ob_ue(b) + 8;
-        if (ob_u(b, 1)) return -2; /* qpprime_y_zero_transform_bypass: High 4:4:4 only */
+        s->transform_bypass = (int)ob_u(b, 1); /* qpprime_y_zero_transform_bypass_flag */
         s->scaling_present = (int)ob_u(b, 1);
         if (s->scaling_present) {
             uint8_t fb4[6][16], fb8[6][64];
@@ -294,6 +295,10 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
     }
     if (ob_u(b, 1) && vui_fails(b)) return -7; /* vui_parameters_present_flag */
     if (s->chroma_format_idc != 1) return -4;
+    /* FFmpeg 4.3: h264_ps.c fails luma / chroma depths that differ ("Different chroma and luma
+     * bit depth") or exceed 14; h264_slice.c get_pixel_format has no 11- or 13-bit format
+     * ("Unsupported bit depth") */
+    if (s->bit_depth != s->bit_depth_c || s->bit_depth > 14 || s->bit_depth == 11 || s->bit_depth == 13) return -4;
     s->valid = 1;
     return 0;
 }
@@ -970,10 +975,66 @@ static int pred_mode_nb(H4Dec *d, int blk, int is8x8, int dir /* 0 A left, 1 B t
 }
 
 /* ---- reconstruction of one macroblock from the parsed levels (8.3, 8.5) ---- */
+/* 8.5.15 intra residual transform-bypass: TransformBypassModeFlag (qpprime_y_zero_transform_bypass_flag
+ * and QP'Y == 0) with a horizontal / vertical intra prediction accumulates the residual along the
+ * prediction direction over the n x n block (FFmpeg h264_mb.c: only for profile_idc 244, through
+ * pred*_add per 4x4 block -- the same samples for valid lossless streams).  dir: 0 vertical, 1 horizontal. */
+static void bypass_dpcm(int *r, int n, int dir) {
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            if (dir == 0 && y > 0) r[y * n + x] += r[(y - 1) * n + x];
+            if (dir == 1 && x > 0) r[y * n + x] += r[y * n + x - 1];
+        }
+}
+
+/* the TransformBypassModeFlag macroblock: residual = the inverse-scanned levels, no scaling, no
+ * transform (8.5.12.1 / 8.5.10 / 8.5.11 with TransformBypassModeFlag 1) */
+static int recon_mb_bypass(H4Dec *d, MbInfo *m) {
+    const int gx = d->mbx * 16, gy = d->mby * 16;
+    const int dpcm = d->s->profile == 244;
+    int pred[256], r[256];
+    if (m->mb_type == MB_I_NXN && !m->t8x8) {
+        for (int blk = 0; blk < 16; blk++) {
+            pred4x4(d, blk, m->ipm[blk], pred);
+            for (int i = 0; i < 16; i++) r[i] = d->lvl4[blk][i];
+            if (dpcm && m->ipm[blk] <= 1) bypass_dpcm(r, 4, m->ipm[blk]);
+            put_block(d, 0, gx + k_blk_x[blk] * 4, gy + k_blk_y[blk] * 4, 4, pred, r);
+        }
+    } else if (m->mb_type == MB_I_NXN) {
+        for (int b8 = 0; b8 < 4; b8++) {
+            pred8x8(d, b8, m->ipm[b8 * 4], pred);
+            for (int i = 0; i < 64; i++) r[i] = d->lvl8[b8][i];
+            if (dpcm && m->ipm[b8 * 4] <= 1) bypass_dpcm(r, 8, m->ipm[b8 * 4]);
+            put_block(d, 0, gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 8, pred, r);
+        }
+    } else {
+        const int mode = (m->mb_type - 1) % 4;
+        pred16x16(d, mode, pred);
+        for (int blk = 0; blk < 16; blk++) { /* 4x4 blocks' levels, DC from the DC matrix */
+            int bx = k_blk_x[blk], by = k_blk_y[blk];
+            for (int i = 0; i < 16; i++) r[(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)] = i ? d->lvl4[blk][i] : d->dc_l[by * 4 + bx];
+        }
+        if (dpcm && mode <= 1) bypass_dpcm(r, 16, mode);
+        put_block(d, 0, gx, gy, 16, pred, r);
+    }
+    for (int c = 0; c < 2; c++) {
+        pred_chroma(d, 1 + c, m->cpm, pred);
+        for (int b4 = 0; b4 < 4; b4++) {
+            int bx = b4 & 1, by = b4 >> 1;
+            for (int i = 0; i < 16; i++) r[(by * 4 + (i >> 2)) * 8 + bx * 4 + (i & 3)] = i ? d->ac_c[c][b4][i] : d->dc_c[c][b4];
+        }
+        /* intra_chroma_pred_mode 1 horizontal, 2 vertical */
+        if (dpcm && (m->cpm == 1 || m->cpm == 2)) bypass_dpcm(r, 8, m->cpm == 2 ? 0 : 1);
+        put_block(d, 1 + c, gx / 2, gy / 2, 8, pred, r);
+    }
+    return 0;
+}
+
 static int recon_mb(H4Dec *d, MbInfo *m) {
     const int gx = d->mbx * 16, gy = d->mby * 16;
     /* ---- reconstruction ---- */
     const int qp = d->qp + d->qpbd; /* QP'Y */
+    if (d->s->transform_bypass && qp == 0) return recon_mb_bypass(d, m);
     const int qm = qp % 6, qd = qp / 6;
     int pred[256], res[64];
     if (m->mb_type == MB_I_NXN && !m->t8x8) {

@@ -175,7 +175,7 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -445,7 +445,7 @@ static void res_dc(const int *lv, int n, int qp, int *r, const int *w) {
 
 /* ------------------------------------------------------------ least-squares quantiser against the decoder basis */
 typedef struct { float *basis; int n, npos; } Basis; /* basis[pos][sample] for unit level */
-static Basis g_b4[64], g_b8[64], g_b16[64], g_bc[2][64];
+static Basis g_b4[88], g_b8[88], g_b16[88], g_bc[2][88]; /* qP up to 51 + QpBdOffset (14-bit: 87) */
 
 /* weightScale matrices in raster order (8.5.6 inverse zig-zag of the active scaling lists):
  * [0..2] Intra Y / Cb / Cr 4x4, g_w8 Intra Y 8x8; flat 16 without scaling matrices */
@@ -533,7 +533,15 @@ static int enc_block_cavlc(G *g, int nC, int maxnum, const int *co) {
         } else {
             prefix = 15; ssz = 12; suffix = code - (15 << sl);
         }
-        if (suffix >= 4096) { fprintf(stderr, "level out of CAVLC range\n"); exit(3); }
+        if (suffix >= 4096) { /* level_prefix >= 16 (high bit depths, 7.4.5.3.2): levelCode adds
+                                * (1 << (level_prefix - 3)) - 4096, suffix of level_prefix - 3 bits */
+            int base = code - suffix; /* levelCode at level_prefix 15, suffix 0 */
+            prefix = 16;
+            while (code >= base + (1 << (prefix - 3)) - 4096 + (1 << (prefix - 3)) && prefix < 28) prefix++;
+            ssz = prefix - 3;
+            suffix = code - (base + (1 << (prefix - 3)) - 4096);
+            if (suffix < 0 || suffix >= (1 << ssz)) { fprintf(stderr, "level out of CAVLC range\n"); exit(3); }
+        }
         bw_put(b, 1, prefix + 1);  /* prefix zeros then 1 */
         if (ssz) bw_put(b, (uint32_t)suffix, ssz);
         if (sl == 0) sl = 1;
@@ -634,6 +642,18 @@ static long var16(G *g) {
     return (s2 - s * s / 256) / 256;
 }
 
+/* --lossless: the inverse of the decoder's 8.5.15 accumulation (vertical: differences down each
+ * column, horizontal: along each row) for horizontal / vertical intra predictions; dir 0 / 1 */
+static void dpcm_diff(const int *r, int *c, int n, int dir) {
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            int v = r[y * n + x];
+            if (dir == 0 && y > 0) v -= r[(y - 1) * n + x];
+            if (dir == 1 && x > 0) v -= r[y * n + x - 1];
+            c[y * n + x] = v;
+        }
+}
+
 static void put(G *g, int c, int gx, int gy, int n, const int *pred, const int *r) {
     int maxv = (1 << g->bd) - 1;
     for (int y = 0; y < n; y++) for (int x = 0; x < n; x++) g->rec[c][(gy + y) * g->st[c] + gx + x] = (uint16_t)clip3(0, maxv, pred[y * n + x] + r[y * n + x]);
@@ -701,10 +721,15 @@ static void encode_mb(G *g) {
         }
         pred16(g, mode16, pred);
         for (int i = 0; i < 256; i++) src[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
-        Basis *Bs = &g_b16[qpl];
-        build_basis(Bs, 2, qpl, g_w4[0]);
-        quantize(Bs, src, lv16, maxlev);
-        fit(2, lv16, qpl, g_w4[0]);
+        if (g->lossless) {  /* transform bypass: the levels are the residual (DPCM for modes 0 / 1) */
+            if (mode16 <= 1) dpcm_diff(src, lv16, 16, mode16);
+            else memcpy(lv16, src, sizeof(lv16));
+        } else {
+            Basis *Bs = &g_b16[qpl];
+            build_basis(Bs, 2, qpl, g_w4[0]);
+            quantize(Bs, src, lv16, maxlev);
+            fit(2, lv16, qpl, g_w4[0]);
+        }
     }
     /* chroma mode + levels need the chroma QP of the final QP */
     int at = B != NULL, al = A != NULL, ad = nb(g, -1, -1) != NULL;
@@ -718,6 +743,11 @@ static void encode_mb(G *g) {
         predc(g, 1 + c, cpm, predc_[c]);
         int x[64];
         for (int i = 0; i < 64; i++) x[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
+        if (g->lossless) {  /* intra_chroma_pred_mode 1 horizontal, 2 vertical */
+            if (cpm == 1 || cpm == 2) dpcm_diff(x, lvc[c], 8, cpm == 2 ? 0 : 1);
+            else memcpy(lvc[c], x, sizeof(x));
+            continue;
+        }
         Basis *Bs = &g_bc[c][qpc[c]];
         build_basis(Bs, 3, qpc[c], g_w4[1 + c]);
         quantize(Bs, x, lvc[c], maxlev);
@@ -804,12 +834,18 @@ static void encode_mb(G *g) {
             predict_nxn(g, n, bm, &o, p);
             int x[64], rr[64];
             for (int k = 0; k < n * n; k++) x[k] = g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k];
-            Basis *Bs = t8 ? &g_b8[qpl] : &g_b4[qpl];
-            build_basis(Bs, t8 ? 1 : 0, qpl, t8 ? g_w8 : g_w4[0]);
             int *lv = t8 ? lv8[i] : lv4[blk];
-            quantize(Bs, x, lv, maxlev);
-            fit(t8 ? 1 : 0, lv, qpl, t8 ? g_w8 : g_w4[0]);
-            if (t8) res8(lv, qpl, rr, g_w8); else res4(lv, qpl, rr, g_w4[0]);
+            if (g->lossless) {  /* transform bypass: exact reconstruction */
+                if (bm <= 1) dpcm_diff(x, lv, n, bm);
+                else memcpy(lv, x, sizeof(int) * (size_t)(n * n));
+                memcpy(rr, x, sizeof(int) * (size_t)(n * n));
+            } else {
+                Basis *Bs = t8 ? &g_b8[qpl] : &g_b4[qpl];
+                build_basis(Bs, t8 ? 1 : 0, qpl, t8 ? g_w8 : g_w4[0]);
+                quantize(Bs, x, lv, maxlev);
+                fit(t8 ? 1 : 0, lv, qpl, t8 ? g_w8 : g_w4[0]);
+                if (t8) res8(lv, qpl, rr, g_w8); else res4(lv, qpl, rr, g_w4[0]);
+            }
             put(g, 0, gx + bx, gy + by, n, p, rr);
         }
     }
@@ -934,13 +970,15 @@ static void encode_mb(G *g) {
     }
     /* reconstruction of I16x16 luma and chroma */
     if (is16) {
-        res_dc(lv16, 16, qpl, r, g_w4[0]);
         pred16(g, mode16, pred);
+        if (g->lossless) for (int i = 0; i < 256; i++) r[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
+        else res_dc(lv16, 16, qpl, r, g_w4[0]);
         put(g, 0, gx, gy, 16, pred, r);
     }
     for (int c = 0; c < 2; c++) {
         int rr[64];
-        res_dc(lvc[c], 8, qpc[c], rr, g_w4[1 + c]);
+        if (g->lossless) for (int i = 0; i < 64; i++) rr[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
+        else res_dc(lvc[c], 8, qpc[c], rr, g_w4[1 + c]);
         put(g, 1 + c, gx / 2, gy / 2, 8, predc_[c], rr);
     }
     if (!is16) for (int i = 0; i < 16; i++) if (t8) {} /* ipm already set */
@@ -1019,7 +1057,7 @@ static void write_sps(FILE *f, G *g, int profile) {
     if (profile >= 100) {
         bw_ue(&b, 1);
         bw_ue(&b, (uint32_t)(g->bd - 8)); bw_ue(&b, (uint32_t)(g->bd - 8));
-        bw_put(&b, 0, 1); /* transform bypass */
+        bw_put(&b, (uint32_t)g->lossless, 1); /* qpprime_y_zero_transform_bypass_flag (--lossless) */
         g_sps_m_on = g->sm == 1 || g->sm == 2;
         bw_put(&b, (uint32_t)g_sps_m_on, 1); /* seq_scaling_matrix_present_flag */
         if (g_sps_m_on) write_matrices(&b, &g_sps_m, NULL, 2);
@@ -1129,11 +1167,15 @@ int main(int argc, char **argv) {
     g->vuireorder = opt_int(argc, argv, "--vuireorder", -1);
     g->vuicpb = opt_int(argc, argv, "--vuicpb", -1);
     g->ilsps = opt_int(argc, argv, "--ilsps", 0);
+    /* --lossless 1: High 4:4:4 Predictive (profile_idc 244) with qpprime_y_zero_transform_bypass_flag,
+     * every macroblock at QP'Y 0 (TransformBypassModeFlag), residual DPCM for H / V predictions */
+    g->lossless = opt_int(argc, argv, "--lossless", 0);
+    if (g->lossless) { g->qp = -6 * (g->bd - 8); g->qpdelta = 0; }
     g->rawcrop[0] = -1;
     if (opt_str(argc, argv, "--crop"))
         sscanf(opt_str(argc, argv, "--crop"), "%lld,%lld,%lld,%lld", &g->rawcrop[0], &g->rawcrop[1], &g->rawcrop[2], &g->rawcrop[3]);
     if (g->delay > 6) { fprintf(stderr, "--delay <= 6 (4-bit POC lsb)\n"); return 2; }
-    int profile = opt_int(argc, argv, "--profile", g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm ? 100 : 77));
+    int profile = opt_int(argc, argv, "--profile", (g->lossless || g->bd > 10) ? 244 : g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm ? 100 : 77));
     g_lim = 1 << (7 + g->bd);
     g->W = (g->outW + 15) & ~15; g->H = g->ilsps ? (g->outH + 31) & ~31 : (g->outH + 15) & ~15;
     if (g->ilsps && (g->H - g->outH) % 4) { fprintf(stderr, "--ilsps: the height must crop in 4-row units\n"); return 2; }
@@ -1171,7 +1213,7 @@ int main(int argc, char **argv) {
         bw_put(&b, 0, 4);                     /* poc lsb */
         if (!g->nonidr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } /* dec_ref_pic_marking (IDR) */
         else bw_put(&b, 0, 1);                /* adaptive_ref_pic_marking_mode_flag */
-        int sqp = clip3(-6 * (g->bd - 8), 51, g->qp + (nslice ? rndn(5) - 2 : 0));
+        int sqp = clip3(-6 * (g->bd - 8), 51, g->qp + (nslice && !g->lossless ? rndn(5) - 2 : 0));
         bw_se(&b, sqp - 26);
         int idc = g->dbidc;
         bw_ue(&b, (uint32_t)idc);

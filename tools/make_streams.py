@@ -248,6 +248,14 @@ PARITY264 = [
     # field MB rows, vertical crop in 4-row units, field_pic_flag in the slice header
     ("a23_416x232_ilsps_frame", 416, 232, 8, 27, 55, 2, ["--ilsps", "1", "--slices", "4"]),
     ("a24_336x180_ilsps_frame_cavlc", 336, 180, 8, 24, 56, 3, ["--ilsps", "1", "--cavlc", "1"]),
+    # High 4:4:4 Predictive (profile_idc 244): lossless transform bypass (qpprime_y_zero_transform_bypass_flag,
+    # QP'Y 0, residual DPCM for vertical / horizontal predictions) and 4:2:0 at 12 / 14 bits
+    ("a25_176x144_lossless_cabac", 176, 144, 8, 0, 57, 6, ["--lossless", "1", "--pcm", "1"]),
+    ("a26_192x112_lossless_cavlc_4x4", 192, 112, 8, 0, 58, 8, ["--lossless", "1", "--cavlc", "1", "--t8x8", "0"]),
+    ("a27_208x128_lossless_14bit", 208, 128, 14, 0, 59, 5, ["--lossless", "1"]),
+    ("a28_256x144_12bit_high444", 256, 144, 12, 22, 60, 4, ["--t8x8", "1", "--slices", "3"]),
+    ("a29_192x112_14bit_cavlc_pcm", 192, 112, 14, 14, 61, 6, ["--cavlc", "1", "--pcm", "1"]),
+    ("a30_160x96_lossless_10bit_slices", 160, 96, 10, 0, 62, 4, ["--lossless", "1", "--slices", "2"]),
 ]
 
 
@@ -357,6 +365,8 @@ MALFORMED = [
     ("m_avc_vui_reorder17", 264, 160, 96, ["--vuireorder", "17"], "fail"),
     ("m_avc_vui_cpb33", 264, 160, 96, ["--vuicpb", "32", "--vuireorder", "0"], "fail"),
     ("m_avc_vui_cpb32_ok", 264, 160, 96, ["--vuicpb", "31", "--vuireorder", "0"], "ok"),
+    # FFmpeg 4.3 has no 11- / 13-bit H.264 output format (h264_slice.c "Unsupported bit depth")
+    ("m_avc_bitdepth11", 264, 160, 96, ["@bd", "11"], "fail"),
 ]
 
 
@@ -366,15 +376,17 @@ def malformed():
     planes = source_planes()
     manifest = []
     for k, (name, codec, W, H, opts, expect) in enumerate(MALFORMED):
-        content = make_content(planes, W, H, 70 + k, 2, 8)
+        bd = int(opts[1]) if opts[:1] == ["@bd"] else 8  # "@bd N": the stream's bit depth
+        gopts = opts[2:] if opts[:1] == ["@bd"] else opts
+        content = make_content(planes, W, H, 70 + k, 2, bd)
         ext = ".h265" if codec == 265 else ".h264"
         path = os.path.join(out_dir, name + ext)
         yuv = path + ".yuv"
         with open(yuv, "wb") as f:
             for p in content:
-                f.write(p.astype(np.uint8).tobytes())
-        subprocess.check_call([GEN if codec == 265 else GEN264, yuv, str(W), str(H), "8", "27", str(70 + k), path]
-                              + opts)
+                f.write(p.astype(np.uint8 if bd == 8 else np.dtype("<u2")).tobytes())
+        subprocess.check_call([GEN if codec == 265 else GEN264, yuv, str(W), str(H), str(bd), "27", str(70 + k), path]
+                              + gopts)
         os.remove(yuv)
         manifest.append({"file": name + ext, "codec": codec, "options": opts, "expect": expect})
         print(f"{path}: {os.path.getsize(path)} B, expect {expect}", flush=True)
