@@ -112,6 +112,17 @@ static const uint8_t k_last8x8[64] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 
 
 /* zigzag scans (frame) */
 static const uint8_t k_zz4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+/* field scans (Table 8-13 / 8.5.7, field macroblocks): raster index y * n + x per scan position */
+static const uint8_t k_fld4[16] = {0, 4, 1, 8, 12, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+static const uint8_t k_fld8[64] = {0,  8,  16, 1,  9,  24, 32, 17, 2,  25, 40, 48, 56, 33, 10, 3,
+                                   18, 41, 49, 57, 26, 11, 4,  19, 34, 42, 50, 58, 27, 12, 5,  20,
+                                   35, 43, 51, 59, 28, 13, 6,  21, 36, 44, 52, 60, 29, 14, 22, 37,
+                                   45, 53, 61, 30, 7,  15, 38, 46, 54, 62, 23, 31, 39, 47, 55, 63};
+/* significant_coeff_flag ctxIdxInc of 8x8 blocks in field macroblocks (Table 9-43, field column) */
+static const uint8_t k_sig8x8_fld[63] = {0,  1,  1,  2,  2,  3,  3,  4,  5,  6,  7,  7,  7,  8,  4,  5,
+                                         6,  9,  10, 10, 8,  11, 12, 11, 9,  9,  10, 10, 8,  11, 12, 11,
+                                         9,  9,  10, 10, 8,  11, 12, 11, 9,  9,  10, 10, 8,  13, 13, 9,
+                                         9,  10, 10, 8,  13, 13, 9,  9,  10, 10, 14, 14, 14, 14, 14};
 static const uint8_t k_zz8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                   12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                   35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
@@ -362,6 +373,8 @@ typedef struct {
     uint8_t cbf_dc[3];  /* luma DC (I16x16), Cb DC, Cr DC */
     uint8_t tc[16];     /* CAVLC: TotalCoeff of each luma 4x4 block (I16x16: AC block) */
     uint8_t tcc[2][4];  /* CAVLC: TotalCoeff of each chroma AC block */
+    int field;          /* MBAFF: mb_field_decoding_flag of the macroblock's pair */
+    int vx, vy;         /* position in the macroblock grid (MBAFF: vy = 2 * pair row + bottom) */
 } MbInfo;
 
 typedef struct {
@@ -375,6 +388,8 @@ typedef struct {
     const H4Sps *s;
     const H4Pps *p;
     int W, H, mbw, mbh, bd, bdc, qpbd, qpbdc;
+    int mbaff; /* MbaffFrameFlag: macroblock pairs; MbInfo at (vx, vy = 2 * pair row + bottom) */
+    int cur_field; /* mb_field_decoding_flag of the pair being decoded */
     uint16_t *pl[3];
     int st[3];
     MbInfo *mb;
@@ -406,28 +421,133 @@ static void init_ctx(H4Dec *d, int qp) {
 static inline int bin(H4Dec *d, int ctx) { return oc_decision(&d->cc, &d->ctx[ctx]); }
 static inline int byp(H4Dec *d) { return oc_bypass(&d->cc); }
 
-/* neighbouring MB (A left, B top, C top-right, D top-left) in the same slice */
-static MbInfo *nb_mb(H4Dec *d, int dx, int dy) {
-    int x = d->mbx + dx, y = d->mby + dy;
+/* the macroblock at grid position (x, y) if it is decoded in the current slice */
+static MbInfo *mb_in_slice(H4Dec *d, int x, int y) {
     if (x < 0 || y < 0 || x >= d->mbw || y >= d->mbh) return NULL;
     MbInfo *m = &d->mb[y * d->mbw + x];
     MbInfo *c = &d->mb[d->mby * d->mbw + d->mbx];
-    if (m->slice < 0 || m->slice != c->slice) return NULL;
-    /* must precede in decoding order (raster): dy < 0, or dy == 0 && dx < 0 */
-    if (dy > 0 || (dy == 0 && dx >= 0)) return NULL;
+    return (m->slice < 0 || m->slice != c->slice) ? NULL : m;
+}
+
+/* 6.4.12: the macroblock covering location (xN, yN) relative to the current macroblock's
+ * upper-left sample (maxW x maxH: 16 x 16 luma, 8 x 8 chroma) and the location (xW, yW) inside
+ * it; NULL when not available.  Non-MBAFF: 6.4.12.1 (raster neighbours, decoding order).  MBAFF:
+ * 6.4.12.2 -- pairs A / B / C / D left / above / above-right / above-left, then Table 6-4. */
+static MbInfo *nb_loc(H4Dec *d, int xN, int yN, int maxW, int maxH, int *xW, int *yW) {
+    MbInfo *cur = &d->mb[d->mby * d->mbw + d->mbx];
+    if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return NULL;
+    *xW = (xN + maxW) % maxW;
+    if (!d->mbaff) {
+        int dx = xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0), dy = yN < 0 ? -1 : 0;
+        *yW = (yN + maxH) % maxH;
+        return (dx == 0 && dy == 0) ? cur : mb_in_slice(d, d->mbx + dx, d->mby + dy);
+    }
+    const int px = d->mbx, py = d->mby >> 1, top = !(d->mby & 1), frame = !cur->field;
+    MbInfo *X = NULL, *N = NULL; /* X: top MB of the neighbouring pair */
+    int yM = yN, bot = 0;        /* N = X (bot 0) or X's bottom MB (bot 1) */
+    if (xN >= 0 && xN <= maxW - 1 && yN >= 0) {
+        *yW = yN;
+        return cur;
+    }
+    if (xN < 0 && yN < 0) { /* D */
+        if (frame && !top) {
+            /* a bottom frame MB's upper-left neighbour: the left pair's top frame MB, last row, or
+             * -- left field pair -- its bottom field MB's middle row (the picture sample above-left;
+             * FFmpeg fill_decode_neighbors: topleft_xy += mb_stride, "take top left ... from the
+             * middle of the mb") */
+            X = mb_in_slice(d, px - 1, 2 * py);
+            if (!X) return NULL;
+            bot = X->field ? 1 : 0;
+            yM = X->field ? (yN + maxH) >> 1 : yN;
+        } else if (frame || !top) {
+            X = mb_in_slice(d, px - 1, 2 * py - 2);
+            bot = 1;
+        } else {
+            X = mb_in_slice(d, px - 1, 2 * py - 2);
+            if (!X) return NULL;
+            if (X->field) bot = 0; else { bot = 1; yM = 2 * yN; }
+        }
+    } else if (xN < 0) { /* A, 0 <= yN <= maxH - 1 */
+        X = mb_in_slice(d, px - 1, 2 * py);
+        if (!X) return NULL;
+        if (frame) {
+            if (top) {
+                if (!X->field) { bot = 0; yM = yN; }
+                else { bot = yN & 1; yM = yN >> 1; }
+            } else {
+                if (!X->field) { bot = 1; yM = yN; }
+                else { bot = yN & 1; yM = (yN + maxH) >> 1; }
+            }
+        } else {
+            if (top) {
+                if (!X->field) { if (yN < maxH / 2) { bot = 0; yM = yN << 1; } else { bot = 1; yM = (yN << 1) - maxH; } }
+                else { bot = 0; yM = yN; }
+            } else {
+                if (!X->field) { if (yN < maxH / 2) { bot = 0; yM = (yN << 1) + 1; } else { bot = 1; yM = (yN << 1) + 1 - maxH; } }
+                else { bot = 1; yM = yN; }
+            }
+        }
+    } else if (xN <= maxW - 1) { /* B, yN < 0 */
+        if (frame && !top) {
+            X = &d->mb[(2 * py) * d->mbw + px]; /* CurrMbAddr - 1: the pair's top MB */
+            bot = 0;
+        } else if (frame || !top) {
+            X = mb_in_slice(d, px, 2 * py - 2);
+            bot = 1;
+        } else {
+            X = mb_in_slice(d, px, 2 * py - 2);
+            if (!X) return NULL;
+            if (X->field) bot = 0; else { bot = 1; yM = 2 * yN; }
+        }
+    } else { /* C, yN < 0 */
+        if (frame && !top) return NULL;
+        if (frame || !top) {
+            X = mb_in_slice(d, px + 1, 2 * py - 2);
+            bot = 1;
+        } else {
+            X = mb_in_slice(d, px + 1, 2 * py - 2);
+            if (!X) return NULL;
+            if (X->field) bot = 0; else { bot = 1; yM = 2 * yN; }
+        }
+    }
+    if (!X) return NULL;
+    N = &d->mb[(X->vy + bot) * d->mbw + X->vx];
+    *yW = (yM + maxH) % maxH;
+    return N;
+}
+
+/* neighbouring MB (A left, B top, C top-right, D top-left): the MB covering luma location
+ * (-1, 0) / (0, -1) / (16, -1) / (-1, -1) (6.4.11.1) */
+static MbInfo *nb_mb(H4Dec *d, int dx, int dy) {
+    int xW, yW;
+    return nb_loc(d, dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
+}
+
+static const uint8_t k_blk_of[4][4] = {{0, 1, 4, 5}, {2, 3, 6, 7}, {8, 9, 12, 13}, {10, 11, 14, 15}};
+/* neighbour 4x4 luma block (6.4.11.4): the block covering luma location (4 bx, 4 by) relative to
+ * the current MB (bx, by in 4x4 units, may be -1 / 4); returns the MB and the block index */
+static MbInfo *nb_blk(H4Dec *d, int bx, int by, int *nblk) {
+    int xW, yW;
+    MbInfo *m = nb_loc(d, bx * 4, by * 4, 16, 16, &xW, &yW);
+    *nblk = m ? k_blk_of[yW >> 2][xW >> 2] : 0;
     return m;
 }
 
-/* neighbour 4x4 luma block: returns MbInfo* and block index; blk coords in 4x4 units relative to MB (may be -1 / 4) */
-static MbInfo *nb_blk(H4Dec *d, int bx, int by, int *nblk) {
-    int dx = 0, dy = 0;
-    if (bx < 0) { dx = -1; bx += 4; }
-    if (by < 0) { dy = -1; by += 4; }
-    if (bx > 3) { dx = 1; bx -= 4; }
-    MbInfo *m = (dx == 0 && dy == 0) ? &d->mb[d->mby * d->mbw + d->mbx] : nb_mb(d, dx, dy);
-    static const uint8_t blk_of[4][4] = {{0, 1, 4, 5}, {2, 3, 6, 7}, {8, 9, 12, 13}, {10, 11, 14, 15}};
-    *nblk = blk_of[by][bx];
-    return m;
+/* picture position of sample (xW, yW) of component c of macroblock N (MBAFF field macroblocks
+ * interleave the rows of their pair: top field even rows, bottom field odd rows) */
+static void mb_phys(const H4Dec *d, const MbInfo *N, int c, int xW, int yW, int *X, int *Y) {
+    const int S = c ? 8 : 16;
+    *X = N->vx * S + xW;
+    if (!d->mbaff) { *Y = N->vy * S + yW; return; }
+    const int py = N->vy >> 1, bot = N->vy & 1;
+    *Y = N->field ? 2 * py * S + 2 * yW + bot : (2 * py + bot) * S + yW;
+}
+/* sample store of the current macroblock at grid position (x, y) of component c */
+static void put_sample(H4Dec *d, int c, int x, int y, int v) {
+    const int S = c ? 8 : 16;
+    int X, Y;
+    mb_phys(d, &d->mb[d->mby * d->mbw + d->mbx], c, x - d->mbx * S, y - d->mby * S, &X, &Y);
+    d->pl[c][Y * d->st[c] + X] = (uint16_t)v;
 }
 
 /* ------------------------------------------------------------ CABAC syntax elements */
@@ -451,16 +571,18 @@ static int dec_cbp(H4Dec *d) {
     for (int b8 = 0; b8 < 4; b8++) {
         int bx = (b8 & 1) * 2, by = (b8 >> 1) * 2;
         int ca, cb;
-        /* left neighbour 8x8 */
+        /* left / upper neighbour 8x8 block (6.4.11.2: the block covering luma location
+         * (x - 1, y) / (x, y - 1); MBAFF through Table 6-4) */
+        int xW, yW;
         if (bx == 0) {
-            MbInfo *A = nb_mb(d, -1, 0);
-            ca = A ? (A->mb_type == MB_I_PCM ? 0 : !((A->cbp >> (b8 + 1)) & 1)) : 0;
+            MbInfo *A = nb_loc(d, -1, by * 4, 16, 16, &xW, &yW);
+            ca = A ? (A->mb_type == MB_I_PCM ? 0 : !((A->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
         } else {
             ca = !((cbp >> (b8 - 1)) & 1);
         }
         if (by == 0) {
-            MbInfo *B = nb_mb(d, 0, -1);
-            cb = B ? (B->mb_type == MB_I_PCM ? 0 : !((B->cbp >> (b8 + 2)) & 1)) : 0;
+            MbInfo *B = nb_loc(d, bx * 4, -1, 16, 16, &xW, &yW);
+            cb = B ? (B->mb_type == MB_I_PCM ? 0 : !((B->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
         } else {
             cb = !((cbp >> (b8 - 2)) & 1);
         }
@@ -523,6 +645,10 @@ static int residual_block(H4Dec *d, int cat, int cbf_inc, int maxNum, int *out) 
     static const int sig_off[6] = {0, 15, 29, 44, 47, 0};
     static const int abs_off[6] = {0, 10, 20, 30, 39, 0};
     memset(out, 0, sizeof(int) * maxNum);
+    /* field macroblocks (MBAFF): significant / last contexts at ctxIdxOffset 277 / 338 (cat < 5)
+     * and 436 / 451 with the field ctxIdxInc table (cat 5) instead of 105 / 166, 402 / 417 */
+    const int fld = d->mb[d->mby * d->mbw + d->mbx].field;
+    const int sig0 = fld ? 277 : 105, last0 = fld ? 338 : 166;
     if (cat != 5) {
         if (!bin(d, 85 + cbf_off[cat] + cbf_inc)) return 0;
     }
@@ -532,15 +658,15 @@ static int residual_block(H4Dec *d, int cat, int cbf_inc, int maxNum, int *out) 
     for (i = 0; i < maxNum - 1; i++) {
         int sctx, lctx;
         if (cat == 5) {
-            sctx = 402 + k_sig8x8[i];
-            lctx = 417 + k_last8x8[i];
+            sctx = fld ? 436 + k_sig8x8_fld[i] : 402 + k_sig8x8[i];
+            lctx = (fld ? 451 : 417) + k_last8x8[i];
         } else if (cat == 3) {
             int inc = i < 2 ? i : 2; /* Min(i / NumC8x8, 2), 4:2:0 */
-            sctx = 105 + sig_off[cat] + inc;
-            lctx = 166 + sig_off[cat] + inc;
+            sctx = sig0 + sig_off[cat] + inc;
+            lctx = last0 + sig_off[cat] + inc;
         } else {
-            sctx = 105 + sig_off[cat] + i;
-            lctx = 166 + sig_off[cat] + i;
+            sctx = sig0 + sig_off[cat] + i;
+            lctx = last0 + sig_off[cat] + i;
         }
         if (bin(d, sctx)) {
             sig[nsig++] = i;
@@ -668,7 +794,18 @@ static int avail_luma(H4Dec *d, int x, int y, int cur_blk4) {
     return b < cur_blk4;
 }
 
-static int px(H4Dec *d, int c, int x, int y) { return d->pl[c][y * d->st[c] + x]; }
+/* sample at grid position (x, y) of component c, seen from the current macroblock (MBAFF: through
+ * the 6.4.12.2 neighbour mapping, e.g. a field MB's row above is the row two picture rows up);
+ * callers read only positions they found available */
+static int px(H4Dec *d, int c, int x, int y) {
+    if (!d->mbaff) return d->pl[c][y * d->st[c] + x];
+    const int S = c ? 8 : 16;
+    int xW, yW, X, Y;
+    MbInfo *N = nb_loc(d, x - d->mbx * S, y - d->mby * S, S, S, &xW, &yW);
+    if (!N) return 0;
+    mb_phys(d, N, c, xW, yW, &X, &Y);
+    return d->pl[c][Y * d->st[c] + X];
+}
 
 static void pred4x4(H4Dec *d, int blk, int mode, int *pred) {
     int x0 = k_blk_x[blk] * 4, y0 = k_blk_y[blk] * 4;
@@ -962,7 +1099,7 @@ static void put_block(H4Dec *d, int c, int gx, int gy, int n, const int *pred, c
     int maxv = (1 << (c ? d->bdc : d->bd)) - 1;
     for (int y = 0; y < n; y++)
         for (int x = 0; x < n; x++)
-            d->pl[c][(gy + y) * d->st[c] + gx + x] = (uint16_t)clip3(0, maxv, pred[y * n + x] + (res ? res[y * n + x] : 0));
+            put_sample(d, c, gx + x, gy + y, clip3(0, maxv, pred[y * n + x] + (res ? res[y * n + x] : 0)));
 }
 
 static int pred_mode_nb(H4Dec *d, int blk, int is8x8, int dir /* 0 A left, 1 B top */) {
@@ -1125,20 +1262,44 @@ static int recon_mb(H4Dec *d, MbInfo *m) {
     return 0;
 }
 
+/* position the decoder on macroblock address `addr` (MBAFF: pair addr / 2, bottom addr & 1) and,
+ * at the top macroblock of an MBAFF pair, read mb_field_decoding_flag (7.3.4: present for the
+ * top MB of every pair in I slices; CABAC ctxIdx 70 + condTermFlagA + condTermFlagB, the left /
+ * upper pair being available field pairs, 9.3.3.1.1.2) */
+static void mb_start(H4Dec *d, int addr, int cabac) {
+    if (!d->mbaff) {
+        d->mbx = addr % d->mbw;
+        d->mby = addr / d->mbw;
+        d->mb[addr].slice = d->nslice;
+        return;
+    }
+    const int pair = addr >> 1;
+    d->mbx = pair % d->mbw;
+    d->mby = 2 * (pair / d->mbw) + (addr & 1);
+    d->mb[d->mby * d->mbw + d->mbx].slice = d->nslice;
+    if (!(addr & 1)) {
+        MbInfo *A = mb_in_slice(d, d->mbx - 1, d->mby), *B = mb_in_slice(d, d->mbx, d->mby - 2);
+        d->cur_field = cabac ? bin(d, 70 + (A && A->field) + (B && B->field)) : ob_bit(&d->bits);
+    }
+}
+
 static int decode_mb(H4Dec *d, int slice_idx) {
     MbInfo *m = &d->mb[d->mby * d->mbw + d->mbx];
     memset(m, 0, sizeof(*m));
     m->slice = slice_idx;
+    m->vx = d->mbx;
+    m->vy = d->mby;
+    m->field = d->mbaff ? d->cur_field : 0;
     m->mb_type = dec_mb_type_I(d);
     const int gx = d->mbx * 16, gy = d->mby * 16;
     if (m->mb_type == MB_I_PCM) {
         OraBits *b = &d->bits;
         b->pos = (b->pos + 7) & ~7L;
         for (int y = 0; y < 16; y++)
-            for (int x = 0; x < 16; x++) d->pl[0][(gy + y) * d->st[0] + gx + x] = (uint16_t)ob_u(b, d->bd);
+            for (int x = 0; x < 16; x++) put_sample(d, 0, gx + x, gy + y, (int)ob_u(b, d->bd));
         for (int c = 1; c < 3; c++)
             for (int y = 0; y < 8; y++)
-                for (int x = 0; x < 8; x++) d->pl[c][(gy / 2 + y) * d->st[c] + gx / 2 + x] = (uint16_t)ob_u(b, d->bdc);
+                for (int x = 0; x < 8; x++) put_sample(d, c, gx / 2 + x, gy / 2 + y, (int)ob_u(b, d->bdc));
         oc_init(&d->cc, b);
         m->qp = d->qp;
         m->cbp = 0x2F;
@@ -1192,6 +1353,7 @@ static int decode_mb(H4Dec *d, int slice_idx) {
     m->qp = d->qp;
     /* ---- residual ---- */
     int coef[64];
+    const uint8_t *z4 = m->field ? k_fld4 : k_zz4, *z8 = m->field ? k_fld8 : k_zz8; /* 8.5.6 / 8.5.7 */
     memset(d->lvl4, 0, sizeof(d->lvl4));
     memset(d->lvl8, 0, sizeof(d->lvl8));
     memset(d->dc_l, 0, sizeof(d->dc_l));
@@ -1201,13 +1363,13 @@ static int decode_mb(H4Dec *d, int slice_idx) {
         int nb, ca = cbf_cond(d, 0, nb_mb(d, -1, 0), 0, 0), cb = cbf_cond(d, 0, nb_mb(d, 0, -1), 0, 0);
         (void)nb;
         m->cbf_dc[0] = (uint8_t)residual_block(d, 0, ca + 2 * cb, 16, coef);
-        for (int k = 0; k < 16; k++) d->dc_l[k_zz4[k]] = coef[k];
+        for (int k = 0; k < 16; k++) d->dc_l[z4[k]] = coef[k];
     }
     for (int b8 = 0; b8 < 4; b8++) {
         if (!((m->cbp >> b8) & 1)) continue;
         if (m->t8x8) {
             residual_block(d, 5, 0, 64, coef);
-            for (int k = 0; k < 64; k++) d->lvl8[b8][k_zz8[k]] = coef[k];
+            for (int k = 0; k < 64; k++) d->lvl8[b8][z8[k]] = coef[k];
             for (int k = 0; k < 4; k++) m->cbf[b8 * 4 + k] = 1;
             continue;
         }
@@ -1220,10 +1382,10 @@ static int decode_mb(H4Dec *d, int slice_idx) {
             int cb = cbf_cond(d, cat, B, nblk, 0);
             if (is16) {
                 m->cbf[blk] = (uint8_t)residual_block(d, 1, ca + 2 * cb, 15, coef);
-                for (int k = 0; k < 15; k++) d->lvl4[blk][k_zz4[k + 1]] = coef[k];
+                for (int k = 0; k < 15; k++) d->lvl4[blk][z4[k + 1]] = coef[k];
             } else {
                 m->cbf[blk] = (uint8_t)residual_block(d, 2, ca + 2 * cb, 16, coef);
-                for (int k = 0; k < 16; k++) d->lvl4[blk][k_zz4[k]] = coef[k];
+                for (int k = 0; k < 16; k++) d->lvl4[blk][z4[k]] = coef[k];
             }
         }
     }
@@ -1238,12 +1400,19 @@ static int decode_mb(H4Dec *d, int slice_idx) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 int bx = b4 & 1, by = b4 >> 1, ca, cb;
+                int xW, yW;
                 if (bx > 0) ca = m->cbf_c[c][b4 - 1];
-                else ca = cbf_cond(d, 4, nb_mb(d, -1, 0), b4 + 1, c);
+                else { /* 6.4.11.5: the chroma block covering chroma location (-1, 4 by) */
+                    MbInfo *A = nb_loc(d, -1, by * 4, 8, 8, &xW, &yW);
+                    ca = cbf_cond(d, 4, A, A ? (yW >> 2) * 2 + (xW >> 2) : 0, c);
+                }
                 if (by > 0) cb = m->cbf_c[c][b4 - 2];
-                else cb = cbf_cond(d, 4, nb_mb(d, 0, -1), b4 + 2, c);
+                else {
+                    MbInfo *B = nb_loc(d, bx * 4, -1, 8, 8, &xW, &yW);
+                    cb = cbf_cond(d, 4, B, B ? (yW >> 2) * 2 + (xW >> 2) : 0, c);
+                }
                 m->cbf_c[c][b4] = (uint8_t)residual_block(d, 4, ca + 2 * cb, 15, coef);
-                for (int k = 0; k < 15; k++) d->ac_c[c][b4][k_zz4[k + 1]] = coef[k];
+                for (int k = 0; k < 15; k++) d->ac_c[c][b4][z4[k + 1]] = coef[k];
             }
     }
     return recon_mb(d, m);
@@ -1344,17 +1513,18 @@ static int cavlc_nc_luma(H4Dec *d, int blk) {
 }
 static int cavlc_nc_chroma(H4Dec *d, MbInfo *m, int c, int b4) {
     int bx = b4 & 1, by = b4 >> 1, na = 0, nb = 0, aa = 1, ab = 1;
+    int xW, yW;
     if (bx) na = m->tcc[c][b4 - 1];
-    else {
-        MbInfo *A = nb_mb(d, -1, 0);
+    else { /* 6.4.11.5 */
+        MbInfo *A = nb_loc(d, -1, by * 4, 8, 8, &xW, &yW);
         if (!A) aa = 0;
-        else na = A->mb_type == MB_I_PCM ? 16 : A->tcc[c][b4 + 1];
+        else na = A->mb_type == MB_I_PCM ? 16 : A->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
     if (by) nb = m->tcc[c][b4 - 2];
     else {
-        MbInfo *B = nb_mb(d, 0, -1);
+        MbInfo *B = nb_loc(d, bx * 4, -1, 8, 8, &xW, &yW);
         if (!B) ab = 0;
-        else nb = B->mb_type == MB_I_PCM ? 16 : B->tcc[c][b4 + 2];
+        else nb = B->mb_type == MB_I_PCM ? 16 : B->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
     if (aa && ab) return (na + nb + 1) >> 1;
     return aa ? na : (ab ? nb : 0);
@@ -1364,6 +1534,9 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     MbInfo *m = &d->mb[d->mby * d->mbw + d->mbx];
     memset(m, 0, sizeof(*m));
     m->slice = slice_idx;
+    m->vx = d->mbx;
+    m->vy = d->mby;
+    m->field = d->mbaff ? d->cur_field : 0;
     OraBits *b = &d->bits;
     uint32_t mbt = ob_ue(b);
     if (mbt > 25) return -1;
@@ -1372,10 +1545,10 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     if (m->mb_type == MB_I_PCM) {
         b->pos = (b->pos + 7) & ~7L;
         for (int y = 0; y < 16; y++)
-            for (int x = 0; x < 16; x++) d->pl[0][(gy + y) * d->st[0] + gx + x] = (uint16_t)ob_u(b, d->bd);
+            for (int x = 0; x < 16; x++) put_sample(d, 0, gx + x, gy + y, (int)ob_u(b, d->bd));
         for (int c = 1; c < 3; c++)
             for (int y = 0; y < 8; y++)
-                for (int x = 0; x < 8; x++) d->pl[c][(gy / 2 + y) * d->st[c] + gx / 2 + x] = (uint16_t)ob_u(b, d->bdc);
+                for (int x = 0; x < 8; x++) put_sample(d, c, gx / 2 + x, gy / 2 + y, (int)ob_u(b, d->bdc));
         m->qp = d->qp;
         m->cbp = 0x2F;
         memset(m->tc, 16, sizeof(m->tc));
@@ -1417,6 +1590,7 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     }
     m->qp = d->qp;
     int coef[64];
+    const uint8_t *z4 = m->field ? k_fld4 : k_zz4, *z8 = m->field ? k_fld8 : k_zz8; /* 8.5.6 / 8.5.7 */
     memset(d->lvl4, 0, sizeof(d->lvl4));
     memset(d->lvl8, 0, sizeof(d->lvl8));
     memset(d->dc_l, 0, sizeof(d->dc_l));
@@ -1424,7 +1598,7 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     memset(d->ac_c, 0, sizeof(d->ac_c));
     if (is16) {
         if (cavlc_block(d, cavlc_nc_luma(d, 0), 16, coef) < 0) return -1;
-        for (int k = 0; k < 16; k++) d->dc_l[k_zz4[k]] = coef[k];
+        for (int k = 0; k < 16; k++) d->dc_l[z4[k]] = coef[k];
     }
     for (int b8 = 0; b8 < 4; b8++) {
         if (!((m->cbp >> b8) & 1)) continue;
@@ -1434,7 +1608,7 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
                 int tc = cavlc_block(d, cavlc_nc_luma(d, blk), 16, coef);
                 if (tc < 0) return -1;
                 m->tc[blk] = (uint8_t)tc;
-                for (int k = 0; k < 16; k++) d->lvl8[b8][k_zz8[4 * k + i4]] = coef[k];
+                for (int k = 0; k < 16; k++) d->lvl8[b8][z8[4 * k + i4]] = coef[k];
             }
             continue;
         }
@@ -1443,8 +1617,8 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
             int tc = cavlc_block(d, cavlc_nc_luma(d, blk), is16 ? 15 : 16, coef);
             if (tc < 0) return -1;
             m->tc[blk] = (uint8_t)tc;
-            if (is16) for (int k = 0; k < 15; k++) d->lvl4[blk][k_zz4[k + 1]] = coef[k];
-            else for (int k = 0; k < 16; k++) d->lvl4[blk][k_zz4[k]] = coef[k];
+            if (is16) for (int k = 0; k < 15; k++) d->lvl4[blk][z4[k + 1]] = coef[k];
+            else for (int k = 0; k < 16; k++) d->lvl4[blk][z4[k]] = coef[k];
         }
     }
     if (m->cbp >> 4) {
@@ -1459,7 +1633,7 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
                 int tc = cavlc_block(d, cavlc_nc_chroma(d, m, c, b4), 15, coef);
                 if (tc < 0) return -1;
                 m->tcc[c][b4] = (uint8_t)tc;
-                for (int k = 0; k < 15; k++) d->ac_c[c][b4][k_zz4[k + 1]] = coef[k];
+                for (int k = 0; k < 15; k++) d->ac_c[c][b4][z4[k + 1]] = coef[k];
             }
     }
     return recon_mb(d, m);
@@ -1576,6 +1750,95 @@ static void deblock_mb(H4Dec *d, int mx, int my) {
     }
 }
 
+/* ---- MBAFF deblocking (8.7 with MbaffFrameFlag 1; FFmpeg h264_loopfilter.c, the decoder behind
+ * /root/reference/src/Decoder.cpp:324).  Every edge is a set of sample lines in picture
+ * coordinates: vertical edges run along picture rows (a field MB's rows are every other picture
+ * row, and the p side of its left MB edge is the left pair's MB holding the same picture row);
+ * horizontal edges step through the MB's own rows (field MB: 2 picture rows) and its top MB edge
+ * reaches up the same way; a frame top MB under a field pair filters its top edge twice in field
+ * mode (8.7: "filtered ... with fieldModeInFrameFilteringFlag 1", FFmpeg filter_mb_dir's "special
+ * case ... done twice").  All-intra bS: 4 on vertical MB edges and on horizontal MB edges between
+ * two frame MBs, 3 otherwise. */
+static MbInfo *pair_mb_at_row(H4Dec *d, int px, int py, int c, int Y) {
+    const int S = c ? 8 : 16;
+    MbInfo *top = &d->mb[(2 * py) * d->mbw + px];
+    const int r = Y - 2 * py * S;
+    const int bot = top->field ? (r & 1) : (r >= S);
+    return &d->mb[(2 * py + bot) * d->mbw + px];
+}
+static void filt_mbaff(H4Dec *d, int c, uint16_t *q, int step, int bs, const MbInfo *P, const MbInfo *Q, const H4Slice *sl) {
+    int qa;
+    if (c == 0) {
+        qa = (mb_qp_for_filter(P) + mb_qp_for_filter(Q) + 1) >> 1;
+    } else {
+        int off = c == 1 ? sl->chroma_qp_offset : sl->chroma_qp_offset2;
+        int qpp = chroma_qp(clip3(-d->qpbdc, 51, mb_qp_for_filter(P) + off));
+        int qpq = chroma_qp(clip3(-d->qpbdc, 51, mb_qp_for_filter(Q) + off));
+        qa = (qpp + qpq + 1) >> 1;
+    }
+    const int bd = c ? d->bdc : d->bd;
+    int ia = clip3(0, 51, qa + sl->alpha_off), ib = clip3(0, 51, qa + sl->beta_off);
+    int alpha = k_alpha[ia] * (1 << (bd - 8)), beta = k_beta[ib] * (1 << (bd - 8));
+    int tc0 = bs < 4 ? k_tc0[ia][bs - 1] * (1 << (bd - 8)) : 0;
+    filt_line(q, step, bs, alpha, beta, tc0, c > 0, (1 << bd) - 1);
+}
+static void deblock_mb_mbaff(H4Dec *d, int mx, int vy) {
+    MbInfo *m = &d->mb[vy * d->mbw + mx];
+    const H4Slice *sl = &d->sl[m->slice];
+    if (sl->disable_deblock == 1) return;
+    const int py = vy >> 1, bot = vy & 1;
+    int left = mx > 0;
+    if (left) {
+        const MbInfo *L = &d->mb[(2 * py) * d->mbw + mx - 1];
+        if (L->slice < 0 || (sl->disable_deblock == 2 && L->slice != m->slice)) left = 0;
+    }
+    int top;
+    if (!m->field && bot) top = 1; /* the pair's internal edge (CurrMbAddr - 1) */
+    else if (py == 0) top = 0;
+    else {
+        const MbInfo *B = &d->mb[(2 * py - 2) * d->mbw + mx];
+        top = B->slice >= 0 && !(sl->disable_deblock == 2 && B->slice != m->slice);
+    }
+    for (int c = 0; c < 3; c++) {
+        const int S = c ? 8 : 16, st = d->st[c];
+        uint16_t *pl = d->pl[c];
+        for (int dir = 0; dir < 2; dir++) {
+            for (int e = 0; e < S; e += 4) {
+                if (c == 0 && (e == 4 || e == 12) && m->t8x8) continue;
+                if (dir == 0) { /* vertical edge at column e */
+                    if (e == 0 && !left) continue;
+                    for (int r = 0; r < S; r++) {
+                        int X, Y;
+                        mb_phys(d, m, c, e, r, &X, &Y);
+                        const MbInfo *P = e == 0 ? pair_mb_at_row(d, mx - 1, py, c, Y) : m;
+                        filt_mbaff(d, c, &pl[Y * st + X], 1, e == 0 ? 4 : 3, P, m, sl);
+                    }
+                    continue;
+                }
+                if (e == 0 && !top) continue;
+                int X0, Yq;
+                mb_phys(d, m, c, 0, e, &X0, &Yq);
+                if (e == 0 && !m->field && !bot && d->mb[(2 * py - 2) * d->mbw + mx].field) {
+                    for (int j = 0; j < 2; j++) { /* top field lines, then bottom field lines */
+                        const MbInfo *P = &d->mb[(2 * py - 2 + j) * d->mbw + mx];
+                        for (int x = 0; x < S; x++) filt_mbaff(d, c, &pl[(Yq + j) * st + X0 + x], 2 * st, 3, P, m, sl);
+                    }
+                    continue;
+                }
+                const int step = m->field ? 2 * st : st;
+                const MbInfo *P = m;
+                int bs = 3;
+                if (e == 0) {
+                    P = (!m->field && bot) ? &d->mb[(2 * py) * d->mbw + mx]
+                                           : pair_mb_at_row(d, mx, py - 1, c, Yq - (m->field ? 2 : 1));
+                    bs = (!m->field && !P->field) ? 4 : 3;
+                }
+                for (int x = 0; x < S; x++) filt_mbaff(d, c, &pl[Yq * st + X0 + x], step, bs, P, m, sl);
+            }
+        }
+    }
+}
+
 /* ------------------------------------------------------------ top level */
 int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture *out) {
     memset(out, 0, sizeof(*out));
@@ -1609,11 +1872,12 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             /* field_pic_flag: a field (PAFF) -- FFmpeg outputs no frame for the first field alone
              * (h264dec.c "Wait for second field"), so the reference returns false */
             if (!s->frame_mbs_only && ob_u(&b, 1)) { ret = -3; goto done; }
-            if (s->mbaff) { ret = -3; goto done; } /* MBAFF: not restated */
+            int field_pic = 0; /* (a field picture returned above) */
+            (void)field_pic;
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
             /* FFmpeg: "first_mb_in_slice overflow" drops the slice; picture 0 is output from the
              * slices already collected, and fails only when none was */
-            if (first_mb < 0 || first_mb >= s->mb_w * s->mb_h) {
+            if (first_mb < 0 || first_mb * (1 + s->mbaff) >= s->mb_w * s->mb_h) {
                 if (have) break;
                 ret = -6;
                 goto done;
@@ -1663,6 +1927,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 d->bd = s->bit_depth;
                 d->bdc = s->bit_depth_c;
                 d->qpbd = 6 * (d->bd - 8);
+                d->mbaff = s->mbaff; /* MbaffFrameFlag = mb_adaptive_frame_field_flag && !field_pic_flag */
                 d->qpbdc = 6 * (d->bdc - 8);
                 for (int c = 0; c < 3; c++) {
                     int w = c ? d->W / 2 : d->W, h = c ? d->H / 2 : d->H;
@@ -1678,7 +1943,8 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             d->p = p;
             d->qp = p->init_qp + qpd;
             d->prev_qpd_nz = 0;
-            int mbaddr = first_mb;
+            /* MBAFF: CurrMbAddr = first_mb_in_slice * 2, macroblocks in pair order (top, bottom) */
+            int mbaddr = first_mb * (1 + d->mbaff);
             if (p->cabac) {
                 /* cabac_alignment_one_bit */
                 while (b.pos & 7) ob_u(&b, 1);
@@ -1687,9 +1953,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 init_ctx(d, d->qp);
                 for (;;) {
                     if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
-                    d->mbx = mbaddr % d->mbw;
-                    d->mby = mbaddr / d->mbw;
-                    d->mb[mbaddr].slice = d->nslice;
+                    mb_start(d, mbaddr, 1);
                     decode_mb(d, d->nslice);
                     if (oc_terminate(&d->cc)) break;
                     mbaddr++;
@@ -1698,9 +1962,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 d->bits = b;
                 for (;;) {
                     if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
-                    d->mbx = mbaddr % d->mbw;
-                    d->mby = mbaddr / d->mbw;
-                    d->mb[mbaddr].slice = d->nslice;
+                    mb_start(d, mbaddr, 0);
                     if (decode_mb_cavlc(d, d->nslice) < 0) { ret = -21; goto done_free; }
                     if (!ob_more_rbsp(&d->bits)) break;
                     mbaddr++;
@@ -1714,9 +1976,16 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
     }
     if (!have) { ret = -9; goto done; }
     if (!(flags & 1)) {
-        for (int my = 0; my < d->mbh; my++)
-            for (int mx = 0; mx < d->mbw; mx++)
-                if (d->mb[my * d->mbw + mx].slice >= 0) deblock_mb(d, mx, my);
+        if (d->mbaff) { /* macroblock address order: pairs in raster order, top MB then bottom MB */
+            for (int pr = 0; pr < d->mbh / 2; pr++)
+                for (int mx = 0; mx < d->mbw; mx++)
+                    for (int bt = 0; bt < 2; bt++)
+                        if (d->mb[(2 * pr + bt) * d->mbw + mx].slice >= 0) deblock_mb_mbaff(d, mx, 2 * pr + bt);
+        } else {
+            for (int my = 0; my < d->mbh; my++)
+                for (int mx = 0; mx < d->mbw; mx++)
+                    if (d->mb[my * d->mbw + mx].slice >= 0) deblock_mb(d, mx, my);
+        }
     }
     {
         const H4Sps *s = d->s;

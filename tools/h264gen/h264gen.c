@@ -160,6 +160,14 @@ static const uint8_t k_last8x8[64] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 
                                       2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4,
                                       4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8, 8};
 static const uint8_t k_zz4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+/* field scans (field macroblocks, 8.5.6 / 8.5.7) and the field-coded 8x8 significance contexts (Table 9-43) */
+static const uint8_t k_fld4[16] = {0, 4, 1, 8, 12, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+static const uint8_t k_fld8[64] = {0, 8, 16, 1, 9, 24, 32, 17, 2, 25, 40, 48, 56, 33, 10, 3, 18, 41, 49, 57, 26, 11,
+                                   4, 19, 34, 42, 50, 58, 27, 12, 5, 20, 35, 43, 51, 59, 28, 13, 6, 21, 36, 44,
+                                   52, 60, 29, 14, 22, 37, 45, 53, 61, 30, 7, 15, 38, 46, 54, 62, 23, 31, 39, 47, 55, 63};
+static const uint8_t k_sig8x8_fld[63] = {0, 1, 1, 2, 2, 3, 3, 4, 5, 6, 7, 7, 7, 8, 4, 5, 6, 9, 10, 10, 8, 11,
+                                         12, 11, 9, 9, 10, 10, 8, 11, 12, 11, 9, 9, 10, 10, 8, 11, 12, 11, 9, 9,
+                                         10, 10, 8, 13, 13, 9, 9, 10, 10, 8, 13, 13, 9, 9, 10, 10, 14, 14, 14, 14, 14};
 static const uint8_t k_zz8[64] = {0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
                                   41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
                                   30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
@@ -172,10 +180,11 @@ typedef struct {
     int slice, mb_type, t8x8, cbp, qp, cpm;
     uint8_t ipm[16], cbf[16], cbf_c[2][4], cbf_dc[3];
     uint8_t tc[16], tcc[2][4];  /* CAVLC TotalCoeff per luma / chroma AC 4x4 block */
+    int field, vx, vy;          /* --mbaff: the pair's mb_field_decoding_flag; grid position (vy = 2 pair row + bottom) */
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless, mbaff, cur_field;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -186,20 +195,78 @@ typedef struct {
     int cur_qp, prev_qpd_nz;
 } G;
 
-static Mb *nb(G *g, int dx, int dy) {
-    int x = g->mbx + dx, y = g->mby + dy;
-    if (x < 0 || y < 0 || x >= g->mbw) return NULL;
-    if (dy > 0 || (dy == 0 && dx >= 0)) return NULL;
+static Mb *mb_in_slice(G *g, int x, int y) {
+    if (x < 0 || y < 0 || x >= g->mbw || y >= g->mbh) return NULL;
     Mb *m = &g->mb[y * g->mbw + x];
     return m->slice == g->cur_slice ? m : NULL;
 }
+/* 6.4.12: macroblock covering (xN, yN) relative to the current MB (maxW x maxH) and the location
+ * (xW, yW) inside it, NULL if unavailable; --mbaff: 6.4.12.2 / Table 6-4 (the decoder's rules) */
+static Mb *nb_loc(G *g, int xN, int yN, int maxW, int maxH, int *xW, int *yW) {
+    Mb *cur = &g->mb[g->mby * g->mbw + g->mbx];
+    if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return NULL;
+    *xW = (xN + maxW) % maxW;
+    if (xN >= 0 && xN <= maxW - 1 && yN >= 0) { *yW = yN; return cur; }
+    if (!g->mbaff) {
+        *yW = (yN + maxH) % maxH;
+        return mb_in_slice(g, g->mbx + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), g->mby + (yN < 0 ? -1 : 0));
+    }
+    const int px = g->mbx, py = g->mby >> 1, top = !(g->mby & 1), frame = !cur->field;
+    Mb *X = NULL;
+    int yM = yN, bot = 0;
+    if (xN < 0 && yN < 0) {
+        if (frame && !top) { X = mb_in_slice(g, px - 1, 2 * py); if (!X) return NULL; bot = X->field; yM = X->field ? (yN + maxH) >> 1 : yN; }
+        else if (frame || !top) { X = mb_in_slice(g, px - 1, 2 * py - 2); bot = 1; }
+        else { X = mb_in_slice(g, px - 1, 2 * py - 2); if (!X) return NULL; if (!X->field) { bot = 1; yM = 2 * yN; } }
+    } else if (xN < 0) {
+        X = mb_in_slice(g, px - 1, 2 * py);
+        if (!X) return NULL;
+        if (frame) {
+            if (!X->field) bot = top ? 0 : 1;
+            else { bot = yN & 1; yM = top ? yN >> 1 : (yN + maxH) >> 1; }
+        } else if (!X->field) {
+            if (yN < maxH / 2) { bot = 0; yM = (yN << 1) + (top ? 0 : 1); }
+            else { bot = 1; yM = (yN << 1) + (top ? 0 : 1) - maxH; }
+        } else bot = top ? 0 : 1;
+    } else if (xN <= maxW - 1) {
+        if (frame && !top) X = &g->mb[(2 * py) * g->mbw + px];
+        else if (frame || !top) { X = mb_in_slice(g, px, 2 * py - 2); bot = 1; }
+        else { X = mb_in_slice(g, px, 2 * py - 2); if (!X) return NULL; if (!X->field) { bot = 1; yM = 2 * yN; } }
+    } else {
+        if (frame && !top) return NULL;
+        if (frame || !top) { X = mb_in_slice(g, px + 1, 2 * py - 2); bot = 1; }
+        else { X = mb_in_slice(g, px + 1, 2 * py - 2); if (!X) return NULL; if (!X->field) { bot = 1; yM = 2 * yN; } }
+    }
+    if (!X) return NULL;
+    *yW = (yM + maxH) % maxH;
+    return &g->mb[(X->vy + bot) * g->mbw + X->vx];
+}
+static Mb *nb(G *g, int dx, int dy) {
+    int xW, yW;
+    return nb_loc(g, dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
+}
 static Mb *nb_blk(G *g, int bx, int by, int *nblk) {
-    int dx = 0, dy = 0;
-    if (bx < 0) { dx = -1; bx += 4; }
-    if (by < 0) { dy = -1; by += 4; }
-    if (bx > 3) { dx = 1; bx -= 4; }
-    *nblk = k_blk_of[by][bx];
-    return (dx == 0 && dy == 0) ? &g->mb[g->mby * g->mbw + g->mbx] : nb(g, dx, dy);
+    int xW, yW;
+    Mb *m = nb_loc(g, bx * 4, by * 4, 16, 16, &xW, &yW);
+    *nblk = m ? k_blk_of[yW >> 2][xW >> 2] : 0;
+    return m;
+}
+/* picture position of sample (xW, yW) of component c of macroblock N (field MBs interleave rows) */
+static int mb_phys(const G *g, const Mb *N, int c, int xW, int yW) {
+    const int S = c ? 8 : 16, X = N->vx * S + xW;
+    int Y;
+    if (!g->mbaff) Y = N->vy * S + yW;
+    else Y = N->field ? 2 * (N->vy >> 1) * S + 2 * yW + (N->vy & 1) : N->vy * S + yW;
+    return Y * g->st[c] + X;
+}
+/* source / reconstruction of the current MB at grid position (x, y) */
+static int srcv(G *g, int c, int x, int y) {
+    const int S = c ? 8 : 16;
+    return g->src[c][mb_phys(g, &g->mb[g->mby * g->mbw + g->mbx], c, x - g->mbx * S, y - g->mby * S)];
+}
+static void recv_put(G *g, int c, int x, int y, int v) {
+    const int S = c ? 8 : 16;
+    g->rec[c][mb_phys(g, &g->mb[g->mby * g->mbw + g->mbx], c, x - g->mbx * S, y - g->mby * S)] = (uint16_t)v;
 }
 static int avail_luma(G *g, int x, int y, int cur_blk4) {
     if (y < 0 && x < 0) return nb(g, -1, -1) != NULL;
@@ -209,7 +276,13 @@ static int avail_luma(G *g, int x, int y, int cur_blk4) {
     if (x >= 16) return 0;
     return k_blk_of[y >> 2][x >> 2] < cur_blk4;
 }
-static int px(G *g, int c, int x, int y) { return g->rec[c][y * g->st[c] + x]; }
+static int px(G *g, int c, int x, int y) {
+    if (!g->mbaff) return g->rec[c][y * g->st[c] + x];
+    const int S = c ? 8 : 16;
+    int xW, yW;
+    Mb *N = nb_loc(g, x - g->mbx * S, y - g->mby * S, S, S, &xW, &yW);
+    return N ? g->rec[c][mb_phys(g, N, c, xW, yW)] : 0;
+}
 
 /* ------------------------------------------------------------ prediction (same formulas as the decoder) */
 typedef struct { int T[16], L[16], C, at, al, ad, atr; } Nb;
@@ -571,9 +644,9 @@ static int nc_luma(G *g, int blk) {
 static int nc_chroma(G *g, Mb *m, int c, int b4) {
     int bx = b4 & 1, by = b4 >> 1, va = 0, vb = 0, aa = 1, ab = 1;
     if (bx) va = m->tcc[c][b4 - 1];
-    else { Mb *A = nb(g, -1, 0); if (!A) aa = 0; else va = A->mb_type == 25 ? 16 : A->tcc[c][b4 + 1]; }
+    else { int xW, yW; Mb *A = nb_loc(g, -1, by * 4, 8, 8, &xW, &yW); if (!A) aa = 0; else va = A->mb_type == 25 ? 16 : A->tcc[c][(yW >> 2) * 2 + (xW >> 2)]; }
     if (by) vb = m->tcc[c][b4 - 2];
-    else { Mb *B = nb(g, 0, -1); if (!B) ab = 0; else vb = B->mb_type == 25 ? 16 : B->tcc[c][b4 + 2]; }
+    else { int xW, yW; Mb *B = nb_loc(g, bx * 4, -1, 8, 8, &xW, &yW); if (!B) ab = 0; else vb = B->mb_type == 25 ? 16 : B->tcc[c][(yW >> 2) * 2 + (xW >> 2)]; }
     return cavlc_nc(va, aa, vb, ab);
 }
 
@@ -597,11 +670,12 @@ static int enc_block(G *g, int cat, int cbf_inc, int maxnum, const int *co) {
     int coded = last >= 0;
     if (cat != 5) bin(g, 85 + cbf_off[cat] + cbf_inc, coded);
     if (!coded) return 0;
+    const int fld = g->mb[g->mby * g->mbw + g->mbx].field, s0 = fld ? 277 : 105, l0 = fld ? 338 : 166;
     for (int i = 0; i < maxnum - 1; i++) {
         int sc, lc;
-        if (cat == 5) { sc = 402 + k_sig8x8[i]; lc = 417 + k_last8x8[i]; }
-        else if (cat == 3) { int inc = i < 2 ? i : 2; sc = 105 + sig_off[3] + inc; lc = 166 + sig_off[3] + inc; }
-        else { sc = 105 + sig_off[cat] + i; lc = 166 + sig_off[cat] + i; }
+        if (cat == 5) { sc = fld ? 436 + k_sig8x8_fld[i] : 402 + k_sig8x8[i]; lc = (fld ? 451 : 417) + k_last8x8[i]; }
+        else if (cat == 3) { int inc = i < 2 ? i : 2; sc = s0 + sig_off[3] + inc; lc = l0 + sig_off[3] + inc; }
+        else { sc = s0 + sig_off[cat] + i; lc = l0 + sig_off[cat] + i; }
         bin(g, sc, co[i] != 0);
         if (co[i]) { bin(g, lc, i == last); if (i == last) break; }
     }
@@ -638,7 +712,7 @@ static int chroma_qp(int qpi) {
 static long var16(G *g) {
     long s = 0, s2 = 0;
     for (int y = 0; y < 16; y++)
-        for (int x = 0; x < 16; x++) { int v = g->src[0][(g->mby * 16 + y) * g->st[0] + g->mbx * 16 + x]; s += v; s2 += (long)v * v; }
+        for (int x = 0; x < 16; x++) { int v = srcv(g, 0, g->mbx * 16 + x, g->mby * 16 + y); s += v; s2 += (long)v * v; }
     return (s2 - s * s / 256) / 256;
 }
 
@@ -656,13 +730,16 @@ static void dpcm_diff(const int *r, int *c, int n, int dir) {
 
 static void put(G *g, int c, int gx, int gy, int n, const int *pred, const int *r) {
     int maxv = (1 << g->bd) - 1;
-    for (int y = 0; y < n; y++) for (int x = 0; x < n; x++) g->rec[c][(gy + y) * g->st[c] + gx + x] = (uint16_t)clip3(0, maxv, pred[y * n + x] + r[y * n + x]);
+    for (int y = 0; y < n; y++) for (int x = 0; x < n; x++) recv_put(g, c, gx + x, gy + y, clip3(0, maxv, pred[y * n + x] + r[y * n + x]));
 }
 
 static void encode_mb(G *g) {
     Mb *m = &g->mb[g->mby * g->mbw + g->mbx];
     memset(m, 0, sizeof(*m));
     m->slice = g->cur_slice;
+    m->vx = g->mbx;
+    m->vy = g->mby;
+    m->field = g->mbaff ? g->cur_field : 0;
     const int gx = g->mbx * 16, gy = g->mby * 16;
     long v = var16(g);
     int scale = 1 << (2 * (g->bd - 8));
@@ -689,14 +766,14 @@ static void encode_mb(G *g) {
         }
         bw_align_zero(g->ce.bw);
         for (int y = 0; y < 16; y++) for (int x = 0; x < 16; x++) {
-            int s = g->src[0][(gy + y) * g->st[0] + gx + x];
+            int s = srcv(g, 0, gx + x, gy + y);
             bw_put(g->ce.bw, (uint32_t)s, g->bd);
-            g->rec[0][(gy + y) * g->st[0] + gx + x] = (uint16_t)s;
+            recv_put(g, 0, gx + x, gy + y, s);
         }
         for (int c = 1; c < 3; c++) for (int y = 0; y < 8; y++) for (int x = 0; x < 8; x++) {
-            int s = g->src[c][(gy / 2 + y) * g->st[c] + gx / 2 + x];
+            int s = srcv(g, c, gx / 2 + x, gy / 2 + y);
             bw_put(g->ce.bw, (uint32_t)s, g->bd);
-            g->rec[c][(gy / 2 + y) * g->st[c] + gx / 2 + x] = (uint16_t)s;
+            recv_put(g, c, gx / 2 + x, gy / 2 + y, s);
         }
         if (!g->cavlc) { BW *bw = g->ce.bw; ce_start(&g->ce, bw); }
         m->mb_type = 25; m->qp = g->cur_qp; m->cbp = 0x2F;
@@ -716,11 +793,11 @@ static void encode_mb(G *g) {
             if ((md == 0 && !at) || (md == 1 && !al) || (md == 3 && !(at && al && ad))) continue;
             pred16(g, md, pred);
             long c = 0;
-            for (int i = 0; i < 256; i++) c += abs(g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i]);
+            for (int i = 0; i < 256; i++) c += abs(srcv(g, 0, gx + (i & 15), gy + (i >> 4)) - pred[i]);
             if (best < 0 || c < best) { best = c; mode16 = md; }
         }
         pred16(g, mode16, pred);
-        for (int i = 0; i < 256; i++) src[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
+        for (int i = 0; i < 256; i++) src[i] = srcv(g, 0, gx + (i & 15), gy + (i >> 4)) - pred[i];
         if (g->lossless) {  /* transform bypass: the levels are the residual (DPCM for modes 0 / 1) */
             if (mode16 <= 1) dpcm_diff(src, lv16, 16, mode16);
             else memcpy(lv16, src, sizeof(lv16));
@@ -742,7 +819,7 @@ static void encode_mb(G *g) {
     for (int c = 0; c < 2; c++) {
         predc(g, 1 + c, cpm, predc_[c]);
         int x[64];
-        for (int i = 0; i < 64; i++) x[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
+        for (int i = 0; i < 64; i++) x[i] = srcv(g, 1 + c, gx / 2 + (i & 7), gy / 2 + (i >> 3)) - predc_[c][i];
         if (g->lossless) {  /* intra_chroma_pred_mode 1 horizontal, 2 vertical */
             if (cpm == 1 || cpm == 2) dpcm_diff(x, lvc[c], 8, cpm == 2 ? 0 : 1);
             else memcpy(lvc[c], x, sizeof(x));
@@ -808,7 +885,7 @@ static void encode_mb(G *g) {
                 if (md > 2 && rndn(3) == 0) continue;
                 predict_nxn(g, n, md, &o, p);
                 long c = 0;
-                for (int k = 0; k < n * n; k++) c += abs(g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k]);
+                for (int k = 0; k < n * n; k++) c += abs(srcv(g, 0, gx + bx + k % n, gy + by + k / n) - p[k]);
                 if (best < 0 || c < best) { best = c; bm = md; }
             }
             /* signal */
@@ -833,7 +910,7 @@ static void encode_mb(G *g) {
             /* residual + recon now (later blocks predict from it) */
             predict_nxn(g, n, bm, &o, p);
             int x[64], rr[64];
-            for (int k = 0; k < n * n; k++) x[k] = g->src[0][(gy + by + k / n) * g->st[0] + gx + bx + k % n] - p[k];
+            for (int k = 0; k < n * n; k++) x[k] = srcv(g, 0, gx + bx + k % n, gy + by + k / n) - p[k];
             int *lv = t8 ? lv8[i] : lv4[blk];
             if (g->lossless) {  /* transform bypass: exact reconstruction */
                 if (bm <= 1) dpcm_diff(x, lv, n, bm);
@@ -879,9 +956,13 @@ static void encode_mb(G *g) {
         int cbp = m->cbp;
         for (int b8 = 0; b8 < 4; b8++) {
             int bx = b8 & 1, by = b8 >> 1, ca, cb;
-            if (bx == 0) ca = A ? (A->mb_type == 25 ? 0 : !((A->cbp >> (b8 + 1)) & 1)) : 0;
+            int xW, yW;
+            Mb *N8;
+            if (bx == 0) { N8 = nb_loc(g, -1, by * 8, 16, 16, &xW, &yW);
+                           ca = N8 ? (N8->mb_type == 25 ? 0 : !((N8->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0; }
             else ca = !((cbp >> (b8 - 1)) & 1);
-            if (by == 0) cb = B ? (B->mb_type == 25 ? 0 : !((B->cbp >> (b8 + 2)) & 1)) : 0;
+            if (by == 0) { N8 = nb_loc(g, bx * 8, -1, 16, 16, &xW, &yW);
+                           cb = N8 ? (N8->mb_type == 25 ? 0 : !((N8->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0; }
             else cb = !((cbp >> (b8 - 2)) & 1);
             bin(g, 73 + ca + 2 * cb, (cbp >> b8) & 1);
         }
@@ -911,10 +992,11 @@ static void encode_mb(G *g) {
     }
     g->prev_qpd_nz = qpd != 0;
     m->qp = g->cur_qp;
-    /* residual syntax */
+    /* residual syntax (field MBs: field scans) */
     int co[64];
+    const uint8_t *z4 = m->field ? k_fld4 : k_zz4, *z8 = m->field ? k_fld8 : k_zz8;
     if (is16) {
-        for (int k = 0; k < 16; k++) { int rr = k_zz4[k]; co[k] = lv16[(rr >> 2) * 4 * 16 + (rr & 3) * 4]; }
+        for (int k = 0; k < 16; k++) { int rr = z4[k]; co[k] = lv16[(rr >> 2) * 4 * 16 + (rr & 3) * 4]; }
         if (g->cavlc) enc_block_cavlc(g, nc_luma(g, 0), 16, co);
         else m->cbf_dc[0] = (uint8_t)enc_block(g, 0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, co);
     }
@@ -922,13 +1004,13 @@ static void encode_mb(G *g) {
         if (!((m->cbp >> b8) & 1)) continue;
         if (t8 && g->cavlc) {
             for (int i4 = 0; i4 < 4; i4++) {
-                for (int k = 0; k < 16; k++) co[k] = lv8[b8][k_zz8[4 * k + i4]];
+                for (int k = 0; k < 16; k++) co[k] = lv8[b8][z8[4 * k + i4]];
                 m->tc[b8 * 4 + i4] = (uint8_t)enc_block_cavlc(g, nc_luma(g, b8 * 4 + i4), 16, co);
             }
             continue;
         }
         if (t8) {
-            for (int k = 0; k < 64; k++) co[k] = lv8[b8][k_zz8[k]];
+            for (int k = 0; k < 64; k++) co[k] = lv8[b8][z8[k]];
             enc_block(g, 5, 0, 64, co);
             for (int k = 0; k < 4; k++) m->cbf[b8 * 4 + k] = 1;
             continue;
@@ -940,11 +1022,11 @@ static void encode_mb(G *g) {
             Mb *NB = nb_blk(g, bx, by - 1, &nb1);
             int cb = cbf_cond(is16 ? 1 : 2, NB, nb1, 0);
             if (is16) {
-                for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lv16[(by * 4 + (rr >> 2)) * 16 + bx * 4 + (rr & 3)]; }
+                for (int k = 0; k < 15; k++) { int rr = z4[k + 1]; co[k] = lv16[(by * 4 + (rr >> 2)) * 16 + bx * 4 + (rr & 3)]; }
                 if (g->cavlc) m->tc[blk] = (uint8_t)enc_block_cavlc(g, nc_luma(g, blk), 15, co);
                 else m->cbf[blk] = (uint8_t)enc_block(g, 1, ca + 2 * cb, 15, co);
             } else {
-                for (int k = 0; k < 16; k++) co[k] = lv4[blk][k_zz4[k]];
+                for (int k = 0; k < 16; k++) co[k] = lv4[blk][z4[k]];
                 if (g->cavlc) m->tc[blk] = (uint8_t)enc_block_cavlc(g, nc_luma(g, blk), 16, co);
                 else m->cbf[blk] = (uint8_t)enc_block(g, 2, ca + 2 * cb, 16, co);
             }
@@ -961,9 +1043,12 @@ static void encode_mb(G *g) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 int bx = b4 & 1, by = b4 >> 1;
-                int ca = bx ? m->cbf_c[c][b4 - 1] : cbf_cond(4, A, b4 + 1, c);
-                int cb = by ? m->cbf_c[c][b4 - 2] : cbf_cond(4, B, b4 + 2, c);
-                for (int k = 0; k < 15; k++) { int rr = k_zz4[k + 1]; co[k] = lvc[c][(by * 4 + (rr >> 2)) * 8 + bx * 4 + (rr & 3)]; }
+                int xW, yW, ca, cb;
+                if (bx) ca = m->cbf_c[c][b4 - 1];
+                else { Mb *N = nb_loc(g, -1, by * 4, 8, 8, &xW, &yW); ca = cbf_cond(4, N, N ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
+                if (by) cb = m->cbf_c[c][b4 - 2];
+                else { Mb *N = nb_loc(g, bx * 4, -1, 8, 8, &xW, &yW); cb = cbf_cond(4, N, N ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
+                for (int k = 0; k < 15; k++) { int rr = z4[k + 1]; co[k] = lvc[c][(by * 4 + (rr >> 2)) * 8 + bx * 4 + (rr & 3)]; }
                 if (g->cavlc) m->tcc[c][b4] = (uint8_t)enc_block_cavlc(g, nc_chroma(g, m, c, b4), 15, co);
                 else m->cbf_c[c][b4] = (uint8_t)enc_block(g, 4, ca + 2 * cb, 15, co);
             }
@@ -971,13 +1056,13 @@ static void encode_mb(G *g) {
     /* reconstruction of I16x16 luma and chroma */
     if (is16) {
         pred16(g, mode16, pred);
-        if (g->lossless) for (int i = 0; i < 256; i++) r[i] = g->src[0][(gy + (i >> 4)) * g->st[0] + gx + (i & 15)] - pred[i];
+        if (g->lossless) for (int i = 0; i < 256; i++) r[i] = srcv(g, 0, gx + (i & 15), gy + (i >> 4)) - pred[i];
         else res_dc(lv16, 16, qpl, r, g_w4[0]);
         put(g, 0, gx, gy, 16, pred, r);
     }
     for (int c = 0; c < 2; c++) {
         int rr[64];
-        if (g->lossless) for (int i = 0; i < 64; i++) rr[i] = g->src[1 + c][(gy / 2 + (i >> 3)) * g->st[1 + c] + gx / 2 + (i & 7)] - predc_[c][i];
+        if (g->lossless) for (int i = 0; i < 64; i++) rr[i] = srcv(g, 1 + c, gx / 2 + (i & 7), gy / 2 + (i >> 3)) - predc_[c][i];
         else res_dc(lvc[c], 8, qpc[c], rr, g_w4[1 + c]);
         put(g, 1 + c, gx / 2, gy / 2, 8, predc_[c], rr);
     }
@@ -1074,7 +1159,7 @@ static void write_sps(FILE *f, G *g, int profile) {
      * crop in units of 4 rows (7.4.2.1.1) */
     bw_ue(&b, (uint32_t)(g->ilsps ? g->mbh / 2 - 1 : g->mbh - 1));
     bw_put(&b, (uint32_t)!g->ilsps, 1); /* frame_mbs_only */
-    if (g->ilsps) bw_put(&b, 0, 1);     /* mb_adaptive_frame_field_flag */
+    if (g->ilsps) bw_put(&b, (uint32_t)g->mbaff, 1); /* mb_adaptive_frame_field_flag (--mbaff: MBAFF frame) */
     bw_put(&b, 1, 1); /* direct_8x8_inference */
     int crop = g->outW != g->W || g->outH != g->H;
     if (g->rawcrop[0] >= 0) { /* --crop l,r,t,b: raw frame_crop offsets (malformed-SPS vectors) */
@@ -1167,6 +1252,11 @@ int main(int argc, char **argv) {
     g->vuireorder = opt_int(argc, argv, "--vuireorder", -1);
     g->vuicpb = opt_int(argc, argv, "--vuicpb", -1);
     g->ilsps = opt_int(argc, argv, "--ilsps", 0);
+    /* --mbaff 1: an MBAFF frame (frame_mbs_only_flag 0, mb_adaptive_frame_field_flag 1): macroblock
+     * pairs, each coded as two frame or two field macroblocks (random per pair, --fieldpct % field) */
+    g->mbaff = opt_int(argc, argv, "--mbaff", 0);
+    if (g->mbaff) g->ilsps = 1;
+    int fieldpct = opt_int(argc, argv, "--fieldpct", 50);
     /* --lossless 1: High 4:4:4 Predictive (profile_idc 244) with qpprime_y_zero_transform_bypass_flag,
      * every macroblock at QP'Y 0 (TransformBypassModeFlag), residual DPCM for H / V predictions */
     g->lossless = opt_int(argc, argv, "--lossless", 0);
@@ -1201,10 +1291,11 @@ int main(int argc, char **argv) {
     write_pps(fo, g, profile >= 100, 0);
     if (g->delay) write_pps(fo, g, 0, 1);
     int rows = g->slice_rows > 0 ? g->slice_rows : g->mbh;
+    if (g->mbaff) rows = (rows + 1) & ~1; /* slices start at pair rows */
     int nslice = 0;
     for (int r0 = 0; r0 < g->mbh; r0 += rows, nslice++) {
         BW b; bw_init(&b);
-        bw_ue(&b, (uint32_t)(r0 == 0 && g->firstmb >= 0 ? g->firstmb : r0 * g->mbw)); /* first_mb (--firstmb: malformed) */
+        bw_ue(&b, (uint32_t)(r0 == 0 && g->firstmb >= 0 ? g->firstmb : (g->mbaff ? r0 / 2 : r0) * g->mbw)); /* first_mb (MBAFF: pair index; --firstmb: malformed) */
         bw_ue(&b, 7);                         /* I (all slices I) */
         bw_ue(&b, 0);                         /* pps */
         bw_put(&b, 0, 4);                     /* frame_num */
@@ -1229,6 +1320,22 @@ int main(int argc, char **argv) {
         g->cur_qp = sqp;
         g->prev_qpd_nz = 0;
         int r1 = r0 + rows < g->mbh ? r0 + rows : g->mbh;
+        if (g->mbaff) { /* pairs in raster order, top MB then bottom MB (7.3.4) */
+            for (int pr = r0 / 2; pr < r1 / 2; pr++)
+                for (int mx = 0; mx < g->mbw; mx++)
+                    for (int bt = 0; bt < 2; bt++) {
+                        g->mbx = mx; g->mby = 2 * pr + bt;
+                        g->mb[g->mby * g->mbw + mx].slice = nslice;
+                        if (!bt) { /* mb_field_decoding_flag: ctxIdx 70 + left / upper pair are field pairs */
+                            g->cur_field = rndn(100) < fieldpct;
+                            Mb *PA = mb_in_slice(g, mx - 1, 2 * pr), *PB = mb_in_slice(g, mx, 2 * pr - 2);
+                            if (g->cavlc) bw_put(g->ce.bw, (uint32_t)g->cur_field, 1);
+                            else bin(g, 70 + (PA && PA->field) + (PB && PB->field), g->cur_field);
+                        }
+                        encode_mb(g);
+                        if (!g->cavlc) ce_term(&g->ce, pr == r1 / 2 - 1 && mx == g->mbw - 1 && bt == 1);
+                    }
+        } else
         for (int my = r0; my < r1; my++)
             for (int mx = 0; mx < g->mbw; mx++) {
                 g->mbx = mx; g->mby = my;

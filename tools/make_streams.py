@@ -256,6 +256,15 @@ PARITY264 = [
     ("a28_256x144_12bit_high444", 256, 144, 12, 22, 60, 4, ["--t8x8", "1", "--slices", "3"]),
     ("a29_192x112_14bit_cavlc_pcm", 192, 112, 14, 14, 61, 6, ["--cavlc", "1", "--pcm", "1"]),
     ("a30_160x96_lossless_10bit_slices", 160, 96, 10, 0, 62, 4, ["--lossless", "1", "--slices", "2"]),
+    # MBAFF frames (frame_mbs_only_flag 0, mb_adaptive_frame_field_flag 1): macroblock pairs coded as
+    # two frame or two field macroblocks (6.4.12.2 neighbours, field scans and contexts, 8.7 MBAFF
+    # deblocking); a36 is a 1080i-sized frame
+    ("a31_336x192_mbaff_cabac_8x8", 336, 192, 8, 24, 63, 6, ["--mbaff", "1", "--t8x8", "1", "--slices", "4"]),
+    ("a32_320x160_mbaff_cavlc_4x4_pcm", 320, 160, 8, 22, 64, 5, ["--mbaff", "1", "--cavlc", "1", "--t8x8", "0", "--pcm", "1"]),
+    ("a33_352x224_mbaff_10bit_dbidc2", 352, 224, 10, 27, 65, 4, ["--mbaff", "1", "--slices", "4", "--dbidc", "2"]),
+    ("a34_256x128_mbaff_all_field", 256, 128, 8, 20, 70, 10, ["--mbaff", "1", "--fieldpct", "100", "--alpha", "3", "--beta", "2"]),
+    ("a35_240x96_mbaff_cavlc_8x8_offsets", 240, 96, 8, 18, 71, 12, ["--mbaff", "1", "--cavlc", "1", "--cqp", "3", "--cqp2", "-2"]),
+    ("a36_1920x1080_mbaff_1080i", 1920, 1080, 8, 26, 68, 3, ["--mbaff", "1", "--t8x8", "1"]),
 ]
 
 
