@@ -413,6 +413,14 @@ DEVI int16_t* h264_res_at(int16_t* res, int mbw, int c, int x, int y) {
     if (c == 0) return res + ((y >> 4) * mbw + (x >> 4)) * 384 + ((y & 15) << 4) + (x & 15);
     return res + ((y >> 3) * mbw + (x >> 3)) * 384 + 256 + (c - 1) * 64 + ((y & 7) << 3) + (x & 7);
 }
+// H.264 MBAFF frames keep TU records and MB records in the macroblock grid (grid row = 2 * pair row
+// + bottom); a field macroblock's row r is picture row 2 * r + bottom of its pair (h2j_ctb.mbflags
+// bit 3).  Picture row of grid row y (component c: 16 / 8 rows per MB).
+DEVI int h264_mbaff_row(const h2j_ctb* C, int mbw, int c, int x, int y) {
+    const int sh = c ? 3 : 4, vy = y >> sh, r = y & ((1 << sh) - 1);
+    const bool fld = (C[vy * mbw + (x >> sh)].mbflags & 8) != 0;
+    return fld ? (((vy >> 1) << (sh + 1)) + 2 * r + (vy & 1)) : y;
+}
 DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint32_t co0, const uint8_t* sl,
                         int16_t* R, int rst, K0LdsHevc& s) {
     const int lane = threadIdx.x;
@@ -1111,6 +1119,8 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                         }
                         mask |= static_cast<uint64_t>(a) << q;
                     }
+                } else if (ufl(fr.mbaff)) {  // MBAFF: 6.4.12.2 availability computed by the host parser
+                    mask = static_cast<uint64_t>(static_cast<uint8_t>(own.qpy) & 15u);
                 } else {
                     const bool nxn = oc == 0 && own.log2n <= 3;
                     for (int q = 0; q < 4; q++) {
@@ -1170,19 +1180,22 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
         const int stc = c ? st1 : st0;
         const int offc = c == 0 ? 0 : (c == 1 ? off1 : off2);
         if (flags & H2J_TU_PCM) {
+            const bool mbaff = !hevc && ufl(fr.mbaff);  // MBAFF: field MBs' rows interleave (h264_mbaff_row)
             if (f.bd == 8) {
                 uint8_t* P = pic + offc;
                 for (int e = lane; e < tu.ncoef; e += 64) {
                     const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
                     const int pos = static_cast<int>(en >> 16);
-                    P[(y0 + (pos >> log2n)) * stc + x0 + (pos & (n - 1))] = static_cast<uint8_t>(en & 0xFF);
+                    const int yy = y0 + (pos >> log2n), row = mbaff ? h264_mbaff_row(C, f.ctb_w, c, x0, yy) : yy;
+                    P[row * stc + x0 + (pos & (n - 1))] = static_cast<uint8_t>(en & 0xFF);
                 }
             } else {
                 uint16_t* P = reinterpret_cast<uint16_t*>(pic) + offc;
                 for (int e = lane; e < tu.ncoef; e += 64) {
                     const uint32_t en = e < 64 ? co0 : CO[tu.coef + e];
                     const int pos = static_cast<int>(en >> 16);
-                    P[(y0 + (pos >> log2n)) * stc + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
+                    const int yy = y0 + (pos >> log2n), row = mbaff ? h264_mbaff_row(C, f.ctb_w, c, x0, yy) : yy;
+                    P[row * stc + x0 + (pos & (n - 1))] = static_cast<uint16_t>(en & 0xFFFF);
                 }
             }
             continue;
@@ -1711,6 +1724,117 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cur ^= 1;
+        }
+    }
+}
+
+// H.264 K1 for MBAFF frames (h2j_frame.mbaff): macroblock pairs, wave w walking pair rows w, w + 16,
+// ... (a pair needs the pair row above finished through the pair to its right, as h264_rows needs
+// the MB row above).  Per MB (top, then bottom of the pair) the window is filled from the picture
+// itself, in the MB's own field / frame view: row r of a field MB is picture row 2 r + bottom of
+// the pair, its row -1 the picture row two above its first row; a frame MB's rows are consecutive.
+// With the 6.4.12.2 neighbour rules those are exactly the samples intra prediction reads (the
+// availability masks come from the host parser).  The MB is reconstructed in the window by the
+// progressive TB code and stored to its picture rows.  Samples pass between MBs / waves through
+// global memory: release / acquire fences around the progress words and between MBs.
+template <typename Pel>
+DEVI void h264_rows_mbaff(const h2j_frame& f, const h2j_tu* T, const h2j_ctb* C, uint8_t* arena, H4WaveLds& s,
+                          uint32_t* prog) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
+    const uint32_t* masks32 = reinterpret_cast<const uint32_t*>(masks);
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
+    constexpr int kSlots = 2 * kAvcWaves;
+    const int mbw = ufl(f.ctb_w), npr = ufl(f.ctb_h) >> 1;
+    const int W = ufl(f.width), Wc = W >> 1;
+    const int bdy = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
+    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
+    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
+    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
+    const int16_t* RY = reinterpret_cast<const int16_t*>(arena + ufl64(f.res));
+    const uint32_t ntot = ufl(f.ntu);
+    H4In& in = s.in[0];
+    for (int pr = w; pr < npr; pr += kAvcWaves) {
+        uint32_t* above = prog + (pr + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + pr % kSlots;
+        uint32_t seen = 0;
+        const int Y0 = pr * 32, Yc0 = pr * 16;
+        for (int x = 0; x < mbw; x++) {
+            if (pr > 0) {
+                const uint32_t need = (static_cast<uint32_t>(pr) << 16) | static_cast<uint32_t>(min(x + 2, mbw));
+                if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrK1Row264);
+            }
+            const bool fld = (C[(2 * pr) * mbw + x].mbflags & 8) != 0;
+            for (int bot = 0; bot < 2; bot++) {
+                const int vy = 2 * pr + bot, cb = vy * mbw + x;
+                const uint4 rg = reinterpret_cast<const uint4*>(rng)[cb];
+                const uint32_t a = rg.x, ntu = min(rg.z - rg.x, static_cast<uint32_t>(kH4MaxTus));
+                // records, masks and the MB's residual tile (h264_res_at) into the window's inputs
+                lds_reads_done();
+                if (lane < kH4MaxTus) {
+                    const uint32_t ri = min(a + static_cast<uint32_t>(lane), max(ntot, 1u) - 1);
+                    lds_dma16(T + ri, lds_addr(in.tus));
+                    lds_dma4(masks32 + 2 * ri, lds_addr(in.mlo));
+                    lds_dma4(masks32 + 2 * ri + 1, lds_addr(in.mhi));
+                }
+                if (lane < 48) lds_dma16(RY + static_cast<size_t>(cb) * 384 + lane * 8, lds_addr(in.ry));
+                // picture rows of this MB's rows -1 .. 15 (luma) / -1 .. 7 (chroma)
+                auto yrow = [&](int r) { return fld ? Y0 + 2 * r + bot : Y0 + 16 * bot + r; };
+                auto crow = [&](int r) { return fld ? Yc0 + 2 * r + bot : Yc0 + 8 * bot + r; };
+                const int ya = fld ? Y0 + bot - 2 : yrow(-1), ca = fld ? Yc0 + bot - 2 : crow(-1);
+                if (lane < 25) {  // luma row -1, x = -1 .. 23
+                    const int xx = x * 16 - 1 + lane;
+                    s.wy[0][lane] = (ya >= 0 && xx >= 0 && xx < W) ? static_cast<uint16_t>(PY[ya * sty + xx]) : 0;
+                } else if (lane < 43) {  // chroma row -1, x = -1 .. 7
+                    const int k = lane - 25, c = k / 9, i = k % 9, xx = x * 8 - 1 + i;
+                    s.wc[c][0][i] = (ca >= 0 && xx >= 0 && xx < Wc) ? static_cast<uint16_t>(PC[c][ca * stc + xx]) : 0;
+                }
+                if (lane < 16) {  // left column
+                    s.wy[lane + 1][0] = x > 0 ? static_cast<uint16_t>(PY[yrow(lane) * sty + x * 16 - 1]) : 0;
+                } else if (lane < 32) {
+                    const int c = (lane - 16) >> 3, r = (lane - 16) & 7;
+                    s.wc[c][r + 1][0] = x > 0 ? static_cast<uint16_t>(PC[c][crow(r) * stc + x * 8 - 1]) : 0;
+                }
+                lds_dma_wait();
+                wave_sync();
+                const bool pcm = ntu > 0 && (in.tus[0].flags & H2J_TU_PCM);
+                if (pcm) {  // samples written by K0 (at this MB's picture rows)
+                    for (int i = lane; i < 256; i += 64) s.wy[(i >> 4) + 1][(i & 15) + 1] = PY[yrow(i >> 4) * sty + x * 16 + (i & 15)];
+                    for (int i = lane; i < 128; i += 64) {
+                        const int c = i >> 6, k = i & 63;
+                        s.wc[c][(k >> 3) + 1][(k & 7) + 1] = PC[c][crow(k >> 3) * stc + x * 8 + (k & 7)];
+                    }
+                    wave_sync();
+                } else {
+                    for (uint32_t t = 0; t < ntu; t++) {
+                        const h2j_tu tu = in.tus[t];
+                        if (tu.c == 1 && tu.log2n == 3 && t + 1 < ntu && in.tus[t + 1].c == 2 && in.tus[t + 1].log2n == 3) {
+                            h264_predict_chroma_pair(tu, in.tus[t + 1], in.mask(t), bdc, s, in, lane);
+                            t++;
+                            continue;
+                        }
+                        h264_predict_tu(tu, in.mask(t), x, vy, tu.c ? bdc : bdy, s, in, lane);
+                    }
+                }
+                // the MB's rows to the picture: luma lane = (row, 4 samples), chroma lane = (comp, row, 2 x 2 samples)
+                {
+                    const int r = lane >> 2, q = (lane & 3) * 4;
+                    Pel* d = PY + yrow(r) * sty + x * 16 + q;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) d[k] = static_cast<Pel>(s.wy[r + 1][q + 1 + k]);
+                    const int c = lane >> 5, rr = (lane >> 2) & 7, qq = (lane & 3) * 2;
+                    Pel* e = PC[c] + crow(rr) * stc + x * 8 + qq;
+                    e[0] = static_cast<Pel>(s.wc[c][rr + 1][qq + 1]);
+                    e[1] = static_cast<Pel>(s.wc[c][rr + 1][qq + 2]);
+                }
+                // the next MB of this wave reads these samples back from the picture
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                wave_sync();
+            }
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(pr) + 1) << 16) | static_cast<uint32_t>(x + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 }
@@ -2588,7 +2712,7 @@ __global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame*
 // grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
 // picture in order, so a band only ever waits on an earlier workgroup)
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
-                                                                  uint8_t* arena, const uint32_t* map) {
+                                                                  const h2j_ctb* ctbs, uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t h4lds[];
     H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(h4lds);
     uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves);
@@ -2602,8 +2726,27 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_fr
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
     const h2j_tu* T = tus + ufl(f.tu);
+    if (ufl(f.mbaff)) return;  // h2j_k1_recon_h264_mbaff
     if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
     else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
+}
+
+// MBAFF frames (h2j_frame.mbaff) in a kernel of their own, so the progressive kernel keeps its
+// register allocation; same (picture, band) map, other pictures return at once.
+__global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264_mbaff(const h2j_frame* frames, const h2j_tu* tus,
+                                                                        const h2j_ctb* ctbs, uint8_t* arena,
+                                                                        const uint32_t* map) {
+    extern __shared__ __align__(16) uint8_t h4lds[];
+    H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(h4lds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves);
+    const h2j_frame& f = frames[map[blockIdx.x] >> 8];
+    if (f.codec != H2J_CODEC_H264 || !ufl(f.mbaff)) return;
+    if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
+    __syncthreads();
+    H4WaveLds& s = wl[threadIdx.x >> 6];
+    const h2j_tu* T = tus + ufl(f.tu);
+    if (f.bit_depth == 8) h264_rows_mbaff<uint8_t>(f, T, ctbs + ufl(f.ctb), arena, s, prog);
+    else h264_rows_mbaff<uint16_t>(f, T, ctbs + ufl(f.ctb), arena, s, prog);
 }
 
 // K1 HEVC, picture pool: one 16-wave workgroup reconstructs P pictures.  Its waves take CTB-row
@@ -2685,7 +2828,7 @@ __global__ void __launch_bounds__(64 * kPoolWaves) h2j_k1_recon_hevc_pool(const 
 // the rows in flight.  `map`: the host's list, longest chains first; bit 31 marks HEVC entries,
 // bit 30 a 16-wave group (bit 0: 0 luma, 1 chroma).
 __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_frame* frames, const h2j_tu* tus,
-                                                                 uint8_t* arena, const uint32_t* map) {
+                                                                 const h2j_ctb* ctbs, uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t anylds[];
     const uint32_t me = map[blockIdx.x];
     const h2j_frame& f = frames[(me >> 8) & 0x3FFFFFu];
@@ -2716,6 +2859,7 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
             if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
             __syncthreads();
         H4WaveLds& s = wl[threadIdx.x >> 6];
+        if (ufl(f.mbaff)) return;  // h2j_k1_recon_h264_mbaff
         if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
         else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
     }
@@ -3456,6 +3600,177 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
 }
 
 // line_w: the widest picture whose line buffer the launch's LDS holds (wider: global memory)
+// ---- H.264 K2 for MBAFF frames (8.7 with MbaffFrameFlag 1; FFmpeg h264_loopfilter.c behind
+// /root/reference/src/Decoder.cpp:324), on the picture in global memory.  Wave w walks pair rows
+// w, w + kDbPairWaves, ...; a pair starts once the pair row above has finished through the pair to
+// its right (its top edges read and change rows that pair's left edge changes).  Per MB (top, then
+// bottom) in 8.7 order: luma vertical edges, luma horizontal edges, chroma vertical, chroma
+// horizontal, one lane per line.  Geometry as in the oracle: vertical edges run along picture rows
+// (the p side of a left MB edge is the left pair's MB holding that picture row); horizontal edges
+// step through the MB's own rows (field MB: every other picture row) and its top MB edge reaches
+// up the same way; a frame top MB under a field pair filters its top edge twice, once per field
+// (bS 3).  All-intra bS: 4 on vertical MB edges and on horizontal MB edges between two frame MBs,
+// else 3.
+template <typename Pel>
+DEVI void db264_mbaff_line(Pel* q, int step, int bs, int alpha, int beta, int tc0, bool chroma, int maxv) {
+    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
+    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+    if (chroma) {
+        if (bs < 4) {
+            const int tc = tc0 + 1, dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+            q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
+            q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
+        } else {
+            q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
+            q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
+        }
+        return;
+    }
+    const int p2 = q[-3 * step], q2 = q[2 * step];
+    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+    if (bs < 4) {
+        const int tc = tc0 + (ap < beta) + (aq < beta), dl = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+        q[-step] = static_cast<Pel>(clip3(0, maxv, p0 + dl));
+        q[0] = static_cast<Pel>(clip3(0, maxv, q0 - dl));
+        if (ap < beta) q[-2 * step] = static_cast<Pel>(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1));
+        if (aq < beta) q[step] = static_cast<Pel>(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1));
+        return;
+    }
+    const int p3 = q[-4 * step], q3 = q[3 * step];
+    const bool strong = abs(p0 - q0) < ((alpha >> 2) + 2);
+    if (ap < beta && strong) {
+        q[-step] = static_cast<Pel>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+        q[-2 * step] = static_cast<Pel>((p2 + p1 + p0 + q0 + 2) >> 2);
+        q[-3 * step] = static_cast<Pel>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+    } else {
+        q[-step] = static_cast<Pel>((2 * p1 + p0 + q1 + 2) >> 2);
+    }
+    if (aq < beta && strong) {
+        q[0] = static_cast<Pel>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+        q[step] = static_cast<Pel>((p0 + q0 + q1 + q2 + 2) >> 2);
+        q[2 * step] = static_cast<Pel>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+    } else {
+        q[0] = static_cast<Pel>((2 * q1 + q0 + p1 + 2) >> 2);
+    }
+}
+
+template <typename Pel>
+DEVI void h264_db_mbaff(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uint8_t* arena, uint32_t* prog) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int kSlots = 2 * kDbPairWaves;
+    const int mbw = ufl(f.ctb_w), npr = ufl(f.ctb_h) >> 1;
+    const int bdy = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c), qpbdc = 6 * (bdc - 8);
+    const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
+    Pel* PL[3] = {reinterpret_cast<Pel*>(arena + ufl64(f.pic)), nullptr, nullptr};
+    PL[1] = PL[0] + ufl(f.pic_off[1]);
+    PL[2] = PL[0] + ufl(f.pic_off[2]);
+    auto qpf = [&](const h2j_ctb& m) { return (m.mbflags & 1) ? 0 : static_cast<int>(m.qp); };  // I_PCM: 0
+    auto cqp = [&](int qpy, int off) {
+        const int qi = clip3(-qpbdc, 51, qpy + off);
+        return qi < 30 ? qi : kChromaQp264[qi - 30];
+    };
+    for (int pr = w; pr < npr; pr += kDbPairWaves) {
+        uint32_t* above = prog + (pr + kSlots - 1) % kSlots;
+        uint32_t* mine = prog + pr % kSlots;
+        uint32_t seen = 0;
+        for (int x = 0; x < mbw; x++) {
+            if (pr > 0) {
+                const uint32_t need = (static_cast<uint32_t>(pr) << 16) | static_cast<uint32_t>(min(x + 2, mbw));
+                if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrDbRow264);
+            }
+            for (int bot = 0; bot < 2; bot++) {
+                const h2j_ctb m = C[(2 * pr + bot) * mbw + x];
+                if (!(m.mbflags & 4)) continue;  // not decoded
+                const h2j_slice sl = SL[m.slice];
+                if (sl.deblock_disabled == 1) continue;
+                const bool fld = (m.mbflags & 8) != 0, t8 = (m.mbflags & 2) != 0;
+                bool left = x > 0;
+                if (left) {
+                    const h2j_ctb& L = C[(2 * pr) * mbw + x - 1];
+                    left = (L.mbflags & 4) && !(sl.deblock_disabled == 2 && SL[L.slice].slice_addr_rs != sl.slice_addr_rs);
+                }
+                bool top;
+                if (!fld && bot) top = true;  // the pair's internal edge
+                else if (pr == 0) top = false;
+                else {
+                    const h2j_ctb& B = C[(2 * pr - 2) * mbw + x];
+                    top = (B.mbflags & 4) && !(sl.deblock_disabled == 2 && SL[B.slice].slice_addr_rs != sl.slice_addr_rs);
+                }
+                const bool above_fld = pr > 0 && (C[(2 * pr - 2) * mbw + x].mbflags & 8);
+                for (int c = 0; c < 3; c += (c == 0 ? 1 : 2)) {  // luma, then both chroma components per pass
+                    const int S = c ? 8 : 16, Y0 = pr * 2 * S;
+                    const int bd = c ? bdc : bdy, maxv = (1 << bd) - 1;
+                    // this lane's component and line
+                    const int cc = c ? 1 + (lane >> 3) : 0, k = c ? (lane & 7) : lane;
+                    const bool act = lane < 16;
+                    const int st = cc ? stc : sty;
+                    Pel* P0 = PL[cc];
+                    const int off = cc == 1 ? sl.cqp_offset[0] : sl.cqp_offset[1];
+                    auto row = [&](int r) { return fld ? Y0 + 2 * r + bot : Y0 + S * bot + r; };
+                    auto edge = [&](Pel* q, int step, int bs, const h2j_ctb& Pm) __attribute__((always_inline)) {
+                        const int qa = cc ? (cqp(qpf(Pm), off) + cqp(qpf(m), off) + 1) >> 1 : (qpf(Pm) + qpf(m) + 1) >> 1;
+                        const int ia = clip3(0, 51, qa + sl.tc_offset), ib = clip3(0, 51, qa + sl.beta_offset);
+                        const int alpha = kAlpha264[ia] << (bd - 8), beta = kBeta264[ib] << (bd - 8);
+                        const int tc0 = bs < 4 ? kTc0_264[ia][bs - 1] << (bd - 8) : 0;
+                        db264_mbaff_line<Pel>(q, step, bs, alpha, beta, tc0, cc != 0, maxv);
+                    };
+                    auto sync = [&]() __attribute__((always_inline)) {  // this pass's stores before the next pass's loads
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        wave_sync();
+                    };
+                    for (int e = 0; e < S; e += 4) {  // vertical edges
+                        if (!c && (e == 4 || e == 12) && t8) continue;
+                        if (e == 0 && !left) continue;
+                        if (act) {
+                            const int Y = row(k);
+                            const h2j_ctb* Pm = &m;
+                            if (e == 0) {
+                                const bool lf = (C[(2 * pr) * mbw + x - 1].mbflags & 8) != 0;
+                                const int r = Y - Y0, lb = lf ? (r & 1) : (r >= S ? 1 : 0);
+                                Pm = &C[(2 * pr + lb) * mbw + x - 1];
+                            }
+                            edge(P0 + Y * st + x * S + e, 1, e == 0 ? 4 : 3, *Pm);
+                        }
+                        sync();
+                    }
+                    for (int e = 0; e < S; e += 4) {  // horizontal edges
+                        if (!c && (e == 4 || e == 12) && t8) continue;
+                        if (e == 0 && !top) continue;
+                        const int Yq = row(e);
+                        if (e == 0 && !fld && !bot && above_fld) {  // twice, once per field of the pair above
+                            for (int j = 0; j < 2; j++) {
+                                if (act) edge(P0 + (Yq + j) * st + x * S + k, 2 * st, 3, C[(2 * pr - 2 + j) * mbw + x]);
+                                sync();
+                            }
+                            continue;
+                        }
+                        if (act) {
+                            const h2j_ctb* Pm = &m;
+                            int bs = 3;
+                            if (e == 0) {
+                                if (!fld && bot) {
+                                    Pm = &C[(2 * pr) * mbw + x];
+                                } else {
+                                    const int r = Yq - (fld ? 2 : 1) - (Y0 - 2 * S), ab = above_fld ? (r & 1) : (r >= S ? 1 : 0);
+                                    Pm = &C[(2 * pr - 2 + ab) * mbw + x];
+                                }
+                                bs = (!fld && !(Pm->mbflags & 8)) ? 4 : 3;
+                            }
+                            edge(P0 + Yq * st + x * S + k, fld ? 2 * st : st, bs, *Pm);
+                        }
+                        sync();
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(mine, ((static_cast<uint32_t>(pr) + 1) << 16) | static_cast<uint32_t>(x + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2j_frame* frames, const h2j_ctb* ctbs,
                                                                       const h2j_slice* slices, uint8_t* arena,
                                                                       const uint32_t* map, int line_w) {
@@ -3484,6 +3799,11 @@ __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2
     if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
         reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
     __syncthreads();
+    if (ufl(f.mbaff)) {  // MBAFF frame (one workgroup per picture: h2j_frame.k1bands 1)
+        if (f.bit_depth == 8) h264_db_mbaff<uint8_t>(f, C, S, arena, prog);
+        else h264_db_mbaff<uint16_t>(f, C, S, arena, prog);
+        return;
+    }
     if (ufl(f.width) <= line_w) {
         if (f.bit_depth == 8) h264_db_pairs<uint8_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
         else h264_db_pairs<uint16_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
@@ -4338,7 +4658,7 @@ static AuxStream* aux_stream(hipStream_t s) {
     return a;
 }
 
-int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
+static int predict_main(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     // two workgroups per HEVC picture (luma, chroma).  Up to 128 pictures every group gets a CU
@@ -4374,7 +4694,7 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
     // fit one workgroup's LDS: then the per-kind launches below)
     if (!wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
         hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
-                           b->arena, b->k1all);
+                           b->ctbs, b->arena, b->k1all);
         return check(hipGetLastError(), "h2j_k1_recon_any");
     }
     // per-kind launches: H.264 on a companion stream forked from (and joined back into) the
@@ -4384,7 +4704,7 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         (void)hipEventRecord(ax->fork, s);
         (void)hipStreamWaitEvent(ax->s2, ax->fork, 0);
         hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, ax->s2, b->frames, b->tus,
-                           b->arena, b->k1map);
+                           b->ctbs, b->arena, b->k1map);
         const int r = check(hipGetLastError(), "h2j_k1_recon_h264");
         (void)hipEventRecord(ax->join, ax->s2);
         if (r) {
@@ -4432,10 +4752,33 @@ int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
         // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
         if (b->k1wgs > 0)
             hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, s, b->frames, b->tus,
-                               b->arena, b->k1map);
+                               b->ctbs, b->arena, b->k1map);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;
+}
+
+// K1 for MBAFF H.264 pictures, after the other K1 launches of the batch (h2j_gpu_predict)
+static int predict_mbaff(const h2j_gpu_batch* b, hipStream_t s) {
+    if (!b->has_mbaff || b->k1wgs <= 0) return 0;
+    static bool attr = false;
+    if (!attr) {
+        const void* fn = reinterpret_cast<const void*>(h2j_k1_recon_h264_mbaff);
+        hipFuncAttributes fa{};
+        const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(160 * 1024 - st));
+        (void)hipGetLastError();
+        attr = true;
+    }
+    const size_t lds = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4;
+    hipLaunchKernelGGL(h2j_k1_recon_h264_mbaff, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds, s, b->frames, b->tus, b->ctbs,
+                       b->arena, b->k1map);
+    return check(hipGetLastError(), "h2j_k1_recon_h264_mbaff");
+}
+
+int h2j_gpu_predict(const h2j_gpu_batch* b, void* stream) {
+    const int r = predict_main(b, stream);
+    return (r || !b) ? r : predict_mbaff(b, static_cast<hipStream_t>(stream));
 }
 
 int h2j_gpu_recon(const h2j_gpu_batch* b, void* stream) {

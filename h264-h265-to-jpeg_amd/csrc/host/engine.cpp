@@ -366,7 +366,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         nsl += j.sl.size();
         // H.264 K1: pictures taller than 1080p run on one workgroup per 16 MB rows
         // (a single 16-wave workgroup would walk 5+ rows per wave)
-        f.k1bands = (f.codec == H2J_CODEC_H264 && f.ctb_h > kK1BandRows) ? (f.ctb_h + 15) / 16 : 1;
+        // (MBAFF frames run on one workgroup: their K1 / deblocking walk macroblock pairs)
+        f.k1bands = (f.codec == H2J_CODEC_H264 && f.ctb_h > kK1BandRows && !f.mbaff) ? (f.ctb_h + 15) / 16 : 1;
         f.xline = 0;
         s.frames[k] = f;
         max_w = std::max(max_w, f.width);
@@ -535,9 +536,11 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.max_ctbs = max_ctbs;
     b.has_hevc = 0;
     b.has_h264 = 0;
+    b.has_mbaff = 0;
     for (int k = 0; k < nf; k++) {
         if (s.frames[k].codec == H2J_CODEC_HEVC) b.has_hevc = 1;
         if (s.frames[k].codec == H2J_CODEC_H264) b.has_h264 = 1;
+        if (s.frames[k].codec == H2J_CODEC_H264 && s.frames[k].mbaff) b.has_mbaff = 1;
     }
     b.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
     b.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);

@@ -95,6 +95,15 @@ const uint8_t kZz8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11
 const uint8_t kBlkX[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
 const uint8_t kBlkY[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
 const uint8_t kBlkOf[4][4] = {{0, 1, 4, 5}, {2, 3, 6, 7}, {8, 9, 12, 13}, {10, 11, 14, 15}};
+// field macroblocks (MBAFF): field scans (8.5.6 / 8.5.7, raster index per scan position) and the
+// field-coded significant_coeff_flag ctxIdxInc of 8x8 blocks (Table 9-43)
+const uint8_t kFld4[16] = {0, 4, 1, 8, 12, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+const uint8_t kFld8[64] = {0,  8,  16, 1,  9,  24, 32, 17, 2,  25, 40, 48, 56, 33, 10, 3,  18, 41, 49, 57, 26, 11,
+                           4,  19, 34, 42, 50, 58, 27, 12, 5,  20, 35, 43, 51, 59, 28, 13, 6,  21, 36, 44, 52, 60,
+                           29, 14, 22, 37, 45, 53, 61, 30, 7,  15, 38, 46, 54, 62, 23, 31, 39, 47, 55, 63};
+const uint8_t kSig8x8Fld[64] = {0, 1,  1,  2,  2,  3,  3,  4,  5,  6,  7,  7,  7,  8,  4,  5,  6,  9,  10, 10, 8,  11,
+                                12, 11, 9, 9, 10, 10, 8,  11, 12, 11, 9,  9,  10, 10, 8,  11, 12, 11, 9,  9,  10, 10,
+                                8,  13, 13, 9, 9, 10, 10, 8,  13, 13, 9,  9,  10, 10, 14, 14, 14, 14, 14, 0};
 
 const uint8_t kDef4Intra[16] = {6, 13, 13, 20, 20, 20, 28, 28, 28, 28, 32, 32, 32, 37, 37, 42};
 const uint8_t kDef4Inter[16] = {10, 14, 14, 20, 20, 20, 24, 24, 24, 24, 27, 27, 27, 30, 30, 34};
@@ -354,6 +363,8 @@ struct Mb {
     uint8_t cbf_dc[3];
     uint8_t tc[16];     // CAVLC TotalCoeff per luma 4x4 block (I16x16: AC block)
     uint8_t tcc[2][4];  // CAVLC TotalCoeff per chroma AC block
+    int field = 0;      // MBAFF: mb_field_decoding_flag of the pair
+    int vx = 0, vy = 0; // grid position (MBAFF: vy = 2 * pair row + bottom)
 };
 
 // MSB-first reader over one slice's RBSP for CAVLC: 64-bit window, peek/skip.
@@ -488,6 +499,7 @@ private:
     std::vector<uint8_t> rbsp_;
     std::vector<Mb> mb_;
     int mbw_ = 0, mbh_ = 0, mbx_ = 0, mby_ = 0, qpbd_ = 0;
+    int mbaff_ = 0, cur_field_ = 0;  // MbaffFrameFlag; mb_field_decoding_flag of the current pair
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
@@ -502,20 +514,41 @@ private:
     int nc_luma(int blk);
     int nc_chroma(const Mb& m, int c, int b4);
     void decode_mb_cavlc();
-    Mb* nb(int dx, int dy) {
-        const int x = mbx_ + dx, y = mby_ + dy;
-        if (x < 0 || y < 0 || x >= mbw_) return nullptr;
-        if (dy > 0 || (dy == 0 && dx >= 0)) return nullptr;
+    Mb* mb_in_slice(int x, int y) {
+        if (x < 0 || y < 0 || x >= mbw_ || y >= mbh_) return nullptr;
         Mb* m = &mb_[y * mbw_ + x];
         return m->slice == cur_slice_ ? m : nullptr;
     }
-    Mb* nb_blk(int bx, int by, int* nblk) {
-        int dx = 0, dy = 0;
-        if (bx < 0) { dx = -1; bx += 4; }
-        if (by < 0) { dy = -1; by += 4; }
-        *nblk = kBlkOf[by][bx];
-        return (dx == 0 && dy == 0) ? &mb_[mby_ * mbw_ + mbx_] : nb(dx, dy);
+    Mb* nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW);
+    // MB covering luma location (-1, 0) / (0, -1) / (16, -1) / (-1, -1) (6.4.11.1)
+    Mb* nb(int dx, int dy) {
+        int xW, yW;
+        return nb_loc(dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
     }
+    // the 4x4 luma block covering location (4 bx, 4 by) relative to the MB (6.4.11.4)
+    Mb* nb_blk(int bx, int by, int* nblk) {
+        int xW, yW;
+        Mb* m = nb_loc(bx * 4, by * 4, 16, 16, &xW, &yW);
+        *nblk = m ? kBlkOf[yW >> 2][xW >> 2] : 0;
+        return m;
+    }
+    // availability of the sample at luma location (x, y) relative to the MB for intra prediction
+    // (inside the MB: earlier in 4x4 block order)
+    bool avail_luma(int x, int y, int cur_blk4) {
+        int xW, yW;
+        if (x >= 16 && y >= 0) return false;
+        if (x < 0 || y < 0 || x >= 16) return nb_loc(x, y, 16, 16, &xW, &yW) != nullptr;
+        return kBlkOf[y >> 2][x >> 2] < cur_blk4;
+    }
+    uint8_t mbaff_mask(int xr, int yr, int log2n, int c) {
+        const int n = 1 << log2n;
+        if (c > 0 || log2n == 4)  // I16x16 / chroma: the MB's neighbours (top, left, top-left)
+            return static_cast<uint8_t>((nb(0, -1) ? 1 : 0) | (nb(-1, 0) ? 2 : 0) | (nb(-1, -1) ? 4 : 0));
+        const int blk = kBlkOf[yr >> 2][xr >> 2];
+        return static_cast<uint8_t>((avail_luma(xr, yr - 1, blk) ? 1 : 0) | (avail_luma(xr - 1, yr, blk) ? 2 : 0) |
+                                    (avail_luma(xr - 1, yr - 1, blk) ? 4 : 0) | (avail_luma(xr + n, yr - 1, blk) ? 8 : 0));
+    }
+    void mb_start(int addr, bool cabac);
     int cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const;
     // residual_block_cabac (7.3.5.3.3): number of non-zero levels (0: coded_block_flag 0);
     // scan indices in pos[], levels in lvl[]
@@ -525,6 +558,98 @@ private:
     // sparse record: entries already (pos << 16) | uint16 level
     void emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n);
 };
+
+// 6.4.12: the MB covering location (xN, yN) relative to the current MB (maxW x maxH: 16 x 16 luma,
+// 8 x 8 chroma) and the location (xW, yW) inside it, nullptr when not available.  Non-MBAFF:
+// 6.4.12.1.  MBAFF: 6.4.12.2 (pairs A / B / C / D, Table 6-4); a bottom frame MB's upper-left
+// neighbour next to a field pair is that pair's bottom field MB, middle row (the picture sample
+// above-left: FFmpeg h264_slice.c fill_decode_neighbors, topleft_xy += mb_stride).  Every
+// neighbour sample is then the picture sample next to the MB in its own field / frame view.
+Mb* H264Parser::nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
+    Mb* cur = &mb_[mby_ * mbw_ + mbx_];
+    if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return nullptr;
+    *xW = (xN + maxW) % maxW;
+    if (xN >= 0 && xN <= maxW - 1 && yN >= 0) {
+        *yW = yN;
+        return cur;
+    }
+    if (!mbaff_) {
+        *yW = (yN + maxH) % maxH;
+        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? -1 : 0));
+    }
+    const int px = mbx_, py = mby_ >> 1;
+    const bool top = !(mby_ & 1), frame = !cur->field;
+    Mb* X = nullptr;
+    int yM = yN, bot = 0;
+    if (xN < 0 && yN < 0) {
+        if (frame && !top) {
+            X = mb_in_slice(px - 1, 2 * py);
+            if (!X) return nullptr;
+            bot = X->field;
+            yM = X->field ? (yN + maxH) >> 1 : yN;
+        } else if (frame || !top) {
+            X = mb_in_slice(px - 1, 2 * py - 2);
+            bot = 1;
+        } else {
+            X = mb_in_slice(px - 1, 2 * py - 2);
+            if (!X) return nullptr;
+            if (!X->field) { bot = 1; yM = 2 * yN; }
+        }
+    } else if (xN < 0) {
+        X = mb_in_slice(px - 1, 2 * py);
+        if (!X) return nullptr;
+        if (frame) {
+            if (!X->field) bot = top ? 0 : 1;
+            else { bot = yN & 1; yM = top ? yN >> 1 : (yN + maxH) >> 1; }
+        } else if (!X->field) {
+            const int o = top ? 0 : 1;
+            if (yN < maxH / 2) { bot = 0; yM = (yN << 1) + o; }
+            else { bot = 1; yM = (yN << 1) + o - maxH; }
+        } else {
+            bot = top ? 0 : 1;
+        }
+    } else if (xN <= maxW - 1) {
+        if (frame && !top) {
+            X = &mb_[(2 * py) * mbw_ + px];  // CurrMbAddr - 1
+        } else if (frame || !top) {
+            X = mb_in_slice(px, 2 * py - 2);
+            bot = 1;
+        } else {
+            X = mb_in_slice(px, 2 * py - 2);
+            if (!X) return nullptr;
+            if (!X->field) { bot = 1; yM = 2 * yN; }
+        }
+    } else {
+        if (frame && !top) return nullptr;
+        X = mb_in_slice(px + 1, 2 * py - 2);
+        if (!X) return nullptr;
+        if (frame || !top) bot = 1;
+        else if (!X->field) { bot = 1; yM = 2 * yN; }
+    }
+    if (!X) return nullptr;
+    *yW = (yM + maxH) % maxH;
+    return &mb_[(X->vy + bot) * mbw_ + X->vx];
+}
+
+// position the parser on macroblock address `addr` (MBAFF: pair addr / 2, bottom addr & 1) and,
+// at the top MB of an MBAFF pair, read mb_field_decoding_flag (7.3.4; CABAC ctxIdx 70 + the left /
+// upper pair being available field pairs, 9.3.3.1.1.2; CAVLC u(1))
+void H264Parser::mb_start(int addr, bool cabac) {
+    if (!mbaff_) {
+        mbx_ = addr % mbw_;
+        mby_ = addr / mbw_;
+        return;
+    }
+    const int pair = addr >> 1;
+    mbx_ = pair % mbw_;
+    mby_ = 2 * (pair / mbw_) + (addr & 1);
+    mb_[mby_ * mbw_ + mbx_].slice = cur_slice_;
+    if (!(addr & 1)) {
+        Mb* A = mb_in_slice(mbx_ - 1, mby_);
+        Mb* B = mb_in_slice(mbx_, mby_ - 2);
+        cur_field_ = cabac ? dec(70 + (A && A->field) + (B && B->field)) : static_cast<int>(vb_.u(1));
+    }
+}
 
 int H264Parser::cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const {
     if (!N) return 1;
@@ -551,23 +676,29 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     }
     int nsig = 0;
     bool last_found = false;
+    // field macroblocks (MBAFF): significance / last contexts at 277 / 338 (436 / 451 with the
+    // field ctxIdxInc table for 8x8 blocks) instead of 105 / 166 (402 / 417), 9.3.3.1.3
+    const bool fld = mb_[mby_ * mbw_ + mbx_].field != 0;
+    const int sig0 = fld ? 277 : 105, last0 = fld ? 338 : 166;
     if (cat == 5) {
+        const uint8_t* sigt = fld ? kSig8x8Fld : kSig8x8;
+        const int s8 = fld ? 436 : 402, l8 = fld ? 451 : 417;
         for (int i = 0; i < max_num - 1; i++)
-            if (cc.decision(ctx[402 + kSig8x8[i]])) {
+            if (cc.decision(ctx[s8 + sigt[i]])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
-                if (cc.decision(ctx[417 + kLast8x8[i]])) { last_found = true; break; }
+                if (cc.decision(ctx[l8 + kLast8x8[i]])) { last_found = true; break; }
             }
     } else if (cat == 3) {
         for (int i = 0; i < max_num - 1; i++) {
             const int inc = i < 2 ? i : 2;
-            if (cc.decision(ctx[105 + kSigOff[3] + inc])) {
+            if (cc.decision(ctx[sig0 + kSigOff[3] + inc])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
-                if (cc.decision(ctx[166 + kSigOff[3] + inc])) { last_found = true; break; }
+                if (cc.decision(ctx[last0 + kSigOff[3] + inc])) { last_found = true; break; }
             }
         }
     } else {
-        CabacState* const sctx = ctx + 105 + kSigOff[cat];
-        CabacState* const lctx = ctx + 166 + kSigOff[cat];
+        CabacState* const sctx = ctx + sig0 + kSigOff[cat];
+        CabacState* const lctx = ctx + last0 + kSigOff[cat];
         for (int i = 0; i < max_num - 1; i++)
             if (cc.decision(sctx[i])) {
                 pos[nsig++] = static_cast<uint8_t>(i);
@@ -614,6 +745,9 @@ void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, c
     t.mode = static_cast<uint8_t>(mode);
     t.qp = static_cast<int8_t>(qp);
     t.qpy = static_cast<int8_t>(qp_);
+    // MBAFF: the reference-availability mask (bits top, left, top-left, top-right) from the 6.4.12.2
+    // neighbours, in qpy (H.264 TBs do not use it otherwise); K0 copies it to the mask array
+    if (mbaff_) t.qpy = static_cast<int8_t>(mbaff_mask(x - mbx_ * (c ? 8 : 16), y - mby_ * (c ? 8 : 16), log2n, c));
     t.coef = static_cast<uint32_t>(job_->coefs.size());
     job_->coefs.insert(job_->coefs.end(), e, e + n);
     t.ncoef = static_cast<uint16_t>(n);
@@ -663,7 +797,10 @@ void H264Parser::decode_mb() {
     const int gx = mbx_ * 16, gy = mby_ * 16;
     h2j_ctb& rec = job_->ctbs[mby_ * mbw_ + mbx_];
     rec.slice = static_cast<uint8_t>(cur_slice_);
-    rec.mbflags = 4;
+    m.vx = mbx_;
+    m.vy = mby_;
+    m.field = mbaff_ ? cur_field_ : 0;
+    rec.mbflags = static_cast<uint8_t>(4 | (m.field ? 8 : 0));  // bit 3: MBAFF field macroblock
     // mb_type (I slice)
     {
         Mb* A = nb(-1, 0);
@@ -753,15 +890,16 @@ void H264Parser::decode_mb() {
         for (int b8 = 0; b8 < 4; b8++) {
             const int bx = b8 & 1, by = b8 >> 1;
             int ca, cb;
+            int xW, yW;  // neighbouring 8x8 blocks (6.4.11.2)
             if (bx == 0) {
-                Mb* A = nb(-1, 0);
-                ca = A ? (A->mb_type == 25 ? 0 : !((A->cbp >> (b8 + 1)) & 1)) : 0;
+                Mb* A = nb_loc(-1, by * 8, 16, 16, &xW, &yW);
+                ca = A ? (A->mb_type == 25 ? 0 : !((A->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
             } else {
                 ca = !((cbp >> (b8 - 1)) & 1);
             }
             if (by == 0) {
-                Mb* B = nb(0, -1);
-                cb = B ? (B->mb_type == 25 ? 0 : !((B->cbp >> (b8 + 2)) & 1)) : 0;
+                Mb* B = nb_loc(bx * 8, -1, 16, 16, &xW, &yW);
+                cb = B ? (B->mb_type == 25 ? 0 : !((B->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
             } else {
                 cb = !((cbp >> (b8 - 2)) & 1);
             }
@@ -799,13 +937,15 @@ void H264Parser::decode_mb() {
     uint32_t mbe[256];  // I16x16: the whole macroblock's levels
     int nmb = 0;
     auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
+    const uint8_t* z4 = m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
+    const uint8_t* z8 = m.field ? kFld8 : kZz8;
     if (is16) {
         Mb* A = nb(-1, 0);
         Mb* B = nb(0, -1);
         const int n = residual_block(0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, pos, lvl);
         m.cbf_dc[0] = static_cast<uint8_t>(n != 0);
         for (int k = 0; k < n; k++) {
-            const int r = kZz4[pos[k]];  // raster index of the DC matrix = 4x4 block position
+            const int r = z4[pos[k]];  // raster index of the DC matrix = 4x4 block position
             mbe[nmb++] = entry((r >> 2) * 4 * 16 + (r & 3) * 4, lvl[k]);
         }
     }
@@ -816,7 +956,7 @@ void H264Parser::decode_mb() {
             int ne = 0;
             if (coded) {
                 const int n = residual_block(5, 0, 64, pos, lvl);
-                for (int k = 0; k < n; k++) e[ne++] = entry(kZz8[pos[k]], lvl[k]);
+                for (int k = 0; k < n; k++) e[ne++] = entry(z8[pos[k]], lvl[k]);
                 for (int k = 0; k < 4; k++) m.cbf[b8 * 4 + k] = 1;
             }
             emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
@@ -836,13 +976,13 @@ void H264Parser::decode_mb() {
                     const int n = residual_block(1, ca + 2 * cb, 15, pos, lvl);
                     m.cbf[blk] = static_cast<uint8_t>(n != 0);
                     for (int k = 0; k < n; k++) {
-                        const int r = kZz4[pos[k] + 1];
+                        const int r = z4[pos[k] + 1];
                         mbe[nmb++] = entry((by * 4 + (r >> 2)) * 16 + bx * 4 + (r & 3), lvl[k]);
                     }
                 } else {
                     const int n = residual_block(2, ca + 2 * cb, 16, pos, lvl);
                     m.cbf[blk] = static_cast<uint8_t>(n != 0);
-                    for (int k = 0; k < n; k++) e[ne++] = entry(kZz4[pos[k]], lvl[k]);
+                    for (int k = 0; k < n; k++) e[ne++] = entry(z4[pos[k]], lvl[k]);
                 }
             }
             if (!is16) emit_sparse(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
@@ -865,12 +1005,15 @@ void H264Parser::decode_mb() {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 const int bx = b4 & 1, by = b4 >> 1;
-                const int ca = bx ? m.cbf_c[c][b4 - 1] : cbf_cond(4, nb(-1, 0), b4 + 1, c);
-                const int cb = by ? m.cbf_c[c][b4 - 2] : cbf_cond(4, nb(0, -1), b4 + 2, c);
+                int xW, yW, ca, cb;  // neighbouring chroma 4x4 blocks (6.4.11.5)
+                if (bx) ca = m.cbf_c[c][b4 - 1];
+                else { const Mb* A = nb_loc(-1, by * 4, 8, 8, &xW, &yW); ca = cbf_cond(4, A, A ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
+                if (by) cb = m.cbf_c[c][b4 - 2];
+                else { const Mb* B = nb_loc(bx * 4, -1, 8, 8, &xW, &yW); cb = cbf_cond(4, B, B ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
                 const int n = residual_block(4, ca + 2 * cb, 15, pos, lvl);
                 m.cbf_c[c][b4] = static_cast<uint8_t>(n != 0);
                 for (int k = 0; k < n; k++) {
-                    const int r = kZz4[pos[k] + 1];
+                    const int r = z4[pos[k] + 1];
                     ce[c][nce[c]++] = entry((by * 4 + (r >> 2)) * 8 + bx * 4 + (r & 3), lvl[k]);
                 }
             }
@@ -974,19 +1117,20 @@ int H264Parser::nc_chroma(const Mb& m, int c, int b4) {
     const int bx = b4 & 1, by = b4 >> 1;
     int cnt_a = 0, cnt_b = 0;
     bool aa = true, ab = true;
+    int xW, yW;  // neighbouring chroma 4x4 blocks (6.4.11.5)
     if (bx) {
         cnt_a = m.tcc[c][b4 - 1];
     } else {
-        Mb* A = nb(-1, 0);
+        Mb* A = nb_loc(-1, by * 4, 8, 8, &xW, &yW);
         if (!A) aa = false;
-        else cnt_a = A->mb_type == 25 ? 16 : A->tcc[c][b4 + 1];
+        else cnt_a = A->mb_type == 25 ? 16 : A->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
     if (by) {
         cnt_b = m.tcc[c][b4 - 2];
     } else {
-        Mb* B = nb(0, -1);
+        Mb* B = nb_loc(bx * 4, -1, 8, 8, &xW, &yW);
         if (!B) ab = false;
-        else cnt_b = B->mb_type == 25 ? 16 : B->tcc[c][b4 + 2];
+        else cnt_b = B->mb_type == 25 ? 16 : B->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
     if (aa && ab) return (cnt_a + cnt_b + 1) >> 1;
     return aa ? cnt_a : (ab ? cnt_b : 0);
@@ -999,7 +1143,10 @@ void H264Parser::decode_mb_cavlc() {
     const int gx = mbx_ * 16, gy = mby_ * 16;
     h2j_ctb& rec = job_->ctbs[mby_ * mbw_ + mbx_];
     rec.slice = static_cast<uint8_t>(cur_slice_);
-    rec.mbflags = 4;
+    m.vx = mbx_;
+    m.vy = mby_;
+    m.field = mbaff_ ? cur_field_ : 0;
+    rec.mbflags = static_cast<uint8_t>(4 | (m.field ? 8 : 0));  // bit 3: MBAFF field macroblock
     const uint32_t mbt = vb_.ue();
     if (mbt > 25) { err_ = -40; return; }
     m.mb_type = static_cast<int>(mbt);
@@ -1071,11 +1218,13 @@ void H264Parser::decode_mb_cavlc() {
     uint32_t mbe[256];
     int nmb = 0;
     auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
+    const uint8_t* z4 = m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
+    const uint8_t* z8 = m.field ? kFld8 : kZz8;
     if (is16) {
         const int n = cavlc_block(nc_luma(0), 16, pos, lvl);
         if (n < 0) { err_ = -44; return; }
         for (int k = 0; k < n; k++) {
-            const int r = kZz4[pos[k]];
+            const int r = z4[pos[k]];
             mbe[nmb++] = entry((r >> 2) * 4 * 16 + (r & 3) * 4, lvl[k]);
         }
     }
@@ -1090,7 +1239,7 @@ void H264Parser::decode_mb_cavlc() {
                     const int n = cavlc_block(nc_luma(blk), 16, pos, lvl);
                     if (n < 0) { err_ = -44; return; }
                     m.tc[blk] = static_cast<uint8_t>(n);
-                    for (int k = 0; k < n; k++) e[ne++] = entry(kZz8[4 * pos[k] + i4], lvl[k]);
+                    for (int k = 0; k < n; k++) e[ne++] = entry(z8[4 * pos[k] + i4], lvl[k]);
                 }
             }
             emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
@@ -1106,10 +1255,10 @@ void H264Parser::decode_mb_cavlc() {
                 m.tc[blk] = static_cast<uint8_t>(n);
                 for (int k = 0; k < n; k++) {
                     if (is16) {
-                        const int r = kZz4[pos[k] + 1];
+                        const int r = z4[pos[k] + 1];
                         mbe[nmb++] = entry((by * 4 + (r >> 2)) * 16 + bx * 4 + (r & 3), lvl[k]);
                     } else {
-                        e[ne++] = entry(kZz4[pos[k]], lvl[k]);
+                        e[ne++] = entry(z4[pos[k]], lvl[k]);
                     }
                 }
             }
@@ -1134,7 +1283,7 @@ void H264Parser::decode_mb_cavlc() {
                 if (n < 0) { err_ = -44; return; }
                 m.tcc[c][b4] = static_cast<uint8_t>(n);
                 for (int k = 0; k < n; k++) {
-                    const int r = kZz4[pos[k] + 1];
+                    const int r = z4[pos[k] + 1];
                     ce[c][nce[c]++] = entry((by * 4 + (r >> 2)) * 8 + bx * 4 + (r & 3), lvl[k]);
                 }
             }
@@ -1177,7 +1326,8 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             }
             const Pps& p = pps_[pps_id];
             const Sps& s = sps_[p.sps_id];
-            const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h) ? static_cast<int>(first_mb_u) : -1;
+            // MBAFF (mb_adaptive_frame_field_flag without field_pic_flag): first_mb_in_slice counts pairs
+            const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h / (1 + s.mbaff)) ? static_cast<int>(first_mb_u) : -1;
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
             if (!s.frame_mbs_only && b.u(1)) {
                 // field_pic_flag: a field picture (PAFF).  The reference's FFmpeg holds a first
@@ -1186,10 +1336,6 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 // first_mb_in_slice that does not increase starts a packet), so it receives no
                 // frame and returns false (/root/reference/src/Decoder.cpp:324-360).
                 job_->message = "field picture (PAFF): the reference decodes no frame from one field";
-                return -3;
-            }
-            if (s.mbaff) {
-                job_->message = "MBAFF frames are not supported";
                 return -3;
             }
             if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
@@ -1247,6 +1393,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 job_->reorder_delay = s.num_reorder_frames > 0;
                 mbw_ = s.mb_w;
                 mbh_ = s.mb_h;
+                mbaff_ = s.mbaff;  // MbaffFrameFlag (field pictures were rejected above)
                 qpbd_ = 6 * (s.bit_depth - 8);
                 mb_.assign(static_cast<size_t>(mbw_) * mbh_, Mb());
                 job_->ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
@@ -1269,6 +1416,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 f.mw = f.width / 4;
                 f.mh = f.height / 4;
                 f.lf_across_tiles = 1;
+                f.mbaff = s.mbaff;
                 if (s.scaling_present || p.scaling_present || p.transform_8x8) {
                     // weight scale tables (raster), used by K1 for every H.264 frame with this flag
                     job_->sl.assign(H2J_SL264_BYTES, 16);
@@ -1370,15 +1518,14 @@ int H264Parser::decode_slice(const SliceWork& w) {
     cur_slice_ = w.index;
     qp_ = w.qp;
     prev_qpd_nz_ = 0;
-    int addr = w.first_mb;
+    int addr = w.first_mb * (1 + mbaff_);  // MBAFF: first_mb_in_slice counts pairs
     if (w.cabac) {
         end_ = w.data.data() + w.nbytes;
         cc_.init(w.data.data(), end_);
         for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_word(kInitI[i][0], kInitI[i][1], qp_);
         for (;;) {
             if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
-            mbx_ = addr % mbw_;
-            mby_ = addr / mbw_;
+            mb_start(addr, true);
             decode_mb();
             if (err_) { job_->message = "macroblock decode error"; return -7; }
             if (cc_.terminate()) break;
@@ -1389,8 +1536,7 @@ int H264Parser::decode_slice(const SliceWork& w) {
         vb_.init(w.data.data(), w.nbytes, w.bitpos);
         for (;;) {
             if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
-            mbx_ = addr % mbw_;
-            mby_ = addr / mbw_;
+            mb_start(addr, false);
             decode_mb_cavlc();
             if (err_) { job_->message = "macroblock decode error"; return -7; }
             if (!vb_.more_rbsp_data(stop_bit_)) break;

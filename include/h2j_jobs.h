@@ -71,7 +71,7 @@ typedef struct {
     int16_t off[3][4];  /* HEVC SaoOffsetVal[1..4] */
     uint16_t tile;      /* tile id */
     int8_t qp;          /* H.264: QPY of the macroblock (deblocking) */
-    uint8_t mbflags;    /* H.264: bit0 I_PCM, bit1 transform_size_8x8_flag, bit2 decoded */
+    uint8_t mbflags;    /* H.264: bit0 I_PCM, bit1 transform_size_8x8_flag, bit2 decoded, bit3 MBAFF field MB */
     uint32_t ts;        /* CtbAddrRsToTs (H.264: macroblock address) */
 } h2j_ctb;
 
@@ -120,6 +120,10 @@ typedef struct {
     int32_t status;                 /* device-side error code */
     int32_t k1bands;                /* H.264 K1: workgroups (16-row bands) this picture runs on */
     uint64_t xline;                 /* H.264 K1 band boundaries: bottom rows handed to the next band (uint16) */
+    int32_t mbaff;                  /* H.264 MBAFF frame: macroblock pairs (h2j_ctb.mbflags bit 3: field
+                                       pair), TU records in the MB grid (grid row = 2 pair row + bottom),
+                                       availability masks from the host (h2j_tu.qpy bits 0-3) */
+    int32_t pad_f;
 } h2j_frame;
 
 /* per-frame JPEG statistics written by the GPU */
