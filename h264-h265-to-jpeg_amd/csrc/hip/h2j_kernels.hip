@@ -3684,16 +3684,19 @@ DEVI void h264_db_mbaff(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* S
                 const h2j_slice sl = SL[m.slice];
                 if (sl.deblock_disabled == 1) continue;
                 const bool fld = (m.mbflags & 8) != 0, t8 = (m.mbflags & 2) != 0;
+                // slice tests on the neighbour of a field MB's own parity (a PAFF pair's fields are
+                // separate slices; an MBAFF pair's MBs share one)
+                const int par = fld ? bot : 0;
                 bool left = x > 0;
                 if (left) {
-                    const h2j_ctb& L = C[(2 * pr) * mbw + x - 1];
+                    const h2j_ctb& L = C[(2 * pr + par) * mbw + x - 1];
                     left = (L.mbflags & 4) && !(sl.deblock_disabled == 2 && SL[L.slice].slice_addr_rs != sl.slice_addr_rs);
                 }
                 bool top;
                 if (!fld && bot) top = true;  // the pair's internal edge
                 else if (pr == 0) top = false;
                 else {
-                    const h2j_ctb& B = C[(2 * pr - 2) * mbw + x];
+                    const h2j_ctb& B = C[(2 * pr - 2 + par) * mbw + x];
                     top = (B.mbflags & 4) && !(sl.deblock_disabled == 2 && SL[B.slice].slice_addr_rs != sl.slice_addr_rs);
                 }
                 const bool above_fld = pr > 0 && (C[(2 * pr - 2) * mbw + x].mbflags & 8);

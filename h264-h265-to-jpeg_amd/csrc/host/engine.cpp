@@ -867,6 +867,12 @@ int Engine::run_batch(Batch& b) {
                     jobs[k].error = -7;
                     jobs[k].message = "decoder delay: no picture before a flush (H2J_STRICT_REFERENCE)";
                 }
+                if (strict_reference && jobs[k].error == 0 && jobs[k].field_pair) {
+                    // one packet holds one field: FFmpeg waits for the second field and the
+                    // reference returns false (/root/reference/src/Decoder.cpp:324, 342-360)
+                    jobs[k].error = -3;
+                    jobs[k].message = "field picture (PAFF): no frame from one field (H2J_STRICT_REFERENCE)";
+                }
                 status[k] = jobs[k].error;
                 if (jobs[k].error == 0) s.live.push_back(k);
             }

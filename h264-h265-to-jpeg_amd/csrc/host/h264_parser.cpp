@@ -479,6 +479,7 @@ struct SliceWork {
     size_t bitpos = 0;          // CAVLC: first bit of the slice data
     size_t stop_bit = 0;        // CAVLC: position of the rbsp_stop_one_bit
     int qp = 0, first_mb = 0, index = 0, pps_id = 0;
+    int parity = 0;  // PAFF: bottom_field_flag
 };
 
 class H264Parser {
@@ -500,6 +501,9 @@ private:
     std::vector<Mb> mb_;
     int mbw_ = 0, mbh_ = 0, mbx_ = 0, mby_ = 0, qpbd_ = 0;
     int mbaff_ = 0, cur_field_ = 0;  // MbaffFrameFlag; mb_field_decoding_flag of the current pair
+    // PAFF field pair: held in the MBAFF layout as all-field pairs (field MB (x, fy) of parity f at
+    // grid (x, 2 fy + f)); parity_ = bottom_field_flag of the slice being decoded
+    int paff_ = 0, parity_ = 0;
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
     Cabac cc_;
     const uint8_t* end_ = nullptr;
@@ -573,9 +577,9 @@ Mb* H264Parser::nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
         *yW = yN;
         return cur;
     }
-    if (!mbaff_) {
+    if (!mbaff_ || paff_) {  // PAFF: 6.4.12.1 on the field's own MB grid
         *yW = (yN + maxH) % maxH;
-        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? -1 : 0));
+        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? (paff_ ? -2 : -1) : 0));
     }
     const int px = mbx_, py = mby_ >> 1;
     const bool top = !(mby_ & 1), frame = !cur->field;
@@ -635,6 +639,13 @@ Mb* H264Parser::nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
 // at the top MB of an MBAFF pair, read mb_field_decoding_flag (7.3.4; CABAC ctxIdx 70 + the left /
 // upper pair being available field pairs, 9.3.3.1.1.2; CAVLC u(1))
 void H264Parser::mb_start(int addr, bool cabac) {
+    if (paff_) {  // field MB address of the current field
+        mbx_ = addr % mbw_;
+        mby_ = 2 * (addr / mbw_) + parity_;
+        mb_[mby_ * mbw_ + mbx_].slice = cur_slice_;
+        cur_field_ = 1;
+        return;
+    }
     if (!mbaff_) {
         mbx_ = addr % mbw_;
         mby_ = addr / mbw_;
@@ -1301,7 +1312,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
     split_annexb(data, size, nals);
     rbsp_.resize(size + 16);
     bool have = false;
-    int first_frame_num = -1, first_idr = -1;
+    int first_frame_num = -1, first_idr = -1, fields_seen = 0;
     int nslice = 0;
     std::vector<SliceWork> works;
     for (const Nal& nal : nals) {
@@ -1326,19 +1337,26 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             }
             const Pps& p = pps_[pps_id];
             const Sps& s = sps_[p.sps_id];
-            // MBAFF (mb_adaptive_frame_field_flag without field_pic_flag): first_mb_in_slice counts pairs
-            const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h / (1 + s.mbaff)) ? static_cast<int>(first_mb_u) : -1;
             const int frame_num = static_cast<int>(b.u(s.log2_max_frame_num));
-            if (!s.frame_mbs_only && b.u(1)) {
-                // field_pic_flag: a field picture (PAFF).  The reference's FFmpeg holds a first
-                // field until its second field arrives ("Wait for second field", h264dec.c), and
-                // the reference sends one packet (one field: the h264 parser splits fields, a
-                // first_mb_in_slice that does not increase starts a packet), so it receives no
-                // frame and returns false (/root/reference/src/Decoder.cpp:324-360).
-                job_->message = "field picture (PAFF): the reference decodes no frame from one field";
-                return -3;
+            // field_pic_flag / bottom_field_flag: a field picture (PAFF).  FFmpeg holds a first field
+            // until the second field of the frame arrives ("Wait for second field", h264dec.c) and
+            // outputs the interleaved frame; the reference sends one packet (one field: FFmpeg's
+            // h264 parser splits fields) and returns false (/root/reference/src/Decoder.cpp:324-360,
+            // H2J_STRICT_REFERENCE).  Picture 0 here is the field pair: the first field and the
+            // other parity's field of the same frame_num.
+            int field_pic = 0, bottom = 0;
+            if (!s.frame_mbs_only) {
+                field_pic = static_cast<int>(b.u(1));
+                if (field_pic) bottom = static_cast<int>(b.u(1));
             }
-            if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            // MBAFF: first_mb_in_slice counts pairs; a field: the field's macroblocks
+            const int first_mb = first_mb_u < static_cast<uint32_t>(s.mb_w * s.mb_h / (1 + (s.mbaff || field_pic))) ? static_cast<int>(first_mb_u) : -1;
+            if (have && !paff_ && (field_pic || first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            if (have && paff_) {
+                if (!field_pic || frame_num != first_frame_num) break;
+                const bool seen = (fields_seen >> bottom) & 1;
+                if (first_mb == 0 ? seen : !seen) break;  // a third field / a slice of an unseen field not at 0
+            }
             // FFmpeg h264_slice.c: "first_mb_in_slice overflow" drops the slice; once a slice of
             // picture 0 is collected the picture is still output, so stop there as at a
             // picture boundary, and fail only when nothing of picture 0 was accepted
@@ -1351,10 +1369,10 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             if (type == 5) b.ue();
             if (s.poc_type == 0) {
                 b.u(s.log2_max_poc_lsb);
-                if (p.bottom_field_pic_order) b.se();
+                if (p.bottom_field_pic_order && !field_pic) b.se();
             } else if (s.poc_type == 1 && !s.delta_pic_order_always_zero) {
                 b.se();
-                if (p.bottom_field_pic_order) b.se();
+                if (p.bottom_field_pic_order && !field_pic) b.se();
             }
             if (p.redundant_pic_cnt) b.ue();
             if (nal_ref_idc) {
@@ -1387,13 +1405,16 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             }
             srec.cqp_offset[0] = static_cast<int8_t>(p.cqp);
             srec.cqp_offset[1] = static_cast<int8_t>(p.cqp2);
-            srec.slice_addr_rs = first_mb;
+            // slice identity for the kernels' slice tests: unique over both fields of a pair
+            srec.slice_addr_rs = first_mb + bottom * (s.mb_w * s.mb_h / 2);
             if (!have) {
                 s_ = &s;
                 job_->reorder_delay = s.num_reorder_frames > 0;
                 mbw_ = s.mb_w;
                 mbh_ = s.mb_h;
-                mbaff_ = s.mbaff;  // MbaffFrameFlag (field pictures were rejected above)
+                mbaff_ = s.mbaff || field_pic;  // MbaffFrameFlag; a field pair uses the same layout
+                paff_ = field_pic;
+                job_->field_pair = field_pic != 0;
                 qpbd_ = 6 * (s.bit_depth - 8);
                 mb_.assign(static_cast<size_t>(mbw_) * mbh_, Mb());
                 job_->ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
@@ -1416,7 +1437,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 f.mw = f.width / 4;
                 f.mh = f.height / 4;
                 f.lf_across_tiles = 1;
-                f.mbaff = s.mbaff;
+                f.mbaff = mbaff_;
                 if (s.scaling_present || p.scaling_present || p.transform_8x8) {
                     // weight scale tables (raster), used by K1 for every H.264 frame with this flag
                     job_->sl.assign(H2J_SL264_BYTES, 16);
@@ -1440,6 +1461,8 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
             w.index = nslice;
             w.pps_id = static_cast<int>(pps_id);
             w.first_mb = first_mb;
+            w.parity = bottom;
+            fields_seen |= field_pic << bottom;
             w.qp = p.init_qp + qpd;
             if (w.qp < -qpbd_ || w.qp > 51) { job_->message = "invalid slice QP"; return -6; }
             w.cabac = p.cabac != 0;
@@ -1467,6 +1490,10 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
         }
     }
     if (!have) { job_->message = "no picture found"; return -9; }
+    if (paff_ && fields_seen != 3) {  // FFmpeg outputs no frame for a field without its pair
+        job_->message = "field picture (PAFF) without the second field of its frame";
+        return -3;
+    }
     // Slices share nothing for parsing (CABAC / CAVLC restart, neighbours in other slices are
     // unavailable): with threads > 1 they decode side by side, slice 0 into this job, the
     // others into their own jobs, appended in decoding order.
@@ -1518,13 +1545,15 @@ int H264Parser::decode_slice(const SliceWork& w) {
     cur_slice_ = w.index;
     qp_ = w.qp;
     prev_qpd_nz_ = 0;
-    int addr = w.first_mb * (1 + mbaff_);  // MBAFF: first_mb_in_slice counts pairs
+    parity_ = w.parity;
+    int addr = w.first_mb * (1 + (mbaff_ && !paff_));  // MBAFF: first_mb_in_slice counts pairs
+    const int nmb = paff_ ? mbw_ * mbh_ / 2 : mbw_ * mbh_;
     if (w.cabac) {
         end_ = w.data.data() + w.nbytes;
         cc_.init(w.data.data(), end_);
         for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_word(kInitI[i][0], kInitI[i][1], qp_);
         for (;;) {
-            if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
+            if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
             mb_start(addr, true);
             decode_mb();
             if (err_) { job_->message = "macroblock decode error"; return -7; }
@@ -1535,7 +1564,7 @@ int H264Parser::decode_slice(const SliceWork& w) {
         stop_bit_ = w.stop_bit;
         vb_.init(w.data.data(), w.nbytes, w.bitpos);
         for (;;) {
-            if (addr >= mbw_ * mbh_) { job_->message = "slice overruns the picture"; return -7; }
+            if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
             mb_start(addr, false);
             decode_mb_cavlc();
             if (err_) { job_->message = "macroblock decode error"; return -7; }

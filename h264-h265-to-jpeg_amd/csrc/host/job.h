@@ -22,6 +22,10 @@ struct FrameJob {
     // sps_max_num_reorder_pics[HighestTid] > 0): FFmpeg holds the picture back until more
     // pictures or a flush arrive (only H2J_STRICT_REFERENCE acts on it)
     bool reorder_delay = false;
+    // H.264 PAFF: picture 0 is a field pair (two field pictures).  FFmpeg outputs the frame after
+    // the second field; the reference sends one packet (one field) and returns false (only
+    // H2J_STRICT_REFERENCE acts on it)
+    bool field_pair = false;
 
     void clear() {
         hdr = h2j_frame{};
@@ -33,6 +37,7 @@ struct FrameJob {
         error = 0;
         message.clear();
         reorder_delay = false;
+        field_pair = false;
     }
 };
 

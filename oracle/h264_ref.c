@@ -390,6 +390,10 @@ typedef struct {
     int W, H, mbw, mbh, bd, bdc, qpbd, qpbdc;
     int mbaff; /* MbaffFrameFlag: macroblock pairs; MbInfo at (vx, vy = 2 * pair row + bottom) */
     int cur_field; /* mb_field_decoding_flag of the pair being decoded */
+    /* PAFF: picture 0 is a field pair (field_pic_flag 1), held in the MBAFF layout as all-field pairs
+     * (field MB (x, fy) of parity f at grid (x, 2 fy + f)); neighbours stay inside a field
+     * (6.4.12.1 on the field's MB grid) */
+    int paff, parity, fields_seen;
     uint16_t *pl[3];
     int st[3];
     MbInfo *mb;
@@ -437,10 +441,11 @@ static MbInfo *nb_loc(H4Dec *d, int xN, int yN, int maxW, int maxH, int *xW, int
     MbInfo *cur = &d->mb[d->mby * d->mbw + d->mbx];
     if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return NULL;
     *xW = (xN + maxW) % maxW;
-    if (!d->mbaff) {
+    if (!d->mbaff || d->paff) {
         int dx = xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0), dy = yN < 0 ? -1 : 0;
         *yW = (yN + maxH) % maxH;
-        return (dx == 0 && dy == 0) ? cur : mb_in_slice(d, d->mbx + dx, d->mby + dy);
+        if (dx == 0 && dy == 0) return cur;
+        return mb_in_slice(d, d->mbx + dx, d->mby + (d->paff ? 2 * dy : dy)); /* PAFF: same field */
     }
     const int px = d->mbx, py = d->mby >> 1, top = !(d->mby & 1), frame = !cur->field;
     MbInfo *X = NULL, *N = NULL; /* X: top MB of the neighbouring pair */
@@ -1267,6 +1272,13 @@ static int recon_mb(H4Dec *d, MbInfo *m) {
  * top MB of every pair in I slices; CABAC ctxIdx 70 + condTermFlagA + condTermFlagB, the left /
  * upper pair being available field pairs, 9.3.3.1.1.2) */
 static void mb_start(H4Dec *d, int addr, int cabac) {
+    if (d->paff) { /* field MB address of the current field */
+        d->mbx = addr % d->mbw;
+        d->mby = 2 * (addr / d->mbw) + d->parity;
+        d->mb[d->mby * d->mbw + d->mbx].slice = d->nslice;
+        d->cur_field = 1;
+        return;
+    }
     if (!d->mbaff) {
         d->mbx = addr % d->mbw;
         d->mby = addr / d->mbw;
@@ -1787,16 +1799,19 @@ static void deblock_mb_mbaff(H4Dec *d, int mx, int vy) {
     const H4Slice *sl = &d->sl[m->slice];
     if (sl->disable_deblock == 1) return;
     const int py = vy >> 1, bot = vy & 1;
+    /* slice tests on the neighbour of the MB's own parity for field MBs (MBAFF pairs share a
+     * slice; the fields of a PAFF pair do not) */
+    const int par = m->field ? bot : 0;
     int left = mx > 0;
     if (left) {
-        const MbInfo *L = &d->mb[(2 * py) * d->mbw + mx - 1];
+        const MbInfo *L = &d->mb[(2 * py + par) * d->mbw + mx - 1];
         if (L->slice < 0 || (sl->disable_deblock == 2 && L->slice != m->slice)) left = 0;
     }
     int top;
     if (!m->field && bot) top = 1; /* the pair's internal edge (CurrMbAddr - 1) */
     else if (py == 0) top = 0;
     else {
-        const MbInfo *B = &d->mb[(2 * py - 2) * d->mbw + mx];
+        const MbInfo *B = &d->mb[(2 * py - 2 + par) * d->mbw + mx];
         top = B->slice >= 0 && !(sl->disable_deblock == 2 && B->slice != m->slice);
     }
     for (int c = 0; c < 3; c++) {
@@ -1869,15 +1884,23 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             const H4Sps *s = &d->sps[p->sps_id];
             if (!s->valid) { ret = -4; goto done; }
             int frame_num = (int)ob_u(&b, s->log2_max_frame_num);
-            /* field_pic_flag: a field (PAFF) -- FFmpeg outputs no frame for the first field alone
-             * (h264dec.c "Wait for second field"), so the reference returns false */
-            if (!s->frame_mbs_only && ob_u(&b, 1)) { ret = -3; goto done; }
-            int field_pic = 0; /* (a field picture returned above) */
-            (void)field_pic;
-            if (have && (first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            /* field_pic_flag / bottom_field_flag: PAFF.  The reference's FFmpeg outputs no frame for a
+             * first field alone (h264dec.c "Wait for second field") and the reference sends one
+             * packet, so it returns false for field pictures; restated here is the field pair, the
+             * frame FFmpeg outputs once both fields are decoded (the build's default mode) */
+            int field_pic = 0, bottom = 0;
+            if (!s->frame_mbs_only) {
+                field_pic = (int)ob_u(&b, 1);
+                if (field_pic) bottom = (int)ob_u(&b, 1);
+            }
+            if (have && !d->paff && (field_pic || first_mb == 0 || frame_num != first_frame_num || (type == 5) != (first_idr == 1))) break;
+            if (have && d->paff) { /* picture 0 = the first field + the other parity's field of the same frame */
+                if (!field_pic || frame_num != first_frame_num) break;
+                if (first_mb == 0 ? (d->fields_seen >> bottom) & 1 : !((d->fields_seen >> bottom) & 1)) break;
+            }
             /* FFmpeg: "first_mb_in_slice overflow" drops the slice; picture 0 is output from the
              * slices already collected, and fails only when none was */
-            if (first_mb < 0 || first_mb * (1 + s->mbaff) >= s->mb_w * s->mb_h) {
+            if (first_mb < 0 || first_mb * (1 + (s->mbaff && !field_pic)) * (1 + field_pic) >= s->mb_w * s->mb_h) {
                 if (have) break;
                 ret = -6;
                 goto done;
@@ -1886,10 +1909,10 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             if (type == 5) ob_ue(&b);                          /* idr_pic_id */
             if (s->poc_type == 0) {
                 ob_u(&b, s->log2_max_poc_lsb);
-                if (p->bottom_field_pic_order) ob_se(&b);
+                if (p->bottom_field_pic_order && !field_pic) ob_se(&b);
             } else if (s->poc_type == 1 && !s->delta_pic_order_always_zero) {
                 ob_se(&b);
-                if (p->bottom_field_pic_order) ob_se(&b);
+                if (p->bottom_field_pic_order && !field_pic) ob_se(&b);
             }
             if (p->redundant_pic_cnt) ob_ue(&b);
             if (nal_ref_idc) {
@@ -1927,7 +1950,8 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 d->bd = s->bit_depth;
                 d->bdc = s->bit_depth_c;
                 d->qpbd = 6 * (d->bd - 8);
-                d->mbaff = s->mbaff; /* MbaffFrameFlag = mb_adaptive_frame_field_flag && !field_pic_flag */
+                d->mbaff = s->mbaff || field_pic; /* MbaffFrameFlag; a PAFF field pair uses the same layout */
+                d->paff = field_pic;
                 d->qpbdc = 6 * (d->bdc - 8);
                 for (int c = 0; c < 3; c++) {
                     int w = c ? d->W / 2 : d->W, h = c ? d->H / 2 : d->H;
@@ -1943,8 +1967,12 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             d->p = p;
             d->qp = p->init_qp + qpd;
             d->prev_qpd_nz = 0;
-            /* MBAFF: CurrMbAddr = first_mb_in_slice * 2, macroblocks in pair order (top, bottom) */
-            int mbaddr = first_mb * (1 + d->mbaff);
+            d->parity = bottom;
+            d->fields_seen |= field_pic << bottom;
+            /* MBAFF: CurrMbAddr = first_mb_in_slice * 2, macroblocks in pair order (top, bottom);
+             * PAFF: field MB addresses (mb_start) */
+            int mbaddr = first_mb * (1 + (d->mbaff && !d->paff));
+            const int nmb = d->paff ? d->mbw * d->mbh / 2 : d->mbw * d->mbh;
             if (p->cabac) {
                 /* cabac_alignment_one_bit */
                 while (b.pos & 7) ob_u(&b, 1);
@@ -1952,7 +1980,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 oc_init(&d->cc, &d->bits);
                 init_ctx(d, d->qp);
                 for (;;) {
-                    if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
+                    if (mbaddr >= nmb) { ret = -7; goto done_free; }
                     mb_start(d, mbaddr, 1);
                     decode_mb(d, d->nslice);
                     if (oc_terminate(&d->cc)) break;
@@ -1961,7 +1989,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
             } else {
                 d->bits = b;
                 for (;;) {
-                    if (mbaddr >= d->mbw * d->mbh) { ret = -7; goto done_free; }
+                    if (mbaddr >= nmb) { ret = -7; goto done_free; }
                     mb_start(d, mbaddr, 0);
                     if (decode_mb_cavlc(d, d->nslice) < 0) { ret = -21; goto done_free; }
                     if (!ob_more_rbsp(&d->bits)) break;
@@ -1975,6 +2003,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
         }
     }
     if (!have) { ret = -9; goto done; }
+    if (d->paff && d->fields_seen != 3) { ret = -3; goto done_free; } /* a field without its pair */
     if (!(flags & 1)) {
         if (d->mbaff) { /* macroblock address order: pairs in raster order, top MB then bottom MB */
             for (int pr = 0; pr < d->mbh / 2; pr++)

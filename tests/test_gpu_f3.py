@@ -79,3 +79,26 @@ def test_strict_reference_mode_on_decoder_delay_streams(engine):
             assert "decoder delay" in strict_engine.frame_error(i), e["file"]
         else:
             assert st == d, e["file"]
+
+
+def test_strict_reference_mode_on_field_pairs(engine):
+    """PAFF field pairs (tests/golden/h264/a37-a40): the default engine outputs the frame FFmpeg
+    outputs after the second field (bit-exact to the oracle in test_gpu_h264.py); with
+    H2J_STRICT_REFERENCE=1 it returns no JPEG, as the reference does for a field picture (one packet
+    holds one field, /root/reference/src/Decoder.cpp:324, 342-360)."""
+    import glob
+    import h2j
+    paths = sorted(glob.glob(golden("h264/*_paff_*.h264")))
+    assert len(paths) >= 4
+    streams = [read(p) for p in paths]
+    default = engine.transcode(streams)
+    os.environ["H2J_STRICT_REFERENCE"] = "1"
+    try:
+        strict_engine = h2j.Engine()
+    finally:
+        del os.environ["H2J_STRICT_REFERENCE"]
+    strict = strict_engine.transcode(streams)
+    for i, (p, d, st) in enumerate(zip(paths, default, strict)):
+        assert d is not None and d == O.transcode(streams[i]), p
+        assert st is None, p
+        assert "field picture" in strict_engine.frame_error(i), p

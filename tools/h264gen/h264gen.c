@@ -184,7 +184,7 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless, mbaff, cur_field;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless, mbaff, cur_field, paff, onefield;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -207,9 +207,9 @@ static Mb *nb_loc(G *g, int xN, int yN, int maxW, int maxH, int *xW, int *yW) {
     if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return NULL;
     *xW = (xN + maxW) % maxW;
     if (xN >= 0 && xN <= maxW - 1 && yN >= 0) { *yW = yN; return cur; }
-    if (!g->mbaff) {
+    if (!g->mbaff || g->paff) { /* --paff: the neighbours of a field MB are in its own field */
         *yW = (yN + maxH) % maxH;
-        return mb_in_slice(g, g->mbx + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), g->mby + (yN < 0 ? -1 : 0));
+        return mb_in_slice(g, g->mbx + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), g->mby + (yN < 0 ? (g->paff ? -2 : -1) : 0));
     }
     const int px = g->mbx, py = g->mby >> 1, top = !(g->mby & 1), frame = !cur->field;
     Mb *X = NULL;
@@ -1159,7 +1159,7 @@ static void write_sps(FILE *f, G *g, int profile) {
      * crop in units of 4 rows (7.4.2.1.1) */
     bw_ue(&b, (uint32_t)(g->ilsps ? g->mbh / 2 - 1 : g->mbh - 1));
     bw_put(&b, (uint32_t)!g->ilsps, 1); /* frame_mbs_only */
-    if (g->ilsps) bw_put(&b, (uint32_t)g->mbaff, 1); /* mb_adaptive_frame_field_flag (--mbaff: MBAFF frame) */
+    if (g->ilsps) bw_put(&b, (uint32_t)(g->mbaff && !g->paff), 1); /* mb_adaptive_frame_field_flag (--mbaff: MBAFF frame) */
     bw_put(&b, 1, 1); /* direct_8x8_inference */
     int crop = g->outW != g->W || g->outH != g->H;
     if (g->rawcrop[0] >= 0) { /* --crop l,r,t,b: raw frame_crop offsets (malformed-SPS vectors) */
@@ -1257,6 +1257,12 @@ int main(int argc, char **argv) {
     g->mbaff = opt_int(argc, argv, "--mbaff", 0);
     if (g->mbaff) g->ilsps = 1;
     int fieldpct = opt_int(argc, argv, "--fieldpct", 50);
+    /* --paff 1: a field pair (field_pic_flag 1): the first field an IDR (or --nonidr) I field, the
+     * second field (the other parity, nal type 1) an I field; --paff 2: bottom field first.  Held
+     * like an MBAFF frame of field pairs: field MB (x, fy) of parity f at grid (x, 2 fy + f) */
+    g->paff = opt_int(argc, argv, "--paff", 0);
+    if (g->paff) g->mbaff = g->ilsps = 1;
+    g->onefield = opt_int(argc, argv, "--onefield", 0); /* --paff with the first field only (malformed) */
     /* --lossless 1: High 4:4:4 Predictive (profile_idc 244) with qpprime_y_zero_transform_bypass_flag,
      * every macroblock at QP'Y 0 (TransformBypassModeFlag), residual DPCM for H / V predictions */
     g->lossless = opt_int(argc, argv, "--lossless", 0);
@@ -1290,19 +1296,23 @@ int main(int argc, char **argv) {
     write_sps(fo, g, profile);
     write_pps(fo, g, profile >= 100, 0);
     if (g->delay) write_pps(fo, g, 0, 1);
-    int rows = g->slice_rows > 0 ? g->slice_rows : g->mbh;
-    if (g->mbaff) rows = (rows + 1) & ~1; /* slices start at pair rows */
+    const int fh = g->paff ? g->mbh / 2 : g->mbh; /* MB rows per coded picture (--paff: per field) */
+    int rows = g->slice_rows > 0 ? g->slice_rows : fh;
+    if (g->mbaff && !g->paff) rows = (rows + 1) & ~1; /* slices start at pair rows */
     int nslice = 0;
-    for (int r0 = 0; r0 < g->mbh; r0 += rows, nslice++) {
+    for (int fld = 0; fld < (g->paff ? 2 - g->onefield : 1); fld++) {
+    const int par = fld ^ (g->paff == 2), idr = !g->nonidr && fld == 0;
+    for (int r0 = 0; r0 < fh; r0 += rows, nslice++) {
         BW b; bw_init(&b);
-        bw_ue(&b, (uint32_t)(r0 == 0 && g->firstmb >= 0 ? g->firstmb : (g->mbaff ? r0 / 2 : r0) * g->mbw)); /* first_mb (MBAFF: pair index; --firstmb: malformed) */
+        bw_ue(&b, (uint32_t)(r0 == 0 && g->firstmb >= 0 ? g->firstmb : (g->mbaff && !g->paff ? r0 / 2 : r0) * g->mbw)); /* first_mb (MBAFF: pair index; --firstmb: malformed) */
         bw_ue(&b, 7);                         /* I (all slices I) */
         bw_ue(&b, 0);                         /* pps */
         bw_put(&b, 0, 4);                     /* frame_num */
-        if (g->ilsps) bw_put(&b, 0, 1);       /* field_pic_flag: a frame */
-        if (!g->nonidr) bw_ue(&b, 0);         /* idr_pic_id */
-        bw_put(&b, 0, 4);                     /* poc lsb */
-        if (!g->nonidr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } /* dec_ref_pic_marking (IDR) */
+        if (g->ilsps) bw_put(&b, (uint32_t)!!g->paff, 1); /* field_pic_flag */
+        if (g->paff) bw_put(&b, (uint32_t)par, 1);        /* bottom_field_flag */
+        if (idr) bw_ue(&b, 0);                /* idr_pic_id */
+        bw_put(&b, (uint32_t)fld, 4);         /* poc lsb */
+        if (idr) { bw_put(&b, 0, 1); bw_put(&b, 0, 1); } /* dec_ref_pic_marking (IDR) */
         else bw_put(&b, 0, 1);                /* adaptive_ref_pic_marking_mode_flag */
         int sqp = clip3(-6 * (g->bd - 8), 51, g->qp + (nslice && !g->lossless ? rndn(5) - 2 : 0));
         bw_se(&b, sqp - 26);
@@ -1319,8 +1329,17 @@ int main(int argc, char **argv) {
         g->cur_slice = nslice;
         g->cur_qp = sqp;
         g->prev_qpd_nz = 0;
-        int r1 = r0 + rows < g->mbh ? r0 + rows : g->mbh;
-        if (g->mbaff) { /* pairs in raster order, top MB then bottom MB (7.3.4) */
+        int r1 = r0 + rows < fh ? r0 + rows : fh;
+        if (g->paff) { /* field MBs in raster order of the field */
+            for (int my = r0; my < r1; my++)
+                for (int mx = 0; mx < g->mbw; mx++) {
+                    g->mbx = mx; g->mby = 2 * my + par;
+                    g->mb[g->mby * g->mbw + mx].slice = nslice;
+                    g->cur_field = 1;
+                    encode_mb(g);
+                    if (!g->cavlc) ce_term(&g->ce, my == r1 - 1 && mx == g->mbw - 1);
+                }
+        } else if (g->mbaff) { /* pairs in raster order, top MB then bottom MB (7.3.4) */
             for (int pr = r0 / 2; pr < r1 / 2; pr++)
                 for (int mx = 0; mx < g->mbw; mx++)
                     for (int bt = 0; bt < 2; bt++) {
@@ -1346,8 +1365,9 @@ int main(int argc, char **argv) {
         if (!g->cavlc) ce_finish(&g->ce);
         bw_put(&b, 1, 1);
         bw_align_zero(&b);
-        write_nal(fo, 3, g->nonidr ? 1 : 5, b.buf, b.n);
+        write_nal(fo, 3, idr ? 5 : 1, b.buf, b.n);
         free(b.buf);
+    }
     }
     /* decoder delay: delay + 1 all-skip P pictures (CAVLC, PPS 1), output order != decoding order:
      * frame_num 1, 2, ..., POC 2(delay+1), 2, 4, ... */

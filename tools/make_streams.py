@@ -265,6 +265,13 @@ PARITY264 = [
     ("a34_256x128_mbaff_all_field", 256, 128, 8, 20, 70, 10, ["--mbaff", "1", "--fieldpct", "100", "--alpha", "3", "--beta", "2"]),
     ("a35_240x96_mbaff_cavlc_8x8_offsets", 240, 96, 8, 18, 71, 12, ["--mbaff", "1", "--cavlc", "1", "--cqp", "3", "--cqp2", "-2"]),
     ("a36_1920x1080_mbaff_1080i", 1920, 1080, 8, 26, 68, 3, ["--mbaff", "1", "--t8x8", "1"]),
+    # PAFF field pairs (field_pic_flag 1): an IDR I field and a non-IDR I field of the other parity,
+    # decoded as the frame FFmpeg outputs after the second field (the reference itself returns false
+    # for a field picture: one packet, "Wait for second field"); --paff 2 = bottom field first
+    ("a37_320x192_paff_cabac_8x8_slices", 320, 192, 8, 24, 72, 6, ["--paff", "1", "--t8x8", "1", "--slices", "2"]),
+    ("a38_256x160_paff_botfirst_cavlc_dbidc2", 256, 160, 8, 22, 73, 5, ["--paff", "2", "--cavlc", "1", "--slices", "2", "--dbidc", "2"]),
+    ("a39_192x128_paff_10bit_pcm_offsets", 192, 128, 10, 26, 74, 8, ["--paff", "1", "--pcm", "1", "--cqp", "2", "--alpha", "2", "--beta", "-1"]),
+    ("a40_1920x1080_paff_1080i", 1920, 1080, 8, 26, 75, 3, ["--paff", "1", "--t8x8", "1"]),
 ]
 
 
@@ -376,6 +383,8 @@ MALFORMED = [
     ("m_avc_vui_cpb32_ok", 264, 160, 96, ["--vuicpb", "31", "--vuireorder", "0"], "ok"),
     # FFmpeg 4.3 has no 11- / 13-bit H.264 output format (h264_slice.c "Unsupported bit depth")
     ("m_avc_bitdepth11", 264, 160, 96, ["@bd", "11"], "fail"),
+    # a PAFF field without the other parity's field: FFmpeg outputs no frame for it
+    ("m_avc_paff_one_field", 264, 160, 96, ["--paff", "1", "--onefield", "1"], "fail"),
 ]
 
 
