@@ -348,6 +348,30 @@ __device__ unsigned long long g_prof[16];
 #define PROF_LAPK(k)
 #define PROF_FLUSH()
 #endif
+// H.264: the counters go to the deblocking pair kernel (default) or, with -DH2J_PROF_AVCK1, to K1
+#if defined(H2J_PROF) && defined(H2J_PROF_AVCK1)
+#define AVP_DECL PROF_DECL
+#define AVP_LAP(i) PROF_LAP(i)
+#define AVP_LAPK(k) PROF_LAPK(k)
+#define AVP_ADD(i, v) PROF_ADD(i, v)
+#define AVP_FLUSH() PROF_FLUSH()
+#define DBP_DECL
+#define DBP_LAP(i)
+#define DBP_LAPK(k)
+#define DBP_ADD(i, v)
+#define DBP_FLUSH()
+#else
+#define AVP_DECL
+#define AVP_LAP(i)
+#define AVP_LAPK(k)
+#define AVP_ADD(i, v)
+#define AVP_FLUSH()
+#define DBP_DECL PROF_DECL
+#define DBP_LAP(i) PROF_LAP(i)
+#define DBP_LAPK(k) PROF_LAPK(k)
+#define DBP_ADD(i, v) PROF_ADD(i, v)
+#define DBP_FLUSH() PROF_FLUSH()
+#endif
 
 // uniform values into scalar registers; records held one per lane, read with readlane
 DEVI uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1343,6 +1367,45 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
 #define WIN(dx, dy) (chroma ? s.wc[c - 1][oy + (dy) + 1][ox + (dx) + 1] : s.wy[oy + (dy) + 1][ox + (dx) + 1])
     // mask bits: 0 top, 1 left, 2 corner, 3 top-right
     const int fl = static_cast<int>(mask & 15);
+    if (c == 0 && log2n == 4) {
+        // Intra 16x16 (8.3.3): lane = (column x, rows 4g .. 4g + 3); references straight from the
+        // window (unavailable ones read as 0, as the reference arrays below hold them), DC and the
+        // plane gradients as wave sums -- no reference arrays, one LDS round trip fewer
+        const int mode = tu.mode;
+        const bool at = fl & 1, al = fl & 2, ad = fl & 4;
+        const int x = lane & 15, y0 = (lane >> 4) * 4;
+        const int tx = at ? s.wy[0][1 + x] : 0;
+        // per sample: pv = (mode 3) clip((base + cc y) >> 5), else sel ? left : uni  (uni: DC or top)
+        int uni = tx, base = 0, cc = 0;
+        if (mode == 2) {
+            const int part = lane < 16 ? tx : (lane < 32 && al ? s.wy[1 + (lane - 16)][0] : 0);
+            const int sum = wave_sum_dpp(part);
+            uni = (at && al) ? (sum + 16) >> 5 : ((at || al) ? (sum + 8) >> 4 : 1 << (bd - 1));
+        } else if (mode == 3) {
+            // H = sum (k + 1)(p[8 + k, -1] - p[6 - k, -1]), V likewise down the left column; the
+            // k = 7 terms reach the corner p[-1, -1]
+            const int k = lane & 7;
+            const bool vl = lane >= 8;
+            const int pbi = 7 - k;  // window index of p[6 - k] (0: the corner)
+            const int pa = vl ? (al ? s.wy[9 + k][0] : 0) : (at ? s.wy[0][9 + k] : 0);
+            const int pb = pbi == 0 ? (ad ? s.wy[0][0] : 0) : (vl ? (al ? s.wy[pbi][0] : 0) : (at ? s.wy[0][pbi] : 0));
+            const int term = lane < 16 ? (k + 1) * (pa - pb) : 0;
+            const int H = wave_sum_dpp(lane < 8 ? term : 0), V = wave_sum_dpp(vl ? term : 0);
+            const int a = 16 * ((al ? s.wy[16][0] : 0) + (at ? s.wy[0][16] : 0));
+            const int b = (5 * H + 32) >> 6;
+            cc = (5 * V + 32) >> 6;
+            base = a + b * (x - 7) - 7 * cc + 16;
+        }
+#pragma unroll 1
+        for (int y = y0; y < y0 + 4; y++) {
+            int pv = mode == 1 ? (al ? s.wy[1 + y][0] : 0) : uni;
+            if (mode == 3) pv = clip3(0, maxv, (base + cc * y) >> 5);
+            const int r = cbf ? in.ry[y][x] : 0;
+            s.wy[1 + y][1 + x] = static_cast<uint16_t>(clip3(0, maxv, pv + r));
+        }
+        wave_sync();
+        return;
+    }
     for (int i = lane; i <= ntop; i += 64) {
         int v = 0;
         if (i == 0) v = (fl & 4) ? WIN(-1, -1) : 0;
@@ -1453,52 +1516,56 @@ DEVI void h264_predict_tu(const h2j_tu& tu, uint64_t mask, int mbx, int mby, int
 // unused by chroma), both predicted + reconstructed per lane (8.3.4).
 DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t mask, int bd, H4WaveLds& s,
                                    const H4In& in, int lane) {
+    // lane = (y, x) of both 8x8 blocks; references read straight from the window (unavailable ones
+    // as 0), the DC quarter sums and the plane gradients by cross-lane adds -- no reference arrays
     const int maxv = (1 << bd) - 1;
     const bool cbf_b = (tb.flags & H2J_TU_CBF) != 0, cbf_r = (tr.flags & H2J_TU_CBF) != 0;
     const int fl = static_cast<int>(mask & 15);  // bits: 0 top, 1 left, 2 corner
-    // lanes 0..8: top (corner first), lanes 16..24: left (corner first), both components
-    if (lane <= 8) {
-        const int i = lane;
-        const bool ok = i == 0 ? (fl & 4) != 0 : (fl & 1) != 0;
-        s.top[i] = ok ? s.wc[0][0][i] : 0;
-        s.ftop[i] = ok ? s.wc[1][0][i] : 0;
-    } else if (lane >= 16 && lane <= 24) {
-        const int i = lane - 16;
-        const bool ok = i == 0 ? (fl & 4) != 0 : (fl & 2) != 0;
-        s.left[i] = ok ? s.wc[0][i][0] : 0;
-        s.fleft[i] = ok ? s.wc[1][i][0] : 0;
-    }
-    wave_sync();
+    const bool at = fl & 1, al = fl & 2, ad = fl & 4;
     const int mode = tb.mode;
     const int x = lane & 7, y = lane >> 3;
-    const bool at = fl & 1, al = fl & 2;
-    auto pred = [&](const int* TT, const int* LL) __attribute__((always_inline)) -> int {
-        if (mode == 1) return LL[y];
-        if (mode == 2) return TT[x];
-        if (mode == 3) {
-            int H = 0, V = 0;
+    int pv[2];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                H += (k + 1) * (TT[4 + k] - TT[2 - k]);
-                V += (k + 1) * (LL[4 + k] - LL[2 - k]);
-            }
-            const int a = 16 * (LL[7] + TT[7]), b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
-            return clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+    for (int c = 0; c < 2; c++) {
+        const int tx = at ? s.wc[c][0][1 + x] : 0, ly = al ? s.wc[c][1 + y][0] : 0;
+        if (mode == 1) {
+            pv[c] = ly;
+        } else if (mode == 2) {
+            pv[c] = tx;
+        } else if (mode == 3) {
+            // lanes 0-3: H terms (k + 1)(p[4 + k, -1] - p[2 - k, -1]), lanes 8-11: V terms (k = 3: the corner)
+            const int k = lane & 3;
+            const bool vl = (lane & 8) != 0;
+            const int pa = vl ? (al ? s.wc[c][5 + k][0] : 0) : (at ? s.wc[c][0][5 + k] : 0);
+            const int pbi = 3 - k;
+            const int pb = pbi == 0 ? (ad ? s.wc[c][0][0] : 0) : (vl ? (al ? s.wc[c][pbi][0] : 0) : (at ? s.wc[c][0][pbi] : 0));
+            const int term = (lane & 0x34) == 0 ? (k + 1) * (pa - pb) : 0;  // lanes 0-3 and 8-11
+            const int H = wave_sum_dpp(vl ? 0 : term), V = wave_sum_dpp(vl ? term : 0);
+            const int a = 16 * ((al ? s.wc[c][8][0] : 0) + (at ? s.wc[c][0][8] : 0));
+            const int b = (34 * H + 32) >> 6, cc = (34 * V + 32) >> 6;
+            pv[c] = clip3(0, maxv, (a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+        } else {
+            // DC per 4x4 quarter: lanes 0-7 hold p[x, -1], lanes 8-15 p[-1, x - 8]; after row_shr 1
+            // and 2 adds lane i holds a[i] + a[i-1] + a[i-2] + a[i-3], so lanes 3, 7, 11, 15 hold the
+            // four quarter sums
+            int v = lane < 8 ? tx : (lane < 16 ? (al ? s.wc[c][1 + (lane - 8)][0] : 0) : 0);
+            v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+            v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+            const int t0 = __builtin_amdgcn_readlane(v, 3), t1 = __builtin_amdgcn_readlane(v, 7);
+            const int l0 = __builtin_amdgcn_readlane(v, 11), l1 = __builtin_amdgcn_readlane(v, 15);
+            const int bx = x >> 2, by = y >> 2;
+            const int st4 = bx ? t1 : t0, sl4 = by ? l1 : l0;
+            const int half = 1 << (bd - 1);
+            int d;
+            if (bx == by) d = (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : half));
+            else if (bx) d = at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : half);
+            else d = al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : half);
+            pv[c] = d;
         }
-        const int bx = x >> 2, by = y >> 2;
-        int st4 = 0, sl4 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) { st4 += TT[bx * 4 + k]; sl4 += LL[by * 4 + k]; }
-        if (bx == by) return (at && al) ? (st4 + sl4 + 4) >> 3 : (at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1)));
-        if (bx) return at ? (st4 + 2) >> 2 : (al ? (sl4 + 2) >> 2 : 1 << (bd - 1));
-        return al ? (sl4 + 2) >> 2 : (at ? (st4 + 2) >> 2 : 1 << (bd - 1));
-    };
-#pragma unroll 1
-    for (int c = 0; c < 2; c++) {  // one code path for both components (register pressure)
-        const int pv = pred(c ? s.ftop + 1 : s.top + 1, c ? s.fleft + 1 : s.left + 1);
-        const int r = (c ? cbf_r : cbf_b) ? in.rc[c][y][x] : 0;
-        s.wc[c][y + 1][x + 1] = static_cast<uint16_t>(clip3(0, maxv, pv + r));
     }
+    const int rb = cbf_b ? in.rc[0][y][x] : 0, rr = cbf_r ? in.rc[1][y][x] : 0;
+    s.wc[0][y + 1][x + 1] = static_cast<uint16_t>(clip3(0, maxv, pv[0] + rb));
+    s.wc[1][y + 1][x + 1] = static_cast<uint16_t>(clip3(0, maxv, pv[1] + rr));
     wave_sync();
 }
 
@@ -1510,7 +1577,11 @@ DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t 
 template <typename Pel>
 DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog,
                     uint16_t* line, int band, int nbands) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    // lane: laundered at every macroblock (below) so the compiler recomputes the lane-dependent
+    // LDS / global addresses inside the loop instead of hoisting dozens of them into registers that
+    // then spill -- each scratch reload is a vmcnt(0), which also waits for the next MB's LDS-DMA
+    int lane = threadIdx.x & 63;
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
     constexpr int kSlots = 2 * kAvcWaves;
@@ -1524,6 +1595,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     uint16_t* LY = line;            // [W]: bottom luma row of the MB row above
     uint16_t* LC = line + W;        // [2][Wc]
     const uint32_t ntot = ufl(f.ntu);
+    AVP_DECL;
     // this workgroup's rows: one band of 16 MB rows (one per wave; tall pictures run on several
     // workgroups, see h2j_frame.k1bands) or, unbanded, rows w, w + 16, ...
     const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
@@ -1550,6 +1622,35 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     uint32_t pre_a = rng[4 * ((rbeg + w) * mbw)];  // first record the prefetch assumed
     in_fetch(0, rbeg + w, pre_a, s.in[0]);
     uint16_t cy_corner = 0, cc_corner[2] = {0, 0};  // carried top-left samples (luma, Cb, Cr)
+    // A staged 4-MB group goes out as 64-sample luma / 32-sample chroma rows (whole 64-byte segments
+    // at 8 bits).  Its stores are issued in the next MB's window step, after that MB's inputs have
+    // been waited for: issued at the end of the group's last MB they sat in the vmcnt(0) wait for
+    // the next MB's LDS-DMA (one counter for loads and stores).
+    int fl_g0 = -1, fl_n = 0, fl_gy = 0, fl_cy = 0;
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (fl_g0 < 0) return;
+        const Pel* SY = reinterpret_cast<const Pel*>(s.stage);
+        const Pel* SC = SY + 16 * 64;
+        {  // luma: lane = (row, 16-sample segment)
+            const int r = lane >> 2, sg = lane & 3;
+            if (sg < fl_n) {
+                const uint4* src = reinterpret_cast<const uint4*>(SY + r * 64 + sg * 16);
+                uint4* dst = reinterpret_cast<uint4*>(PY + (fl_gy + r) * sty + fl_g0 * 16 + sg * 16);
+                dst[0] = src[0];
+                if (sizeof(Pel) == 2) dst[1] = src[1];
+            }
+        }
+        {  // chroma: lane = (component, row, 8-sample segment)
+            const int c = lane >> 5, cr = (lane >> 2) & 7, sg = lane & 3;
+            if (sg < fl_n) {
+                const Pel* src = SC + (c * 8 + cr) * 32 + sg * 8;
+                Pel* dst = PC[c] + (fl_cy + cr) * stc + fl_g0 * 8 + sg * 8;
+                if (sizeof(Pel) == 1) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
+                else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+            }
+        }
+        fl_g0 = -1;
+    };
     for (int row = rbeg + w; row < rend; row += kAvcWaves) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
@@ -1560,10 +1661,21 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
         const uint64_t o_xin = o_xl + 4ull * (band - 1) * W, o_xout = o_xl + 4ull * band * W;
         const int gy = row * 16, cy = row * 8;
         for (int mx = 0; mx < mbw; mx++) {
+            asm volatile("" : "+v"(lane));
             const int gx = mx * 16, cx = mx * 8;
             const int cb = row * mbw + mx;
             const uint4 rg = reinterpret_cast<const uint4*>(rng)[cb];
             const uint32_t a = rg.x, ntu = min(rg.z - rg.x, static_cast<uint32_t>(kH4MaxTus));
+            // the wave's next MB and its first record (loaded here, with rg: a load still in flight
+            // when the prefetch DMA is issued makes the compiler wait vmcnt(0) -- for the DMA too --
+            // at its first use)
+            int nx = mx + 1, ny = row;
+            uint32_t na = rg.z;
+            if (nx == mbw) {
+                nx = 0;
+                ny += kAvcWaves;
+                na = ny < mbh ? rng[4 * (ny * mbw)] : 0;
+            }
             if (from_band) {  // the row above belongs to another workgroup: bounded wait on its global word
                 const uint32_t need = static_cast<uint32_t>(min(mx + 2, mbw));
                 if (seen < need) {
@@ -1582,14 +1694,17 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 const uint32_t need = (static_cast<uint32_t>(row) << 16) | static_cast<uint32_t>(min(mx + 2, mbw));
                 if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrK1Row264);
             }
+            AVP_LAP(0);
             // ---- window: the DMA'd inputs, line above from LDS, left column carried
             H4In& in = s.in[cur];
             lds_dma_wait();
+            asm volatile("" ::"v"(na));  // its load retired here, with the DMA wait
             if (pre_a != a) {  // an MB without records before this one: reload the records
                 lds_reads_done();
                 in_recs(a, in);
                 lds_dma_wait();
             }
+            flush();  // the previous group's rows (staged and synced at the end of the previous MB)
             if (from_band) {  // boundary row of the band above (uint16 pairs in dwords, agent-scope loads)
                 int x = -1, e = 0;
                 if (lane < 25) { x = gx - 1 + lane; e = x; }
@@ -1615,13 +1730,6 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 else if (lane < 32) s.wc[(lane - 16) >> 3][((lane - 16) & 7) + 1][0] = 0;
             }
             {  // prefetch the wave's next MB (its records follow this MB's in raster order)
-                int nx = mx + 1, ny = row;
-                uint32_t na = rg.z;
-                if (nx == mbw) {
-                    nx = 0;
-                    ny += kAvcWaves;
-                    na = ny < mbh ? rng[4 * (ny * mbw)] : 0;
-                }
                 if (ny < mbh) {
                     lds_reads_done();  // the other buffer's last reader, the previous MB, has finished
                     in_fetch(nx, ny, na, s.in[cur ^ 1]);
@@ -1634,6 +1742,9 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             cc_corner[0] = s.wc[0][0][8];
             cc_corner[1] = s.wc[1][0][8];
             const bool pcm = ntu > 0 && (in.tus[0].flags & H2J_TU_PCM);
+            AVP_LAP(1);
+            AVP_ADD(6, 1);
+            AVP_ADD(5, ntu);
             if (pcm) {  // samples written by K0: pull them into the window
                 for (int i = lane; i < 256; i += 64) s.wy[(i >> 4) + 1][(i & 15) + 1] = PY[(gy + (i >> 4)) * sty + gx + (i & 15)];
                 for (int i = lane; i < 128; i += 64) {
@@ -1646,12 +1757,16 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                     const h2j_tu tu = in.tus[t];
                     if (tu.c == 1 && tu.log2n == 3 && t + 1 < ntu && in.tus[t + 1].c == 2 && in.tus[t + 1].log2n == 3) {  // Cb + Cr in one pass
                         h264_predict_chroma_pair(tu, in.tus[t + 1], in.mask(t), bdc, s, in, lane);
+                        AVP_LAPK(6);
                         t++;
                         continue;
                     }
                     h264_predict_tu(tu, in.mask(t), mx, row, tu.c ? bdc : bdy, s, in, lane);
+                    // 8: 4x4, 9: 8x8, 10: 16x16 (+ 3 when the mode is DC), 14: lone chroma
+                    AVP_LAPK(tu.c ? 6 : tu.log2n - 2 + (tu.mode == 2 ? 3 : 0));
                 }
             }
+            AVP_LAP(2);
             // ---- stage the macroblock in the wave's 4-MB-wide staging rows; every 4th MB (and the
             // row's last) the group goes out as 64-sample luma / 32-sample chroma rows, whole
             // 64-byte segments at 8 bits instead of 16-byte pieces per MB (a PCM MB's samples,
@@ -1666,29 +1781,11 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 SC[(c * 8 + rr) * 32 + scx + c2] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 1]);
                 SC[(c * 8 + rr) * 32 + scx + c2 + 1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
             }
-            if ((mx & 3) == 3 || mx == mbw - 1) {
-                wave_sync();
-                const Pel* SY = reinterpret_cast<const Pel*>(s.stage);
-                const Pel* SC = SY + 16 * 64;
-                const int g0 = mx & ~3, nmb = mx - g0 + 1;
-                {  // luma: lane = (row, 16-sample segment)
-                    const int r = lane >> 2, sg = lane & 3;
-                    if (sg < nmb) {
-                        const uint4* src = reinterpret_cast<const uint4*>(SY + r * 64 + sg * 16);
-                        uint4* dst = reinterpret_cast<uint4*>(PY + (gy + r) * sty + g0 * 16 + sg * 16);
-                        dst[0] = src[0];
-                        if (sizeof(Pel) == 2) dst[1] = src[1];
-                    }
-                }
-                {  // chroma: lane = (component, row, 8-sample segment)
-                    const int c = lane >> 5, cr = (lane >> 2) & 7, sg = lane & 3;
-                    if (sg < nmb) {
-                        const Pel* src = SC + (c * 8 + cr) * 32 + sg * 8;
-                        Pel* dst = PC[c] + (cy + cr) * stc + g0 * 8 + sg * 8;
-                        if (sizeof(Pel) == 1) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
-                        else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-                    }
-                }
+            if ((mx & 3) == 3 || mx == mbw - 1) {  // the group is complete: stored in the next MB's window step
+                fl_g0 = mx & ~3;
+                fl_n = mx - fl_g0 + 1;
+                fl_gy = gy;
+                fl_cy = cy;
             }
             // bottom row for the MB row below; right column becomes the next MB's left column
             if (to_band) {  // hand the bottom row to the band below: data, wait for completion, then progress
@@ -1724,8 +1821,11 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(row) + 1) << 16) | static_cast<uint32_t>(mx + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cur ^= 1;
+            AVP_LAP(3);
         }
     }
+    flush();  // the wave's last group (synced at the end of its last MB)
+    AVP_FLUSH();
 }
 
 // H.264 K1 for MBAFF frames (h2j_frame.mbaff): macroblock pairs, wave w walking pair rows w, w + 16,
@@ -3286,7 +3386,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
     const int npairs = (rend - rbeg + 1) >> 1;
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
     if (wv >= npairs) return;
-    PROF_DECL;
+    DBP_DECL;
     // filter lanes of a half: 0-15 luma lines, 16-23 Cb, 24-31 Cr
     const bool luma_lane = hl < 16, chroma = !luma_lane;
     const int cc = (hl >> 3) & 1, ck = hl & 7;
@@ -3339,7 +3439,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     if (seen < need) seen = wait_progress(above, need, dev_error_word(arena, f), kDevErrDbRow264);
                 }
             }
-            PROF_LAP(0);
+            DBP_LAP(0);
             if (live) {
                 // window: the MB body (prefetched), the rows above (line buffer), left columns carried
                 {
@@ -3383,7 +3483,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 if (ny < mbh) db264_fetch2<Pel>(PY, PC, sty, stc, nx, ny, pf, hl);
             }
             wave_sync();
-            PROF_LAP(1);
+            DBP_LAP(1);
             const uint32_t cur = ninfo;
             if (live) {  // parameters of the half's next MB
                 int nx = mx + 1, ny = row;
@@ -3409,7 +3509,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
             const int beo = static_cast<int8_t>(s0 & 0xFF), tco = static_cast<int8_t>((s0 >> 8) & 0xFF);
             const int cq0 = static_cast<int8_t>((s1 >> 16) & 0xFF), cq1 = static_cast<int8_t>(s1 >> 24);
             const int saddr = static_cast<int>(s2), tsaddr = static_cast<int>(ts2);
-            PROF_LAP(2);
+            DBP_LAP(2);
             if (live && (mf & 4) && dd != 1) {
                 // thresholds of the lane's component, per lane (no cross-lane traffic): the left and
                 // top MB edges and the internal edges (8.7.2.2; chroma QPs through Table 8-15)
@@ -3451,7 +3551,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     for (int i = 1; i < 19; i++)
                         if (luma_lane || (i >= 3 && i <= 8)) dst[i * stp] = static_cast<uint16_t>(v[i]);
                     wave_sync();
-                    PROF_LAPK(dir * 4);
+                    DBP_LAPK(dir * 4);
                 }
             }
             if (live) {
@@ -3592,11 +3692,11 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
             if (lane == 0 && two && s >= kDbLag)
                 __hip_atomic_store(mine, ((static_cast<uint32_t>(r0) + 2) << 16) | static_cast<uint32_t>(s - kDbLag + 1),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            PROF_LAP(3);
-            PROF_ADD(6, 1 + (two && s >= kDbLag && s - kDbLag < mbw ? 1 : 0) - (s < mbw ? 0 : 1));
+            DBP_LAP(3);
+            DBP_ADD(6, 1 + (two && s >= kDbLag && s - kDbLag < mbw ? 1 : 0) - (s < mbw ? 0 : 1));
         }
     }
-    PROF_FLUSH();
+    DBP_FLUSH();
 }
 
 // line_w: the widest picture whose line buffer the launch's LDS holds (wider: global memory)

@@ -35,6 +35,14 @@ for path in files:
     tot = sum(v[0:4]) + sum(v[8:16])
     ntu, nctb = v[5], v[6]
     print(f"{os.path.basename(path)}: {n} frames, K1 {st['recon_ms']:.2f} ms, TUs {ntu}, CTBs {nctb}")
+    if path.endswith((".h264", ".264")) and os.environ.get("K1PROF_AVCK1"):
+        # H.264 K1 (build with PROFDEFS="-DH2J_PROF -DH2J_PROF_AVCK1"), per macroblock
+        print(f"  MBs {nctb}, TUs {ntu}")
+        for i, nm in enumerate(["wait", "window", "tb-setup", "store"]):
+            print(f"  {nm:10s} {v[i] / max(1, nctb):10.0f} cyc/MB  {100 * v[i] / tot:5.1f}%")
+        for k, nm in enumerate(["I4x4", "I8x8", "I16x16", "I4x4 DC", "I8x8 DC", "I16x16 DC", "chroma", "-"]):
+            print(f"  {nm:10s} {v[8 + k] / max(1, nctb):10.0f} cyc/MB  {100 * v[8 + k] / tot:5.1f}%")
+        continue
     if path.endswith((".h264", ".264")):
         # H.264: the counters are the K2 deblock wave's (h264_db_rows), per macroblock
         names = ["wait", "window", "params", "store"]
