@@ -256,7 +256,10 @@ constexpr int kK0Tus = 62;  // H.264 TUs per K0 wave (records held one per lane)
 static_assert(kK0Tus >= 1 && kK0Tus <= 62, "K0 records per wave: 62 at most");
 constexpr int kK0TusHevc = 62;  // HEVC: 62 records + the two neighbours of the range in lanes 62, 63
 constexpr int kK1WavesWide = 16;  // HEVC K1, launches of <= 128 pictures: waves per group (one group per CU)
-constexpr int kAvcWaves = 16;  // H.264 K1: waves (macroblock rows in flight) per picture
+constexpr int kAvcWaves = 16;  // waves of the MBAFF / mixed-batch K1 workgroups (macroblock rows in flight)
+// H.264 K1 (h2j_k1_recon_h264): 8-wave workgroups, two per CU (LDS), so one picture's last row
+// round -- rows left over after the waves' full rounds -- overlaps the other workgroup's work
+constexpr int kAvcK1Waves = 8;
 
 struct K0Lds {    // H.264
     int blk[32 * 32];  // up to 4 Intra16x16 MBs' levels ([G][16][16], h264_i16_group)
@@ -1574,7 +1577,7 @@ DEVI void h264_predict_chroma_pair(const h2j_tu& tb, const h2j_tu& tr, uint64_t 
 // MB's records start where this MB's end; no registers are held across the MB), the line above
 // from a per-picture LDS line buffer (each row leaves its unfiltered bottom samples there; the
 // top-left corner is carried), the prediction chain in the LDS window, one store of the MB.
-template <typename Pel>
+template <typename Pel, int NW>
 DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveLds& s, uint32_t* prog,
                     uint16_t* line, int band, int nbands) {
     const int w = threadIdx.x >> 6;
@@ -1584,7 +1587,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     int lane = threadIdx.x & 63;
     const uint64_t* masks = reinterpret_cast<const uint64_t*>(arena + ufl64(f.aux));
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(arena + ufl64(f.ctbrng));
-    constexpr int kSlots = 2 * kAvcWaves;
+    constexpr int kSlots = 2 * NW;
     const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h);
     const int W = ufl(f.width), Wc = W >> 1;
     const int bdy = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
@@ -1651,7 +1654,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
         }
         fl_g0 = -1;
     };
-    for (int row = rbeg + w; row < rend; row += kAvcWaves) {
+    for (int row = rbeg + w; row < rend; row += NW) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
         uint32_t* mine = prog + row % kSlots;
         uint32_t seen = 0;
@@ -1673,7 +1676,7 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             uint32_t na = rg.z;
             if (nx == mbw) {
                 nx = 0;
-                ny += kAvcWaves;
+                ny += NW;
                 na = ny < mbh ? rng[4 * (ny * mbw)] : 0;
             }
             if (from_band) {  // the row above belongs to another workgroup: bounded wait on its global word
@@ -2811,24 +2814,24 @@ __global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame*
 
 // grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
 // picture in order, so a band only ever waits on an earlier workgroup)
-__global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
-                                                                  const h2j_ctb* ctbs, uint8_t* arena, const uint32_t* map) {
+__global__ void __launch_bounds__(64 * kAvcK1Waves, 4) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
+                                                                    const h2j_ctb* ctbs, uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t h4lds[];
     H4WaveLds* wl = reinterpret_cast<H4WaveLds*>(h4lds);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves);
-    uint16_t* line = reinterpret_cast<uint16_t*>(h4lds + sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(h4lds + sizeof(H4WaveLds) * kAvcK1Waves);
+    uint16_t* line = reinterpret_cast<uint16_t*>(h4lds + sizeof(H4WaveLds) * kAvcK1Waves + 2 * kAvcK1Waves * 4);
     const uint32_t me = map[blockIdx.x];
     const h2j_frame& f = frames[me >> 8];
     const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264) return;
     const int nbands = ufl(f.k1bands);
-    if (threadIdx.x < 2 * kAvcWaves) prog[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kAvcK1Waves) prog[threadIdx.x] = 0;
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
     const h2j_tu* T = tus + ufl(f.tu);
     if (ufl(f.mbaff)) return;  // h2j_k1_recon_h264_mbaff
-    if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
-    else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
+    if (f.bit_depth == 8) h264_rows<uint8_t, kAvcK1Waves>(f, T, arena, s, prog, line, band, nbands);
+    else h264_rows<uint16_t, kAvcK1Waves>(f, T, arena, s, prog, line, band, nbands);
 }
 
 // MBAFF frames (h2j_frame.mbaff) in a kernel of their own, so the progressive kernel keeps its
@@ -2960,8 +2963,8 @@ __global__ void __launch_bounds__(64 * kAvcWaves) h2j_k1_recon_any(const h2j_fra
             __syncthreads();
         H4WaveLds& s = wl[threadIdx.x >> 6];
         if (ufl(f.mbaff)) return;  // h2j_k1_recon_h264_mbaff
-        if (f.bit_depth == 8) h264_rows<uint8_t>(f, T, arena, s, prog, line, band, nbands);
-        else h264_rows<uint16_t>(f, T, arena, s, prog, line, band, nbands);
+        if (f.bit_depth == 8) h264_rows<uint8_t, kAvcWaves>(f, T, arena, s, prog, line, band, nbands);
+        else h264_rows<uint16_t, kAvcWaves>(f, T, arena, s, prog, line, band, nbands);
     }
 }
 
@@ -3440,6 +3443,10 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 }
             }
             DBP_LAP(0);
+            // this MB's parameters (loaded one MB ahead) are taken before the next MB's loads are
+            // issued: consumed after them, the compiler's vmcnt wait for them covered those loads too
+            const uint32_t cur = ninfo;
+            asm volatile("" ::"v"(cur));  // (the copy's wait here, not where ninfo's register is reloaded)
             if (live) {
                 // window: the MB body (prefetched), the rows above (line buffer), left columns carried
                 {
@@ -3477,19 +3484,16 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // 2 comps x 2 rows x 8 columns
                     w.c[c2][cr][k2 + 2] = LC[(c2 * 2 + cr) * cw + mx * 8 + k2];
                 }
-                // prefetch the half's next MB (its next row: two pairs on)
+                // prefetch the half's next MB (its next row: two pairs on) and its parameters
                 int nx = mx + 1, ny = row;
                 if (nx == mbw) { nx = 0; ny += 2 * kDbPairWaves; }
-                if (ny < mbh) db264_fetch2<Pel>(PY, PC, sty, stc, nx, ny, pf, hl);
+                if (ny < mbh) {
+                    db264_fetch2<Pel>(PY, PC, sty, stc, nx, ny, pf, hl);
+                    ninfo = db264_info_raw(mbs, mbw, nx, ny, hl);
+                }
             }
             wave_sync();
             DBP_LAP(1);
-            const uint32_t cur = ninfo;
-            if (live) {  // parameters of the half's next MB
-                int nx = mx + 1, ny = row;
-                if (nx == mbw) { nx = 0; ny += 2 * kDbPairWaves; }
-                if (ny < mbh) ninfo = db264_info_raw(mbs, mbw, nx, ny, hl);
-            }
             auto pick = [&](int k) __attribute__((always_inline)) {
                 const uint32_t a = __builtin_amdgcn_readlane(cur, k), b = __builtin_amdgcn_readlane(cur, 32 + k);
                 return h ? b : a;
@@ -3502,9 +3506,14 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
             uint32_t s0, s1, s2, ts2 = ~0u;
             const uint32_t* TBS = reinterpret_cast<const uint32_t*>(TB.sl);
             const uint32_t* GS = reinterpret_cast<const uint32_t*>(slices);
+            // (slices past the LDS copy: global loads, waited inside their branch -- a wait at the
+            // merged first use would also wait for the next MB's prefetch loads)
             if (csl < kDbSlices) { s0 = TBS[3 * csl]; s1 = TBS[3 * csl + 1]; s2 = TBS[3 * csl + 2]; }
-            else { s0 = GS[3 * csl]; s1 = GS[3 * csl + 1]; s2 = GS[3 * csl + 2]; }
-            if (row > 0) ts2 = tsl < kDbSlices ? TBS[3 * tsl + 2] : GS[3 * tsl + 2];
+            else { s0 = GS[3 * csl]; s1 = GS[3 * csl + 1]; s2 = GS[3 * csl + 2]; asm volatile("" ::"v"(s0), "v"(s1), "v"(s2)); }
+            if (row > 0) {
+                if (tsl < kDbSlices) ts2 = TBS[3 * tsl + 2];
+                else { ts2 = GS[3 * tsl + 2]; asm volatile("" ::"v"(ts2)); }
+            }
             const int dd = static_cast<int>((s1 >> 8) & 0xFF);
             const int beo = static_cast<int8_t>(s0 & 0xFF), tco = static_cast<int8_t>((s0 >> 8) & 0xFF);
             const int cq0 = static_cast<int8_t>((s1 >> 16) & 0xFF), cq1 = static_cast<int8_t>(s1 >> 24);
@@ -4770,7 +4779,8 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     const bool wide = b->nframes <= 128;
     const int pels = b->hevc_pels;  // bit 0: 8-bit HEVC pictures, bit 1: high bit depth
     const int kinds = ((pels & 1) ? 1 : 0) + ((pels & 2) ? 1 : 0) + (b->has_h264 && b->k1wgs > 0 ? 1 : 0);
-    const size_t lds264 = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4 + 4 * static_cast<size_t>(b->max_w);
+    const size_t lds264 = sizeof(H4WaveLds) * kAvcK1Waves + 2 * kAvcK1Waves * 4 + 4 * static_cast<size_t>(b->max_w);
+    const size_t lds264any = sizeof(H4WaveLds) * kAvcWaves + 2 * kAvcWaves * 4 + 4 * static_cast<size_t>(b->max_w);
     static bool attr = false;
     if (!attr) {
         const void* fns[] = {reinterpret_cast<const void*>(h2j_k1_recon_hevc<uint8_t, kK1WavesWide>),
@@ -4792,7 +4802,7 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     const size_t wbytes = k1_fixed_lds(kK1WavesWide) + line_bytes;
     // merged launch: an HEVC picture workgroup runs the pool's job loop with P = 1 (hevc_pool_jobs)
     const size_t pool1 = k1_pool_lds(1, (b->max_h + 15) / 16, 2 * b->max_w + 192);
-    const size_t lds_any = std::max(std::max(pool1, lds264), wbytes);
+    const size_t lds_any = std::max(std::max(pool1, lds264any), wbytes);
     // one launch for every kind of picture (unless the widest picture's line buffers would not
     // fit one workgroup's LDS: then the per-kind launches below)
     if (!wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
@@ -4806,7 +4816,7 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     if (ax) {
         (void)hipEventRecord(ax->fork, s);
         (void)hipStreamWaitEvent(ax->s2, ax->fork, 0);
-        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, ax->s2, b->frames, b->tus,
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcK1Waves), lds264, ax->s2, b->frames, b->tus,
                            b->ctbs, b->arena, b->k1map);
         const int r = check(hipGetLastError(), "h2j_k1_recon_h264");
         (void)hipEventRecord(ax->join, ax->s2);
@@ -4854,7 +4864,7 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     if (b->has_h264 && !ax) {
         // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
         if (b->k1wgs > 0)
-            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcWaves), lds264, s, b->frames, b->tus,
+            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcK1Waves), lds264, s, b->frames, b->tus,
                                b->ctbs, b->arena, b->k1map);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
