@@ -518,19 +518,30 @@ private:
     int nc_luma(int blk);
     int nc_chroma(const Mb& m, int c, int b4);
     void decode_mb_cavlc();
-    Mb* mb_in_slice(int x, int y) {
+    __attribute__((always_inline)) Mb* mb_in_slice(int x, int y) {
         if (x < 0 || y < 0 || x >= mbw_ || y >= mbh_) return nullptr;
         Mb* m = &mb_[y * mbw_ + x];
         return m->slice == cur_slice_ ? m : nullptr;
     }
-    Mb* nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW);
+    // 6.4.12 (see nb_loc_mbaff): frames and PAFF field pairs inline (every neighbour query of a
+    // macroblock goes through here: out of line it cost ~9 % of the progressive parse), MBAFF out
+    // of line
+    __attribute__((always_inline)) Mb* nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
+        if (__builtin_expect(mbaff_ && !paff_, 0)) return nb_loc_mbaff(xN, yN, maxW, maxH, xW, yW);
+        if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return nullptr;
+        *xW = (xN + maxW) & (maxW - 1);  // maxW, maxH: 8 or 16; xN, yN >= -1
+        *yW = (yN + maxH) & (maxH - 1);
+        if (xN >= 0 && xN <= maxW - 1 && yN >= 0) return &mb_[mby_ * mbw_ + mbx_];
+        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? (paff_ ? -2 : -1) : 0));
+    }
+    __attribute__((noinline)) Mb* nb_loc_mbaff(int xN, int yN, int maxW, int maxH, int* xW, int* yW);
     // MB covering luma location (-1, 0) / (0, -1) / (16, -1) / (-1, -1) (6.4.11.1)
-    Mb* nb(int dx, int dy) {
+    __attribute__((always_inline)) Mb* nb(int dx, int dy) {
         int xW, yW;
         return nb_loc(dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
     }
     // the 4x4 luma block covering location (4 bx, 4 by) relative to the MB (6.4.11.4)
-    Mb* nb_blk(int bx, int by, int* nblk) {
+    __attribute__((always_inline)) Mb* nb_blk(int bx, int by, int* nblk) {
         int xW, yW;
         Mb* m = nb_loc(bx * 4, by * 4, 16, 16, &xW, &yW);
         *nblk = m ? kBlkOf[yW >> 2][xW >> 2] : 0;
@@ -556,7 +567,15 @@ private:
     int cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const;
     // residual_block_cabac (7.3.5.3.3): number of non-zero levels (0: coded_block_flag 0);
     // scan indices in pos[], levels in lvl[]
-    int residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl);
+    // FLD: field macroblock (MBAFF / PAFF) context sets; a compile-time choice, so the frame
+    // decoder keeps constant context offsets in its bin loops (r04r: the runtime choice cost the
+    // progressive parse ~12 % on the box CPU)
+    template <bool FLD>
+    int residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl);
+    int residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl) {
+        return mb_[mby_ * mbw_ + mbx_].field ? residual_block_t<true>(cat, cbf_inc, max_num, pos, lvl)
+                                             : residual_block_t<false>(cat, cbf_inc, max_num, pos, lvl);
+    }
     void decode_mb();
     void emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos, bool pcm);
     // sparse record: entries already (pos << 16) | uint16 level
@@ -569,7 +588,7 @@ private:
 // neighbour next to a field pair is that pair's bottom field MB, middle row (the picture sample
 // above-left: FFmpeg h264_slice.c fill_decode_neighbors, topleft_xy += mb_stride).  Every
 // neighbour sample is then the picture sample next to the MB in its own field / frame view.
-Mb* H264Parser::nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
+Mb* H264Parser::nb_loc_mbaff(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
     Mb* cur = &mb_[mby_ * mbw_ + mbx_];
     if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return nullptr;
     *xW = (xN + maxW) % maxW;
@@ -675,7 +694,8 @@ int H264Parser::cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const {
     return 0;
 }
 
-int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl) {
+template <bool FLD>
+int H264Parser::residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl) {
     static const int kCbfOff[5] = {0, 4, 8, 12, 16};
     static const int kSigOff[6] = {0, 15, 29, 44, 47, 0};
     static const int kAbsOff[6] = {0, 10, 20, 30, 39, 0};
@@ -689,11 +709,10 @@ int H264Parser::residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, 
     bool last_found = false;
     // field macroblocks (MBAFF): significance / last contexts at 277 / 338 (436 / 451 with the
     // field ctxIdxInc table for 8x8 blocks) instead of 105 / 166 (402 / 417), 9.3.3.1.3
-    const bool fld = mb_[mby_ * mbw_ + mbx_].field != 0;
-    const int sig0 = fld ? 277 : 105, last0 = fld ? 338 : 166;
+    constexpr int sig0 = FLD ? 277 : 105, last0 = FLD ? 338 : 166;
     if (cat == 5) {
-        const uint8_t* sigt = fld ? kSig8x8Fld : kSig8x8;
-        const int s8 = fld ? 436 : 402, l8 = fld ? 451 : 417;
+        const uint8_t* const sigt = FLD ? kSig8x8Fld : kSig8x8;
+        constexpr int s8 = FLD ? 436 : 402, l8 = FLD ? 451 : 417;
         for (int i = 0; i < max_num - 1; i++)
             if (cc.decision(ctx[s8 + sigt[i]])) {
                 pos[nsig++] = static_cast<uint8_t>(i);

@@ -1,0 +1,4 @@
+# r04s: H.264 parse speed on the box's host CPU: f76aaa6 (before MBAFF / PAFF) vs HEAD (neighbour
+# derivation inline again for frames), both with ROCm clang as the product builds it.
+cd $GRAFT_REPO_ROOT
+SETS="bench264" BINS="pb_old pb_new pb_tmpl" REPS=4 bash tools/gpu_parse_ab.sh
