@@ -539,7 +539,7 @@ private:
         int ye = std::min((y0 + n) >> 2, mh), xe = std::min((x0 + n) >> 2, mw);
         for (int y = y0 >> 2; y < ye; y++) std::memset(&qp_[y * mw + (x0 >> 2)], qp & 0xFF, static_cast<size_t>(xe - (x0 >> 2)));
     }
-    int dec(int ctx) { return cc_.decision(ctx_[ctx]); }
+    __attribute__((always_inline)) int dec(int ctx) { return cc_.decision(ctx_[ctx]); }  // (inline: box CPU hevc1080 3.40 -> 3.34 ms, r04u)
 };
 
 int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, const SliceHdr* prev) {
