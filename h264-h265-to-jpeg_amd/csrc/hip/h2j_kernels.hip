@@ -3604,52 +3604,86 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 lqp = mqp;
                 lsaddr = saddr;
                 // write back (the rules of h264_db_rows): rows 12..15 of MB (x, y - 1), rows of
-                // MB (x - 1, y), and on the row's last MB its own rows; staged 4 MBs wide
+                // MB (x - 1, y), and on the row's last MB its own rows; staged G MBs wide: 8 at
+                // 8 bits (128-byte luma / 64-byte chroma rows: whole lines, where 4-MB groups left
+                // 32-byte chroma halves that cost 0.2x the picture in extra HBM writes, r04o), 4 at
+                // 16 bits (the staging buffers hold either)
+                constexpr int G = sizeof(Pel) == 1 ? 8 : 4, LW = 16 * G, CW = 8 * G;
+                constexpr int SS = 16 / static_cast<int>(sizeof(Pel));  // samples per 16-byte piece
                 const bool last_row = row == mbh - 1, last = mx == mbw - 1;
                 const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
-                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][64] | chroma [2][2][32]
-                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][64] | chroma [2][8][32]
+                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][LW] | chroma [2][2][CW]
+                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][LW] | chroma [2][8][CW]
+                Pel* const SAc = SA + 4 * LW;
+                Pel* const SBc = SB + 16 * LW;
+                // 16-byte chroma pieces: one store when the row is 16-byte aligned (at 8 bits the
+                // chroma width may be an odd multiple of 8)
+                auto cput16 = [&](Pel* d, const Pel* q) __attribute__((always_inline)) {
+                    if (sizeof(Pel) == 2 || (stc & 15) == 0) {
+                        db264_copy<Pel, SS>(d, q);
+                    } else {
+                        db264_copy<Pel, 8>(d, q);
+                        db264_copy<Pel, 8>(d + 8, q + 8);
+                    }
+                };
                 if (row > 0) {
                     if (hl < 16) {
                         const int tr = hl >> 2, c4 = (hl & 3) * 4;
-                        db_st4<Pel>(SA + tr * 64 + (mx & 3) * 16 + c4, db_ld4a8(&w.y[tr][c4 + 4]));
+                        db_st4<Pel>(SA + tr * LW + (mx % G) * 16 + c4, db_ld4a8(&w.y[tr][c4 + 4]));
                     } else if (hl < 24) {  // chroma rows 6..7
                         const int k = hl - 16, c2 = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
-                        db_st4<Pel>(SA + 256 + (c2 * 2 + cr) * 32 + (mx & 3) * 8 + c4, db_ld4a4(&w.c[c2][cr][c4 + 2]));
+                        db_st4<Pel>(SAc + (c2 * 2 + cr) * CW + (mx % G) * 8 + c4, db_ld4a4(&w.c[c2][cr][c4 + 2]));
                     }
-                    if ((mx & 3) == 3 || last) {  // the group's rows 12..15 out
+                    if (mx % G == G - 1 || last) {  // the group's rows 12..15 / chroma 6..7 out
                         wave_sync();
-                        const int g0 = mx & ~3, nmb = mx - g0 + 1;
-                        const int tr = hl >> 3, sg = hl & 7;  // luma: 4 rows x 8 segments of 8
-                        if (sg < 2 * nmb) db264_copy<Pel, 8>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * 8, SA + tr * 64 + sg * 8);
-                        const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;  // chroma: 2 x 2 rows x 8 segments of 4
-                        if (cs < 2 * nmb)
-                            db264_copy<Pel, 4>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * 4, SA + 256 + (c2 * 2 + cr) * 32 + cs * 4);
+                        const int g0 = mx - mx % G, nmb = mx - g0 + 1;
+                        {  // luma: 4 rows x 8 pieces of 16 bytes
+                            const int tr = hl >> 3, sg = hl & 7;
+                            if (sg * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS, SA + tr * LW + sg * SS);
+                        }
+                        {  // chroma: 2 comps x 2 rows x 8 pieces of 8 bytes
+                            constexpr int S8 = 8 / static_cast<int>(sizeof(Pel));
+                            const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;
+                            if (cs * S8 < nmb * 8)
+                                db264_copy<Pel, S8>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8, SAc + (c2 * 2 + cr) * CW + cs * S8);
+                        }
                     }
                 }
                 auto flush_b = [&](int g0, int nmb) __attribute__((always_inline)) {
                     wave_sync();
-                    const int r = hl >> 1, sp = (hl & 1) * 2;  // luma: 16 rows x 2 x 2 segments of 16
-                    if (r < nr) {
-                        if (sp < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sp * 16, SB + r * 64 + sp * 16);
-                        if (sp + 1 < nmb) db264_copy<Pel, 16>(PY + (row * 16 + r) * sty + g0 * 16 + sp * 16 + 16, SB + r * 64 + sp * 16 + 16);
+                    {  // luma: 16 rows x 2 halves of 4 pieces of 16 bytes
+                        const int r = hl >> 1;
+                        if (r < nr) {
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                const int sp = (hl & 1) * 4 + k;
+                                if (sp * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 + r) * sty + g0 * 16 + sp * SS, SB + r * LW + sp * SS);
+                            }
+                        }
                     }
-                    const int c2 = hl >> 4, cr = (hl >> 1) & 7;  // chroma: 2 comps x 8 rows x 2 x 2 segments of 8
-                    if (cr < ncr) {
-                        Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8 + sp * 8;
-                        const Pel* q = SB + 1024 + (c2 * 8 + cr) * 32 + sp * 8;
-                        if (sp < nmb) db264_copy<Pel, 8>(d, q);
-                        if (sp + 1 < nmb) db264_copy<Pel, 8>(d + 8, q + 8);
+                    {  // chroma: 2 comps x 8 rows x 2 halves of 2 pieces of 16 bytes
+                        constexpr int MPS = SS / 8;  // MBs per piece
+                        const int c2 = hl >> 4, cr = (hl >> 1) & 7;
+                        if (cr < ncr) {
+                            Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8;
+                            const Pel* q = SBc + (c2 * 8 + cr) * CW;
+#pragma unroll
+                            for (int k = 0; k < 2; k++) {
+                                const int sg = (hl & 1) * 2 + k;
+                                if ((sg + 1) * MPS <= nmb) cput16(d + sg * SS, q + sg * SS);
+                                else if (sg * MPS < nmb) db264_copy<Pel, 8>(d + sg * SS, q + sg * SS);  // 8 bits: an odd last MB
+                            }
+                        }
                     }
                 };
                 if (mx > 0) {  // the previous MB: columns 0..11 saved in py, 12..15 in the window
-                    const int sx = ((mx - 1) & 3) * 16;
+                    const int sx = ((mx - 1) % G) * 16;
                     {
                         const int r = hl >> 1, c8 = (hl & 1) * 8;
                         if (r < nr) {
                             const uint2 a = db_ld4a8(&w.py[r][c8]);
                             const uint2 b = c8 ? db_ld4a8(&w.y[r + 4][0]) : db_ld4a8(&w.py[r][4]);
-                            db_st8<Pel>(SB + r * 64 + sx + c8, a, b);
+                            db_st8<Pel>(SB + r * LW + sx + c8, a, b);
                         }
                     }
                     {
@@ -3657,10 +3691,10 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                         if (cr < ncr) {  // chroma column 7 sits in the window
                             uint2 a = db_ld4a8(&w.pc[c2][cr][c4]);
                             if (c4) a.y = (a.y & 0xFFFFu) | (static_cast<uint32_t>(w.c[c2][cr + 2][1]) << 16);
-                            db_st4<Pel>(SB + 1024 + (c2 * 8 + cr) * 32 + (sx >> 1) + c4, a);
+                            db_st4<Pel>(SBc + (c2 * 8 + cr) * CW + (sx >> 1) + c4, a);
                         }
                     }
-                    if (((mx - 1) & 3) == 3) flush_b(mx - 4, 4);
+                    if ((mx - 1) % G == G - 1) flush_b(mx - G, G);
                 }
                 // this MB's columns 0..11 / chroma 0..7 wait for the next MB (in-order LDS)
                 {
@@ -3671,16 +3705,16 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     *reinterpret_cast<uint2*>(&w.pc[c2][cr][c4]) = db_ld4a4(&w.c[c2][cr + 2][c4 + 2]);
                 }
                 if (last) {  // the row's last MB: its rows are final now
-                    const int sx = (mx & 3) * 16;
+                    const int sx = (mx % G) * 16;
                     {
                         const int r = hl >> 1, c8 = (hl & 1) * 8;
-                        if (r < nr) db_st8<Pel>(SB + r * 64 + sx + c8, db_ld4a8(&w.y[r + 4][c8 + 4]), db_ld4a8(&w.y[r + 4][c8 + 8]));
+                        if (r < nr) db_st8<Pel>(SB + r * LW + sx + c8, db_ld4a8(&w.y[r + 4][c8 + 4]), db_ld4a8(&w.y[r + 4][c8 + 8]));
                     }
                     {
                         const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
-                        if (cr < ncr) db_st4<Pel>(SB + 1024 + (c2 * 8 + cr) * 32 + (sx >> 1) + c4, db_ld4a4(&w.c[c2][cr + 2][c4 + 2]));
+                        if (cr < ncr) db_st4<Pel>(SBc + (c2 * 8 + cr) * CW + (sx >> 1) + c4, db_ld4a4(&w.c[c2][cr + 2][c4 + 2]));
                     }
-                    flush_b(mx & ~3, (mx & 3) + 1);
+                    flush_b(mx - mx % G, mx % G + 1);
                 }
                 // line buffer for the row below: the MB's bottom rows (columns final so far) and the
                 // previous MB's last columns, which this MB's left edge has just finished
