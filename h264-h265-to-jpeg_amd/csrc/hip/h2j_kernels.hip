@@ -1345,7 +1345,7 @@ static_assert(offsetof(H4In, rc) == offsetof(H4In, ry) + 512 && offsetof(H4In, r
               "one 48-lane dwordx4 DMA fills ry then rc");
 struct alignas(16) H4WaveLds {
     H4In in[2];     // ping-pong: the MB being reconstructed / the next one
-    alignas(16) uint8_t stage[3 * 16 * 64];  // reconstructed MBs (Pel): luma [16][64] (4 MBs), chroma [2][8][64] (8 MBs) at 8 bits / [2][8][32] (4 MBs) above
+    alignas(16) uint8_t stage[3 * 16 * 64];  // reconstructed MBs (Pel): luma [16][16 G] + chroma [2][8][8 G], G = 8 MBs at 8 bits, 4 above
     uint16_t wy[17][25];
     uint16_t wc[2][9][9];
     int top[40];    // top[0] = corner, top[1 + i] = p[i, -1]
@@ -1629,40 +1629,43 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     // at 8 bits).  Its stores are issued in the next MB's window step, after that MB's inputs have
     // been waited for: issued at the end of the group's last MB they sat in the vmcnt(0) wait for
     // the next MB's LDS-DMA (one counter for loads and stores).
-    // Chroma groups are 8 MBs at 8 bits (64-byte chroma rows, as luma's 4-MB groups): 32-byte
-    // halves of a line written at different times left K1's WRITE at 1.39x the picture (r04m)
-    constexpr int CG = sizeof(Pel) == 1 ? 8 : 4, CW = 8 * CG;  // MBs per chroma group, staging row width
-    int fl_g0 = -1, fl_n = 0, fl_gy = 0, flc_g0 = -1, flc_n = 0, flc_cy = 0;
+    // Groups are 8 MBs at 8 bits (128-byte luma / 64-byte chroma rows: whole lines -- 32-byte
+    // halves of a line written at different times left K1's WRITE at 1.39x the picture, r04m) and
+    // 4 MBs at 16 bits (the staging tile holds either)
+    constexpr int G = sizeof(Pel) == 1 ? 8 : 4, LW = 16 * G, CW = 8 * G;  // MBs per group, row widths
+    constexpr int SS = 16 / static_cast<int>(sizeof(Pel));                 // samples per 16-byte piece
+    int fl_g0 = -1, fl_n = 0, fl_gy = 0, fl_cy = 0;
     auto flush = [&]() __attribute__((always_inline)) {
+        if (fl_g0 < 0) return;
         const Pel* SY = reinterpret_cast<const Pel*>(s.stage);
-        const Pel* SC = SY + 16 * 64;  // [2][8][CW]
-        if (fl_g0 >= 0) {  // luma: lane = (row, 16-sample segment)
-            const int r = lane >> 2, sg = lane & 3;
-            if (sg < fl_n) {
-                const uint4* src = reinterpret_cast<const uint4*>(SY + r * 64 + sg * 16);
-                uint4* dst = reinterpret_cast<uint4*>(PY + (fl_gy + r) * sty + fl_g0 * 16 + sg * 16);
-                dst[0] = src[0];
-                if (sizeof(Pel) == 2) dst[1] = src[1];
+        const Pel* SC = SY + 16 * LW;  // [2][8][CW]
+        {  // luma: lane = (row, 2 pieces of 16 bytes)
+            const int r = lane >> 2;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int sp = (lane & 3) * 2 + k;
+                if (sp * SS < fl_n * 16)
+                    *reinterpret_cast<uint4*>(PY + (fl_gy + r) * sty + fl_g0 * 16 + sp * SS) =
+                        *reinterpret_cast<const uint4*>(SY + r * LW + sp * SS);
             }
-            fl_g0 = -1;
         }
-        if (flc_g0 >= 0) {  // chroma: lane = (component, row, 16-byte segment: 2 MBs at 8 bits, 1 at 16)
-            constexpr int MPS = 16 / (8 * static_cast<int>(sizeof(Pel)));  // MBs per segment
+        {  // chroma: lane = (component, row, 16-byte piece: 2 MBs at 8 bits, 1 at 16)
+            constexpr int MPS = SS / 8;  // MBs per piece
             const int c = lane >> 5, cr = (lane >> 2) & 7, sg = lane & 3;
-            const Pel* src = SC + (c * 8 + cr) * CW + sg * 8 * MPS;
-            Pel* dst = PC[c] + (flc_cy + cr) * stc + flc_g0 * 8 + sg * 8 * MPS;
-            if (sg * MPS + MPS <= flc_n) {
+            const Pel* src = SC + (c * 8 + cr) * CW + sg * SS;
+            Pel* dst = PC[c] + (fl_cy + cr) * stc + fl_g0 * 8 + sg * SS;
+            if (sg * MPS + MPS <= fl_n) {
                 if (sizeof(Pel) == 2 || (stc & 15) == 0) {
                     *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
                 } else {  // 8-byte-aligned chroma rows (width an odd multiple of 16)
                     reinterpret_cast<uint2*>(dst)[0] = reinterpret_cast<const uint2*>(src)[0];
                     reinterpret_cast<uint2*>(dst)[1] = reinterpret_cast<const uint2*>(src)[1];
                 }
-            } else if (sg * MPS < flc_n) {  // 8-bit: a group's odd last MB
+            } else if (sg * MPS < fl_n) {  // 8 bits: a group's odd last MB
                 *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
             }
-            flc_g0 = -1;
         }
+        fl_g0 = -1;
     };
     for (int row = rbeg + w; row < rend; row += NW) {
         uint32_t* above = prog + (row + kSlots - 1) % kSlots;
@@ -1786,24 +1789,20 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
             // already in the picture, are rewritten unchanged)
             {
                 Pel* SY = reinterpret_cast<Pel*>(s.stage);
-                Pel* SC = SY + 16 * 64;  // [2][8][CW]
-                const int r = lane >> 2, c4 = (lane & 3) * 4, sx = (mx & 3) * 16;
+                Pel* SC = SY + 16 * LW;  // [2][8][CW]
+                const int r = lane >> 2, c4 = (lane & 3) * 4, sx = (mx % G) * 16;
 #pragma unroll
-                for (int k = 0; k < 4; k++) SY[r * 64 + sx + c4 + k] = static_cast<Pel>(s.wy[r + 1][c4 + 1 + k]);
-                const int c = lane >> 5, kk = lane & 31, rr = kk >> 2, c2 = (kk & 3) * 2, scx = (mx % CG) * 8;
+                for (int k = 0; k < 4; k++) SY[r * LW + sx + c4 + k] = static_cast<Pel>(s.wy[r + 1][c4 + 1 + k]);
+                const int c = lane >> 5, kk = lane & 31, rr = kk >> 2, c2 = (kk & 3) * 2, scx = (mx % G) * 8;
                 SC[(c * 8 + rr) * CW + scx + c2] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 1]);
                 SC[(c * 8 + rr) * CW + scx + c2 + 1] = static_cast<Pel>(s.wc[c][rr + 1][c2 + 2]);
             }
-            // complete groups are stored in the next MB's window step
-            if ((mx & 3) == 3 || mx == mbw - 1) {
-                fl_g0 = mx & ~3;
+            // a complete group is stored in the next MB's window step
+            if (mx % G == G - 1 || mx == mbw - 1) {
+                fl_g0 = mx - mx % G;
                 fl_n = mx - fl_g0 + 1;
                 fl_gy = gy;
-            }
-            if (mx % CG == CG - 1 || mx == mbw - 1) {
-                flc_g0 = mx - mx % CG;
-                flc_n = mx - flc_g0 + 1;
-                flc_cy = cy;
+                fl_cy = cy;
             }
             // bottom row for the MB row below; right column becomes the next MB's left column
             if (to_band) {  // hand the bottom row to the band below: data, wait for completion, then progress
