@@ -1470,6 +1470,10 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 first_idr = type == 5;
             }
             p_ = &p;
+            if (&s != s_) {  // picture size, bit depth and MBAFF come from the first slice's SPS
+                job_->message = "slices of one picture reference different SPSs";
+                return -4;
+            }
             if (job_->hdr.scaling_list == 0 && (p.transform_8x8 || p.scaling_present || s.scaling_present)) {
                 job_->message = "scaling matrices changed inside the picture";
                 return -6;
