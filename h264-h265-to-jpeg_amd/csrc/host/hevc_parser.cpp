@@ -1650,7 +1650,9 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
                 job_->reorder_delay = s_->num_reorder_pics > 0;
                 have_pic = true;
             }
-            p_ = &pps_[sh.pps_id];
+            // all slice segments of a picture use one PPS (7.4.7.1; FFmpeg: "PPS changed between
+            // slices"): tiles, entry points and the SAO / deblocking layout come from it
+            if (&pps_[sh.pps_id] != p_) { job_->message = "PPS change inside picture"; return -6; }
             if (&sps_[p_->sps_id] != s_) { job_->message = "SPS change inside picture"; return -6; }
             // slice data: the RBSP after the header, kept for the decode pass
             const size_t off = b.byte_pos();
