@@ -505,7 +505,7 @@ private:
     // grid (x, 2 fy + f)); parity_ = bottom_field_flag of the slice being decoded
     int paff_ = 0, parity_ = 0;
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
-    Cabac cc_;
+    CabacOutlineRefill cc_;
     const uint8_t* end_ = nullptr;
     CabacState ctx_[460];
     int err_ = 0;
@@ -699,7 +699,7 @@ int H264Parser::residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos
     static const int kCbfOff[5] = {0, 4, 8, 12, 16};
     static const int kSigOff[6] = {0, 15, 29, 44, 47, 0};
     static const int kAbsOff[6] = {0, 10, 20, 30, 39, 0};
-    Cabac cc = cc_;  // engine state in registers for the block
+    CabacOutlineRefill cc = cc_;  // engine state in registers for the block
     CabacState* const ctx = ctx_;
     if (cat != 5 && !cc.decision(ctx[85 + kCbfOff[cat] + cbf_inc])) {
         cc_ = cc;

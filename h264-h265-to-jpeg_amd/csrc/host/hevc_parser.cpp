@@ -512,6 +512,7 @@ private:
     }
     bool same_region(int xc, int yc, int xn, int yn) const {
         if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
+        if (((xn ^ xc) | (yn ^ yc)) >> log2ctb == 0) return true;  // inside the current CTB
         int cn = (yn >> log2ctb) * ctbW + (xn >> log2ctb);
         int cc = (yc >> log2ctb) * ctbW + (xc >> log2ctb);
         if (tile_id_[rs2ts_[cn]] != tile_id_[rs2ts_[cc]] || ctb_slice_[cn] < 0) return false;
@@ -1010,6 +1011,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         greater1_ctx = 1;
         unsigned g1mask = 0;
         int numG1 = 0, lastG1 = -1;
+        unsigned m_uncoded = 0;  // significant positions past the first eight (no greater1 bin)
         const int lastSig = 31 - __builtin_clz(sigmask), firstSig = __builtin_ctz(sigmask);
         CabacState* const g1c = gt1ctx + ctxSet * 4;
         {
@@ -1037,32 +1039,32 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             g1c[1] = w1;
             g1c[2] = w2;
             g1c[3] = w3;
+            m_uncoded = m;
             greater1_ctx = seen ? 0 : 1;  // only "== 0" matters (ctxSet of the next sub-block)
         }
         if (g1mask) lastG1 = 31 - __builtin_clz(g1mask);
         const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
         int g2 = 0;
         if (lastG1 != -1) g2 = cc.decision(ctx[C_GT2 + ctxSet + (c ? 4 : 0)]);
-        unsigned signs = 0;
         const unsigned signed_mask = (sdh && hidden) ? (sigmask & ~(1u << firstSig)) : sigmask;
-        {
-            // all sign bins at once; bin i (MSB first) belongs to the i-th highest position
-            const int ns = __builtin_popcount(signed_mask);
-            uint32_t q = ns > 1 ? cc.bypass_batch(ns) : (ns ? static_cast<uint32_t>(cc.bypass()) : 0u);
-            for (unsigned m = signed_mask; m;) {
-                const int nn = __builtin_ctz(m);  // lowest position takes the last bin
-                m &= m - 1;
-                signs |= (q & 1u) << nn;
-                q >>= 1;
-            }
-        }
-        int numSig = 0, sumAbs = 0, rice = 0;
-        for (unsigned m = sigmask; m;) {
-            const int nn = 31 - __builtin_clz(m);
-            m &= ~(1u << nn);
-            int baseL = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0);
-            int lvl = baseL;
-            if (baseL == ((numSig < 8) ? ((nn == lastG1) ? 3 : 2) : 1)) {
+        // all sign bins at once; bin i (MSB first) belongs to the i-th highest position, so the
+        // output loop below (highest position first) takes them from the top of qs
+        const int ns = __builtin_popcount(signed_mask);
+        const uint32_t q = ns > 1 ? cc.bypass_batch(ns) : (ns ? static_cast<uint32_t>(cc.bypass()) : 0u);
+        uint32_t qs = ns ? q << (32 - ns) : 0u;
+        // positions that carry coeff_abs_level_remaining (baseLevel reached its cap): greater1
+        // set (greater2 set for the one position that has it) among the first eight, and every
+        // position past them (left in m by the greater1 loop).  Decoding them in their own loop
+        // keeps the per-coefficient "escape or not" branch off the output loop.
+        unsigned esc = g1mask | m_uncoded;
+        if (lastG1 >= 0 && !g2) esc &= ~(1u << lastG1);
+        int remv[16] = {};
+        int rice = 0;
+        for (unsigned e = esc; e;) {
+            const int nn = 31 - __builtin_clz(e);
+            e &= ~(1u << nn);
+            const int baseL = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0);
+            {
                 // coeff_abs_level_remaining: unary prefix + suffix, usually both inside one
                 // 20-bin peek (one division instead of a bin loop with a mispredicted exit)
                 constexpr int kPeek = 20;
@@ -1089,19 +1091,25 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
                         rem = (((1 << pm3) + 2) << rice) + static_cast<int>(cc.bypass_bits(pm3 + rice));
                     }
                 }
-                lvl = baseL + rem;
-                if (lvl > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
+                remv[nn] = rem;
+                if (baseL + rem > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
             }
-            int v = ((signs >> nn) & 1) ? -lvl : lvl;
-            if (sdh && hidden) {
-                sumAbs += lvl;
-                if (nn == firstSig && (sumAbs & 1)) v = -v;
-            }
+        }
+        // sign data hiding: the lowest position (processed last) flips when the level sum is odd
+        const int flip_last = (sdh && hidden) ? 1 : 0;
+        int sumAbs = 0;
+        for (unsigned mm = sigmask; mm;) {
+            const int nn = 31 - __builtin_clz(mm);
+            mm &= ~(1u << nn);
+            const int lvl = 1 + ((g1mask >> nn) & 1) + (nn == lastG1 ? g2 : 0) + remv[nn];
+            sumAbs += lvl;
+            const int neg = static_cast<int>(qs >> 31) ^ (mm == 0 ? (flip_last & sumAbs) : 0);
+            qs <<= 1;
+            int v = neg ? -lvl : lvl;
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
             const int xC = (xs << 2) + sc[2][nn][0], yC = (ys << 2) + sc[2][nn][1];
             out[nout++] = (static_cast<uint32_t>(yC * n + xC) << 16) | static_cast<uint16_t>(v);
-            numSig++;
         }
     }
     cc_ = cc;
