@@ -12,6 +12,9 @@ extern thread_local unsigned long long g_bins_ctx, g_bins_byp;
 #define H2J_COUNT(v, n) ((void)0)
 #endif
 
+// Tables are internal to the library: hidden, so the -fPIC code reaches them RIP-relative and not
+// through a GOT load that held a register in the bin loops.
+#pragma GCC visibility push(hidden)
 extern const uint8_t kCabacLps[64][4];
 extern const uint8_t kCabacTransLps[64];
 extern const uint8_t kCabacRenorm[32];
@@ -29,6 +32,7 @@ extern const uint64_t kCabacWord[128];
 
 extern const uint64_t kCabacNextMpsW[128];
 extern const uint64_t kCabacNextLpsW[128];
+#pragma GCC visibility pop
 
 
 inline uint8_t cabac_init_state(int m, int n, int qp) {

@@ -141,7 +141,10 @@ int main(int argc, char** argv) {
     };
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
-    for (int k = 0; k < threads; k++) pool.emplace_back(worker);
+    // one thread: parse on the main thread (the -DH2J_SAMPLE process timer signals the main thread)
+    if (threads == 1) worker();
+    else
+        for (int k = 0; k < threads; k++) pool.emplace_back(worker);
     for (auto& th : pool) th.join();
     if (failed) return 1;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
