@@ -40,3 +40,22 @@ def test_slice_parallel_parse_is_identical(parse_bench, path):
     one = _digest(parse_bench, path, 1)
     assert _digest(parse_bench, path, 8) == one
     assert _digest(parse_bench, path, 2) == one
+
+
+# Record digests of the benchmark sets as the round-4 parser produced them before its speed work
+# (0784438; DESIGN.md §6 "Round 4: host entropy"): engine / residual-loop changes must leave every
+# TU, coefficient, CTB and slice record bit-identical.
+PINNED = {
+    "bench": "f9d574ef25e13d13",
+    "bench_heavy": "46d227bd85837eb8",
+    "bench264": "03609146691cbedd",
+    "bench4k": "c2630db4567d8cfa",
+}
+
+
+@pytest.mark.parametrize("name", sorted(PINNED))
+def test_parse_records_pinned(parse_bench, name):
+    paths = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", name, "*.h26?")))
+    assert len(paths) >= 4
+    out = subprocess.check_output([parse_bench] + paths + ["-r", "1", "-d"], text=True)
+    assert out.split()[-1] == PINNED[name]
