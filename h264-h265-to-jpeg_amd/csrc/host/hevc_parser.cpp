@@ -348,6 +348,9 @@ int parse_pps(BitReader& b, Pps* tab) {
 
 uint8_t g_scan_diag[4][64][2], g_scan_hor[4][64][2], g_scan_ver[4][64][2];
 uint8_t g_scan_inv[3][4][64];  // [scanIdx][log2 size][y * size + x] -> scan position
+// [scanIdx][log2 TB size - 2][n]: raster offset (y * TB size + x) of 4x4 scan position n inside a
+// sub-block, so a coefficient's position is the sub-block's corner offset plus one table entry
+uint16_t g_scan_off[3][4][16];
 uint8_t g_diag_pos4[16];  // raster (y*4+x) of 4x4 diag scan
 uint8_t g_diag_pos8[64];
 // context index (C_SIG-relative) of sig_coeff_flag (9.3.4.2.5):
@@ -419,6 +422,11 @@ void init_scans() {
                             }
                             g_sigctx[c][lsb][si][pc][sb][nn] = static_cast<uint8_t>(C_SIG + (c == 0 ? sigCtx : 27 + sigCtx));
                         }
+    for (int si = 0; si < 3; si++) {
+        const uint8_t(*sc)[64][2] = si == 0 ? g_scan_diag : (si == 1 ? g_scan_hor : g_scan_ver);
+        for (int l = 0; l < 4; l++)
+            for (int i = 0; i < 16; i++) g_scan_off[si][l][i] = static_cast<uint16_t>(sc[2][i][1] * (4 << l) + sc[2][i][0]);
+    }
     for (int i = 0; i < 16; i++) g_diag_pos4[i] = static_cast<uint8_t>(g_scan_diag[2][i][1] * 4 + g_scan_diag[2][i][0]);
     for (int i = 0; i < 64; i++) g_diag_pos8[i] = static_cast<uint8_t>(g_scan_diag[3][i][1] * 8 + g_scan_diag[3][i][0]);
     g_scans_ready = true;
@@ -949,6 +957,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     const int sbw = 1 << lsb;
     uint32_t out[32 * 32];
     int nout = 0;
+    const uint16_t* const posTab = g_scan_off[scanIdx][lsb];
     const uint8_t(*const sigtab)[2][16] = g_sigctx[c ? 1 : 0][lsb][scanIdx];
     CabacState* const gt1ctx = ctx + C_GT1 + (c ? 16 : 0);
     for (int i = lastSub; i >= 0; i--) {
@@ -1097,6 +1106,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         }
         // sign data hiding: the lowest position (processed last) flips when the level sum is odd
         const int flip_last = (sdh && hidden) ? 1 : 0;
+        const int sb_off = ((ys << 2) << log2n) + (xs << 2);
         int sumAbs = 0;
         for (unsigned mm = sigmask; mm;) {
             const int nn = 31 - __builtin_clz(mm);
@@ -1108,8 +1118,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             int v = neg ? -lvl : lvl;
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
-            const int xC = (xs << 2) + sc[2][nn][0], yC = (ys << 2) + sc[2][nn][1];
-            out[nout++] = (static_cast<uint32_t>(yC * n + xC) << 16) | static_cast<uint16_t>(v);
+            out[nout++] = (static_cast<uint32_t>(sb_off + posTab[nn]) << 16) | static_cast<uint16_t>(v);
         }
     }
     cc_ = cc;
