@@ -416,7 +416,7 @@ DEVI uint64_t mask_from_lanes(const uint2& m, int l) {
 // HEVC dequantisation (8.6.2-8.6.3) + transform skip / bypass (8.6.4) of one TB
 // into R (int16, stride rst); regular transforms: hevc_residual_group.
 struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
-    int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo;
+    int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo, rext;
     uint32_t sl;
 };
 // Sample (x, y) of component c in the tiled HEVC residual planes (h2j_res_q, include/h2j_gpu.h);
@@ -482,10 +482,33 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
     }
     wave_sync();
     if (!bypass) {  // transform skip (regular transforms run batched: hevc_residual_group)
-        const int bdS = 20 - bd;
-        for (int i = lane; i < nn; i += 64) s.blk[i] = (s.blk[i] * 128 + (1 << (bdS - 1))) >> bdS;
+        if ((f.rext & H2J_REXT_TS_ROT) && n == 4) {  // RExt rotation: r[x][y] = d[3-x][3-y]
+            const int v = lane < 16 ? s.blk[15 - lane] : 0;
+            wave_sync();
+            if (lane < 16) s.blk[lane] = v;
+            wave_sync();
+        }
+        // tsShift = 5 + log2n then bdShift = 20 - bitDepth (RExt 8.6.4.2): one shift by
+        // 15 - bitDepth - log2n, left (int16 wrap) when negative, as FFmpeg's dequant()
+        const int sh = 15 - bd - log2n;
+        for (int i = lane; i < nn; i += 64)
+            s.blk[i] = sh > 0 ? (s.blk[i] + (1 << (sh - 1))) >> sh : static_cast<int16_t>(s.blk[i] * (1 << -sh));
     }
     wave_sync();
+    if ((f.rext & H2J_REXT_RDPCM) && (tu.mode == 10 || tu.mode == 26)) {
+        // RExt implicit RDPCM (transform skip and bypass): the residual accumulates down the
+        // columns (mode 26) / along the rows (mode 10), int16 as FFmpeg's coefficient buffer
+        const bool vert = tu.mode == 26;
+        if (lane < n) {
+            int acc = 0;
+            for (int k = 0; k < n; k++) {
+                const int i = vert ? k * n + lane : lane * n + k;
+                acc = static_cast<int16_t>(acc + s.blk[i]);
+                s.blk[i] = acc;
+            }
+        }
+        wave_sync();
+    }
     for (int i = lane; i < nn; i += 64) R[(i >> log2n) * rst + (i & (n - 1))] = static_cast<int16_t>(s.blk[i]);
     wave_sync();
 }
@@ -1051,6 +1074,7 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
     f.height = ufl(fr.height);
     f.mw = ufl(fr.mw);
     f.topo = ufl(fr.topo);
+    f.rext = ufl(fr.rext);
     const h2j_ctb* C = ctbs + ufl(fr.ctb);
     const h2j_slice* S = slices + ufl(fr.slice);
     const h2j_tu* T = tus + ufl(fr.tu);
@@ -2107,7 +2131,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     }
     const int mode = tu.mode;
     bool filt = false;
-    if (c == 0 && mode != 1 && n != 4) {
+    if (c == 0 && mode != 1 && n != 4 && !(u.strong & H2J_NO_INTRA_SMOOTHING)) {
         const int d26 = abs(mode - 26), d10 = abs(mode - 10);
         const int md = d26 < d10 ? d26 : d10;
         const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
@@ -2168,7 +2192,7 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     wave_sync();
     if (filt) {
         const int corner = s.sub[2 * n];
-        const bool strong = u.strong && n == 32 &&
+        const bool strong = (u.strong & 1) && n == 32 &&
                             abs(corner + s.sub[4 * n] - 2 * s.sub[3 * n]) < (1 << (bd - 5)) &&
                             abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
         if (strong) {

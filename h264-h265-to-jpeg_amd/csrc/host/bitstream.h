@@ -8,6 +8,7 @@
 // avformat_find_stream_info at :153 decodes the frame a second time).
 #pragma once
 #include <cstddef>
+#include <algorithm>
 #include <cstdint>
 #include <vector>
 
@@ -69,6 +70,26 @@ inline int ceil_log2(int v) {
     int r = 0;
     while ((1 << r) < v) r++;
     return r;
+}
+
+// The left crop of a decoded picture as FFmpeg 4.3 applies it: decode.c apply_cropping calls
+// av_frame_apply_cropping (libavutil/frame.c) without AV_FRAME_CROP_UNALIGNED, which lowers
+// crop_left until every cropped plane's data pointer keeps the alignment of FFmpeg's frame pool
+// (linesizes are multiples of STRIDE_ALIGN >= 32, so the left part of each plane offset decides):
+// crop_left &= ~((1 << (5 + log2(crop_left alignment) - min plane log2 alignment)) - 1) when a
+// plane offset is less than 32-byte aligned, AVERROR_BUG when the crop's alignment is below a
+// plane's.  yuv420p / yuv420pN (chroma at crop_left >> 1), bps bytes per sample.
+// Returns the effective left crop, -1 for AVERROR_BUG (avcodec_receive_frame fails).
+inline int ff_crop_left(int cl, int bps) {
+    if (cl <= 0) return cl;
+    const int lca = __builtin_ctz(static_cast<unsigned>(cl));
+    int m = 1000;
+    const long part[2] = {static_cast<long>(cl) * bps, static_cast<long>(cl >> 1) * bps};
+    for (long v : part)
+        if (v && __builtin_ctzl(static_cast<unsigned long>(v)) < 5) m = std::min(m, __builtin_ctzl(static_cast<unsigned long>(v)));
+    if (m == 1000) return cl;
+    if (lca < m) return -1;
+    return cl & ~((1 << (5 + lca - m)) - 1);
 }
 
 // 0 unknown, 264, 265 — content probe in the spirit of FFmpeg's raw

@@ -1,4 +1,5 @@
-// H.264 (progressive, 4:2:0, CABAC) intra entropy decoding on the host.
+// H.264 intra entropy decoding on the host (CABAC / CAVLC; progressive, MBAFF and PAFF; 4:2:0 and
+// 4:0:0 -- the latter's chroma is FFmpeg's DC_128 / 1 << (BitDepth - 1), see decode_mb).
 //
 // Replaces the parsing half of FFmpeg's h264 decoder reached through
 // avcodec_send_packet (/root/reference/src/Decoder.cpp:324): SPS/PPS/slice
@@ -278,19 +279,20 @@ int parse_sps(BitReader& b, Sps* tab) {
     b.u(1);
     if (b.u(1)) {
         // frame cropping in CropUnitX = 2 / CropUnitY = 2 * (2 - frame_mbs_only) sample units
-        // (4:2:0, 7.4.2.1.1).  FFmpeg 4.3 h264_ps.c
+        // (4:2:0, 7.4.2.1.1; 4:0:0: 1 and 2 - frame_mbs_only).  FFmpeg 4.3 h264_ps.c
         // (libavcodec 58.x, the reference's decoder) rejects the SPS ("crop values invalid",
         // goto fail) when an offset exceeds INT_MAX / 4 / step or the window leaves no
         // picture, so no frame is decoded; only its HEVC SPS parser ignores such a window.
         const uint32_t cl = b.ue(), cr = b.ue(), ct = b.ue(), cb = b.ue();
         const uint64_t w = static_cast<uint64_t>(s.mb_w) * 16, h = static_cast<uint64_t>(s.mb_h) * 16;
-        const uint32_t uy = 2u * (2u - static_cast<uint32_t>(s.frame_mbs_only));
-        const uint32_t lim = 0x7fffffffu / 4 / 2, limy = 0x7fffffffu / 4 / uy;
-        if (cl > lim || cr > lim || ct > limy || cb > limy || (static_cast<uint64_t>(cl) + cr) * 2 >= w ||
+        const uint32_t ux = s.chroma_format_idc == 0 ? 1u : 2u;
+        const uint32_t uy = (s.chroma_format_idc == 0 ? 1u : 2u) * (2u - static_cast<uint32_t>(s.frame_mbs_only));
+        const uint32_t lim = 0x7fffffffu / 4 / ux, limy = 0x7fffffffu / 4 / uy;
+        if (cl > lim || cr > lim || ct > limy || cb > limy || (static_cast<uint64_t>(cl) + cr) * ux >= w ||
             (static_cast<uint64_t>(ct) + cb) * uy >= h)
             return -6;
-        s.crop_l = static_cast<int>(cl) * 2;
-        s.crop_r = static_cast<int>(cr) * 2;
+        s.crop_l = static_cast<int>(cl * ux);
+        s.crop_r = static_cast<int>(cr * ux);
         s.crop_t = static_cast<int>(ct * uy);
         s.crop_b = static_cast<int>(cb * uy);
     }
@@ -299,11 +301,11 @@ int parse_sps(BitReader& b, Sps* tab) {
         s.num_reorder_frames = parse_vui_reorder(b);
         if (s.num_reorder_frames < 0) return -1;
     }
-    // FFmpeg 4.3 decodes 4:2:0 at 8, 9, 10, 12 and 14 bits with equal luma / chroma depths
-    // (h264_ps.c "Different chroma and luma bit depth"; h264_slice.c get_pixel_format has no 11- or
-    // 13-bit format, "Unsupported bit depth")
-    if (s.chroma_format_idc != 1 || s.bit_depth_c != s.bit_depth || s.bit_depth > 14 || s.bit_depth == 11 ||
-        s.bit_depth == 13)
+    // FFmpeg 4.3 decodes 4:2:0 and 4:0:0 (into yuv420p) at 8, 9, 10, 12 and 14 bits with equal
+    // luma / chroma depths (h264_ps.c "Different chroma and luma bit depth"; h264_slice.c
+    // get_pixel_format has no 11- or 13-bit format, "Unsupported bit depth")
+    if ((s.chroma_format_idc != 1 && s.chroma_format_idc != 0) || s.bit_depth_c != s.bit_depth || s.bit_depth > 14 ||
+        s.bit_depth == 11 || s.bit_depth == 13)
         return -4;
     s.valid = true;
     return 0;
@@ -504,6 +506,9 @@ private:
     // PAFF field pair: held in the MBAFF layout as all-field pairs (field MB (x, fy) of parity f at
     // grid (x, 2 fy + f)); parity_ = bottom_field_flag of the slice being decoded
     int paff_ = 0, parity_ = 0;
+    // 4:0:0: no chroma syntax; chroma TBs are DC predicted without residual (every chroma sample
+    // 1 << (BitDepth - 1), as FFmpeg's DC_128_PRED8x8) and I_PCM chroma is that value
+    bool mono_ = false;
     int qp_ = 0, prev_qpd_nz_ = 0, cur_slice_ = 0;
     CabacOutlineRefill cc_;
     const uint8_t* end_ = nullptr;
@@ -855,7 +860,7 @@ void H264Parser::decode_mb() {
         for (int i = 0; i < 256; i++) lv[i] = static_cast<int>(b.u(s_->bit_depth));
         emit(gx, gy, 4, 0, 0, H2J_TU_PCM, 0, lv, 256, true);
         for (int c = 1; c < 3; c++) {
-            for (int i = 0; i < 64; i++) lv[i] = static_cast<int>(b.u(s_->bit_depth_c));
+            for (int i = 0; i < 64; i++) lv[i] = mono_ ? 1 << (s_->bit_depth - 1) : static_cast<int>(b.u(s_->bit_depth_c));
             emit(gx / 2, gy / 2, 3, c, 0, H2J_TU_PCM, 0, lv, 64, true);
         }
         cc_.init(p + b.byte_pos(), end_);
@@ -904,7 +909,7 @@ void H264Parser::decode_mb() {
     } else {
         for (int i = 0; i < 16; i++) m.ipm[i] = 2;
     }
-    {
+    if (!mono_) {
         Mb* A = nb(-1, 0);
         Mb* B = nb(0, -1);
         const int ctx = (A && A->mb_type != 25 && A->cpm != 0) + (B && B->mb_type != 25 && B->cpm != 0);
@@ -935,11 +940,13 @@ void H264Parser::decode_mb() {
             }
             cbp |= dec(73 + ca + 2 * cb) << b8;
         }
-        Mb* A = nb(-1, 0);
-        Mb* B = nb(0, -1);
-        const int ac = A ? (A->mb_type == 25 ? 2 : (A->cbp >> 4)) : 0;
-        const int bc = B ? (B->mb_type == 25 ? 2 : (B->cbp >> 4)) : 0;
-        if (dec(77 + (ac > 0) + 2 * (bc > 0))) cbp |= (1 + dec(77 + 4 + (ac == 2) + 2 * (bc == 2))) << 4;
+        if (!mono_) {  // CodedBlockPatternChroma bins (none for ChromaArrayType 0)
+            Mb* A = nb(-1, 0);
+            Mb* B = nb(0, -1);
+            const int ac = A ? (A->mb_type == 25 ? 2 : (A->cbp >> 4)) : 0;
+            const int bc = B ? (B->mb_type == 25 ? 2 : (B->cbp >> 4)) : 0;
+            if (dec(77 + (ac > 0) + 2 * (bc > 0))) cbp |= (1 + dec(77 + 4 + (ac == 2) + 2 * (bc == 2))) << 4;
+        }
         m.cbp = cbp;
     }
     int qpd = 0;
@@ -1022,7 +1029,7 @@ void H264Parser::decode_mb() {
     // chroma
     uint32_t ce[2][64];
     int nce[2] = {0, 0};
-    if (m.cbp >> 4) {
+    if (!mono_ && (m.cbp >> 4)) {
         for (int c = 0; c < 2; c++) {
             Mb* A = nb(-1, 0);
             Mb* B = nb(0, -1);
@@ -1031,7 +1038,7 @@ void H264Parser::decode_mb() {
             for (int k = 0; k < n; k++) ce[c][nce[c]++] = entry((pos[k] >> 1) * 4 * 8 + (pos[k] & 1) * 4, lvl[k]);
         }
     }
-    if ((m.cbp >> 4) == 2) {
+    if (!mono_ && (m.cbp >> 4) == 2) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 const int bx = b4 & 1, by = b4 >> 1;
@@ -1186,7 +1193,7 @@ void H264Parser::decode_mb_cavlc() {
         for (int i = 0; i < 256; i++) lv[i] = static_cast<int>(vb_.u(s_->bit_depth));
         emit(gx, gy, 4, 0, 0, H2J_TU_PCM, 0, lv, 256, true);
         for (int c = 1; c < 3; c++) {
-            for (int i = 0; i < 64; i++) lv[i] = static_cast<int>(vb_.u(s_->bit_depth_c));
+            for (int i = 0; i < 64; i++) lv[i] = mono_ ? 1 << (s_->bit_depth - 1) : static_cast<int>(vb_.u(s_->bit_depth_c));
             emit(gx / 2, gy / 2, 3, c, 0, H2J_TU_PCM, 0, lv, 64, true);
         }
         m.qp = qp_;
@@ -1223,16 +1230,20 @@ void H264Parser::decode_mb_cavlc() {
     } else {
         for (int i = 0; i < 16; i++) m.ipm[i] = 2;
     }
-    const uint32_t cpm = vb_.ue();
-    if (cpm > 3) { err_ = -41; return; }
-    m.cpm = static_cast<int>(cpm);
+    if (!mono_) {
+        const uint32_t cpm = vb_.ue();
+        if (cpm > 3) { err_ = -41; return; }
+        m.cpm = static_cast<int>(cpm);
+    }
     if (is16) {
         const int t = m.mb_type - 1;
         m.cbp = (((t / 4) % 3) << 4) | (t >= 12 ? 15 : 0);
     } else {
+        // Table 9-4 (me(v)): ChromaArrayType 0 maps codeNum 0..15 to luma-only patterns
+        static const uint8_t kCbpIntraGray[16] = {15, 0, 7, 11, 13, 14, 3, 5, 10, 12, 1, 2, 4, 8, 6, 9};
         const uint32_t cn = vb_.ue();
-        if (cn > 47) { err_ = -42; return; }
-        m.cbp = kCbpIntra[cn];
+        if (cn > (mono_ ? 15u : 47u)) { err_ = -42; return; }
+        m.cbp = mono_ ? kCbpIntraGray[cn] : kCbpIntra[cn];
     }
     if ((m.cbp & 15) || (m.cbp >> 4) || is16) {
         const int qpd = vb_.se();
@@ -1298,14 +1309,14 @@ void H264Parser::decode_mb_cavlc() {
     if (is16) emit_sparse(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
     uint32_t ce[2][64];
     int nce[2] = {0, 0};
-    if (m.cbp >> 4) {
+    if (!mono_ && (m.cbp >> 4)) {
         for (int c = 0; c < 2; c++) {
             const int n = cavlc_block(-1, 4, pos, lvl);
             if (n < 0) { err_ = -44; return; }
             for (int k = 0; k < n; k++) ce[c][nce[c]++] = entry((pos[k] >> 1) * 4 * 8 + (pos[k] & 1) * 4, lvl[k]);
         }
     }
-    if ((m.cbp >> 4) == 2) {
+    if (!mono_ && (m.cbp >> 4) == 2) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 const int bx = b4 & 1, by = b4 >> 1;
@@ -1435,6 +1446,7 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 paff_ = field_pic;
                 job_->field_pair = field_pic != 0;
                 qpbd_ = 6 * (s.bit_depth - 8);
+                mono_ = s.chroma_format_idc == 0;
                 mb_.assign(static_cast<size_t>(mbw_) * mbh_, Mb());
                 job_->ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
                 for (int i = 0; i < mbw_ * mbh_; i++) job_->ctbs[i].ts = static_cast<uint32_t>(i);
@@ -1444,9 +1456,15 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 f.codec = H2J_CODEC_H264;
                 f.width = mbw_ * 16;
                 f.height = mbh_ * 16;
-                f.crop_x = s.crop_l;
+                // decode.c apply_cropping: the left crop as av_frame_apply_cropping aligns it
+                const int cl = ff_crop_left(s.crop_l, s.bit_depth > 8 ? 2 : 1);
+                if (cl < 0) {
+                    job_->message = "left crop FFmpeg's av_frame_apply_cropping rejects (AVERROR_BUG: no frame)";
+                    return -6;
+                }
+                f.crop_x = cl;
                 f.crop_y = s.crop_t;
-                f.out_w = f.width - s.crop_l - s.crop_r;
+                f.out_w = f.width - cl - s.crop_r;
                 f.out_h = f.height - s.crop_t - s.crop_b;
                 f.bit_depth = s.bit_depth;
                 f.bit_depth_c = s.bit_depth_c;

@@ -1,4 +1,5 @@
-// HEVC (H.265 v1 Main/Main10, 4:2:0) intra entropy decoding on the host.
+// HEVC (H.265 Main/Main10, and 4:2:0 range extensions at 8/9/10/12 bits) intra entropy
+// decoding on the host.
 //
 // Replaces the parsing half of FFmpeg's hevc decoder that the reference
 // reaches through avcodec_send_packet (/root/reference/src/Decoder.cpp:324):
@@ -60,6 +61,10 @@ struct Sps {
     int num_st_rps = 0;
     int st_num_delta[65];
     int long_term_present = 0, num_lt_sps = 0, temporal_mvp = 0, strong_intra_smoothing = 0;
+    int profile_idc = 0;  // general_profile_idc (4: FF_PROFILE_HEVC_REXT)
+    // sps_range_extension (H.265 v2 7.3.2.2.2)
+    int ts_rotation = 0, ts_context = 0, implicit_rdpcm = 0, explicit_rdpcm = 0, ext_precision = 0;
+    int smoothing_disabled = 0, high_prec_offsets = 0, persistent_rice = 0, bypass_alignment = 0;
 };
 
 struct Pps {
@@ -74,12 +79,15 @@ struct Pps {
     uint8_t sl[4][6][64];
     uint8_t sl_dc[4][6];
     int slice_header_ext = 0;
+    // pps_range_extension (7.3.2.3.2), read only for the RExt profile (FFmpeg hevc_ps.c)
+    int log2_max_ts = 2, cross_component = 0, cqo_list_enabled = 0, sao_scale_luma = 0, sao_scale_chroma = 0;
 };
 
 struct SliceHdr {
     int first_in_pic = 0, dependent = 0, address = 0, slice_addr_rs = 0, pps_id = 0, type = 0;
     int sao_luma = 0, sao_chroma = 0, qp_delta = 0, cb_qp_offset = 0, cr_qp_offset = 0;
     int deblock_disabled = 0, beta_offset = 0, tc_offset = 0, lf_across_slices = 0, slice_qp = 26;
+    int cu_chroma_qp_offset_enabled = 0;
     std::vector<uint32_t> entry;  // entry_point_offset_minus1[i] + 1 (bytes, emulation prevention included)
 };
 
@@ -134,8 +142,14 @@ void parse_scaling_list(BitReader& b, uint8_t sl[4][6][64], uint8_t dc[4][6]) {
         }
 }
 
-void skip_ptl(BitReader& b, int msl) {
-    b.u(8); b.u(32); b.u(4); b.u(32); b.u(11); b.u(1); b.u(8);
+// profile_tier_level (7.3.3): general_profile_idc, taken from the compatibility flags when it is 0
+// (FFmpeg hevc_ps.c decode_profile_tier_level); sub-layer entries skipped
+int parse_ptl(BitReader& b, int msl) {
+    b.u(3);
+    int prof = static_cast<int>(b.u(5));
+    for (int j = 0; j < 32; j++)
+        if (b.u(1) && prof == 0 && j > 0) prof = j;
+    b.u(4); b.u(32); b.u(11); b.u(1); b.u(8);
     int pp[8] = {0}, lp[8] = {0};
     for (int i = 0; i < msl; i++) { pp[i] = static_cast<int>(b.u(1)); lp[i] = static_cast<int>(b.u(1)); }
     if (msl > 0)
@@ -144,6 +158,64 @@ void skip_ptl(BitReader& b, int msl) {
         if (pp[i]) { b.u(32); b.u(32); b.u(24); }
         if (lp[i]) b.u(8);
     }
+    return prof;
+}
+
+// hrd_parameters (E.2.2) + sub_layer_hrd_parameters (E.2.3), skipped (FFmpeg decode_hrd)
+bool skip_hrd(BitReader& b, int max_sub_layers) {
+    const int nal = static_cast<int>(b.u(1)), vcl = static_cast<int>(b.u(1));
+    int sub_pic = 0;
+    if (nal || vcl) {
+        sub_pic = static_cast<int>(b.u(1));
+        if (sub_pic) b.u(19);
+        b.u(8);
+        if (sub_pic) b.u(4);
+        b.u(15);
+    }
+    for (int i = 0; i < max_sub_layers; i++) {
+        int low_delay = 0;
+        uint32_t nb_cpb = 1;
+        int fixed = static_cast<int>(b.u(1));
+        if (!fixed) fixed = static_cast<int>(b.u(1));
+        if (fixed) b.ue();
+        else low_delay = static_cast<int>(b.u(1));
+        if (!low_delay) {
+            nb_cpb = b.ue() + 1;
+            if (nb_cpb < 1 || nb_cpb > 32) return false;
+        }
+        for (int k = 0; k < nal + vcl; k++)
+            for (uint32_t j = 0; j < nb_cpb; j++) {
+                b.ue(); b.ue();
+                if (sub_pic) { b.ue(); b.ue(); }
+                b.u(1);
+            }
+        if (b.overrun()) return false;
+    }
+    return true;
+}
+
+// vui_parameters (E.2.1), skipped: nothing in it changes decoded samples (FFmpeg applies the default
+// display window only with its apply_defdispwin option, off by default)
+bool skip_vui(BitReader& b, int max_sub_layers) {
+    if (b.u(1) && b.u(8) == 255) b.u(32);
+    if (b.u(1)) b.u(1);
+    if (b.u(1)) {
+        b.u(4);
+        if (b.u(1)) b.u(24);
+    }
+    if (b.u(1)) { b.ue(); b.ue(); }
+    b.u(3);
+    if (b.u(1)) { b.ue(); b.ue(); b.ue(); b.ue(); }
+    if (b.u(1)) {
+        b.u(32); b.u(32);
+        if (b.u(1)) b.ue();
+        if (b.u(1) && !skip_hrd(b, max_sub_layers)) return false;
+    }
+    if (b.u(1)) {
+        b.u(3);
+        for (int i = 0; i < 5; i++) b.ue();
+    }
+    return !b.overrun();
 }
 
 bool parse_st_rps(BitReader& b, Sps& s, int idx) {
@@ -176,11 +248,12 @@ int parse_sps(BitReader& b, Sps* tab) {
     b.u(4);
     int msl = static_cast<int>(b.u(3));
     b.u(1);
-    skip_ptl(b, msl);
+    const int prof = parse_ptl(b, msl);
     uint32_t id = b.ue();
     if (id > 15) return -1;
     Sps& s = tab[id];
     s = Sps();
+    s.profile_idc = prof;
     s.chroma_format_idc = static_cast<int>(b.ue());
     if (s.chroma_format_idc == 3) b.u(1);
     const uint32_t w = b.ue(), h = b.ue();
@@ -252,9 +325,32 @@ int parse_sps(BitReader& b, Sps* tab) {
     }
     s.temporal_mvp = static_cast<int>(b.u(1));
     s.strong_intra_smoothing = static_cast<int>(b.u(1));
+    if (b.u(1) && !skip_vui(b, msl + 1)) return -1;
+    if (b.u(1)) {                                    // sps_extension_present_flag
+        const int range = static_cast<int>(b.u(1));  // sps_range_extension_flag
+        b.u(7);                                      // multilayer / 3d / scc / 4bits: not read (FFmpeg 4.3)
+        if (range) {
+            s.ts_rotation = static_cast<int>(b.u(1));
+            s.ts_context = static_cast<int>(b.u(1));
+            s.implicit_rdpcm = static_cast<int>(b.u(1));
+            s.explicit_rdpcm = static_cast<int>(b.u(1));
+            s.ext_precision = static_cast<int>(b.u(1));
+            s.smoothing_disabled = static_cast<int>(b.u(1));
+            s.high_prec_offsets = static_cast<int>(b.u(1));
+            s.persistent_rice = static_cast<int>(b.u(1));
+            s.bypass_alignment = static_cast<int>(b.u(1));
+        }
+    }
     if (s.chroma_format_idc != 1) return -2;
-    if (s.log2_ctb > 6 || s.log2_ctb < 4 || s.log2_max_tb > 5 || s.bit_depth > 12 || s.bit_depth_c != s.bit_depth)
-        return -3;
+    // FFmpeg hevc_ps.c map_pixel_format: 4:2:0 exists at 8, 9, 10 and 12 bits only; luma and
+    // chroma depths must match
+    if ((s.bit_depth != 8 && s.bit_depth != 9 && s.bit_depth != 10 && s.bit_depth != 12) || s.bit_depth_c != s.bit_depth)
+        return -12;
+    // RExt tools FFmpeg 4.3 parses but does not implement ("... not yet implemented"): the picture
+    // fails with its own message instead of decoding differently from the encoder's intent
+    if (s.ext_precision) return -13;
+    if (s.bypass_alignment) return -14;
+    if (s.log2_ctb > 6 || s.log2_ctb < 4 || s.log2_max_tb > 5) return -3;
     // FFmpeg hevc_ps.c: "Invalid value for log2_min_tb_size", "Invalid coded frame dimensions",
     // "max transform block size out of range", "max_transform_hierarchy_depth_intra out of range",
     // "PCM bit depth ... is greater than normal bit depth"
@@ -268,13 +364,14 @@ int parse_sps(BitReader& b, Sps* tab) {
     return 0;
 }
 
-int parse_pps(BitReader& b, Pps* tab) {
+int parse_pps(BitReader& b, Pps* tab, const Sps* stab) {
     uint32_t id = b.ue();
     if (id > 63) return -1;
     Pps& p = tab[id];
     p = Pps();
     const uint32_t sps_id = b.ue();
-    if (sps_id > 15) return -1;
+    if (sps_id > 15 || !stab[sps_id].valid) return -1;  // FFmpeg: "SPS %u does not exist"
+    const Sps& sps = stab[sps_id];
     p.sps_id = static_cast<int>(sps_id);
     p.dependent_slices = static_cast<int>(b.u(1));
     p.output_flag_present = static_cast<int>(b.u(1));
@@ -341,6 +438,30 @@ int parse_pps(BitReader& b, Pps* tab) {
     b.u(1);
     b.ue();
     p.slice_header_ext = static_cast<int>(b.u(1));
+    if (b.u(1)) {                                    // pps_extension_present_flag
+        const int range = static_cast<int>(b.u(1));  // pps_range_extension_flag
+        b.u(7);
+        if (range && sps.profile_idc == 4) {         // FFmpeg reads it for FF_PROFILE_HEVC_REXT only
+            if (p.transform_skip) {
+                const uint32_t v = b.ue();
+                if (v > 3) return -1;
+                p.log2_max_ts = static_cast<int>(v) + 2;
+            }
+            p.cross_component = static_cast<int>(b.u(1));  // 4:4:4 only: no effect on 4:2:0
+            p.cqo_list_enabled = static_cast<int>(b.u(1));
+            if (p.cqo_list_enabled) {
+                b.ue();
+                const uint32_t len = b.ue();
+                if (len > 5) return -1;
+                for (uint32_t i = 0; i <= len; i++) { b.se(); b.se(); }
+            }
+            const uint32_t sl = b.ue(), sc = b.ue();
+            const uint32_t lim = sps.bit_depth > 10 ? static_cast<uint32_t>(sps.bit_depth - 10) : 0u;
+            if (sl > lim || sc > lim) return -1;
+            p.sao_scale_luma = static_cast<int>(sl);
+            p.sao_scale_chroma = static_cast<int>(sc);
+        }
+    }
     if (b.overrun()) return -1;
     p.valid = true;
     return 0;
@@ -494,6 +615,10 @@ private:
     Cabac cc_;
     const uint8_t* end_ = nullptr;
     CabacState ctx_[NUM_CTX], ctx_wpp_[NUM_CTX], ctx_ds_[NUM_CTX];
+    // StatCoeff (RExt persistent_rice_adaptation, 9.3.2.2): initialised, stored and synchronised
+    // together with the context variables (FFmpeg cabac_init_state / save_states / load_states)
+    int stat_[4] = {0, 0, 0, 0}, stat_wpp_[4] = {0, 0, 0, 0}, stat_ds_[4] = {0, 0, 0, 0};
+    bool rext_ = false;  // a range-extension residual tool is on (residual<true>)
     bool have_ds_ = false;
     int qp_y_ = 0, qg_pred_ = 0, qpd_val_ = 0, last_cu_qp_ = 0;
     bool is_qpd_coded_ = false, first_qg_ = true;
@@ -517,6 +642,7 @@ private:
             int iv = kInitI[i];
             ctx_[i] = cabac_init_word((iv >> 4) * 5 - 45, ((iv & 15) << 3) - 16, qp);
         }
+        std::memset(stat_, 0, sizeof(stat_));
     }
     bool same_region(int xc, int yc, int xn, int yn) const {
         if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
@@ -534,6 +660,7 @@ private:
                         int intra_split, int pcb, int pcr, int cm, int cux, int cuy, int log2cb);
     void transform_unit(int x0, int y0, int xb, int yb, int log2n, int blk, int cbf_l, int cbf_cb,
                         int cbf_cr, int cm, int cux, int cuy, int log2cb);
+    template <bool RExt>
     void residual(int log2n, int c, int mode, h2j_tu& tu);
     void emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int pred_mode_for_scan);
     void split_ctb_records(size_t first);
@@ -640,6 +767,7 @@ int HevcParser::parse_slice_header(BitReader& b, int nal_type, SliceHdr& sh, con
                 p.cr_qp_offset + sh.cr_qp_offset < -12 || p.cr_qp_offset + sh.cr_qp_offset > 12)
                 return -1;
         }
+        if (p.cqo_list_enabled) sh.cu_chroma_qp_offset_enabled = static_cast<int>(b.u(1));
         int override_ = 0;
         if (p.deblock_override) override_ = static_cast<int>(b.u(1));
         sh.deblock_disabled = p.deblock_disabled;
@@ -712,16 +840,21 @@ bool HevcParser::setup_picture() {
     f.codec = H2J_CODEC_HEVC;
     f.width = W;
     f.height = H;
-    f.crop_x = s_->conf_l;
+    // decode.c apply_cropping: the left offset as av_frame_apply_cropping aligns it (4:2:0
+    // conformance offsets are even, which never hits its AVERROR_BUG case)
+    const int cl = ff_crop_left(s_->conf_l, s_->bit_depth > 8 ? 2 : 1);
+    f.crop_x = cl;
     f.crop_y = s_->conf_t;
-    f.out_w = W - s_->conf_l - s_->conf_r;
+    f.out_w = W - cl - s_->conf_r;
     f.out_h = H - s_->conf_t - s_->conf_b;
     f.bit_depth = s_->bit_depth;
     f.bit_depth_c = s_->bit_depth_c;
     f.log2ctb = log2ctb;
     f.ctb_w = ctbW;
     f.ctb_h = ctbH;
-    f.strong_smoothing = s_->strong_intra_smoothing;
+    f.strong_smoothing = s_->strong_intra_smoothing | (s_->smoothing_disabled ? H2J_NO_INTRA_SMOOTHING : 0);
+    f.rext = (s_->implicit_rdpcm ? H2J_REXT_RDPCM : 0) | (s_->ts_rotation ? H2J_REXT_TS_ROT : 0);
+    rext_ = s_->persistent_rice || s_->ts_context || s_->implicit_rdpcm || p_->log2_max_ts > 2;
     f.sao_enabled = s_->sao;
     f.lf_across_tiles = p_->lf_across_tiles;
     f.cb_qp_offset = p_->cb_qp_offset;
@@ -852,9 +985,11 @@ void HevcParser::parse_sao(int rx, int ry) {
     }
     const int bd = s_->bit_depth;
     const int cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
-    const int shift = bd - (bd < 10 ? bd : 10);
     for (int c = 0; c < 3; c++) {
         if ((c == 0 && !cur_->sao_luma) || (c > 0 && !cur_->sao_chroma)) continue;
+        // SaoOffsetVal = offset << log2OffsetScale: the PPS range extension's log2_sao_offset_scale,
+        // 0 without it (FFmpeg hls_sao_param; not v1's bitDepth - Min(bitDepth, 10))
+        const int shift = c ? p_->sao_scale_chroma : p_->sao_scale_luma;
         if (c == 2) {
             r.type[2] = r.type[1];
             r.eo_class[2] = r.eo_class[1];
@@ -911,14 +1046,31 @@ uint8_t HevcParser::edge_flags(int x0, int y0) const {
     return f;
 }
 
+// RExt transform_skip_context_enabled_flag: every significance bin of a transform-skip / bypass
+// block uses context 42 (luma) / 16 + 27 (chroma) (9.3.4.2.5)
+const uint8_t kSigTs[2][16] = {{C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42,
+                                C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42, C_SIG + 42},
+                               {C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43,
+                                C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43, C_SIG + 43}};
+
+// RExt = false: H.265 v1 residual coding (the hot path, unchanged).  RExt = true adds the range
+// extensions' residual tools as FFmpeg 4.3 hevc_cabac.c decodes them: transform skip up to
+// log2_max_transform_skip_block_size, transform-skip contexts, sign data hiding off under implicit
+// RDPCM, persistent Rice adaptation (StatCoeff init / update, Rice parameter not capped at 4).
+template <bool RExt>
 void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     // hot path: engine state in a local (registers), contexts by pointer,
     // coefficients into a local buffer appended once per TU
     Cabac cc = cc_;
     CabacState* const ctx = ctx_;
     const int n = 1 << log2n;
-    if (p_->transform_skip && !cu_bypass_ && log2n <= 2 && cc.decision(ctx[C_TSKIP + (c ? 1 : 0)]))
+    if (p_->transform_skip && !cu_bypass_ && log2n <= (RExt ? p_->log2_max_ts : 2) && cc.decision(ctx[C_TSKIP + (c ? 1 : 0)]))
         tu.flags |= H2J_TU_TSKIP;
+    const bool tsb = (tu.flags & H2J_TU_TSKIP) != 0 || cu_bypass_;
+    const bool ts_ctx = RExt && s_->ts_context && tsb;
+    const bool no_sdh = RExt && s_->implicit_rdpcm && (tu.flags & H2J_TU_TSKIP) && (pred_mode == 10 || pred_mode == 26);
+    const bool price = RExt && s_->persistent_rice;
+    int* const stat = &stat_[2 * (c == 0 ? 1 : 0) + (tsb ? 1 : 0)];
     // last_sig_coeff prefix/suffix
     int off, shift;
     if (c == 0) {
@@ -1001,7 +1153,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             int prevCsbf = 0;
             if (xs + 1 < sbw) prevCsbf |= csbf[xs + 1][ys];
             if (ys + 1 < sbw) prevCsbf |= csbf[xs][ys + 1] << 1;
-            const uint8_t* sig = sigtab[prevCsbf][(xs | ys) ? 1 : 0];
+            const uint8_t* sig = ts_ctx ? kSigTs[c ? 1 : 0] : sigtab[prevCsbf][(xs | ys) ? 1 : 0];
             // bins feed the mask arithmetically (no data-dependent branch per bin).  Consecutive
             // positions often share a context: the word of the previous bin's context stays in a
             // register and is taken by a select when the next bin uses it again, and only the
@@ -1072,7 +1224,7 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
             greater1_ctx = seen ? 0 : 1;  // only "== 0" matters (ctxSet of the next sub-block)
         }
         if (g1mask) lastG1 = 31 - __builtin_clz(g1mask);
-        const bool hidden = !cu_bypass_ && (lastSig - firstSig > 3);
+        const bool hidden = !cu_bypass_ && !no_sdh && (lastSig - firstSig > 3);
         int g2 = 0;
         if (lastG1 != -1) g2 = cc.decision(ctx[C_GT2 + ctxSet + (c ? 4 : 0)]);
         const unsigned signed_mask = (sdh && hidden) ? (sigmask & ~(1u << firstSig)) : sigmask;
@@ -1088,7 +1240,8 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
         unsigned esc = g1mask | m_uncoded;
         if (lastG1 >= 0 && !g2) esc &= ~(1u << lastG1);
         int remv[16] = {};
-        int rice = 0;
+        int rice = price ? *stat / 4 : 0;
+        bool stat_done = false;
         for (unsigned e = esc; e;) {
             const int nn = 31 - __builtin_clz(e);
             e &= ~(1u << nn);
@@ -1121,7 +1274,13 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
                     }
                 }
                 remv[nn] = rem;
-                if (baseL + rem > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
+                if (baseL + rem > 3 * (1 << rice)) rice = price ? rice + 1 : (rice < 4 ? rice + 1 : 4);
+                if (price && !stat_done) {  // StatCoeff update from the sub-block's first remaining level
+                    const int ri = *stat / 4;
+                    if (rem >= (3 << ri)) ++*stat;
+                    else if (2 * rem < (1 << ri) && *stat > 0) --*stat;
+                    stat_done = true;
+                }
             }
         }
         // sign data hiding: the lowest position (processed last) flips when the level sum is odd
@@ -1172,7 +1331,10 @@ void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags
     tu.qpy = 0;
     tu.ncoef = 0;
     tu.coef = 0;
-    if (cbf) residual(log2n, c, mode, tu);
+    if (cbf) {
+        if (rext_) residual<true>(log2n, c, mode, tu);
+        else residual<false>(log2n, c, mode, tu);
+    }
     job_->tus.push_back(tu);
 }
 
@@ -1422,10 +1584,15 @@ void HevcParser::ctb_start_contexts(int rs, int ts, bool first) {
         init_contexts(cur_->slice_qp);
     } else if (row_start) {
         const int xr = x0 + ctbs, yr = y0 - ctbs;
-        if (xr < W && yr >= 0 && same_region(x0, y0, xr, yr)) std::memcpy(ctx_, ctx_wpp_, sizeof(ctx_));
-        else init_contexts(cur_->slice_qp);
+        if (xr < W && yr >= 0 && same_region(x0, y0, xr, yr)) {
+            std::memcpy(ctx_, ctx_wpp_, sizeof(ctx_));
+            std::memcpy(stat_, stat_wpp_, sizeof(stat_));
+        } else {
+            init_contexts(cur_->slice_qp);
+        }
     } else if (cur_->dependent && have_ds_) {
         std::memcpy(ctx_, ctx_ds_, sizeof(ctx_));
+        std::memcpy(stat_, stat_ds_, sizeof(stat_));
     } else {
         init_contexts(cur_->slice_qp);
     }
@@ -1465,7 +1632,10 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         int endf = cc_.terminate();
         if (p_->wpp) {
             for (size_t i = 0; i + 1 < col_bd_.size(); i++)
-                if (rx == col_bd_[i] + 1 && col_bd_[i] + 1 < col_bd_[i + 1]) std::memcpy(ctx_wpp_, ctx_, sizeof(ctx_));
+                if (rx == col_bd_[i] + 1 && col_bd_[i] + 1 < col_bd_[i + 1]) {
+                    std::memcpy(ctx_wpp_, ctx_, sizeof(ctx_));
+                    std::memcpy(stat_wpp_, stat_, sizeof(stat_));
+                }
         }
         ts++;
         if (endf) break;
@@ -1483,6 +1653,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
         rs = nrs;
     }
     std::memcpy(ctx_ds_, ctx_, sizeof(ctx_));
+    std::memcpy(stat_ds_, stat_, sizeof(stat_));
     have_ds_ = true;
     return 0;
 }
@@ -1493,6 +1664,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
 struct HevcParser::WppRows {
     std::unique_ptr<std::atomic<int>[]> done;      // per row: CTBs finished
     std::vector<std::array<CabacState, NUM_CTX>> ctx;  // per row: contexts after its 2nd CTB
+    std::vector<std::array<int, 4>> stat;              // per row: StatCoeff after its 2nd CTB
     std::atomic<bool> failed{false};
 };
 
@@ -1516,8 +1688,12 @@ int HevcParser::decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t
         ctb_slice_[rs] = shi;
         ctb_addr_rs_[rs] = sh.slice_addr_rs;
         if (rx == 0) {
-            if (row > 0 && ctbW > 1) std::memcpy(ctx_, w.ctx[row - 1].data(), sizeof(ctx_));
-            else init_contexts(sh.slice_qp);
+            if (row > 0 && ctbW > 1) {
+                std::memcpy(ctx_, w.ctx[row - 1].data(), sizeof(ctx_));
+                std::memcpy(stat_, w.stat[row - 1].data(), sizeof(stat_));
+            } else {
+                init_contexts(sh.slice_qp);
+            }
         }
         parse_sao(rx, row);
         const size_t first_tu = job_->tus.size();
@@ -1525,7 +1701,10 @@ int HevcParser::decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t
         if (err_) return err_;
         split_ctb_records(first_tu);
         const int endf = cc_.terminate();
-        if (rx == 1) std::memcpy(w.ctx[row].data(), ctx_, sizeof(ctx_));
+        if (rx == 1) {
+            std::memcpy(w.ctx[row].data(), ctx_, sizeof(ctx_));
+            std::memcpy(w.stat[row].data(), stat_, sizeof(stat_));
+        }
         w.done[row].store(rx + 1, std::memory_order_release);
         if (endf != (row == ctbH - 1 && rx == ctbW - 1)) return -30;
     }
@@ -1538,6 +1717,7 @@ int HevcParser::run_wpp(const std::vector<uint8_t>& seg, const std::vector<uint3
     w.done.reset(new std::atomic<int>[ctbH]);
     for (int r = 0; r < ctbH; r++) w.done[r].store(0);
     w.ctx.resize(ctbH);
+    w.stat.resize(ctbH);
     std::vector<FrameJob> part(ctbH);
     const int nt = std::min(threads, ctbH);
     std::vector<std::unique_ptr<HevcParser>> wk(nt);
@@ -1663,10 +1843,17 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
         BitReader b(rbsp_.data(), rn);
         if (type == 33) {
             if (have_pic) break;
-            if (parse_sps(b, sps_) < 0) { job_->message = "unsupported or invalid SPS"; return -2; }
+            const int e = parse_sps(b, sps_);
+            if (e < 0) {
+                job_->message = e == -12 ? "unsupported bit depth (FFmpeg 4.3 has no HEVC 4:2:0 format at it)"
+                              : e == -13 ? "unsupported HEVC range extension tool: extended_precision_processing_flag (FFmpeg 4.3: not implemented)"
+                              : e == -14 ? "unsupported HEVC range extension tool: cabac_bypass_alignment_enabled_flag (FFmpeg 4.3: not implemented)"
+                                         : "unsupported or invalid SPS";
+                return -2;
+            }
         } else if (type == 34) {
             if (have_pic) break;
-            if (parse_pps(b, pps_) < 0) { job_->message = "invalid PPS"; return -3; }
+            if (parse_pps(b, pps_, sps_) < 0) { job_->message = "invalid PPS"; return -3; }
         } else if (type <= 21) {
             if (type >= 10 && type <= 15) continue;
             const int first = (rbsp_[0] >> 7) & 1;
@@ -1679,6 +1866,10 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
             if (r < 0) {
                 job_->message = r == -2 ? "non-intra first picture (P/B slices) unsupported" : "invalid slice header";
                 return r == -2 ? -5 : -6;
+            }
+            if (sh.cu_chroma_qp_offset_enabled) {
+                job_->message = "unsupported HEVC range extension tool: chroma_qp_offset_list (cu_chroma_qp_offset_enabled_flag)";
+                return -6;
             }
             if (!have_pic) {
                 p_ = &pps_[sh.pps_id];

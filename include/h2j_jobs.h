@@ -93,7 +93,7 @@ typedef struct {
     int32_t out_w, out_h;           /* cropped output size (luma) */
     int32_t bit_depth, bit_depth_c;
     int32_t log2ctb, ctb_w, ctb_h;
-    int32_t strong_smoothing;
+    int32_t strong_smoothing;       /* bit 0 strong_intra_smoothing; H2J_NO_INTRA_SMOOTHING (RExt) */
     int32_t sao_enabled;
     int32_t lf_across_tiles;
     int32_t cb_qp_offset, cr_qp_offset; /* pps offsets (deblocking) */
@@ -123,8 +123,15 @@ typedef struct {
     int32_t mbaff;                  /* H.264 MBAFF frame: macroblock pairs (h2j_ctb.mbflags bit 3: field
                                        pair), TU records in the MB grid (grid row = 2 pair row + bottom),
                                        availability masks from the host (h2j_tu.qpy bits 0-3) */
-    int32_t pad_f;
+    int32_t rext;                   /* HEVC range-extension residual tools K0 applies: H2J_REXT_* */
 } h2j_frame;
+
+/* h2j_frame.strong_smoothing bit 1: RExt intra_smoothing_disabled_flag (no reference filtering) */
+#define H2J_NO_INTRA_SMOOTHING 2
+/* h2j_frame.rext: implicit RDPCM of transform-skip / bypass TBs predicted with mode 10 / 26;
+ * 180-degree rotation of 4x4 transform-skip residuals (FFmpeg 4.3: not of bypass blocks) */
+#define H2J_REXT_RDPCM 1
+#define H2J_REXT_TS_ROT 2
 
 /* per-frame JPEG statistics written by the GPU */
 typedef struct {

@@ -100,6 +100,27 @@ static inline int ob_more_rbsp(OraBits *b) {
     long stop = last * 8 + (7 - tz);
     return b->pos < stop;
 }
+/* FFmpeg 4.3 av_frame_apply_cropping (libavutil/frame.c) as decode.c applies it to every decoded
+ * frame (AVCodecContext.apply_cropping 1, no AV_CODEC_FLAG_UNALIGNED): the left crop is lowered
+ * until the cropped planes' data pointers keep the alignment FFmpeg's frame pool gives them
+ * (linesizes are multiples of STRIDE_ALIGN >= 32, so only the left part of each plane's offset
+ * decides): crop_left &= ~((1 << (5 + log2_crop_align - min_log2_align)) - 1) when
+ * min_log2_align < 5, and AVERROR_BUG (no frame) when log2_crop_align < min_log2_align.
+ * yuv420p / yuv420pN: planes at crop_left and crop_left >> 1, bps bytes per sample.  Returns the
+ * effective left crop, -1 for AVERROR_BUG. */
+static inline int ora_ff_crop_left(int cl, int bps) {
+    if (cl <= 0) return cl;
+    const int lca = __builtin_ctz((unsigned)cl);
+    int m = 1000;
+    const long part[2] = {(long)cl * bps, (long)(cl >> 1) * bps};
+    for (int i = 0; i < 2; i++)
+        if (part[i] && __builtin_ctzl((unsigned long)part[i]) < 5 && __builtin_ctzl((unsigned long)part[i]) < m)
+            m = __builtin_ctzl((unsigned long)part[i]);
+    if (m == 1000) return cl; /* every offset 32-byte aligned: unchanged */
+    if (lca < m) return -1;
+    return cl & ~((1 << (5 + lca - m)) - 1);
+}
+
 static inline int ora_ceil_log2(int v) {
     int r = 0;
     while ((1 << r) < v) r++;

@@ -305,7 +305,7 @@ static int parse_sps(OraBits *b, H4Sps *tab) {
         s->crop_b = (int)cb * cy;
     }
     if (ob_u(b, 1) && vui_fails(b)) return -7; /* vui_parameters_present_flag */
-    if (s->chroma_format_idc != 1) return -4;
+    if (s->chroma_format_idc != 1 && s->chroma_format_idc != 0) return -4;
     /* FFmpeg 4.3: h264_ps.c fails luma / chroma depths that differ ("Different chroma and luma
      * bit depth") or exceed 14; h264_slice.c get_pixel_format has no 11- or 13-bit format
      * ("Unsupported bit depth") */
@@ -394,6 +394,10 @@ typedef struct {
      * (field MB (x, fy) of parity f at grid (x, 2 fy + f)); neighbours stay inside a field
      * (6.4.12.1 on the field's MB grid) */
     int paff, parity, fields_seen;
+    /* 4:0:0 (chroma_format_idc 0, High profiles): no chroma syntax; FFmpeg (h264_cabac.c /
+     * h264_cavlc.c decode_chroma = 0) predicts both chroma blocks with DC_128_PRED8x8 and writes
+     * 1 << (BitDepth - 1) for I_PCM, into a yuv420p frame */
+    int mono;
     uint16_t *pl[3];
     int st[3];
     MbInfo *mb;
@@ -593,6 +597,7 @@ static int dec_cbp(H4Dec *d) {
         }
         cbp |= bin(d, 73 + ca + 2 * cb) << b8;
     }
+    if (d->mono) return cbp; /* no CodedBlockPatternChroma bins (9.3.2.4) */
     MbInfo *A = nb_mb(d, -1, 0), *B = nb_mb(d, 0, -1);
     int ac = A ? (A->mb_type == MB_I_PCM ? 2 : (A->cbp >> 4)) : 0;
     int bc = B ? (B->mb_type == MB_I_PCM ? 2 : (B->cbp >> 4)) : 0;
@@ -1129,6 +1134,14 @@ static void bypass_dpcm(int *r, int n, int dir) {
         }
 }
 
+/* 4:0:0: both chroma blocks DC_128_PRED8x8 (1 << (BitDepth - 1)), no residual (FFmpeg) */
+static int mono_chroma(H4Dec *d, int gx, int gy) {
+    for (int c = 1; c < 3; c++)
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++) put_sample(d, c, gx / 2 + x, gy / 2 + y, 1 << (d->bd - 1));
+    return 0;
+}
+
 /* the TransformBypassModeFlag macroblock: residual = the inverse-scanned levels, no scaling, no
  * transform (8.5.12.1 / 8.5.10 / 8.5.11 with TransformBypassModeFlag 1) */
 static int recon_mb_bypass(H4Dec *d, MbInfo *m) {
@@ -1159,6 +1172,7 @@ static int recon_mb_bypass(H4Dec *d, MbInfo *m) {
         if (dpcm && mode <= 1) bypass_dpcm(r, 16, mode);
         put_block(d, 0, gx, gy, 16, pred, r);
     }
+    if (d->mono) return mono_chroma(d, gx, gy);
     for (int c = 0; c < 2; c++) {
         pred_chroma(d, 1 + c, m->cpm, pred);
         for (int b4 = 0; b4 < 4; b4++) {
@@ -1238,6 +1252,7 @@ static int recon_mb(H4Dec *d, MbInfo *m) {
         }
     }
     /* chroma */
+    if (d->mono) return mono_chroma(d, gx, gy);
     for (int c = 0; c < 2; c++) {
         int off = c == 0 ? d->p->chroma_qp_offset : d->p->chroma_qp_offset2;
         int qpc = chroma_qp(clip3(-d->qpbdc, 51, d->qp + off)) + d->qpbdc;
@@ -1311,7 +1326,8 @@ static int decode_mb(H4Dec *d, int slice_idx) {
             for (int x = 0; x < 16; x++) put_sample(d, 0, gx + x, gy + y, (int)ob_u(b, d->bd));
         for (int c = 1; c < 3; c++)
             for (int y = 0; y < 8; y++)
-                for (int x = 0; x < 8; x++) put_sample(d, c, gx / 2 + x, gy / 2 + y, (int)ob_u(b, d->bdc));
+                for (int x = 0; x < 8; x++)
+                    put_sample(d, c, gx / 2 + x, gy / 2 + y, d->mono ? 1 << (d->bd - 1) : (int)ob_u(b, d->bdc));
         oc_init(&d->cc, b);
         m->qp = d->qp;
         m->cbp = 0x2F;
@@ -1348,7 +1364,7 @@ static int decode_mb(H4Dec *d, int slice_idx) {
     } else {
         for (int i = 0; i < 16; i++) m->ipm[i] = 2;
     }
-    m->cpm = dec_chroma_pred(d);
+    m->cpm = d->mono ? 0 : dec_chroma_pred(d);
     if (is16) {
         int t = m->mb_type - 1;
         m->cbp = ((t / 4) % 3) << 4 | (t >= 12 ? 15 : 0);
@@ -1401,14 +1417,14 @@ static int decode_mb(H4Dec *d, int slice_idx) {
             }
         }
     }
-    if (m->cbp >> 4) {
+    if (!d->mono && (m->cbp >> 4)) {
         for (int c = 0; c < 2; c++) {
             int ca = cbf_cond(d, 3, nb_mb(d, -1, 0), 0, c), cb = cbf_cond(d, 3, nb_mb(d, 0, -1), 0, c);
             m->cbf_dc[1 + c] = (uint8_t)residual_block(d, 3, ca + 2 * cb, 4, coef);
             for (int k = 0; k < 4; k++) d->dc_c[c][k] = coef[k];
         }
     }
-    if ((m->cbp >> 4) == 2) {
+    if (!d->mono && (m->cbp >> 4) == 2) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 int bx = b4 & 1, by = b4 >> 1, ca, cb;
@@ -1560,7 +1576,8 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
             for (int x = 0; x < 16; x++) put_sample(d, 0, gx + x, gy + y, (int)ob_u(b, d->bd));
         for (int c = 1; c < 3; c++)
             for (int y = 0; y < 8; y++)
-                for (int x = 0; x < 8; x++) put_sample(d, c, gx / 2 + x, gy / 2 + y, (int)ob_u(b, d->bdc));
+                for (int x = 0; x < 8; x++)
+                    put_sample(d, c, gx / 2 + x, gy / 2 + y, d->mono ? 1 << (d->bd - 1) : (int)ob_u(b, d->bdc));
         m->qp = d->qp;
         m->cbp = 0x2F;
         memset(m->tc, 16, sizeof(m->tc));
@@ -1585,16 +1602,20 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
     } else {
         for (int i = 0; i < 16; i++) m->ipm[i] = 2;
     }
-    uint32_t cpm = ob_ue(b);
-    if (cpm > 3) return -1;
-    m->cpm = (int)cpm;
+    if (!d->mono) {
+        uint32_t cpm = ob_ue(b);
+        if (cpm > 3) return -1;
+        m->cpm = (int)cpm;
+    }
     if (is16) {
         int t = m->mb_type - 1;
         m->cbp = ((t / 4) % 3) << 4 | (t >= 12 ? 15 : 0);
     } else {
         uint32_t cn = ob_ue(b);
-        if (cn > 47) return -1;
-        m->cbp = k_cbp_intra[cn];
+        /* Table 9-4: ChromaArrayType 0 maps codeNum 0..15 to luma-only patterns */
+        static const uint8_t k_cbp_intra_gray[16] = {15, 0, 7, 11, 13, 14, 3, 5, 10, 12, 1, 2, 4, 8, 6, 9};
+        if (cn > (d->mono ? 15u : 47u)) return -1;
+        m->cbp = d->mono ? k_cbp_intra_gray[cn] : k_cbp_intra[cn];
     }
     if ((m->cbp & 15) || (m->cbp >> 4) || is16) {
         int qpd = ob_se(b);
@@ -1633,13 +1654,13 @@ static int decode_mb_cavlc(H4Dec *d, int slice_idx) {
             else for (int k = 0; k < 16; k++) d->lvl4[blk][z4[k]] = coef[k];
         }
     }
-    if (m->cbp >> 4) {
+    if (!d->mono && (m->cbp >> 4)) {
         for (int c = 0; c < 2; c++) {
             if (cavlc_block(d, -1, 4, coef) < 0) return -1;
             for (int k = 0; k < 4; k++) d->dc_c[c][k] = coef[k];
         }
     }
-    if ((m->cbp >> 4) == 2) {
+    if (!d->mono && (m->cbp >> 4) == 2) {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 int tc = cavlc_block(d, cavlc_nc_chroma(d, m, c, b4), 15, coef);
@@ -1949,6 +1970,7 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
                 d->H = d->mbh * 16;
                 d->bd = s->bit_depth;
                 d->bdc = s->bit_depth_c;
+                d->mono = s->chroma_format_idc == 0;
                 d->qpbd = 6 * (d->bd - 8);
                 d->mbaff = s->mbaff || field_pic; /* MbaffFrameFlag; a PAFF field pair uses the same layout */
                 d->paff = field_pic;
@@ -2018,17 +2040,21 @@ int oracle_h264_decode(const uint8_t *data, long size, int flags, OraclePicture 
     }
     {
         const H4Sps *s = d->s;
-        int w = d->W - s->crop_l - s->crop_r, h = d->H - s->crop_t - s->crop_b;
+        /* decode.c apply_cropping: the left crop as av_frame_apply_cropping aligns it */
+        const int cl = ora_ff_crop_left(s->crop_l, d->bd > 8 ? 2 : 1);
+        if (cl < 0) { ret = -10; goto done_free; } /* AVERROR_BUG: avcodec_receive_frame fails */
+        int w = d->W - cl - s->crop_r, h = d->H - s->crop_t - s->crop_b;
         out->width = w;
         out->height = h;
         out->bit_depth = d->bd;
         out->chroma_format = 1;
         for (int c = 0; c < 3; c++) {
-            int sh = c ? 1 : 0, cw = w >> sh, ch = h >> sh;
+            /* chroma planes of an odd-sized (4:0:0 crop) picture: AV_CEIL_RSHIFT */
+            int sh = c ? 1 : 0, cw = (w + sh) >> sh, ch = (h + sh) >> sh;
             out->planes[c] = (uint16_t *)malloc((size_t)cw * ch * 2);
             out->stride[c] = cw;
             for (int y = 0; y < ch; y++)
-                memcpy(out->planes[c] + (size_t)y * cw, d->pl[c] + (size_t)(y + (s->crop_t >> sh)) * d->st[c] + (s->crop_l >> sh),
+                memcpy(out->planes[c] + (size_t)y * cw, d->pl[c] + (size_t)(y + (s->crop_t >> sh)) * d->st[c] + (cl >> sh),
                        (size_t)cw * 2);
         }
     }

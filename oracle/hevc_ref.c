@@ -16,8 +16,22 @@
  *
  * Scope: I slices only (the reference uses the first picture only; stills
  * are IDR/CRA), tiles, WPP, dependent slice segments, PCM, transquant
- * bypass, transform skip, scaling lists, sign data hiding.  RExt tools are
- * not supported (Main/Main10 profiles).
+ * bypass, transform skip, scaling lists, sign data hiding; 8/9/10/12-bit
+ * 4:2:0 (FFmpeg hevc_ps.c map_pixel_format: no 11-bit format).
+ * Range extensions (H.265 v2 7.3.2.2.2 / 7.3.2.3.2), restated as FFmpeg 4.3
+ * hevc_ps.c / hevc_cabac.c / hevcpred_template.c decode them for intra 4:2:0:
+ *   implicit RDPCM (transform-skip and transquant-bypass TBs, modes 10 / 26),
+ *   transform-skip rotation (4x4, transform skip only -- FFmpeg does not rotate
+ *   bypass blocks), transform-skip contexts, persistent Rice adaptation
+ *   (FFmpeg does not cap the Rice parameter at 4 then), intra smoothing
+ *   disabled, log2_max_transform_skip_block_size, log2_sao_offset_scale
+ *   (SaoOffsetVal = offset << scale, in place of v1's bitDepth - 10 shift).
+ *   Explicit RDPCM / high-precision offsets only act on inter blocks and
+ *   cross-component prediction only in 4:4:4 (no effect here).
+ *   Rejected (the picture fails, as the product's): extended precision
+ *   processing and CABAC bypass alignment (FFmpeg 4.3: "not yet
+ *   implemented"), and chroma QP offset lists enabled in a slice.
+ * RExt behaviour has no reference-held fixture: parity unpinned.
  */
 #include <stdio.h>
 #include <stdint.h>
@@ -96,6 +110,10 @@ typedef struct {
     int st_num_delta[65];
     int long_term_present, num_lt_sps;
     int temporal_mvp, strong_intra_smoothing;
+    int profile_idc; /* general_profile_idc (4 = FF_PROFILE_HEVC_REXT) */
+    /* sps_range_extension (7.3.2.2.2) */
+    int ts_rotation, ts_context, implicit_rdpcm, explicit_rdpcm, ext_precision, smoothing_disabled,
+        high_prec_offsets, persistent_rice, bypass_alignment;
 } Sps;
 
 typedef struct {
@@ -110,6 +128,10 @@ typedef struct {
     uint8_t sl[4][6][64];
     uint8_t sl_dc[4][6];
     int slice_header_ext;
+    /* pps_range_extension (7.3.2.3.2), read only for the RExt profile as FFmpeg does */
+    int log2_max_ts, cross_component, cqo_list_enabled, cqo_depth, cqo_len;
+    int cb_qo_list[6], cr_qo_list[6];
+    int sao_scale_luma, sao_scale_chroma;
 } Pps;
 
 typedef struct {
@@ -118,6 +140,7 @@ typedef struct {
     int sao_luma, sao_chroma;
     int qp_delta, cb_qp_offset, cr_qp_offset;
     int deblock_disabled, beta_offset, tc_offset, lf_across_slices;
+    int cu_chroma_qp_offset_enabled;
     int num_entry;
     int slice_qp;
 } SliceHdr;
@@ -186,9 +209,13 @@ static void parse_scaling_list(OraBits *b, uint8_t sl[4][6][64], uint8_t dc[4][6
         }
 }
 
-static void skip_ptl(OraBits *b, int max_sub_layers_minus1) {
-    ob_u(b, 8);       /* profile space, tier, profile idc */
-    ob_u(b, 32);      /* compat flags */
+/* profile_tier_level (7.3.3); returns general_profile_idc, taken from the compatibility flags
+ * when it is 0 (FFmpeg hevc_ps.c decode_profile_tier_level) */
+static int parse_ptl(OraBits *b, int max_sub_layers_minus1) {
+    ob_u(b, 3);       /* profile space, tier */
+    int prof = (int)ob_u(b, 5);
+    for (int j = 0; j < 32; j++)
+        if (ob_u(b, 1) && prof == 0 && j > 0) prof = j;
     ob_u(b, 4);       /* progressive, interlaced, non-packed, frame-only */
     ob_u(b, 32);
     ob_u(b, 11);      /* 43 reserved bits */
@@ -205,6 +232,68 @@ static void skip_ptl(OraBits *b, int max_sub_layers_minus1) {
         if (pp[i]) { ob_u(b, 32); ob_u(b, 32); ob_u(b, 24); }
         if (lp[i]) ob_u(b, 8);
     }
+    return prof;
+}
+
+/* hrd_parameters (E.2.2) and sub_layer_hrd_parameters (E.2.3): skipped (FFmpeg decode_hrd) */
+static int skip_hrd(OraBits *b, int common, int max_sub_layers) {
+    int nal = 0, vcl = 0, sub_pic = 0;
+    if (common) {
+        nal = (int)ob_u(b, 1);
+        vcl = (int)ob_u(b, 1);
+        if (nal || vcl) {
+            sub_pic = (int)ob_u(b, 1);
+            if (sub_pic) ob_u(b, 19);
+            ob_u(b, 8);
+            if (sub_pic) ob_u(b, 4);
+            ob_u(b, 15);
+        }
+    }
+    for (int i = 0; i < max_sub_layers; i++) {
+        int low_delay = 0;
+        uint32_t nb_cpb = 1;
+        int fixed = (int)ob_u(b, 1);
+        if (!fixed) fixed = (int)ob_u(b, 1);
+        if (fixed) ob_ue(b);
+        else low_delay = (int)ob_u(b, 1);
+        if (!low_delay) {
+            nb_cpb = ob_ue(b) + 1;
+            if (nb_cpb < 1 || nb_cpb > 32) return -1;
+        }
+        for (int k = 0; k < nal + vcl; k++)
+            for (uint32_t j = 0; j < nb_cpb; j++) {
+                ob_ue(b);
+                ob_ue(b);
+                if (sub_pic) { ob_ue(b); ob_ue(b); }
+                ob_u(b, 1);
+            }
+    }
+    return 0;
+}
+
+/* vui_parameters (E.2.1), skipped: nothing in it changes the decoded samples (the default display
+ * window is not applied by default, FFmpeg's apply_defdispwin = 0) */
+static int skip_vui(OraBits *b, int max_sub_layers) {
+    if (ob_u(b, 1) && ob_u(b, 8) == 255) ob_u(b, 32); /* aspect_ratio_idc, EXTENDED_SAR */
+    if (ob_u(b, 1)) ob_u(b, 1);                        /* overscan */
+    if (ob_u(b, 1)) {                                  /* video signal type */
+        ob_u(b, 4);
+        if (ob_u(b, 1)) ob_u(b, 24);
+    }
+    if (ob_u(b, 1)) { ob_ue(b); ob_ue(b); }            /* chroma loc */
+    ob_u(b, 3); /* neutral chroma, field_seq, frame_field_info */
+    if (ob_u(b, 1)) { ob_ue(b); ob_ue(b); ob_ue(b); ob_ue(b); } /* default display window */
+    if (ob_u(b, 1)) {                                  /* timing */
+        ob_u(b, 32);
+        ob_u(b, 32);
+        if (ob_u(b, 1)) ob_ue(b);
+        if (ob_u(b, 1) && skip_hrd(b, 1, max_sub_layers) < 0) return -1;
+    }
+    if (ob_u(b, 1)) {                                  /* bitstream restriction */
+        ob_u(b, 3);
+        for (int i = 0; i < 5; i++) ob_ue(b);
+    }
+    return 0;
 }
 
 static int parse_st_rps(OraBits *b, Sps *s, int idx) {
@@ -240,11 +329,12 @@ static int parse_sps(OraBits *b, Sps *tab) {
     ob_u(b, 4);
     int msl = (int)ob_u(b, 3);
     ob_u(b, 1);
-    skip_ptl(b, msl);
+    int prof = parse_ptl(b, msl);
     int id = (int)ob_ue(b);
     if (id > 15) return -1;
     Sps *s = &tab[id];
     memset(s, 0, sizeof(*s));
+    s->profile_idc = prof;
     s->chroma_format_idc = (int)ob_ue(b);
     if (s->chroma_format_idc == 3) ob_u(b, 1);
     uint32_t w = ob_ue(b), h = ob_ue(b);
@@ -302,8 +392,27 @@ static int parse_sps(OraBits *b, Sps *tab) {
     }
     s->temporal_mvp = (int)ob_u(b, 1);
     s->strong_intra_smoothing = (int)ob_u(b, 1);
-    /* VUI and extensions are not needed for Main/Main10 decoding */
+    if (ob_u(b, 1) && skip_vui(b, msl + 1) < 0) return -1;
+    if (ob_u(b, 1)) {                  /* sps_extension_present_flag */
+        int range = (int)ob_u(b, 1);  /* sps_range_extension_flag */
+        ob_u(b, 7);                    /* multilayer, 3d, scc, 4bits: not read (FFmpeg 4.3) */
+        if (range) {
+            s->ts_rotation = (int)ob_u(b, 1);
+            s->ts_context = (int)ob_u(b, 1);
+            s->implicit_rdpcm = (int)ob_u(b, 1);
+            s->explicit_rdpcm = (int)ob_u(b, 1);
+            s->ext_precision = (int)ob_u(b, 1);
+            s->smoothing_disabled = (int)ob_u(b, 1);
+            s->high_prec_offsets = (int)ob_u(b, 1);
+            s->persistent_rice = (int)ob_u(b, 1);
+            s->bypass_alignment = (int)ob_u(b, 1);
+        }
+    }
     if (s->chroma_format_idc != 1) return -2;
+    /* FFmpeg map_pixel_format: 4:2:0 at 8, 9, 10, 12 bits; luma and chroma depths equal */
+    if (s->bit_depth != 8 && s->bit_depth != 9 && s->bit_depth != 10 && s->bit_depth != 12) return -3;
+    if (s->bit_depth_c != s->bit_depth) return -3;
+    if (s->ext_precision || s->bypass_alignment) return -11; /* unsupported RExt tool */
     if (s->log2_ctb > 6 || s->log2_ctb < 4 || s->log2_max_tb > 5) return -3;
     /* FFmpeg hevc_ps.c: "Invalid coded frame dimensions" */
     if ((s->width & ((1 << s->log2_min_cb) - 1)) || (s->height & ((1 << s->log2_min_cb) - 1))) return -1;
@@ -311,12 +420,15 @@ static int parse_sps(OraBits *b, Sps *tab) {
     return 0;
 }
 
-static int parse_pps(OraBits *b, Pps *tab) {
+static int parse_pps(OraBits *b, Pps *tab, const Sps *stab) {
     int id = (int)ob_ue(b);
     if (id > 63) return -1;
     Pps *p = &tab[id];
     memset(p, 0, sizeof(*p));
     p->sps_id = (int)ob_ue(b);
+    if (p->sps_id > 15 || !stab[p->sps_id].valid) return -1; /* FFmpeg: "SPS %u does not exist" */
+    const Sps *sps = &stab[p->sps_id];
+    p->log2_max_ts = 2;
     p->dependent_slices = (int)ob_u(b, 1);
     p->output_flag_present = (int)ob_u(b, 1);
     p->num_extra_bits = (int)ob_u(b, 3);
@@ -368,6 +480,34 @@ static int parse_pps(OraBits *b, Pps *tab) {
     ob_u(b, 1); /* lists_modification_present */
     ob_ue(b);   /* log2_parallel_merge_level */
     p->slice_header_ext = (int)ob_u(b, 1);
+    if (ob_u(b, 1)) {                  /* pps_extension_present_flag */
+        int range = (int)ob_u(b, 1);
+        ob_u(b, 7);
+        if (range && sps->profile_idc == 4) {  /* FFmpeg: only for FF_PROFILE_HEVC_REXT */
+            if (p->transform_skip) {
+                uint32_t v = ob_ue(b);
+                if (v > 3) return -1;
+                p->log2_max_ts = (int)v + 2;
+            }
+            p->cross_component = (int)ob_u(b, 1);
+            p->cqo_list_enabled = (int)ob_u(b, 1);
+            if (p->cqo_list_enabled) {
+                p->cqo_depth = (int)ob_ue(b);
+                uint32_t len = ob_ue(b);
+                if (len > 5) return -1;
+                p->cqo_len = (int)len + 1;
+                for (int i = 0; i < p->cqo_len; i++) {
+                    p->cb_qo_list[i] = ob_se(b);
+                    p->cr_qo_list[i] = ob_se(b);
+                }
+            }
+            uint32_t sl = ob_ue(b), sc = ob_ue(b);
+            int lim = sps->bit_depth > 10 ? sps->bit_depth - 10 : 0;
+            if (sl > (uint32_t)lim || sc > (uint32_t)lim) return -1;
+            p->sao_scale_luma = (int)sl;
+            p->sao_scale_chroma = (int)sc;
+        }
+    }
     p->valid = 1;
     return 0;
 }
@@ -398,6 +538,9 @@ typedef struct {
     uint8_t ctx[NUM_CTX];
     uint8_t ctx_wpp[NUM_CTX];
     uint8_t ctx_ds[NUM_CTX]; /* end of previous slice segment (dependent slices) */
+    /* StatCoeff (persistent_rice_adaptation, 9.3.2.2): initialised, stored and synchronised with
+     * the context variables (FFmpeg cabac_init_state / ff_hevc_save_states / load_states) */
+    int stat[4], stat_wpp[4], stat_ds[4];
     int have_ds;
     int qp_y, qp_pred_prev, is_qpd_coded, qpd_val, first_qg, qg_pred, last_cu_qp;
     int cu_bypass;
@@ -439,6 +582,7 @@ static void init_contexts(Dec *d, int qp) {
         int st = mps ? pre - 64 : 63 - pre;
         d->ctx[i] = (uint8_t)((st << 1) | mps);
     }
+    memset(d->stat, 0, sizeof(d->stat));
 }
 
 static inline int dec_bin(Dec *d, int ctx) { return oc_decision(&d->cc, &d->ctx[ctx]); }
@@ -550,7 +694,7 @@ static void intra_pred(Dec *d, int c, int x0, int y0, int log2n, int mode) {
     uint16_t *pl = d->pl[c];
     const int st = d->st[c];
     /* ref samples: p[-1][-1+k] for k=0..2n (left incl corner), p[-1+k][-1] (top incl corner) */
-    int ref_l[129], ref_t[129]; /* ref_l[k] = p[-1][k-1] k=0..2n ; ref_t[k] = p[k-1][-1] */
+    int ref_l[129] = {0}, ref_t[129] = {0}; /* ref_l[k] = p[-1][k-1] k=0..2n ; ref_t[k] = p[k-1][-1] */
     int av_l[129], av_t[129];
     int xl = x0 << sh, yl = y0 << sh; /* current luma location */
     int cnt = 0;
@@ -591,8 +735,8 @@ static void intra_pred(Dec *d, int c, int x0, int y0, int log2n, int mode) {
         for (int k = 1; k <= 2 * n; k++) ref_t[k] = seq[m++];
         ref_t[0] = ref_l[0];
     }
-    /* 8.4.4.2.3 filtering (luma only for 4:2:0) */
-    if (c == 0 && mode != 1 && n != 4) {
+    /* 8.4.4.2.3 filtering (luma only for 4:2:0; none with RExt intra_smoothing_disabled_flag) */
+    if (c == 0 && mode != 1 && n != 4 && !d->s->smoothing_disabled) {
         int mdist = abs(mode - 26) < abs(mode - 10) ? abs(mode - 26) : abs(mode - 10);
         int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
         if (mode == 0 || mdist > thr) {
@@ -746,8 +890,14 @@ static void residual_coding(Dec *d, int x0, int y0, int log2n, int c, int pred_m
     int16_t *coef = d->coeff;
     memset(coef, 0, sizeof(int16_t) * n * n);
     int tskip = 0;
-    if (d->p->transform_skip && !d->cu_bypass && log2n <= 2) tskip = dec_bin(d, C_TSKIP + (c ? 1 : 0));
+    if (d->p->transform_skip && !d->cu_bypass && log2n <= d->p->log2_max_ts) tskip = dec_bin(d, C_TSKIP + (c ? 1 : 0));
     *tskip_out = tskip;
+    const Sps *sps = d->s;
+    /* RExt: transform-skip / bypass blocks use one significance context per component */
+    const int ts_ctx = sps->ts_context && (tskip || d->cu_bypass);
+    /* implicit RDPCM (intra, transform skip, mode 10 / 26) turns sign data hiding off */
+    const int rdpcm_ts = sps->implicit_rdpcm && tskip && (pred_mode == 10 || pred_mode == 26);
+    const int sb_type = 2 * (c == 0 ? 1 : 0) + ((tskip || d->cu_bypass) ? 1 : 0);
     int lx = decode_last_prefix(d, C_LAST_X, log2n, c);
     int ly = decode_last_prefix(d, C_LAST_Y, log2n, c);
     if (lx > 3) {
@@ -814,7 +964,9 @@ static void residual_coding(Dec *d, int x0, int y0, int log2n, int c, int pred_m
             int xC = (xs << 2) + xp, yC = (ys << 2) + yp;
             if (csbf[xs][ys] && (nn > 0 || !infer_dc)) {
                 int sigCtx;
-                if (log2n == 2) {
+                if (ts_ctx) {
+                    sigCtx = c == 0 ? 42 : 16;
+                } else if (log2n == 2) {
                     static const uint8_t ctxIdxMap[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
                     sigCtx = ctxIdxMap[(yC << 2) + xC];
                 } else if (xC + yC == 0) {
@@ -866,11 +1018,14 @@ static void residual_coding(Dec *d, int x0, int y0, int log2n, int c, int pred_m
             if (lastSig == -1) lastSig = nn;
             firstSig = nn;
         }
-        int signHidden = d->cu_bypass ? 0 : (lastSig - firstSig > 3);
+        int signHidden = (d->cu_bypass || rdpcm_ts) ? 0 : (lastSig - firstSig > 3);
         if (lastG1Pos != -1) g2[lastG1Pos] = dec_bin(d, C_GT2 + ctxSet + (c ? 4 : 0));
         for (int nn = 15; nn >= 0; nn--)
             if (sig[nn] && (!sign_hiding_en || !signHidden || nn != firstSig)) sgn[nn] = dec_byp(d);
-        int numSig = 0, sumAbs = 0, rice = 0;
+        /* Rice parameter: 0, or StatCoeff[sbType] / 4 with persistent_rice_adaptation, which also
+         * leaves it uncapped (FFmpeg hevc_cabac.c) and updates StatCoeff from the sub-block's
+         * first coeff_abs_level_remaining (9.3.3.11) */
+        int numSig = 0, sumAbs = 0, rice = sps->persistent_rice ? d->stat[sb_type] / 4 : 0, stat_done = 0;
         for (int nn = 15; nn >= 0; nn--) {
             if (!sig[nn]) continue;
             int base = 1 + g1[nn] + g2[nn];
@@ -878,7 +1033,13 @@ static void residual_coding(Dec *d, int x0, int y0, int log2n, int c, int pred_m
             if (base == ((numSig < 8) ? ((nn == lastG1Pos) ? 3 : 2) : 1)) {
                 int rem = decode_alr(d, rice);
                 lvl = base + rem;
-                if (lvl > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
+                if (lvl > 3 * (1 << rice)) rice = sps->persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+                if (sps->persistent_rice && !stat_done) {
+                    int ri = d->stat[sb_type] / 4;
+                    if (rem >= (3 << ri)) d->stat[sb_type]++;
+                    else if (2 * rem < (1 << ri) && d->stat[sb_type] > 0) d->stat[sb_type]--;
+                    stat_done = 1;
+                }
             }
             int v = sgn[nn] ? -lvl : lvl;
             if (sign_hiding_en && signHidden) {
@@ -894,15 +1055,29 @@ static void residual_coding(Dec *d, int x0, int y0, int log2n, int c, int pred_m
     (void)y0;
 }
 
-/* scale + transform + add (8.6.2-8.6.4) */
+/* RExt residual DPCM (8.6.8 / FFmpeg hevcdsp transform_rdpcm): accumulate down the columns
+ * (vertical, mode 26) or along the rows (mode 10), in int16 as FFmpeg's coefficient buffer */
+static void rdpcm(int *r, int n, int vertical) {
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            if (vertical ? y == 0 : x == 0) continue;
+            int prev = vertical ? r[(y - 1) * n + x] : r[y * n + x - 1];
+            r[y * n + x] = (int16_t)(r[y * n + x] + prev);
+        }
+}
+
+/* scale + transform + add (8.6.2-8.6.4); mode: the TB's intra prediction mode (RExt RDPCM) */
 static void reconstruct_residual(Dec *d, int c, int x0, int y0, int log2n, int qp, int tskip,
-                                 int dst) {
+                                 int dst, int mode) {
     const int n = 1 << log2n;
     const int bd = c ? d->bdc : d->bd;
     const int maxv = (1 << bd) - 1;
+    const int hv = mode == 10 || mode == 26;
     int r[32 * 32];
     if (d->cu_bypass) {
         for (int i = 0; i < n * n; i++) r[i] = d->coeff[i];
+        /* FFmpeg: bypass blocks take implicit RDPCM but no transform-skip rotation */
+        if (d->s->implicit_rdpcm && hv) rdpcm(r, n, mode == 26);
     } else {
         static const int ls[6] = {40, 45, 51, 57, 64, 72};
         int dd[32 * 32];
@@ -931,8 +1106,18 @@ static void reconstruct_residual(Dec *d, int c, int x0, int y0, int log2n, int q
                 dd[y * n + x] = (int)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
             }
         if (tskip) {
-            int bdS = 20 - bd;
-            for (int i = 0; i < n * n; i++) r[i] = (dd[i] * 128 + (1 << (bdS - 1))) >> bdS;
+            /* rotation (RExt, 4x4): r[x][y] = d[n-1-x][n-1-y] */
+            if (d->s->ts_rotation && n == 4)
+                for (int i = 0; i < 8; i++) {
+                    int t = dd[i];
+                    dd[i] = dd[15 - i];
+                    dd[15 - i] = t;
+                }
+            /* tsShift = 5 + log2n, bdShift = 20 - bitDepth; FFmpeg dequant(): one shift by
+             * 15 - bitDepth - log2n (left when negative) on the int16 coefficient */
+            int sh = 15 - bd - log2n;
+            for (int i = 0; i < n * n; i++) r[i] = sh > 0 ? (dd[i] + (1 << (sh - 1))) >> sh : (int16_t)(dd[i] * (1 << -sh));
+            if (d->s->implicit_rdpcm && hv) rdpcm(r, n, mode == 26);
         } else {
             inv_transform(dd, r, n, dst, bd);
         }
@@ -1029,7 +1214,7 @@ static void transform_unit_recon(Dec *d, CuCtx *cu, int x0, int y0, int xb, int 
     intra_pred(d, 0, x0, y0, log2n, mode);
     if (cbf_l) {
         residual_coding(d, x0, y0, log2n, 0, mode, &tskip);
-        reconstruct_residual(d, 0, x0, y0, log2n, qpy, tskip, log2n == 2 && !tskip);
+        reconstruct_residual(d, 0, x0, y0, log2n, qpy, tskip, log2n == 2 && !tskip, mode);
     }
     mark_tu_edges(d, x0, y0, 1 << log2n);
     int cm = cu->intra_chroma_mode;
@@ -1038,24 +1223,24 @@ static void transform_unit_recon(Dec *d, CuCtx *cu, int x0, int y0, int xb, int 
         intra_pred(d, 1, xc, yc, l2, cm);
         if (cbf_cb) {
             residual_coding(d, xc, yc, l2, 1, cm, &tskip);
-            reconstruct_residual(d, 1, xc, yc, l2, qpc[0], tskip, 0);
+            reconstruct_residual(d, 1, xc, yc, l2, qpc[0], tskip, 0, cm);
         }
         intra_pred(d, 2, xc, yc, l2, cm);
         if (cbf_cr) {
             residual_coding(d, xc, yc, l2, 2, cm, &tskip);
-            reconstruct_residual(d, 2, xc, yc, l2, qpc[1], tskip, 0);
+            reconstruct_residual(d, 2, xc, yc, l2, qpc[1], tskip, 0, cm);
         }
     } else if (blk == 3) {
         int xc = xb >> 1, yc = yb >> 1;
         intra_pred(d, 1, xc, yc, 2, cm);
         if (cbf_cb) {
             residual_coding(d, xc, yc, 2, 1, cm, &tskip);
-            reconstruct_residual(d, 1, xc, yc, 2, qpc[0], tskip, 0);
+            reconstruct_residual(d, 1, xc, yc, 2, qpc[0], tskip, 0, cm);
         }
         intra_pred(d, 2, xc, yc, 2, cm);
         if (cbf_cr) {
             residual_coding(d, xc, yc, 2, 2, cm, &tskip);
-            reconstruct_residual(d, 2, xc, yc, 2, qpc[1], tskip, 0);
+            reconstruct_residual(d, 2, xc, yc, 2, qpc[1], tskip, 0, cm);
         }
     }
 }
@@ -1256,7 +1441,9 @@ static void parse_sao(Dec *d, int rx, int ry) {
             while (v < cmax && dec_byp(d)) v++;
             abs_[i] = v;
         }
-        int shift = bd - (bd < 10 ? bd : 10);
+        /* SaoOffsetVal = offset << log2OffsetScale (FFmpeg hls_sao_param: the PPS range extension's
+         * log2_sao_offset_scale, 0 without it -- not v1's bitDepth - Min(bitDepth, 10)) */
+        int shift = c ? d->p->sao_scale_chroma : d->p->sao_scale_luma;
         if (sp->type[c] == 1) {
             for (int i = 0; i < 4; i++) {
                 if (abs_[i] && dec_byp(d)) abs_[i] = -abs_[i];
@@ -1386,10 +1573,15 @@ static void ctb_start_contexts(Dec *d, SliceHdr *sh, int ctbAddrRs, int ctbAddrT
     } else if (row_start) {
         int xr = x0 + d->ctbs, yr = y0 - d->ctbs;
         /* the CTB must belong to the current slice for 6.4.1: mark it first */
-        if (xr < d->W && yr >= 0 && avail(d, x0, y0, xr, yr)) memcpy(d->ctx, d->ctx_wpp, NUM_CTX);
-        else init_contexts(d, sh->slice_qp);
+        if (xr < d->W && yr >= 0 && avail(d, x0, y0, xr, yr)) {
+            memcpy(d->ctx, d->ctx_wpp, NUM_CTX);
+            memcpy(d->stat, d->stat_wpp, sizeof(d->stat));
+        } else {
+            init_contexts(d, sh->slice_qp);
+        }
     } else if (sh->dependent && d->have_ds) {
         memcpy(d->ctx, d->ctx_ds, NUM_CTX);
+        memcpy(d->stat, d->stat_ds, sizeof(d->stat));
     } else {
         init_contexts(d, sh->slice_qp);
     }
@@ -1431,7 +1623,10 @@ static int decode_slice_data(Dec *d, int shi) {
             int second = 0;
             for (int i = 0; i < d->p->ntc; i++)
                 if (rx == d->col_bd[i] + 1 && d->col_bd[i] + 1 < d->col_bd[i + 1]) second = 1;
-            if (second) memcpy(d->ctx_wpp, d->ctx, NUM_CTX);
+            if (second) {
+                memcpy(d->ctx_wpp, d->ctx, NUM_CTX);
+                memcpy(d->stat_wpp, d->stat, sizeof(d->stat));
+            }
         }
         ctbAddrTs++;
         if (end) break;
@@ -1452,6 +1647,7 @@ static int decode_slice_data(Dec *d, int shi) {
         ctbAddrRs = nextRs;
     }
     memcpy(d->ctx_ds, d->ctx, NUM_CTX);
+    memcpy(d->stat_ds, d->stat, sizeof(d->stat));
     d->have_ds = 1;
     return 0;
 }
@@ -1518,6 +1714,7 @@ static int parse_slice_header(Dec *d, OraBits *b, int nal_type, SliceHdr *sh, co
             sh->cb_qp_offset = ob_se(b);
             sh->cr_qp_offset = ob_se(b);
         }
+        if (p->cqo_list_enabled) sh->cu_chroma_qp_offset_enabled = (int)ob_u(b, 1);
         int override = 0;
         if (p->deblock_override) override = (int)ob_u(b, 1);
         sh->deblock_disabled = p->deblock_disabled;
@@ -1791,10 +1988,13 @@ int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture 
         OraBits b = {rbsp, rn, 0};
         if (type == 33) {
             if (have_pic) break;
-            if (parse_sps(&b, d->sps) < 0) { ret = -2; goto done; }
+            {
+                int e = parse_sps(&b, d->sps);
+                if (e < 0) { ret = e == -11 ? -11 : -2; goto done; }
+            }
         } else if (type == 34) {
             if (have_pic) break;
-            if (parse_pps(&b, d->pps) < 0) { ret = -3; goto done; }
+            if (parse_pps(&b, d->pps, d->sps) < 0) { ret = -3; goto done; }
         } else if (type <= 21) {
             if (type >= 10 && type <= 15) continue; /* reserved */
             int first = (rbsp[0] >> 7) & 1;
@@ -1804,6 +2004,7 @@ int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture 
             SliceHdr *sh = &d->sh[d->nsh];
             int r = parse_slice_header(d, &b, type, sh, prev);
             if (r < 0) { ret = r == -2 ? -5 : -6; goto done; }
+            if (sh->cu_chroma_qp_offset_enabled) { ret = -12; goto done; } /* unsupported RExt tool */
             if (!have_pic) {
                 d->p = &d->pps[sh->pps_id];
                 d->s = &d->sps[d->p->sps_id];
@@ -1828,7 +2029,10 @@ int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture 
     /* crop */
     {
         const Sps *s = d->s;
-        int w = d->W - s->conf_l - s->conf_r, h = d->H - s->conf_t - s->conf_b;
+        /* decode.c apply_cropping: the left offset as av_frame_apply_cropping aligns it (4:2:0
+         * offsets are even: never AVERROR_BUG) */
+        const int cl = ora_ff_crop_left(s->conf_l, d->bd > 8 ? 2 : 1);
+        int w = d->W - cl - s->conf_r, h = d->H - s->conf_t - s->conf_b;
         out->width = w;
         out->height = h;
         out->bit_depth = d->bd;
@@ -1839,7 +2043,7 @@ int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture 
             out->stride[c] = cw;
             for (int y = 0; y < ch; y++)
                 memcpy(out->planes[c] + (size_t)y * cw,
-                       d->pl[c] + (size_t)(y + (s->conf_t >> sh)) * d->st[c] + (s->conf_l >> sh), (size_t)cw * 2);
+                       d->pl[c] + (size_t)(y + (s->conf_t >> sh)) * d->st[c] + (cl >> sh), (size_t)cw * 2);
         }
     }
     ret = 0;

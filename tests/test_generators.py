@@ -59,6 +59,10 @@ H264_CASES = [
     ("sm_pps_cavlc", 96, 64, 8, 20, ["--sm", "3", "--cavlc", "1"]),
     ("nonidr_first", 96, 64, 8, 26, ["--nonidr", "1", "--slices", "2"]),
     ("delay2", 96, 64, 8, 26, ["--delay", "2"]),
+    # 4:0:0: CABAC / CAVLC, 8- and 10-bit, PCM, lossless
+    ("mono_cabac_pcm", 128, 96, 8, 24, ["--mono", "1", "--pcm", "1"]),
+    ("mono_cavlc_10bit", 96, 64, 10, 20, ["--mono", "1", "--cavlc", "1"]),
+    ("mono_lossless_cavlc", 96, 64, 8, 0, ["--mono", "1", "--lossless", "1", "--cavlc", "1"]),
 ]
 
 
@@ -80,6 +84,13 @@ HEVC_CASES = [
     ("cra_first_slices", 128, 96, 8, 27, ["--nut", "21", "--slices", "1"]),
     ("bla_first_delay", 96, 64, 8, 27, ["--nut", "16", "--delay", "2"]),
     ("delay1", 136, 72, 8, 30, ["--delay", "1"]),
+    # 9 / 12 bits and the range-extension tools, fresh content each run
+    ("bits9_pcm", 96, 64, 9, 25, ["--pcm", "1"]),
+    ("bits12_bypass", 128, 64, 12, 20, ["--bypass", "1", "--depth", "2"]),
+    ("rext_all_12bit", 128, 96, 12, 18, ["--rext", "167", "--maxts", "5", "--saoscale", "1,2", "--bypass", "1"]),
+    ("rext_ts_rdpcm_wpp", 128, 96, 8, 24, ["--profile", "4", "--rext", "135", "--maxts", "3", "--wpp", "1", "--ctb", "16"]),
+    ("rext_nosmooth_rice_10bit", 128, 96, 10, 16, ["--profile", "4", "--rext", "160", "--slices", "1"]),
+    ("vui_ppsext_main", 96, 64, 8, 27, ["--vui", "1", "--ppsext", "1", "--maxts", "5"]),
 ]
 
 

@@ -58,6 +58,8 @@ def test_malformed_parameter_sets(engine):
         else:
             assert o is None, e["file"]
             assert engine.frame_error(i), e["file"]  # a per-picture message, not the engine-wide one
+            if "message" in e:
+                assert e["message"] in engine.frame_error(i), (e["file"], engine.frame_error(i))
 
 
 def test_strict_reference_mode_on_decoder_delay_streams(engine):

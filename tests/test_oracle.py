@@ -72,3 +72,15 @@ def test_h264_transcode_matches_fixture_jpeg():
     """The golden img01.h264.jpeg was written by the x86_64 build: byte-exact,
     COM 'Lavc58.117.101' included."""
     assert O.transcode(read(golden("img01.h264"))) == read(golden("img01.h264.jpeg"))
+
+
+def test_oracle_mono_chroma_is_half_range():
+    """4:0:0 H.264 (tests/golden/h264/a41..a45): FFmpeg decodes into yuv420p with every chroma
+    sample 1 << (BitDepth - 1) (DC_128 prediction, I_PCM memset), so the oracle's chroma planes are
+    flat at that value (parity unpinned: no reference-held monochrome fixture)."""
+    import glob
+    import os
+    for p in sorted(glob.glob(golden("h264/a4[1-5]_*mono*.h264"))):
+        y, u, v, bd = O.decode(read(p), 264)
+        assert (u == 1 << (bd - 1)).all() and (v == 1 << (bd - 1)).all(), os.path.basename(p)
+        assert y.std() > 1.0  # a real luma picture

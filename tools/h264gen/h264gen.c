@@ -20,6 +20,8 @@
  *   --sm 0..3 (scaling matrices, see write_matrices)
  *   --nonidr 1 (first picture: non-IDR I, nal_unit_type 1)
  *   --delay K (VUI max_num_reorder_frames = K, then K + 1 all-skip P pictures)
+ *   --mono 1 (4:0:0, chroma_format_idc 0: no chroma syntax; the reconstruction's chroma planes are
+ *             1 << (bitdepth - 1), FFmpeg's output for monochrome streams)
  */
 #include <math.h>
 #include <stdint.h>
@@ -184,7 +186,7 @@ typedef struct {
 } Mb;
 
 typedef struct {
-    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless, mbaff, cur_field, paff, onefield;
+    int W, H, outW, outH, mbw, mbh, bd, qp, t8x8, pcm, qpdelta, slice_rows, alpha, beta, dbidc, cqp, cqp2, cavlc, sm, nonidr, delay, firstmb, vuireorder, vuicpb, ilsps, lossless, mbaff, cur_field, paff, onefield, mono;
     long long rawcrop[4];
     uint16_t *src[3], *rec[3];
     int st[3];
@@ -771,8 +773,8 @@ static void encode_mb(G *g) {
             recv_put(g, 0, gx + x, gy + y, s);
         }
         for (int c = 1; c < 3; c++) for (int y = 0; y < 8; y++) for (int x = 0; x < 8; x++) {
-            int s = srcv(g, c, gx / 2 + x, gy / 2 + y);
-            bw_put(g->ce.bw, (uint32_t)s, g->bd);
+            int s = srcv(g, c, gx / 2 + x, gy / 2 + y); /* --mono: the flat chroma source, not coded */
+            if (!g->mono) bw_put(g->ce.bw, (uint32_t)s, g->bd);
             recv_put(g, c, gx / 2 + x, gy / 2 + y, s);
         }
         if (!g->cavlc) { BW *bw = g->ce.bw; ce_start(&g->ce, bw); }
@@ -812,6 +814,7 @@ static void encode_mb(G *g) {
     int at = B != NULL, al = A != NULL, ad = nb(g, -1, -1) != NULL;
     int cpm = rndn(4);
     if ((cpm == 1 && !al) || (cpm == 2 && !at) || (cpm == 3 && !(at && al && ad))) cpm = 0;
+    if (g->mono) cpm = 0; /* no intra_chroma_pred_mode: the flat chroma source predicts exactly */
     /* chroma residual is computed after luma (recon order doesn't matter: chroma pred uses neighbour MBs only) */
     int qpc[2];
     for (int c = 0; c < 2; c++) qpc[c] = chroma_qp(clip3(-6 * (g->bd - 8), 51, qp_use + (c ? g->cqp2 : g->cqp))) + 6 * (g->bd - 8);
@@ -937,8 +940,8 @@ static void encode_mb(G *g) {
         }
         m->cbp = cbp;
     }
-    /* chroma pred mode */
-    {
+    /* chroma pred mode (none in 4:0:0) */
+    if (!g->mono) {
         int c2 = (A && A->mb_type != 25 && A->cpm != 0) + (B && B->mb_type != 25 && B->cpm != 0);
         if (g->cavlc) {
             bw_ue(g->ce.bw, (uint32_t)cpm);
@@ -949,8 +952,10 @@ static void encode_mb(G *g) {
         m->cpm = cpm;
     }
     if (!is16 && g->cavlc) {
+        static const uint8_t k_gray[16] = {15, 0, 7, 11, 13, 14, 3, 5, 10, 12, 1, 2, 4, 8, 6, 9}; /* Table 9-4, 4:0:0 */
         int cn = 0;
-        while (kCbpIntra[cn] != m->cbp) cn++;
+        if (g->mono) while (k_gray[cn] != m->cbp) cn++;
+        else while (kCbpIntra[cn] != m->cbp) cn++;
         bw_ue(g->ce.bw, (uint32_t)cn);
     } else if (!is16) {
         int cbp = m->cbp;
@@ -967,8 +972,10 @@ static void encode_mb(G *g) {
             bin(g, 73 + ca + 2 * cb, (cbp >> b8) & 1);
         }
         int ac = A ? (A->mb_type == 25 ? 2 : (A->cbp >> 4)) : 0, bc = B ? (B->mb_type == 25 ? 2 : (B->cbp >> 4)) : 0;
-        bin(g, 77 + (ac > 0) + 2 * (bc > 0), cbp_c != 0);
-        if (cbp_c) bin(g, 77 + 4 + (ac == 2) + 2 * (bc == 2), cbp_c == 2);
+        if (!g->mono) {
+            bin(g, 77 + (ac > 0) + 2 * (bc > 0), cbp_c != 0);
+            if (cbp_c) bin(g, 77 + 4 + (ac == 2) + 2 * (bc == 2), cbp_c == 2);
+        }
     }
     /* mb_qp_delta: the levels were quantised at qp_use; if the MB codes a
      * delta it must be qp_use - cur_qp, else QP stays cur_qp (only possible
@@ -1140,7 +1147,7 @@ static void write_sps(FILE *f, G *g, int profile) {
     bw_put(&b, 40, 8);
     bw_ue(&b, 0);
     if (profile >= 100) {
-        bw_ue(&b, 1);
+        bw_ue(&b, g->mono ? 0 : 1); /* chroma_format_idc */
         bw_ue(&b, (uint32_t)(g->bd - 8)); bw_ue(&b, (uint32_t)(g->bd - 8));
         bw_put(&b, (uint32_t)g->lossless, 1); /* qpprime_y_zero_transform_bypass_flag (--lossless) */
         g_sps_m_on = g->sm == 1 || g->sm == 2;
@@ -1167,7 +1174,9 @@ static void write_sps(FILE *f, G *g, int profile) {
         for (int i = 0; i < 4; i++) bw_ue(&b, (uint32_t)g->rawcrop[i]);
     } else {
         bw_put(&b, (uint32_t)crop, 1);
-        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / 2); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / (g->ilsps ? 4 : 2)); }
+        /* CropUnitX / CropUnitY: 2 / 2 (2 - frame_mbs_only) in 4:2:0, 1 / 2 - frame_mbs_only in 4:0:0 */
+        const int ux = g->mono ? 1 : 2, uy = (g->mono ? 1 : 2) * (g->ilsps ? 2 : 1);
+        if (crop) { bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->W - g->outW) / ux); bw_ue(&b, 0); bw_ue(&b, (uint32_t)(g->H - g->outH) / uy); }
     }
     /* --vuireorder K: the VUI's reorder depth alone (no extra pictures; malformed-SPS vectors use
      * K > 16); --vuicpb K: a NAL HRD with cpb_cnt_minus1 = K (K > 31 is malformed) */
@@ -1266,12 +1275,13 @@ int main(int argc, char **argv) {
     /* --lossless 1: High 4:4:4 Predictive (profile_idc 244) with qpprime_y_zero_transform_bypass_flag,
      * every macroblock at QP'Y 0 (TransformBypassModeFlag), residual DPCM for H / V predictions */
     g->lossless = opt_int(argc, argv, "--lossless", 0);
+    g->mono = opt_int(argc, argv, "--mono", 0);
     if (g->lossless) { g->qp = -6 * (g->bd - 8); g->qpdelta = 0; }
     g->rawcrop[0] = -1;
     if (opt_str(argc, argv, "--crop"))
         sscanf(opt_str(argc, argv, "--crop"), "%lld,%lld,%lld,%lld", &g->rawcrop[0], &g->rawcrop[1], &g->rawcrop[2], &g->rawcrop[3]);
     if (g->delay > 6) { fprintf(stderr, "--delay <= 6 (4-bit POC lsb)\n"); return 2; }
-    int profile = opt_int(argc, argv, "--profile", (g->lossless || g->bd > 10) ? 244 : g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm ? 100 : 77));
+    int profile = opt_int(argc, argv, "--profile", (g->lossless || g->bd > 10) ? 244 : g->bd > 8 ? 110 : (g->t8x8 || g->cqp2 != g->cqp || g->sm || g->mono ? 100 : 77));
     g_lim = 1 << (7 + g->bd);
     g->W = (g->outW + 15) & ~15; g->H = g->ilsps ? (g->outH + 31) & ~31 : (g->outH + 15) & ~15;
     if (g->ilsps && (g->H - g->outH) % 4) { fprintf(stderr, "--ilsps: the height must crop in 4-row units\n"); return 2; }
@@ -1288,6 +1298,7 @@ int main(int argc, char **argv) {
             g->src[c][y * w + x] = (uint16_t)(v < 0 ? 0 : v);
         }
         for (int y = 0; y < h; y++) for (int x = 0; x < w; x++) g->src[c][y * w + x] = g->src[c][(y < ih ? y : ih - 1) * w + (x < iw ? x : iw - 1)];
+        if (c && g->mono) for (int i = 0; i < w * h; i++) g->src[c][i] = (uint16_t)(1 << (g->bd - 1));
     }
     fclose(fi);
     g->mb = (Mb *)calloc((size_t)g->mbw * g->mbh, sizeof(Mb));

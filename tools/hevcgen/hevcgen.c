@@ -21,6 +21,18 @@
  *            --depth D (max_transform_hierarchy_depth_intra) --ctb 16|32|64
  *            --beta B --tc T --recon out.yuv --cbqp N --crqp N
  *            --sl 0..4 (scaling lists, see write_scaling_list_data)
+ *   range extensions (H.265 v2): --profile P (general_profile_idc; default 1 / 2 / 4 for
+ *            8 / 10 / other bit depths), --vui 1 (a VUI with HRD parameters),
+ *            --rext MASK (sps_range_extension flags: 1 transform_skip_rotation, 2
+ *            transform_skip_context, 4 implicit_rdpcm, 8 explicit_rdpcm, 16
+ *            extended_precision_processing, 32 intra_smoothing_disabled, 64
+ *            high_precision_offsets, 128 persistent_rice_adaptation, 256
+ *            cabac_bypass_alignment), --maxts L (log2_max_transform_skip_block_size),
+ *            --saoscale L,C (log2_sao_offset_scale luma, chroma), --cqo 1|2 (chroma QP offset
+ *            list in the PPS; 2: also enabled in the slice header), --ppsext 1 (write the
+ *            pps_range_extension even when the profile is not RExt: decoders then ignore it)
+ *   The encoder uses the tools as the decoder will see them; streams with extended precision,
+ *   bypass alignment or slice-level chroma QP offsets are only for rejection tests.
  */
 #include <math.h>
 #include <stdint.h>
@@ -213,7 +225,14 @@ typedef struct {
     int delay; /* sps_max_num_reorder_pics; the stream then carries delay + 1 all-skip P pictures */
     long long rawconf[4]; /* --conf: raw conformance window offsets (-1: derived from the size) */
     int wdelta;           /* --wdelta: subtracted from the signalled picture width */
+    int profile, vui, rext, maxts, sao_scale[2], cqo, ppsext;
+    int eff_maxts;        /* log2 max transform-skip size the decoder uses (2 without the PPS range ext) */
 } Opt;
+#define RX_ROT 1
+#define RX_CTX 2
+#define RX_RDPCM 4
+#define RX_NOSMOOTH 32
+#define RX_RICE 128
 
 typedef struct {
     Opt o;
@@ -232,6 +251,7 @@ typedef struct {
     int qg_pred, qpd_val, is_qpd_coded, first_qg, last_cu_qp, qp_y, target_qp;
     int cu_bypass;
     int qpbd;
+    int stat[4]; /* StatCoeff (persistent_rice_adaptation) */
 } G;
 
 static int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -245,6 +265,7 @@ static void init_contexts(G *g, int qp) {
         int mps = pre <= 63 ? 0 : 1;
         g->ctx[i] = (uint8_t)(((mps ? pre - 64 : 63 - pre) << 1) | mps);
     }
+    memset(g->stat, 0, sizeof(g->stat));
 }
 
 static int zs(G *g, int x, int y) {
@@ -346,7 +367,7 @@ static void build_refs(G *g, int c, int x0, int y0, int log2n, Refs *R) {
 
 static void filter_refs(G *g, int c, int mode, Refs *R) {
     const int n = R->n, bd = g->o.bd;
-    if (c != 0 || mode == 1 || n == 4) return;
+    if (c != 0 || mode == 1 || n == 4 || (g->o.rext & RX_NOSMOOTH)) return;
     int d26 = abs(mode - 26), d10 = abs(mode - 10), md = d26 < d10 ? d26 : d10;
     int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
     if (!(mode == 0 || md > thr)) return;
@@ -486,7 +507,10 @@ static void enc_alr(G *g, int v, int rice) {
 /* coef[y*n+x] levels; mode for scan; writes syntax */
 static void enc_residual(G *g, int *coef, int log2n, int c, int pred_mode, int tskip) {
     const int n = 1 << log2n;
-    if (g->o.tskip && !g->cu_bypass && log2n <= 2) ce_bin(&g->ce, &g->ctx[C_TSKIP + (c ? 1 : 0)], tskip);
+    if (g->o.tskip && !g->cu_bypass && log2n <= g->o.eff_maxts) ce_bin(&g->ce, &g->ctx[C_TSKIP + (c ? 1 : 0)], tskip);
+    const int ts_ctx = (g->o.rext & RX_CTX) && (tskip || g->cu_bypass);
+    const int rdpcm_ts = (g->o.rext & RX_RDPCM) && tskip && (pred_mode == 10 || pred_mode == 26);
+    const int rice_on = (g->o.rext & RX_RICE) != 0, sb_type = 2 * (c == 0) + ((tskip || g->cu_bypass) ? 1 : 0);
     int scanIdx = 0;
     if (log2n == 2 || (log2n == 3 && c == 0)) {
         if (pred_mode >= 6 && pred_mode <= 14) scanIdx = 2;
@@ -548,7 +572,9 @@ static void enc_residual(G *g, int *coef, int log2n, int c, int pred_mode, int t
                 int xC = (xs << 2) + xp, yC = (ys << 2) + yp;
                 if (nn > 0 || !infer_dc) {
                     int sigCtx;
-                    if (log2n == 2) {
+                    if (ts_ctx) {
+                        sigCtx = c == 0 ? 42 : 16;
+                    } else if (log2n == 2) {
                         static const uint8_t m[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
                         sigCtx = m[(yC << 2) + xC];
                     } else if (xC + yC == 0) {
@@ -590,7 +616,7 @@ static void enc_residual(G *g, int *coef, int log2n, int c, int pred_mode, int t
             if (lastSig == -1) lastSig = nn;
             firstSig = nn;
         }
-        int signHidden = !g->cu_bypass && (lastSig - firstSig > 3);
+        int signHidden = !g->cu_bypass && !rdpcm_ts && (lastSig - firstSig > 3);
         int g2 = 0;
         if (lastG1 != -1) {
             g2 = abs(lv[lastG1]) > 2;
@@ -598,14 +624,20 @@ static void enc_residual(G *g, int *coef, int log2n, int c, int pred_mode, int t
         }
         for (int nn = 15; nn >= 0; nn--)
             if (lv[nn] && (!g->o.sdh || !signHidden || nn != firstSig)) ce_byp(&g->ce, lv[nn] < 0);
-        int numSig = 0, rice = 0;
+        int numSig = 0, rice = rice_on ? g->stat[sb_type] / 4 : 0, stat_done = 0;
         for (int nn = 15; nn >= 0; nn--) {
             if (!lv[nn]) continue;
             int base = 1 + g1[nn] + (nn == lastG1 ? g2 : 0);
             if (base == ((numSig < 8) ? ((nn == lastG1) ? 3 : 2) : 1)) {
                 int rem = abs(lv[nn]) - base;
                 enc_alr(g, rem, rice);
-                if (abs(lv[nn]) > 3 * (1 << rice)) rice = rice < 4 ? rice + 1 : 4;
+                if (abs(lv[nn]) > 3 * (1 << rice)) rice = rice_on ? rice + 1 : (rice < 4 ? rice + 1 : 4);
+                if (rice_on && !stat_done) { /* StatCoeff update (9.3.3.11) */
+                    int ri = g->stat[sb_type] / 4;
+                    if (rem >= (3 << ri)) g->stat[sb_type]++;
+                    else if (2 * rem < (1 << ri) && g->stat[sb_type] > 0) g->stat[sb_type]--;
+                    stat_done = 1;
+                }
             }
             numSig++;
         }
@@ -616,9 +648,10 @@ static void enc_residual(G *g, int *coef, int log2n, int c, int pred_mode, int t
  * the subblock's absolute sum (decoder rule in residual_coding) by growing
  * the highest-frequency coefficient of the subblock by one.  Applied before
  * reconstruction so encoder and decoder agree. */
-static void sdh_fix(G *g, int *coef, int log2n, int c, int pred_mode) {
+static void sdh_fix(G *g, int *coef, int log2n, int c, int pred_mode, int tskip) {
     const int n = 1 << log2n;
     if (!g->o.sdh || g->cu_bypass) return;
+    if ((g->o.rext & RX_RDPCM) && tskip && (pred_mode == 10 || pred_mode == 26)) return; /* no hiding */
     int scanIdx = 0;
     if (log2n == 2 || (log2n == 3 && c == 0)) {
         if (pred_mode >= 6 && pred_mode <= 14) scanIdx = 2;
@@ -739,6 +772,24 @@ static int sf(int c, int log2n, int i) { return g_sl_on ? g_sf[log2n - 2][c][i] 
 static const int k_qscale[6] = {26214, 23302, 20560, 18396, 16384, 14564};
 static const int k_ls[6] = {40, 45, 51, 57, 64, 72};
 
+/* RExt residual DPCM (8.6.8): accumulate down the columns (mode 26) / along the rows (mode 10),
+ * int16 as in the decoder's coefficient buffer; diff_dpcm is its inverse (encoder side) */
+static void acc_dpcm(int *r, int n, int vertical) {
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            if (vertical ? y == 0 : x == 0) continue;
+            r[y * n + x] = (int16_t)(r[y * n + x] + (vertical ? r[(y - 1) * n + x] : r[y * n + x - 1]));
+        }
+}
+static void diff_dpcm(int *r, int n, int vertical) {
+    for (int y = n - 1; y >= 0; y--)
+        for (int x = n - 1; x >= 0; x--) {
+            if (vertical ? y == 0 : x == 0) continue;
+            r[y * n + x] -= vertical ? r[(y - 1) * n + x] : r[y * n + x - 1];
+        }
+}
+static int uses_rdpcm(G *g, int mode) { return (g->o.rext & RX_RDPCM) && (mode == 10 || mode == 26); }
+
 /* Encode-side processing of one transform block: prediction already in
  * rec; computes levels into coef, reconstructs rec.  Returns cbf. */
 static int code_block(G *g, int c, int x0, int y0, int log2n, int pred_mode, int qp, int *coef, int *tskip_out,
@@ -750,14 +801,19 @@ static int code_block(G *g, int c, int x0, int y0, int log2n, int pred_mode, int
     int nz = 0;
     int tskip = 0;
     int dst = (c == 0 && log2n == 2);
+    (void)maxv;
     if (g->cu_bypass) {
+        if (uses_rdpcm(g, pred_mode)) diff_dpcm(res, n, pred_mode == 26); /* lossless: levels = differences */
         for (int i = 0; i < n * n; i++) { coef[i] = res[i]; nz |= res[i] != 0; }
     } else {
         int tc[1024];
-        if (g->o.tskip && log2n == 2 && rndn(5) == 0) tskip = 1;
+        if (g->o.tskip && log2n <= g->o.eff_maxts && rndn(log2n == 2 ? 5 : 3) == 0) tskip = 1;
         if (tskip) {
+            if (uses_rdpcm(g, pred_mode)) diff_dpcm(res, n, pred_mode == 26); /* open-loop DPCM */
             int shift = 15 - bd - log2n; /* HM: transformSkipShift */
-            for (int i = 0; i < 16; i++) tc[i] = shift >= 0 ? res[i] << shift : res[i] >> -shift;
+            for (int i = 0; i < n * n; i++) tc[i] = shift >= 0 ? res[i] * (1 << shift) : res[i] >> -shift;
+            if ((g->o.rext & RX_ROT) && n == 4)
+                for (int i = 0; i < 8; i++) { int t = tc[i]; tc[i] = tc[15 - i]; tc[15 - i] = t; }
         } else {
             fwd_transform(res, tc, n, log2n, dst, bd);
         }
@@ -765,7 +821,8 @@ static int code_block(G *g, int c, int x0, int y0, int log2n, int pred_mode, int
         long add = (171L << (qbits - 9));
         for (int i = 0; i < n * n; i++) {
             long a = labs((long)tc[i]);
-            int l = (int)((a * k_qscale[qp % 6] * 16 / sf(c, log2n, i) + add) >> qbits);
+            int m = (tskip && n > 4) ? 16 : sf(c, log2n, i);
+            int l = (int)((a * k_qscale[qp % 6] * 16 / m + add) >> qbits);
             if (l > 32767) l = 32767;
             coef[i] = tc[i] < 0 ? -l : l;
             nz |= l != 0;
@@ -776,25 +833,30 @@ static int code_block(G *g, int c, int x0, int y0, int log2n, int pred_mode, int
 }
 
 static void recon_block(G *g, int c, int x0, int y0, int log2n, int qp, const int *coef, int tskip, const int *pred,
-                        int cbf) {
+                        int cbf, int mode) {
     const int n = 1 << log2n, st = g->st[c], bd = g->o.bd, maxv = (1 << bd) - 1;
     int r[1024];
     memset(r, 0, sizeof(int) * n * n);
     if (cbf) {
         if (g->cu_bypass) {
             for (int i = 0; i < n * n; i++) r[i] = coef[i];
+            if (uses_rdpcm(g, mode)) acc_dpcm(r, n, mode == 26);
         } else {
             int d[1024];
             int bdShift = bd + log2n - 5;
             for (int i = 0; i < n * n; i++) {
-                long v = (long)coef[i] * sf(c, log2n, i) * k_ls[qp % 6];
+                int m = (tskip && n > 4) ? 16 : sf(c, log2n, i);
+                long v = (long)coef[i] * m * k_ls[qp % 6];
                 v = (v << (qp / 6)) + (1L << (bdShift - 1));
                 v >>= bdShift;
                 d[i] = (int)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
             }
             if (tskip) {
-                int bdS = 20 - bd;
-                for (int i = 0; i < n * n; i++) r[i] = (d[i] * 128 + (1 << (bdS - 1))) >> bdS;
+                if ((g->o.rext & RX_ROT) && n == 4)
+                    for (int i = 0; i < 8; i++) { int t = d[i]; d[i] = d[15 - i]; d[15 - i] = t; }
+                int sh = 15 - bd - log2n;
+                for (int i = 0; i < n * n; i++) r[i] = sh > 0 ? (d[i] + (1 << (sh - 1))) >> sh : (int16_t)(d[i] * (1 << -sh));
+                if (uses_rdpcm(g, mode)) acc_dpcm(r, n, mode == 26);
             } else {
                 inv_transform(d, r, n, c == 0 && log2n == 2, bd);
             }
@@ -897,8 +959,8 @@ static int tree_compute(G *g, Cu *cu, int x0, int y0, int xb, int yb, int log2n,
     predict(g, 0, lmode, &R, pred);
     int qpy = g->target_qp + g->qpbd;
     t->cbf_l = code_block(g, 0, x0, y0, log2n, lmode, qpy, t->coef_l, &t->tsl, pred);
-    if (t->cbf_l) sdh_fix(g, t->coef_l, log2n, 0, lmode);
-    recon_block(g, 0, x0, y0, log2n, qpy, t->coef_l, t->tsl, pred, t->cbf_l);
+    if (t->cbf_l) sdh_fix(g, t->coef_l, log2n, 0, lmode, t->tsl);
+    recon_block(g, 0, x0, y0, log2n, qpy, t->coef_l, t->tsl, pred, t->cbf_l, lmode);
     int qpc[2];
     for (int k = 0; k < 2; k++) {
         int off = k == 0 ? g->o.cbqp : g->o.crqp;
@@ -913,8 +975,8 @@ static int tree_compute(G *g, Cu *cu, int x0, int y0, int xb, int yb, int log2n,
             int *co = c == 1 ? t->coef_cb : t->coef_cr;
             int *ts = c == 1 ? &t->tscb : &t->tscr;
             int cbf = code_block(g, c, xc, yc, l2, cm, qpc[c - 1], co, ts, pred);
-            if (cbf) sdh_fix(g, co, l2, c, cm);
-            recon_block(g, c, xc, yc, l2, qpc[c - 1], co, *ts, pred, cbf);
+            if (cbf) sdh_fix(g, co, l2, c, cm, *ts);
+            recon_block(g, c, xc, yc, l2, qpc[c - 1], co, *ts, pred, cbf, cm);
             if (c == 1) t->cbf_cb = cbf; else t->cbf_cr = cbf;
         }
     }
@@ -1187,10 +1249,9 @@ static void write_sao(G *g, int rx, int ry, Sao *tab) {
 }
 
 /* ------------------------------------------------------------ parameter sets */
-static void ptl(BW *b, int bd) {
+static void ptl(BW *b, int prof) {
     bw_put(b, 0, 2);          /* profile space */
     bw_put(b, 0, 1);          /* tier */
-    int prof = bd > 8 ? 2 : 1;
     bw_put(b, (uint32_t)prof, 5);
     for (int j = 0; j < 32; j++) bw_put(b, (j == prof || (prof == 1 && j == 2)) ? 1 : 0, 1);
     bw_put(b, 1, 1); /* progressive */
@@ -1203,11 +1264,11 @@ static void ptl(BW *b, int bd) {
     bw_put(b, 123, 8); /* level 4.1 */
 }
 
-static void write_vps(FILE *f, int bd, int delay) {
+static void write_vps(FILE *f, int prof, int delay) {
     BW b; bw_init(&b);
     bw_put(&b, 0, 4); bw_put(&b, 1, 1); bw_put(&b, 1, 1); bw_put(&b, 0, 6); bw_put(&b, 0, 3); bw_put(&b, 1, 1);
     bw_put(&b, 0xffff, 16);
-    ptl(&b, bd);
+    ptl(&b, prof);
     bw_put(&b, 0, 1); /* sub layer ordering info present */
     bw_ue(&b, (uint32_t)(delay ? delay + 1 : 0)); bw_ue(&b, (uint32_t)delay); bw_ue(&b, 0); /* dpb size, reorder, latency */
     bw_put(&b, 0, 6); bw_ue(&b, 0); bw_put(&b, 0, 1); bw_put(&b, 0, 1);
@@ -1219,7 +1280,7 @@ static void write_vps(FILE *f, int bd, int delay) {
 static void write_sps(FILE *f, const Opt *o) {
     BW b; bw_init(&b);
     bw_put(&b, 0, 4); bw_put(&b, 0, 3); bw_put(&b, 1, 1);
-    ptl(&b, o->bd);
+    ptl(&b, o->profile);
     bw_ue(&b, 0);          /* sps id */
     bw_ue(&b, 1);          /* 4:2:0 */
     bw_ue(&b, (uint32_t)(o->CW - o->wdelta)); /* --wdelta: malformed (not a MinCbSize multiple) */
@@ -1258,8 +1319,35 @@ static void write_sps(FILE *f, const Opt *o) {
     bw_put(&b, 0, 1);      /* long term */
     bw_put(&b, 0, 1);      /* temporal mvp */
     bw_put(&b, (uint32_t)o->strong, 1);
-    bw_put(&b, 0, 1);      /* vui */
-    bw_put(&b, 0, 1);      /* extension */
+    bw_put(&b, (uint32_t)o->vui, 1); /* vui_parameters_present_flag */
+    if (o->vui) { /* E.2.1 with every optional part present, HRD (E.2.2) with NAL + VCL parameters */
+        bw_put(&b, 1, 1); bw_put(&b, 255, 8); bw_put(&b, 4, 16); bw_put(&b, 3, 16); /* EXTENDED_SAR 4:3 */
+        bw_put(&b, 1, 1); bw_put(&b, 0, 1);                                         /* overscan */
+        bw_put(&b, 1, 1); bw_put(&b, 5, 3); bw_put(&b, 1, 1);                       /* video signal, full range */
+        bw_put(&b, 1, 1); bw_put(&b, 1, 8); bw_put(&b, 1, 8); bw_put(&b, 1, 8);     /* BT.709 */
+        bw_put(&b, 1, 1); bw_ue(&b, 1); bw_ue(&b, 2);                               /* chroma loc */
+        bw_put(&b, 0, 3);
+        bw_put(&b, 1, 1); bw_ue(&b, 2); bw_ue(&b, 0); bw_ue(&b, 1); bw_ue(&b, 3);   /* default display window */
+        bw_put(&b, 1, 1); bw_put(&b, 1001, 32); bw_put(&b, 60000, 32);              /* timing */
+        bw_put(&b, 1, 1); bw_ue(&b, 0);                                             /* poc proportional */
+        bw_put(&b, 1, 1);                                                           /* hrd_parameters */
+        bw_put(&b, 1, 1); bw_put(&b, 1, 1); bw_put(&b, 1, 1);                       /* nal, vcl, sub_pic */
+        bw_put(&b, 23, 8); bw_put(&b, 4, 5); bw_put(&b, 0, 1); bw_put(&b, 6, 5);
+        bw_put(&b, 3, 4); bw_put(&b, 5, 4); bw_put(&b, 2, 4);
+        bw_put(&b, 23, 5); bw_put(&b, 23, 5); bw_put(&b, 4, 5);
+        bw_put(&b, 0, 1); bw_put(&b, 1, 1); bw_ue(&b, 0);                           /* fixed within cvs */
+        bw_ue(&b, 1);                                                               /* cpb_cnt_minus1 */
+        for (int k = 0; k < 2; k++)
+            for (int j = 0; j < 2; j++) { bw_ue(&b, 1000 + j); bw_ue(&b, 2000); bw_ue(&b, 300); bw_ue(&b, 77); bw_put(&b, j, 1); }
+        bw_put(&b, 1, 1); bw_put(&b, 5, 3);                                         /* bitstream restriction */
+        bw_ue(&b, 0); bw_ue(&b, 2); bw_ue(&b, 1); bw_ue(&b, 15); bw_ue(&b, 15);
+    }
+    bw_put(&b, o->rext != 0, 1); /* sps_extension_present_flag */
+    if (o->rext) {
+        bw_put(&b, 1, 1);        /* sps_range_extension_flag */
+        bw_put(&b, 0, 7);
+        for (int k = 0; k < 9; k++) bw_put(&b, (uint32_t)((o->rext >> k) & 1), 1);
+    }
     bw_trailing(&b);
     write_nal(f, 33, b.buf, b.n);
     free(b.buf);
@@ -1302,7 +1390,20 @@ static void write_pps(FILE *f, const Opt *o) {
         write_scaling_list_data(&b, &L);
         sl_expand(&L); /* the PPS lists replace the SPS lists */
     }
-    bw_put(&b, 0, 1); bw_ue(&b, 0); bw_put(&b, 0, 1); bw_put(&b, 0, 1);
+    bw_put(&b, 0, 1); bw_ue(&b, 0); bw_put(&b, 0, 1);
+    bw_put(&b, (uint32_t)o->ppsext, 1); /* pps_extension_present_flag */
+    if (o->ppsext) {
+        bw_put(&b, 1, 1); /* pps_range_extension_flag */
+        bw_put(&b, 0, 7);
+        if (o->tskip) bw_ue(&b, (uint32_t)(o->maxts - 2));
+        bw_put(&b, 0, 1); /* cross_component_prediction_enabled_flag */
+        bw_put(&b, o->cqo != 0, 1);
+        if (o->cqo) {
+            bw_ue(&b, 1); bw_ue(&b, 1); /* diff_cu_chroma_qp_offset_depth, list_len_minus1 */
+            bw_se(&b, -2); bw_se(&b, 3); bw_se(&b, 4); bw_se(&b, -1);
+        }
+        bw_ue(&b, (uint32_t)o->sao_scale[0]); bw_ue(&b, (uint32_t)o->sao_scale[1]);
+    }
     bw_trailing(&b);
     write_nal(f, 34, b.buf, b.n);
     free(b.buf);
@@ -1422,6 +1523,15 @@ int main(int argc, char **argv) {
     o->rawconf[0] = -1;
     if (opt_str(argc, argv, "--conf"))
         sscanf(opt_str(argc, argv, "--conf"), "%lld,%lld,%lld,%lld", &o->rawconf[0], &o->rawconf[1], &o->rawconf[2], &o->rawconf[3]);
+    o->profile = opt_int(argc, argv, "--profile", o->bd == 8 ? 1 : (o->bd == 10 ? 2 : 4));
+    o->vui = opt_int(argc, argv, "--vui", 0);
+    o->rext = opt_int(argc, argv, "--rext", 0);
+    o->maxts = opt_int(argc, argv, "--maxts", 2);
+    o->cqo = opt_int(argc, argv, "--cqo", 0);
+    if (opt_str(argc, argv, "--saoscale")) sscanf(opt_str(argc, argv, "--saoscale"), "%d,%d", &o->sao_scale[0], &o->sao_scale[1]);
+    o->ppsext = opt_int(argc, argv, "--ppsext", 0) || o->maxts != 2 || o->cqo || o->sao_scale[0] || o->sao_scale[1];
+    /* decoders read the pps_range_extension only for the RExt profile (FFmpeg hevc_ps.c) */
+    o->eff_maxts = (o->ppsext && o->profile == 4) ? o->maxts : 2;
     g_sl_on = o->sl != 0;
     o->strong = 1;
     int ctb = opt_int(argc, argv, "--ctb", 64);
@@ -1495,7 +1605,7 @@ int main(int argc, char **argv) {
     Sao *sao = (Sao *)calloc((size_t)nctb, sizeof(Sao));
 
     FILE *fo = fopen(argv[7], "wb");
-    write_vps(fo, o->bd, o->delay);
+    write_vps(fo, o->profile, o->delay);
     write_sps(fo, o);
     write_pps(fo, o);
     int rows_per_slice = o->slice_rows > 0 ? o->slice_rows : g->ctbH;
@@ -1523,6 +1633,7 @@ int main(int argc, char **argv) {
         if (o->qpdelta && nslice > 0) sqp_delta = rndn(5) - 2;
         g->slice_qp = clip3(-g->qpbd, 51, o->qp + sqp_delta);
         bw_se(&b, g->slice_qp - 26);
+        if (o->cqo && o->profile == 4) bw_put(&b, o->cqo == 2, 1); /* cu_chroma_qp_offset_enabled_flag */
         /* pps_loop_filter_across_slices_enabled: signal slice flag */
         if (1) bw_put(&b, (uint32_t)(nslice % 2 == 0), 1);
         /* slice data: one substream per CTB row with WPP (7.3.8.1 end_of_subset_one_bit +
@@ -1540,6 +1651,7 @@ int main(int argc, char **argv) {
         }
         BW *sub = (BW *)calloc((size_t)nsub, sizeof(BW));
         uint8_t wpp_ctx[NUM_CTX];
+        int wpp_stat[4] = {0, 0, 0, 0};
         bw_init(&sub[0]);
         init_contexts(g, g->slice_qp);
         ce_start(&g->ce, &sub[0]);
@@ -1561,7 +1673,7 @@ int main(int argc, char **argv) {
                 /* 9.3.1: initialise at a tile start; at a WPP row start synchronise with the
                  * contexts after the 2nd CTB of the row above when that CTB is available */
                 if (!tile_start && ry > 0 && rx + 1 < g->col_bd[tc + 1] && g->ctb_slice[rs - g->ctbW + 1] == nslice)
-                    memcpy(g->ctx, wpp_ctx, NUM_CTX);
+                    { memcpy(g->ctx, wpp_ctx, NUM_CTX); memcpy(g->stat, wpp_stat, sizeof(wpp_stat)); }
                 else init_contexts(g, g->slice_qp);
                 g->first_qg = 1;
                 g->last_cu_qp = g->slice_qp; /* qPY_PREV of the first QG (8.6.1) */
@@ -1569,7 +1681,7 @@ int main(int argc, char **argv) {
             g->ctb_slice[rs] = nslice;
             if (o->sao) write_sao(g, rx, ry, sao);
             coding_quadtree(g, rx << o->log2ctb, ry << o->log2ctb, o->log2ctb, 0, log2qg);
-            if (o->wpp && rx == g->col_bd[tc] + 1) memcpy(wpp_ctx, g->ctx, NUM_CTX);
+            if (o->wpp && rx == g->col_bd[tc] + 1) { memcpy(wpp_ctx, g->ctx, NUM_CTX); memcpy(wpp_stat, g->stat, sizeof(wpp_stat)); }
             ce_term(&g->ce, ts == ts1 - 1); /* end_of_slice_segment_flag */
         }
         ce_finish(&g->ce);

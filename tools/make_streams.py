@@ -197,6 +197,22 @@ PARITY = [
     ("p22_416x240_sl_sps_explicit", 416, 240, 8, 22, 33, 3, ["--sl", "2", "--depth", "2"]),
     ("p23_480x272_sl_sps_pps_ctb32", 480, 272, 8, 30, 34, 2, ["--sl", "3", "--ctb", "32", "--bypass", "1"]),
     ("p24_352x288_10bit_sl_pps_over_default", 352, 288, 10, 20, 35, 2, ["--sl", "4", "--pcm", "1"]),
+    # 9- and 12-bit 4:2:0 (FFmpeg yuv420p9 / yuv420p12; RExt profile), SAO offsets unscaled at 12 bits
+    ("p26_416x240_9bit", 416, 240, 9, 27, 36, 2, ["--pcm", "1", "--bypass", "1"]),
+    ("p27_416x240_12bit", 416, 240, 12, 24, 37, 2, ["--pcm", "1", "--depth", "2"]),
+    # range extensions (--rext bits: 1 ts rotation, 2 ts contexts, 4 implicit RDPCM, 8 explicit RDPCM,
+    # 32 intra smoothing off, 64 high-precision offsets, 128 persistent Rice adaptation)
+    ("p28_416x240_12bit_rext_all", 416, 240, 12, 22, 38, 3,
+     ["--rext", "167", "--maxts", "5", "--saoscale", "2,1", "--bypass", "1", "--vui", "1"]),
+    ("p29_416x240_rext_ts_rdpcm_rice_wpp", 416, 240, 8, 26, 39, 2,
+     ["--profile", "4", "--rext", "135", "--maxts", "4", "--bypass", "1", "--wpp", "1", "--ctb", "32"]),
+    ("p30_352x288_10bit_rext_nosmooth_rice_slices", 352, 288, 10, 20, 40, 2,
+     ["--profile", "4", "--rext", "160", "--slices", "1", "--depth", "2", "--maxts", "3"]),
+    # Main profile with a VUI and a pps_range_extension the decoder must ignore (not RExt)
+    ("p31_416x240_vui_ppsext_ignored", 416, 240, 8, 28, 41, 2, ["--vui", "1", "--ppsext", "1", "--maxts", "5"]),
+    # RExt flags without effect on intra pictures, chroma QP offset list present but off in the slice
+    ("p32_320x192_rext_noop_cqo_list", 320, 192, 8, 30, 42, 2,
+     ["--profile", "4", "--rext", "75", "--cqo", "1", "--tilecols", "2"]),
 ]
 
 
@@ -214,6 +230,7 @@ def parity():
         manifest.append({"file": name + ".h265", "w": W, "h": H, "bit_depth": bd, "qp": qp, "options": opts})
         print(f"{path}: {nb} B", flush=True)
     json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
+    leftcrop()  # p25 (its own recipe) stays in the manifest
 
 
 PARITY264 = [
@@ -272,6 +289,13 @@ PARITY264 = [
     ("a38_256x160_paff_botfirst_cavlc_dbidc2", 256, 160, 8, 22, 73, 5, ["--paff", "2", "--cavlc", "1", "--slices", "2", "--dbidc", "2"]),
     ("a39_192x128_paff_10bit_pcm_offsets", 192, 128, 10, 26, 74, 8, ["--paff", "1", "--pcm", "1", "--cqp", "2", "--alpha", "2", "--beta", "-1"]),
     ("a40_1920x1080_paff_1080i", 1920, 1080, 8, 26, 75, 3, ["--paff", "1", "--t8x8", "1"]),
+    # 4:0:0 (High profile monochrome): no chroma syntax; FFmpeg outputs yuv420p with
+    # chroma 1 << (BitDepth - 1); crop units 1 x (2 - frame_mbs_only)
+    ("a41_400x232_mono_cabac_8x8_pcm", 400, 232, 8, 26, 76, 3, ["--mono", "1", "--pcm", "1", "--slices", "3"]),
+    ("a42_336x192_mono_cavlc_10bit", 336, 192, 10, 24, 77, 4, ["--mono", "1", "--cavlc", "1", "--pcm", "1"]),
+    ("a43_320x160_mono_mbaff_cavlc", 320, 160, 8, 22, 78, 5, ["--mono", "1", "--mbaff", "1", "--cavlc", "1", "--t8x8", "0"]),
+    ("a44_256x144_mono_paff_12bit", 256, 144, 12, 20, 79, 4, ["--mono", "1", "--paff", "1", "--t8x8", "1"]),
+    ("a45_208x128_mono_lossless", 208, 128, 8, 0, 80, 6, ["--mono", "1", "--lossless", "1", "--pcm", "1"]),
 ]
 
 
@@ -385,6 +409,21 @@ MALFORMED = [
     ("m_avc_bitdepth11", 264, 160, 96, ["@bd", "11"], "fail"),
     # a PAFF field without the other parity's field: FFmpeg outputs no frame for it
     ("m_avc_paff_one_field", 264, 160, 96, ["--paff", "1", "--onefield", "1"], "fail"),
+    # HEVC range-extension tools FFmpeg 4.3 does not decode ("not yet implemented":
+    # extended precision, CABAC bypass alignment) and slice-level chroma QP offset lists fail the
+    # picture with their own message; FFmpeg has no 11-bit HEVC pixel format
+    ("m_hevc_rext_extprec", 265, 160, 96, ["--rext", "16"], "fail:extended_precision"),
+    ("m_hevc_rext_bypass_align", 265, 160, 96, ["--rext", "256"], "fail:cabac_bypass_alignment"),
+    ("m_hevc_rext_cqo_slice", 265, 160, 96, ["--profile", "4", "--cqo", "2"], "fail:chroma_qp_offset"),
+    ("m_hevc_bitdepth11", 265, 160, 96, ["@bd", "11"], "fail:bit depth"),
+    # left crops as FFmpeg 4.3 applies them (decode.c apply_cropping -> av_frame_apply_cropping, which
+    # lowers crop_left to keep the planes 32-byte aligned: 8-bit 4:2:0 to a multiple of 64, 16-bit to
+    # a multiple of 32; AVERROR_BUG, no frame, when a plane's alignment exceeds the crop's)
+    ("m_avc_crop_left8", 264, 400, 232, ["--crop", "4,0,0,4"], "ok"),
+    ("m_hevc_conf_left16", 265, 400, 232, ["--conf", "8,0,0,0"], "ok"),
+    ("m_hevc_conf_left48_10bit", 265, 400, 240, ["@bd", "10", "--conf", "24,0,4,0"], "ok"),
+    ("m_avc_mono_crop_left1", 264, 160, 96, ["--mono", "1", "--crop", "1,0,0,0"], "ok"),
+    ("m_avc_mono_crop_left3_10bit", 264, 160, 96, ["@bd", "10", "--mono", "1", "--crop", "3,0,0,0"], "fail:AVERROR_BUG"),
 ]
 
 
@@ -406,7 +445,10 @@ def malformed():
         subprocess.check_call([GEN if codec == 265 else GEN264, yuv, str(W), str(H), str(bd), "27", str(70 + k), path]
                               + gopts)
         os.remove(yuv)
-        manifest.append({"file": name + ext, "codec": codec, "options": opts, "expect": expect})
+        e = {"file": name + ext, "codec": codec, "options": opts, "expect": expect.split(":")[0]}
+        if ":" in expect:
+            e["message"] = expect.split(":", 1)[1]  # substring of the picture's own error message
+        manifest.append(e)
         print(f"{path}: {os.path.getsize(path)} B, expect {expect}", flush=True)
     json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
 
