@@ -37,7 +37,8 @@ WORKLOADS = {
                      data="16 hevcgen 1080p HEVC Main I-frame streams (tests/golden/bench)"),
     "avc1080": dict(streams="tests/golden/bench264/avc1080_*.h264", w=1920, h=1080, bps=1,
                     desc="configs[2]: batch of 1024 x 1080p H.264 High (8x8 transform) I-frames -> JPEG per GPU",
-                    data="16 h264gen 1080p H.264 High CABAC I-frame streams (tests/golden/bench264)"),
+                    data="16 h264gen 1080p H.264 High I-frame streams, 2/16 CAVLC (SURVEY.md §8(d) mix: "
+                         "avc1080_07 / _15) (tests/golden/bench264)"),
     "hevc2160": dict(streams="tests/golden/bench4k/hevc2160_10b_*.h265", w=3840, h=2160, bps=2,
                      desc="configs[3]: 4K H.265 Main10 I-frames, 10-bit decode -> 8-bit JPEG per GPU",
                      data="4 hevcgen 2160p HEVC Main10 I-frame streams (tests/golden/bench4k)"),
@@ -45,6 +46,11 @@ WORKLOADS = {
                            desc="configs[1] on heavier streams (~100-250 KB per picture, SURVEY.md §8(d) aim): "
                                 "batch of 1024 x 1080p H.265 Main 8-bit I-frames -> JPEG per GPU",
                            data="16 hevcgen 1080p HEVC Main I-frame streams, QP 18-24, noise sigma 0-2 (tests/golden/bench_heavy)"),
+    "avc1080_heavy": dict(streams="tests/golden/bench264_heavy/avc1080h_*.h264", w=1920, h=1080, bps=1,
+                          desc="configs[2] on heavier streams (~75-230 KB per picture, SURVEY.md §8(d) aim): "
+                               "batch of 1024 x 1080p H.264 High I-frames -> JPEG per GPU",
+                          data="16 h264gen 1080p H.264 High I-frame streams, QP 18-24, noise sigma 0-1, 2/16 CAVLC "
+                               "(tests/golden/bench264_heavy)"),
     "mixed": dict(streams=None, w=None, h=None, bps=None,
                   desc="configs[4]: mixed 720p/1080p/4K (40/40/20 by count) x H.264/H.265 (50/50) stills, "
                        "LPT-sharded over the GPUs (frames = per-GPU share of the global list)",
@@ -519,12 +525,14 @@ def main():
         # N = 1 only: configs[1] on the SURVEY.md §8(d)-aim set (100-250 KB per picture), and the
         # end-to-end rate against the host entropy threads on this one GPU (DESIGN.md §7 predicts
         # the 1 -> 8 GPU curve from it)
-        if world == 1 and args.workload == "hevc1080" and not args.no_aim:
-            heavy = load_streams(WORKLOADS["hevc1080_heavy"]["streams"])
+        if world == 1 and args.workload in ("hevc1080", "avc1080") and not args.no_aim:
+            hkey = args.workload + "_heavy"
+            heavy = load_streams(WORKLOADS[hkey]["streams"])
             hbatch = [heavy[i % len(heavy)] for i in range(n)]
             fps, hper = timed_batches(eng, hbatch, 4, 1)
             res["value_aim"] = fps
-            res["value_aim_def"] = ("configs[1] on tests/golden/bench_heavy (16 hevcgen 1080p streams, "
+            res["value_aim_def"] = (f"{'configs[1]' if args.workload == 'hevc1080' else 'configs[2]'} on "
+                                    f"{WORKLOADS[hkey]['streams'].rsplit('/', 1)[0]} (16 generator 1080p streams, "
                                     f"{sum(len(b) for b in hbatch) / n / 1024:.1f} KB/picture), same engine and timing")
             res["value_aim_parse_core_us_per_kb"] = parse_core_us_per_kb(hper, host["threads"], hbatch)
             sweep = {}

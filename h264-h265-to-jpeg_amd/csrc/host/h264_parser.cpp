@@ -1395,7 +1395,12 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 job_->message = "first_mb_in_slice outside the picture";
                 return -6;
             }
-            if (slice_type % 5 != 2) { job_->message = "first picture is not intra (P/B slices unsupported)"; return -5; }
+            if (slice_type % 5 != 2) {
+                // an I field followed by a P / B field (broadcast 1080i) names its cause
+                job_->message = have && paff_ ? "PAFF second field is P/B (unsupported: intra field pairs only)"
+                                              : "first picture is not intra (P/B slices unsupported)";
+                return -5;
+            }
             if (type == 5) b.ue();
             if (s.poc_type == 0) {
                 b.u(s.log2_max_poc_lsb);
@@ -1450,6 +1455,11 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
                 mb_.assign(static_cast<size_t>(mbw_) * mbh_, Mb());
                 job_->ctbs.assign(static_cast<size_t>(mbw_) * mbh_, h2j_ctb());
                 for (int i = 0; i < mbw_ * mbh_; i++) job_->ctbs[i].ts = static_cast<uint32_t>(i);
+                // PAFF: every macroblock of the pair layout is a field MB (h2j_ctb.mbflags bit 3), also
+                // the ones a truncated field leaves undecoded, so K0 / K1 / the deblocker map rows
+                // alike
+                if (paff_)
+                    for (auto& c : job_->ctbs) c.mbflags = 8;
                 job_->tus.reserve(static_cast<size_t>(mbw_) * mbh_ * 10);
                 job_->coefs.reserve(static_cast<size_t>(mbw_) * mbh_ * 64);
                 h2j_frame& f = job_->hdr;

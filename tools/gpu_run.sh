@@ -12,6 +12,8 @@
 #   pmc:KERNEL:WL[:sq|hbm]    PMC passes of one kernel (hbm: FETCH_SIZE / WRITE_SIZE passes)
 #   ab:WL:BDIR[:STEPS]        same-box ABAB bench lines: this build vs the libraries in BDIR
 #   parse[:ROUNDS]            host entropy speed, one thread (tools/parse_bench)
+#   prof:WL                   kernel stats + FETCH_SIZE / WRITE_SIZE passes (tools/gpu_prof.sh), summarised by
+#                             tools/prof_summary.py into gpurun_out/TAG_WL_summary.md (the roofline `traffic`)
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -86,6 +88,12 @@ PY
     R=${A1:-3}
     timeout -k 10 600 bash tools/gpu_parse_min.sh $R > gpurun_out/${TAG}_parse.log 2>&1 || { tail -20 gpurun_out/${TAG}_parse.log; exit 1; }
     tail -8 gpurun_out/${TAG}_parse.log ;;
+  prof)
+    WL=${A1:-hevc1080}
+    bash tools/gpu_prof.sh ${TAG}_$WL 1024 $WL > /dev/null
+    python3 tools/prof_summary.py ${TAG}_$WL $WL > /dev/null
+    cp profiles/${TAG}_${WL}_summary.md profiles/${TAG}_${WL}_kernel_stats.csv gpurun_out/ 2>/dev/null || true
+    head -16 profiles/${TAG}_${WL}_summary.md ;;
   *)
     echo "unknown step $STEP"; exit 2 ;;
   esac

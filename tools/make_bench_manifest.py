@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle_py as O  # noqa: E402
 
-SETS = ["bench/*.h265", "bench_heavy/*.h265", "bench264/*.h264", "bench4k/*.h265", "mixed/*.h26[45]"]
+SETS = ["bench/*.h265", "bench_heavy/*.h265", "bench264/*.h264", "bench264_heavy/*.h264", "bench4k/*.h265", "mixed/*.h26[45]"]
 
 
 def main():

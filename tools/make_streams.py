@@ -333,6 +333,26 @@ def bench264(n=16):
     print("total", total)
 
 
+def heavy264(n=16):
+    """configs[2] on heavier content: ~100-250 KB per 1080p picture (SURVEY.md §8(d) aim), the
+    value_aim set of the avc1080 bench line; streams 3 and 11 are CAVLC (2/16, the §8(d) mix)."""
+    out_dir = os.path.join(ROOT, "tests/golden/bench264_heavy")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    qps = [18, 20, 22, 24]
+    sigmas = [0, 1, 0, 1]
+    total = 0
+    for i in range(n):
+        qp, sigma = qps[i % 4], sigmas[(i // 4) % 4]
+        content = make_content(planes, 1920, 1080, 600 + i, sigma, 8)
+        path = os.path.join(out_dir, f"avc1080h_{i:02d}.h264")
+        opts = ["--t8x8", "1"] + (["--cavlc", "1"] if i % 8 == 3 else [])
+        nb = encode(content, 1920, 1080, 8, qp, 600 + i, path, opts, codec=264)
+        total += nb
+        print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+    print("total", total, "mean", total // n)
+
+
 def mixed():
     """configs[4] ingredients: 720p H.265 + H.264, 4K H.264 (1080p and 4K H.265
     come from the bench / bench4k sets)."""
@@ -534,4 +554,4 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
      "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy,
-     "wide264": wide264, "leftcrop": leftcrop}[what]()
+     "wide264": wide264, "leftcrop": leftcrop, "heavy264": heavy264}[what]()
