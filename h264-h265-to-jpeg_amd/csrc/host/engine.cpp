@@ -211,8 +211,12 @@ struct Slot {
 // stats slots (h2j_engine_stats): times in ms summed over chunks; ST_RECON is K1 only, ST_PREP is K0
 // ST_PARSE: submission -> last picture parsed (includes waiting behind the previous batch's parse);
 // ST_PARSE_RUN: first -> last picture parsed (the pool's time on this batch)
+// ST_D2H_STATS / ST_D2H_PAY: the two parts of ST_D2H (per-picture jstat records; JPEG payloads, whose
+// copy is enqueued once the host has read their total), ST_PAY_BYTES: payload bytes copied,
+// ST_HOST_GROW: host ms spent growing the pinned payload buffer
 enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
-       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_PARSE_RUN, ST_N };  // ST_PACK: host time packing records into staging
+       ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_PARSE_RUN, ST_D2H_STATS, ST_D2H_PAY, ST_PAY_BYTES, ST_HOST_GROW,
+       ST_H2D_BYTES, ST_N };  // ST_PACK: host time packing records into staging
 
 // H.264 pictures with more MB rows than this are reconstructed by several K1 workgroups
 constexpr int kK1BandRows = 68;
@@ -570,6 +574,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     int r = 0;
     r |= h2j_gpu_event_record(s.ev[0], st);
     r |= h2j_gpu_memcpy_h2d(din, hin, in_bytes, st);
+    stats[ST_H2D_BYTES] += static_cast<double>(in_bytes);
     r |= h2j_gpu_memset(s.d_arena.p, 0, s.zero_bytes, st);
     r |= h2j_gpu_event_record(s.ev[1], st);
     if (r) return drain_fail(s, std::string("upload failed: ") + h2j_gpu_last_error());
@@ -609,7 +614,10 @@ int Engine::sync(Slot& s) {
     if (s.entropy) {
         uint64_t total = 0;
         std::memcpy(&total, s.h_js.p, 8);
+        const double tg = now_ms();
         if (!s.h_seg.ensure(total + 16)) return fail("pinned host allocation failed");
+        stats[ST_HOST_GROW] += now_ms() - tg;
+        stats[ST_PAY_BYTES] += static_cast<double>(total);
         h2j_gpu_event_record(s.ev[10], s.stream);
         if (total && h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
             return fail(std::string("download failed: ") + h2j_gpu_last_error());
@@ -625,8 +633,11 @@ int Engine::sync(Slot& s) {
     stats[ST_JPEG] += h2j_gpu_event_elapsed_ms(s.ev[4], s.ev[5]);
     stats[ST_ENTROPY] += h2j_gpu_event_elapsed_ms(s.ev[5], s.ev[6]);
     // copies only (the payload copy is enqueued once the host has read the sizes)
-    stats[ST_D2H] += h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]) +
-                     (s.entropy ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[7]) : 0.0f);
+    const double d2h_stats = h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]);
+    const double d2h_pay = s.entropy ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[7]) : 0.0;
+    stats[ST_D2H] += d2h_stats + d2h_pay;
+    stats[ST_D2H_STATS] += d2h_stats;
+    stats[ST_D2H_PAY] += d2h_pay;
     ChunkTime ct;
     ct.frames = static_cast<int>(s.live.size());
     ct.k1_ms = h2j_gpu_event_elapsed_ms(s.ev[8], s.ev[2]);
