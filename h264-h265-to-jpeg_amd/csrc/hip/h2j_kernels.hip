@@ -3314,16 +3314,22 @@ DEVI void h264_filt_line(int (&v)[20], bool on, int bs, int alpha, int beta, int
 // columns left of it); the rows above come from a per-picture line buffer that every row leaves
 // behind, the columns on the left are carried from the previous MB.  After the 8 luma + 4 chroma
 // edge passes the window is written back once.
+// r05: the staging is Pel-typed (luma 4, chroma 8 MBs wide at 8 bits) and the previous MB is kept
+// in it rather than in a copy, so an 8-bit window is 3.7 KB: with the 8-bit LDS line buffer (6 bytes
+// per column) two 8-wave workgroups of the 8-bit kernel share a CU (4 waves per SIMD, where one
+// 104 KB workgroup left 2)
+constexpr int kDbGL = 4;  // luma staging group (MBs): 64-byte rows at 8 bits
+template <typename Pel>
+constexpr int kDbGC = sizeof(Pel) == 1 ? 8 : 4;  // chroma staging group: 64-byte rows
+template <typename Pel>
 struct alignas(16) DbWin {
     uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
     uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
-    uint16_t py[16][12];    // previous MB, columns 0..11 (final, not yet stored)
-    uint16_t pc[2][8][8];   // previous MB, chroma columns 0..6 (+ pad)
-    // final samples staged 4 MBs wide (Pel) and written as whole rows: rows 12..15 of the MBs
-    // above (luma [4][64], chroma [2][2][32]) and rows of this row's MBs (luma [16][64], chroma
-    // [2][8][32])
-    alignas(16) uint8_t sa[2 * (4 * 64 + 2 * 2 * 32)];
-    alignas(16) uint8_t sb[2 * (16 * 64 + 2 * 8 * 32)];
+    // final samples staged and written as whole rows: rows 12..15 of the MBs above (luma
+    // [4][16 GL], chroma [2][2][8 GC]) and rows of this row's MBs (luma [16][16 GL], chroma
+    // [2][8][8 GC])
+    alignas(16) Pel sa[4 * 16 * kDbGL + 2 * 2 * 8 * kDbGC<Pel>];
+    alignas(16) Pel sb[16 * 16 * kDbGL + 2 * 8 * 8 * kDbGC<Pel>];
 };
 // n (4, 8 or 16) Pel between 16-byte-aligned LDS staging and the picture
 template <typename Pel, int N>
@@ -3409,24 +3415,36 @@ DEVI uint2 db_ld4a4(const uint16_t* p) {                                        
 }
 DEVI uint32_t db_u16pair(const uint16_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 DEVI void db_put_u16pair(uint16_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+// two line-buffer samples as a window pair (low half the first): uint16 lines as they are, the
+// 8-bit kernel's LDS line widened / narrowed by byte permutes
+DEVI uint32_t db_line2(const uint16_t* p) { return db_u16pair(p); }
+DEVI uint32_t db_line2(const uint8_t* p) {
+    return __builtin_amdgcn_perm(0u, static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(p)), 0x0c010c00u);
+}
+DEVI void db_put_line2(uint16_t* p, uint32_t v) { db_put_u16pair(p, v); }
+DEVI void db_put_line2(uint8_t* p, uint32_t v) {
+    *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(__builtin_amdgcn_perm(0u, v, 0x0c0c0200u));
+}
 
-template <typename Pel, bool GLine>
-DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin* W,
-                        uint32_t* prog, uint16_t* line, int band, int nbands, const DbTables& TB) {
+// Line: the line buffer's sample type (GLine: uint16 in global memory; else Pel, in LDS)
+template <typename Pel, bool GLine, typename Line>
+DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice* slices, uint8_t* arena, DbWin<Pel>* W,
+                        uint32_t* prog, Line* line, int band, int nbands, const DbTables& TB) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, hl = lane & 31;
-    DbWin& w = W[2 * wv + h];
+    DbWin<Pel>& w = W[2 * wv + h];
     const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
     const int bd = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
     const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
     Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
     Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
-    uint16_t* LY = line;              // [4][width]: rows 12..15 of the MB row above
-    uint16_t* LC = line + 4 * width;  // [2 comps][2 rows][width / 2]: chroma rows 6..7
+    Line* LY = line;              // [4][width]: rows 12..15 of the MB row above
+    Line* LC = line + 4 * width;  // [2 comps][2 rows][width / 2]: chroma rows 6..7
     const int cw = width >> 1;
     const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
     const int npairs = (rend - rbeg + 1) >> 1;
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
     if (wv >= npairs) return;
+    const int hl_ln = hl;
     DBP_DECL;
     // filter lanes of a half: 0-15 luma lines, 16-23 Cb, 24-31 Cr
     const bool luma_lane = hl < 16, chroma = !luma_lane;
@@ -3486,6 +3504,12 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
             const uint32_t cur = ninfo;
             asm volatile("" ::"v"(cur));  // (the copy's wait here, not where ninfo's register is reloaded)
             if (live) {
+                // the lane index laundered per MB in the window and write-back sections: the
+                // compiler then recomputes their lane-dependent LDS / global addresses there
+                // instead of keeping dozens of them live across the MB loop (r05: 208 -> 110
+                // VGPRs, 4 waves per SIMD; laundering the filter sections too measured slower)
+                int hl = hl_ln;
+                asm volatile("" : "+v"(hl));
                 // window: the MB body (prefetched), the rows above (line buffer), left columns carried
                 {
                     uint16_t* d = &w.y[(hl >> 1) + 4][(hl & 1) * 8 + 4];  // 8-byte aligned
@@ -3518,9 +3542,9 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } else if (row > 0) {
                     const int tr = hl >> 3, tc = (hl & 7) * 2;  // 4 rows x 16 luma columns, 2 per lane
-                    db_put_u16pair(&w.y[tr][tc + 4], db_u16pair(LY + tr * width + mx * 16 + tc));
+                    db_put_u16pair(&w.y[tr][tc + 4], db_line2(LY + tr * width + mx * 16 + tc));
                     const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // 2 comps x 2 rows x 8 columns
-                    w.c[c2][cr][k2 + 2] = LC[(c2 * 2 + cr) * cw + mx * 8 + k2];
+                    w.c[c2][cr][k2 + 2] = static_cast<uint16_t>(LC[(c2 * 2 + cr) * cw + mx * 8 + k2]);
                 }
                 // prefetch the half's next MB (its next row: two pairs on) and its parameters
                 int nx = mx + 1, ny = row;
@@ -3623,20 +3647,23 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 }
             }
             if (live) {
+                int hl = hl_ln;
+                asm volatile("" : "+v"(hl));
                 lmf = mf;
                 lqp = mqp;
                 lsaddr = saddr;
                 // write back (the rules of h264_db_rows): rows 12..15 of MB (x, y - 1), rows of
-                // MB (x - 1, y), and on the row's last MB its own rows; staged G MBs wide: 8 at
-                // 8 bits (128-byte luma / 64-byte chroma rows: whole lines, where 4-MB groups left
-                // 32-byte chroma halves that cost 0.2x the picture in extra HBM writes, r04o), 4 at
-                // 16 bits (the staging buffers hold either)
-                constexpr int G = sizeof(Pel) == 1 ? 8 : 4, LW = 16 * G, CW = 8 * G;
+                // MB (x - 1, y), and on the row's last MB its own rows.  Staged kDbGL (luma) /
+                // kDbGC (chroma) MBs wide so every flush writes rows of 64 bytes or more (r05:
+                // 32-byte chroma pieces made the L2 fetch each line they touch, FETCH 1.3x -> 5x the
+                // picture).  An MB's samples go to the staging as soon as the MB is done; the next
+                // MB's left edge then rewrites the columns it changed (luma 12..15, chroma 7).
+                constexpr int GL = kDbGL, GC = kDbGC<Pel>, LW = 16 * GL, CW = 8 * GC;
                 constexpr int SS = 16 / static_cast<int>(sizeof(Pel));  // samples per 16-byte piece
                 const bool last_row = row == mbh - 1, last = mx == mbw - 1;
                 const int nr = last_row ? 16 : 12, ncr = last_row ? 8 : 6;
-                Pel* SA = reinterpret_cast<Pel*>(w.sa);  // luma [4][LW] | chroma [2][2][CW]
-                Pel* SB = reinterpret_cast<Pel*>(w.sb);  // luma [16][LW] | chroma [2][8][CW]
+                Pel* SA = w.sa;  // luma [4][LW] | chroma [2][2][CW]
+                Pel* SB = w.sb;  // luma [16][LW] | chroma [2][8][CW]
                 Pel* const SAc = SA + 4 * LW;
                 Pel* const SBc = SB + 16 * LW;
                 // 16-byte chroma pieces: one store when the row is 16-byte aligned (at 8 bits the
@@ -3652,92 +3679,72 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 if (row > 0) {
                     if (hl < 16) {
                         const int tr = hl >> 2, c4 = (hl & 3) * 4;
-                        db_st4<Pel>(SA + tr * LW + (mx % G) * 16 + c4, db_ld4a8(&w.y[tr][c4 + 4]));
+                        db_st4<Pel>(SA + tr * LW + (mx % GL) * 16 + c4, db_ld4a8(&w.y[tr][c4 + 4]));
                     } else if (hl < 24) {  // chroma rows 6..7
                         const int k = hl - 16, c2 = k >> 2, cr = (k >> 1) & 1, c4 = (k & 1) * 4;
-                        db_st4<Pel>(SAc + (c2 * 2 + cr) * CW + (mx % G) * 8 + c4, db_ld4a4(&w.c[c2][cr][c4 + 2]));
+                        db_st4<Pel>(SAc + (c2 * 2 + cr) * CW + (mx % GC) * 8 + c4, db_ld4a4(&w.c[c2][cr][c4 + 2]));
                     }
-                    if (mx % G == G - 1 || last) {  // the group's rows 12..15 / chroma 6..7 out
-                        wave_sync();
-                        const int g0 = mx - mx % G, nmb = mx - g0 + 1;
-                        {  // luma: 4 rows x 8 pieces of 16 bytes
-                            const int tr = hl >> 3, sg = hl & 7;
-                            if (sg * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS, SA + tr * LW + sg * SS);
-                        }
-                        {  // chroma: 2 comps x 2 rows x 8 pieces of 8 bytes
-                            constexpr int S8 = 8 / static_cast<int>(sizeof(Pel));
-                            const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;
-                            if (cs * S8 < nmb * 8)
-                                db264_copy<Pel, S8>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8, SAc + (c2 * 2 + cr) * CW + cs * S8);
-                        }
+                    const bool fl = mx % GL == GL - 1 || last, fc = mx % GC == GC - 1 || last;
+                    if (fl || fc) wave_sync();
+                    if (fl) {  // the group's luma rows 12..15: 4 rows x LW / SS pieces of 16 bytes
+                        const int g0 = mx - mx % GL, nmb = mx - g0 + 1;
+                        const int tr = hl >> 3, sg = hl & 7;
+                        if (sg * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS, SA + tr * LW + sg * SS);
+                    }
+                    if (fc) {  // chroma rows 6..7: 2 comps x 2 rows x 8 pieces of 8 bytes
+                        constexpr int S8 = 8 / static_cast<int>(sizeof(Pel));
+                        const int g0 = mx - mx % GC, nmb = mx - g0 + 1;
+                        const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;
+                        if (cs * S8 < nmb * 8)
+                            db264_copy<Pel, S8>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8, SAc + (c2 * 2 + cr) * CW + cs * S8);
                     }
                 }
-                auto flush_b = [&](int g0, int nmb) __attribute__((always_inline)) {
-                    wave_sync();
-                    {  // luma: 16 rows x 2 halves of 4 pieces of 16 bytes
-                        const int r = hl >> 1;
-                        if (r < nr) {
+                auto flush_bl = [&](int g0, int nmb) __attribute__((always_inline)) {
+                    // luma: 16 rows x LW / SS pieces of 16 bytes, piece e = hl + 32 k
+                    constexpr int PR = LW / SS;
 #pragma unroll
-                            for (int k = 0; k < 4; k++) {
-                                const int sp = (hl & 1) * 4 + k;
-                                if (sp * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 + r) * sty + g0 * 16 + sp * SS, SB + r * LW + sp * SS);
-                            }
-                        }
+                    for (int k = 0; k < 16 * PR / 32; k++) {
+                        const int e = hl + 32 * k, r = e / PR, sp = e % PR;
+                        if (r < nr && sp * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 + r) * sty + g0 * 16 + sp * SS, SB + r * LW + sp * SS);
                     }
-                    {  // chroma: 2 comps x 8 rows x 2 halves of 2 pieces of 16 bytes
-                        constexpr int MPS = SS / 8;  // MBs per piece
-                        const int c2 = hl >> 4, cr = (hl >> 1) & 7;
-                        if (cr < ncr) {
-                            Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8;
-                            const Pel* q = SBc + (c2 * 8 + cr) * CW;
+                };
+                auto flush_bc = [&](int g0, int nmb) __attribute__((always_inline)) {
+                    // chroma: 2 comps x 8 rows x 4 pieces of 16 bytes (CW is 64 bytes at either size)
+                    static_assert(CW == 4 * SS, "chroma staging rows of four 16-byte pieces");
 #pragma unroll
-                            for (int k = 0; k < 2; k++) {
-                                const int sg = (hl & 1) * 2 + k;
-                                if ((sg + 1) * MPS <= nmb) cput16(d + sg * SS, q + sg * SS);
-                                else if (sg * MPS < nmb) db264_copy<Pel, 8>(d + sg * SS, q + sg * SS);  // 8 bits: an odd last MB
-                            }
+                    for (int k = 0; k < 2; k++) {
+                        const int e = hl + 32 * k, c2 = e >> 5, cr = (e >> 2) & 7, sg = e & 3;
+                        if (cr < ncr) {
+                            Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8 + sg * SS;
+                            const Pel* q = SBc + (c2 * 8 + cr) * CW + sg * SS;
+                            if ((sg + 1) * SS <= nmb * 8) cput16(d, q);
+                            else if (sg * SS < nmb * 8) db264_copy<Pel, 8>(d, q);  // 8 bits: an odd last MB
                         }
                     }
                 };
-                if (mx > 0) {  // the previous MB: columns 0..11 saved in py, 12..15 in the window
-                    const int sx = ((mx - 1) % G) * 16;
-                    {
-                        const int r = hl >> 1, c8 = (hl & 1) * 8;
-                        if (r < nr) {
-                            const uint2 a = db_ld4a8(&w.py[r][c8]);
-                            const uint2 b = c8 ? db_ld4a8(&w.y[r + 4][0]) : db_ld4a8(&w.py[r][4]);
-                            db_st8<Pel>(SB + r * LW + sx + c8, a, b);
-                        }
+                if (mx > 0) {  // the previous MB's columns the left edge just finished
+                    const int px = mx - 1;
+                    if (hl < 16) {
+                        db_st4<Pel>(SB + hl * LW + (px % GL) * 16 + 12, db_ld4a8(&w.y[hl + 4][0]));
+                    } else {
+                        const int k = hl - 16, c2 = k >> 3, cr = k & 7;
+                        SBc[(c2 * 8 + cr) * CW + (px % GC) * 8 + 7] = static_cast<Pel>(w.c[c2][cr + 2][1]);
                     }
-                    {
-                        const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
-                        if (cr < ncr) {  // chroma column 7 sits in the window
-                            uint2 a = db_ld4a8(&w.pc[c2][cr][c4]);
-                            if (c4) a.y = (a.y & 0xFFFFu) | (static_cast<uint32_t>(w.c[c2][cr + 2][1]) << 16);
-                            db_st4<Pel>(SBc + (c2 * 8 + cr) * CW + (sx >> 1) + c4, a);
-                        }
-                    }
-                    if ((mx - 1) % G == G - 1) flush_b(mx - G, G);
+                    const bool fl = px % GL == GL - 1, fc = px % GC == GC - 1;
+                    if (fl || fc) wave_sync();
+                    if (fl) flush_bl(px - (GL - 1), GL);
+                    if (fc) flush_bc(px - (GC - 1), GC);
                 }
-                // this MB's columns 0..11 / chroma 0..7 wait for the next MB (in-order LDS)
-                {
-                    const int r = hl >> 1, c6 = (hl & 1) * 6;
-#pragma unroll
-                    for (int k = 0; k < 6; k += 2) db_put_u16pair(&w.py[r][c6 + k], db_u16pair(&w.y[r + 4][c6 + k + 4]));
-                    const int c2 = hl >> 4, cr = (hl >> 1) & 7, c4 = (hl & 1) * 4;
-                    *reinterpret_cast<uint2*>(&w.pc[c2][cr][c4]) = db_ld4a4(&w.c[c2][cr + 2][c4 + 2]);
+                {  // this MB's rows into the staging (in-order LDS: after the flush's reads above)
+                    const int r = hl >> 1, c8 = (hl & 1) * 8;
+                    db_st8<Pel>(SB + r * LW + (mx % GL) * 16 + c8, db_ld4a8(&w.y[r + 4][c8 + 4]), db_ld4a8(&w.y[r + 4][c8 + 8]));
+                    const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
+                    db_st4<Pel>(SBc + (c2 * 8 + cr) * CW + (mx % GC) * 8 + c4, db_ld4a4(&w.c[c2][cr + 2][c4 + 2]));
                 }
                 if (last) {  // the row's last MB: its rows are final now
-                    const int sx = (mx % G) * 16;
-                    {
-                        const int r = hl >> 1, c8 = (hl & 1) * 8;
-                        if (r < nr) db_st8<Pel>(SB + r * LW + sx + c8, db_ld4a8(&w.y[r + 4][c8 + 4]), db_ld4a8(&w.y[r + 4][c8 + 8]));
-                    }
-                    {
-                        const int c2 = hl >> 4, k = hl & 15, cr = k >> 1, c4 = (k & 1) * 4;
-                        if (cr < ncr) db_st4<Pel>(SBc + (c2 * 8 + cr) * CW + (sx >> 1) + c4, db_ld4a4(&w.c[c2][cr + 2][c4 + 2]));
-                    }
-                    flush_b(mx - mx % G, mx % G + 1);
+                    wave_sync();
+                    flush_bl(mx - mx % GL, mx % GL + 1);
+                    flush_bc(mx - mx % GC, mx % GC + 1);
                 }
                 // line buffer for the row below: the MB's bottom rows (columns final so far) and the
                 // previous MB's last columns, which this MB's left edge has just finished
@@ -3770,15 +3777,15 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 } else if (row + 1 < mbh) {
                     {
                         const int tr = hl >> 3, tc = (hl & 7) * 2;  // rows 12..15 of this MB, 2 per lane
-                        if (tc < 12 || last) db_put_u16pair(LY + tr * width + mx * 16 + tc, db_u16pair(&w.y[tr + 16][tc + 4]));
+                        if (tc < 12 || last) db_put_line2(LY + tr * width + mx * 16 + tc, db_u16pair(&w.y[tr + 16][tc + 4]));
                     }
                     if (mx > 0 && hl < 8) {
                         const int tr = hl >> 1, tc = (hl & 1) * 2;
-                        db_put_u16pair(LY + tr * width + mx * 16 - 4 + tc, db_u16pair(&w.y[tr + 16][tc]));
+                        db_put_line2(LY + tr * width + mx * 16 - 4 + tc, db_u16pair(&w.y[tr + 16][tc]));
                     }
                     const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // chroma rows 6..7
-                    if (k2 < 6 || last) LC[(c2 * 2 + cr) * cw + mx * 8 + k2] = w.c[c2][cr + 8][k2 + 2];
-                    if (mx > 0 && k2 < 2) LC[(c2 * 2 + cr) * cw + mx * 8 - 2 + k2] = w.c[c2][cr + 8][k2];
+                    if (k2 < 6 || last) LC[(c2 * 2 + cr) * cw + mx * 8 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2 + 2]);
+                    if (mx > 0 && k2 < 2) LC[(c2 * 2 + cr) * cw + mx * 8 - 2 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2]);
                 }
                 wave_sync();
                 {  // carry the last columns into the next MB's left strip
@@ -3976,19 +3983,23 @@ DEVI void h264_db_mbaff(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* S
     }
 }
 
+// One kernel per sample type (its window and LDS line sizes differ: the 8-bit one fits two
+// workgroups per CU) and one for MBAFF frames (no windows: its LDS is the progress words); each
+// skips the pictures of the others.  Launched for the kinds present (h2j_gpu_batch.h264_pels).
+template <typename Pel>
 __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2j_frame* frames, const h2j_ctb* ctbs,
                                                                       const h2j_slice* slices, uint8_t* arena,
                                                                       const uint32_t* map, int line_w) {
     // LDS: windows (two per wave) | progress | tables | line buffer (h2j_gpu_deblock)
     extern __shared__ __align__(16) uint8_t dblds[];
-    DbWin* W = reinterpret_cast<DbWin*>(dblds);
-    uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin) * 2 * kDbPairWaves);
-    DbTables& TB = *reinterpret_cast<DbTables*>(dblds + sizeof(DbWin) * 2 * kDbPairWaves + kDbPairSlots * 4);
-    uint16_t* line = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(&TB) + sizeof(DbTables));
+    DbWin<Pel>* W = reinterpret_cast<DbWin<Pel>*>(dblds);
+    uint32_t* prog = reinterpret_cast<uint32_t*>(dblds + sizeof(DbWin<Pel>) * 2 * kDbPairWaves);
+    DbTables& TB = *reinterpret_cast<DbTables*>(dblds + sizeof(DbWin<Pel>) * 2 * kDbPairWaves + kDbPairSlots * 4);
+    Pel* line = reinterpret_cast<Pel*>(reinterpret_cast<uint8_t*>(&TB) + sizeof(DbTables));
     const uint32_t me = map[blockIdx.x];  // same (picture, band) map as K1
     const h2j_frame& f = frames[me >> 8];
     const int band = static_cast<int>(me & 0xFF);
-    if (f.codec != H2J_CODEC_H264) return;
+    if (f.codec != H2J_CODEC_H264 || ufl(f.mbaff) || (ufl(f.bit_depth) == 8) != (sizeof(Pel) == 1)) return;
     const int nbands = ufl(f.k1bands);
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
@@ -4004,19 +4015,27 @@ __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2
     if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
         reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
     __syncthreads();
-    if (ufl(f.mbaff)) {  // MBAFF frame (one workgroup per picture: h2j_frame.k1bands 1)
-        if (f.bit_depth == 8) h264_db_mbaff<uint8_t>(f, C, S, arena, prog);
-        else h264_db_mbaff<uint16_t>(f, C, S, arena, prog);
-        return;
-    }
     if (ufl(f.width) <= line_w) {
-        if (f.bit_depth == 8) h264_db_pairs<uint8_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
-        else h264_db_pairs<uint16_t, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
+        h264_db_pairs<Pel, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
     } else {  // one line buffer per band in the picture's residual region (12 bytes per column)
         uint16_t* gl = reinterpret_cast<uint16_t*>(arena + ufl64(f.res)) + static_cast<size_t>(band) * 6 * ufl(f.width);
-        if (f.bit_depth == 8) h264_db_pairs<uint8_t, true>(f, C, S, arena, W, prog, gl, band, nbands, TB);
-        else h264_db_pairs<uint16_t, true>(f, C, S, arena, W, prog, gl, band, nbands, TB);
+        h264_db_pairs<Pel, true>(f, C, S, arena, W, prog, gl, band, nbands, TB);
     }
+}
+
+// MBAFF frames (one workgroup per picture: h2j_frame.k1bands 1)
+__global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264m(const h2j_frame* frames, const h2j_ctb* ctbs,
+                                                                      const h2j_slice* slices, uint8_t* arena,
+                                                                      const uint32_t* map) {
+    __shared__ uint32_t prog[kDbPairSlots];
+    const h2j_frame& f = frames[map[blockIdx.x] >> 8];
+    if (f.codec != H2J_CODEC_H264 || !ufl(f.mbaff)) return;
+    const h2j_ctb* C = ctbs + f.ctb;
+    const h2j_slice* S = slices + f.slice;
+    if (threadIdx.x < kDbPairSlots) prog[threadIdx.x] = 0;
+    __syncthreads();
+    if (ufl(f.bit_depth) == 8) h264_db_mbaff<uint8_t>(f, C, S, arena, prog);
+    else h264_db_mbaff<uint16_t>(f, C, S, arena, prog);
 }
 
 // ---------------------------------------------------------------- K3: SAO
@@ -5005,22 +5024,38 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         r = check(hipGetLastError(), "h2j_k2_deblock(h)");
         if (r) return r;
     }
-    if (!b->has_h264) return 0;
-    static size_t cap = 0;  // dynamic LDS limit: 160 KB minus the kernel's static LDS
-    if (!cap) {  // (line buffers of pictures wider than ~3.6K need more than the 64 KB default)
-        const void* fn = reinterpret_cast<const void*>(h2j_k2_deblock264p);
-        hipFuncAttributes fa{};
-        const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
-        cap = 160 * 1024 - st;
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(cap));
-        (void)hipGetLastError();
+    if (!b->has_h264 || b->k1wgs <= 0) return 0;
+    // dynamic LDS: windows, progress, tables and a line buffer of the batch's widest picture
+    // (6 samples per column) when it fits the CU's 160 KB (wider: global memory)
+    auto launch = [&](auto pel, const void* fn, const char* name) -> int {
+        using Pel = decltype(pel);
+        static size_t cap[2] = {0, 0};  // 160 KB minus the kernel's static LDS
+        size_t& c = cap[sizeof(Pel) - 1];
+        if (!c) {
+            hipFuncAttributes fa{};
+            const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
+            c = 160 * 1024 - st;
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(c));
+            (void)hipGetLastError();
+        }
+        const size_t fixed = sizeof(DbWin<Pel>) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
+        const int line_w = std::min(b->max_w, static_cast<int>((c - fixed) / (6 * sizeof(Pel))) & ~15);
+        hipLaunchKernelGGL(h2j_k2_deblock264p<Pel>, dim3(b->k1wgs), dim3(64 * kDbPairWaves),
+                           fixed + 6 * sizeof(Pel) * static_cast<size_t>(line_w), s, b->frames, b->ctbs, b->slices,
+                           b->arena, b->k1map, line_w);
+        return check(hipGetLastError(), name);
+    };
+    int r = 0;
+    if (b->h264_pels & 1)
+        r = launch(uint8_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint8_t>), "h2j_k2_deblock264p<u8>");
+    if (!r && (b->h264_pels & 2))
+        r = launch(uint16_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint16_t>), "h2j_k2_deblock264p<u16>");
+    if (!r && b->has_mbaff) {
+        hipLaunchKernelGGL(h2j_k2_deblock264m, dim3(b->k1wgs), dim3(64 * kDbPairWaves), 0, s, b->frames, b->ctbs,
+                           b->slices, b->arena, b->k1map);
+        r = check(hipGetLastError(), "h2j_k2_deblock264m");
     }
-    if (b->k1wgs <= 0) return 0;
-    const size_t fixed = sizeof(DbWin) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
-    const int line_w = std::min(b->max_w, static_cast<int>((cap - fixed) / 12) & ~15);
-    hipLaunchKernelGGL(h2j_k2_deblock264p, dim3(b->k1wgs), dim3(64 * kDbPairWaves), fixed + 12 * static_cast<size_t>(line_w), s,
-                       b->frames, b->ctbs, b->slices, b->arena, b->k1map, line_w);
-    return check(hipGetLastError(), "h2j_k2_deblock264p");
+    return r;
 }
 
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {

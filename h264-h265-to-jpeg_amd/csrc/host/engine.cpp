@@ -541,10 +541,14 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.has_hevc = 0;
     b.has_h264 = 0;
     b.has_mbaff = 0;
+    b.h264_pels = 0;
     for (int k = 0; k < nf; k++) {
-        if (s.frames[k].codec == H2J_CODEC_HEVC) b.has_hevc = 1;
-        if (s.frames[k].codec == H2J_CODEC_H264) b.has_h264 = 1;
-        if (s.frames[k].codec == H2J_CODEC_H264 && s.frames[k].mbaff) b.has_mbaff = 1;
+        const h2j_frame& fk = s.frames[k];
+        if (fk.codec == H2J_CODEC_HEVC) b.has_hevc = 1;
+        if (fk.codec != H2J_CODEC_H264) continue;
+        b.has_h264 = 1;
+        if (fk.mbaff) b.has_mbaff = 1;
+        else b.h264_pels |= fk.bit_depth == 8 ? 1 : 2;
     }
     b.frames = reinterpret_cast<const h2j_frame*>(din + o_frames);
     b.tus = reinterpret_cast<const h2j_tu*>(din + o_tus);

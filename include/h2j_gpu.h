@@ -108,6 +108,7 @@ typedef struct {
     int32_t k4a_frames;         /* frames whose MB variances K4a sums (the others are summed by K3 SAO,
                                    h2j_sao_folds_variance); 0: K4a is not launched */
     int32_t has_mbaff;          /* H.264 MBAFF frames present (K1 runs h2j_k1_recon_h264_mbaff for them) */
+    int32_t h264_pels;          /* non-MBAFF H.264 sample types present: bit 0 8-bit, bit 1 high bit depth */
 } h2j_gpu_batch;
 
 /* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
