@@ -3389,12 +3389,13 @@ struct DbPrefetch2 {  // one MB per half: 8 luma + 4 chroma samples per lane, as
     typename std::conditional<sizeof(Pel) == 1, uint32_t, uint2>::type c;
 };
 template <typename Pel>
-DEVI void db264_fetch2(const Pel* PY, const Pel* const* PC, int sty, int stc, int mx, int my, DbPrefetch2<Pel>& r, int hl) {
+DEVI void db264_fetch2(const uint8_t* PB, uint32_t oc0, uint32_t oc1, int sty, int stc, int mx, int my, DbPrefetch2<Pel>& r, int hl) {
     using TY = decltype(r.y);
     using TC = decltype(r.c);
-    r.y = *reinterpret_cast<const TY*>(PY + (my * 16 + (hl >> 1)) * sty + mx * 16 + (hl & 1) * 8);
+    constexpr uint32_t B = sizeof(Pel);
+    r.y = *reinterpret_cast<const TY*>(PB + static_cast<uint32_t>((my * 16 + (hl >> 1)) * sty + mx * 16 + (hl & 1) * 8) * B);
     const int k = hl & 15;
-    r.c = *reinterpret_cast<const TC*>(PC[hl >> 4] + (my * 8 + (k >> 1)) * stc + mx * 8 + (k & 1) * 4);
+    r.c = *reinterpret_cast<const TC*>(PB + ((hl >> 4) ? oc1 : oc0) + static_cast<uint32_t>((my * 8 + (k >> 1)) * stc + mx * 8 + (k & 1) * 4) * B);
 }
 // 4 uint16 window samples (two dwords) as 4 Pel of the picture / staging
 DEVI uint32_t db_pk8(uint2 v) { return __builtin_amdgcn_perm(v.y, v.x, 0x06040200u); }
@@ -3435,8 +3436,17 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
     const int mbw = ufl(f.ctb_w), mbh = ufl(f.ctb_h), width = ufl(f.width);
     const int bd = ufl(f.bit_depth), bdc = ufl(f.bit_depth_c);
     const int sty = ufl(f.pic_stride[0]), stc = ufl(f.pic_stride[1]);
-    Pel* PY = reinterpret_cast<Pel*>(arena + ufl64(f.pic));
-    Pel* PC[2] = {PY + ufl(f.pic_off[1]), PY + ufl(f.pic_off[2])};
+    // picture addresses as the uniform base plus a 32-bit byte offset (the saddr form of the global
+    // accesses: no 64-bit address arithmetic per access)
+    uint8_t* const PB = arena + ufl64(f.pic);
+    const uint32_t oc0 = ufl(f.pic_off[1]) * static_cast<uint32_t>(sizeof(Pel));
+    const uint32_t oc1 = ufl(f.pic_off[2]) * static_cast<uint32_t>(sizeof(Pel));
+    auto py_at = [&](int o) __attribute__((always_inline)) {
+        return reinterpret_cast<Pel*>(PB + static_cast<uint32_t>(o) * static_cast<uint32_t>(sizeof(Pel)));
+    };
+    auto pc_at = [&](int c, int o) __attribute__((always_inline)) {
+        return reinterpret_cast<Pel*>(PB + (c ? oc1 : oc0) + static_cast<uint32_t>(o) * static_cast<uint32_t>(sizeof(Pel)));
+    };
     Line* LY = line;              // [4][width]: rows 12..15 of the MB row above
     Line* LC = line + 4 * width;  // [2 comps][2 rows][width / 2]: chroma rows 6..7
     const int cw = width >> 1;
@@ -3456,7 +3466,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
     {
         const int r = rbeg + 2 * wv + h;
         if (r < rend) {
-            db264_fetch2<Pel>(PY, PC, sty, stc, 0, r, pf, hl);
+            db264_fetch2<Pel>(PB, oc0, oc1, sty, stc, 0, r, pf, hl);
             ninfo = db264_info_raw(mbs, mbw, 0, r, hl);
         }
     }
@@ -3550,7 +3560,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 int nx = mx + 1, ny = row;
                 if (nx == mbw) { nx = 0; ny += 2 * kDbPairWaves; }
                 if (ny < mbh) {
-                    db264_fetch2<Pel>(PY, PC, sty, stc, nx, ny, pf, hl);
+                    db264_fetch2<Pel>(PB, oc0, oc1, sty, stc, nx, ny, pf, hl);
                     ninfo = db264_info_raw(mbs, mbw, nx, ny, hl);
                 }
             }
@@ -3689,14 +3699,14 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     if (fl) {  // the group's luma rows 12..15: 4 rows x LW / SS pieces of 16 bytes
                         const int g0 = mx - mx % GL, nmb = mx - g0 + 1;
                         const int tr = hl >> 3, sg = hl & 7;
-                        if (sg * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS, SA + tr * LW + sg * SS);
+                        if (sg * SS < nmb * 16) db264_copy<Pel, SS>(py_at((row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS), SA + tr * LW + sg * SS);
                     }
                     if (fc) {  // chroma rows 6..7: 2 comps x 2 rows x 8 pieces of 8 bytes
                         constexpr int S8 = 8 / static_cast<int>(sizeof(Pel));
                         const int g0 = mx - mx % GC, nmb = mx - g0 + 1;
                         const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;
                         if (cs * S8 < nmb * 8)
-                            db264_copy<Pel, S8>(PC[c2] + (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8, SAc + (c2 * 2 + cr) * CW + cs * S8);
+                            db264_copy<Pel, S8>(pc_at(c2, (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8), SAc + (c2 * 2 + cr) * CW + cs * S8);
                     }
                 }
                 auto flush_bl = [&](int g0, int nmb) __attribute__((always_inline)) {
@@ -3705,7 +3715,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
 #pragma unroll
                     for (int k = 0; k < 16 * PR / 32; k++) {
                         const int e = hl + 32 * k, r = e / PR, sp = e % PR;
-                        if (r < nr && sp * SS < nmb * 16) db264_copy<Pel, SS>(PY + (row * 16 + r) * sty + g0 * 16 + sp * SS, SB + r * LW + sp * SS);
+                        if (r < nr && sp * SS < nmb * 16) db264_copy<Pel, SS>(py_at((row * 16 + r) * sty + g0 * 16 + sp * SS), SB + r * LW + sp * SS);
                     }
                 };
                 auto flush_bc = [&](int g0, int nmb) __attribute__((always_inline)) {
@@ -3715,7 +3725,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     for (int k = 0; k < 2; k++) {
                         const int e = hl + 32 * k, c2 = e >> 5, cr = (e >> 2) & 7, sg = e & 3;
                         if (cr < ncr) {
-                            Pel* d = PC[c2] + (row * 8 + cr) * stc + g0 * 8 + sg * SS;
+                            Pel* d = pc_at(c2, (row * 8 + cr) * stc + g0 * 8 + sg * SS);
                             const Pel* q = SBc + (c2 * 8 + cr) * CW + sg * SS;
                             if ((sg + 1) * SS <= nmb * 8) cput16(d, q);
                             else if (sg * SS < nmb * 8) db264_copy<Pel, 8>(d, q);  // 8 bits: an odd last MB
