@@ -2057,18 +2057,20 @@ __host__ __device__ constexpr size_t k1_fixed_lds(int waves) { return sizeof(QWa
 // 24-bit signed multiply (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate): every use
 // multiplies a sample (<= 16 bits) or a window / angle index by a small factor
 DEVI int m24(int a, int b) { return __mul24(a, b); }
-DEVI int hevc_angle(int m) {
+// Both from k = |d| with no compare chain (r05: resolving invAngle by comparing the angle against
+// its eight values compiled to ~40 scalar instructions and branches per angular TB).
+struct HevcAng {
+    int angle, inv;  // inv: only used for angle < 0, -round(8192 / |angle|)
+};
+DEVI HevcAng hevc_ang(int m) {
     const int d = m >= 18 ? m - 26 : 10 - m;
     const int k = d < 0 ? -d : d;
     const int mag = k == 8 ? 32 : static_cast<int>((0x1A15110D09050200ull >> (8 * k)) & 0xFF);
-    return d < 0 ? -mag : mag;
-}
-DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / |angle|)
-    const int k = angle == -2 ? 1 : angle == -5 ? 2 : angle == -9 ? 3 : angle == -13 ? 4 : angle == -17 ? 5
-                : angle == -21 ? 6 : angle == -26 ? 7 : 8;
-    const int v = k <= 4 ? static_cast<int>((0x0276038E06661000ull >> (16 * (k - 1))) & 0xFFFF)
-                         : static_cast<int>((0x0100013B018601E2ull >> (16 * (k - 5))) & 0xFFFF);
-    return -v;
+    // |invAngle| for k = 1..8: 4096, 1638, 910, 630 | 482, 390, 315, 256 (k = 0: unused)
+    const int km = (k - 1) & 3;
+    const uint64_t tab = k <= 4 ? 0x0276038E06661000ull : 0x0100013B018601E2ull;
+    const int v = static_cast<int>((tab >> (16 * km)) & 0xFFFF);
+    return HevcAng{d < 0 ? -mag : mag, -v};
 }
 
 
@@ -2082,7 +2084,7 @@ DEVI int hevc_inv_angle(int angle) {  // only used for angle < 0: -round(8192 / 
 // size, from tu.log2n).
 template <int LN>
 DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, int oy, int S, int16_t* body,
-                          const int16_t* top, const int16_t* left, K1WaveLds& s, int lane) {
+                          int topo, int lefto, K1WaveLds& s, int lane) {
     const int c = tu.c, log2n = LN >= 0 ? LN : tu.log2n, n = 1 << log2n, nn = n * n;
     const int bd = c ? u.bdc : u.bd;
     const int maxv = (1 << bd) - 1;
@@ -2108,8 +2110,8 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                            : (m[1] ? 64 + __ffsll(static_cast<long long>(m[1])) - 1 : 128);
     const int last0 = m[0] ? 63 - __clzll(m[0]) : first;
     const int fb[3] = {first, last0, m[1] ? 127 - __clzll(m[1]) : last0};
-    // neighbour sample -> element index relative to `body` (top / left sit at fixed offsets)
-    const int topo = static_cast<int>(top - body), lefto = static_cast<int>(left - body);
+    // neighbour sample -> element index relative to `body` (topo / lefto: the element offsets of
+    // the carried top / left arrays from it)
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
     int dcpart = 0, v0 = 0;
 #pragma unroll
@@ -2157,14 +2159,13 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
             pv = (m24(n - 1 - x, left) + m24(x + 1, tr) + m24(n - 1 - y, above) + m24(y + 1, bl) + n) >> (log2n + 1);
         } else if (mode == 1) {
             const int above = __shfl(r, 2 * n + 1 + x, 64), left = __shfl(r, 2 * n - 1 - y, 64);
-            pv = dc;
-            if (edge && (x == 0 || y == 0)) {
-                if (x == 0 && y == 0) pv = (left + 2 * dc + above + 2) >> 2;
-                else if (y == 0) pv = (above + 3 * dc + 2) >> 2;
-                else pv = (left + 3 * dc + 2) >> 2;
-            }
+            // edge samples by selects (lane-divergent branches cost exec-mask scalar work)
+            const int pc = (left + 2 * dc + above + 2) >> 2, pt = (above + 3 * dc + 2) >> 2, pl = (left + 3 * dc + 2) >> 2;
+            const int pe = x == 0 ? (y == 0 ? pc : pl) : pt;
+            pv = edge && (x == 0 || y == 0) ? pe : dc;
         } else {
-            const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+            const HevcAng ang = hevc_ang(mode);
+            const int angle = ang.angle, inv = ang.inv;
             const bool vert = mode >= 18;
             const int sgn = vert ? 1 : -1;
             const bool bnd = edge && (mode == 26 || mode == 10);
@@ -2197,7 +2198,10 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                             abs(corner + s.sub[0] - 2 * s.sub[n]) < (1 << (bd - 5));
         if (strong) {
             const int bl = s.sub[0], tr = s.sub[4 * n];
-            for (int k = lane; k < L; k += 64) {
+#pragma unroll
+            for (int it = 0; it < nch; it++) {  // uniform trip count (lane-strided loops juggle exec)
+                const int k = lane + 64 * it;
+                if (k >= L) break;
                 int v;
                 if (k == 0 || k == 4 * n || k == 2 * n) v = s.sub[k];
                 else if (k < 2 * n) { const int y = 2 * n - 1 - k; v = (m24(63 - y, corner) + m24(y + 1, bl) + 32) >> 6; }
@@ -2205,7 +2209,10 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                 s.ref[k] = v;
             }
         } else {
-            for (int k = lane; k < L; k += 64) {
+#pragma unroll
+            for (int it = 0; it < nch; it++) {
+                const int k = lane + 64 * it;
+                if (k >= L) break;
                 const int v = (k == 0 || k == 4 * n) ? s.sub[k] : (s.sub[k - 1] + 2 * s.sub[k] + s.sub[k + 1] + 2) >> 2;
                 s.ref[k] = v;
             }
@@ -2234,7 +2241,9 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
     };
     if (mode == 0) {
         const int tr = R[3 * n + 1], bl = R[n - 1];
-        for (int i = lane; i < nq4; i += 64) {
+        #pragma unroll 1
+        for (int it = 0; it < (nq4 >> 6); it++) {  // n >= 16 here: nq4 a multiple of 64
+            const int i = lane + 64 * it;
             const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
             const int ly = R[2 * n - 1 - y];
             const int base = m24(y + 1, bl) + n, wy = n - 1 - y, dd = tr - ly;
@@ -2243,23 +2252,25 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                  (a0 + 2 * dd + m24(wy, R[2 * n + 3 + x])) >> (log2n + 1), (a0 + 3 * dd + m24(wy, R[2 * n + 4 + x])) >> (log2n + 1));
         }
     } else if (mode == 1) {
-        for (int i = lane; i < nq4; i += 64) {
+        #pragma unroll 1
+        for (int it = 0; it < (nq4 >> 6); it++) {  // n >= 16 here: nq4 a multiple of 64
+            const int i = lane + 64 * it;
             const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
             int p0 = dc, p1 = dc, p2 = dc, p3 = dc;
-            if (edge && (x == 0 || y == 0)) {
-                if (y == 0) {
-                    p0 = x == 0 ? (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2 : (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                    p1 = (R[2 * n + 2 + x] + 3 * dc + 2) >> 2;
-                    p2 = (R[2 * n + 3 + x] + 3 * dc + 2) >> 2;
-                    p3 = (R[2 * n + 4 + x] + 3 * dc + 2) >> 2;
-                } else {
-                    p0 = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
-                }
+            if (edge) {  // uniform; the edge samples by selects
+                const bool top = y == 0, lft = x == 0;
+                const int t0 = R[2 * n + 1 + x], c0 = (R[2 * n - 1] + 2 * dc + t0 + 2) >> 2;
+                const int l0 = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                p0 = top ? (lft ? c0 : (t0 + 3 * dc + 2) >> 2) : (lft ? l0 : dc);
+                p1 = top ? (R[2 * n + 2 + x] + 3 * dc + 2) >> 2 : dc;
+                p2 = top ? (R[2 * n + 3 + x] + 3 * dc + 2) >> 2 : dc;
+                p3 = top ? (R[2 * n + 4 + x] + 3 * dc + 2) >> 2 : dc;
             }
             put4(x, y, p0, p1, p2, p3);
         }
     } else {
-        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+        const HevcAng ang = hevc_ang(mode);
+        const int angle = ang.angle, inv = ang.inv;
         const bool vert = mode >= 18;
         // vertical: main = top row (refV(k) = R[2n + k], k < 0 projected from the left column);
         // horizontal: main = left column (refH(k) = R[2n - k], k < 0 projected from the top row)
@@ -2269,7 +2280,10 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         // k < 0 projects onto the side reference through invAngle), M[n + k] for k = -n .. 2n + 1, in
         // the reference array R is not: the sample loop then reads entries with no projection
         int16_t* M = filt ? s.sub : s.ref;
-        for (int k = lane; k < 3 * n + 2; k += 64) {
+#pragma unroll
+        for (int it = 0; it < (3 * n + 2 + 63) / 64; it++) {
+            const int k = lane + 64 * it;
+            if (k >= 3 * n + 2) break;
             const int kk = k - n;
             const int o = kk >= 0 ? kk : -((m24(kk, inv) + 128) >> 8);
             // (entry 2n + 1 is only ever read with weight 0 -- clamped into R)
@@ -2278,7 +2292,9 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
         wave_sync();
         auto lerp = [](int fr, int a, int b) __attribute__((always_inline)) { return (m24(32 - fr, a) + m24(fr, b) + 16) >> 5; };
         if (vert) {  // the quad shares its row, so its position along the angle: five entries
-            for (int i = lane; i < nq4; i += 64) {
+            #pragma unroll 1
+            for (int it = 0; it < (nq4 >> 6); it++) {  // n >= 16 here: nq4 a multiple of 64
+            const int i = lane + 64 * it;
                 const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
                 const int pos = m24(y + 1, angle), fr = pos & 31;
                 const int k1 = n + x + (pos >> 5) + 1;
@@ -2288,7 +2304,9 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
                 put4(x, y, p0, lerp(fr, m1, m2), lerp(fr, m2, m3), lerp(fr, m3, m4));
             }
         } else {
-            for (int i = lane; i < nq4; i += 64) {
+            #pragma unroll 1
+            for (int it = 0; it < (nq4 >> 6); it++) {  // n >= 16 here: nq4 a multiple of 64
+            const int i = lane + 64 * it;
                 const int x = (i & ((n >> 2) - 1)) * 4, y = i >> qsh;
                 int p[4];
 #pragma unroll
@@ -2310,8 +2328,8 @@ DEVI void hevc_predict_tb(const FU& u, const h2j_tu& tu, uint64_t mask, int ox, 
 // indices are computed once and applied to two register sets (lane k: Cb and Cr reference k).
 template <int LN>  // TB size 1 << LN (2 or 3), compile-time
 DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, uint64_t mask, int ox, int oy,
-                                   int S, int16_t* bcb, int16_t* bcr, const int16_t* tcb, const int16_t* lcb,
-                                   const int16_t* tcr, const int16_t* lcr, int lane) {
+                                   int S, int16_t* bcb, int16_t* bcr, int top_cb, int left_cb, int top_cr, int left_cr,
+                                   int lane) {
     constexpr int log2n = LN, n = 1 << log2n, nn = n * n;
     const int maxv = (1 << u.bdc) - 1;
     const bool cbf_cb = (tb.flags & H2J_TU_CBF) != 0;
@@ -2326,8 +2344,6 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
     const int j = le ? 63 - static_cast<int>(__clzll(le)) : first;
     const int xn = j > 2 * n ? ox + (j - 2 * n - 1) : ox - 1;
     const int yn = j < 2 * n ? oy + (2 * n - 1 - j) : oy - 1;
-    const int top_cb = static_cast<int>(tcb - bcb), left_cb = static_cast<int>(lcb - bcb);
-    const int top_cr = static_cast<int>(tcr - bcr), left_cr = static_cast<int>(lcr - bcr);
     const int in = m24(yn, S) + xn;
     const int icb = yn < 0 ? top_cb + xn + 1 : (xn < 0 ? left_cb + yn : in);
     const int icr = yn < 0 ? top_cr + xn + 1 : (xn < 0 ? left_cr + yn : in);
@@ -2353,7 +2369,8 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
         pb = dcb;
         pr = dcr;
     } else {
-        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+        const HevcAng ang = hevc_ang(mode);
+        const int angle = ang.angle, inv = ang.inv;
         const bool vert = mode >= 18;
         const int a = vert ? y : x, b = vert ? x : y;
         const int pos = m24(a + 1, angle), idx = pos >> 5, fr = pos & 31;
@@ -2378,8 +2395,8 @@ DEVI void hevc_predict_chroma_pair(const FU& u, const h2j_tu& tb, bool cbf_cr, u
 // for both components.  Cb references in s.sub, Cr in s.ref (chroma is never filtered, no
 // boundary smoothing), the angular modes' extended main references after them (from index 66).
 DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr, uint64_t mask, int ox, int oy, int S,
-                                     int16_t* bcb, int16_t* bcr, const int16_t* tcb, const int16_t* lcb,
-                                     const int16_t* tcr, const int16_t* lcr, K1WaveLds& s, int lane) {
+                                     int16_t* bcb, int16_t* bcr, int top_cb, int left_cb, int top_cr, int left_cr,
+                                     K1WaveLds& s, int lane) {
     constexpr int log2n = 4, n = 16, L = 4 * n + 1, nu = n, nh = n * n / 2;  // unit = 2 chroma samples
     const int maxv = (1 << u.bdc) - 1;
     const bool cbf_cb = (tb.flags & H2J_TU_CBF) != 0;
@@ -2394,8 +2411,6 @@ DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr,
     const int first = m[0] ? __ffsll(static_cast<long long>(m[0])) - 1
                            : (m[1] ? 64 + __ffsll(static_cast<long long>(m[1])) - 1 : 128);
     const int fb[2] = {first, m[0] ? 63 - __clzll(m[0]) : first};
-    const int top_cb = static_cast<int>(tcb - bcb), left_cb = static_cast<int>(lcb - bcb);
-    const int top_cr = static_cast<int>(tcr - bcr), left_cr = static_cast<int>(lcr - bcr);
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
     const int half = 1 << (u.bdc - 1);
     int dsb = 0, dsr = 0;
@@ -2432,7 +2447,8 @@ DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr,
     };
     if (mode == 0) {
         const int trb = Rb[3 * n + 1], blb = Rb[n - 1], trr = Rr[3 * n + 1], blr = Rr[n - 1];
-        for (int i = lane; i < nh; i += 64) {
+        for (int it = 0; it < nh / 64; it++) {  // uniform trip count
+            const int i = lane + 64 * it;
             const int x = (i & 7) * 2, y = i >> 3, wy = n - 1 - y;
             const int lb = Rb[2 * n - 1 - y], lr = Rr[2 * n - 1 - y];
             const int bb = m24(y + 1, blb) + n, br = m24(y + 1, blr) + n;
@@ -2444,9 +2460,10 @@ DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr,
         }
     } else if (mode == 1) {
         const int dcb = (wave_sum_dpp(dsb) + n) >> (log2n + 1), dcr = (wave_sum_dpp(dsr) + n) >> (log2n + 1);
-        for (int i = lane; i < nh; i += 64) put2((i & 7) * 2, i >> 3, dcb, dcb, dcr, dcr);
+        for (int it = 0; it < nh / 64; it++) put2(((lane + 64 * it) & 7) * 2, (lane + 64 * it) >> 3, dcb, dcb, dcr, dcr);
     } else {
-        const int angle = hevc_angle(mode), inv = hevc_inv_angle(angle);
+        const HevcAng ang = hevc_ang(mode);
+        const int angle = ang.angle, inv = ang.inv;
         const bool vert = mode >= 18;
         const int sgn = vert ? 1 : -1;
         int16_t* Mb = s.sub + 66;  // M[n + k], k = -n .. 2n + 1 (as hevc_predict_tb)
@@ -2459,7 +2476,8 @@ DEVI void hevc_predict_chroma_pair16(const FU& u, const h2j_tu& tb, bool cbf_cr,
             Mr[lane] = Rr[ix];
         }
         wave_sync();
-        for (int i = lane; i < nh; i += 64) {
+        for (int it = 0; it < nh / 64; it++) {  // uniform trip count
+            const int i = lane + 64 * it;
             const int x = (i & 7) * 2, y = i >> 3;
             if (vert) {
                 const int pos = m24(y + 1, angle), fr = pos & 31, k1 = n + x + (pos >> 5) + 1;
@@ -2645,22 +2663,31 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                     if (ox >= Qc || oy >= Qc) break;  // first TB of a later quadrant
                     const int ci = c == 2 ? 1 : 0;
                     int16_t* body = w.body[cur] + ci * 256;
+                    // element offsets of the carried top / left arrays of component ci from the
+                    // window of component cj, from the layout (scalar; pointer differences of the
+                    // generic LDS pointers cost a shared-aperture conversion each)
+                    auto nbo = [&](int cj, int ci2, bool left) __attribute__((always_inline)) {
+                        return static_cast<int>((offsetof(QWave, cs) + static_cast<size_t>(ci2) * sizeof(QComp) +
+                                                 (left ? offsetof(QComp, left) : offsetof(QComp, top)) -
+                                                 offsetof(QWave, body) - static_cast<size_t>(cur) * sizeof(w.body[0]) -
+                                                 static_cast<size_t>(cj) * 512) / 2);
+                    };
                     if (c == 1 && tu.log2n <= 4 && l + 1 < 64 && t + 1 < b && !(tu.flags & H2J_TU_PCM)) {
                         // Cb TB followed by the Cr TB at the same place: one pass for both
                         const h2j_tu tr = tu_from_lanes(rec, l + 1);
                         if (tr.c == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2n == tu.log2n && !(tr.flags & H2J_TU_PCM)) {
                             if (tu.log2n == 4)
                                 hevc_predict_chroma_pair16(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
-                                                           body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
-                                                           w.cs[1].left, w.k, lane);
+                                                           body, w.body[cur] + 256, nbo(0, 0, false), nbo(0, 0, true),
+                                                           nbo(1, 1, false), nbo(1, 1, true), w.k, lane);
                             else if (tu.log2n == 2)
                                 hevc_predict_chroma_pair<2>(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
-                                                            body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
-                                                            w.cs[1].left, lane);
+                                                            body, w.body[cur] + 256, nbo(0, 0, false), nbo(0, 0, true),
+                                                            nbo(1, 1, false), nbo(1, 1, true), lane);
                             else
                                 hevc_predict_chroma_pair<3>(u, tu, (tr.flags & H2J_TU_CBF) != 0, mask_from_lanes(msk, l), ox, oy, Qc,
-                                                            body, w.body[cur] + 256, w.cs[0].top, w.cs[0].left, w.cs[1].top,
-                                                            w.cs[1].left, lane);
+                                                            body, w.body[cur] + 256, nbo(0, 0, false), nbo(0, 0, true),
+                                                            nbo(1, 1, false), nbo(1, 1, true), lane);
                             PROF_ADD(5, 2);
                             PROF_LAPK(tu.log2n - 2 + 4);
                             t += 2;
@@ -2676,13 +2703,13 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
                         wave_sync();
                     } else {
                         if (tu.log2n == 2)
-                            hevc_predict_tb<2>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                            hevc_predict_tb<2>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, nbo(ci, ci, false), nbo(ci, ci, true), w.k, lane);
                         else if (tu.log2n == 3)
-                            hevc_predict_tb<3>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                            hevc_predict_tb<3>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, nbo(ci, ci, false), nbo(ci, ci, true), w.k, lane);
                         else if (tu.log2n == 4)
-                            hevc_predict_tb<4>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                            hevc_predict_tb<4>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, nbo(ci, ci, false), nbo(ci, ci, true), w.k, lane);
                         else  // 32x32 (TB sizes are 4..32)
-                            hevc_predict_tb<5>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, w.cs[ci].top, w.cs[ci].left, w.k, lane);
+                            hevc_predict_tb<5>(u, tu, mask_from_lanes(msk, l), ox, oy, Qc, body, nbo(ci, ci, false), nbo(ci, ci, true), w.k, lane);
                     }
                     PROF_ADD(5, 1);
                     PROF_LAPK(tu.log2n - 2 + (c ? 4 : 0));
