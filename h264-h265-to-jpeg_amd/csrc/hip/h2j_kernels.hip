@@ -3351,7 +3351,10 @@ constexpr int kDbGC = sizeof(Pel) == 1 ? 8 : 4;  // chroma staging group: 64-byt
 template <typename Pel>
 struct alignas(16) DbWin {
     uint16_t y[20][20];     // luma: (row, col) = (y + 4, x + 4) relative to the MB
-    uint16_t c[2][10][10];  // chroma: (y + 2, x + 2)
+    // chroma: (y + 2, x + 2); rows of 12 (2 unused): the filter's dword / sample loads of the chroma
+    // lines then fall on banks the luma lines leave free more often (modelled 54 -> 48 LDS cycles
+    // per MB for the edge loads)
+    uint16_t c[2][10][12];
     // final samples staged and written as whole rows: rows 12..15 of the MBs above (luma
     // [4][16 GL], chroma [2][2][8 GC]) and rows of this row's MBs (luma [16][16 GL], chroma
     // [2][8][8 GC])
@@ -3644,12 +3647,12 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     if (mb_edge && dd == 2 && (vert ? lsaddr : tsaddr) != saddr) mb_edge = false;
                     const int aM = vert ? aL : aT, bM = vert ? bL : bT;
                     // the line of this lane, as in h264_db_rows (chroma at v[2..11])
-                    const int stp = vert ? 1 : (luma_lane ? 20 : 10);
+                    const int stp = vert ? 1 : (luma_lane ? 20 : 12);
                     const uint16_t* base = luma_lane ? (vert ? &w.y[hl + 4][0] : &w.y[0][hl + 4])
                                                      : (vert ? &w.c[cc][ck + 2][0] : &w.c[cc][0][ck + 2]) - 2 * stp;
                     int v[20];
                     // vertical edges: the lane's line is a window row, 4-byte aligned (luma rows 40 B,
-                    // chroma rows 20 B from column -2): ten dword loads / stores instead of twenty
+                    // chroma rows 24 B from column -2): ten dword loads / stores instead of twenty
                     // / eighteen 16-bit ones (r04m: LDS bank conflicts were 68 % of LDS cycles)
                     if (vert) {
                         const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);

@@ -494,6 +494,10 @@ public:
 private:
     H264Parser(const H264Parser&) = default;
     int decode_slice(const SliceWork& w);
+    template <bool AFF>
+    int mb_loop_cabac(int addr, int nmb);
+    template <bool AFF>
+    int mb_loop_cavlc(int addr, int nmb);
     FrameJob* job_;
     Sps sps_[32];
     Pps pps_[256];
@@ -520,8 +524,13 @@ private:
     int dec(int c) { return cc_.decision(ctx_[c]); }
     // CAVLC (7.3.5.3.2 / 9.2)
     int cavlc_block(int nC, int maxnum, uint8_t* pos, int* lvl);
+    // AFF: MbaffFrameFlag (MBAFF frames and PAFF field pairs); the macroblock layer is compiled
+    // once per value so progressive pictures run no interlace tests
+    template <bool AFF>
     int nc_luma(int blk);
+    template <bool AFF>
     int nc_chroma(const Mb& m, int c, int b4);
+    template <bool AFF>
     void decode_mb_cavlc();
     __attribute__((always_inline)) Mb* mb_in_slice(int x, int y) {
         if (x < 0 || y < 0 || x >= mbw_ || y >= mbh_) return nullptr;
@@ -531,24 +540,27 @@ private:
     // 6.4.12 (see nb_loc_mbaff): frames and PAFF field pairs inline (every neighbour query of a
     // macroblock goes through here: out of line it cost ~9 % of the progressive parse), MBAFF out
     // of line
+    template <bool AFF>
     __attribute__((always_inline)) Mb* nb_loc(int xN, int yN, int maxW, int maxH, int* xW, int* yW) {
-        if (__builtin_expect(mbaff_ && !paff_, 0)) return nb_loc_mbaff(xN, yN, maxW, maxH, xW, yW);
+        if (AFF && mbaff_ && !paff_) return nb_loc_mbaff(xN, yN, maxW, maxH, xW, yW);
         if (yN > maxH - 1 || (xN > maxW - 1 && yN >= 0)) return nullptr;
         *xW = (xN + maxW) & (maxW - 1);  // maxW, maxH: 8 or 16; xN, yN >= -1
         *yW = (yN + maxH) & (maxH - 1);
         if (xN >= 0 && xN <= maxW - 1 && yN >= 0) return &mb_[mby_ * mbw_ + mbx_];
-        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? (paff_ ? -2 : -1) : 0));
+        return mb_in_slice(mbx_ + (xN < 0 ? -1 : (xN > maxW - 1 ? 1 : 0)), mby_ + (yN < 0 ? (AFF && paff_ ? -2 : -1) : 0));
     }
     __attribute__((noinline)) Mb* nb_loc_mbaff(int xN, int yN, int maxW, int maxH, int* xW, int* yW);
     // MB covering luma location (-1, 0) / (0, -1) / (16, -1) / (-1, -1) (6.4.11.1)
+    template <bool AFF>
     __attribute__((always_inline)) Mb* nb(int dx, int dy) {
         int xW, yW;
-        return nb_loc(dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
+        return nb_loc<AFF>(dx < 0 ? -1 : (dx > 0 ? 16 : 0), dy < 0 ? -1 : 0, 16, 16, &xW, &yW);
     }
     // the 4x4 luma block covering location (4 bx, 4 by) relative to the MB (6.4.11.4)
+    template <bool AFF>
     __attribute__((always_inline)) Mb* nb_blk(int bx, int by, int* nblk) {
         int xW, yW;
-        Mb* m = nb_loc(bx * 4, by * 4, 16, 16, &xW, &yW);
+        Mb* m = nb_loc<AFF>(bx * 4, by * 4, 16, 16, &xW, &yW);
         *nblk = m ? kBlkOf[yW >> 2][xW >> 2] : 0;
         return m;
     }
@@ -557,17 +569,18 @@ private:
     bool avail_luma(int x, int y, int cur_blk4) {
         int xW, yW;
         if (x >= 16 && y >= 0) return false;
-        if (x < 0 || y < 0 || x >= 16) return nb_loc(x, y, 16, 16, &xW, &yW) != nullptr;
+        if (x < 0 || y < 0 || x >= 16) return nb_loc<true>(x, y, 16, 16, &xW, &yW) != nullptr;
         return kBlkOf[y >> 2][x >> 2] < cur_blk4;
     }
     uint8_t mbaff_mask(int xr, int yr, int log2n, int c) {
         const int n = 1 << log2n;
         if (c > 0 || log2n == 4)  // I16x16 / chroma: the MB's neighbours (top, left, top-left)
-            return static_cast<uint8_t>((nb(0, -1) ? 1 : 0) | (nb(-1, 0) ? 2 : 0) | (nb(-1, -1) ? 4 : 0));
+            return static_cast<uint8_t>((nb<true>(0, -1) ? 1 : 0) | (nb<true>(-1, 0) ? 2 : 0) | (nb<true>(-1, -1) ? 4 : 0));
         const int blk = kBlkOf[yr >> 2][xr >> 2];
         return static_cast<uint8_t>((avail_luma(xr, yr - 1, blk) ? 1 : 0) | (avail_luma(xr - 1, yr, blk) ? 2 : 0) |
                                     (avail_luma(xr - 1, yr - 1, blk) ? 4 : 0) | (avail_luma(xr + n, yr - 1, blk) ? 8 : 0));
     }
+    template <bool AFF>
     void mb_start(int addr, bool cabac);
     int cbf_cond(int cat, const Mb* N, int nblk, int icbcr) const;
     // residual_block_cabac (7.3.5.3.3): number of non-zero levels (0: coded_block_flag 0);
@@ -577,13 +590,16 @@ private:
     // progressive parse ~12 % on the box CPU)
     template <bool FLD>
     int residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl);
+    template <bool AFF>
     int residual_block(int cat, int cbf_inc, int max_num, uint8_t* pos, int* lvl) {
-        return mb_[mby_ * mbw_ + mbx_].field ? residual_block_t<true>(cat, cbf_inc, max_num, pos, lvl)
+        return AFF && mb_[mby_ * mbw_ + mbx_].field ? residual_block_t<true>(cat, cbf_inc, max_num, pos, lvl)
                                              : residual_block_t<false>(cat, cbf_inc, max_num, pos, lvl);
     }
+    template <bool AFF>
     void decode_mb();
     void emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos, bool pcm);
     // sparse record: entries already (pos << 16) | uint16 level
+    template <bool AFF>
     void emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n);
 };
 
@@ -662,15 +678,16 @@ Mb* H264Parser::nb_loc_mbaff(int xN, int yN, int maxW, int maxH, int* xW, int* y
 // position the parser on macroblock address `addr` (MBAFF: pair addr / 2, bottom addr & 1) and,
 // at the top MB of an MBAFF pair, read mb_field_decoding_flag (7.3.4; CABAC ctxIdx 70 + the left /
 // upper pair being available field pairs, 9.3.3.1.1.2; CAVLC u(1))
+template <bool AFF>
 void H264Parser::mb_start(int addr, bool cabac) {
-    if (paff_) {  // field MB address of the current field
+    if (AFF && paff_) {  // field MB address of the current field
         mbx_ = addr % mbw_;
         mby_ = 2 * (addr / mbw_) + parity_;
         mb_[mby_ * mbw_ + mbx_].slice = cur_slice_;
         cur_field_ = 1;
         return;
     }
-    if (!mbaff_) {
+    if (!AFF || !mbaff_) {
         mbx_ = addr % mbw_;
         mby_ = addr / mbw_;
         return;
@@ -771,6 +788,7 @@ int H264Parser::residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos
     return nsig;
 }
 
+template <bool AFF>
 void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n) {
     h2j_tu t;
     t.x = static_cast<uint16_t>(x);
@@ -782,7 +800,7 @@ void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, c
     t.qpy = static_cast<int8_t>(qp_);
     // MBAFF: the reference-availability mask (bits top, left, top-left, top-right) from the 6.4.12.2
     // neighbours, in qpy (H.264 TBs do not use it otherwise); K0 copies it to the mask array
-    if (mbaff_) t.qpy = static_cast<int8_t>(mbaff_mask(x - mbx_ * (c ? 8 : 16), y - mby_ * (c ? 8 : 16), log2n, c));
+    if (AFF && mbaff_) t.qpy = static_cast<int8_t>(mbaff_mask(x - mbx_ * (c ? 8 : 16), y - mby_ * (c ? 8 : 16), log2n, c));
     t.coef = static_cast<uint32_t>(job_->coefs.size());
     job_->coefs.insert(job_->coefs.end(), e, e + n);
     t.ncoef = static_cast<uint16_t>(n);
@@ -825,6 +843,7 @@ int chroma_qp_264(int qpi) {
     return qpi < 30 ? qpi : t[qpi - 30];
 }
 
+template <bool AFF>
 void H264Parser::decode_mb() {
     Mb& m = mb_[mby_ * mbw_ + mbx_];
     m = Mb();
@@ -834,12 +853,12 @@ void H264Parser::decode_mb() {
     rec.slice = static_cast<uint8_t>(cur_slice_);
     m.vx = mbx_;
     m.vy = mby_;
-    m.field = mbaff_ ? cur_field_ : 0;
+    m.field = AFF && mbaff_ ? cur_field_ : 0;
     rec.mbflags = static_cast<uint8_t>(4 | (m.field ? 8 : 0));  // bit 3: MBAFF field macroblock
     // mb_type (I slice)
     {
-        Mb* A = nb(-1, 0);
-        Mb* B = nb(0, -1);
+        Mb* A = nb<AFF>(-1, 0);
+        Mb* B = nb<AFF>(0, -1);
         const int ctx = (A && A->mb_type != 0) + (B && B->mb_type != 0);
         if (!dec(3 + ctx)) {
             m.mb_type = 0;
@@ -877,8 +896,8 @@ void H264Parser::decode_mb() {
     }
     const bool is16 = m.mb_type >= 1 && m.mb_type <= 24;
     if (m.mb_type == 0 && p_->transform_8x8) {
-        Mb* A = nb(-1, 0);
-        Mb* B = nb(0, -1);
+        Mb* A = nb<AFF>(-1, 0);
+        Mb* B = nb<AFF>(0, -1);
         m.t8x8 = dec(399 + (A && A->t8x8) + (B && B->t8x8));
     }
     if (m.mb_type == 0) {
@@ -894,9 +913,9 @@ void H264Parser::decode_mb() {
             }
             int nblk;
             const int bx = kBlkX[blk], by = kBlkY[blk];
-            Mb* A = nb_blk(bx - 1, by, &nblk);
+            Mb* A = nb_blk<AFF>(bx - 1, by, &nblk);
             const int ma = !A ? -1 : (A->mb_type != 0 ? 2 : A->ipm[nblk]);
-            Mb* B = nb_blk(bx, by - 1, &nblk);
+            Mb* B = nb_blk<AFF>(bx, by - 1, &nblk);
             const int mb = !B ? -1 : (B->mb_type != 0 ? 2 : B->ipm[nblk]);
             const int pm = (ma < 0 || mb < 0) ? 2 : std::min(ma, mb);
             const int mode = prev ? pm : (rem < pm ? rem : rem + 1);
@@ -910,8 +929,8 @@ void H264Parser::decode_mb() {
         for (int i = 0; i < 16; i++) m.ipm[i] = 2;
     }
     if (!mono_) {
-        Mb* A = nb(-1, 0);
-        Mb* B = nb(0, -1);
+        Mb* A = nb<AFF>(-1, 0);
+        Mb* B = nb<AFF>(0, -1);
         const int ctx = (A && A->mb_type != 25 && A->cpm != 0) + (B && B->mb_type != 25 && B->cpm != 0);
         if (!dec(64 + ctx)) m.cpm = 0;
         else if (!dec(67)) m.cpm = 1;
@@ -927,13 +946,13 @@ void H264Parser::decode_mb() {
             int ca, cb;
             int xW, yW;  // neighbouring 8x8 blocks (6.4.11.2)
             if (bx == 0) {
-                Mb* A = nb_loc(-1, by * 8, 16, 16, &xW, &yW);
+                Mb* A = nb_loc<AFF>(-1, by * 8, 16, 16, &xW, &yW);
                 ca = A ? (A->mb_type == 25 ? 0 : !((A->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
             } else {
                 ca = !((cbp >> (b8 - 1)) & 1);
             }
             if (by == 0) {
-                Mb* B = nb_loc(bx * 8, -1, 16, 16, &xW, &yW);
+                Mb* B = nb_loc<AFF>(bx * 8, -1, 16, 16, &xW, &yW);
                 cb = B ? (B->mb_type == 25 ? 0 : !((B->cbp >> ((yW >> 3) * 2 + (xW >> 3))) & 1)) : 0;
             } else {
                 cb = !((cbp >> (b8 - 2)) & 1);
@@ -941,8 +960,8 @@ void H264Parser::decode_mb() {
             cbp |= dec(73 + ca + 2 * cb) << b8;
         }
         if (!mono_) {  // CodedBlockPatternChroma bins (none for ChromaArrayType 0)
-            Mb* A = nb(-1, 0);
-            Mb* B = nb(0, -1);
+            Mb* A = nb<AFF>(-1, 0);
+            Mb* B = nb<AFF>(0, -1);
             const int ac = A ? (A->mb_type == 25 ? 2 : (A->cbp >> 4)) : 0;
             const int bc = B ? (B->mb_type == 25 ? 2 : (B->cbp >> 4)) : 0;
             if (dec(77 + (ac > 0) + 2 * (bc > 0))) cbp |= (1 + dec(77 + 4 + (ac == 2) + 2 * (bc == 2))) << 4;
@@ -974,12 +993,12 @@ void H264Parser::decode_mb() {
     uint32_t mbe[256];  // I16x16: the whole macroblock's levels
     int nmb = 0;
     auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
-    const uint8_t* z4 = m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
-    const uint8_t* z8 = m.field ? kFld8 : kZz8;
+    const uint8_t* z4 = AFF && m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
+    const uint8_t* z8 = AFF && m.field ? kFld8 : kZz8;
     if (is16) {
-        Mb* A = nb(-1, 0);
-        Mb* B = nb(0, -1);
-        const int n = residual_block(0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, pos, lvl);
+        Mb* A = nb<AFF>(-1, 0);
+        Mb* B = nb<AFF>(0, -1);
+        const int n = residual_block<AFF>(0, cbf_cond(0, A, 0, 0) + 2 * cbf_cond(0, B, 0, 0), 16, pos, lvl);
         m.cbf_dc[0] = static_cast<uint8_t>(n != 0);
         for (int k = 0; k < n; k++) {
             const int r = z4[pos[k]];  // raster index of the DC matrix = 4x4 block position
@@ -992,11 +1011,11 @@ void H264Parser::decode_mb() {
             uint32_t e[64];
             int ne = 0;
             if (coded) {
-                const int n = residual_block(5, 0, 64, pos, lvl);
+                const int n = residual_block<AFF>(5, 0, 64, pos, lvl);
                 for (int k = 0; k < n; k++) e[ne++] = entry(z8[pos[k]], lvl[k]);
                 for (int k = 0; k < 4; k++) m.cbf[b8 * 4 + k] = 1;
             }
-            emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
+            emit_sparse<AFF>(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
             continue;
         }
         for (int b4 = 0; b4 < 4; b4++) {
@@ -1005,35 +1024,35 @@ void H264Parser::decode_mb() {
             int ne = 0;
             if (coded) {
                 int nblk;
-                Mb* A = nb_blk(bx - 1, by, &nblk);
+                Mb* A = nb_blk<AFF>(bx - 1, by, &nblk);
                 const int ca = cbf_cond(is16 ? 1 : 2, A, nblk, 0);
-                Mb* B = nb_blk(bx, by - 1, &nblk);
+                Mb* B = nb_blk<AFF>(bx, by - 1, &nblk);
                 const int cb = cbf_cond(is16 ? 1 : 2, B, nblk, 0);
                 if (is16) {
-                    const int n = residual_block(1, ca + 2 * cb, 15, pos, lvl);
+                    const int n = residual_block<AFF>(1, ca + 2 * cb, 15, pos, lvl);
                     m.cbf[blk] = static_cast<uint8_t>(n != 0);
                     for (int k = 0; k < n; k++) {
                         const int r = z4[pos[k] + 1];
                         mbe[nmb++] = entry((by * 4 + (r >> 2)) * 16 + bx * 4 + (r & 3), lvl[k]);
                     }
                 } else {
-                    const int n = residual_block(2, ca + 2 * cb, 16, pos, lvl);
+                    const int n = residual_block<AFF>(2, ca + 2 * cb, 16, pos, lvl);
                     m.cbf[blk] = static_cast<uint8_t>(n != 0);
                     for (int k = 0; k < n; k++) e[ne++] = entry(z4[pos[k]], lvl[k]);
                 }
             }
-            if (!is16) emit_sparse(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
+            if (!is16) emit_sparse<AFF>(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
         }
     }
-    if (is16) emit_sparse(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
+    if (is16) emit_sparse<AFF>(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
     // chroma
     uint32_t ce[2][64];
     int nce[2] = {0, 0};
     if (!mono_ && (m.cbp >> 4)) {
         for (int c = 0; c < 2; c++) {
-            Mb* A = nb(-1, 0);
-            Mb* B = nb(0, -1);
-            const int n = residual_block(3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, pos, lvl);
+            Mb* A = nb<AFF>(-1, 0);
+            Mb* B = nb<AFF>(0, -1);
+            const int n = residual_block<AFF>(3, cbf_cond(3, A, 0, c) + 2 * cbf_cond(3, B, 0, c), 4, pos, lvl);
             m.cbf_dc[1 + c] = static_cast<uint8_t>(n != 0);
             for (int k = 0; k < n; k++) ce[c][nce[c]++] = entry((pos[k] >> 1) * 4 * 8 + (pos[k] & 1) * 4, lvl[k]);
         }
@@ -1044,10 +1063,10 @@ void H264Parser::decode_mb() {
                 const int bx = b4 & 1, by = b4 >> 1;
                 int xW, yW, ca, cb;  // neighbouring chroma 4x4 blocks (6.4.11.5)
                 if (bx) ca = m.cbf_c[c][b4 - 1];
-                else { const Mb* A = nb_loc(-1, by * 4, 8, 8, &xW, &yW); ca = cbf_cond(4, A, A ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
+                else { const Mb* A = nb_loc<AFF>(-1, by * 4, 8, 8, &xW, &yW); ca = cbf_cond(4, A, A ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
                 if (by) cb = m.cbf_c[c][b4 - 2];
-                else { const Mb* B = nb_loc(bx * 4, -1, 8, 8, &xW, &yW); cb = cbf_cond(4, B, B ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
-                const int n = residual_block(4, ca + 2 * cb, 15, pos, lvl);
+                else { const Mb* B = nb_loc<AFF>(bx * 4, -1, 8, 8, &xW, &yW); cb = cbf_cond(4, B, B ? (yW >> 2) * 2 + (xW >> 2) : 0, c); }
+                const int n = residual_block<AFF>(4, ca + 2 * cb, 15, pos, lvl);
                 m.cbf_c[c][b4] = static_cast<uint8_t>(n != 0);
                 for (int k = 0; k < n; k++) {
                     const int r = z4[pos[k] + 1];
@@ -1058,7 +1077,7 @@ void H264Parser::decode_mb() {
     for (int c = 0; c < 2; c++) {
         const int off = c == 0 ? p_->cqp : p_->cqp2;
         const int qpi = std::max(-qpbd_, std::min(51, qp_ + off));
-        emit_sparse(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
+        emit_sparse<AFF>(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
     }
 }
 
@@ -1140,16 +1159,18 @@ int H264Parser::cavlc_block(int nC, int maxnum, uint8_t* pos, int* lvl) {
 }
 
 // nC (9.2.1): average of the neighbours' TotalCoeff, I_PCM counts 16
+template <bool AFF>
 int H264Parser::nc_luma(int blk) {
     int nblk, cnt_a = 0, cnt_b = 0;
-    Mb* A = nb_blk(kBlkX[blk] - 1, kBlkY[blk], &nblk);
+    Mb* A = nb_blk<AFF>(kBlkX[blk] - 1, kBlkY[blk], &nblk);
     if (A) cnt_a = A->mb_type == 25 ? 16 : A->tc[nblk];
-    Mb* B = nb_blk(kBlkX[blk], kBlkY[blk] - 1, &nblk);
+    Mb* B = nb_blk<AFF>(kBlkX[blk], kBlkY[blk] - 1, &nblk);
     if (B) cnt_b = B->mb_type == 25 ? 16 : B->tc[nblk];
     if (A && B) return (cnt_a + cnt_b + 1) >> 1;
     return A ? cnt_a : (B ? cnt_b : 0);
 }
 
+template <bool AFF>
 int H264Parser::nc_chroma(const Mb& m, int c, int b4) {
     const int bx = b4 & 1, by = b4 >> 1;
     int cnt_a = 0, cnt_b = 0;
@@ -1158,14 +1179,14 @@ int H264Parser::nc_chroma(const Mb& m, int c, int b4) {
     if (bx) {
         cnt_a = m.tcc[c][b4 - 1];
     } else {
-        Mb* A = nb_loc(-1, by * 4, 8, 8, &xW, &yW);
+        Mb* A = nb_loc<AFF>(-1, by * 4, 8, 8, &xW, &yW);
         if (!A) aa = false;
         else cnt_a = A->mb_type == 25 ? 16 : A->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
     if (by) {
         cnt_b = m.tcc[c][b4 - 2];
     } else {
-        Mb* B = nb_loc(bx * 4, -1, 8, 8, &xW, &yW);
+        Mb* B = nb_loc<AFF>(bx * 4, -1, 8, 8, &xW, &yW);
         if (!B) ab = false;
         else cnt_b = B->mb_type == 25 ? 16 : B->tcc[c][(yW >> 2) * 2 + (xW >> 2)];
     }
@@ -1173,6 +1194,7 @@ int H264Parser::nc_chroma(const Mb& m, int c, int b4) {
     return aa ? cnt_a : (ab ? cnt_b : 0);
 }
 
+template <bool AFF>
 void H264Parser::decode_mb_cavlc() {
     Mb& m = mb_[mby_ * mbw_ + mbx_];
     m = Mb();
@@ -1182,7 +1204,7 @@ void H264Parser::decode_mb_cavlc() {
     rec.slice = static_cast<uint8_t>(cur_slice_);
     m.vx = mbx_;
     m.vy = mby_;
-    m.field = mbaff_ ? cur_field_ : 0;
+    m.field = AFF && mbaff_ ? cur_field_ : 0;
     rec.mbflags = static_cast<uint8_t>(4 | (m.field ? 8 : 0));  // bit 3: MBAFF field macroblock
     const uint32_t mbt = vb_.ue();
     if (mbt > 25) { err_ = -40; return; }
@@ -1215,9 +1237,9 @@ void H264Parser::decode_mb_cavlc() {
             const int rem = prev ? 0 : static_cast<int>(vb_.u(3));
             int nblk;
             const int bx = kBlkX[blk], by = kBlkY[blk];
-            Mb* A = nb_blk(bx - 1, by, &nblk);
+            Mb* A = nb_blk<AFF>(bx - 1, by, &nblk);
             const int ma = !A ? -1 : (A->mb_type != 0 ? 2 : A->ipm[nblk]);
-            Mb* B = nb_blk(bx, by - 1, &nblk);
+            Mb* B = nb_blk<AFF>(bx, by - 1, &nblk);
             const int mb = !B ? -1 : (B->mb_type != 0 ? 2 : B->ipm[nblk]);
             const int pm = (ma < 0 || mb < 0) ? 2 : std::min(ma, mb);
             const int mode = prev ? pm : (rem < pm ? rem : rem + 1);
@@ -1259,10 +1281,10 @@ void H264Parser::decode_mb_cavlc() {
     uint32_t mbe[256];
     int nmb = 0;
     auto entry = [](int p, int v) { return H2J_COEF264(p, v); };
-    const uint8_t* z4 = m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
-    const uint8_t* z8 = m.field ? kFld8 : kZz8;
+    const uint8_t* z4 = AFF && m.field ? kFld4 : kZz4;  // field MBs: field scans (8.5.6 / 8.5.7)
+    const uint8_t* z8 = AFF && m.field ? kFld8 : kZz8;
     if (is16) {
-        const int n = cavlc_block(nc_luma(0), 16, pos, lvl);
+        const int n = cavlc_block(nc_luma<AFF>(0), 16, pos, lvl);
         if (n < 0) { err_ = -44; return; }
         for (int k = 0; k < n; k++) {
             const int r = z4[pos[k]];
@@ -1277,13 +1299,13 @@ void H264Parser::decode_mb_cavlc() {
             if (coded) {
                 for (int i4 = 0; i4 < 4; i4++) {
                     const int blk = b8 * 4 + i4;
-                    const int n = cavlc_block(nc_luma(blk), 16, pos, lvl);
+                    const int n = cavlc_block(nc_luma<AFF>(blk), 16, pos, lvl);
                     if (n < 0) { err_ = -44; return; }
                     m.tc[blk] = static_cast<uint8_t>(n);
                     for (int k = 0; k < n; k++) e[ne++] = entry(z8[4 * pos[k] + i4], lvl[k]);
                 }
             }
-            emit_sparse(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
+            emit_sparse<AFF>(gx + (b8 & 1) * 8, gy + (b8 >> 1) * 8, 3, 0, m.ipm[b8 * 4], qpl, e, ne);
             continue;
         }
         for (int b4 = 0; b4 < 4; b4++) {
@@ -1291,7 +1313,7 @@ void H264Parser::decode_mb_cavlc() {
             uint32_t e[16];
             int ne = 0;
             if (coded) {
-                const int n = cavlc_block(nc_luma(blk), is16 ? 15 : 16, pos, lvl);
+                const int n = cavlc_block(nc_luma<AFF>(blk), is16 ? 15 : 16, pos, lvl);
                 if (n < 0) { err_ = -44; return; }
                 m.tc[blk] = static_cast<uint8_t>(n);
                 for (int k = 0; k < n; k++) {
@@ -1303,10 +1325,10 @@ void H264Parser::decode_mb_cavlc() {
                     }
                 }
             }
-            if (!is16) emit_sparse(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
+            if (!is16) emit_sparse<AFF>(gx + bx * 4, gy + by * 4, 2, 0, m.ipm[blk], qpl, e, ne);
         }
     }
-    if (is16) emit_sparse(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
+    if (is16) emit_sparse<AFF>(gx, gy, 4, 0, (m.mb_type - 1) % 4, qpl, mbe, nmb);
     uint32_t ce[2][64];
     int nce[2] = {0, 0};
     if (!mono_ && (m.cbp >> 4)) {
@@ -1320,7 +1342,7 @@ void H264Parser::decode_mb_cavlc() {
         for (int c = 0; c < 2; c++)
             for (int b4 = 0; b4 < 4; b4++) {
                 const int bx = b4 & 1, by = b4 >> 1;
-                const int n = cavlc_block(nc_chroma(m, c, b4), 15, pos, lvl);
+                const int n = cavlc_block(nc_chroma<AFF>(m, c, b4), 15, pos, lvl);
                 if (n < 0) { err_ = -44; return; }
                 m.tcc[c][b4] = static_cast<uint8_t>(n);
                 for (int k = 0; k < n; k++) {
@@ -1332,7 +1354,7 @@ void H264Parser::decode_mb_cavlc() {
     for (int c = 0; c < 2; c++) {
         const int off = c == 0 ? p_->cqp : p_->cqp2;
         const int qpi = std::max(-qpbd_, std::min(51, qp_ + off));
-        emit_sparse(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
+        emit_sparse<AFF>(gx / 2, gy / 2, 3, 1 + c, m.cpm, chroma_qp_264(qpi) + qpbd_, ce[c], nce[c]);
     }
     if (vb_.overrun()) err_ = -45;
 }
@@ -1591,6 +1613,32 @@ int H264Parser::run(const uint8_t* data, size_t size, int threads) {
     return 0;
 }
 
+template <bool AFF>
+int H264Parser::mb_loop_cabac(int addr, int nmb) {
+    for (;;) {
+        if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
+        mb_start<AFF>(addr, true);
+        decode_mb<AFF>();
+        if (err_) { job_->message = "macroblock decode error"; return -7; }
+        if (cc_.terminate()) break;
+        addr++;
+    }
+    return 0;
+}
+
+template <bool AFF>
+int H264Parser::mb_loop_cavlc(int addr, int nmb) {
+    for (;;) {
+        if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
+        mb_start<AFF>(addr, false);
+        decode_mb_cavlc<AFF>();
+        if (err_) { job_->message = "macroblock decode error"; return -7; }
+        if (!vb_.more_rbsp_data(stop_bit_)) break;
+        addr++;
+    }
+    return 0;
+}
+
 int H264Parser::decode_slice(const SliceWork& w) {
     p_ = &pps_[w.pps_id];  // this parser's own copy of the parameter sets
     cur_slice_ = w.index;
@@ -1603,27 +1651,12 @@ int H264Parser::decode_slice(const SliceWork& w) {
         end_ = w.data.data() + w.nbytes;
         cc_.init(w.data.data(), end_);
         for (int i = 0; i < 460; i++) ctx_[i] = cabac_init_word(kInitI[i][0], kInitI[i][1], qp_);
-        for (;;) {
-            if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
-            mb_start(addr, true);
-            decode_mb();
-            if (err_) { job_->message = "macroblock decode error"; return -7; }
-            if (cc_.terminate()) break;
-            addr++;
-        }
+        return mbaff_ ? mb_loop_cabac<true>(addr, nmb) : mb_loop_cabac<false>(addr, nmb);
     } else {
         stop_bit_ = w.stop_bit;
         vb_.init(w.data.data(), w.nbytes, w.bitpos);
-        for (;;) {
-            if (addr >= nmb) { job_->message = "slice overruns the picture"; return -7; }
-            mb_start(addr, false);
-            decode_mb_cavlc();
-            if (err_) { job_->message = "macroblock decode error"; return -7; }
-            if (!vb_.more_rbsp_data(stop_bit_)) break;
-            addr++;
-        }
+        return mbaff_ ? mb_loop_cavlc<true>(addr, nmb) : mb_loop_cavlc<false>(addr, nmb);
     }
-    return 0;
 }
 
 }  // namespace
