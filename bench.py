@@ -513,7 +513,8 @@ def main():
             "stages_ms_per_step": {k: round(v, 3) for k, v in per.items() if k.endswith("_ms")},
             # the JPEG payload copy's own rate (PCIe, pinned host buffer)
             "d2h_payload_MB_per_step": round(per.get("payload_bytes", 0.0) / 1e6, 2),
-            "d2h_payload_GBps": round(per.get("payload_bytes", 0.0) / max(per.get("d2h_payload_ms", 0.0), 1e-9) / 1e6, 2),
+            "d2h_payload_copied_MB_per_step": round(per.get("payload_copied_bytes", 0.0) / 1e6, 2),
+            "d2h_payload_GBps": round(per.get("payload_copied_bytes", 0.0) / max(per.get("d2h_payload_ms", 0.0), 1e-9) / 1e6, 2),
             "h2d_MB_per_step": round(per.get("h2d_bytes", 0.0) / 1e6, 2),
             "h2d_GBps": round(per.get("h2d_bytes", 0.0) / max(per.get("h2d_ms", 0.0), 1e-9) / 1e6, 2),
             "outputs_verified": bool(manifest) and bad_all == 0,

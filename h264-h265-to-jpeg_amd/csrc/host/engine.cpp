@@ -182,7 +182,8 @@ int parse_any(const uint8_t* d, size_t n, FrameJob& job) {
 // One in-flight chunk: its stream, buffers and layout.
 struct Slot {
     void* stream = nullptr;
-    void* ev[11] = {nullptr};  // 9: after the stats D2H, 10: before the payload D2H
+    void* ev[12] = {nullptr};  // 9: after the stats D2H, 10 / 11: around the payload D2H
+    size_t pay_pre = 0;        // payload bytes already copied in-stream by launch() (h_seg's capacity)
     DevBuf d_in, d_arena, d_seg, d_scratch;
     HostBuf h_in, h_js, h_seg;
     std::vector<h2j_frame> frames;
@@ -211,12 +212,13 @@ struct Slot {
 // stats slots (h2j_engine_stats): times in ms summed over chunks; ST_RECON is K1 only, ST_PREP is K0
 // ST_PARSE: submission -> last picture parsed (includes waiting behind the previous batch's parse);
 // ST_PARSE_RUN: first -> last picture parsed (the pool's time on this batch)
-// ST_D2H_STATS / ST_D2H_PAY: the two parts of ST_D2H (per-picture jstat records; JPEG payloads, whose
-// copy is enqueued once the host has read their total), ST_PAY_BYTES: payload bytes copied,
-// ST_HOST_GROW: host ms spent growing the pinned payload buffer
+// ST_D2H_STATS / ST_D2H_PAY: the two parts of ST_D2H (per-picture jstat records; JPEG payloads),
+// ST_PAY_BYTES: payload bytes produced, ST_PAY_COPIED: payload bytes moved (the in-stream copy moves
+// the pinned buffer's capacity), ST_HOST_GROW: host ms spent growing the pinned payload buffer
+// 
 enum { ST_PARSE, ST_H2D, ST_RECON, ST_DEBLOCK, ST_SAO, ST_JPEG, ST_D2H, ST_ASSEMBLE, ST_TOTAL, ST_FRAMES, ST_BYTES,
        ST_ENTROPY, ST_PREP, ST_CHUNKS, ST_PACK, ST_PARSE_RUN, ST_D2H_STATS, ST_D2H_PAY, ST_PAY_BYTES, ST_HOST_GROW,
-       ST_H2D_BYTES, ST_N };  // ST_PACK: host time packing records into staging
+       ST_H2D_BYTES, ST_PAY_COPIED, ST_N };  // ST_PACK: host time packing records into staging
 
 // H.264 pictures with more MB rows than this are reconstructed by several K1 workgroups
 constexpr int kK1BandRows = 68;
@@ -601,6 +603,20 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         if (r) return drain_fail(s, std::string("download failed: ") + h2j_gpu_last_error());
     }
     h2j_gpu_event_record(s.ev[9], st);
+    // the payloads follow in the same stream, sized by the pinned buffer (1.25x the largest total
+    // seen): no host round trip between the kernels and the copy.  r04/r05 enqueued the copy in
+    // sync() once the host had read the total: at 4K its interval measured 40-78 ms per step for
+    // 121 MB against 4 ms for the bare copy (tools/d2h_probe: 30 GB/s pinned) -- the submitting
+    // driver thread waited for CPU behind the 16 entropy threads (profiles/r05_4k_d2h.md).  A
+    // total above the capacity (first chunks, growth) is copied again whole in sync().
+    s.pay_pre = 0;
+    if (entropy && s.h_seg.cap > 0) {
+        s.pay_pre = std::min(s.h_seg.cap, seg_cap);
+        h2j_gpu_event_record(s.ev[10], st);
+        if (h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, s.pay_pre, st))
+            return drain_fail(s, std::string("download failed: ") + h2j_gpu_last_error());
+        h2j_gpu_event_record(s.ev[11], st);
+    }
     s.pending = true;
     double bytes = 0;
     for (int k = 0; k < nf; k++) {
@@ -615,16 +631,24 @@ int Engine::sync(Slot& s) {
     if (!s.pending) return 0;
     s.pending = false;
     if (h2j_gpu_stream_sync(s.stream)) return fail(std::string("GPU execution failed: ") + h2j_gpu_last_error());
+    bool pay_late = false;
     if (s.entropy) {
         uint64_t total = 0;
         std::memcpy(&total, s.h_js.p, 8);
-        const double tg = now_ms();
-        if (!s.h_seg.ensure(total + 16)) return fail("pinned host allocation failed");
-        stats[ST_HOST_GROW] += now_ms() - tg;
         stats[ST_PAY_BYTES] += static_cast<double>(total);
-        h2j_gpu_event_record(s.ev[10], s.stream);
-        if (total && h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
-            return fail(std::string("download failed: ") + h2j_gpu_last_error());
+        if (total > s.pay_pre) {  // not (all) copied in-stream: grow with headroom, copy it whole
+            const double tg = now_ms();
+            if (!s.h_seg.ensure(total + total / 4 + 16)) return fail("pinned host allocation failed");
+            stats[ST_HOST_GROW] += now_ms() - tg;
+            stats[ST_PAY_COPIED] += static_cast<double>(total);
+            pay_late = true;
+            h2j_gpu_event_record(s.ev[10], s.stream);
+            if (h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
+                return fail(std::string("download failed: ") + h2j_gpu_last_error());
+            h2j_gpu_event_record(s.ev[11], s.stream);
+        } else {
+            stats[ST_PAY_COPIED] += static_cast<double>(s.pay_pre);
+        }
     }
     if (h2j_gpu_event_record(s.ev[7], s.stream) || h2j_gpu_stream_sync(s.stream))
         return fail(std::string("download failed: ") + h2j_gpu_last_error());
@@ -638,7 +662,7 @@ int Engine::sync(Slot& s) {
     stats[ST_ENTROPY] += h2j_gpu_event_elapsed_ms(s.ev[5], s.ev[6]);
     // copies only (the payload copy is enqueued once the host has read the sizes)
     const double d2h_stats = h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]);
-    const double d2h_pay = s.entropy ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[7]) : 0.0;
+    const double d2h_pay = s.entropy && (pay_late || s.pay_pre) ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[11]) : 0.0;
     stats[ST_D2H] += d2h_stats + d2h_pay;
     stats[ST_D2H_STATS] += d2h_stats;
     stats[ST_D2H_PAY] += d2h_pay;

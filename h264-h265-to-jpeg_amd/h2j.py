@@ -84,7 +84,8 @@ def _u8(buf: bytes):
 
 STAT_KEYS = ["parse_ms", "h2d_ms", "recon_ms", "deblock_ms", "sao_ms", "jpeg_ms", "d2h_ms",
              "assemble_ms", "total_ms", "frames", "alg_bytes", "entropy_ms", "prep_ms", "chunks", "pack_ms",
-             "parse_run_ms", "d2h_stats_ms", "d2h_payload_ms", "payload_bytes", "host_grow_ms", "h2d_bytes"]
+             "parse_run_ms", "d2h_stats_ms", "d2h_payload_ms", "payload_bytes", "host_grow_ms", "h2d_bytes",
+             "payload_copied_bytes"]
 
 
 class Engine:
