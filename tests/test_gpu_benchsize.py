@@ -68,3 +68,24 @@ def test_planes_inside_bench_sized_batch(engine, key, n, pick, stage):
     for g, o, name in ((gy, oy, "Y"), (gu, ou, "U"), (gv, ov, "V")):
         diff = np.argwhere(g != o)
         assert diff.size == 0, f"{name}: {len(diff)} mismatches, first {diff[:4].tolist()}"
+
+
+def test_payload_copy_across_buffer_growth():
+    """r05: the JPEG payloads follow the kernels in-stream, sized by the slot's pinned buffer; a
+    chunk whose payload outgrows it is copied again whole after the host reads the total.  A fresh
+    engine (empty buffers) goes small -> large -> small, sequentially and pipelined, and every JPEG
+    must still equal the oracle's."""
+    import h2j
+    small = [read(golden("img01.h265"))]
+    large = _streams("hevc1080")
+    ref = _oracle_jpegs(small + large)
+    eng = h2j.Engine(0)
+    plan = [small * 4, large[:8] * 8, small * 16, large * 4]
+    for batch in plan:  # one chunk per call: each slot sees the growth on its own buffer
+        outs = eng.transcode(batch)
+        assert all(o == ref[s] for s, o in zip(batch, outs)), "sequential"
+    fresh = h2j.Engine(0)
+    outs_all = fresh.transcode_async(plan)
+    for batch, outs in zip(plan, outs_all):
+        bad = [i for i, (s, o) in enumerate(zip(batch, outs)) if o != ref[s]]
+        assert not bad, f"pipelined: {len(bad)} of {len(batch)} differ"
