@@ -92,7 +92,7 @@ PY
     WL=${A1:-hevc1080}
     bash tools/gpu_prof.sh ${TAG}_$WL 1024 $WL > /dev/null
     python3 tools/prof_summary.py ${TAG}_$WL $WL > /dev/null
-    cp profiles/${TAG}_${WL}_summary.md profiles/${TAG}_${WL}_kernel_stats.csv gpurun_out/ 2>/dev/null || true
+    cp profiles/${TAG}_${WL}_summary.md profiles/${TAG}_${WL}_kernel_stats.csv profiles/pmc_k1_${WL}.json gpurun_out/ 2>/dev/null || true
     head -16 profiles/${TAG}_${WL}_summary.md ;;
   *)
     echo "unknown step $STEP"; exit 2 ;;
