@@ -4055,7 +4055,11 @@ __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2
     if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
         reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
     __syncthreads();
-    if (ufl(f.width) <= line_w) {
+    if constexpr (sizeof(Pel) == 1) {
+        // 8 bits: the LDS line buffer (6 bytes per column) holds any width the parser accepts
+        // (512 MBs; h2j_gpu_deblock checks line_w), so there is no global-memory variant
+        h264_db_pairs<Pel, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
+    } else if (ufl(f.width) <= line_w) {
         h264_db_pairs<Pel, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
     } else {  // one line buffer per band in the picture's residual region (12 bytes per column)
         uint16_t* gl = reinterpret_cast<uint16_t*>(arena + ufl64(f.res)) + static_cast<size_t>(band) * 6 * ufl(f.width);
@@ -5080,6 +5084,10 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         }
         const size_t fixed = sizeof(DbWin<Pel>) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
         const int line_w = std::min(b->max_w, static_cast<int>((c - fixed) / (6 * sizeof(Pel))) & ~15);
+        if (sizeof(Pel) == 1 && line_w < b->max_w) {  // never for parser-legal widths (<= 8192)
+            snprintf(g_err, sizeof(g_err), "h2j_k2_deblock264p<u8>: a %d-sample line does not fit LDS", b->max_w);
+            return -1;
+        }
         hipLaunchKernelGGL(h2j_k2_deblock264p<Pel>, dim3(b->k1wgs), dim3(64 * kDbPairWaves),
                            fixed + 6 * sizeof(Pel) * static_cast<size_t>(line_w), s, b->frames, b->ctbs, b->slices,
                            b->arena, b->k1map, line_w);

@@ -515,10 +515,13 @@ def leftcrop():
 
 
 WIDE264 = [
-    # pictures wider than the H.264 deblocking kernel's LDS line buffer holds (~5.9K): the
-    # line buffer then lives in global memory (h2j_k2_deblock264p, GLine)
+    # wide pictures.  r05: the 8-bit deblocking kernel holds an LDS line buffer for any legal
+    # width (8192 = 512 MBs, the parser's limit) and the 16-bit one up to ~6.6K columns, so w03
+    # (8192 wide, 10-bit) is the vector on the global line-buffer path (h2j_k2_deblock264p, GLine);
+    # w01 / w02 keep the widest LDS line buffers
     ("w01_8192x48_wide", 8192, 48, 8, 28, 53, 3, ["--slices", "2"]),
     ("w02_6144x32_wide_10bit", 6144, 32, 10, 24, 54, 2, ["--t8x8", "0"]),
+    ("w03_8192x32_wide_10bit", 8192, 32, 10, 26, 55, 2, ["--slices", "2"]),
 ]
 
 
