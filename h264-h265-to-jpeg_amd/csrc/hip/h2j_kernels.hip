@@ -3070,11 +3070,17 @@ DEVI void st4(Pel* p, const int (&v)[4]) {
 // windows of different edges of one pass never overlap: each line is read and written back as
 // whole 4-sample words (vertical edges: 2 words per line; horizontal edges: one word per row
 // of 4 lines).  P[k][i] / Q[k][i]: line k, distance i from the edge.
+// a sample of a plane by a 32-bit element offset from its (uniform) base: the global access then
+// takes the saddr form, no 64-bit address arithmetic per access (r05)
+template <typename Pel>
+DEVI Pel* at32(Pel* base, int off) {
+    return reinterpret_cast<Pel*>(reinterpret_cast<uint8_t*>(base) + static_cast<uint32_t>(off) * static_cast<uint32_t>(sizeof(Pel)));
+}
 template <typename Pel>
 DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fmap, const int8_t* qmap,
                          const h2j_slice& sl, bool vert, int xe, int ye) {
     const int xp = vert ? xe - 1 : xe, yp = vert ? ye : ye - 1;
-    const int qpq = qmap[(ye >> 2) * f.mw + (xe >> 2)], qpp = qmap[(yp >> 2) * f.mw + (xp >> 2)];
+    const int qpq = qmap[m24(ye >> 2, f.mw) + (xe >> 2)], qpp = qmap[m24(yp >> 2, f.mw) + (xp >> 2)];
     const int qpl = (qpq + qpp + 1) >> 1;
     const int bd = f.bit_depth;
     const int beta = kBeta[clip3(0, 51, qpl + sl.beta_offset)] * (1 << (bd - 8));
@@ -3085,8 +3091,8 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             int a[4], c[4];
-            ld4(pl + (ye + k) * st + xe - 4, a);
-            ld4(pl + (ye + k) * st + xe, c);
+            ld4(at32(pl, m24(ye + k, st) + xe - 4), a);
+            ld4(at32(pl, m24(ye + k, st) + xe), c);
 #pragma unroll
             for (int i = 0; i < 4; i++) { P[k][i] = a[3 - i]; Q[k][i] = c[i]; }
         }
@@ -3094,8 +3100,8 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             int a[4], c[4];
-            ld4(pl + (ye - 1 - i) * st + xe, a);
-            ld4(pl + (ye + i) * st + xe, c);
+            ld4(at32(pl, m24(ye - 1 - i, st) + xe), a);
+            ld4(at32(pl, m24(ye + i, st) + xe), c);
 #pragma unroll
             for (int k = 0; k < 4; k++) { P[k][i] = a[k]; Q[k][i] = c[k]; }
         }
@@ -3110,8 +3116,8 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
                     (abs(P[3][0] - Q[3][0]) < ((5 * tc + 1) >> 1));
     const bool dEp = dp < ((beta + (beta >> 1)) >> 3);
     const bool dEq = dq < ((beta + (beta >> 1)) >> 3);
-    const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
-    const bool nfq = fmap[(ye >> 2) * f.mw + (xe >> 2)] & 4;
+    const bool nfp = fmap[m24(yp >> 2, f.mw) + (xp >> 2)] & 4;
+    const bool nfq = fmap[m24(ye >> 2, f.mw) + (xe >> 2)] & 4;
     int NP[4][4], NQ[4][4];  // filtered lines (unfiltered samples keep their value)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -3145,16 +3151,16 @@ DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fma
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int a[4] = {NP[k][3], NP[k][2], NP[k][1], NP[k][0]};
-            if (!nfp) st4(pl + (ye + k) * st + xe - 4, a);
-            if (!nfq) st4(pl + (ye + k) * st + xe, NQ[k]);
+            if (!nfp) st4(at32(pl, m24(ye + k, st) + xe - 4), a);
+            if (!nfq) st4(at32(pl, m24(ye + k, st) + xe), NQ[k]);
         }
     } else {
 #pragma unroll
         for (int i = 0; i < 3; i++) {  // rows at distance 3 are never modified
             const int a[4] = {NP[0][i], NP[1][i], NP[2][i], NP[3][i]};
             const int c[4] = {NQ[0][i], NQ[1][i], NQ[2][i], NQ[3][i]};
-            if (!nfp) st4(pl + (ye - 1 - i) * st + xe, a);
-            if (!nfq) st4(pl + (ye + i) * st + xe, c);
+            if (!nfp) st4(at32(pl, m24(ye - 1 - i, st) + xe), a);
+            if (!nfq) st4(at32(pl, m24(ye + i, st) + xe), c);
         }
     }
 }
@@ -3167,32 +3173,32 @@ DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, 
                            const int8_t* qmap, const h2j_slice& sl, int cqpoff, bool vert, int xc, int yc) {
     const int xl = xc * 2, yl = yc * 2;
     const int xp = vert ? xl - 1 : xl, yp = vert ? yl : yl - 1;
-    const int qpq = qmap[(yl >> 2) * f.mw + (xl >> 2)], qpp = qmap[(yp >> 2) * f.mw + (xp >> 2)];
+    const int qpq = qmap[m24(yl >> 2, f.mw) + (xl >> 2)], qpp = qmap[m24(yp >> 2, f.mw) + (xp >> 2)];
     const int qpc = chroma_qp_tab(((qpq + qpp + 1) >> 1) + cqpoff);
     const int bd = f.bit_depth_c;
     const int tc = kTc[clip3(0, 53, qpc + 2 + sl.tc_offset)] * (1 << (bd - 8));
     const int maxv = (1 << bd) - 1;
-    const bool nfp = fmap[(yp >> 2) * f.mw + (xp >> 2)] & 4;
-    const bool nfq = fmap[(yl >> 2) * f.mw + (xl >> 2)] & 4;
+    const bool nfp = fmap[m24(yp >> 2, f.mw) + (xp >> 2)] & 4;
+    const bool nfq = fmap[m24(yl >> 2, f.mw) + (xl >> 2)] & 4;
     if (vert) {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (yc + k >= ph) break;
-            Pel* row = pl + (yc + k) * st + xc;
+            const int ro = m24(yc + k, st) + xc;
             int a[4], c[4];
-            ld4(row - 4, a);
-            ld4(row, c);
+            ld4(at32(pl, ro - 4), a);
+            ld4(at32(pl, ro), c);
             const int p0 = a[3], p1 = a[2], q0 = c[0], q1 = c[1];
             const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
             a[3] = clip3(0, maxv, p0 + delta);
             c[0] = clip3(0, maxv, q0 - delta);
-            if (!nfp) st4(row - 4, a);
-            if (!nfq) st4(row, c);
+            if (!nfp) st4(at32(pl, ro - 4), a);
+            if (!nfq) st4(at32(pl, ro), c);
         }
     } else {
         int r[4][4];  // rows yc - 2 .. yc + 1, columns xc .. xc + 3 (chroma widths are multiples of 4)
 #pragma unroll
-        for (int j = 0; j < 4; j++) ld4(pl + (yc - 2 + j) * st + xc, r[j]);
+        for (int j = 0; j < 4; j++) ld4(at32(pl, m24(yc - 2 + j, st) + xc), r[j]);
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int p1 = r[0][k], p0 = r[1][k], q0 = r[2][k], q1 = r[3][k];
@@ -3200,15 +3206,15 @@ DEVI void hevc_chroma_edge(const h2j_frame& f, Pel* pl, int st, int pw, int ph, 
             r[1][k] = clip3(0, maxv, p0 + delta);
             r[2][k] = clip3(0, maxv, q0 - delta);
         }
-        if (!nfp) st4(pl + (yc - 1) * st + xc, r[1]);
-        if (!nfq) st4(pl + yc * st + xc, r[2]);
+        if (!nfp) st4(at32(pl, m24(yc - 1, st) + xc), r[1]);
+        if (!nfq) st4(at32(pl, m24(yc, st) + xc), r[2]);
     }
 }
 
 template <typename Pel>
 DEVI void deblock_thread(const h2j_frame& f, const h2j_ctb* ctbs, const h2j_slice* slices, uint8_t* arena,
                          bool vert, int x4, int y4) {
-    const int idx = y4 * f.mw + x4;
+    const int idx = m24(y4, f.mw) + x4;
     const uint8_t* fmap = arena + f.maps;
     const int8_t* qmap = reinterpret_cast<const int8_t*>(fmap + static_cast<size_t>(f.mw) * f.mh);
     const uint8_t fl = fmap[idx];
@@ -3381,8 +3387,8 @@ static_assert(offsetof(h2j_ctb, slice) == 9 && offsetof(h2j_ctb, qp) == 36 && of
                   sizeof(h2j_ctb) % 4 == 0,
               "h2j_ctb layout assumed by db264_info_raw");
 DEVI uint32_t db264_info_raw(const h2j_ctb* mbs, int mbw, int mx, int my, int lane) {
-    const int top = my > 0 ? (my - 1) * mbw + mx : my * mbw + mx;
-    const int idx = (lane & 2) ? top : my * mbw + mx;
+    const int top = my > 0 ? m24(my - 1, mbw) + mx : m24(my, mbw) + mx;
+    const int idx = (lane & 2) ? top : m24(my, mbw) + mx;
     return reinterpret_cast<const uint32_t*>(mbs + idx)[(lane & 1) ? 9 : 2];
 }
 // LDS copies of the H.264 deblocking tables (per-lane lookups, no scalar-load chains)
@@ -3423,9 +3429,9 @@ DEVI void db264_fetch2(const uint8_t* PB, uint32_t oc0, uint32_t oc1, int sty, i
     using TY = decltype(r.y);
     using TC = decltype(r.c);
     constexpr uint32_t B = sizeof(Pel);
-    r.y = *reinterpret_cast<const TY*>(PB + static_cast<uint32_t>((my * 16 + (hl >> 1)) * sty + mx * 16 + (hl & 1) * 8) * B);
+    r.y = *reinterpret_cast<const TY*>(PB + static_cast<uint32_t>(m24(my * 16 + (hl >> 1), sty) + mx * 16 + (hl & 1) * 8) * B);
     const int k = hl & 15;
-    r.c = *reinterpret_cast<const TC*>(PB + ((hl >> 4) ? oc1 : oc0) + static_cast<uint32_t>((my * 8 + (k >> 1)) * stc + mx * 8 + (k & 1) * 4) * B);
+    r.c = *reinterpret_cast<const TC*>(PB + ((hl >> 4) ? oc1 : oc0) + static_cast<uint32_t>(m24(my * 8 + (k >> 1), stc) + mx * 8 + (k & 1) * 4) * B);
 }
 // 4 uint16 window samples (two dwords) as 4 Pel of the picture / staging
 DEVI uint32_t db_pk8(uint2 v) { return __builtin_amdgcn_perm(v.y, v.x, 0x06040200u); }
@@ -3582,9 +3588,9 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } else if (row > 0) {
                     const int tr = hl >> 3, tc = (hl & 7) * 2;  // 4 rows x 16 luma columns, 2 per lane
-                    db_put_u16pair(&w.y[tr][tc + 4], db_line2(LY + tr * width + mx * 16 + tc));
+                    db_put_u16pair(&w.y[tr][tc + 4], db_line2(LY + m24(tr, width) + mx * 16 + tc));
                     const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // 2 comps x 2 rows x 8 columns
-                    w.c[c2][cr][k2 + 2] = static_cast<uint16_t>(LC[(c2 * 2 + cr) * cw + mx * 8 + k2]);
+                    w.c[c2][cr][k2 + 2] = static_cast<uint16_t>(LC[m24(c2 * 2 + cr, cw) + mx * 8 + k2]);
                 }
                 // prefetch the half's next MB (its next row: two pairs on) and its parameters
                 int nx = mx + 1, ny = row;
@@ -3729,14 +3735,14 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     if (fl) {  // the group's luma rows 12..15: 4 rows x LW / SS pieces of 16 bytes
                         const int g0 = mx - mx % GL, nmb = mx - g0 + 1;
                         const int tr = hl >> 3, sg = hl & 7;
-                        if (sg * SS < nmb * 16) db264_copy<Pel, SS>(py_at((row * 16 - 4 + tr) * sty + g0 * 16 + sg * SS), SA + tr * LW + sg * SS);
+                        if (sg * SS < nmb * 16) db264_copy<Pel, SS>(py_at(m24(row * 16 - 4 + tr, sty) + g0 * 16 + sg * SS), SA + tr * LW + sg * SS);
                     }
                     if (fc) {  // chroma rows 6..7: 2 comps x 2 rows x 8 pieces of 8 bytes
                         constexpr int S8 = 8 / static_cast<int>(sizeof(Pel));
                         const int g0 = mx - mx % GC, nmb = mx - g0 + 1;
                         const int c2 = hl >> 4, cr = (hl >> 3) & 1, cs = hl & 7;
                         if (cs * S8 < nmb * 8)
-                            db264_copy<Pel, S8>(pc_at(c2, (row * 8 - 2 + cr) * stc + g0 * 8 + cs * S8), SAc + (c2 * 2 + cr) * CW + cs * S8);
+                            db264_copy<Pel, S8>(pc_at(c2, m24(row * 8 - 2 + cr, stc) + g0 * 8 + cs * S8), SAc + (c2 * 2 + cr) * CW + cs * S8);
                     }
                 }
                 auto flush_bl = [&](int g0, int nmb) __attribute__((always_inline)) {
@@ -3745,7 +3751,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
 #pragma unroll
                     for (int k = 0; k < 16 * PR / 32; k++) {
                         const int e = hl + 32 * k, r = e / PR, sp = e % PR;
-                        if (r < nr && sp * SS < nmb * 16) db264_copy<Pel, SS>(py_at((row * 16 + r) * sty + g0 * 16 + sp * SS), SB + r * LW + sp * SS);
+                        if (r < nr && sp * SS < nmb * 16) db264_copy<Pel, SS>(py_at(m24(row * 16 + r, sty) + g0 * 16 + sp * SS), SB + r * LW + sp * SS);
                     }
                 };
                 auto flush_bc = [&](int g0, int nmb) __attribute__((always_inline)) {
@@ -3755,7 +3761,7 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                     for (int k = 0; k < 2; k++) {
                         const int e = hl + 32 * k, c2 = e >> 5, cr = (e >> 2) & 7, sg = e & 3;
                         if (cr < ncr) {
-                            Pel* d = pc_at(c2, (row * 8 + cr) * stc + g0 * 8 + sg * SS);
+                            Pel* d = pc_at(c2, m24(row * 8 + cr, stc) + g0 * 8 + sg * SS);
                             const Pel* q = SBc + (c2 * 8 + cr) * CW + sg * SS;
                             if ((sg + 1) * SS <= nmb * 8) cput16(d, q);
                             else if (sg * SS < nmb * 8) db264_copy<Pel, 8>(d, q);  // 8 bits: an odd last MB
@@ -3817,15 +3823,15 @@ DEVI void h264_db_pairs(const h2j_frame& f, const h2j_ctb* mbs, const h2j_slice*
                 } else if (row + 1 < mbh) {
                     {
                         const int tr = hl >> 3, tc = (hl & 7) * 2;  // rows 12..15 of this MB, 2 per lane
-                        if (tc < 12 || last) db_put_line2(LY + tr * width + mx * 16 + tc, db_u16pair(&w.y[tr + 16][tc + 4]));
+                        if (tc < 12 || last) db_put_line2(LY + m24(tr, width) + mx * 16 + tc, db_u16pair(&w.y[tr + 16][tc + 4]));
                     }
                     if (mx > 0 && hl < 8) {
                         const int tr = hl >> 1, tc = (hl & 1) * 2;
-                        db_put_line2(LY + tr * width + mx * 16 - 4 + tc, db_u16pair(&w.y[tr + 16][tc]));
+                        db_put_line2(LY + m24(tr, width) + mx * 16 - 4 + tc, db_u16pair(&w.y[tr + 16][tc]));
                     }
                     const int c2 = hl >> 4, cr = (hl >> 3) & 1, k2 = hl & 7;  // chroma rows 6..7
-                    if (k2 < 6 || last) LC[(c2 * 2 + cr) * cw + mx * 8 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2 + 2]);
-                    if (mx > 0 && k2 < 2) LC[(c2 * 2 + cr) * cw + mx * 8 - 2 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2]);
+                    if (k2 < 6 || last) LC[m24(c2 * 2 + cr, cw) + mx * 8 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2 + 2]);
+                    if (mx > 0 && k2 < 2) LC[m24(c2 * 2 + cr, cw) + mx * 8 - 2 + k2] = static_cast<Line>(w.c[c2][cr + 8][k2]);
                 }
                 wave_sync();
                 {  // carry the last columns into the next MB's left strip
