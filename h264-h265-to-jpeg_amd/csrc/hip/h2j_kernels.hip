@@ -419,6 +419,10 @@ struct K0F {  // frame fields K0 uses, in scalar registers (see FU)
     int bd, bdc, slist, log2ctb, ctb_w, width, height, mw, topo, rext;
     uint32_t sl;
 };
+// 24-bit signed multiply (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate) for index
+// arithmetic whose operands fit 24 bits (sample / block coordinates, strides, small factors)
+DEVI int m24(int a, int b) { return __mul24(a, b); }
+
 // Sample (x, y) of component c in the tiled HEVC residual planes (h2j_res_q, include/h2j_gpu.h);
 // rows of a tile are 1 << h2j_res_q(log2ctb, c) elements apart.
 DEVI int16_t* hevc_res_at(int16_t* res, int width, int height, int log2ctb, int c, int x, int y) {
@@ -437,8 +441,10 @@ DEVI int16_t* hevc_res_at(int16_t* res, int width, int height, int log2ctb, int 
 // fetches an MB as one contiguous piece (h264_rows).  Rows of a block are 16 (luma) / 8 (chroma)
 // elements apart.
 DEVI int16_t* h264_res_at(int16_t* res, int mbw, int c, int x, int y) {
-    if (c == 0) return res + ((y >> 4) * mbw + (x >> 4)) * 384 + ((y & 15) << 4) + (x & 15);
-    return res + ((y >> 3) * mbw + (x >> 3)) * 384 + 256 + (c - 1) * 64 + ((y & 7) << 3) + (x & 7);
+    // (24-bit multiplies and a 32-bit byte offset from the uniform base: r05)
+    const int o = c == 0 ? m24(m24(y >> 4, mbw) + (x >> 4), 384) + ((y & 15) << 4) + (x & 15)
+                         : m24(m24(y >> 3, mbw) + (x >> 3), 384) + 256 + (c - 1) * 64 + ((y & 7) << 3) + (x & 7);
+    return reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(res) + static_cast<uint32_t>(o) * 2u);
 }
 // H.264 MBAFF frames keep TU records and MB records in the macroblock grid (grid row = 2 * pair row
 // + bottom); a field macroblock's row r is picture row 2 * r + bottom of its pair (h2j_ctb.mbflags
@@ -2053,10 +2059,8 @@ __host__ __device__ constexpr size_t k1_fixed_lds(int waves) { return sizeof(QWa
 
 // intraPredAngle / invAngle (H.265 Tables 8-4, 8-5) from the mode with scalar
 // arithmetic on packed constants (no memory round trip per TB):
-// d = m - 26 (vertical) or 10 - m (horizontal), angle = sign(d) * mag[|d|].
-// 24-bit signed multiply (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate): every use
-// multiplies a sample (<= 16 bits) or a window / angle index by a small factor
-DEVI int m24(int a, int b) { return __mul24(a, b); }
+// d = m - 26 (vertical) or 10 - m (horizontal), angle = sign(d) * mag[|d|].  (m24 -- see its
+// definition -- multiplies a sample (<= 16 bits) or a window / angle index by a small factor.)
 // Both from k = |d| with no compare chain (r05: resolving invAngle by comparing the angle against
 // its eight values compiled to ~40 scalar instructions and branches per angular TB).
 struct HevcAng {
@@ -3075,6 +3079,10 @@ DEVI void st4(Pel* p, const int (&v)[4]) {
 template <typename Pel>
 DEVI Pel* at32(Pel* base, int off) {
     return reinterpret_cast<Pel*>(reinterpret_cast<uint8_t*>(base) + static_cast<uint32_t>(off) * static_cast<uint32_t>(sizeof(Pel)));
+}
+template <typename Pel>
+DEVI const Pel* at32(const Pel* base, int off) {
+    return reinterpret_cast<const Pel*>(reinterpret_cast<const uint8_t*>(base) + static_cast<uint32_t>(off) * static_cast<uint32_t>(sizeof(Pel)));
 }
 template <typename Pel>
 DEVI void hevc_luma_edge(const h2j_frame& f, Pel* pl, int st, const uint8_t* fmap, const int8_t* qmap,
@@ -4154,11 +4162,11 @@ DEVI void sao_stage_load(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, in
         const int i = tid + 256 * k, r = i >> g.lq, ch = i & ((1 << g.lq) - 1);
         const int y = g.y0 + r - 1, x = g.x0 + 4 * ch;
         iv[k] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (r < g.h + 2 && 4 * ch < g.w && y >= 0 && y < g.ph) iv[k] = sao_load4(P + y * st + x);
+        if (r < g.h + 2 && 4 * ch < g.w && y >= 0 && y < g.ph) iv[k] = sao_load4(at32(P, m24(y, st) + x));
     }
     const int r = tid >> 1, x = (tid & 1) ? g.x0 + g.w : g.x0 - 1, y = g.y0 + r - 1;
     bv = -1;
-    if (r < g.h + 2 && x >= 0 && x < g.pw && y >= 0 && y < g.ph) bv = static_cast<int16_t>(P[y * st + x]);
+    if (r < g.h + 2 && x >= 0 && x < g.pw && y >= 0 && y < g.ph) bv = static_cast<int16_t>(*at32(P, m24(y, st) + x));
 }
 template <int NI>
 DEVI void sao_stage_store(const SaoGeo& g, int16_t* T, const uint2 (&iv)[NI], int16_t bv) {
@@ -4275,7 +4283,7 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
                           (static_cast<unsigned long long>(s4 * wgt) << 32) | (n4 * wgt));
             }
         }
-        Pel* d = D + (g.y0 + y) * st + g.x0 + x;
+        Pel* d = at32(D, m24(g.y0 + y, st) + g.x0 + x);
         if (sizeof(Pel) == 1) {
             *reinterpret_cast<uint32_t*>(d) = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 8) |
                                               (static_cast<uint32_t>(o[2]) << 16) | (static_cast<uint32_t>(o[3]) << 24);
