@@ -4402,10 +4402,10 @@ DEVI void sao_ctb(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* SL, uin
 __global__ void __launch_bounds__(256, 8) h2j_k3_sao(const h2j_frame* __restrict__ frames,
                                                  const h2j_ctb* __restrict__ ctbs,
                                                  const h2j_slice* __restrict__ slices, uint8_t* __restrict__ arena,
-                                                 int fold) {
+                                                 int fold, const uint32_t* __restrict__ ymap) {
     const GridPos gp = xcd_grid_pos();
     __shared__ SaoLds L;
-    const h2j_frame& f = frames[gp.y];
+    const h2j_frame& f = frames[ymap[gp.y]];  // gp.y: picture of this launch's CTB-count class
     if (f.codec != H2J_CODEC_HEVC || f.pic2 == f.pic) return;
     const int ctb = gp.x;
     if (ctb >= f.ctb_w * f.ctb_h) return;
@@ -5123,10 +5123,16 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
 int h2j_gpu_sao(const h2j_gpu_batch* b, void* stream) {
     if (!b || b->nframes <= 0 || !b->has_hevc) return 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    // CTB grid of the largest picture at the smallest CTB size present is bounded by max_ctbs
-    dim3 grid(static_cast<unsigned>(b->max_ctbs), b->nframes);
-    hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1);
-    return check(hipGetLastError(), "h2j_k3_sao");
+    // one launch per CTB-count class (h2j_gpu_batch.sao_map): grid = the class's largest CTB count
+    // x its pictures, so a mixed batch's small pictures do not run the 4K grid's empty workgroups
+    for (int g = 0; g < b->sao_groups && g < H2J_SAO_GROUPS; g++) {
+        if (b->sao_count[g] <= 0 || b->sao_ctbs[g] <= 0) continue;
+        dim3 grid(static_cast<unsigned>(b->sao_ctbs[g]), static_cast<unsigned>(b->sao_count[g]));
+        hipLaunchKernelGGL(h2j_k3_sao, grid, dim3(256), 0, s, b->frames, b->ctbs, b->slices, b->arena, 1,
+                           b->sao_map + b->sao_first[g]);
+        if (int rc = check(hipGetLastError(), "h2j_k3_sao")) return rc;
+    }
+    return 0;
 }
 
 int h2j_gpu_jpeg(const h2j_gpu_batch* b, void* stream) {

@@ -377,7 +377,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         f.xline = 0;
         s.frames[k] = f;
         max_w = std::max(max_w, f.width);
-        max_ctbs = std::max(max_ctbs, f.ctb_w * f.ctb_h);
+        if (f.codec == H2J_CODEC_HEVC) max_ctbs = std::max(max_ctbs, f.ctb_w * f.ctb_h);
         max_h = std::max(max_h, f.height);
         const int mcu = ((f.out_w + 15) >> 4) * ((f.out_h + 15) >> 4);
         max_mcu = std::max(max_mcu, mcu);
@@ -493,9 +493,34 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
                          [](const std::pair<int, uint32_t>& a, const std::pair<int, uint32_t>& b) { return a.first < b.first; });
         for (const auto& x : e) k1all.push_back(x.second);
     }
+    // K3 SAO map: the HEVC pictures with SAO, most CTBs first, cut into CTB-count classes (a picture
+    // joins the current class while it has more than half the class's CTBs; the last class takes
+    // the rest), one launch each, so no class pays for the largest picture's grid width
+    std::vector<uint32_t> saomap;
+    int sao_groups = 0, sao_first[H2J_SAO_GROUPS] = {}, sao_count[H2J_SAO_GROUPS] = {}, sao_ctbs[H2J_SAO_GROUPS] = {};
+    {
+        std::vector<std::pair<int, uint32_t>> e;
+        for (int k = 0; k < nf; k++) {
+            const h2j_frame& f = s.frames[k];
+            if (f.codec == H2J_CODEC_HEVC && f.pic2 != f.pic) e.emplace_back(f.ctb_w * f.ctb_h, static_cast<uint32_t>(k));
+        }
+        std::stable_sort(e.begin(), e.end(),
+                         [](const std::pair<int, uint32_t>& a, const std::pair<int, uint32_t>& b) { return a.first > b.first; });
+        for (size_t i = 0; i < e.size(); i++) {
+            const bool same = sao_groups > 0 && (sao_groups == H2J_SAO_GROUPS || 2 * e[i].first > sao_ctbs[sao_groups - 1]);
+            if (!same) {
+                sao_first[sao_groups] = static_cast<int>(i);
+                sao_ctbs[sao_groups] = e[i].first;
+                sao_groups++;
+            }
+            sao_count[sao_groups - 1]++;
+            saomap.push_back(e[i].second);
+        }
+    }
     const size_t o_map = align_up(o_sl + nsl + 16, 256);
     const size_t o_all = align_up(o_map + k1map.size() * 4 + 16, 256);
-    const size_t in_bytes = align_up(o_all + k1all.size() * 4 + 16, 256);
+    const size_t o_sao = align_up(o_all + k1all.size() * 4 + 16, 256);
+    const size_t in_bytes = align_up(o_sao + saomap.size() * 4 + 16, 256);
     if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
     if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
     if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
@@ -510,6 +535,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     std::memcpy(s.h_in.p + o_frames, s.frames.data(), nf * sizeof(h2j_frame));
     if (!k1map.empty()) std::memcpy(s.h_in.p + o_map, k1map.data(), k1map.size() * 4);
     if (!k1all.empty()) std::memcpy(s.h_in.p + o_all, k1all.data(), k1all.size() * 4);
+    if (!saomap.empty()) std::memcpy(s.h_in.p + o_sao, saomap.data(), saomap.size() * 4);
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -562,6 +588,13 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.k1wgs = static_cast<int32_t>(k1map.size());
     b.k1all = reinterpret_cast<const uint32_t*>(din + o_all);
     b.k1all_n = static_cast<int32_t>(k1all.size());
+    b.sao_map = reinterpret_cast<const uint32_t*>(din + o_sao);
+    b.sao_groups = sao_groups;
+    for (int g = 0; g < H2J_SAO_GROUPS; g++) {
+        b.sao_first[g] = sao_first[g];
+        b.sao_count[g] = sao_count[g];
+        b.sao_ctbs[g] = sao_ctbs[g];
+    }
     b.hevc_pels = 0;
     for (int k = 0; k < nf; k++)
         if (s.frames[k].codec == H2J_CODEC_HEVC) b.hevc_pels |= (s.frames[k].bit_depth > 8 || s.frames[k].bit_depth_c > 8) ? 2 : 1;

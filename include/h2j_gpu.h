@@ -78,6 +78,8 @@ constexpr bool h2j_sao_folds_variance(const h2j_frame &f) {
 #define H2J_JSYM_MAX 68
 #define H2J_JTILE_BYTES (H2J_JSYM_MAX * 256 * 4 + 256 + 512)
 
+#define H2J_SAO_GROUPS 4
+
 /* One batch of pictures resident in HBM.  All pointers are device pointers. */
 typedef struct {
     int32_t nframes;
@@ -85,7 +87,7 @@ typedef struct {
     int32_t max_mcu;            /* max JPEG MCUs over the batch */
     int32_t max_ntu;            /* max transform-block records over the batch */
     int32_t has_hevc, has_h264; /* codecs present in the batch */
-    int32_t max_ctbs;           /* max CTBs (H.264: macroblocks) of one picture over the batch */
+    int32_t max_ctbs;           /* max CTBs of one HEVC picture over the batch */
     int32_t k1wgs;              /* H.264 K1 workgroups (sum of h2j_frame.k1bands over H.264 pictures) */
     const uint32_t *k1map;      /* H.264 K1 workgroup -> (frame << 8) | band, dependency order */
     int32_t hevc_pels;          /* HEVC sample types present: bit 0 8-bit, bit 1 high bit depth */
@@ -109,6 +111,11 @@ typedef struct {
                                    h2j_sao_folds_variance); 0: K4a is not launched */
     int32_t has_mbaff;          /* H.264 MBAFF frames present (K1 runs h2j_k1_recon_h264_mbaff for them) */
     int32_t h264_pels;          /* non-MBAFF H.264 sample types present: bit 0 8-bit, bit 1 high bit depth */
+    /* K3 SAO: one launch per CTB-count class of the HEVC pictures with SAO (a mixed batch's 720p,
+       1080p and 4K pictures each get a grid of their own width instead of the largest one's) */
+    int32_t sao_groups;         /* launches (0..H2J_SAO_GROUPS) */
+    int32_t sao_first[H2J_SAO_GROUPS], sao_count[H2J_SAO_GROUPS], sao_ctbs[H2J_SAO_GROUPS];
+    const uint32_t *sao_map;    /* frame indices of the HEVC pictures with SAO, most CTBs first */
 } h2j_gpu_batch;
 
 /* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
