@@ -4040,7 +4040,10 @@ DEVI void h264_db_mbaff(const h2j_frame& f, const h2j_ctb* C, const h2j_slice* S
 // One kernel per sample type (its window and LDS line sizes differ: the 8-bit one fits two
 // workgroups per CU) and one for MBAFF frames (no windows: its LDS is the progress words); each
 // skips the pictures of the others.  Launched for the kinds present (h2j_gpu_batch.h264_pels).
-template <typename Pel>
+// kWide: the pictures wider than the launch's LDS line (line_w) with their line buffer in global
+// memory; the LDS-line launch sizes its line for two workgroups per CU at 8 bits, so a batch with
+// 4K pictures does not drop every picture's deblocking to one workgroup per CU.
+template <typename Pel, bool kWide>
 __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2j_frame* frames, const h2j_ctb* ctbs,
                                                                       const h2j_slice* slices, uint8_t* arena,
                                                                       const uint32_t* map, int line_w) {
@@ -4054,6 +4057,7 @@ __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2
     const h2j_frame& f = frames[me >> 8];
     const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264 || ufl(f.mbaff) || (ufl(f.bit_depth) == 8) != (sizeof(Pel) == 1)) return;
+    if ((static_cast<int>(ufl(f.width)) > line_w) != kWide) return;  // the other launch's picture
     const int nbands = ufl(f.k1bands);
     const h2j_ctb* C = ctbs + f.ctb;
     const h2j_slice* S = slices + f.slice;
@@ -4069,11 +4073,7 @@ __global__ void __launch_bounds__(64 * kDbPairWaves) h2j_k2_deblock264p(const h2
     if (t < nsl * static_cast<int>(sizeof(h2j_slice) / 4))
         reinterpret_cast<uint32_t*>(TB.sl)[t] = reinterpret_cast<const uint32_t*>(S)[t];
     __syncthreads();
-    if constexpr (sizeof(Pel) == 1) {
-        // 8 bits: the LDS line buffer (6 bytes per column) holds any width the parser accepts
-        // (512 MBs; h2j_gpu_deblock checks line_w), so there is no global-memory variant
-        h264_db_pairs<Pel, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
-    } else if (ufl(f.width) <= line_w) {
+    if constexpr (!kWide) {
         h264_db_pairs<Pel, false>(f, C, S, arena, W, prog, line, band, nbands, TB);
     } else {  // one line buffer per band in the picture's residual region (12 bytes per column)
         uint16_t* gl = reinterpret_cast<uint16_t*>(arena + ufl64(f.res)) + static_cast<size_t>(band) * 6 * ufl(f.width);
@@ -5083,35 +5083,55 @@ int h2j_gpu_deblock(const h2j_gpu_batch* b, void* stream) {
         if (r) return r;
     }
     if (!b->has_h264 || b->k1wgs <= 0) return 0;
-    // dynamic LDS: windows, progress, tables and a line buffer of the batch's widest picture
-    // (6 samples per column) when it fits the CU's 160 KB (wider: global memory)
-    auto launch = [&](auto pel, const void* fn, const char* name) -> int {
+    // dynamic LDS: windows, progress, tables and a line buffer (6 samples per column) of the batch's
+    // widest picture up to line_w: at 8 bits the width that keeps two workgroups per CU (80 KB),
+    // at 16 bits what fits the CU's 160 KB.  Wider pictures: a second launch, line in global memory.
+    auto launch = [&](auto pel, const void* fn, const void* fn_wide, const char* name) -> int {
         using Pel = decltype(pel);
-        static size_t cap[2] = {0, 0};  // 160 KB minus the kernel's static LDS
+        static size_t cap[2] = {0, 0};  // LDS budget minus the kernel's static LDS
         size_t& c = cap[sizeof(Pel) - 1];
+        const size_t fixed = sizeof(DbWin<Pel>) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
         if (!c) {
             hipFuncAttributes fa{};
             const size_t st = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : 0;
-            c = 160 * 1024 - st;
-            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(c));
+            c = (sizeof(Pel) == 1 ? 80 : 160) * 1024 - st;
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(160 * 1024 - st));
+            (void)hipFuncSetAttribute(fn_wide, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fixed));
             (void)hipGetLastError();
         }
-        const size_t fixed = sizeof(DbWin<Pel>) * 2 * kDbPairWaves + kDbPairSlots * 4 + sizeof(DbTables);
         const int line_w = std::min(b->max_w, static_cast<int>((c - fixed) / (6 * sizeof(Pel))) & ~15);
-        if (sizeof(Pel) == 1 && line_w < b->max_w) {  // never for parser-legal widths (<= 8192)
-            snprintf(g_err, sizeof(g_err), "h2j_k2_deblock264p<u8>: a %d-sample line does not fit LDS", b->max_w);
-            return -1;
+        // the wide pictures (long banded chains) on the companion stream, started first and
+        // running beside the LDS-line launch instead of after its tail
+        const bool wide = b->max_w > line_w;
+        AuxStream* ax = wide ? aux_stream(s) : nullptr;
+        if (ax) {
+            (void)hipEventRecord(ax->fork, s);
+            (void)hipStreamWaitEvent(ax->s2, ax->fork, 0);
         }
-        hipLaunchKernelGGL(h2j_k2_deblock264p<Pel>, dim3(b->k1wgs), dim3(64 * kDbPairWaves),
+        if (wide) {
+            hipLaunchKernelGGL((h2j_k2_deblock264p<Pel, true>), dim3(b->k1wgs), dim3(64 * kDbPairWaves), fixed,
+                               ax ? ax->s2 : s, b->frames, b->ctbs, b->slices, b->arena, b->k1map, line_w);
+            const int rw = check(hipGetLastError(), name);
+            if (ax) (void)hipEventRecord(ax->join, ax->s2);
+            if (rw) {
+                if (ax) (void)hipStreamWaitEvent(s, ax->join, 0);
+                return rw;
+            }
+        }
+        hipLaunchKernelGGL((h2j_k2_deblock264p<Pel, false>), dim3(b->k1wgs), dim3(64 * kDbPairWaves),
                            fixed + 6 * sizeof(Pel) * static_cast<size_t>(line_w), s, b->frames, b->ctbs, b->slices,
                            b->arena, b->k1map, line_w);
-        return check(hipGetLastError(), name);
+        const int rc = check(hipGetLastError(), name);
+        if (ax) (void)hipStreamWaitEvent(s, ax->join, 0);
+        return rc;
     };
     int r = 0;
     if (b->h264_pels & 1)
-        r = launch(uint8_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint8_t>), "h2j_k2_deblock264p<u8>");
+        r = launch(uint8_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint8_t, false>),
+                   reinterpret_cast<const void*>(h2j_k2_deblock264p<uint8_t, true>), "h2j_k2_deblock264p<u8>");
     if (!r && (b->h264_pels & 2))
-        r = launch(uint16_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint16_t>), "h2j_k2_deblock264p<u16>");
+        r = launch(uint16_t{}, reinterpret_cast<const void*>(h2j_k2_deblock264p<uint16_t, false>),
+                   reinterpret_cast<const void*>(h2j_k2_deblock264p<uint16_t, true>), "h2j_k2_deblock264p<u16>");
     if (!r && b->has_mbaff) {
         hipLaunchKernelGGL(h2j_k2_deblock264m, dim3(b->k1wgs), dim3(64 * kDbPairWaves), 0, s, b->frames, b->ctbs,
                            b->slices, b->arena, b->k1map);
