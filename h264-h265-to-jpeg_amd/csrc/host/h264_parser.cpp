@@ -790,7 +790,9 @@ int H264Parser::residual_block_t(int cat, int cbf_inc, int max_num, uint8_t* pos
 
 template <bool AFF>
 void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, const uint32_t* e, int n) {
-    h2j_tu t;
+    // built in place (a local record copied in would wait on store-to-load forwarding of its fields)
+    job_->tus.emplace_back();
+    h2j_tu& t = job_->tus.back();
     t.x = static_cast<uint16_t>(x);
     t.y = static_cast<uint16_t>(y);
     t.log2n = static_cast<uint8_t>(log2n);
@@ -817,12 +819,12 @@ void H264Parser::emit_sparse(int x, int y, int log2n, int c, int mode, int qp, c
             if (h) t.flags |= H2J_TU_DPCM_H;
         }
     }
-    job_->tus.push_back(t);
 }
 
 void H264Parser::emit(int x, int y, int log2n, int c, int mode, uint8_t flags, int qp, const int* lv, int npos,
                       bool pcm) {
-    h2j_tu t;
+    job_->tus.emplace_back();
+    h2j_tu& t = job_->tus.back();
     t.x = static_cast<uint16_t>(x);
     t.y = static_cast<uint16_t>(y);
     t.log2n = static_cast<uint8_t>(log2n);
@@ -835,7 +837,6 @@ void H264Parser::emit(int x, int y, int log2n, int c, int mode, uint8_t flags, i
         if (lv[i] || pcm) job_->coefs.push_back((static_cast<uint32_t>(i) << 16) | static_cast<uint16_t>(lv[i]));
     t.ncoef = static_cast<uint16_t>(job_->coefs.size() - t.coef);
     t.flags = flags | (t.ncoef ? H2J_TU_CBF : 0);
-    job_->tus.push_back(t);
 }
 
 int chroma_qp_264(int qpi) {

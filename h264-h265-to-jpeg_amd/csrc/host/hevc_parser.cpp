@@ -1320,7 +1320,10 @@ void HevcParser::split_ctb_records(size_t first) {
 }
 
 void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags, bool cbf, int) {
-    h2j_tu tu;
+    // built in place: a local record filled field by field and then copied into the vector made
+    // the copy's 16-byte load wait for the narrow stores (store-to-load forwarding fails)
+    job_->tus.emplace_back();
+    h2j_tu& tu = job_->tus.back();
     tu.x = static_cast<uint16_t>(x);
     tu.y = static_cast<uint16_t>(y);
     tu.log2n = static_cast<uint8_t>(log2n);
@@ -1335,7 +1338,6 @@ void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags
         if (rext_) residual<true>(log2n, c, mode, tu);
         else residual<false>(log2n, c, mode, tu);
     }
-    job_->tus.push_back(tu);
 }
 
 void HevcParser::transform_unit(int x0, int y0, int xb, int yb, int log2n, int blk, int cbf_l, int cbf_cb,
