@@ -452,11 +452,21 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     // H.264 K1 workgroup map: banded pictures first (their long chains start early), bands in order,
     // then the others by transform-block count, most first (the dispatcher hands workgroups out in
     // map order: the heaviest pictures start in the first round, not in the launch's tail)
+    // Banded pictures band-major (every picture's band 0, then every band 1, ...): a band waits on
+    // the band above, and picture-major order had each picture's lower bands holding workgroup
+    // slots while they waited (a batch of 4K H.264 pictures ran at a fraction of the GPU).  A band
+    // still follows the band above it in the map, so it never waits on one not yet dispatched.
     std::vector<uint32_t> k1map;
-    for (int k = 0; k < nf; k++) {
-        const h2j_frame& f = s.frames[k];
-        if (f.codec != H2J_CODEC_H264 || f.k1bands <= 1) continue;
-        for (int bnd = 0; bnd < f.k1bands; bnd++) k1map.push_back((static_cast<uint32_t>(k) << 8) | bnd);
+    {
+        int maxb = 0;
+        for (int k = 0; k < nf; k++)
+            if (s.frames[k].codec == H2J_CODEC_H264 && s.frames[k].k1bands > 1) maxb = std::max(maxb, static_cast<int>(s.frames[k].k1bands));
+        for (int bnd = 0; bnd < maxb; bnd++)
+            for (int k = 0; k < nf; k++) {
+                const h2j_frame& f = s.frames[k];
+                if (f.codec != H2J_CODEC_H264 || f.k1bands <= 1 || bnd >= static_cast<int>(f.k1bands)) continue;
+                k1map.push_back((static_cast<uint32_t>(k) << 8) | static_cast<uint32_t>(bnd));
+            }
     }
     {
         std::vector<std::pair<uint32_t, uint32_t>> un;
