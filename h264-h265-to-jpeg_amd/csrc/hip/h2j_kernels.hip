@@ -1629,9 +1629,10 @@ DEVI void h264_rows(const h2j_frame& f, const h2j_tu* T, uint8_t* arena, H4WaveL
     uint16_t* LC = line + W;        // [2][Wc]
     const uint32_t ntot = ufl(f.ntu);
     AVP_DECL;
-    // this workgroup's rows: one band of 16 MB rows (one per wave; tall pictures run on several
-    // workgroups, see h2j_frame.k1bands) or, unbanded, rows w, w + 16, ...
-    const int rbeg = band * 16, rend = nbands > 1 ? min(mbh, rbeg + 16) : mbh;
+    // this workgroup's rows: one band of NW MB rows (one per wave; tall pictures run on several
+    // workgroups: 16-row bands in the merged launch, 8-row ones in h2j_k1_recon_h264) or,
+    // unbanded, rows w, w + NW, ...
+    const int rbeg = band * NW, rend = nbands > 1 ? min(mbh, rbeg + NW) : mbh;
     // band hand-off: per-row progress words (4th word of the row's first CTB range, zeroed) and
     // the boundary rows, both accessed with agent-scope atomics (coherent across CUs / XCDs)
     const uint64_t o_flag = ufl64(f.ctbrng) + 12, o_xl = ufl64(f.xline);
@@ -2881,8 +2882,8 @@ __global__ void __launch_bounds__(64 * W_, 4) h2j_k1_recon_hevc(const h2j_frame*
                        static_cast<int>(threadIdx.x >> 6), W_);
 }
 
-// grid = h2j_gpu_batch.k1wgs: workgroup -> (picture, band) from the host's map (bands of a
-// picture in order, so a band only ever waits on an earlier workgroup)
+// grid = h2j_gpu_batch.k1wgs8: workgroup -> (picture, band of kAvcK1Waves rows) from the host's
+// map (band-major, so a band only ever waits on an earlier workgroup)
 __global__ void __launch_bounds__(64 * kAvcK1Waves, 4) h2j_k1_recon_h264(const h2j_frame* frames, const h2j_tu* tus,
                                                                     const h2j_ctb* ctbs, uint8_t* arena, const uint32_t* map) {
     extern __shared__ __align__(16) uint8_t h4lds[];
@@ -2893,7 +2894,7 @@ __global__ void __launch_bounds__(64 * kAvcK1Waves, 4) h2j_k1_recon_h264(const h
     const h2j_frame& f = frames[me >> 8];
     const int band = static_cast<int>(me & 0xFF);
     if (f.codec != H2J_CODEC_H264) return;
-    const int nbands = ufl(f.k1bands);
+    const int nbands = ufl(f.k1bands) > 1 ? (static_cast<int>(ufl(f.ctb_h)) + kAvcK1Waves - 1) / kAvcK1Waves : 1;
     if (threadIdx.x < 2 * kAvcK1Waves) prog[threadIdx.x] = 0;
     __syncthreads();
     H4WaveLds& s = wl[threadIdx.x >> 6];
@@ -4986,8 +4987,8 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     if (ax) {
         (void)hipEventRecord(ax->fork, s);
         (void)hipStreamWaitEvent(ax->s2, ax->fork, 0);
-        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcK1Waves), lds264, ax->s2, b->frames, b->tus,
-                           b->ctbs, b->arena, b->k1map);
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs8), dim3(64 * kAvcK1Waves), lds264, ax->s2, b->frames, b->tus,
+                           b->ctbs, b->arena, b->k1map8);
         const int r = check(hipGetLastError(), "h2j_k1_recon_h264");
         (void)hipEventRecord(ax->join, ax->s2);
         if (r) {
@@ -5034,8 +5035,8 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     if (b->has_h264 && !ax) {
         // dynamic LDS: per-wave windows, progress counters, line buffer (luma + 2 chroma, uint16)
         if (b->k1wgs > 0)
-            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs), dim3(64 * kAvcK1Waves), lds264, s, b->frames, b->tus,
-                               b->ctbs, b->arena, b->k1map);
+            hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs8), dim3(64 * kAvcK1Waves), lds264, s, b->frames, b->tus,
+                               b->ctbs, b->arena, b->k1map8);
         return check(hipGetLastError(), "h2j_k1_recon_h264");
     }
     return 0;

@@ -437,8 +437,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         f.aux = off;
         off = align_up(off + static_cast<size_t>(f.ntu) * 8, 256);
         if (f.k1bands > 1) {  // per band boundary: K1 1 luma + 2 chroma rows, K2 4 luma + 2x2 chroma rows (uint16)
-            f.xline = off;
-            off = align_up(off + static_cast<size_t>(f.k1bands - 1) * 6 * f.width * 2, 256);
+            f.xline = off;   // K1's 8-row bands and K2's 16-row bands use it one after the other
+            const size_t k2b = static_cast<size_t>(f.k1bands - 1) * 6 * f.width * 2;
+            const size_t k1b = static_cast<size_t>((f.ctb_h + 7) / 8 - 1) * 2 * f.width * 2;
+            off = align_up(off + std::max(k1b, k2b), 256);
         }
     }
     const size_t arena_bytes = off;
@@ -468,6 +470,20 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
                 k1map.push_back((static_cast<uint32_t>(k) << 8) | static_cast<uint32_t>(bnd));
             }
     }
+    // the same for h2j_k1_recon_h264's 8-wave workgroups: bands of 8 rows (16-row bands took two
+    // row rounds each, so a band below started a whole row time after the band above)
+    std::vector<uint32_t> k1map8;
+    {
+        int maxb = 0;
+        for (int k = 0; k < nf; k++)
+            if (s.frames[k].codec == H2J_CODEC_H264 && s.frames[k].k1bands > 1) maxb = std::max(maxb, (s.frames[k].ctb_h + 7) / 8);
+        for (int bnd = 0; bnd < maxb; bnd++)
+            for (int k = 0; k < nf; k++) {
+                const h2j_frame& f = s.frames[k];
+                if (f.codec != H2J_CODEC_H264 || f.k1bands <= 1 || bnd >= (f.ctb_h + 7) / 8) continue;
+                k1map8.push_back((static_cast<uint32_t>(k) << 8) | static_cast<uint32_t>(bnd));
+            }
+    }
     {
         std::vector<std::pair<uint32_t, uint32_t>> un;
         for (int k = 0; k < nf; k++) {
@@ -477,7 +493,10 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
         std::stable_sort(un.begin(), un.end(), [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
                 return a.first > b.first;
             });
-        for (const auto& x : un) k1map.push_back(x.second << 8);
+        for (const auto& x : un) {
+            k1map.push_back(x.second << 8);
+            k1map8.push_back(x.second << 8);
+        }
     }
     // mixed-batch K1 map (h2j_k1_recon_any): every HEVC picture and H.264 band, tallest first so
     // the longest chains start first; bands of one picture stay in order
@@ -530,7 +549,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const size_t o_map = align_up(o_sl + nsl + 16, 256);
     const size_t o_all = align_up(o_map + k1map.size() * 4 + 16, 256);
     const size_t o_sao = align_up(o_all + k1all.size() * 4 + 16, 256);
-    const size_t in_bytes = align_up(o_sao + saomap.size() * 4 + 16, 256);
+    const size_t o_map8 = align_up(o_sao + saomap.size() * 4 + 16, 256);
+    const size_t in_bytes = align_up(o_map8 + k1map8.size() * 4 + 16, 256);
     if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
     if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
     if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
@@ -546,6 +566,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     if (!k1map.empty()) std::memcpy(s.h_in.p + o_map, k1map.data(), k1map.size() * 4);
     if (!k1all.empty()) std::memcpy(s.h_in.p + o_all, k1all.data(), k1all.size() * 4);
     if (!saomap.empty()) std::memcpy(s.h_in.p + o_sao, saomap.data(), saomap.size() * 4);
+    if (!k1map8.empty()) std::memcpy(s.h_in.p + o_map8, k1map8.data(), k1map8.size() * 4);
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -598,6 +619,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.k1wgs = static_cast<int32_t>(k1map.size());
     b.k1all = reinterpret_cast<const uint32_t*>(din + o_all);
     b.k1all_n = static_cast<int32_t>(k1all.size());
+    b.k1map8 = reinterpret_cast<const uint32_t*>(din + o_map8);
+    b.k1wgs8 = static_cast<int32_t>(k1map8.size());
     b.sao_map = reinterpret_cast<const uint32_t*>(din + o_sao);
     b.sao_groups = sao_groups;
     for (int g = 0; g < H2J_SAO_GROUPS; g++) {

@@ -116,6 +116,10 @@ typedef struct {
     int32_t sao_groups;         /* launches (0..H2J_SAO_GROUPS) */
     int32_t sao_first[H2J_SAO_GROUPS], sao_count[H2J_SAO_GROUPS], sao_ctbs[H2J_SAO_GROUPS];
     const uint32_t *sao_map;    /* frame indices of the HEVC pictures with SAO, most CTBs first */
+    /* H.264 K1 launch of kAvcK1Waves-wave workgroups (h2j_k1_recon_h264): tall pictures in bands of
+       as many rows as the workgroup has waves (one row round per band), band-major */
+    int32_t k1wgs8;
+    const uint32_t *k1map8;     /* workgroup -> (frame << 8) | band of 8 macroblock rows */
 } h2j_gpu_batch;
 
 /* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
