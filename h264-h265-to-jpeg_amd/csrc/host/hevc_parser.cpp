@@ -29,7 +29,7 @@ enum {
     C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_PART_MODE = 6,
     C_PREV_INTRA = 7, C_CHROMA_MODE = 8, C_SPLIT_TF = 9, C_CBF_LUMA = 12, C_CBF_CHROMA = 14,
     C_TSKIP = 18, C_LAST_X = 20, C_LAST_Y = 38, C_CSBF = 56, C_SIG = 60, C_GT1 = 104,
-    C_GT2 = 128, C_QP_DELTA = 134, NUM_CTX = 136
+    C_GT2 = 128, C_QP_DELTA = 134, C_CQO_FLAG = 136, C_CQO_IDX = 137, NUM_CTX = 138
 };
 
 // initValue for initType 0 (I slices), H.265 Tables 9-5 .. 9-37
@@ -45,7 +45,8 @@ const uint8_t kInitI[NUM_CTX] = {
     140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166,
     182, 140, 227, 122, 197,
     138, 153, 136, 167, 152, 152,
-    154, 154};
+    154, 154,
+    154, 154};  // cu_chroma_qp_offset_flag, cu_chroma_qp_offset_idx (Tables 9-34 / 9-35 of H.265 v3)
 
 struct Sps {
     bool valid = false;
@@ -81,6 +82,9 @@ struct Pps {
     int slice_header_ext = 0;
     // pps_range_extension (7.3.2.3.2), read only for the RExt profile (FFmpeg hevc_ps.c)
     int log2_max_ts = 2, cross_component = 0, cqo_list_enabled = 0, sao_scale_luma = 0, sao_scale_chroma = 0;
+    // chroma QP offset lists: entries past chroma_qp_offset_list_len_minus1 stay 0 (FFmpeg's
+    // zeroed PPS; its idx parse can reach index 5 whatever the list length)
+    int cqo_depth = 0, cqo_len_minus1 = 0, cb_qo[6] = {0, 0, 0, 0, 0, 0}, cr_qo[6] = {0, 0, 0, 0, 0, 0};
 };
 
 struct SliceHdr {
@@ -346,10 +350,8 @@ int parse_sps(BitReader& b, Sps* tab) {
     // chroma depths must match
     if ((s.bit_depth != 8 && s.bit_depth != 9 && s.bit_depth != 10 && s.bit_depth != 12) || s.bit_depth_c != s.bit_depth)
         return -12;
-    // RExt tools FFmpeg 4.3 parses but does not implement ("... not yet implemented"): the picture
-    // fails with its own message instead of decoding differently from the encoder's intent
-    if (s.ext_precision) return -13;
-    if (s.bypass_alignment) return -14;
+    // extended_precision_processing_flag and cabac_bypass_alignment_enabled_flag: FFmpeg 4.3
+    // (hevc_ps.c) logs "... not yet implemented" and decodes as if both were 0; so does this parser
     if (s.log2_ctb > 6 || s.log2_ctb < 4 || s.log2_max_tb > 5) return -3;
     // FFmpeg hevc_ps.c: "Invalid value for log2_min_tb_size", "Invalid coded frame dimensions",
     // "max transform block size out of range", "max_transform_hierarchy_depth_intra out of range",
@@ -450,10 +452,17 @@ int parse_pps(BitReader& b, Pps* tab, const Sps* stab) {
             p.cross_component = static_cast<int>(b.u(1));  // 4:4:4 only: no effect on 4:2:0
             p.cqo_list_enabled = static_cast<int>(b.u(1));
             if (p.cqo_list_enabled) {
-                b.ue();
+                // FFmpeg 4.3 hevc_ps.c: depth unchecked, "chroma_qp_offset_list_len_minus1 shall be in
+                // the range [0, 5]", list entries unchecked (only logged): they are clamped here to a
+                // range whose sum with any QP still saturates as FFmpeg's unclamped int sum does
+                p.cqo_depth = static_cast<int>(std::min<uint32_t>(b.ue(), 64u));
                 const uint32_t len = b.ue();
                 if (len > 5) return -1;
-                for (uint32_t i = 0; i <= len; i++) { b.se(); b.se(); }
+                p.cqo_len_minus1 = static_cast<int>(len);
+                for (uint32_t i = 0; i <= len; i++) {
+                    p.cb_qo[i] = std::max(-128, std::min(128, b.se()));
+                    p.cr_qo[i] = std::max(-128, std::min(128, b.se()));
+                }
             }
             const uint32_t sl = b.ue(), sc = b.ue();
             const uint32_t lim = sps.bit_depth > 10 ? static_cast<uint32_t>(sps.bit_depth - 10) : 0u;
@@ -622,6 +631,9 @@ private:
     bool have_ds_ = false;
     int qp_y_ = 0, qg_pred_ = 0, qpd_val_ = 0, last_cu_qp_ = 0;
     bool is_qpd_coded_ = false, first_qg_ = true;
+    // chroma QP offsets (H.265 v2 7.3.8.10 / 9.3.4.2): IsCuChromaQpOffsetCoded, CuQpOffsetCb / Cr
+    bool cqo_coded_ = false;
+    int cu_qo_cb_ = 0, cu_qo_cr_ = 0;
     int cu_bypass_ = 0;
     int cu_tu_begin_ = 0;
     int err_ = 0;
@@ -1360,6 +1372,21 @@ void HevcParser::transform_unit(int x0, int y0, int xb, int yb, int log2n, int b
         qp_y_ = qp_wrap(qg_pred_ + v + 52 + 2 * qpbd) - qpbd;
         set_qp(cux, cuy, 1 << log2cb, qp_y_);
     }
+    // FFmpeg 4.3 hls_transform_unit: once per chroma QP offset group, at the first TU with a chroma
+    // cbf in a CU without transquant bypass; ff_hevc_cu_chroma_qp_offset_idx reads the index as a
+    // truncated unary code with cMax FFMAX(5, len_minus1) = 5 (the spec's cMax is len_minus1: the two
+    // agree unless a stream codes idx == len_minus1 < 5), and only when len_minus1 > 0
+    if ((cbf_cb || cbf_cr) && cur_->cu_chroma_qp_offset_enabled && !cu_bypass_ && !cqo_coded_) {
+        int idx = -1;
+        if (dec(C_CQO_FLAG)) {
+            idx = 0;
+            if (p_->cqo_len_minus1 > 0)
+                while (idx < 5 && dec(C_CQO_IDX)) idx++;
+        }
+        cu_qo_cb_ = idx < 0 ? 0 : p_->cb_qo[idx];
+        cu_qo_cr_ = idx < 0 ? 0 : p_->cr_qo[idx];
+        cqo_coded_ = true;
+    }
     const int lmode = ipm_[(y0 >> 2) * mw + (x0 >> 2)];
     uint8_t fl = edge_flags(x0, y0);
     if (cu_bypass_) fl |= H2J_TU_BYPASS | H2J_TU_NOFILT;
@@ -1529,11 +1556,13 @@ void HevcParser::coding_unit(int x0, int y0, int log2cb) {
         }
         transform_tree(x0, y0, x0, y0, log2cb, 0, 0, s_->max_th_depth_intra + part_nxn, part_nxn, 0, 0, cm, x0, y0, log2cb);
     }
-    // patch the CU's QP into its transform blocks (QpY is final now)
+    // patch the CU's QP into its transform blocks (QpY is final now; so are CuQpOffsetCb / Cr for
+    // every chroma block with a residual: the offsets are coded before the CU's first chroma cbf)
     const int qpy = qp_y_ + qpbd;
     int qpc[2];
     for (int k = 0; k < 2; k++) {
-        int off = k == 0 ? p_->cb_qp_offset + cur_->cb_qp_offset : p_->cr_qp_offset + cur_->cr_qp_offset;
+        int off = k == 0 ? p_->cb_qp_offset + cur_->cb_qp_offset + cu_qo_cb_
+                         : p_->cr_qp_offset + cur_->cr_qp_offset + cu_qo_cr_;
         int qpi = qp_y_ + off;
         if (qpi < -qpbd) qpi = -qpbd;
         if (qpi > 57) qpi = 57;
@@ -1561,6 +1590,7 @@ void HevcParser::coding_quadtree(int x0, int y0, int log2cb, int depth) {
     }
     if ((p_->cu_qp_delta && log2cb >= log2ctb - p_->diff_cu_qp_delta_depth) || (!p_->cu_qp_delta && log2cb == log2ctb))
         qg_start(x0, y0);
+    if (cur_->cu_chroma_qp_offset_enabled && log2cb >= log2ctb - p_->cqo_depth) cqo_coded_ = false;
     if (split) {
         const int h = n >> 1;
         coding_quadtree(x0, y0, log2cb - 1, depth + 1);
@@ -1616,6 +1646,7 @@ int HevcParser::decode_slice_data(int shi, const uint8_t* p, const uint8_t* end)
     if (!sh.dependent) {
         first_qg_ = true;
         last_cu_qp_ = sh.slice_qp;
+        cu_qo_cb_ = cu_qo_cr_ = 0;
     }
     bool first = true;
     for (;;) {
@@ -1678,6 +1709,7 @@ int HevcParser::decode_wpp_row(int shi, int row, const uint8_t* p, const uint8_t
     cc_.init(p, end);
     first_qg_ = true;  // qPY_PREV = SliceQpY at a WPP row start (8.6.1)
     last_cu_qp_ = sh.slice_qp;
+    cu_qo_cb_ = cu_qo_cr_ = 0;  // a chroma QP offset group never spans CTBs: the value never carries
     for (int rx = 0; rx < ctbW; rx++) {
         const int rs = row * ctbW + rx;
         if (row > 0) {
@@ -1776,6 +1808,7 @@ int HevcParser::decode_tile(int shi, int ts0, int ts1, bool last, const uint8_t*
     init_contexts(sh.slice_qp);
     first_qg_ = true;
     last_cu_qp_ = sh.slice_qp;
+    cu_qo_cb_ = cu_qo_cr_ = 0;
     for (int ts = ts0; ts < ts1; ts++) {
         const int rs = ts2rs_[ts];
         parse_sao(rs % ctbW, rs / ctbW);
@@ -1848,8 +1881,6 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
             const int e = parse_sps(b, sps_);
             if (e < 0) {
                 job_->message = e == -12 ? "unsupported bit depth (FFmpeg 4.3 has no HEVC 4:2:0 format at it)"
-                              : e == -13 ? "unsupported HEVC range extension tool: extended_precision_processing_flag (FFmpeg 4.3: not implemented)"
-                              : e == -14 ? "unsupported HEVC range extension tool: cabac_bypass_alignment_enabled_flag (FFmpeg 4.3: not implemented)"
                                          : "unsupported or invalid SPS";
                 return -2;
             }
@@ -1868,10 +1899,6 @@ int HevcParser::run(const uint8_t* data, size_t size, int threads) {
             if (r < 0) {
                 job_->message = r == -2 ? "non-intra first picture (P/B slices) unsupported" : "invalid slice header";
                 return r == -2 ? -5 : -6;
-            }
-            if (sh.cu_chroma_qp_offset_enabled) {
-                job_->message = "unsupported HEVC range extension tool: chroma_qp_offset_list (cu_chroma_qp_offset_enabled_flag)";
-                return -6;
             }
             if (!have_pic) {
                 p_ = &pps_[sh.pps_id];

@@ -65,7 +65,9 @@ enum {
     C_GT1 = 104,         /* 24 */
     C_GT2 = 128,         /* 6 */
     C_QP_DELTA = 134,    /* 2 */
-    NUM_CTX = 136
+    C_CQO_FLAG = 136,    /* 1 */
+    C_CQO_IDX = 137,     /* 1 */
+    NUM_CTX = 138
 };
 
 static const uint8_t k_init_I[NUM_CTX] = {
@@ -90,6 +92,8 @@ static const uint8_t k_init_I[NUM_CTX] = {
     182, 140, 227, 122, 197,                               /* greater1 */
     138, 153, 136, 167, 152, 152,                          /* greater2 */
     154, 154,                                              /* cu_qp_delta_abs */
+    154,                                                   /* cu_chroma_qp_offset_flag */
+    154,                                                   /* cu_chroma_qp_offset_idx */
 };
 
 /* ------------------------------------------------------------ param sets */
@@ -412,7 +416,8 @@ static int parse_sps(OraBits *b, Sps *tab) {
     /* FFmpeg map_pixel_format: 4:2:0 at 8, 9, 10, 12 bits; luma and chroma depths equal */
     if (s->bit_depth != 8 && s->bit_depth != 9 && s->bit_depth != 10 && s->bit_depth != 12) return -3;
     if (s->bit_depth_c != s->bit_depth) return -3;
-    if (s->ext_precision || s->bypass_alignment) return -11; /* unsupported RExt tool */
+    /* extended_precision_processing_flag / cabac_bypass_alignment_enabled_flag: FFmpeg 4.3 hevc_ps.c
+     * logs "... not yet implemented" and decodes as if they were 0 (no other effect here either) */
     if (s->log2_ctb > 6 || s->log2_ctb < 4 || s->log2_max_tb > 5) return -3;
     /* FFmpeg hevc_ps.c: "Invalid coded frame dimensions" */
     if ((s->width & ((1 << s->log2_min_cb) - 1)) || (s->height & ((1 << s->log2_min_cb) - 1))) return -1;
@@ -544,6 +549,7 @@ typedef struct {
     int have_ds;
     int qp_y, qp_pred_prev, is_qpd_coded, qpd_val, first_qg, qg_pred, last_cu_qp;
     int cu_bypass;
+    int cqo_coded, cu_qo_cb, cu_qo_cr; /* IsCuChromaQpOffsetCoded, CuQpOffsetCb / Cr */
     int sl_enabled;
     const uint8_t (*slist)[6][64];
     const uint8_t (*slist_dc)[6];
@@ -1202,10 +1208,30 @@ static void transform_unit_recon(Dec *d, CuCtx *cu, int x0, int y0, int xb, int 
         d->qp_y = ((d->qg_pred + v + 52 + 2 * d->qpbd) % (52 + d->qpbd)) - d->qpbd;
         set_qp_cu(d, cu->x0, cu->y0, 1 << cu->log2cb, d->qp_y);
     }
+    /* FFmpeg 4.3 hls_transform_unit: cu_chroma_qp_offset_flag once per chroma QP offset group, at
+     * the first TU with a chroma cbf of a CU without transquant bypass; the index is read only when
+     * chroma_qp_offset_list_len_minus1 > 0, by ff_hevc_cu_chroma_qp_offset_idx as a truncated unary
+     * code with cMax FFMAX(5, len_minus1) = 5 (H.265 9.3.3.x: cMax = len_minus1; the two agree unless
+     * a stream codes idx == len_minus1 < 5); list entries past the list are 0 (zeroed PPS) */
+    if ((cbf_cb || cbf_cr) && d->cur->cu_chroma_qp_offset_enabled && !d->cu_bypass && !d->cqo_coded) {
+        if (dec_bin(d, C_CQO_FLAG)) {
+            int idx = 0;
+            if (d->p->cqo_len > 1)
+                while (idx < 5 && dec_bin(d, C_CQO_IDX)) idx++;
+            d->cu_qo_cb = d->p->cb_qo_list[idx];
+            d->cu_qo_cr = d->p->cr_qo_list[idx];
+        } else {
+            d->cu_qo_cb = d->cu_qo_cr = 0;
+        }
+        d->cqo_coded = 1;
+    }
     const int qpy = d->qp_y + d->qpbd;
     int qpc[2];
     for (int k = 0; k < 2; k++) {
-        int off = k == 0 ? d->p->cb_qp_offset + d->cur->cb_qp_offset : d->p->cr_qp_offset + d->cur->cr_qp_offset;
+        /* H.265 8.6.1: CuQpOffsetCb / Cr enter the dequantisation QP only (deblocking uses
+         * pps_cb_qp_offset alone, 8.7.2.5.5; FFmpeg chroma_tc likewise) */
+        int off = k == 0 ? d->p->cb_qp_offset + d->cur->cb_qp_offset + d->cu_qo_cb
+                         : d->p->cr_qp_offset + d->cur->cr_qp_offset + d->cu_qo_cr;
         int qpi = clip3(-d->qpbdc, 57, d->qp_y + off);
         qpc[k] = chroma_qp_table(qpi) + d->qpbdc;
     }
@@ -1382,6 +1408,7 @@ static void coding_quadtree(Dec *d, int x0, int y0, int log2cb, int depth) {
         d->qp_pred_prev = d->last_cu_qp;
         qg_start(d, x0, y0);
     }
+    if (d->cur->cu_chroma_qp_offset_enabled && log2cb >= d->log2ctb - d->p->cqo_depth) d->cqo_coded = 0;
     if (split) {
         int h = n >> 1;
         coding_quadtree(d, x0, y0, log2cb - 1, depth + 1);
@@ -2004,7 +2031,6 @@ int oracle_hevc_decode(const uint8_t *data, long size, int flags, OraclePicture 
             SliceHdr *sh = &d->sh[d->nsh];
             int r = parse_slice_header(d, &b, type, sh, prev);
             if (r < 0) { ret = r == -2 ? -5 : -6; goto done; }
-            if (sh->cu_chroma_qp_offset_enabled) { ret = -12; goto done; } /* unsupported RExt tool */
             if (!have_pic) {
                 d->p = &d->pps[sh->pps_id];
                 d->s = &d->sps[d->p->sps_id];

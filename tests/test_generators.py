@@ -91,9 +91,34 @@ HEVC_CASES = [
     ("rext_ts_rdpcm_wpp", 128, 96, 8, 24, ["--profile", "4", "--rext", "135", "--maxts", "3", "--wpp", "1", "--ctb", "16"]),
     ("rext_nosmooth_rice_10bit", 128, 96, 10, 16, ["--profile", "4", "--rext", "160", "--slices", "1"]),
     ("vui_ppsext_main", 96, 64, 8, 27, ["--vui", "1", "--ppsext", "1", "--maxts", "5"]),
+    # VERDICT r05 #1 (round 6): tools FFmpeg 4.3 decodes -- extended precision / bypass alignment read
+    # and ignored, CU chroma QP offsets (flag + index, list lengths 1 / 3 / 6, group depths 0-3)
+    ("extprec_8bit", 96, 64, 8, 20, ["--rext", "16", "--bypass", "1"]),
+    ("bypass_align_rext", 96, 64, 8, 24, ["--profile", "4", "--rext", "384"]),
+    ("cqo_len1", 128, 96, 8, 24, ["--profile", "4", "--cqo", "2", "--cqolist", "5,-7"]),
+    ("cqo_len3_depth0_10bit", 128, 96, 10, 20, ["--profile", "4", "--cqo", "2", "--cqolist", "-4,2,6,-3,1,1",
+                                                 "--cqodepth", "0", "--ctb", "32"]),
+    ("cqo_len6_depth3_bypass", 128, 96, 8, 26, ["--profile", "4", "--cqo", "2", "--cqolist",
+                                                 "-12,12,5,-5,0,0,3,7,-6,-2,10,-9", "--cqodepth", "3", "--bypass", "1"]),
 ]
 
 
 @pytest.mark.parametrize("name,W,H,bd,qp,opts", HEVC_CASES, ids=[c[0] for c in HEVC_CASES])
 def test_hevcgen_oracle_roundtrip(tmp_path, name, W, H, bd, qp, opts):
     _roundtrip(tmp_path, _build("hevcgen"), 265, W, H, bd, qp, 5, opts)
+
+
+def test_cqo_offsets_reach_the_chroma_dequantisation(tmp_path):
+    """The round trips above only pin the oracle if the CU chroma QP offsets change the picture:
+    the same seed with an all-zero list and with large offsets gives different chroma and the
+    same luma (the offsets enter the Cb / Cr QP only)."""
+    gen = _build("hevcgen")
+    recs = []
+    for lst in ("0,0,0,0,0,0,0,0,0,0,0,0", "12,-12,9,9,-12,12,6,-6,-9,3,12,12"):
+        d = tmp_path / lst[:2]
+        d.mkdir()
+        _roundtrip(d, gen, 265, 128, 96, 8, 24, 5, ["--profile", "4", "--cqo", "2", "--cqolist", lst, "--cqodepth", "2"])
+        recs.append(np.fromfile(d / "rec.yuv", dtype=np.uint8))
+    ys = 128 * 96
+    assert np.array_equal(recs[0][:ys], recs[1][:ys])
+    assert not np.array_equal(recs[0][ys:], recs[1][ys:])

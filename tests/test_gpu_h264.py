@@ -71,15 +71,32 @@ def test_h264_bench_streams_sample(engine):
         assert o == O.transcode(s), p
 
 
-def test_h264_tall_picture_banded(engine):
-    """configs[4] 3840x2160 H.264: 135 MB rows run on 9 K1 workgroups of 16 rows
-    (the last band 7 rows) handing boundary rows across workgroups."""
-    s = read(golden("mixed/avc2160_00.h264"))
+TALL264 = [golden("mixed/avc2160_00.h264")] + sorted(glob.glob(os.path.join(golden("h264tall"), "*.h264")))
+
+
+@pytest.mark.parametrize("path", TALL264, ids=[os.path.basename(p) for p in TALL264])
+def test_h264_tall_picture_banded(engine, path):
+    """Pictures taller than 68 MB rows (engine.cpp kK1BandRows) run h2j_k1_recon_h264 in 8-row
+    bands, one 8-wave workgroup each, dispatched band-major, and the deblocking in 16-row bands,
+    both handing boundary rows across workgroups through the xline buffer: 3840x2160 (135 MB rows:
+    17 K1 bands, the last 7 rows; 9 deblocking bands), a 10-bit 256x1152 (72 rows: 9 K1 bands of
+    8, h264_rows<uint16_t>; 5 deblocking bands) and an 8-bit CAVLC 192x1408 (88 rows: 11 / 6)."""
+    s = read(path)
     for stage, skip in ((1, True), (0, False)):
         gy, gu, gv, bd = engine.decode(s, stage=stage)
         oy, ou, ov, obd = O.decode(s, 264, skip_loop_filter=skip)
         assert bd == obd
         _cmp((gy, gu, gv), (oy, ou, ov), f"stage {stage}")
+
+
+def test_h264_tall_pictures_one_batch(engine):
+    """Banded pictures of three heights and two sample types in one batch (shared band-major K1
+    map, per-picture xline regions); every JPEG byte-exact."""
+    streams = [read(p) for p in TALL264] + [read(TALL264[1])]
+    outs = engine.transcode(streams)
+    for s, o, p in zip(streams, outs, TALL264 + TALL264[1:2]):
+        assert o is not None, p
+        assert o == O.transcode(s), p
 
 
 def test_mixed_workload_batch(engine):

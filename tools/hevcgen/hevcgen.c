@@ -29,10 +29,17 @@
  *            high_precision_offsets, 128 persistent_rice_adaptation, 256
  *            cabac_bypass_alignment), --maxts L (log2_max_transform_skip_block_size),
  *            --saoscale L,C (log2_sao_offset_scale luma, chroma), --cqo 1|2 (chroma QP offset
- *            list in the PPS; 2: also enabled in the slice header), --ppsext 1 (write the
+ *            list in the PPS; 2: also enabled in the slice header, so every chroma QP offset
+ *            group codes cu_chroma_qp_offset_flag / _idx with a random choice), --cqolist
+ *            cb0,cr0[,cb1,cr1...] (up to 6 pairs; default -2,3,4,-1), --cqodepth D
+ *            (diff_cu_chroma_qp_offset_depth, default 1), --ppsext 1 (write the
  *            pps_range_extension even when the profile is not RExt: decoders then ignore it)
- *   The encoder uses the tools as the decoder will see them; streams with extended precision,
- *   bypass alignment or slice-level chroma QP offsets are only for rejection tests.
+ *   The encoder uses the tools as the decoder will see them.  extended_precision_processing and
+ *   cabac_bypass_alignment are written but coded as FFmpeg 4.3 decodes them (as if 0: "not yet
+ *   implemented"); with extended precision the level escapes stay short enough that the spec's
+ *   limited EGk reads them the same way (checked: the encoder stops otherwise).  A chroma QP
+ *   offset index equal to chroma_qp_offset_list_len_minus1 < 5 is never coded: FFmpeg 4.3 reads the
+ *   index with cMax 5 whatever the list length, the spec with cMax len_minus1.
  */
 #include <math.h>
 #include <stdint.h>
@@ -197,7 +204,8 @@ static void ce_finish(Enc *e) {
 enum {
     C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_PART_MODE = 6, C_PREV_INTRA = 7,
     C_CHROMA_MODE = 8, C_SPLIT_TF = 9, C_CBF_LUMA = 12, C_CBF_CHROMA = 14, C_TSKIP = 18, C_LAST_X = 20,
-    C_LAST_Y = 38, C_CSBF = 56, C_SIG = 60, C_GT1 = 104, C_GT2 = 128, C_QP_DELTA = 134, NUM_CTX = 136
+    C_LAST_Y = 38, C_CSBF = 56, C_SIG = 60, C_GT1 = 104, C_GT2 = 128, C_QP_DELTA = 134, C_CQO_FLAG = 136,
+    C_CQO_IDX = 137, NUM_CTX = 138
 };
 static const uint8_t k_init_I[NUM_CTX] = {
     153, 200, 139, 141, 157, 154, 184, 184, 63, 153, 138, 138, 111, 141, 94, 138, 182, 154, 139, 139,
@@ -208,7 +216,7 @@ static const uint8_t k_init_I[NUM_CTX] = {
     179, 153, 125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153,
     136, 139, 111, 136, 139, 111, 141, 111,
     140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166,
-    182, 140, 227, 122, 197, 138, 153, 136, 167, 152, 152, 154, 154};
+    182, 140, 227, 122, 197, 138, 153, 136, 167, 152, 152, 154, 154, 154, 154};
 
 /* ------------------------------------------------------------ options + state */
 typedef struct {
@@ -226,11 +234,13 @@ typedef struct {
     long long rawconf[4]; /* --conf: raw conformance window offsets (-1: derived from the size) */
     int wdelta;           /* --wdelta: subtracted from the signalled picture width */
     int profile, vui, rext, maxts, sao_scale[2], cqo, ppsext;
+    int cqo_len, cqo_depth, cqo_cb[6], cqo_cr[6]; /* chroma QP offset list (--cqolist, --cqodepth) */
     int eff_maxts;        /* log2 max transform-skip size the decoder uses (2 without the PPS range ext) */
 } Opt;
 #define RX_ROT 1
 #define RX_CTX 2
 #define RX_RDPCM 4
+#define RX_EXTPREC 16
 #define RX_NOSMOOTH 32
 #define RX_RICE 128
 
@@ -250,6 +260,8 @@ typedef struct {
     int slice_idx, slice_qp;
     int qg_pred, qpd_val, is_qpd_coded, first_qg, last_cu_qp, qp_y, target_qp;
     int cu_bypass;
+    int cqo_on;                      /* cu_chroma_qp_offset_enabled_flag of the slice */
+    int cqo_coded, cqo_choice;       /* IsCuChromaQpOffsetCoded; the group's choice: -1 flag 0, else idx */
     int qpbd;
     int stat[4]; /* StatCoeff (persistent_rice_adaptation) */
 } G;
@@ -498,6 +510,10 @@ static void enc_alr(G *g, int v, int rice) {
     /* value = (((1<<pm3)+2) << rice) + suffix(pm3 + rice bits), prefix = pm3 + 3 */
     int pm3 = 0;
     while ((((1 << (pm3 + 1)) + 2) << rice) <= v) pm3++;
+    if ((g->o.rext & RX_EXTPREC) && pm3 >= 12) {
+        fprintf(stderr, "level escape too long for extended_precision_processing (limited EGk)\n");
+        exit(3);
+    }
     int base = ((1 << pm3) + 2) << rice;
     for (int i = 0; i < pm3 + 3; i++) ce_byp(&g->ce, 1);
     ce_byp(&g->ce, 0);
@@ -964,6 +980,8 @@ static int tree_compute(G *g, Cu *cu, int x0, int y0, int xb, int yb, int log2n,
     int qpc[2];
     for (int k = 0; k < 2; k++) {
         int off = k == 0 ? g->o.cbqp : g->o.crqp;
+        /* the group's chroma QP offset: coded before the group's first chroma residual */
+        if (g->cqo_on && g->cqo_choice >= 0) off += k == 0 ? g->o.cqo_cb[g->cqo_choice] : g->o.cqo_cr[g->cqo_choice];
         qpc[k] = chroma_qp_table(clip3(-g->qpbd, 57, g->target_qp + off)) + g->qpbd;
     }
     int cm = cu->cm;
@@ -1006,6 +1024,15 @@ static void tree_write(G *g, Cu *cu, int id, int x0, int y0, int xb, int yb, int
     }
     ce_bin(&g->ce, &g->ctx[C_CBF_LUMA + (depth == 0 ? 1 : 0)], t->cbf_l);
     if ((t->cbf_l || cbf_cb || cbf_cr) && g->o.qpdelta && !g->is_qpd_coded) write_qp_delta(g);
+    if ((cbf_cb || cbf_cr) && g->cqo_on && !g->cu_bypass && !g->cqo_coded) {
+        ce_bin(&g->ce, &g->ctx[C_CQO_FLAG], g->cqo_choice >= 0);
+        if (g->cqo_choice >= 0 && g->o.cqo_len > 1) {
+            /* truncated unary; idx < cMax for both FFmpeg (5) and the spec (len_minus1) unless idx == 5 */
+            for (int i = 0; i < g->cqo_choice; i++) ce_bin(&g->ce, &g->ctx[C_CQO_IDX], 1);
+            if (g->cqo_choice < 5) ce_bin(&g->ce, &g->ctx[C_CQO_IDX], 0);
+        }
+        g->cqo_coded = 1;
+    }
     int lmode = g->ipm[(y0 >> 2) * g->mw + (x0 >> 2)];
     if (t->cbf_l) enc_residual(g, t->coef_l, log2n, 0, lmode, t->tsl);
     if (log2n > 2) {
@@ -1186,6 +1213,12 @@ static void coding_quadtree(G *g, int x0, int y0, int log2cb, int depth, int log
         split = log2cb > 3;
     }
     if (log2cb >= log2qg) qg_start(g, x0, y0);
+    if (g->cqo_on && log2cb >= g->o.log2ctb - g->o.cqo_depth) {
+        /* a new chroma QP offset group: flag 0, or an index FFmpeg and the spec read alike */
+        int nidx = g->o.cqo_len - (g->o.cqo_len < 6 && g->o.cqo_len > 1 ? 1 : 0);
+        g->cqo_coded = 0;
+        g->cqo_choice = rndn(nidx + 1) - 1;
+    }
     if (split) {
         int h = n >> 1;
         coding_quadtree(g, x0, y0, log2cb - 1, depth + 1, log2qg);
@@ -1399,8 +1432,8 @@ static void write_pps(FILE *f, const Opt *o) {
         bw_put(&b, 0, 1); /* cross_component_prediction_enabled_flag */
         bw_put(&b, o->cqo != 0, 1);
         if (o->cqo) {
-            bw_ue(&b, 1); bw_ue(&b, 1); /* diff_cu_chroma_qp_offset_depth, list_len_minus1 */
-            bw_se(&b, -2); bw_se(&b, 3); bw_se(&b, 4); bw_se(&b, -1);
+            bw_ue(&b, (uint32_t)o->cqo_depth); bw_ue(&b, (uint32_t)(o->cqo_len - 1));
+            for (int i = 0; i < o->cqo_len; i++) { bw_se(&b, o->cqo_cb[i]); bw_se(&b, o->cqo_cr[i]); }
         }
         bw_ue(&b, (uint32_t)o->sao_scale[0]); bw_ue(&b, (uint32_t)o->sao_scale[1]);
     }
@@ -1528,6 +1561,21 @@ int main(int argc, char **argv) {
     o->rext = opt_int(argc, argv, "--rext", 0);
     o->maxts = opt_int(argc, argv, "--maxts", 2);
     o->cqo = opt_int(argc, argv, "--cqo", 0);
+    o->cqo_depth = opt_int(argc, argv, "--cqodepth", 1);
+    {
+        const char *l = opt_str(argc, argv, "--cqolist");
+        int v[12], n = 0;
+        if (!l) l = "-2,3,4,-1";
+        while (n < 12 && sscanf(l, "%d", &v[n]) == 1) {
+            n++;
+            l = strchr(l, ',');
+            if (!l) break;
+            l++;
+        }
+        if (n < 2 || (n & 1)) { fprintf(stderr, "--cqolist wants cb,cr pairs\n"); return 2; }
+        o->cqo_len = n / 2;
+        for (int i = 0; i < o->cqo_len; i++) { o->cqo_cb[i] = v[2 * i]; o->cqo_cr[i] = v[2 * i + 1]; }
+    }
     if (opt_str(argc, argv, "--saoscale")) sscanf(opt_str(argc, argv, "--saoscale"), "%d,%d", &o->sao_scale[0], &o->sao_scale[1]);
     o->ppsext = opt_int(argc, argv, "--ppsext", 0) || o->maxts != 2 || o->cqo || o->sao_scale[0] || o->sao_scale[1];
     /* decoders read the pps_range_extension only for the RExt profile (FFmpeg hevc_ps.c) */
@@ -1634,6 +1682,7 @@ int main(int argc, char **argv) {
         g->slice_qp = clip3(-g->qpbd, 51, o->qp + sqp_delta);
         bw_se(&b, g->slice_qp - 26);
         if (o->cqo && o->profile == 4) bw_put(&b, o->cqo == 2, 1); /* cu_chroma_qp_offset_enabled_flag */
+        g->cqo_on = o->cqo == 2 && o->profile == 4;
         /* pps_loop_filter_across_slices_enabled: signal slice flag */
         if (1) bw_put(&b, (uint32_t)(nslice % 2 == 0), 1);
         /* slice data: one substream per CTB row with WPP (7.3.8.1 end_of_subset_one_bit +
