@@ -4,7 +4,8 @@ The K1 launch shape depends on the batch: h2j_gpu_predict runs the per-picture k
 128 pictures and the picture pool above, with P = min(4, pictures / 256) pictures per
 workgroup (h2j_kernels.hip, h2j_k1_recon_hevc_pool), staged CTB-wide row stores and, at 1080p
 CTB64, 17 rows per picture near the 160 KB LDS cap.  These tests run the exact configurations
-of BASELINE.json configs[1]-[3]: 1024 hevc1080 pictures (P = 4), 1024 avc1080 pictures and 256
+of BASELINE.json configs[1]-[3]: 1024 hevc1080 pictures (P = 4; the 64-stream §8(d) set and the
+lighter round 1-5 set), 1024 avc1080 pictures and 256
 hevc2160 Main10 pictures (pool<u16>), through h2j_engine_submit / h2j_engine_wait like the
 bench, and compare every JPEG with the oracle's; planes are read from inside bench-sized
 batches with h2j_engine_decode_batch (P = 4, P = 3 with a partly filled last workgroup)."""
@@ -21,7 +22,8 @@ from conftest import golden, read
 pytestmark = pytest.mark.gpu
 
 SETS = {
-    "hevc1080": ("bench", "hevc1080_*.h265", 265, 1024),
+    "hevc1080": ("bench_aim", "hevc1080a_*.h265", 265, 1024),       # the bench's headline set (r06)
+    "hevc1080_light": ("bench", "hevc1080_*.h265", 265, 1024),
     "avc1080": ("bench264", "avc1080_*.h264", 264, 1024),
     "hevc2160": ("bench4k", "hevc2160_10b_*.h265", 265, 256),
 }
@@ -56,6 +58,7 @@ def test_bench_sized_batch_every_jpeg(engine, key):
     ("hevc1080", 1024, 6, 1),      # P = 4, pre-loop-filter planes
     ("hevc1080", 1022, 1021, 0),   # P = 3, last workgroup holds 2 pictures
     ("hevc1080", 768, 400, 0),     # P = 3
+    ("hevc1080_light", 1024, 1000, 0),
     ("hevc2160", 256, 255, 0),     # pool<u16>, 4K Main10
     ("avc1080", 1024, 1023, 0),
 ])

@@ -8,7 +8,8 @@
 #   tests[:EXPR]              -m gpu suite (EXPR: a pytest -k expression)     -> gpurun_out/TAG_tests.log
 #   smoke                     __graft_entry__.smoke()                         -> gpurun_out/TAG_smoke.log
 #   bench:WL[:STEPS[:ARGS]]   bench.py line (ARGS: extra flags, ',' for ' ')  -> gpurun_out/TAG_bench_WL.json
-#   kstats:WL                 rocprofv3 --kernel-trace --stats, one step      -> gpurun_out/TAG_kstats_WL/
+#   kstats:WL[:ARGS[:SUF]]    rocprofv3 --kernel-trace --stats, two steps (ARGS: extra bench flags, ',' for ' ';
+#                             SUF: suffix of the output names)                -> gpurun_out/TAG_kstats_WL[SUF]/
 #   pmc:KERNEL:WL[:sq|hbm]    PMC passes of one kernel (hbm: FETCH_SIZE / WRITE_SIZE passes)
 #   ab:WL:BDIR[:STEPS]        same-box ABAB bench lines: this build vs the libraries in BDIR
 #   parse[:ROUNDS]            host entropy speed, one thread (tools/parse_bench)
@@ -41,13 +42,13 @@ for STEP in "$@"; do
       > gpurun_out/${TAG}_bench_$WL.json 2> gpurun_out/${TAG}_bench_$WL.err || { tail -20 gpurun_out/${TAG}_bench_$WL.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('$WL', round(d['value']), 'aim', d.get('value_aim'), 'us/KB', d.get('parse_core_us_per_kb'), 'hbm_res', round(d.get('hbm_resident_fps', 0)), 'frac', d['roofline']['frac'], 'verified', d.get('outputs_verified'))" gpurun_out/${TAG}_bench_$WL.json ;;
   kstats)
-    WL=${A1:-hevc1080}; D=gpurun_out/${TAG}_kstats_$WL
+    WL=${A1:-hevc1080}; EXTRA=${A2//,/ }; D=gpurun_out/${TAG}_kstats_$WL$A3
     rm -rf $D
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o stats -- \
-      python3 bench.py --workload $WL --steps 2 --warmup 1 --no-cpu-baseline --no-aim --no-single-call > $D.log 2>&1 \
+      python3 bench.py --workload $WL --steps 2 --warmup 1 --no-cpu-baseline --no-aim --no-single-call $EXTRA > $D.log 2>&1 \
       || { tail -20 $D.log; exit 1; }
     f=$(find $D -name "*kernel_stats.csv" | head -1)
-    cp "$f" gpurun_out/${TAG}_kstats_${WL}.csv
+    cp "$f" gpurun_out/${TAG}_kstats_${WL}$A3.csv
     python3 -c "
 import csv,sys
 for r in csv.DictReader(open(sys.argv[1])):

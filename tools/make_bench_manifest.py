@@ -1,6 +1,6 @@
 """Expected-output manifest for bench.py's post-timing check.
 
-For every stream bench.py can put in a batch (tests/golden/{bench,bench_heavy,bench264,bench4k,
+For every stream bench.py can put in a batch (tests/golden/{bench,bench_aim,bench_heavy,bench264,bench4k,
 mixed}), records md5(stream bytes) -> md5(oracle JPEG) in tests/golden/bench_manifest.json.
 bench.py hashes the JPEGs of its last timed step after the timed region and reports
 "outputs_verified".  The oracle (test infrastructure) runs only here, when minting; bench.py
@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle_py as O  # noqa: E402
 
-SETS = ["bench/*.h265", "bench_heavy/*.h265", "bench264/*.h264", "bench264_heavy/*.h264", "bench4k/*.h265", "mixed/*.h26[45]"]
+SETS = ["bench/*.h265", "bench_aim/*.h265", "bench_heavy/*.h265", "bench264/*.h264", "bench264_heavy/*.h264", "bench4k/*.h265", "mixed/*.h26[45]"]
 
 
 def main():

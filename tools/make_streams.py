@@ -18,6 +18,7 @@ reconstruction bit-for-bit.
   python tools/make_streams.py f3        -> tests/golden/f3/ (decoder delay, non-IDR / CRA / BLA first pictures)
   python tools/make_streams.py malformed -> tests/golden/malformed/ (out-of-range SPS / slice header values)
   python tools/make_streams.py heavy     -> tests/golden/bench_heavy/hevc1080h_XX.h265 (16 streams, ~100-250 KB)
+  python tools/make_streams.py aim       -> tests/golden/bench_aim/hevc1080a_XX.h265 (64 streams, QP 22-37, 110-220 KB)
 """
 import glob
 import json
@@ -130,6 +131,42 @@ def heavy(n=16):
         nb = encode(content, 1920, 1080, 8, qp, 400 + i, path)
         total += nb
         print(f"{path}: qp {qp} sigma {sigma} -> {nb} B", flush=True)
+    print("total", total, "mean", total // n)
+
+
+def aim(n=64):
+    """configs[1] exactly as SURVEY.md §8(d) specifies it: QP cycling {22, 27, 32, 37},
+    seeded crops / flips of the fixture content plus Gaussian noise, 100-250 KB per 1080p picture.  The
+    noise level is searched per stream (starting from a per-QP guess) until the picture lands in
+    [110, 220] KB, so every QP contributes pictures of the aimed size.  64 distinct streams (seeds
+    700..763), tiled x16 into the bench's 1024-picture batch: the bench's headline workload."""
+    out_dir = os.path.join(ROOT, "tests/golden/bench_aim")
+    os.makedirs(out_dir, exist_ok=True)
+    planes = source_planes()
+    qps = [22, 27, 32, 37]
+    guess = {22: 2.0, 27: 4.0, 32: 7.5, 37: 11.0}
+    total = 0
+    rows = []
+    for i in range(n):
+        qp, seed = qps[i % 4], 700 + i
+        path = os.path.join(out_dir, f"hevc1080a_{i:02d}.h265")
+        lo, hi, sigma = 0.0, 24.0, guess[qp] + 0.5 * ((i // 4) % 3 - 1)
+        for _ in range(8):
+            content = make_content(planes, 1920, 1080, seed, sigma, 8)
+            nb = encode(content, 1920, 1080, 8, qp, seed, path)
+            if nb < 110_000:
+                lo = sigma
+            elif nb > 220_000:
+                hi = sigma
+            else:
+                break
+            sigma = (lo + hi) / 2 if hi < 24.0 else sigma * 1.25 + 0.5
+        else:
+            raise SystemExit(f"{path}: no noise level within 110-220 KB")
+        total += nb
+        rows.append({"file": os.path.basename(path), "qp": qp, "sigma": round(sigma, 3), "bytes": nb})
+        print(f"{path}: qp {qp} sigma {sigma:.3f} -> {nb} B", flush=True)
+    json.dump(rows, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
     print("total", total, "mean", total // n)
 
 
@@ -601,4 +638,4 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "bench"
     {"bench": bench, "parity": parity, "4k": fourk, "parity264": parity264, "bench264": bench264,
      "mixed": mixed, "f3": f3, "heavy": heavy, "malformed": malformed, "nosdh": nosdh, "entropy": entropy,
-     "wide264": wide264, "leftcrop": leftcrop, "heavy264": heavy264, "tall264": tall264}[what]()
+     "wide264": wide264, "leftcrop": leftcrop, "heavy264": heavy264, "tall264": tall264, "aim": aim}[what]()
