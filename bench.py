@@ -553,6 +553,14 @@ def main():
                                  f"{WORKLOADS[hkey]['streams'].rsplit('/', 1)[0]} ({len(heavy)} generator 1080p streams, "
                                  f"{sum(len(b) for b in hbatch) / n / 1024:.1f} KB/picture), same engine and timing")
             res[key + "_parse_core_us_per_kb"] = parse_core_us_per_kb(hper, host["threads"], hbatch)
+            # the dominant kernel on that set too (same definitions as `roofline`)
+            hch = max(1, round(hper.get("chunks", 1)))
+            hk1 = hper["recon_ms"] / hch
+            hach = alg_bytes_per_frame(WORKLOADS[hkey]) * n / hch / (hk1 / 1e3) / 1e9
+            res[key + "_roofline"] = {"kernel": k1_name, "avg_launch_ms": hk1, "frames_per_launch": n / hch,
+                                      "achieved": hach, "frac": hach / HBM_PEAK_GBPS,
+                                      "hbm_resident_fps": n / ((hper["prep_ms"] + hper["recon_ms"] + hper["deblock_ms"] +
+                                                                hper["sao_ms"] + hper["jpeg_ms"] + hper["entropy_ms"]) / 1e3)}
             sweep = {}
             for t in (2, 4, 8, 16):
                 if t > host["threads"]:

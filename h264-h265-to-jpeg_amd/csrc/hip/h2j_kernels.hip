@@ -2572,8 +2572,6 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
     };
     uint32_t na, nb;
     grange(row * u.ctb_w, na, nb);
-    uint4 nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
-    uint2 nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
     {
         uint32_t seen = 0;
         const bool below = row + 1 < u.ctb_h;
@@ -2583,13 +2581,11 @@ DEVI void hevc_row(const FU& u, const h2j_tu* T, const uint64_t* masks, const ui
             // this CTB's record range + first batch (prefetched); prefetch the next CTB's
             const uint32_t a = na, b = nb;
             uint32_t t = a, tb = a;
-            uint4 rec = nrec;
-            uint2 msk = nmsk;
-            if (cx + 1 < u.ctb_w) {
-                grange(row * u.ctb_w + cx + 1, na, nb);
-                nrec = reinterpret_cast<const uint4*>(T)[min(na + lane, max(nb, 1u) - 1)];
-                nmsk = reinterpret_cast<const uint2*>(masks)[min(na + lane, max(nb, 1u) - 1)];
-            }
+            // (r06: the first record batch is loaded here, not prefetched a CTB ahead: six VGPRs held
+            // across the whole CTB had the pool kernel spill 25 VGPRs, 8 without them)
+            uint4 rec = reinterpret_cast<const uint4*>(T)[min(a + lane, max(b, 1u) - 1)];
+            uint2 msk = reinterpret_cast<const uint2*>(masks)[min(a + lane, max(b, 1u) - 1)];
+            if (cx + 1 < u.ctb_w) grange(row * u.ctb_w + cx + 1, na, nb);
             for (int q = 0; q < nq; q++) {
                 if (!q_inside(cx, q)) continue;
                 const int qx = q & 1, qy = q >> 1;
@@ -4873,6 +4869,9 @@ int h2j_gpu_event_destroy(void* e) { return check(hipEventDestroy(static_cast<hi
 int h2j_gpu_event_record(void* e, void* s) {
     return check(hipEventRecord(static_cast<hipEvent_t>(e), static_cast<hipStream_t>(s)), "hipEventRecord");
 }
+int h2j_gpu_stream_wait_event(void* s, void* e) {
+    return check(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent");
+}
 float h2j_gpu_event_elapsed_ms(void* a, void* b) {
     float ms = -1.f;
     if (check(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)), "hipEventElapsedTime"))
@@ -4977,9 +4976,27 @@ static int predict_main(const h2j_gpu_batch* b, void* stream) {
     // one launch for every kind of picture (unless the widest picture's line buffers would not
     // fit one workgroup's LDS: then the per-kind launches below)
     if (!wide && kinds >= 2 && b->k1all && b->k1all_n > 0 && lds_any <= 160 * 1024) {
-        hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
-                           b->ctbs, b->arena, b->k1all);
-        return check(hipGetLastError(), "h2j_k1_recon_any");
+        AuxStream* ax2 = (b->has_h264 && b->k1wgs8 > 0 && b->k1hevc_n > 0) ? aux_stream(s) : nullptr;
+        if (!ax2) {
+            hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1all_n), dim3(64 * kAvcWaves), lds_any, s, b->frames, b->tus,
+                               b->ctbs, b->arena, b->k1all);
+            return check(hipGetLastError(), "h2j_k1_recon_any");
+        }
+        // the HEVC pictures' merged launch and the H.264 pictures' own launch (8-wave workgroups, two
+        // per CU, 8-row bands) side by side on two streams (r06: 18.45 -> 17.72 ms per 1024 configs[4]
+        // pictures against every kind in h2j_k1_recon_any, profiles/r06_ab_runs.txt)
+        (void)hipEventRecord(ax2->fork, s);
+        (void)hipStreamWaitEvent(ax2->s2, ax2->fork, 0);
+        hipLaunchKernelGGL(h2j_k1_recon_h264, dim3(b->k1wgs8), dim3(64 * kAvcK1Waves), lds264, ax2->s2, b->frames, b->tus,
+                           b->ctbs, b->arena, b->k1map8);
+        const int r2 = check(hipGetLastError(), "h2j_k1_recon_h264");
+        (void)hipEventRecord(ax2->join, ax2->s2);
+        const size_t lds_hev = std::max(pool1, wbytes);
+        hipLaunchKernelGGL(h2j_k1_recon_any, dim3(b->k1hevc_n), dim3(64 * kAvcWaves), lds_hev, s, b->frames, b->tus,
+                           b->ctbs, b->arena, b->k1hevc);
+        const int r1 = check(hipGetLastError(), "h2j_k1_recon_any");
+        (void)hipStreamWaitEvent(s, ax2->join, 0);
+        return r1 ? r1 : r2;
     }
     // per-kind launches: H.264 on a companion stream forked from (and joined back into) the
     // chunk's stream, so its workgroups fill the CUs the HEVC launches leave idle

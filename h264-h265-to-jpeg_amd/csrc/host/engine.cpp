@@ -182,8 +182,13 @@ int parse_any(const uint8_t* d, size_t n, FrameJob& job) {
 // One in-flight chunk: its stream, buffers and layout.
 struct Slot {
     void* stream = nullptr;
-    void* ev[12] = {nullptr};  // 9: after the stats D2H, 10 / 11: around the payload D2H
-    size_t pay_pre = 0;        // payload bytes already copied in-stream by launch() (h_seg's capacity)
+    // 9: after the stats D2H, 10 / 11: around the in-stream payload D2H, 12 / 13: around the wait for
+    // the other slot, 14 / 15: around a second (whole) payload copy
+    void* ev[16] = {nullptr};
+    size_t pay_pre = 0;        // payload bytes already copied in-stream by enqueue() (estimated, <= h_seg's capacity)
+    double px = 0;             // output pixels of the chunk (payload estimate)
+    int small_runs = 0;        // consecutive chunks whose payload used < 1/4 of h_seg (shrink after 8)
+    size_t small_max = 0;      // the largest payload of that run
     DevBuf d_in, d_arena, d_seg, d_scratch;
     HostBuf h_in, h_js, h_seg;
     std::vector<h2j_frame> frames;
@@ -288,6 +293,7 @@ struct Engine {
     Slot slot[2];
     double stats[ST_N] = {0};  // working stats of the batch being driven
     double slot_hbm_budget = 64e9;  // per slot; shared with the other engines on the device
+    double pay_per_px = 0;          // JPEG payload bytes per output pixel, running estimate (both slots)
     bool strict_reference = false;  // H2J_STRICT_REFERENCE=1: fail where the reference returns false
 
     ~Engine() {
@@ -339,12 +345,14 @@ struct Engine {
     // Lay out, pack and enqueue the GPU work of jobs[live] on slot s.
     // stages: 1 recon, 2 +deblock, 3 +sao, 4 +jpeg forward path; entropy: +K5.
     // pool_free: the thread pool may be used for packing (not busy parsing).
-    int enqueue(Slot& s, int stages, bool entropy, bool pool_free = true);  // s.jobs must be set
+    // `after`: the other slot, when its kernels are still in flight -- this slot's kernels start once
+    // they have finished (its copies and the host's assembly still overlap them)
+    int enqueue(Slot& s, int stages, bool entropy, bool pool_free = true, const Slot* after = nullptr);  // s.jobs must be set
     // Wait for slot s and copy its payloads down (entropy chunks).
     int sync(Slot& s);
 };
 
-int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
+int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free, const Slot* after) {
     const int nf = static_cast<int>(s.live.size());
     s.stages = stages;
     s.entropy = entropy;
@@ -522,6 +530,9 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
                          [](const std::pair<int, uint32_t>& a, const std::pair<int, uint32_t>& b) { return a.first < b.first; });
         for (const auto& x : e) k1all.push_back(x.second);
     }
+    std::vector<uint32_t> k1hevc;
+    for (uint32_t m : k1all)
+        if (m & 0x80000000u) k1hevc.push_back(m);
     // K3 SAO map: the HEVC pictures with SAO, most CTBs first, cut into CTB-count classes (a picture
     // joins the current class while it has more than half the class's CTBs; the last class takes
     // the rest), one launch each, so no class pays for the largest picture's grid width
@@ -550,7 +561,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     const size_t o_all = align_up(o_map + k1map.size() * 4 + 16, 256);
     const size_t o_sao = align_up(o_all + k1all.size() * 4 + 16, 256);
     const size_t o_map8 = align_up(o_sao + saomap.size() * 4 + 16, 256);
-    const size_t in_bytes = align_up(o_map8 + k1map8.size() * 4 + 16, 256);
+    const size_t o_hev = align_up(o_map8 + k1map8.size() * 4 + 16, 256);
+    const size_t in_bytes = align_up(o_hev + k1hevc.size() * 4 + 16, 256);
     if (!s.h_in.ensure(in_bytes)) return fail("pinned host allocation failed");
     if (!s.d_in.ensure(in_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
     if (!s.d_arena.ensure(arena_bytes)) return fail(std::string("device allocation failed: ") + h2j_gpu_last_error());
@@ -567,6 +579,7 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     if (!k1all.empty()) std::memcpy(s.h_in.p + o_all, k1all.data(), k1all.size() * 4);
     if (!saomap.empty()) std::memcpy(s.h_in.p + o_sao, saomap.data(), saomap.size() * 4);
     if (!k1map8.empty()) std::memcpy(s.h_in.p + o_map8, k1map8.data(), k1map8.size() * 4);
+    if (!k1hevc.empty()) std::memcpy(s.h_in.p + o_hev, k1hevc.data(), k1hevc.size() * 4);
     std::vector<size_t> bt(nf), bc(nf), bk(nf), bs(nf), bl(nf);
     {
         size_t a = 0, b = 0, c = 0, d = 0, e = 0;
@@ -621,6 +634,8 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     b.k1all_n = static_cast<int32_t>(k1all.size());
     b.k1map8 = reinterpret_cast<const uint32_t*>(din + o_map8);
     b.k1wgs8 = static_cast<int32_t>(k1map8.size());
+    b.k1hevc = reinterpret_cast<const uint32_t*>(din + o_hev);
+    b.k1hevc_n = static_cast<int32_t>(k1hevc.size());
     b.sao_map = reinterpret_cast<const uint32_t*>(din + o_sao);
     b.sao_groups = sao_groups;
     for (int g = 0; g < H2J_SAO_GROUPS; g++) {
@@ -646,7 +661,14 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     int r = 0;
     r |= h2j_gpu_event_record(s.ev[0], st);
     r |= h2j_gpu_memcpy_h2d(din, hin, in_bytes, st);
+    r |= h2j_gpu_event_record(s.ev[12], st);
     stats[ST_H2D_BYTES] += static_cast<double>(in_bytes);
+    // two GPU sub-chunks of one parsed range (4K batches, mixed batches past the slot's HBM budget)
+    // would otherwise run their kernels side by side: the GPU is not the bound (the host entropy
+    // threads are), and concurrent launches inflated every stage's event time and rocprof duration
+    // (r05: 4K K4b 1.14 ms and the arena fill 1.18 ms per 256 pictures, 0.004 / 0.037 ms alone)
+    if (after && after->pending) r |= h2j_gpu_stream_wait_event(st, after->ev[6]);
+    r |= h2j_gpu_event_record(s.ev[13], st);
     r |= h2j_gpu_memset(s.d_arena.p, 0, s.zero_bytes, st);
     r |= h2j_gpu_event_record(s.ev[1], st);
     if (r) return drain_fail(s, std::string("upload failed: ") + h2j_gpu_last_error());
@@ -675,9 +697,24 @@ int Engine::enqueue(Slot& s, int stages, bool entropy, bool pool_free) {
     // 121 MB against 4 ms for the bare copy (tools/d2h_probe: 30 GB/s pinned) -- the submitting
     // driver thread waited for CPU behind the 16 entropy threads (profiles/r05_4k_d2h.md).  A
     // total above the capacity (first chunks, growth) is copied again whole in sync().
+    if (s.small_runs >= 8) {  // the slot's last chunk has been assembled: h_seg is free to go
+        const double tg = now_ms();
+        const size_t keep = s.small_max + s.small_max / 4 + 16;
+        s.h_seg.release();
+        if (!s.h_seg.ensure(keep)) return fail("pinned host allocation failed");
+        stats[ST_HOST_GROW] += now_ms() - tg;
+        s.small_runs = 0;
+    }
     s.pay_pre = 0;
+    s.px = 0;
+    for (int k = 0; k < nf; k++) s.px += static_cast<double>(s.frames[k].out_w) * s.frames[k].out_h;
     if (entropy && s.h_seg.cap > 0) {
-        s.pay_pre = std::min(s.h_seg.cap, seg_cap);
+        // the copy is sized by the engine's payload-per-pixel estimate (1.3x, 4 KB
+        // granules), not by the buffer's high-water mark: a small chunk after a 4K one moves its own
+        // few MB, not the 4K chunk's 150 MB
+        size_t want = seg_cap;
+        if (pay_per_px > 0) want = (static_cast<size_t>(1.3 * pay_per_px * s.px) + 65536 + 4095) & ~static_cast<size_t>(4095);
+        s.pay_pre = std::min(std::min(s.h_seg.cap, seg_cap), want);
         h2j_gpu_event_record(s.ev[10], st);
         if (h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, s.pay_pre, st))
             return drain_fail(s, std::string("download failed: ") + h2j_gpu_last_error());
@@ -702,24 +739,35 @@ int Engine::sync(Slot& s) {
         uint64_t total = 0;
         std::memcpy(&total, s.h_js.p, 8);
         stats[ST_PAY_BYTES] += static_cast<double>(total);
+        if (s.px > 0) {  // payload per pixel: a running mean, never below the last chunk's
+            const double ratio = static_cast<double>(total) / s.px;
+            pay_per_px = pay_per_px > 0 ? std::max(ratio, 0.7 * pay_per_px + 0.3 * ratio) : ratio;
+        }
+        stats[ST_PAY_COPIED] += static_cast<double>(s.pay_pre);  // the in-stream copy, used or not
         if (total > s.pay_pre) {  // not (all) copied in-stream: grow with headroom, copy it whole
             const double tg = now_ms();
             if (!s.h_seg.ensure(total + total / 4 + 16)) return fail("pinned host allocation failed");
             stats[ST_HOST_GROW] += now_ms() - tg;
             stats[ST_PAY_COPIED] += static_cast<double>(total);
             pay_late = true;
-            h2j_gpu_event_record(s.ev[10], s.stream);
+            h2j_gpu_event_record(s.ev[14], s.stream);
             if (h2j_gpu_memcpy_d2h(s.h_seg.p, s.d_seg.p, total, s.stream))
                 return fail(std::string("download failed: ") + h2j_gpu_last_error());
-            h2j_gpu_event_record(s.ev[11], s.stream);
+            h2j_gpu_event_record(s.ev[15], s.stream);
+        }
+        // the pinned buffer shrinks after 8 chunks in a row that used less than a quarter of it
+        if (total * 4 < s.h_seg.cap) {
+            s.small_max = s.small_runs ? std::max(s.small_max, static_cast<size_t>(total)) : static_cast<size_t>(total);
+            s.small_runs++;
         } else {
-            stats[ST_PAY_COPIED] += static_cast<double>(s.pay_pre);
+            s.small_runs = 0;
         }
     }
     if (h2j_gpu_event_record(s.ev[7], s.stream) || h2j_gpu_stream_sync(s.stream))
         return fail(std::string("download failed: ") + h2j_gpu_last_error());
-    stats[ST_H2D] += h2j_gpu_event_elapsed_ms(s.ev[0], s.ev[1]);
-    stats[ST_PREP] += h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[8]);
+    // the H2D copy alone; the arena fill (after any wait for the other slot's kernels) counts with K0
+    stats[ST_H2D] += h2j_gpu_event_elapsed_ms(s.ev[0], s.ev[12]);
+    stats[ST_PREP] += h2j_gpu_event_elapsed_ms(s.ev[13], s.ev[8]);
     stats[ST_RECON] += h2j_gpu_event_elapsed_ms(s.ev[8], s.ev[2]);
     stats[ST_CHUNKS] += 1;
     stats[ST_DEBLOCK] += h2j_gpu_event_elapsed_ms(s.ev[2], s.ev[3]);
@@ -728,14 +776,17 @@ int Engine::sync(Slot& s) {
     stats[ST_ENTROPY] += h2j_gpu_event_elapsed_ms(s.ev[5], s.ev[6]);
     // copies only (the payload copy is enqueued once the host has read the sizes)
     const double d2h_stats = h2j_gpu_event_elapsed_ms(s.ev[6], s.ev[9]);
-    const double d2h_pay = s.entropy && (pay_late || s.pay_pre) ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[11]) : 0.0;
+    // both payload copies when the in-stream one fell short (the second one's events had
+    // overwritten the first's)
+    const double d2h_pay = (s.entropy && s.pay_pre ? h2j_gpu_event_elapsed_ms(s.ev[10], s.ev[11]) : 0.0) +
+                           (pay_late ? h2j_gpu_event_elapsed_ms(s.ev[14], s.ev[15]) : 0.0);
     stats[ST_D2H] += d2h_stats + d2h_pay;
     stats[ST_D2H_STATS] += d2h_stats;
     stats[ST_D2H_PAY] += d2h_pay;
     ChunkTime ct;
     ct.frames = static_cast<int>(s.live.size());
     ct.k1_ms = h2j_gpu_event_elapsed_ms(s.ev[8], s.ev[2]);
-    ct.kernels_ms = h2j_gpu_event_elapsed_ms(s.ev[1], s.ev[6]);
+    ct.kernels_ms = h2j_gpu_event_elapsed_ms(s.ev[13], s.ev[6]);
     chunk_log.push_back(ct);
     return 0;
 }
@@ -981,8 +1032,8 @@ int Engine::run_batch(Batch& b) {
                 status[k] = jobs[k].error;
                 if (jobs[k].error == 0) s.live.push_back(k);
             }
-            if (enqueue(s, 4, true, true)) { fail = 1; break; }
             Slot& prev = slot[(sc + 1) & 1];
+            if (enqueue(s, 4, true, true, &prev)) { fail = 1; break; }
             if (sc > 0 && prev.pending && assemble(prev)) { fail = 1; break; }
             sc++;
             i = j;

@@ -48,6 +48,8 @@ int h2j_gpu_memset(void *dst, int value, size_t bytes, void *stream);
 void *h2j_gpu_event_create(void);
 int h2j_gpu_event_destroy(void *ev);
 int h2j_gpu_event_record(void *ev, void *stream);
+/* `stream` runs nothing enqueued after this call until `ev` (recorded on another stream) has completed */
+int h2j_gpu_stream_wait_event(void *stream, void *ev);
 float h2j_gpu_event_elapsed_ms(void *start, void *stop);
 const char *h2j_gpu_last_error(void);
 
@@ -120,6 +122,10 @@ typedef struct {
        as many rows as the workgroup has waves (one row round per band), band-major */
     int32_t k1wgs8;
     const uint32_t *k1map8;     /* workgroup -> (frame << 8) | band of 8 macroblock rows */
+    /* the HEVC entries of k1all alone, same order: a mixed batch's HEVC K1 (h2j_k1_recon_any) beside
+       the H.264 K1 (h2j_k1_recon_h264 on k1map8) on a companion stream */
+    int32_t k1hevc_n;
+    const uint32_t *k1hevc;
 } h2j_gpu_batch;
 
 /* K0 + K1: K0 (all TUs in parallel) availability masks, CTB->TU ranges,
