@@ -61,7 +61,11 @@ PARITY = sorted(glob.glob(os.path.join(HEVC_DIR, "*.h265")))
 
 @pytest.mark.parametrize("path", PARITY, ids=[os.path.basename(p) for p in PARITY])
 def test_parity_vectors_prelf_and_final(engine, path):
-    """hevcgen vectors (PCM, bypass, slices, 10-bit, CTB16/32, offsets, SDH...)."""
+    """hevcgen vectors (PCM, bypass, slices, 10-bit, CTB16/32, offsets, SDH, scaling lists, WPP, tiles,
+    9 / 12 bits, RExt tools; r06: p33-p39 -- extended_precision_processing and cabac_bypass_alignment
+    decoded as FFmpeg 4.3 decodes them (as if 0), CU chroma QP offsets with lists of 1 / 2 / 3 / 6
+    entries at group depths 0-3, in the Cb / Cr dequantisation QP only).  Pre-loop-filter and final
+    planes equal the oracle's (parity unpinned against the reference for the RExt vectors)."""
     s = read(path)
     for stage, skip in ((1, True), (0, False)):
         gy, gu, gv, bd = engine.decode(s, stage=stage)
