@@ -1,7 +1,6 @@
-# round-6 batch: GPU suite, end-to-end A/B of the host library (clang -mtune=znver5 parsers) against build/gcchost,
-# H.264 parse flags on the box CPU
+# round-6: host parse variants on the box CPU (tools/parse_bench pb_A / pb_B / pb_C, see profiles/r06_parse_flags.txt)
 set -e
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_run.sh r06i tests ab:hevc1080:build/gcchost:4 ab:avc1080:build/gcchost:4
-SETS="bench264 bench264_heavy bench_aim" BINS="pb_A pb_B" ROUNDS=3 REPS=5 timeout -k 10 500 bash tools/gpu_parse_min.sh > gpurun_out/r06i_parse.log 2>&1
-cat gpurun_out/r06i_parse.log
+mkdir -p gpurun_out
+SETS="bench_aim bench264" BINS="pb_A pb_B pb_C" ROUNDS=3 REPS=5 timeout -k 10 600 bash tools/gpu_parse_min.sh > gpurun_out/r06j_parse.log 2>&1
+cat gpurun_out/r06j_parse.log
