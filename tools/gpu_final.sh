@@ -14,6 +14,8 @@ case $2 in
   tail -c 600 gpurun_out/${TAG}_bench_default.json ;;
 2)
   bash tools/gpu_run.sh $TAG bench:hevc1080:20 bench:avc1080:20 bench:hevc2160:10 bench:mixed:10 ;;
+ab)  # an environment A/B before the final lines: ab VAR "V1 V2" WL
+  bash tools/gpu_ab_env.sh $TAG $3 "$4" $5 3 ;;
 3)
   bash tools/gpu_run.sh $TAG prof:hevc1080 prof:avc1080 ;;
 4)
