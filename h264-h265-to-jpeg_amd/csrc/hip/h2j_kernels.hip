@@ -537,28 +537,55 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
     for (int i = lane * 8; i < G * NN; i += 512) *reinterpret_cast<uint4*>(blk + i) = make_uint4(0, 0, 0, 0);
     wave_sync();
     int mx = 0, my = 0;
-    uint64_t mm = gm;
-    for (int g = 0; g < G; g++) {
-        const int kg = __ffsll(static_cast<long long>(mm)) - 1;
-        mm &= mm - 1;
-        const h2j_tu tu = tu_from_lanes(rec, kg);
+    {
+        // the group's coefficients in one round: lane = (TB g of the group, sub-lane), 64 / Gmax
+        // sub-lanes per TB, each taking entries sub, sub + LPT, ... -- every load of the group is in
+        // flight at once (r06: a loop over the G TBs waited out one global-load latency per TB; the
+        // 150 KB configs[1] pictures carry ~16k 4x4 TBs with residual each)
+        constexpr int LPT = N;          // lanes per TB: the group holds 64 / N TBs of N x N
+        constexpr int GMAX = 64 / LPT;
+        constexpr int EPL = NN / LPT;   // entries per lane (a TB has at most NN)
+        constexpr int CH = EPL < 4 ? EPL : 4;  // loads in flight per lane and round (K0 runs at 72 VGPRs)
+        const int g = lane / LPT, sub = lane % LPT;
+        uint64_t mg = gm;
+        for (int i = 0; i < g && i < GMAX; i++) mg &= mg - 1;
+        const int kg = mg ? __ffsll(static_cast<long long>(mg)) - 1 : 0;
+        const bool live = g < G;
+        const uint32_t w1 = __shfl(rec.y, kg, 64), w2 = __shfl(rec.z, kg, 64), w3 = __shfl(rec.w, kg, 64);
+        uint32_t wq[4] = {0u, w1, w2, w3};
+        h2j_tu tu;
+        memcpy(&tu, wq, sizeof(tu));
         const int c = tu.c, bd = c ? f.bdc : f.bd, qp = tu.qp;
         const int bdShift = bd + LOG2N - 5;
         const long long ls = static_cast<long long>(kLevelScale[qp % 6] << (qp / 6));
         const uint8_t* slt = f.slist ? sl + f.sl + (LOG2N == 2 ? c * 16 : LOG2N == 3 ? 48 + c * 64 : LOG2N == 4 ? 240 + c * 256 : 1008)
                                      : nullptr;
-        for (int e = lane; e < tu.ncoef; e += 64) {
-            const uint32_t en = CO[tu.coef + e];
-            const int pos = static_cast<int>(en >> 16);
-            const int lvl = static_cast<int16_t>(en & 0xFFFF);
-            const int m = slt ? slt[pos] : 16;
-            long long v = static_cast<long long>(lvl) * m * ls;
-            v = (v + (1ll << (bdShift - 1))) >> bdShift;
-            const int jr = pos >> LOG2N, xc = pos & (N - 1);
-            blk[g * NN + 2 * (k0_pslot<N>(jr) * N + xc) + k0_phalf<N>(jr)] =
-                static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
-            mx = max(mx, pos & (N - 1));
-            my = max(my, pos >> LOG2N);
+        const int nco = live ? static_cast<int>(tu.ncoef) : 0;
+        int ncm = nco;  // the group's largest entry count: rounds past it load nothing
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ncm = max(ncm, __shfl_xor(ncm, o, 64));
+        const int rounds = (ufl(ncm) + LPT - 1) / LPT;
+        for (int r0 = 0; r0 < rounds; r0 += CH) {
+            uint32_t en[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const int e = sub + (r0 + j) * LPT;
+                en[j] = e < nco ? CO[tu.coef + e] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                if (sub + (r0 + j) * LPT >= nco) continue;
+                const int pos = static_cast<int>(en[j] >> 16);
+                const int lvl = static_cast<int16_t>(en[j] & 0xFFFF);
+                const int m = slt ? slt[pos] : 16;
+                long long v = static_cast<long long>(lvl) * m * ls;
+                v = (v + (1ll << (bdShift - 1))) >> bdShift;
+                const int jr = pos >> LOG2N, xc = pos & (N - 1);
+                blk[g * NN + 2 * (k0_pslot<N>(jr) * N + xc) + k0_phalf<N>(jr)] =
+                    static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+                mx = max(mx, pos & (N - 1));
+                my = max(my, pos >> LOG2N);
+            }
         }
     }
 #pragma unroll
