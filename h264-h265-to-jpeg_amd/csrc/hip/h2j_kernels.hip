@@ -525,10 +525,13 @@ DEVI void hevc_residual(const K0F& f, const h2j_tu& tu, const h2j_coef* CO, uint
 // input rows / columns (bounded by the group's largest coefficient position); the matrix row of a
 // step is uniform (scalar loads).  The intermediate goes through LDS (int16), the result straight
 // to the residual plane.  `gm`: record lanes of the group's G TBs (slot g = g-th set bit).
-// Transform-skip and bypass TBs are not batched (hevc_residual).
-template <int LOG2N>
+// TS: 4x4 transform-skip TBs (no rotation / RDPCM in the picture), 16 per pass: the dequantised
+// level shifted by tsShift + bdShift (8.6.4.2) is the residual.  Bypass TBs and the other
+// transform-skip TBs are not batched (hevc_residual).
+template <int LOG2N, bool TS = false>
 DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G, const h2j_coef* CO,
                               const uint8_t* sl, int16_t* res, K0LdsHevc& s) {
+    static_assert(!TS || LOG2N == 2, "batched transform skip: 4x4 TBs only");
     constexpr int N = 1 << LOG2N, NN = N * N;
     constexpr int P = N + 2, NP = N * P;  // tmp row stride (int16): odd dword stride across lanes
     const int lane = threadIdx.x;
@@ -580,13 +583,36 @@ DEVI void hevc_residual_group(const K0F& f, const uint4& rec, uint64_t gm, int G
                 const int m = slt ? slt[pos] : 16;
                 long long v = static_cast<long long>(lvl) * m * ls;
                 v = (v + (1ll << (bdShift - 1))) >> bdShift;
-                const int jr = pos >> LOG2N, xc = pos & (N - 1);
-                blk[g * NN + 2 * (k0_pslot<N>(jr) * N + xc) + k0_phalf<N>(jr)] =
-                    static_cast<int16_t>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
-                mx = max(mx, pos & (N - 1));
-                my = max(my, pos >> LOG2N);
+                const int d = static_cast<int>(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+                if constexpr (TS) {  // tsShift = 5 + log2n, bdShift = 20 - bitDepth: one right shift (>= 1 up to 12 bits)
+                    const int sh = 15 - bd - LOG2N;
+                    blk[g * NN + pos] = static_cast<int16_t>((d + (1 << (sh - 1))) >> sh);
+                } else {
+                    const int jr = pos >> LOG2N, xc = pos & (N - 1);
+                    blk[g * NN + 2 * (k0_pslot<N>(jr) * N + xc) + k0_phalf<N>(jr)] = static_cast<int16_t>(d);
+                    mx = max(mx, pos & (N - 1));
+                    my = max(my, pos >> LOG2N);
+                }
             }
         }
+    }
+    if constexpr (TS) {  // rows straight from LDS: lane = (TB, row)
+        wave_sync();
+        const int g = lane >> LOG2N, q = lane & (N - 1);
+        uint64_t ml = gm;
+        for (int i = 0; i < g && i < G - 1; i++) ml &= ml - 1;
+        const int k = __ffsll(static_cast<long long>(ml)) - 1;
+        // (shuffles with every lane active: a bpermute from a lane outside the exec mask reads garbage)
+        const uint32_t w0 = __shfl(rec.x, k, 64), w1 = __shfl(rec.y, k, 64), w2 = __shfl(rec.z, k, 64);
+        uint32_t wq[4] = {w0, w1, w2, 0};
+        h2j_tu mine;
+        memcpy(&mine, wq, sizeof(mine));
+        if (g < G) {
+            int16_t* R = hevc_res_at(res, f.width, f.height, f.log2ctb, mine.c, mine.x, mine.y) + (q << h2j_res_q(f.log2ctb, mine.c));
+            *reinterpret_cast<uint2*>(R) = *reinterpret_cast<const uint2*>(blk + g * NN + q * N);
+        }
+        wave_sync();
+        return;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1167,17 +1193,33 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
             // first chroma record of the CTB (HEVC records are luma first, then chroma)
             if (oc > 0 && (pcb != ocb || pc == 0)) rng[4 * ocb + 1] = t;
             const uint8_t flags = own.flags;
-            if (hevc && oc == 0) {  // deblocking maps (luma TBs)
+            if (hevc && oc == 0) {  // deblocking maps (luma TBs): a row of the TB's nb 4x4 units per store
+                // (r06: byte stores per unit, nb * nb <= 64 steps with a division each on every lane
+                // of a wave holding one 32x32 TB); rows stored whole when the map rows keep the
+                // TB's alignment (mw a multiple of 8, as at 1080p), else in 1-byte pieces
                 const int nb = on >> 2;
-                for (int q = 0; q < nb * nb; q++) {
-                    const int bx = q % nb, by = q / nb;
-                    const int idx = ((oy0 >> 2) + by) * f.mw + (ox0 >> 2) + bx;
-                    uint8_t fl = 0;
-                    if (bx == 0 && (flags & H2J_TU_EDGE_L)) fl |= 1;
-                    if (by == 0 && (flags & H2J_TU_EDGE_T)) fl |= 2;
-                    if (flags & H2J_TU_NOFILT) fl |= 4;
-                    fmap[idx] = fl;
-                    qmap[idx] = own.qpy;
+                const int pc = (f.mw & 7) == 0 ? nb : 1;  // bytes per store
+                const uint32_t base = (flags & H2J_TU_NOFILT) ? 0x04040404u : 0u;
+                const uint32_t qv = 0x01010101u * static_cast<uint8_t>(own.qpy);
+                for (int by = 0; by < nb; by++) {
+                    const uint32_t rowv = base | (by == 0 && (flags & H2J_TU_EDGE_T) ? 0x02020202u : 0u);
+                    for (int bx = 0; bx < nb; bx += pc) {
+                        const int idx = ((oy0 >> 2) + by) * f.mw + (ox0 >> 2) + bx;
+                        const uint32_t fv = rowv | (bx == 0 && (flags & H2J_TU_EDGE_L) ? 1u : 0u);
+                        if (pc == 8) {
+                            *reinterpret_cast<uint2*>(fmap + idx) = make_uint2(fv, rowv);
+                            *reinterpret_cast<uint2*>(qmap + idx) = make_uint2(qv, qv);
+                        } else if (pc == 4) {
+                            *reinterpret_cast<uint32_t*>(fmap + idx) = fv;
+                            *reinterpret_cast<uint32_t*>(qmap + idx) = qv;
+                        } else if (pc == 2) {
+                            *reinterpret_cast<uint16_t*>(fmap + idx) = static_cast<uint16_t>(fv);
+                            *reinterpret_cast<uint16_t*>(qmap + idx) = static_cast<uint16_t>(qv);
+                        } else {
+                            fmap[idx] = static_cast<uint8_t>(fv);
+                            qmap[idx] = static_cast<int8_t>(qv);
+                        }
+                    }
                 }
             }
             // reference availability mask; without several slices / tiles it is pure
@@ -1188,20 +1230,40 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                     const int u = oc ? 2 : 4, nu = (2 * on) / u;
                     const int l2 = f.log2ctb, m = (1 << l2) - 1;
                     const int zc = zorder4((oxl & m) >> 2, (oyl & m) >> 2);
-                    for (int q = 0; q <= 2 * nu; q++) {
-                        int xn, yn;
-                        if (q < nu) { xn = ox0 - 1; yn = oy0 + 2 * on - 1 - q * u; }
-                        else if (q == nu) { xn = ox0 - 1; yn = oy0 - 1; }
-                        else { xn = ox0 + (q - nu - 1) * u; yn = oy0 - 1; }
-                        const int xnl = xn << oshc, ynl = yn << oshc;
-                        bool a = false;
-                        if (f.topo) {
-                            a = avail(fr, C, S, oxl, oyl, xnl, ynl);
-                        } else if (xnl >= 0 && ynl >= 0 && xnl < f.width && ynl < f.height) {
-                            const int cn = (ynl >> l2) * f.ctb_w + (xnl >> l2);
-                            a = cn == ocb ? zorder4((xnl & m) >> 2, (ynl & m) >> 2) <= zc : cn < ocb;
+                    if (f.topo) {  // slices / tiles: every unit by the full rule
+                        for (int q = 0; q <= 2 * nu; q++) {
+                            int xn, yn;
+                            if (q < nu) { xn = ox0 - 1; yn = oy0 + 2 * on - 1 - q * u; }
+                            else if (q == nu) { xn = ox0 - 1; yn = oy0 - 1; }
+                            else { xn = ox0 + (q - nu - 1) * u; yn = oy0 - 1; }
+                            mask |= static_cast<uint64_t>(avail(fr, C, S, oxl, oyl, xn << oshc, yn << oshc)) << q;
                         }
-                        mask |= static_cast<uint64_t>(a) << q;
+                    } else {
+                        // geometry alone, in closed form (r06: the per-unit loop ran 2nu + 1 <= 33
+                        // steps on every lane of a wave holding one 32x32 luma / 16x16 chroma TB).
+                        // The left and upper halves and the corner neighbour an aligned TB from
+                        // blocks that precede it; the below-left / above-right halves each lie in
+                        // one aligned block of the TB's size, before the TB in z-order / CTB order
+                        // entirely or not at all: test its first unit, then cut at the picture edge.
+                        auto geo = [&](int xn, int yn) __attribute__((always_inline)) {
+                            const int xnl = xn << oshc, ynl = yn << oshc;
+                            if (xnl < 0 || ynl < 0 || xnl >= f.width || ynl >= f.height) return false;
+                            const int cn = (ynl >> l2) * f.ctb_w + (xnl >> l2);
+                            return cn == ocb ? zorder4((xnl & m) >> 2, (ynl & m) >> 2) <= zc : cn < ocb;
+                        };
+                        const int nh = nu >> 1, Wc = f.width >> oshc, Hc = f.height >> oshc;
+                        const uint64_t half = (1ull << nh) - 1;
+                        if (ox0 > 0) mask |= half << nh;
+                        if (ox0 > 0 && oy0 > 0) mask |= 1ull << nu;
+                        if (oy0 > 0) mask |= half << (nu + 1);
+                        if (geo(ox0 - 1, oy0 + on + u - 1)) {
+                            const int fit = min(nh, (Hc - oy0 - on) / u);
+                            mask |= ((1ull << fit) - 1) << (nh - fit);
+                        }
+                        if (geo(ox0 + on, oy0 - 1)) {
+                            const int fit = min(nh, (Wc - ox0 - on + u - 1) / u);
+                            mask |= ((1ull << fit) - 1) << (nu + nh + 1);
+                        }
                     }
                 } else if (ufl(fr.mbaff)) {  // MBAFF: 6.4.12.2 availability computed by the host parser
                     mask = static_cast<uint64_t>(static_cast<uint8_t>(own.qpy) & 15u);
@@ -1248,7 +1310,11 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
     // ... and the Intra16x16 luma TBs, four per pass
     const bool grp264i = !hevc && mine && (own.flags & H2J_TU_CBF) && !(own.flags & (H2J_TU_PCM | H2J_TU_BYPASS)) &&
                          own.c == 0 && own.log2n == 4;
-    uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && ((own.flags & H2J_TU_PCM) ||
+    // ... and HEVC 4x4 transform-skip TBs of pictures without rotation / implicit RDPCM, 16 per pass
+    const bool grpts = hevc && mine && (own.flags & H2J_TU_CBF) && (own.flags & H2J_TU_TSKIP) &&
+                       !(own.flags & (H2J_TU_PCM | H2J_TU_BYPASS)) && own.log2n == 2 &&
+                       !(f.rext & (H2J_REXT_TS_ROT | H2J_REXT_RDPCM));
+    uint64_t work = __ballot(mine && !grp264 && !grp264c && !grp264i && !grpts && ((own.flags & H2J_TU_PCM) ||
                                       ((own.flags & H2J_TU_CBF) && (!hevc || (own.flags & (H2J_TU_TSKIP | H2J_TU_BYPASS))))));
     uint32_t nco = (!hevc && work) ? fetch_co(tu_from_lanes(rec, __ffsll(static_cast<long long>(work)) - 1)) : 0u;
     while (work) {
@@ -1350,6 +1416,17 @@ __global__ void __launch_bounds__(64, 7) h2j_k0_prep(const h2j_frame* frames, co
                     default: hevc_residual_group<5>(f, rec, gm, cnt, CO, sl, res, s); break;
                 }
             }
+        }
+        uint64_t m = __ballot(grpts);
+        while (m) {
+            uint64_t gm = 0;
+            int cnt = 0;
+            while (m && cnt < 16) {
+                gm |= m & (0 - m);
+                m &= m - 1;
+                cnt++;
+            }
+            hevc_residual_group<2, true>(f, rec, gm, cnt, CO, sl, res, s);
         }
     }
 }
