@@ -23,6 +23,9 @@
 #include "job.h"
 
 namespace h2j {
+#ifdef H2J_CORO
+extern thread_local void (*g_h2j_yield)();  // tools/parse_bench/coro.h experiment
+#endif
 namespace {
 
 enum {
@@ -1145,6 +1148,9 @@ void HevcParser::residual(int log2n, int c, int pred_mode, h2j_tu& tu) {
     const uint8_t(*const sigtab)[2][16] = g_sigctx[c ? 1 : 0][lsb][scanIdx];
     CabacState* const gt1ctx = ctx + C_GT1 + (c ? 16 : 0);
     for (int i = lastSub; i >= 0; i--) {
+#ifdef H2J_CORO_SB
+        if (i < lastSub && g_h2j_yield) g_h2j_yield();
+#endif
         const int xs = sc[lsb][i][0], ys = sc[lsb][i][1];
         bool infer_dc = false;
         if (i < lastSub && i > 0) {
@@ -1347,6 +1353,9 @@ void HevcParser::emit_tu(int x, int y, int log2n, int c, int mode, uint8_t flags
     tu.ncoef = 0;
     tu.coef = 0;
     if (cbf) {
+#ifdef H2J_CORO
+        if (g_h2j_yield) g_h2j_yield();
+#endif
         if (rext_) residual<true>(log2n, c, mode, tu);
         else residual<false>(log2n, c, mode, tu);
     }

@@ -20,6 +20,50 @@
 #include "sampler.h"
 #endif
 
+#ifdef H2J_CORO
+#include "coro.h"
+namespace h2j {
+thread_local void (*g_h2j_yield)() = nullptr;
+}
+namespace {
+// -c: the stream list parsed by two coroutines on this thread (even / odd entries), switched
+// before every residual block; the other one alone once a coroutine has run out of pictures
+struct CoPair {
+    h2j_coro::Co co[2], main;
+    int cur = 0;
+    const std::vector<std::vector<uint8_t>>* streams;
+    int reps;
+    double best[2];
+};
+thread_local CoPair* g_pair = nullptr;
+void co_yield() {
+    CoPair& p = *g_pair;
+    const int o = p.cur ^ 1;
+    if (p.co[o].done) return;
+    const int me = p.cur;
+    p.cur = o;
+    h2j_ctx_swap(&p.co[me].sp, p.co[o].sp);
+}
+void co_body(void* arg) {
+    CoPair& p = *g_pair;
+    const int me = static_cast<int>(reinterpret_cast<intptr_t>(arg));
+    h2j::FrameJob job;
+    for (int r = 0; r < p.reps; r++)
+        for (size_t i = me; i < p.streams->size(); i += 2) {
+            const auto& s = (*p.streams)[i];
+            if (h2j::hevc_parse_picture(s.data(), s.size(), job)) std::abort();
+        }
+    p.co[me].done = true;
+    const int o = me ^ 1;
+    if (!p.co[o].done) {
+        p.cur = o;
+        h2j_ctx_swap(&p.co[me].sp, p.co[o].sp);
+    }
+    h2j_ctx_swap(&p.co[me].sp, p.main.sp);
+    std::abort();
+}
+}  // namespace
+#endif
 #ifdef H2J_CABAC_COUNT
 namespace h2j {
 thread_local unsigned long long g_bins_ctx = 0, g_bins_byp = 0;
@@ -35,6 +79,8 @@ int main(int argc, char** argv) {
         return 2;
     }
     int reps = 3, threads = 1, pthreads = 1;
+    bool coro = false;
+    (void)coro;
     bool want_digest = false, want_hist = false, want_min = false;
     std::vector<std::vector<uint8_t>> streams;
     for (int i = 1; i < argc; i++) {
@@ -45,6 +91,10 @@ int main(int argc, char** argv) {
         }
         if (a == "-d") {
             want_digest = true;
+            continue;
+        }
+        if (a == "-c") {  // coroutine-paired parse (-DH2J_CORO builds)
+            coro = true;
             continue;
         }
         if (a == "-m") {  // min-of-reps per stream (robust to a noisy host): sum of per-stream minima
@@ -72,6 +122,38 @@ int main(int argc, char** argv) {
         std::fclose(f);
         streams.push_back(d);
     }
+#ifdef H2J_CORO
+    if (coro) {  // paired (two coroutines) vs sequential, interleaved rounds, one thread
+        for (int round = 0; round < 3; round++) {
+            auto t0 = std::chrono::steady_clock::now();
+            {
+                h2j::FrameJob job;
+                for (int r = 0; r < reps; r++)
+                    for (const auto& s : streams)
+                        if (h2j::hevc_parse_picture(s.data(), s.size(), job)) return 1;
+            }
+            const double seq = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            CoPair p;
+            p.streams = &streams;
+            p.reps = reps;
+            g_pair = &p;
+            h2j::g_h2j_yield = co_yield;
+            h2j_coro::make(p.co[0], 8 << 20, co_body, reinterpret_cast<void*>(0));
+            h2j_coro::make(p.co[1], 8 << 20, co_body, reinterpret_cast<void*>(1));
+            t0 = std::chrono::steady_clock::now();
+            p.cur = 0;
+            h2j_ctx_swap(&p.main.sp, p.co[0].sp);
+            const double par = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            h2j::g_h2j_yield = nullptr;
+            std::free(p.co[0].stack);
+            std::free(p.co[1].stack);
+            const double nf = static_cast<double>(reps) * streams.size();
+            std::printf("round %d: sequential %.4f ms/frame, paired %.4f ms/frame (%+.1f %%)\n", round, seq / nf, par / nf,
+                        100.0 * (par - seq) / seq);
+        }
+        return 0;
+    }
+#endif
     if (want_min) {
         h2j::FrameJob job;
         double sum = 0;
