@@ -4314,57 +4314,86 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
     const int vy = cls == 0 ? 0 : -1;
     const int sh = c ? 1 : 0, l2b = f.log2ctb - 2;
     const int ts = g.ts;
-    // offsets as 6-bit signed fields (|SaoOffsetVal| <= 31 without range extensions; else the
-    // select form): etab by edgeIdx + 2 = 0..4 (categories 1, 2, none, 3, 4), btab by band 0..3
-    const auto f6 = [](int v) { return static_cast<uint32_t>(v) & 63u; };
+    // |SaoOffsetVal| <= 31 without range extensions: the packed forms below; else the select form
     const bool packed = max(max(abs(o0), abs(o1)), max(abs(o2), abs(o3))) <= 31;
-    const int etab = static_cast<int>(f6(o0) | (f6(o1) << 6) | (f6(o2) << 18) | (f6(o3) << 24));
-    const int btab = static_cast<int>(f6(o0) | (f6(o1) << 6) | (f6(o2) << 12) | (f6(o3) << 18));
     const int da = vy * ts + hx;  // element offset of neighbour a (b is at -da)
+    // packed forms (r06): two samples per instruction as int16 halves (v_pk_* ops); the offset of a
+    // sample picked by v_perm_b32 from a byte table of offset + 64 (high byte of each half 0x00),
+    // edge index (sa + sb) & 7 = 6, 7, 0, 1, 2 for edgeIdx 0..4, band index min(band delta, 4)
+    const auto b64 = [](int v) { return static_cast<uint32_t>(v + 64) & 0xFFu; };
+    const uint32_t eo_lo = 64u | (b64(o2) << 8) | (b64(o3) << 16), eo_hi = (b64(o0) << 16) | (b64(o1) << 24);
+    const uint32_t bo_lo = b64(o0) | (b64(o1) << 8) | (b64(o2) << 16) | (b64(o3) << 24), bo_hi = 64u;
+    const s16x2 k64 = {64, 64}, kmax = {static_cast<short>(maxv), static_cast<short>(maxv)}, kzero = {0, 0};
+    const auto h2 = [](uint32_t v) { return __builtin_bit_cast(s16x2, v); };
+    const auto u2 = [](s16x2 v) { return __builtin_bit_cast(uint32_t, v); };
+    const auto apply = [&](uint32_t v, uint32_t t) __attribute__((always_inline)) {  // clip(v + t - 64)
+        const s16x2 r = h2(v) + h2(t) - k64;
+        return u2(__builtin_elementwise_min(__builtin_elementwise_max(r, kzero), kmax));
+    };
+    // (the sign clamps and the sentinel shift as v_pk_max/min/ashr by asm: the compiler turns the
+    // C form into per-half compares and selects)
+    const auto sgn2 = [](uint32_t d) __attribute__((always_inline)) {  // clamp(d, -1, 1) per int16 half
+        uint32_t r;
+        asm("v_pk_max_i16 %0, %1, %2\n\tv_pk_min_i16 %0, %0, %3" : "=&v"(r) : "v"(d), "s"(0xFFFFFFFFu), "s"(0x00010001u));
+        return r;
+    };
+    const auto eo2 = [&](uint32_t v, uint32_t a, uint32_t b) __attribute__((always_inline)) {
+        const uint32_t sa = sgn2(u2(h2(v) - h2(a))), sb = sgn2(u2(h2(v) - h2(b)));
+        const uint32_t t = __builtin_amdgcn_perm(eo_hi, eo_lo, (u2(h2(sa) + h2(sb)) & 0x00070007u) | 0x0C000C00u);
+        uint32_t inv;  // 0xFFFF in a half whose a or b is -1 (unusable): that sample keeps v
+        asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(inv) : "s"(0x000F000Fu), "v"(a | b));
+        return (inv & v) | (~inv & apply(v, t));
+    };
+    const auto bo2 = [&](uint32_t v) __attribute__((always_inline)) {
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const u16x2 d = __builtin_bit_cast(u16x2, u2((h2(v) >> static_cast<short>(bd - 5)) - h2(0x00010001u * static_cast<uint32_t>(band))) & 0x001F001Fu);
+        const u16x2 four = {4, 4};
+        const uint32_t bi = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, four));
+        return apply(v, __builtin_amdgcn_perm(bo_hi, bo_lo, bi | 0x0C000C00u));
+    };
     for (int i = tid; i < (g.h << g.lq); i += 256) {
         const int y = i >> g.lq, x = (i & ((1 << g.lq) - 1)) * 4;
         if (x >= g.w) continue;
         const uint2 vv = *reinterpret_cast<const uint2*>(T + (y + 1) * ts + 4 + x);
-        const int v[4] = {static_cast<int>(vv.x & 0xFFFF), static_cast<int>(vv.x >> 16), static_cast<int>(vv.y & 0xFFFF),
-                          static_cast<int>(vv.y >> 16)};
         // samples of pcm (loop filter off) / transquant-bypass blocks stay untouched
         const bool keep = type == 0 || L.keep[(((y << sh) >> 2) << l2b) + ((x << sh) >> 2)] != 0;
-        int o[4];
-        if (type == 2 && packed) {  // edge offset, table form
+        uint32_t px, py;  // the four output samples as int16 pairs
+        if (type == 2 && packed) {  // edge offset, packed
             const int16_t* C0 = T + (y + 1) * ts + 4 + x;
+            uint2 av, bv;
+            __builtin_memcpy(&av, C0 + da, 8);
+            __builtin_memcpy(&bv, C0 - da, 8);
+            px = eo2(vv.x, av.x, bv.x);
+            py = eo2(vv.y, av.y, bv.y);
+            if (keep) { px = vv.x; py = vv.y; }
+        } else if (type == 1 && packed) {  // band offset, packed
+            px = bo2(vv.x);
+            py = bo2(vv.y);
+            if (keep) { px = vv.x; py = vv.y; }
+        } else {
+            const int v[4] = {static_cast<int>(vv.x & 0xFFFF), static_cast<int>(vv.x >> 16), static_cast<int>(vv.y & 0xFFFF),
+                              static_cast<int>(vv.y >> 16)};
+            int o[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const int a = C0[k + da], bb = C0[k - da];
-                const int sa = max(-1, min(1, v[k] - a)), sb = max(-1, min(1, v[k] - bb));
-                const int off = __builtin_amdgcn_sbfe(etab, 6 * (2 + sa + sb), 6);
-                o[k] = (keep || (a | bb) < 0) ? v[k] : clip3(0, maxv, v[k] + off);
-            }
-        } else if (type == 1 && packed) {  // band offset, table form
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int bi = ((v[k] >> (bd - 5)) - band) & 31;
-                const int off = bi < 4 ? __builtin_amdgcn_sbfe(btab, 6 * bi, 6) : 0;
+                int sel = -1;  // offset index 0..3, -1 none
+                if (type == 1) {
+                    const int b = ((v[k] >> (bd - 5)) - band) & 31;
+                    sel = b < 4 ? b : -1;
+                } else if (type == 2) {
+                    const int xa = x + k + hx, ya = y + vy, xb = x + k - hx, yb = y - vy;
+                    const int a = T[(ya + 1) * ts + 4 + xa], bb = T[(yb + 1) * ts + 4 + xb];
+                    if (a >= 0 && bb >= 0) {
+                        const int e = 2 + ((v[k] > a) - (v[k] < a)) + ((v[k] > bb) - (v[k] < bb));
+                        // edgeIdx 0, 1, 2, 3, 4 -> category 1, 2, 0, 3, 4 -> offset index 0, 1, -, 2, 3
+                        sel = e == 0 ? 0 : (e == 1 ? 1 : (e == 2 ? -1 : e - 1));
+                    }
+                }
+                const int off = sel == 0 ? o0 : (sel == 1 ? o1 : (sel == 2 ? o2 : (sel == 3 ? o3 : 0)));
                 o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
             }
-        } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            int sel = -1;  // offset index 0..3, -1 none
-            if (type == 1) {
-                const int b = ((v[k] >> (bd - 5)) - band) & 31;
-                sel = b < 4 ? b : -1;
-            } else if (type == 2) {
-                const int xa = x + k + hx, ya = y + vy, xb = x + k - hx, yb = y - vy;
-                const int a = T[(ya + 1) * ts + 4 + xa], bb = T[(yb + 1) * ts + 4 + xb];
-                if (a >= 0 && bb >= 0) {
-                    const int e = 2 + ((v[k] > a) - (v[k] < a)) + ((v[k] > bb) - (v[k] < bb));
-                    // edgeIdx 0, 1, 2, 3, 4 -> category 1, 2, 0, 3, 4 -> offset index 0, 1, -, 2, 3
-                    sel = e == 0 ? 0 : (e == 1 ? 1 : (e == 2 ? -1 : e - 1));
-                }
-            }
-            const int off = sel == 0 ? o0 : (sel == 1 ? o1 : (sel == 2 ? o2 : (sel == 3 ? o3 : 0)));
-            o[k] = keep ? v[k] : clip3(0, maxv, v[k] + off);
-        }
+            px = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 16);
+            py = static_cast<uint32_t>(o[2]) | (static_cast<uint32_t>(o[3]) << 16);
         }
         if (vacc) {  // luma of a sao_sums_variance picture: K4a's sums, per MB of the CTB
             // output rows below the picture repeat its last row (jpeg_sample), so that row counts
@@ -4373,25 +4402,28 @@ DEVI void sao_filter(const h2j_frame& f, uint8_t* arena, const SaoGeo& g, int c,
             const unsigned wgt = (oy < 0 || ox < 0 || ox >= f.out_w) ? 0u : (oy < last ? 1u : (oy == last ? 16u - (last & 15) : 0u));
             if (wgt) {
                 unsigned s4 = 0, n4 = 0;
+                if (bd == 8) {  // sums and squares of the int16 pairs by v_dot2
+                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                    const u16x2 ux = __builtin_bit_cast(u16x2, px), uy = __builtin_bit_cast(u16x2, py), one = {1, 1};
+                    s4 = __builtin_amdgcn_udot2(uy, one, __builtin_amdgcn_udot2(ux, one, 0u, false), false);
+                    n4 = __builtin_amdgcn_udot2(uy, uy, __builtin_amdgcn_udot2(ux, ux, 0u, false), false);
+                } else {
+                    const int o[4] = {static_cast<int>(px & 0xFFFF), static_cast<int>(px >> 16), static_cast<int>(py & 0xFFFF),
+                                      static_cast<int>(py >> 16)};
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const unsigned u = bd > 8 ? min(static_cast<unsigned>(o[k] + (1 << (bd - 9))) >> (bd - 8), 255u)
-                                              : static_cast<unsigned>(o[k]);
-                    s4 += u;
-                    n4 += u * u;
+                    for (int k = 0; k < 4; k++) {
+                        const unsigned u = min(static_cast<unsigned>(o[k] + (1 << (bd - 9))) >> (bd - 8), 255u);
+                        s4 += u;
+                        n4 += u * u;
+                    }
                 }
                 atomicAdd(&vacc[((y >> 4) << (f.log2ctb - 4)) + (x >> 4)],
                           (static_cast<unsigned long long>(s4 * wgt) << 32) | (n4 * wgt));
             }
         }
         Pel* d = at32(D, m24(g.y0 + y, st) + g.x0 + x);
-        if (sizeof(Pel) == 1) {
-            *reinterpret_cast<uint32_t*>(d) = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 8) |
-                                              (static_cast<uint32_t>(o[2]) << 16) | (static_cast<uint32_t>(o[3]) << 24);
-        } else {
-            *reinterpret_cast<uint2*>(d) = make_uint2(static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 16),
-                                                      static_cast<uint32_t>(o[2]) | (static_cast<uint32_t>(o[3]) << 16));
-        }
+        if (sizeof(Pel) == 1) *reinterpret_cast<uint32_t*>(d) = __builtin_amdgcn_perm(py, px, 0x06040200u);
+        else *reinterpret_cast<uint2*>(d) = make_uint2(px, py);
     }
 }
 

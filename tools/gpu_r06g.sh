@@ -1,4 +1,6 @@
-# round-6 batch: SQ counters of the H.264 deblocking and K1 on avc1080 (configs[2])
+# round-6 batch: GPU suite + same-box A/B against build/base (HEAD before: SAO packed int16 forms)
 set -e
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_run.sh r06q "pmc:h2j_k2_deblock264p:avc1080:sq" "pmc:h2j_k1_recon_h264:avc1080:sq"
+mkdir -p gpurun_out
+bash tools/gpu_run.sh r06r tests ab:hevc1080:build/base:3
+for f in gpurun_out/r06r_ab_*.json; do python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['stages_ms_per_step']; print(sys.argv[1], 'sao', round(k['sao_ms'],3), 'prep', round(k['prep_ms'],3), 'k1', round(d['roofline']['avg_launch_ms'],3), 'verified', d['outputs_verified'])" $f; done
