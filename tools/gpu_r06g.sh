@@ -2,3 +2,4 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 bash tools/gpu_final.sh r06fin3 1
+bash tools/gpu_r06h.sh
