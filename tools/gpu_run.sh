@@ -81,8 +81,8 @@ PY
       for v in A B; do
         if [ $v = A ]; then D=$PKG; else D=$BD; fi
         H2J_LIB_DIR=$D timeout -k 10 300 python bench.py --workload $WL --steps $ST --no-cpu-baseline --no-single-call --no-aim \
-          > gpurun_out/${TAG}_ab_$v$rep.json 2> gpurun_out/${TAG}_ab_$v$rep.err || { tail -5 gpurun_out/${TAG}_ab_$v$rep.err; exit 1; }
-        python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_ab_$v$rep.json')); print('$v$rep', round(d['value'],1), 'hbm_res', round(d['hbm_resident_fps']), 'k1', d['roofline'].get('avg_launch_ms'), 'busy', d['host_cpu_busy_cores'])"
+          > gpurun_out/${TAG}_ab_${WL}_$v$rep.json 2> gpurun_out/${TAG}_ab_${WL}_$v$rep.err || { tail -5 gpurun_out/${TAG}_ab_${WL}_$v$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_ab_${WL}_$v$rep.json')); print('$WL $v$rep', round(d['value'],1), 'hbm_res', round(d['hbm_resident_fps']), 'k1', d['roofline'].get('avg_launch_ms'), 'busy', d['host_cpu_busy_cores'])"
       done
     done ;;
   parse)
