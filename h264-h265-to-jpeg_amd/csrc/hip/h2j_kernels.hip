@@ -4734,6 +4734,70 @@ DEVI void fdct_ap922(int16_t* b) {
     }
 }
 
+// The same AP-922 FDCT on column pairs (r06): P[r][m] holds samples (row r, columns 2m and 2m + 1) as
+// int16 halves, so the column pass runs two columns per v_pk_* instruction and its output is already
+// the row pass's pairs; the row pass's 32 multiply-adds are 16 v_dot2 (int32 accumulation, as the
+// scalar form).  The saturations of the scalar form never act for samples in [0, 255] (every sample
+// K4 reads is): the largest intermediate is 32640 (checked against fdct_ap922 on 4 M random and
+// extreme 0 / 255 blocks, tools/diag/fdct_pk_check.cpp), so plain wrapping int16 arithmetic is exact.
+DEVI s16x2 fd_h2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+DEVI uint32_t fd_u(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+DEVI s16x2 fd_mh(s16x2 a, int c) {  // (a * c) >> 16 per half: two products, their high halves by one v_perm
+    const int lo = static_cast<int>(a.x) * c, hi = static_cast<int>(a.y) * c;
+    return fd_h2(__builtin_amdgcn_perm(static_cast<uint32_t>(hi), static_cast<uint32_t>(lo), 0x07060302u));
+}
+DEVI void fdct_ap922_pk(const uint32_t (&P)[8][4], int16_t (&b)[64]) {
+    const s16x2 one = {1, 1};
+    s16x2 T[8][4];  // column pass output, same pair layout: T[row][m]
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const s16x2 x0 = fd_h2(P[0][m]), x1 = fd_h2(P[1][m]), x2 = fd_h2(P[2][m]), x3 = fd_h2(P[3][m]);
+        const s16x2 x4 = fd_h2(P[4][m]), x5 = fd_h2(P[5][m]), x6 = fd_h2(P[6][m]), x7 = fd_h2(P[7][m]);
+        const s16x2 t0 = (x0 + x7) << 3, t1 = (x1 + x6) << 3, t2 = (x2 + x5) << 3, t3 = (x3 + x4) << 3;
+        const s16x2 tp03 = t0 + t3, tm03 = t0 - t3, tp12 = t1 + t2, tm12 = t1 - t2;
+        T[0][m] = tp03 + tp12;
+        T[4][m] = tp03 - tp12;
+        T[2][m] = (tm03 + fd_mh(tm12, 27146)) | one;
+        T[6][m] = (fd_mh(tm03, 27146) - tm12) | one;
+        const s16x2 d16 = (x1 - x6) << 4, d25 = (x2 - x5) << 4;
+        const s16x2 tp65 = fd_mh(d16 + d25, 23170) | one, tm65 = fd_mh(d16 - d25, 23170);
+        const s16x2 t4 = (x3 - x4) << 3, t7 = (x0 - x7) << 3;
+        const s16x2 tp465 = t4 + tm65, tm465 = t4 - tm65, tp765 = t7 + tp65, tm765 = t7 - tp65;
+        T[1][m] = (tp765 + fd_mh(tp465, 13036)) | one;
+        T[7][m] = fd_mh(tp765, 13036) - tp465;
+        T[3][m] = tm765 - (fd_mh(tm465, -21746) + tm465);
+        T[5][m] = (fd_mh(tm765, -21746) + tm765) + tm465;
+    }
+    constexpr short kRow[4][7] = {{22725, 21407, 19266, 16384, 12873, 8867, 4520},
+                                  {31521, 29692, 26722, 22725, 17855, 12299, 6270},
+                                  {29692, 27969, 25172, 21407, 16819, 11585, 5906},
+                                  {26722, 25172, 22654, 19266, 15137, 10426, 5315}};
+    constexpr int kSel[8] = {0, 1, 2, 3, 0, 3, 2, 1};
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const short* cc = kRow[kSel[r]];
+        const short C1 = cc[0], C2 = cc[1], C3 = cc[2], C4 = cc[3], C5 = cc[4], C6 = cc[5], C7 = cc[6];
+        const uint32_t u67 = fd_u(T[r][3]), u45 = fd_u(T[r][2]);
+        const s16x2 x76 = fd_h2((u67 >> 16) | (u67 << 16)), x54 = fd_h2((u45 >> 16) | (u45 << 16));
+        const s16x2 s01 = T[r][0] + x76, s23 = T[r][1] + x54, d01 = T[r][0] - x76, d23 = T[r][1] - x54;
+        auto dt = [](s16x2 a, short p, short q, s16x2 c, short u, short v) __attribute__((always_inline)) {
+            // (the output rounding's + 65536 as the accumulator's start)
+            return __builtin_amdgcn_sdot2(c, s16x2{u, v}, __builtin_amdgcn_sdot2(a, s16x2{p, q}, 65536, false), false);
+        };
+        int Y[8];
+        Y[0] = dt(s01, C4, C4, s23, C4, C4);
+        Y[4] = dt(s01, C4, static_cast<short>(-C4), s23, static_cast<short>(-C4), C4);
+        Y[2] = dt(s01, C2, C6, s23, static_cast<short>(-C6), static_cast<short>(-C2));
+        Y[6] = dt(s01, C6, static_cast<short>(-C2), s23, C2, static_cast<short>(-C6));
+        Y[1] = dt(d01, C1, C3, d23, C5, C7);
+        Y[3] = dt(d01, C3, static_cast<short>(-C7), d23, static_cast<short>(-C1), static_cast<short>(-C5));
+        Y[5] = dt(d01, C5, static_cast<short>(-C1), d23, C7, C3);
+        Y[7] = dt(d01, C7, static_cast<short>(-C5), d23, C3, static_cast<short>(-C1));
+#pragma unroll
+        for (int k = 0; k < 8; k++) b[r * 8 + k] = static_cast<int16_t>(Y[k] >> 17);
+    }
+}
+
 template <typename Pel>
 DEVI void jpeg_block(const h2j_frame& f, uint8_t* arena, int bi) {
     const int mbw = (f.out_w + 15) >> 4;
@@ -4792,21 +4856,20 @@ DEVI void jpeg_block_coefs(const h2j_frame& f, const uint8_t* arena, int bi, int
     int c, x0, y0;
     if (b < 4) { c = 0; x0 = mx * 16 + (b & 1) * 8; y0 = my * 16 + (b >> 1) * 8; }
     else { c = b - 3; x0 = mx * 8; y0 = my * 8; }
-    int16_t blk[64];
+    uint32_t P[8][4];  // row j, columns (2m, 2m + 1) as int16 halves (fdct_ap922_pk)
     const int shc = c ? 1 : 0;
     const int pw = f.out_w >> shc, ph = f.out_h >> shc;
     const int cx = f.crop_x >> shc, cy = f.crop_y >> shc;
     if (sizeof(Pel) == 1 && x0 + 8 <= pw && y0 + 8 <= ph && ((cx + x0) & 7) == 0 && (f.pic_stride[c] & 7) == 0) {
-        // the block lies inside the picture: eight 8-byte row loads
+        // the block lies inside the picture: eight 8-byte row loads, bytes to int16 pairs by v_perm
         const uint8_t* p = arena + f.pic2 + f.pic_off[c] + static_cast<size_t>(cy + y0) * f.pic_stride[c] + cx + x0;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint2 v = *reinterpret_cast<const uint2*>(p + static_cast<size_t>(j) * f.pic_stride[c]);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                blk[j * 8 + i] = static_cast<int16_t>((v.x >> (8 * i)) & 0xFF);
-                blk[j * 8 + 4 + i] = static_cast<int16_t>((v.y >> (8 * i)) & 0xFF);
-            }
+            P[j][0] = __builtin_amdgcn_perm(0u, v.x, 0x0C010C00u);
+            P[j][1] = __builtin_amdgcn_perm(0u, v.x, 0x0C030C02u);
+            P[j][2] = __builtin_amdgcn_perm(0u, v.y, 0x0C010C00u);
+            P[j][3] = __builtin_amdgcn_perm(0u, v.y, 0x0C030C02u);
         }
     } else if (sizeof(Pel) == 2 && x0 + 8 <= pw && y0 + 8 <= ph && ((cx + x0) & 7) == 0 && (f.pic_stride[c] & 7) == 0) {
         // 16-bit samples inside the picture: eight 16-byte row loads, converted as jpeg_sample does
@@ -4818,22 +4881,25 @@ DEVI void jpeg_block_coefs(const h2j_frame& f, const uint8_t* arena, int bi, int
             const uint4 v = *reinterpret_cast<const uint4*>(p + static_cast<size_t>(j) * f.pic_stride[c]);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                int u = static_cast<int>((w[i >> 1] >> (16 * (i & 1))) & 0xFFFF);
+            for (int m = 0; m < 4; m++) {
+                uint32_t u0 = w[m] & 0xFFFFu, u1 = w[m] >> 16;
                 if (bd > 8) {
-                    u = (u + (1 << (bd - 9))) >> (bd - 8);
-                    u = u > 255 ? 255 : u;
+                    u0 = min((u0 + (1u << (bd - 9))) >> (bd - 8), 255u);
+                    u1 = min((u1 + (1u << (bd - 9))) >> (bd - 8), 255u);
                 }
-                blk[j * 8 + i] = static_cast<int16_t>(u);
+                P[j][m] = u0 | (u1 << 16);
             }
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 8; j++)
 #pragma unroll
-            for (int i = 0; i < 8; i++) blk[j * 8 + i] = static_cast<int16_t>(jpeg_sample<Pel>(f, arena, c, x0 + i, y0 + j));
+            for (int m = 0; m < 4; m++)
+                P[j][m] = static_cast<uint32_t>(jpeg_sample<Pel>(f, arena, c, x0 + 2 * m, y0 + j)) |
+                          (static_cast<uint32_t>(jpeg_sample<Pel>(f, arena, c, x0 + 2 * m + 1, y0 + j)) << 16);
     }
-    fdct_ap922(blk);
+    int16_t blk[64];
+    fdct_ap922_pk(P, blk);
     const h2j_jstat* js = reinterpret_cast<const h2j_jstat*>(arena + f.jstat);
     out[0] = static_cast<int16_t>(((blk[0] >> 2) + 8) / 16);
 #pragma unroll

@@ -1,8 +1,6 @@
-# host-only (box CPU): HEVC parser code-generation variants, one thread, min-of-5, 3 interleaved rounds:
-# pb_A product flags (clang -march=x86-64-v3 -mtune=znver5), pb_B + -falign-loops=32,
-# pb_C + -falign-loops=64, pb_D -march=znver4 (the box's ISA; not portable, for reference)
+# round-6 batch: GPU suite + same-box A/B against build/base (HEAD before: K4c FDCT on column pairs, v_pk / v_dot2)
 set -e
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-SETS="bench_aim" BINS="pb_A pb_B pb_C pb_D" ROUNDS=3 REPS=5 timeout -k 10 600 bash tools/gpu_parse_min.sh > gpurun_out/r06w_parse.log 2>&1
-cat gpurun_out/r06w_parse.log
+bash tools/gpu_run.sh r06x tests ab:hevc1080:build/base:3 ab:avc1080:build/base:3
+for f in gpurun_out/r06x_ab_*.json; do python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['stages_ms_per_step']; print(sys.argv[1], d['config']['workload'], 'jpeg', round(k['jpeg_ms'],3), 'k1', round(d['roofline']['avg_launch_ms'],3), 'hbm_res', round(d['hbm_resident_fps']), 'verified', d['outputs_verified'])" $f; done
