@@ -82,7 +82,7 @@ PY
         if [ $v = A ]; then D=$PKG; else D=$BD; fi
         H2J_LIB_DIR=$D timeout -k 10 300 python bench.py --workload $WL --steps $ST --no-cpu-baseline --no-single-call --no-aim \
           > gpurun_out/${TAG}_ab_${WL}_$v$rep.json 2> gpurun_out/${TAG}_ab_${WL}_$v$rep.err || { tail -5 gpurun_out/${TAG}_ab_${WL}_$v$rep.err; exit 1; }
-        python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_ab_${WL}_$v$rep.json')); print('$WL $v$rep', round(d['value'],1), 'hbm_res', round(d['hbm_resident_fps']), 'k1', d['roofline'].get('avg_launch_ms'), 'busy', d['host_cpu_busy_cores'])"
+        python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_ab_${WL}_$v$rep.json')); k=d['stages_ms_per_step']; print('$WL $v$rep', round(d['value'],1), 'hbm_res', round(d['hbm_resident_fps']), 'k1', round(d['roofline'].get('avg_launch_ms'),3), 'prep', round(k.get('prep_ms',0),3), 'sao', round(k.get('sao_ms',0),3), 'jpeg', round(k.get('jpeg_ms',0),3), 'busy', d['host_cpu_busy_cores'])"
       done
     done ;;
   parse)
